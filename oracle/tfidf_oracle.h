@@ -1,0 +1,107 @@
+/*
+ * tfidf_oracle.h — CPU ORACLE (test infrastructure only).
+ *
+ * A plain-C, single-threaded restatement of the reference's hot path, which
+ * lives in Apache Lucene 9.8.0 (org.apache.lucene:lucene-core /
+ * lucene-queryparser / lucene-analysis-common 9.8.0, pinned at
+ * TF-IDF-System-Core/pom.xml:77-93; not vendored under /root/reference).
+ * Call sites restated:
+ *   Worker.addDocToIndex  TF-IDF-System-Core/src/main/java/me/zookeeper/leader_election/worker/Worker.java:190-220
+ *   Worker.searchIndex    .../worker/Worker.java:222-241
+ *   Leader.start merge    .../leader/Leader.java:39-92
+ *
+ * Pinned by: tests/golden/lucene_sample8.json, decoded from the reference's
+ * committed Lucene 9.8.0 index (TF, DF, norm bytes, docCount, sumTotalTermFreq,
+ * sumDocFreq).  BM25 scores are NOT pinned by any reference artefact
+ * ("parity unpinned" for scores).
+ *
+ * ONLY tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may
+ * load this library, and only as the checker / the timed CPU baseline.  The
+ * product (libtfidf) never links or calls it.
+ */
+#ifndef TFIDF_ORACLE_H
+#define TFIDF_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ORC_OK 0
+#define ORC_E_ARG (-1)
+#define ORC_E_UNSUPPORTED (-2) /* non-ASCII byte, or AND/OR/NOT operator word */
+#define ORC_E_NOMEM (-3)
+#define ORC_E_CAP (-4)         /* caller buffer too small; *n_out = needed */
+
+/* StandardTokenizer (ASCII subset of UAX#29) + LowerCaseFilter.
+ * Writes token start offsets / lengths (into the ORIGINAL bytes; lower-case
+ * folding is ASCII A-Z -> a-z and is applied by callers).  Returns the number
+ * of tokens (may exceed cap: only the first cap are written), or
+ * ORC_E_UNSUPPORTED when a byte >= 0x80 is present. */
+int64_t orc_tokenize(const uint8_t *s, uint64_t n, uint32_t max_token_len,
+                     uint32_t *starts, uint32_t *lens, uint64_t cap);
+
+/* SmallFloat.intToByte4 / byte4ToInt (BM25Similarity.computeNorm, LENGTH_TABLE). */
+uint8_t orc_int_to_byte4(int32_t i);
+int32_t orc_byte4_to_int(uint8_t b);
+
+typedef struct orc_index orc_index;
+
+orc_index *orc_create(float k1, float b);
+void orc_destroy(orc_index *ix);
+/* updateDocument(Term("path", key), doc): replaces a live doc with the same key. */
+int orc_add_doc(orc_index *ix, const uint8_t *key, uint64_t key_len,
+                const uint8_t *text, uint64_t n);
+int orc_commit(orc_index *ix);
+
+uint64_t orc_num_docs(const orc_index *ix);      /* live docs (maxDoc after compaction) */
+uint64_t orc_doc_count(const orc_index *ix);     /* docs with >= 1 token */
+uint64_t orc_sum_ttf(const orc_index *ix);
+uint64_t orc_num_terms(const orc_index *ix);
+uint32_t orc_doc_len(const orc_index *ix, uint64_t doc);
+uint8_t orc_doc_norm(const orc_index *ix, uint64_t doc);
+/* key of doc; returns length, copies up to cap bytes */
+uint64_t orc_doc_key(const orc_index *ix, uint64_t doc, uint8_t *buf, uint64_t cap);
+/* Distinct terms of a doc sorted by bytes: terms NUL-separated into buf.
+ * Returns the number of distinct terms (or ORC_E_CAP with nothing written). */
+int64_t orc_doc_terms(const orc_index *ix, uint64_t doc, char *buf, uint64_t buf_cap,
+                      uint32_t *tfs, uint64_t cap);
+int64_t orc_df(const orc_index *ix, const uint8_t *term, uint64_t len);
+/* Vocabulary export: all terms NUL-separated (index order) + df. */
+int64_t orc_vocab(const orc_index *ix, char *buf, uint64_t buf_cap, uint32_t *df, uint64_t cap);
+
+/* GLOBAL-stats override (the 1-worker semantics of a sharded corpus):
+ * per-term df by string, plus docCount / sumTotalTermFreq.  Pass
+ * doc_count == 0 to revert to the shard's own statistics. */
+int orc_set_global_stats(orc_index *ix, uint64_t doc_count, uint64_t sum_ttf);
+int orc_set_global_df(orc_index *ix, const uint8_t *term, uint64_t len, uint64_t df);
+
+/* Worker.searchIndex: parse(escape(q)) -> BM25 disjunction -> hits ordered
+ * (score desc, doc asc).  k == 0 returns all hits (searcher.search(q, MAX)).
+ * Returns ORC_OK / ORC_E_UNSUPPORTED / ORC_E_CAP (n_out = needed). */
+int orc_search(const orc_index *ix, const uint8_t *q, uint64_t q_len, uint32_t k,
+               uint32_t *docs, float *scores, uint64_t cap, uint64_t *n_out);
+
+/* Query analysis used by orc_search: distinct terms (first appearance order)
+ * NUL-separated + boost (occurrence count).  Returns #terms or error. */
+int64_t orc_query_terms(const uint8_t *q, uint64_t q_len, char *buf, uint64_t buf_cap,
+                        float *boosts, uint64_t cap);
+
+/* BM25 pieces in Java float/double order (BM25Similarity 9.8.0). */
+float orc_idf(uint64_t doc_freq, uint64_t doc_count);
+float orc_avgdl(uint64_t sum_ttf, uint64_t doc_count);
+void orc_norm_cache(float k1, float b, float avgdl, float cache[256]);
+float orc_bm25(float weight, uint32_t tf, float norm_inverse);
+
+/* Leader.start merge: names (concatenated, offsets[n+1]) with double scores in
+ * worker-response order -> distinct names sorted by String.compareTo (ASCII
+ * byte order) with Double::sum totals.  Output: index of first occurrence of
+ * each distinct name in sorted order + sums.  Returns #distinct. */
+int64_t orc_leader_merge(const uint8_t *names, const uint64_t *offsets, uint64_t n,
+                         const double *scores, uint64_t *out_first, double *out_sum);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
