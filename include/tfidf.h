@@ -1,0 +1,182 @@
+/*
+ * tfidf.h — C ABI of libtfidf, the MI355X-native TF-IDF/BM25 engine.
+ *
+ * Drop-in boundary for the reference's hot path (kheder-hassoun/
+ * Tf-IDF-Distributed-System, Java + Lucene 9.8.0).  The reference has no
+ * plugin API: the path sits behind direct Lucene calls in two Java methods
+ * and one merge loop.  Each entry point below names the reference interface
+ * it replaces (paths relative to TF-IDF-System-Core/src/main/java/):
+ *
+ *   tfidf_create / tfidf_destroy
+ *       me/zookeeper/leader_election/worker/Worker.java:67-73
+ *       (FSDirectory.open + new IndexWriter(dir, IndexWriterConfig(new StandardAnalyzer())))
+ *   tfidf_add_docs / tfidf_add_docs_device
+ *       Worker.java:190-220 addDocToIndex -> indexWriter.updateDocument(Term("path", rel), doc)
+ *       (called from the Files.walk loop Worker.java:77-86 and upload Worker.java:136-139)
+ *   tfidf_commit
+ *       Worker.java:88 and :138 indexWriter.commit() (+ DirectoryReader.open at :223 sees it)
+ *   tfidf_search / tfidf_search_batch
+ *       Worker.java:222-241 searchIndex: QueryParser("contents", StandardAnalyzer)
+ *       .parse(QueryParser.escape(q)); searcher.search(query, Integer.MAX_VALUE)
+ *   tfidf_doc_key
+ *       Worker.java:235-236 searcher.doc(sd.doc).get("path")
+ *   tfidf_stats
+ *       Worker.java:147-172 /worker/index-size (device bytes) + Lucene CollectionStatistics
+ *   tfidf_vocab_* / tfidf_set_global_*
+ *       no reference counterpart: GLOBAL statistics across GPU shards (the
+ *       reference's 1-worker semantics, Leader.java:39-92 with one worker)
+ *   tfidf_leader_merge
+ *       me/zookeeper/leader_election/leader/Leader.java:73-88 (sum per name, TreeMap order)
+ *
+ * Conventions: every call returns an int status (TFIDF_OK == 0); the message
+ * of the last failure on the calling thread is tfidf_last_error().  Buffers
+ * are caller-owned and only borrowed for the duration of a call.  Searches on
+ * a committed index are safe to issue from several threads; add/commit are
+ * serialised by the caller (Worker.java:136 synchronized(indexWriter)).
+ * Scores are IEEE float32 bit-identical to Lucene 9.8.0 BM25Similarity
+ * (k1 = 1.2, b = 0.75); hits are ordered by (score desc, doc asc).
+ */
+#ifndef TFIDF_H
+#define TFIDF_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TFIDF_OK 0
+#define TFIDF_E_INVALID_ARG 1
+#define TFIDF_E_HIP 2
+#define TFIDF_E_OOM 3
+#define TFIDF_E_UNSUPPORTED_INPUT 4 /* non-ASCII document, token > 255 chars, tf >= 2^24 */
+#define TFIDF_E_UNSUPPORTED_QUERY 5 /* non-ASCII query, AND/OR/NOT operator words */
+#define TFIDF_E_CAPACITY 6          /* vocabulary capacity exceeded */
+#define TFIDF_E_STATE 7             /* e.g. search before commit */
+#define TFIDF_E_BUFFER 8            /* caller buffer too small; *n_out holds the size needed */
+#define TFIDF_E_NO_DEVICE 9
+
+#define TFIDF_STATS_SHARD 0  /* per-shard statistics: the reference's N-worker semantics */
+#define TFIDF_STATS_GLOBAL 1 /* statistics imported from all shards: 1-worker semantics */
+
+typedef struct tfidf_index tfidf_index;
+
+typedef struct tfidf_config {
+  float k1;                     /* BM25 k1, default 1.2f (BM25Similarity()) */
+  float b;                      /* BM25 b,  default 0.75f */
+  int32_t stats_mode;           /* TFIDF_STATS_SHARD (default) or TFIDF_STATS_GLOBAL */
+  int32_t device;               /* HIP device ordinal */
+  uint32_t vocab_capacity_log2; /* dictionary slots = 2^x; default 18 (<= ~200k terms) */
+  uint32_t max_token_len;       /* StandardAnalyzer.DEFAULT_MAX_TOKEN_LENGTH = 255 (only value supported) */
+} tfidf_config;
+
+typedef struct tfidf_index_stats {
+  uint64_t num_docs;      /* live documents (maxDoc after compaction) */
+  uint64_t doc_count;     /* documents with >= 1 token (CollectionStatistics.docCount) */
+  uint64_t sum_ttf;       /* sumTotalTermFreq */
+  uint64_t num_terms;     /* distinct terms in this shard */
+  uint64_t nnz;           /* (doc, term) postings = sumDocFreq */
+  uint64_t device_bytes;  /* HBM held by the index (feeds /worker/index-size) */
+  uint64_t long_docs;     /* documents indexed by the long-document path */
+  uint64_t text_bytes;    /* corpus bytes resident on the device */
+} tfidf_index_stats;
+
+/* Per-phase device times of the last commit, measured with HIP events on the
+ * index's stream around each kernel. */
+typedef struct tfidf_commit_timing {
+  float ms_total;
+  float ms_tokenize;   /* tfidf_tokenize_count: text -> per-doc TF rows (CSR) */
+  float ms_long;       /* long-document path */
+  float ms_df;         /* per (doc block, term range) DF histograms */
+  float ms_blockscan;  /* DF reduction over blocks + posting offsets */
+  float ms_colscan;    /* exclusive scan of DF -> posting-list starts */
+  float ms_scatter;    /* CSR -> block-segmented inverted postings */
+  uint64_t text_bytes;
+  uint64_t num_docs;
+  uint64_t nnz;
+} tfidf_commit_timing;
+
+const char *tfidf_version(void);
+const char *tfidf_last_error(void);
+int tfidf_config_init(tfidf_config *cfg);
+
+int tfidf_create(const tfidf_config *cfg, tfidf_index **out);
+int tfidf_destroy(tfidf_index *ix);
+
+/* Host corpus: n_docs documents, document i = utf8[offsets[i] .. offsets[i+1]).
+ * keys (may be NULL) = relative paths, key i = keys[key_offsets[i] .. key_offsets[i+1]);
+ * a key already present replaces that document (updateDocument by Term("path", key)).
+ * With keys == NULL the key of a document is its decimal ordinal in this index. */
+int tfidf_add_docs(tfidf_index *ix, const uint8_t *utf8, const uint64_t *offsets, uint64_t n_docs,
+                   const uint8_t *keys, const uint64_t *key_offsets);
+/* Device-resident corpus (e.g. produced by tfidf_synth_corpus): copied device-to-device. */
+int tfidf_add_docs_device(tfidf_index *ix, const void *d_utf8, const void *d_offsets, uint64_t n_docs,
+                          uint64_t total_bytes);
+
+int tfidf_commit(tfidf_index *ix);
+int tfidf_get_commit_timing(const tfidf_index *ix, tfidf_commit_timing *out);
+int tfidf_stats(const tfidf_index *ix, tfidf_index_stats *out);
+
+/* Single query. k == 0 returns all hits (searcher.search(q, Integer.MAX_VALUE)).
+ * doc_ids are local document ordinals; scores are float32. */
+int tfidf_search(tfidf_index *ix, const uint8_t *q, uint64_t q_len, uint32_t k, uint32_t *doc_ids,
+                 float *scores, uint64_t cap, uint64_t *n_out);
+/* n_q queries; query i = q_utf8[q_offsets[i] .. q_offsets[i+1]).  1 <= k <= 1024.
+ * Outputs are n_q x k (row i holds counts[i] valid hits). */
+int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const uint64_t *q_offsets, uint32_t n_q,
+                       uint32_t k, uint32_t *doc_ids, float *scores, uint32_t *counts);
+/* Per-query device time of the last search call (HIP events, index stream). */
+int tfidf_last_search_ms(const tfidf_index *ix, float *ms_scoring, float *ms_total);
+
+int tfidf_doc_key(const tfidf_index *ix, uint64_t doc, uint8_t *buf, uint64_t cap, uint64_t *n_out);
+int tfidf_doc_len(tfidf_index *ix, uint64_t doc, uint32_t *len, uint8_t *norm);
+/* Distinct terms of one document: NUL-separated strings (sorted by bytes) + tf. */
+int tfidf_doc_terms(tfidf_index *ix, uint64_t doc, char *terms, uint64_t terms_cap, uint32_t *tfs,
+                    uint64_t cap, uint64_t *n_out);
+int tfidf_term_df(tfidf_index *ix, const uint8_t *term, uint64_t len, uint64_t *df_local,
+                  uint64_t *df_effective);
+
+/* ---- GLOBAL statistics across shards (no reference counterpart) ----
+ * 1. tfidf_vocab_export_device: this shard's term keys (16 B each, sorted
+ *    ascending as (hi, lo)) and local df into caller device buffers.
+ * 2. caller all-gathers the key lists (RCCL), then
+ *    tfidf_vocab_canonicalize_device: sorted union of all shards' keys ->
+ *    canonical term ids; fills d_df_canonical (u32[n_canonical]) with this
+ *    shard's df in canonical order (zero elsewhere).
+ * 3. caller all-reduces d_df_canonical and {doc_count, sum_ttf} (RCCL SUM), then
+ *    tfidf_set_global_stats_device imports them. */
+int tfidf_vocab_size(const tfidf_index *ix, uint64_t *n);
+int tfidf_vocab_export_device(tfidf_index *ix, void *d_keys, void *d_df, uint64_t cap, uint64_t *n_out);
+int tfidf_vocab_canonicalize_device(tfidf_index *ix, const void *d_all_keys, uint64_t n_all,
+                                    void *d_df_canonical, uint64_t cap, uint64_t *n_canonical);
+int tfidf_set_global_stats_device(tfidf_index *ix, const void *d_df_canonical, uint64_t n_canonical,
+                                  uint64_t doc_count, uint64_t sum_ttf);
+/* Host-buffer form of the same import: df for arbitrary keys (2 x u64 per key: lo, hi). */
+int tfidf_set_global_stats(tfidf_index *ix, const uint64_t *keys_lohi, const uint64_t *df, uint64_t n,
+                           uint64_t doc_count, uint64_t sum_ttf);
+int tfidf_clear_global_stats(tfidf_index *ix);
+
+/* Term key of an analysed (lower-cased) token, as the device computes it. */
+int tfidf_term_key(const uint8_t *term, uint64_t len, uint64_t *lo, uint64_t *hi);
+
+/* Leader.start merge (Leader.java:73-88): names (concatenated, offsets[n+1])
+ * with double scores in worker-response order -> distinct names sorted by
+ * String.compareTo with Double::sum totals.  out_first[i] = index of the
+ * first occurrence of the i-th distinct name.  n_out = #distinct. */
+int tfidf_leader_merge(const uint8_t *names, const uint64_t *offsets, uint64_t n, const double *scores,
+                       uint64_t *out_first, double *out_sum, uint64_t *n_out);
+
+/* ---- synthetic corpus (bench/test input generator, device side) ----
+ * Zipf(s) over V ranks, rank r -> bijective base-26 word of
+ * (r + 18278), doc lengths uniform in [len_min, len_max], ' ' separators and
+ * '\n' after every 16th token and after the last.  cdf = double[V] (host). */
+int tfidf_synth_corpus(int device, uint64_t seed, uint64_t n_docs, uint64_t doc_base, const double *cdf,
+                       uint32_t V, uint32_t len_min, uint32_t len_max, void **d_text, void **d_offsets,
+                       uint64_t *total_bytes);
+int tfidf_device_free(int device, void *d_ptr);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TFIDF_H */

@@ -1,0 +1,93 @@
+"""C-ABI library checks that need no GPU: the .so loads, exports every entry
+point declared in include/tfidf.h, and its pure-host functions (term keys,
+leader merge, config) behave.  No compute call touches a device here."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+from tfidf_amd import _lib as L
+from tfidf_amd.engine import leader_merge, term_key
+from oracle import oracle as O
+
+HEADER = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "tfidf.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(tfidf_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = C.CDLL(L.LIB_PATH)
+    names = header_functions()
+    assert len(names) >= 25
+    missing = [n for n in names if not hasattr(lib, n)]
+    assert missing == []
+    assert set(names) == set(L.SIGNATURES), "ctypes signatures out of sync with the header"
+
+
+def test_version_and_config_defaults():
+    lib = L.load()
+    assert b"gfx950" in lib.tfidf_version()
+    cfg = L.Config()
+    assert lib.tfidf_config_init(C.byref(cfg)) == 0
+    assert abs(cfg.k1 - 1.2) < 1e-7 and abs(cfg.b - 0.75) < 1e-7
+    assert cfg.max_token_len == 255 and cfg.vocab_capacity_log2 == 18
+
+
+def test_create_without_device_fails_loudly():
+    # This container has no GPU: creation must fail, never fall back to CPU.
+    try:
+        import torch
+        if torch.cuda.is_available():
+            pytest.skip("GPU present")
+    except Exception:
+        pass
+    lib = L.load()
+    cfg = L.Config()
+    lib.tfidf_config_init(C.byref(cfg))
+    h = C.c_void_p()
+    rc = lib.tfidf_create(C.byref(cfg), C.byref(h))
+    assert rc != 0
+    assert rc in (L.E_NO_DEVICE, L.E_HIP)
+
+
+def _pack7(term: bytes):
+    v = 0
+    for j, c in enumerate(term):
+        v |= c << (7 * j)
+    return v & ((1 << 64) - 1), (v >> 64) | (1 << 63)
+
+
+@pytest.mark.parametrize("term", [b"a", b"fast", b"kheder", b"wireless", b"u.s.a", b"3,14", b"abcdefghi",
+                                  b"abcdefghij", b"x" * 18])
+def test_short_term_keys_are_exact_7bit_packing(term):
+    assert term_key(term) == _pack7(term)
+
+
+def test_long_term_keys_hashed_and_distinct():
+    a = term_key(b"a" * 19)
+    b = term_key(b"a" * 20)
+    c = term_key(b"b" + b"a" * 18)
+    assert len({a, b, c}) == 3
+    for lo, hi in (a, b, c):
+        assert hi >> 62 == 3 and lo & 1 == 1       # VALID | LONG flags, lo != 0
+
+
+def test_leader_merge_matches_oracle():
+    rng = np.random.default_rng(1)
+    names = [b"file%d.txt" % i for i in range(20)]
+    for trial in range(20):
+        responses = []
+        for w in range(rng.integers(1, 5)):
+            picks = rng.choice(len(names), size=rng.integers(0, 12), replace=False)
+            responses.append([(names[i], float(np.float32(rng.random()))) for i in picks])
+        assert leader_merge(responses) == O.leader_merge(responses)
+
+
+def test_leader_merge_empty():
+    assert leader_merge([]) == []

@@ -1,0 +1,337 @@
+"""GPU parity: the HIP engine (through the C ABI) against the CPU oracle and
+the golden fixture decoded from the reference's Lucene 9.8.0 index.
+
+Bar: TF, DF, norms, doc lengths, docCount, sumTotalTermFreq, hit sets and
+top-k doc ids bit-exact; scores compared as float32 bit patterns (the engine
+reproduces Lucene's float operation order, so the tolerance is zero; the
+north_star tolerance for fp32 would be 1e-4 relative).
+"""
+import os
+import random
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from tfidf_amd import synth
+from tfidf_amd.engine import ShardIndex
+from tfidf_amd._lib import UnsupportedInput, UnsupportedQuery
+
+pytestmark = pytest.mark.gpu
+
+
+def f32bits(x):
+    return np.float32(x).view(np.int32).item()
+
+
+def assert_hits_equal(got, want):
+    assert [d for d, _ in got] == [d for d, _ in want]
+    assert [f32bits(s) for _, s in got] == [f32bits(s) for _, s in want]
+
+
+def build_pair(texts, keys=None, cap_log2=18):
+    g = ShardIndex(vocab_capacity_log2=cap_log2)
+    g.add_documents(texts, keys)
+    g.commit()
+    o = O.OracleIndex()
+    for i, t in enumerate(texts):
+        o.add_doc(keys[i] if keys else str(i).encode(), t)
+    o.commit()
+    return g, o
+
+
+# ---------------------------------------------------------------------------
+# golden fixture (reference's committed Lucene index)
+
+@pytest.fixture(scope="module")
+def fx(lucene_fixture):
+    texts = [d["text"].encode() for d in lucene_fixture["docs"]]
+    keys = [d["name"].encode() for d in lucene_fixture["docs"]]
+    g, o = build_pair(texts, keys)
+    yield g, o, lucene_fixture
+    g.close()
+    o.close()
+
+
+def test_fixture_collection_stats(fx):
+    g, _, f = fx
+    s = g.stats()
+    assert s["doc_count"] == f["field_stats"]["docCount"] == 8
+    assert s["sum_ttf"] == f["field_stats"]["sumTotalTermFreq"] == 252
+    assert s["num_terms"] == f["field_stats"]["numTerms"] == 13
+    assert s["nnz"] == f["field_stats"]["sumDocFreq"] == 58
+    assert s["num_docs"] == 8
+
+
+def test_fixture_tf_df_norms(fx):
+    g, _, f = fx
+    per_doc = {}
+    for t in f["terms"]:
+        assert g.df(t["term"].encode())[0] == t["df"]
+        for d, tf in t["postings"]:
+            per_doc.setdefault(d, {})[t["term"].encode()] = tf
+    for d in range(8):
+        assert g.doc_terms(d) == per_doc[d]
+        ln, nm = g.doc_len(d)
+        assert ln == f["doc_lengths_from_postings"][d]
+        assert nm == f["norms"][d]
+
+
+@pytest.mark.parametrize("q", [b"fast food", b"cat", b"best wireless earbuds", b"kheder", b"at night",
+                               b"fast fast food", b"FAST Food!", b"2024 helo", b"nothing here", b"",
+                               b"+fast -(food)", b"e-mail kheder:helo"])
+def test_fixture_search_all_hits(fx, q):
+    g, o, _ = fx
+    assert_hits_equal(g.search(q, k=0), o.search(q, k=0))
+
+
+@pytest.mark.parametrize("k", [1, 3, 5, 100])
+def test_fixture_search_topk(fx, k):
+    g, o, _ = fx
+    for q in [b"fast food", b"kheder", b"cat at night causes"]:
+        assert_hits_equal(g.search(q, k=k), o.search(q, k=k))
+
+
+def test_operator_words_rejected(fx):
+    g, _, _ = fx
+    with pytest.raises(UnsupportedQuery):
+        g.search(b"fast AND food")
+
+
+def test_reference_worker_and_leader(tmp_path, lucene_fixture):
+    from tfidf_amd.reference_api import Leader, Worker
+    docs = tmp_path / "documents"
+    docs.mkdir()
+    for d in lucene_fixture["docs"]:
+        (docs / d["name"]).write_bytes(d["text"].encode())
+    w = Worker(str(docs), str(docs / ".luceneIndex"))
+    w.init()
+    o = O.OracleIndex()
+    for d in sorted(lucene_fixture["docs"], key=lambda d: d["name"]):
+        o.add_doc(d["name"].encode(), d["text"].encode())
+    o.commit()
+    for q in ["fast food", "kheder", "best wireless earbuds"]:
+        got = w.process_documents(q)
+        want = [{"document": {"name": o.doc_key(d).decode()}, "score": s} for d, s in o.search(q.encode())]
+        assert got == want
+    assert w.process_documents("fast AND food") == []          # Worker.java:182-185
+    out = Leader([w]).start("fast food")
+    assert list(out) == sorted(out)                              # TreeMap order
+    assert list(out) == ["file.txt", "file3.txt", "file5.txt", "file6.txt", "file7.txt", "file8.txt"]
+    assert w.get_index_size() > 0
+    w.close()
+
+
+# ---------------------------------------------------------------------------
+# synthetic Zipf corpora
+
+@pytest.fixture(scope="module")
+def zipf():
+    texts = synth.corpus(3000, V=20000, len_min=30, len_max=220)
+    g, o = build_pair(texts)
+    yield g, o, texts
+    g.close()
+    o.close()
+
+
+def test_zipf_stats(zipf):
+    g, o, _ = zipf
+    s = g.stats()
+    assert s["doc_count"] == o.doc_count
+    assert s["sum_ttf"] == o.sum_ttf
+    assert s["num_terms"] == o.num_terms
+    assert s["long_docs"] == 0
+
+
+def test_zipf_tf_rows(zipf):
+    g, o, texts = zipf
+    for d in list(range(0, 3000, 97)) + [2999]:
+        assert g.doc_terms(d) == o.doc_terms(d)
+        assert g.doc_len(d) == (o.doc_len(d), o.doc_norm(d))
+
+
+def test_zipf_df(zipf):
+    g, o, _ = zipf
+    vocab = o.vocab()
+    rng = random.Random(3)
+    for t in rng.sample(sorted(vocab), 400):
+        assert g.df(t)[0] == vocab[t]
+
+
+def test_zipf_queries_all_hits(zipf):
+    g, o, _ = zipf
+    for q in synth.queries(25, lo=1, hi=3000) + [b"aaaa", b"aaaa aaab aaac aaad"]:
+        assert_hits_equal(g.search(q, 0), o.search(q, 0))
+
+
+def test_zipf_queries_topk_and_batch(zipf):
+    g, o, _ = zipf
+    qs = synth.queries(40, lo=1, hi=5000) + [b"aaaa aaab", b"zzzzz"]
+    for k in (10, 100):
+        docs, scores, counts = g.search_batch(qs, k)
+        for i, q in enumerate(qs):
+            want = o.search(q, k)
+            got = list(zip(docs[i, :counts[i]].tolist(), scores[i, :counts[i]].tolist()))
+            assert_hits_equal(got, want)
+            assert_hits_equal(g.search(q, k), want)
+
+
+def test_zipf_ties_many_equal_scores():
+    # one short term repeated identically in many docs -> huge tie groups
+    texts = [b"alpha beta" if i % 3 else b"alpha gamma delta" for i in range(20000)]
+    g, o = build_pair(texts)
+    for k in (0, 7, 1000):
+        assert_hits_equal(g.search(b"alpha", k), o.search(b"alpha", k))
+    g.close()
+    o.close()
+
+
+# ---------------------------------------------------------------------------
+# tokenizer edge cases, long documents, updates, errors
+
+ALPHABET = "abcXYZ019_:.',; -\n\t"
+
+
+def random_text(rng, n):
+    return "".join(rng.choice(ALPHABET) for _ in range(n)).encode()
+
+
+def test_punctuation_corpus_parity():
+    rng = random.Random(7)
+    texts = [random_text(rng, rng.randint(0, 3000)) for _ in range(400)]
+    texts += [b"", b"   ", b"___", b"...", b"a.b.c", b"3,14;15", b"don't", b"x" * 18, b"y" * 19, b"z" * 255]
+    g, o = build_pair(texts)
+    s = g.stats()
+    assert (s["doc_count"], s["sum_ttf"], s["num_terms"]) == (o.doc_count, o.sum_ttf, o.num_terms)
+    for d in range(len(texts)):
+        assert g.doc_terms(d) == o.doc_terms(d), d
+        assert g.doc_len(d) == (o.doc_len(d), o.doc_norm(d))
+    for q in [b"a", b"b.c x", b"3,14", b"abc xyz", b"_", b"y" * 19]:
+        assert_hits_equal(g.search(q, 0), o.search(q, 0))
+    g.close()
+    o.close()
+
+
+def test_long_documents_path():
+    rng = random.Random(11)
+    cdf = synth.zipf_cdf(50000)
+    texts = synth.corpus(200, V=50000, len_min=10, len_max=400)
+    # long docs: > 4 KB and/or > 1024 tokens, up to ~120k tokens
+    for n in (700, 1500, 5000, 40000, 120000):
+        ranks = synth.doc_ranks(99, n, n, n, cdf)
+        texts.insert(rng.randrange(len(texts)), b" ".join(synth.word(int(r)) for r in ranks))
+    texts.insert(5, b"ab " * 2000)                  # 6 KB, 2000 tokens of one term
+    texts.insert(9, random_text(rng, 20000))        # punctuation-heavy long doc
+    g, o = build_pair(texts, cap_log2=18)
+    s = g.stats()
+    assert s["long_docs"] >= 7
+    assert (s["doc_count"], s["sum_ttf"], s["num_terms"], s["nnz"]) == \
+        (o.doc_count, o.sum_ttf, o.num_terms, sum(o.vocab().values()))
+    for d in range(len(texts)):
+        if len(texts[d]) > 4096 or d % 17 == 0:
+            assert g.doc_terms(d) == o.doc_terms(d), d
+            assert g.doc_len(d) == (o.doc_len(d), o.doc_norm(d))
+    for q in synth.queries(15, lo=1, hi=2000) + [b"ab", b"a b c"]:
+        assert_hits_equal(g.search(q, 0), o.search(q, 0))
+        assert_hits_equal(g.search(q, 10), o.search(q, 10))
+    g.close()
+    o.close()
+
+
+def test_update_document_replaces_by_key():
+    texts = [b"fast food", b"cat meowing", b"night at night", b"fast cat"]
+    keys = [b"a.txt", b"b.txt", b"a.txt", b"c.txt"]
+    g, o = build_pair(texts, keys)
+    assert g.stats()["num_docs"] == o.num_docs == 3
+    assert [g.doc_key(d) for d in range(3)] == [o.doc_key(d) for d in range(3)] == [b"b.txt", b"a.txt", b"c.txt"]
+    for q in [b"fast", b"night", b"cat"]:
+        assert_hits_equal(g.search(q, 0), o.search(q, 0))
+    g.close()
+    o.close()
+
+
+def test_incremental_add_then_recommit():
+    a = synth.corpus(500, V=3000, len_min=20, len_max=80)
+    b = synth.corpus(300, V=3000, len_min=20, len_max=80, doc_base=500)
+    g = ShardIndex()
+    g.add_documents(a)
+    g.commit()
+    g.add_documents(b)
+    g.commit()
+    o = O.OracleIndex()
+    for i, t in enumerate(a + b):
+        o.add_doc(str(i).encode(), t)
+    o.commit()
+    for q in synth.queries(10, lo=1, hi=500):
+        assert_hits_equal(g.search(q, 0), o.search(q, 0))
+    g.close()
+    o.close()
+
+
+def test_non_ascii_document_rejected():
+    g = ShardIndex()
+    g.add_documents([b"fine text", "café".encode()])
+    with pytest.raises(UnsupportedInput):
+        g.commit()
+    g.close()
+
+
+def test_empty_index_and_empty_docs():
+    g = ShardIndex()
+    g.add_documents([b"", b"  ..  ", b""])
+    g.commit()
+    s = g.stats()
+    assert s["doc_count"] == 0 and s["num_terms"] == 0 and s["num_docs"] == 3
+    assert g.search(b"anything", 0) == []
+    g.close()
+
+
+# ---------------------------------------------------------------------------
+# GLOBAL statistics across shards (device vocabulary canonicalisation)
+
+def test_global_stats_two_shards_equal_single_index():
+    import torch
+    texts = synth.corpus(4000, V=8000, len_min=20, len_max=120)
+    halves = [texts[:1700], texts[1700:]]
+    shards = []
+    for h in halves:
+        s = ShardIndex()
+        s.add_documents(h)
+        s.commit()
+        shards.append(s)
+    dev = torch.device("cuda:0")
+    keys = []
+    for s in shards:
+        n = s.vocab_size()
+        k = torch.zeros((n, 2), dtype=torch.int64, device=dev)
+        df = torch.zeros(n, dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        s.vocab_export_device(k.data_ptr(), df.data_ptr(), n)
+        keys.append(k)
+    all_keys = torch.cat(keys).contiguous()
+    dfcs = []
+    for s in shards:
+        dfc = torch.zeros(all_keys.shape[0], dtype=torch.int32, device=dev)
+        n = s.vocab_canonicalize_device(all_keys.data_ptr(), all_keys.shape[0], dfc.data_ptr(), all_keys.shape[0])
+        dfcs.append(dfc[:n])
+    assert dfcs[0].shape == dfcs[1].shape
+    total = (dfcs[0] + dfcs[1]).contiguous()
+    st = [s.stats() for s in shards]
+    dc = sum(x["doc_count"] for x in st)
+    ttf = sum(x["sum_ttf"] for x in st)
+    for s in shards:
+        s.set_global_stats_device(total.data_ptr(), total.shape[0], dc, ttf)
+    o = O.OracleIndex()
+    for i, t in enumerate(texts):
+        o.add_doc(str(i).encode(), t)
+    o.commit()
+    for q in synth.queries(20, lo=1, hi=2000):
+        want = o.search(q, 0)
+        got = []
+        for base, s in zip((0, 1700), shards):
+            got += [(d + base, sc) for d, sc in s.search(q, 0)]
+        got.sort(key=lambda x: (-x[1], x[0]))
+        assert_hits_equal(got, want)
+    for s in shards:
+        s.close()
+    o.close()

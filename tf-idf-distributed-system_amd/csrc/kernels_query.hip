@@ -1,0 +1,266 @@
+// kernels_query.hip — BM25 scoring + ranking (Worker.searchIndex of the
+// reference, Worker.java:222-241: IndexSearcher.search(query, MAX) with
+// Lucene 9.8.0 BM25Similarity and TopScoreDocCollector), for gfx950.
+//
+//   score_blocks : grid (doc block, query).  For each query term (in query
+//                  order) the workgroup streams that term's posting segment
+//                  for the block (contiguous, coalesced u64 loads) and
+//                  computes  s = w - w / (1f + (float)tf * cache[norm])  in
+//                  float (no contraction), accumulating (double)s per doc in
+//                  LDS — the disjunction's double sum — then rounds once to
+//                  float.  Top-k within the block: 4-pass 8-bit radix select
+//                  on the float bits, ties resolved by ascending doc via a
+//                  block scan over the hit bitmap (HitQueue order).
+//   merge_topk   : per query, radix select over all block candidates on the
+//                  64-bit key (score bits << 32 | ~doc), then a bitonic sort
+//                  in LDS -> (score desc, doc asc).
+#include <hip/hip_runtime.h>
+
+#include "tfidf_common.h"
+#include "tfidf_internal.h"
+
+namespace tfidf {
+
+constexpr uint32_t kScoreThreads = 512;
+constexpr uint32_t kDocsPerThread = kBlockDocs / kScoreThreads;  // 16
+
+__device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t *sh, uint32_t *total) {
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  uint32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) sh[wid] = x;
+  __syncthreads();
+  uint32_t base = 0, tot = 0;
+  for (uint32_t w = 0; w < nw; w++) {
+    uint32_t s = sh[w];
+    if (w < wid) base += s;
+    tot += s;
+  }
+  __syncthreads();
+  *total = tot;
+  return base + x - v;
+}
+
+// BM25Scorer.score in Java float order; volatile-free: compiled with
+// -ffp-contract=off so no FMA is formed.
+__device__ __forceinline__ float bm25_term(float w, uint32_t tf, float norm_inverse) {
+  const float t = (float)tf * norm_inverse;
+  const float u = 1.0f + t;
+  const float v = w / u;
+  return w - v;
+}
+
+struct ScoreSmem {
+  double acc[kBlockDocs];
+  uint32_t hitbits[kBlockDocs / 32];
+  uint16_t hitlist[kBlockDocs];
+  float cache[256];
+  uint32_t hist[256];
+  uint32_t scan[16];
+  uint32_t nhit, prefix, remaining, outn;
+};
+
+__global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
+  __shared__ ScoreSmem sm;
+  const uint32_t b = blockIdx.x, q = blockIdx.y, tid = threadIdx.x;
+  const uint64_t d0 = (uint64_t)b * kBlockDocs;
+  for (uint32_t i = tid; i < kBlockDocs / 32; i += blockDim.x) sm.hitbits[i] = 0;
+  for (uint32_t i = tid; i < 256; i += blockDim.x) sm.cache[i] = p.cache[i];
+  if (tid == 0) { sm.nhit = 0; sm.outn = 0; }
+  __syncthreads();
+  const uint32_t t0 = p.q_off[q], t1 = p.q_off[q + 1];
+  for (uint32_t j = t0; j < t1; j++) {
+    const uint32_t slot = p.q_slot[j];
+    if (slot == kInvalidSlot) continue;                   // uniform
+    const float w = p.q_w[j];
+    const uint64_t cp = p.col_ptr[slot];
+    const uint64_t lo = cp + p.blk[(size_t)b * p.C + slot];
+    const uint64_t hi = cp + p.blk[(size_t)(b + 1) * p.C + slot];
+    for (uint64_t i = lo + tid; i < hi; i += blockDim.x) {
+      const uint64_t e = p.post[i];
+      const uint32_t ld = (uint32_t)(e & 0xFFFFFFFFu) - (uint32_t)d0;
+      const uint32_t tfn = (uint32_t)(e >> 32);
+      const float s = bm25_term(w, tfn >> 8, sm.cache[tfn & 255u]);
+      const uint32_t bit = 1u << (ld & 31);
+      const uint32_t old = atomicOr(&sm.hitbits[ld >> 5], bit);
+      if (old & bit) {
+        sm.acc[ld] += (double)s;
+      } else {
+        sm.acc[ld] = (double)s;
+        sm.hitlist[atomicAdd(&sm.nhit, 1u)] = (uint16_t)ld;
+      }
+    }
+    __syncthreads();
+  }
+  const uint32_t nhit = sm.nhit;
+  const uint32_t k = p.k;
+  if (k == 0) {
+    // all-hits mode: dump every hit key of the block
+    for (uint32_t i = tid; i < nhit; i += blockDim.x) {
+      const uint32_t ld = sm.hitlist[i];
+      const float sc = (float)sm.acc[ld];
+      p.hits[(size_t)b * kBlockDocs + i] =
+          ((uint64_t)__float_as_uint(sc) << 32) | (uint64_t)(~(uint32_t)(d0 + ld));
+    }
+    if (tid == 0) p.hits_n[b] = nhit;
+    return;
+  }
+  uint64_t *cand = p.cand + ((size_t)q * p.n_blocks + b) * k;
+  if (nhit <= k) {
+    for (uint32_t i = tid; i < nhit; i += blockDim.x) {
+      const uint32_t ld = sm.hitlist[i];
+      cand[i] = ((uint64_t)__float_as_uint((float)sm.acc[ld]) << 32) | (uint64_t)(~(uint32_t)(d0 + ld));
+    }
+    if (tid == 0) p.cand_n[(size_t)q * p.n_blocks + b] = nhit;
+    return;
+  }
+  // radix select: threshold T = k-th largest score bits
+  if (tid == 0) { sm.prefix = 0; sm.remaining = k; }
+  for (int pass = 0; pass < 4; pass++) {
+    const int sh = 24 - 8 * pass;
+    for (uint32_t i = tid; i < 256; i += blockDim.x) sm.hist[i] = 0;
+    __syncthreads();
+    const uint32_t prefix = sm.prefix;
+    const uint32_t hmask = pass == 0 ? 0u : (0xFFFFFFFFu << (sh + 8));
+    for (uint32_t i = tid; i < nhit; i += blockDim.x) {
+      const uint32_t sb = __float_as_uint((float)sm.acc[sm.hitlist[i]]);
+      if ((sb & hmask) == (prefix & hmask)) atomicAdd(&sm.hist[(sb >> sh) & 255u], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      uint32_t rem = sm.remaining, cum = 0;
+      for (int bin = 255; bin >= 0; bin--) {
+        const uint32_t h = sm.hist[bin];
+        if (cum + h >= rem) {
+          sm.prefix = prefix | ((uint32_t)bin << sh);
+          sm.remaining = rem - cum;
+          break;
+        }
+        cum += h;
+      }
+    }
+    __syncthreads();
+  }
+  const uint32_t T = sm.prefix, take_ties = sm.remaining;
+  // collection in ascending doc order: thread owns docs [16 tid, 16 tid + 16)
+  const uint32_t bits = (sm.hitbits[tid >> 1] >> (16 * (tid & 1))) & 0xFFFFu;
+  uint32_t nties = 0;
+  for (uint32_t x = bits; x; x &= x - 1) {
+    const uint32_t ld = tid * kDocsPerThread + (__ffs(x) - 1);
+    nties += __float_as_uint((float)sm.acc[ld]) == T;
+  }
+  uint32_t tot;
+  uint32_t tie_rank = block_excl_scan(nties, sm.scan, &tot);
+  for (uint32_t x = bits; x; x &= x - 1) {
+    const uint32_t ld = tid * kDocsPerThread + (__ffs(x) - 1);
+    const uint32_t sb = __float_as_uint((float)sm.acc[ld]);
+    bool take = sb > T;
+    if (sb == T) take = tie_rank++ < take_ties;
+    if (take) cand[atomicAdd(&sm.outn, 1u)] = ((uint64_t)sb << 32) | (uint64_t)(~(uint32_t)(d0 + ld));
+  }
+  __syncthreads();
+  if (tid == 0) p.cand_n[(size_t)q * p.n_blocks + b] = sm.outn;
+}
+
+// One workgroup (1024 threads) per query.
+struct MergeSmem {
+  uint64_t keys[1024];
+  uint32_t hist[256];
+  uint64_t prefix;
+  uint32_t remaining, outn;
+};
+
+__global__ void __launch_bounds__(1024) k_merge_topk(QueryParams p) {
+  __shared__ MergeSmem sm;
+  const uint32_t q = blockIdx.x, tid = threadIdx.x, k = p.k;
+  const uint32_t nb = p.n_blocks;
+  const uint64_t *cand = p.cand + (size_t)q * nb * k;
+  const uint32_t *cn = p.cand_n + (size_t)q * nb;
+  // total candidates
+  uint32_t M = 0;
+  for (uint32_t b = 0; b < nb; b++) M += cn[b];
+  const uint32_t kk = M < k ? M : k;
+  if (tid == 0) { sm.prefix = 0; sm.remaining = kk; sm.outn = 0; }
+  __syncthreads();
+  if (M > k) {
+    for (int pass = 0; pass < 8; pass++) {
+      const int sh = 56 - 8 * pass;
+      for (uint32_t i = tid; i < 256; i += blockDim.x) sm.hist[i] = 0;
+      __syncthreads();
+      const uint64_t prefix = sm.prefix;
+      const uint64_t hmask = pass == 0 ? 0ull : (~0ull << (sh + 8));
+      for (uint32_t b = 0; b < nb; b++) {
+        const uint32_t n = cn[b];
+        for (uint32_t i = tid; i < n; i += blockDim.x) {
+          const uint64_t key = cand[(size_t)b * k + i];
+          if ((key & hmask) == (prefix & hmask)) atomicAdd(&sm.hist[(key >> sh) & 255u], 1u);
+        }
+      }
+      __syncthreads();
+      if (tid == 0) {
+        uint32_t rem = sm.remaining, cum = 0;
+        for (int bin = 255; bin >= 0; bin--) {
+          const uint32_t h = sm.hist[bin];
+          if (cum + h >= rem) {
+            sm.prefix = prefix | ((uint64_t)bin << sh);
+            sm.remaining = rem - cum;
+            break;
+          }
+          cum += h;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const uint64_t T = (M > k) ? sm.prefix : 0ull;   // keys are unique: take key >= T
+  for (uint32_t b = 0; b < nb; b++) {
+    const uint32_t n = cn[b];
+    for (uint32_t i = tid; i < n; i += blockDim.x) {
+      const uint64_t key = cand[(size_t)b * k + i];
+      if (key >= T) {
+        const uint32_t pos = atomicAdd(&sm.outn, 1u);
+        if (pos < 1024) sm.keys[pos] = key;
+      }
+    }
+  }
+  __syncthreads();
+  // bitonic sort (descending) of kk keys padded to a power of two
+  uint32_t P = 1;
+  while (P < kk) P <<= 1;
+  for (uint32_t i = kk + tid; i < P; i += blockDim.x) sm.keys[i] = 0;
+  __syncthreads();
+  for (uint32_t size = 2; size <= P; size <<= 1) {
+    for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+      for (uint32_t i = tid; i < P; i += blockDim.x) {
+        const uint32_t j = i ^ stride;
+        if (j > i) {
+          const bool desc = (i & size) == 0;
+          const uint64_t a = sm.keys[i], c = sm.keys[j];
+          if (desc ? (a < c) : (a > c)) { sm.keys[i] = c; sm.keys[j] = a; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (uint32_t i = tid; i < kk; i += blockDim.x) {
+    const uint64_t key = sm.keys[i];
+    p.out_doc[(size_t)q * k + i] = ~(uint32_t)(key & 0xFFFFFFFFu);
+    p.out_score[(size_t)q * k + i] = __uint_as_float((uint32_t)(key >> 32));
+  }
+  if (tid == 0) p.out_n[q] = kk;
+}
+
+hipError_t launch_score_blocks(const QueryParams &p, hipStream_t s) {
+  hipLaunchKernelGGL(k_score_blocks, dim3(p.n_blocks, p.n_q), dim3(kScoreThreads), 0, s, p);
+  return hipGetLastError();
+}
+hipError_t launch_merge_topk(const QueryParams &p, hipStream_t s) {
+  hipLaunchKernelGGL(k_merge_topk, dim3(p.n_q), dim3(1024), 0, s, p);
+  return hipGetLastError();
+}
+
+}  // namespace tfidf

@@ -1,0 +1,1046 @@
+// tfidf_capi.hip — the C ABI (include/tfidf.h): index lifetime, corpus
+// staging, commit orchestration, query analysis and result materialisation.
+// All hot-path arithmetic runs in the kernels of kernels_*.hip; this file is
+// the host runtime around them (memory, streams, events, error mapping).
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/tfidf.h"
+#include "analysis.h"
+#include "tfidf_common.h"
+#include "tfidf_internal.h"
+
+namespace tfidf {
+hipError_t add_u64(uint64_t *v, uint64_t n, uint64_t delta, hipStream_t s);
+hipError_t sort_u64_desc(const uint64_t *in, uint64_t *out, uint64_t n, void *tmp, size_t *tmp_bytes, hipStream_t s);
+hipError_t sort_unique_keys128(const uint64_t *keys, uint64_t n, uint64_t *out, uint64_t *n_unique, hipStream_t s);
+hipError_t slot_to_canon(const uint64_t *dict, uint32_t C, const uint64_t *canon, uint64_t n_canon,
+                         uint32_t *canon_of_slot, hipStream_t s);
+hipError_t scatter_df_canon(const uint32_t *df, const uint32_t *canon_of_slot, uint32_t C, uint32_t *out,
+                            hipStream_t s);
+hipError_t gather_df_canon(const uint32_t *dfc, const uint32_t *canon_of_slot, uint32_t C, uint32_t *gdf,
+                           hipStream_t s);
+}  // namespace tfidf
+
+using namespace tfidf;
+
+// ---------------------------------------------------------------------------
+// errors
+
+static thread_local std::string g_err;
+
+static int fail(int code, const char *fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                                \
+  do {                                                                                               \
+    hipError_t _e = (expr);                                                                          \
+    if (_e != hipSuccess) return fail(TFIDF_E_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(_e), \
+                                      __FILE__, __LINE__);                                           \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// device buffers
+
+struct DevBuf {
+  void *p = nullptr;
+  size_t bytes = 0;
+  hipError_t reserve(size_t n) {
+    if (n <= bytes && p) return hipSuccess;
+    if (p) { hipFree(p); p = nullptr; bytes = 0; }
+    if (n == 0) n = 16;
+    hipError_t e = hipMalloc(&p, n);
+    if (e == hipSuccess) bytes = n;
+    return e;
+  }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <class T> T *as() const { return reinterpret_cast<T *>(p); }
+};
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    hipGetDevice(&prev);
+    if (prev != dev) hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    hipGetDevice(&cur);
+    if (prev >= 0 && cur != prev) hipSetDevice(prev);
+  }
+};
+
+enum { EV_START, EV_TOK, EV_L0, EV_LONG, EV_D0, EV_DF, EV_BSCAN, EV_CSCAN, EV_SCAT, EV_Q0, EV_Q1, EV_Q2, EV_N };
+
+struct tfidf_index {
+  tfidf_config cfg;
+  std::mutex mu;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[EV_N];
+  int num_cus = 256;
+
+  // staged corpus
+  DevBuf text, offsets;            // offsets: u64[n_staged + 1]
+  uint64_t text_bytes = 0, n_staged = 0;
+  std::vector<uint64_t> h_offsets{0};
+  std::string key_arena;
+  std::vector<uint64_t> key_off{0};
+  std::vector<uint8_t> key_synth;  // 1 = key is the decimal ordinal
+  std::vector<uint8_t> staged_live;
+  std::unordered_map<std::string, uint64_t> key_to_staged;
+  uint64_t n_dead = 0;
+
+  // committed
+  bool committed = false;
+  uint64_t n_docs = 0;
+  std::vector<uint32_t> live_map;  // committed -> staged (empty = identity)
+  DevBuf d_live_map;
+  uint32_t cap_log2 = 18, C = 0, range_shift = 15, R = 1, n_blocks = 0;
+  DevBuf dict, csr_col, csr_tf, doc_len, doc_nuniq, doc_norm, rsplit, long_list, counters, blk, col_ptr, post;
+  DevBuf lt_keys, lt_cnt, lt_g;
+  uint32_t lt_log2 = 0, lt_wgs = 64;
+  std::vector<uint64_t> h_dict;
+  std::vector<uint32_t> h_df;
+  uint64_t doc_count = 0, sum_ttf = 0, nnz = 0, num_terms = 0, long_docs = 0;
+  tfidf_commit_timing timing{};
+
+  // statistics in force
+  bool has_global = false;
+  std::vector<uint32_t> gdf;       // per slot (GLOBAL)
+  uint64_t g_doc_count = 0, g_sum_ttf = 0;
+  DevBuf canon_of_slot;
+  uint64_t n_canon = 0;
+
+  // query scratch
+  DevBuf q_off, q_slot, q_w, cache, cand, cand_n, out_doc, out_score, out_n, hits, hits_n, hits_c, hits_s, sort_tmp;
+  float last_ms_scoring = 0, last_ms_total = 0;
+};
+
+// ---------------------------------------------------------------------------
+
+extern "C" const char *tfidf_version(void) { return "libtfidf 0.1.0 (gfx950)"; }
+extern "C" const char *tfidf_last_error(void) { return g_err.c_str(); }
+
+extern "C" int tfidf_config_init(tfidf_config *cfg) {
+  if (!cfg) return fail(TFIDF_E_INVALID_ARG, "cfg is NULL");
+  cfg->k1 = 1.2f;
+  cfg->b = 0.75f;
+  cfg->stats_mode = TFIDF_STATS_SHARD;
+  cfg->device = 0;
+  cfg->vocab_capacity_log2 = 18;
+  cfg->max_token_len = 255;
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_create(const tfidf_config *cfg, tfidf_index **out) {
+  if (!cfg || !out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  if (cfg->max_token_len != 255) return fail(TFIDF_E_INVALID_ARG, "only max_token_len = 255 is supported");
+  uint32_t lg = cfg->vocab_capacity_log2 ? cfg->vocab_capacity_log2 : 18;
+  if (lg < 10 || lg > 21) return fail(TFIDF_E_INVALID_ARG, "vocab_capacity_log2 must be in [10, 21]");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(TFIDF_E_NO_DEVICE, "no HIP device");
+  if (cfg->device < 0 || cfg->device >= ndev) return fail(TFIDF_E_NO_DEVICE, "device %d out of range", cfg->device);
+  DeviceGuard g(cfg->device);
+  tfidf_index *ix = new tfidf_index();
+  ix->cfg = *cfg;
+  ix->cfg.vocab_capacity_log2 = lg;
+  ix->cap_log2 = lg;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, cfg->device) == hipSuccess) ix->num_cus = prop.multiProcessorCount;
+  if (hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ix;
+    return fail(TFIDF_E_HIP, "hipStreamCreate failed");
+  }
+  for (int i = 0; i < EV_N; i++) hipEventCreate(&ix->ev[i]);
+  hipError_t e = ix->offsets.reserve(64);
+  if (e != hipSuccess) { delete ix; return fail(TFIDF_E_OOM, "hipMalloc offsets"); }
+  uint64_t zero = 0;
+  hipMemcpy(ix->offsets.p, &zero, 8, hipMemcpyHostToDevice);
+  *out = ix;
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_destroy(tfidf_index *ix) {
+  if (!ix) return TFIDF_OK;
+  DeviceGuard g(ix->cfg.device);
+  hipStreamSynchronize(ix->stream);
+  DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->d_live_map, &ix->dict, &ix->csr_col, &ix->csr_tf, &ix->doc_len,
+                    &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->long_list, &ix->counters, &ix->blk,
+                    &ix->col_ptr, &ix->post, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->canon_of_slot,
+                    &ix->q_off, &ix->q_slot, &ix->q_w, &ix->cache, &ix->cand, &ix->cand_n, &ix->out_doc,
+                    &ix->out_score, &ix->out_n, &ix->hits, &ix->hits_n, &ix->hits_c, &ix->hits_s, &ix->sort_tmp};
+  for (DevBuf *b : bufs) b->release();
+  for (int i = 0; i < EV_N; i++) hipEventDestroy(ix->ev[i]);
+  hipStreamDestroy(ix->stream);
+  delete ix;
+  return TFIDF_OK;
+}
+
+// grow the device corpus to hold `extra` more bytes (plus read slack)
+static int grow_text(tfidf_index *ix, uint64_t extra) {
+  const uint64_t need = ix->text_bytes + extra + 128;
+  if (need <= ix->text.bytes) return TFIDF_OK;
+  uint64_t cap = ix->text.bytes ? ix->text.bytes : (1ull << 20);
+  while (cap < need) cap = cap + cap / 2 + (1ull << 20);
+  void *p = nullptr;
+  HIP_TRY(hipMalloc(&p, cap));
+  HIP_TRY(hipMemsetAsync(p, 0, cap, ix->stream));
+  if (ix->text.p && ix->text_bytes) HIP_TRY(hipMemcpyAsync(p, ix->text.p, ix->text_bytes, hipMemcpyDeviceToDevice, ix->stream));
+  HIP_TRY(hipStreamSynchronize(ix->stream));
+  ix->text.release();
+  ix->text.p = p;
+  ix->text.bytes = cap;
+  return TFIDF_OK;
+}
+
+static int grow_offsets(tfidf_index *ix, uint64_t extra_docs) {
+  const uint64_t need = (ix->n_staged + extra_docs + 1) * 8;
+  if (need <= ix->offsets.bytes) return TFIDF_OK;
+  uint64_t cap = ix->offsets.bytes;
+  while (cap < need) cap = cap * 2 + 64;
+  void *p = nullptr;
+  HIP_TRY(hipMalloc(&p, cap));
+  HIP_TRY(hipMemcpyAsync(p, ix->offsets.p, (ix->n_staged + 1) * 8, hipMemcpyDeviceToDevice, ix->stream));
+  HIP_TRY(hipStreamSynchronize(ix->stream));
+  ix->offsets.release();
+  ix->offsets.p = p;
+  ix->offsets.bytes = cap;
+  return TFIDF_OK;
+}
+
+static void register_key(tfidf_index *ix, const uint8_t *k, uint64_t n, bool synth) {
+  const uint64_t idx = ix->n_staged;
+  if (!synth) {
+    std::string key((const char *)k, n);
+    auto it = ix->key_to_staged.find(key);
+    if (it != ix->key_to_staged.end()) {       // updateDocument: delete-by-term, then add
+      if (ix->staged_live[it->second]) { ix->staged_live[it->second] = 0; ix->n_dead++; }
+      it->second = idx;
+    } else {
+      ix->key_to_staged.emplace(std::move(key), idx);
+    }
+    ix->key_arena.append((const char *)k, n);
+  }
+  ix->key_off.push_back(ix->key_arena.size());
+  ix->key_synth.push_back(synth ? 1 : 0);
+  ix->staged_live.push_back(1);
+}
+
+extern "C" int tfidf_add_docs(tfidf_index *ix, const uint8_t *utf8, const uint64_t *offsets, uint64_t n_docs,
+                              const uint8_t *keys, const uint64_t *key_offsets) {
+  if (!ix || (!utf8 && n_docs) || !offsets) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  if (keys && !key_offsets) return fail(TFIDF_E_INVALID_ARG, "keys without key_offsets");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DeviceGuard g(ix->cfg.device);
+  for (uint64_t i = 0; i < n_docs; i++)
+    if (offsets[i + 1] < offsets[i]) return fail(TFIDF_E_INVALID_ARG, "offsets must be non-decreasing");
+  const uint64_t nbytes = offsets[n_docs] - offsets[0];
+  if (ix->n_staged + n_docs >= 0xFFFFFFF0ull) return fail(TFIDF_E_CAPACITY, "more than 2^32 documents per shard");
+  int rc = grow_text(ix, nbytes);
+  if (rc) return rc;
+  rc = grow_offsets(ix, n_docs);
+  if (rc) return rc;
+  if (nbytes)
+    HIP_TRY(hipMemcpyAsync(ix->text.as<uint8_t>() + ix->text_bytes, utf8 + offsets[0], nbytes,
+                           hipMemcpyHostToDevice, ix->stream));
+  std::vector<uint64_t> no(n_docs);
+  for (uint64_t i = 0; i < n_docs; i++) no[i] = ix->text_bytes + (offsets[i + 1] - offsets[0]);
+  if (n_docs)
+    HIP_TRY(hipMemcpyAsync(ix->offsets.as<uint64_t>() + ix->n_staged + 1, no.data(), n_docs * 8,
+                           hipMemcpyHostToDevice, ix->stream));
+  HIP_TRY(hipStreamSynchronize(ix->stream));
+  for (uint64_t i = 0; i < n_docs; i++) {
+    if (keys) register_key(ix, keys + key_offsets[i], key_offsets[i + 1] - key_offsets[i], false);
+    else register_key(ix, nullptr, 0, true);
+    ix->h_offsets.push_back(no[i]);
+    ix->n_staged++;
+  }
+  ix->text_bytes += nbytes;
+  ix->committed = false;
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_add_docs_device(tfidf_index *ix, const void *d_utf8, const void *d_offsets, uint64_t n_docs,
+                                     uint64_t total_bytes) {
+  if (!ix || !d_offsets) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DeviceGuard g(ix->cfg.device);
+  if (ix->n_staged + n_docs >= 0xFFFFFFF0ull) return fail(TFIDF_E_CAPACITY, "more than 2^32 documents per shard");
+  std::vector<uint64_t> ho(n_docs + 1);
+  HIP_TRY(hipMemcpy(ho.data(), d_offsets, (n_docs + 1) * 8, hipMemcpyDeviceToHost));
+  if (ho[n_docs] - ho[0] != total_bytes) return fail(TFIDF_E_INVALID_ARG, "total_bytes != offsets[n] - offsets[0]");
+  int rc = grow_text(ix, total_bytes);
+  if (rc) return rc;
+  rc = grow_offsets(ix, n_docs);
+  if (rc) return rc;
+  if (total_bytes)
+    HIP_TRY(hipMemcpyAsync(ix->text.as<uint8_t>() + ix->text_bytes, (const uint8_t *)d_utf8 + ho[0], total_bytes,
+                           hipMemcpyDeviceToDevice, ix->stream));
+  uint64_t *dst = ix->offsets.as<uint64_t>() + ix->n_staged + 1;
+  HIP_TRY(hipMemcpyAsync(dst, (const uint64_t *)d_offsets + 1, n_docs * 8, hipMemcpyDeviceToDevice, ix->stream));
+  HIP_TRY(add_u64(dst, n_docs, ix->text_bytes - ho[0], ix->stream));
+  HIP_TRY(hipStreamSynchronize(ix->stream));
+  for (uint64_t i = 0; i < n_docs; i++) {
+    register_key(ix, nullptr, 0, true);
+    ix->h_offsets.push_back(ix->text_bytes + (ho[i + 1] - ho[0]));
+    ix->n_staged++;
+  }
+  ix->text_bytes += total_bytes;
+  ix->committed = false;
+  return TFIDF_OK;
+}
+
+// BM25 norm cache for the statistics in force (BM25Similarity.scorer, float ops)
+static void norm_cache(float k1, float b, float avgdl, float *cache) {
+  for (int i = 0; i < 256; i++) {
+    volatile float len = (float)byte4_to_int((uint32_t)i);
+    volatile float t1 = 1.0f - b;
+    volatile float t2 = b * len;
+    volatile float t3 = t2 / avgdl;
+    volatile float t4 = t1 + t3;
+    volatile float t5 = k1 * t4;
+    cache[i] = 1.0f / t5;
+  }
+}
+
+static float bm25_idf(uint64_t df, uint64_t doc_count) {
+  const double x = ((double)((int64_t)doc_count - (int64_t)df) + 0.5) / ((double)df + 0.5);
+  return (float)log(1.0 + x);
+}
+
+static uint64_t eff_doc_count(const tfidf_index *ix) { return ix->has_global ? ix->g_doc_count : ix->doc_count; }
+static uint64_t eff_sum_ttf(const tfidf_index *ix) { return ix->has_global ? ix->g_sum_ttf : ix->sum_ttf; }
+
+static int upload_cache(tfidf_index *ix) {
+  float c[256];
+  const uint64_t dc = eff_doc_count(ix);
+  if (dc == 0) {
+    for (int i = 0; i < 256; i++) c[i] = 0.0f;
+  } else {
+    const float avgdl = (float)((double)eff_sum_ttf(ix) / (double)dc);
+    norm_cache(ix->cfg.k1, ix->cfg.b, avgdl, c);
+  }
+  HIP_TRY(ix->cache.reserve(256 * 4));
+  HIP_TRY(hipMemcpyAsync(ix->cache.p, c, sizeof c, hipMemcpyHostToDevice, ix->stream));
+  HIP_TRY(hipStreamSynchronize(ix->stream));
+  return TFIDF_OK;
+}
+
+static float ev_ms(tfidf_index *ix, int a, int b) {
+  float ms = 0;
+  hipEventElapsedTime(&ms, ix->ev[a], ix->ev[b]);
+  return ms;
+}
+
+extern "C" int tfidf_commit(tfidf_index *ix) {
+  if (!ix) return fail(TFIDF_E_INVALID_ARG, "NULL index");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DeviceGuard g(ix->cfg.device);
+  hipStream_t s = ix->stream;
+  // live documents
+  ix->n_docs = ix->n_staged - ix->n_dead;
+  ix->live_map.clear();
+  if (ix->n_dead) {
+    ix->live_map.reserve(ix->n_docs);
+    for (uint64_t i = 0; i < ix->n_staged; i++)
+      if (ix->staged_live[i]) ix->live_map.push_back((uint32_t)i);
+    HIP_TRY(ix->d_live_map.reserve(ix->n_docs * 4 + 4));
+    HIP_TRY(hipMemcpyAsync(ix->d_live_map.p, ix->live_map.data(), ix->n_docs * 4, hipMemcpyHostToDevice, s));
+  }
+  const uint64_t N = ix->n_docs;
+  ix->C = 1u << ix->cap_log2;
+  const uint32_t C = ix->C;
+  const uint32_t RS = C < kRangeSlots ? C : kRangeSlots;
+  ix->range_shift = 0;
+  while ((1u << ix->range_shift) < RS) ix->range_shift++;
+  ix->R = C >> ix->range_shift;
+  ix->n_blocks = (uint32_t)((N + kBlockDocs - 1) / kBlockDocs);
+  const uint64_t row_cap = (ix->text_bytes + ix->n_staged) / 2 + 2;
+
+  HIP_TRY(ix->dict.reserve((size_t)2 * C * 8));
+  HIP_TRY(ix->csr_col.reserve(row_cap * 4));
+  HIP_TRY(ix->csr_tf.reserve(row_cap * 4));
+  HIP_TRY(ix->doc_len.reserve(N * 4 + 4));
+  HIP_TRY(ix->doc_nuniq.reserve(N * 4 + 4));
+  HIP_TRY(ix->doc_norm.reserve(N + 16));
+  HIP_TRY(ix->rsplit.reserve(N * ix->R * 4 + 4));
+  HIP_TRY(ix->long_list.reserve(N * 4 + 4));
+  HIP_TRY(ix->counters.reserve(64));
+  HIP_TRY(ix->blk.reserve((size_t)(ix->n_blocks + 1) * C * 4));
+  HIP_TRY(ix->col_ptr.reserve((size_t)(C + 1) * 8));
+
+  // counters: [0..2] stats u64, [3] err flags u32 + [3].hi first doc, [4] long_count
+  uint64_t *ctr = ix->counters.as<uint64_t>();
+  HIP_TRY(hipMemsetAsync(ix->counters.p, 0, 64, s));
+  HIP_TRY(hipMemsetAsync(ix->dict.p, 0, (size_t)2 * C * 8, s));
+
+  BuildParams bp{};
+  bp.text = ix->text.as<uint8_t>();
+  bp.offsets = ix->offsets.as<uint64_t>();
+  bp.live_map = ix->n_dead ? ix->d_live_map.as<uint32_t>() : nullptr;
+  bp.n_docs = N;
+  bp.dict = ix->dict.as<uint64_t>();
+  bp.cap_mask = C - 1;
+  bp.range_shift = ix->range_shift;
+  bp.n_ranges = ix->R;
+  bp.csr_col = ix->csr_col.as<uint32_t>();
+  bp.csr_tf = ix->csr_tf.as<uint32_t>();
+  bp.doc_len = ix->doc_len.as<uint32_t>();
+  bp.doc_nuniq = ix->doc_nuniq.as<uint32_t>();
+  bp.doc_norm = ix->doc_norm.as<uint8_t>();
+  bp.rsplit = ix->rsplit.as<uint32_t>();
+  bp.long_list = ix->long_list.as<uint32_t>();
+  bp.long_count = reinterpret_cast<uint32_t *>(ctr + 4);
+  bp.stats = reinterpret_cast<unsigned long long *>(ctr);
+  bp.err = reinterpret_cast<uint32_t *>(ctr + 3);
+
+  HIP_TRY(hipEventRecord(ix->ev[EV_START], s));
+  if (N) {
+    const uint64_t grid = std::min<uint64_t>(N, (uint64_t)ix->num_cus * 4);
+    HIP_TRY(launch_tokenize_short(bp, (int)grid, s));
+  }
+  HIP_TRY(hipEventRecord(ix->ev[EV_TOK], s));
+  uint32_t n_long = 0;
+  HIP_TRY(hipMemcpyAsync(&n_long, ctr + 4, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  ix->long_docs = n_long;
+  if (n_long) {
+    uint32_t lg = ix->cap_log2 + 1;
+    // table size needed by the longest long document (2x its token bound)
+    uint64_t maxlen = 0;
+    for (uint64_t d = 0; d < ix->n_staged; d++) maxlen = std::max(maxlen, ix->h_offsets[d + 1] - ix->h_offsets[d]);
+    uint32_t need = 10;
+    while (need < 22 && (1ull << need) < maxlen + 2) need++;
+    lg = std::min(lg, need);
+    ix->lt_log2 = lg;
+    const uint32_t wgs = std::min<uint32_t>(n_long, ix->lt_wgs);
+    HIP_TRY(ix->lt_keys.reserve((size_t)wgs * 2 * (1ull << lg) * 8));
+    HIP_TRY(ix->lt_cnt.reserve((size_t)wgs * (1ull << lg) * 4));
+    HIP_TRY(ix->lt_g.reserve((size_t)wgs * (1ull << lg) * 4));
+    bp.lt_keys = ix->lt_keys.as<uint64_t>();
+    bp.lt_cnt = ix->lt_cnt.as<uint32_t>();
+    bp.lt_g = ix->lt_g.as<uint32_t>();
+    bp.lt_slots_log2 = lg;
+    HIP_TRY(hipEventRecord(ix->ev[EV_L0], s));
+    HIP_TRY(launch_tokenize_long(bp, (int)wgs, s));
+    HIP_TRY(hipEventRecord(ix->ev[EV_LONG], s));
+  }
+  uint64_t hctr[5];
+  HIP_TRY(hipMemcpyAsync(hctr, ctr, sizeof hctr, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  const uint32_t err = (uint32_t)(hctr[3] & 0xFFFFFFFFu), err_doc = (uint32_t)(hctr[3] >> 32);
+  if (err) {
+    ix->committed = false;
+    if (err & kErrCapacity)
+      return fail(TFIDF_E_CAPACITY, "vocabulary exceeds 2^%u dictionary slots (raise vocab_capacity_log2)",
+                  ix->cap_log2);
+    if (err & kErrNonAscii)
+      return fail(TFIDF_E_UNSUPPORTED_INPUT, "document %u contains non-ASCII bytes (ASCII analyzer only)", err_doc);
+    if (err & kErrTokenTooLong)
+      return fail(TFIDF_E_UNSUPPORTED_INPUT, "document %u has a token longer than 255 chars", err_doc);
+    return fail(TFIDF_E_UNSUPPORTED_INPUT, "index build error flags 0x%x (doc %u)", err, err_doc);
+  }
+  ix->doc_count = hctr[0];
+  ix->sum_ttf = hctr[1];
+  ix->nnz = hctr[2];
+  if (ix->nnz >= 0xFFFFFFFFull) return fail(TFIDF_E_CAPACITY, "more than 2^32 postings per shard");
+  HIP_TRY(ix->post.reserve(ix->nnz * 8 + 8));
+
+  PostingParams pp{};
+  pp.offsets = bp.offsets;
+  pp.live_map = bp.live_map;
+  pp.n_docs = N;
+  pp.C = C;
+  pp.range_shift = ix->range_shift;
+  pp.n_ranges = ix->R;
+  pp.n_blocks = ix->n_blocks;
+  pp.csr_col = bp.csr_col;
+  pp.csr_tf = bp.csr_tf;
+  pp.rsplit = bp.rsplit;
+  pp.doc_norm = bp.doc_norm;
+  pp.blk = ix->blk.as<uint32_t>();
+  pp.col_ptr = ix->col_ptr.as<uint64_t>();
+  pp.post = ix->post.as<uint64_t>();
+  pp.err = bp.err;
+  HIP_TRY(hipEventRecord(ix->ev[EV_D0], s));
+  if (ix->n_blocks) {
+    HIP_TRY(launch_df_partial(pp, s));
+  } else {
+    HIP_TRY(hipMemsetAsync(ix->blk.p, 0, (size_t)C * 4, s));
+  }
+  HIP_TRY(hipEventRecord(ix->ev[EV_DF], s));
+  HIP_TRY(launch_block_scan(pp, s));
+  HIP_TRY(hipEventRecord(ix->ev[EV_BSCAN], s));
+  HIP_TRY(launch_col_scan(pp, s));
+  HIP_TRY(hipEventRecord(ix->ev[EV_CSCAN], s));
+  if (ix->n_blocks) HIP_TRY(launch_scatter(pp, s));
+  HIP_TRY(hipEventRecord(ix->ev[EV_SCAT], s));
+  // host mirrors for query analysis: dictionary keys + df
+  ix->h_dict.resize((size_t)2 * C);
+  ix->h_df.resize(C);
+  HIP_TRY(hipMemcpyAsync(ix->h_dict.data(), ix->dict.p, (size_t)2 * C * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(ix->h_df.data(), ix->blk.as<uint32_t>() + (size_t)ix->n_blocks * C, (size_t)C * 4,
+                         hipMemcpyDeviceToHost, s));
+  uint32_t err2 = 0;
+  HIP_TRY(hipMemcpyAsync(&err2, ctr + 3, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  if (err2 & kErrTfTooLarge) return fail(TFIDF_E_UNSUPPORTED_INPUT, "a term frequency exceeds 2^24 - 1");
+  uint64_t nt = 0;
+  for (uint32_t i = 0; i < C; i++) nt += ix->h_dict[2 * (size_t)i] != 0;
+  ix->num_terms = nt;
+
+  tfidf_commit_timing &t = ix->timing;
+  t.ms_tokenize = ev_ms(ix, EV_START, EV_TOK);
+  t.ms_long = n_long ? ev_ms(ix, EV_L0, EV_LONG) : 0.0f;
+  t.ms_df = ev_ms(ix, EV_D0, EV_DF);
+  t.ms_blockscan = ev_ms(ix, EV_DF, EV_BSCAN);
+  t.ms_colscan = ev_ms(ix, EV_BSCAN, EV_CSCAN);
+  t.ms_scatter = ev_ms(ix, EV_CSCAN, EV_SCAT);
+  t.ms_total = t.ms_tokenize + t.ms_long + ev_ms(ix, EV_D0, EV_SCAT);   // device time, host syncs excluded
+  t.text_bytes = ix->text_bytes;
+  t.num_docs = N;
+  t.nnz = ix->nnz;
+
+  ix->has_global = false;
+  ix->gdf.clear();
+  ix->committed = true;
+  return upload_cache(ix);
+}
+
+extern "C" int tfidf_get_commit_timing(const tfidf_index *ix, tfidf_commit_timing *out) {
+  if (!ix || !out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  *out = ix->timing;
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_stats(const tfidf_index *ix, tfidf_index_stats *out) {
+  if (!ix || !out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  out->num_docs = ix->committed ? ix->n_docs : 0;
+  out->doc_count = ix->doc_count;
+  out->sum_ttf = ix->sum_ttf;
+  out->num_terms = ix->num_terms;
+  out->nnz = ix->nnz;
+  out->long_docs = ix->long_docs;
+  out->text_bytes = ix->text_bytes;
+  const DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->dict, &ix->csr_col, &ix->csr_tf, &ix->doc_len,
+                          &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->blk, &ix->col_ptr, &ix->post};
+  uint64_t tot = 0;
+  for (const DevBuf *b : bufs) tot += b->bytes;
+  out->device_bytes = tot;
+  return TFIDF_OK;
+}
+
+// ---------------------------------------------------------------------------
+// dictionary (host mirror)
+
+static uint32_t host_lookup(const tfidf_index *ix, uint64_t lo, uint64_t hi) {
+  if (ix->C == 0) return kInvalidSlot;
+  const uint32_t mask = ix->C - 1;
+  uint32_t s = (uint32_t)key_hash(lo, hi) & mask;
+  for (uint32_t it = 0; it <= mask; it++) {
+    const uint64_t clo = ix->h_dict[2 * (size_t)s], chi = ix->h_dict[2 * (size_t)s + 1];
+    if (clo == 0) return kInvalidSlot;
+    if (clo == lo && chi == hi) return s;
+    s = (s + 1) & mask;
+  }
+  return kInvalidSlot;
+}
+
+struct PreparedQuery {
+  std::vector<uint32_t> slot;
+  std::vector<float> w;
+};
+
+static int prepare_query(tfidf_index *ix, const uint8_t *q, uint64_t n, PreparedQuery *pq) {
+  std::vector<QueryTerm> terms;
+  const int rc = parse_query(q, n, &terms);
+  if (rc == 1) return fail(TFIDF_E_UNSUPPORTED_QUERY, "non-ASCII query");
+  if (rc == 2) return fail(TFIDF_E_UNSUPPORTED_QUERY, "AND/OR/NOT operator words are not supported");
+  const uint64_t dc = eff_doc_count(ix);
+  for (const QueryTerm &t : terms) {
+    uint64_t lo, hi;
+    term_key(t.term, &lo, &hi);
+    const uint32_t s = host_lookup(ix, lo, hi);
+    if (s == kInvalidSlot || dc == 0) continue;        // absent term contributes nothing
+    const uint64_t df = ix->has_global ? ix->gdf[s] : ix->h_df[s];
+    const float idf = bm25_idf(df, dc);
+    volatile float w = t.boost * idf;                  // BM25Scorer: weight = boost * idf
+    const float wv = w;
+    pq->slot.push_back(s);
+    pq->w.push_back(wv);
+  }
+  return TFIDF_OK;
+}
+
+static int run_scoring(tfidf_index *ix, const std::vector<uint32_t> &qoff, const std::vector<uint32_t> &slots,
+                       const std::vector<float> &ws, uint32_t n_q, uint32_t k) {
+  hipStream_t s = ix->stream;
+  HIP_TRY(ix->q_off.reserve(qoff.size() * 4));
+  HIP_TRY(ix->q_slot.reserve(slots.size() * 4 + 4));
+  HIP_TRY(ix->q_w.reserve(ws.size() * 4 + 4));
+  HIP_TRY(hipMemcpyAsync(ix->q_off.p, qoff.data(), qoff.size() * 4, hipMemcpyHostToDevice, s));
+  if (!slots.empty()) {
+    HIP_TRY(hipMemcpyAsync(ix->q_slot.p, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(ix->q_w.p, ws.data(), ws.size() * 4, hipMemcpyHostToDevice, s));
+  }
+  QueryParams qp{};
+  qp.post = ix->post.as<uint64_t>();
+  qp.col_ptr = ix->col_ptr.as<uint64_t>();
+  qp.blk = ix->blk.as<uint32_t>();
+  qp.C = ix->C;
+  qp.n_blocks = ix->n_blocks;
+  qp.n_docs = ix->n_docs;
+  qp.cache = ix->cache.as<float>();
+  qp.q_off = ix->q_off.as<uint32_t>();
+  qp.q_slot = ix->q_slot.as<uint32_t>();
+  qp.q_w = ix->q_w.as<float>();
+  qp.n_q = n_q;
+  qp.k = k;
+  if (k) {
+    HIP_TRY(ix->cand.reserve((size_t)n_q * ix->n_blocks * k * 8 + 8));
+    HIP_TRY(ix->cand_n.reserve((size_t)n_q * ix->n_blocks * 4 + 4));
+    HIP_TRY(ix->out_doc.reserve((size_t)n_q * k * 4));
+    HIP_TRY(ix->out_score.reserve((size_t)n_q * k * 4));
+    HIP_TRY(ix->out_n.reserve((size_t)n_q * 4));
+    qp.cand = ix->cand.as<uint64_t>();
+    qp.cand_n = ix->cand_n.as<uint32_t>();
+    qp.out_doc = ix->out_doc.as<uint32_t>();
+    qp.out_score = ix->out_score.as<float>();
+    qp.out_n = ix->out_n.as<uint32_t>();
+  } else {
+    HIP_TRY(ix->hits.reserve((size_t)ix->n_blocks * kBlockDocs * 8 + 8));
+    HIP_TRY(ix->hits_n.reserve((size_t)ix->n_blocks * 4 + 4));
+    qp.hits = ix->hits.as<uint64_t>();
+    qp.hits_n = ix->hits_n.as<uint32_t>();
+  }
+  HIP_TRY(hipEventRecord(ix->ev[EV_Q0], s));
+  HIP_TRY(launch_score_blocks(qp, s));
+  HIP_TRY(hipEventRecord(ix->ev[EV_Q1], s));
+  if (k) HIP_TRY(launch_merge_topk(qp, s));
+  HIP_TRY(hipEventRecord(ix->ev[EV_Q2], s));
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_search(tfidf_index *ix, const uint8_t *q, uint64_t q_len, uint32_t k, uint32_t *doc_ids,
+                            float *scores, uint64_t cap, uint64_t *n_out) {
+  if (!ix || (!q && q_len) || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  *n_out = 0;
+  std::lock_guard<std::mutex> lk(ix->mu);
+  if (!ix->committed) return fail(TFIDF_E_STATE, "search before commit");
+  if (k > 1024) return fail(TFIDF_E_INVALID_ARG, "k must be <= 1024 (0 = all hits)");
+  DeviceGuard g(ix->cfg.device);
+  PreparedQuery pq;
+  int rc = prepare_query(ix, q, q_len, &pq);
+  if (rc) return rc;
+  if (pq.slot.empty() || ix->n_docs == 0) { ix->last_ms_scoring = ix->last_ms_total = 0; return TFIDF_OK; }
+  std::vector<uint32_t> qoff{0, (uint32_t)pq.slot.size()};
+  rc = run_scoring(ix, qoff, pq.slot, pq.w, 1, k);
+  if (rc) return rc;
+  hipStream_t s = ix->stream;
+  if (k) {
+    uint32_t n = 0;
+    HIP_TRY(hipMemcpyAsync(&n, ix->out_n.p, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    *n_out = n;
+    if (n > cap) return fail(TFIDF_E_BUFFER, "need %u result slots", n);
+    if (n) {
+      HIP_TRY(hipMemcpyAsync(doc_ids, ix->out_doc.p, n * 4, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipMemcpyAsync(scores, ix->out_score.p, n * 4, hipMemcpyDeviceToHost, s));
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    ix->last_ms_scoring = ev_ms(ix, EV_Q0, EV_Q1);
+    ix->last_ms_total = ev_ms(ix, EV_Q0, EV_Q2);
+    return TFIDF_OK;
+  }
+  // all hits: compact the per-block hit keys, radix-sort descending
+  std::vector<uint32_t> hn(ix->n_blocks);
+  HIP_TRY(hipMemcpyAsync(hn.data(), ix->hits_n.p, hn.size() * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  uint64_t H = 0;
+  for (uint32_t v : hn) H += v;
+  *n_out = H;
+  if (H > cap) return fail(TFIDF_E_BUFFER, "need %llu result slots", (unsigned long long)H);
+  if (H == 0) return TFIDF_OK;
+  HIP_TRY(ix->hits_c.reserve(H * 8));
+  HIP_TRY(ix->hits_s.reserve(H * 8));
+  uint64_t off = 0;
+  for (uint32_t b = 0; b < ix->n_blocks; b++) {
+    if (hn[b])
+      HIP_TRY(hipMemcpyAsync(ix->hits_c.as<uint64_t>() + off, ix->hits.as<uint64_t>() + (size_t)b * kBlockDocs,
+                             (size_t)hn[b] * 8, hipMemcpyDeviceToDevice, s));
+    off += hn[b];
+  }
+  size_t tb = 0;
+  HIP_TRY(sort_u64_desc(ix->hits_c.as<uint64_t>(), ix->hits_s.as<uint64_t>(), H, nullptr, &tb, s));
+  HIP_TRY(ix->sort_tmp.reserve(tb));
+  HIP_TRY(sort_u64_desc(ix->hits_c.as<uint64_t>(), ix->hits_s.as<uint64_t>(), H, ix->sort_tmp.p, &tb, s));
+  std::vector<uint64_t> keys(H);
+  HIP_TRY(hipMemcpyAsync(keys.data(), ix->hits_s.p, H * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipEventRecord(ix->ev[EV_Q2], s));
+  HIP_TRY(hipStreamSynchronize(s));
+  for (uint64_t i = 0; i < H; i++) {
+    doc_ids[i] = ~(uint32_t)(keys[i] & 0xFFFFFFFFu);
+    uint32_t sb = (uint32_t)(keys[i] >> 32);
+    memcpy(&scores[i], &sb, 4);
+  }
+  ix->last_ms_scoring = ev_ms(ix, EV_Q0, EV_Q1);
+  ix->last_ms_total = ev_ms(ix, EV_Q0, EV_Q2);
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const uint64_t *q_offsets, uint32_t n_q,
+                                  uint32_t k, uint32_t *doc_ids, float *scores, uint32_t *counts) {
+  if (!ix || !q_offsets || !doc_ids || !scores || !counts) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  if (k == 0 || k > 1024) return fail(TFIDF_E_INVALID_ARG, "batch search needs 1 <= k <= 1024");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  if (!ix->committed) return fail(TFIDF_E_STATE, "search before commit");
+  DeviceGuard g(ix->cfg.device);
+  std::vector<uint32_t> qoff{0}, slots;
+  std::vector<float> ws;
+  for (uint32_t i = 0; i < n_q; i++) {
+    PreparedQuery pq;
+    int rc = prepare_query(ix, q_utf8 + q_offsets[i], q_offsets[i + 1] - q_offsets[i], &pq);
+    if (rc) return rc;
+    slots.insert(slots.end(), pq.slot.begin(), pq.slot.end());
+    ws.insert(ws.end(), pq.w.begin(), pq.w.end());
+    qoff.push_back((uint32_t)slots.size());
+  }
+  if (n_q == 0) return TFIDF_OK;
+  if (ix->n_docs == 0) {
+    memset(counts, 0, n_q * 4);
+    return TFIDF_OK;
+  }
+  int rc = run_scoring(ix, qoff, slots, ws, n_q, k);
+  if (rc) return rc;
+  hipStream_t s = ix->stream;
+  HIP_TRY(hipMemcpyAsync(counts, ix->out_n.p, (size_t)n_q * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(doc_ids, ix->out_doc.p, (size_t)n_q * k * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(scores, ix->out_score.p, (size_t)n_q * k * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  ix->last_ms_scoring = ev_ms(ix, EV_Q0, EV_Q1);
+  ix->last_ms_total = ev_ms(ix, EV_Q0, EV_Q2);
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_last_search_ms(const tfidf_index *ix, float *ms_scoring, float *ms_total) {
+  if (!ix) return fail(TFIDF_E_INVALID_ARG, "NULL index");
+  if (ms_scoring) *ms_scoring = ix->last_ms_scoring;
+  if (ms_total) *ms_total = ix->last_ms_total;
+  return TFIDF_OK;
+}
+
+// ---------------------------------------------------------------------------
+// inspection
+
+static uint64_t staged_of(const tfidf_index *ix, uint64_t doc) {
+  return ix->live_map.empty() ? doc : ix->live_map[doc];
+}
+
+extern "C" int tfidf_doc_key(const tfidf_index *ix, uint64_t doc, uint8_t *buf, uint64_t cap, uint64_t *n_out) {
+  if (!ix || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  if (!ix->committed || doc >= ix->n_docs) return fail(TFIDF_E_INVALID_ARG, "doc out of range");
+  const uint64_t st = staged_of(ix, doc);
+  std::string k;
+  if (ix->key_synth[st]) k = std::to_string(st);
+  else k.assign(ix->key_arena.data() + ix->key_off[st], ix->key_off[st + 1] - ix->key_off[st]);
+  *n_out = k.size();
+  if (k.size() > cap) return fail(TFIDF_E_BUFFER, "key needs %zu bytes", k.size());
+  if (buf && !k.empty()) memcpy(buf, k.data(), k.size());
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_doc_len(tfidf_index *ix, uint64_t doc, uint32_t *len, uint8_t *norm) {
+  if (!ix) return fail(TFIDF_E_INVALID_ARG, "NULL index");
+  if (!ix->committed || doc >= ix->n_docs) return fail(TFIDF_E_INVALID_ARG, "doc out of range");
+  DeviceGuard g(ix->cfg.device);
+  uint32_t l = 0;
+  uint8_t n = 0;
+  HIP_TRY(hipMemcpy(&l, ix->doc_len.as<uint32_t>() + doc, 4, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(&n, ix->doc_norm.as<uint8_t>() + doc, 1, hipMemcpyDeviceToHost));
+  if (len) *len = l;
+  if (norm) *norm = n;
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_doc_terms(tfidf_index *ix, uint64_t doc, char *terms, uint64_t terms_cap, uint32_t *tfs,
+                               uint64_t cap, uint64_t *n_out) {
+  if (!ix || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  if (!ix->committed || doc >= ix->n_docs) return fail(TFIDF_E_INVALID_ARG, "doc out of range");
+  DeviceGuard g(ix->cfg.device);
+  uint32_t nu = 0;
+  HIP_TRY(hipMemcpy(&nu, ix->doc_nuniq.as<uint32_t>() + doc, 4, hipMemcpyDeviceToHost));
+  const uint64_t st = staged_of(ix, doc);
+  const uint64_t base = csr_row_base(ix->h_offsets.data(), st);
+  std::vector<uint32_t> col(nu), tf(nu);
+  if (nu) {
+    HIP_TRY(hipMemcpy(col.data(), ix->csr_col.as<uint32_t>() + base, nu * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(tf.data(), ix->csr_tf.as<uint32_t>() + base, nu * 4, hipMemcpyDeviceToHost));
+  }
+  std::vector<std::pair<std::string, uint32_t>> rows;
+  for (uint32_t i = 0; i < nu; i++) {
+    char b[32];
+    const uint64_t lo = ix->h_dict[2 * (size_t)col[i]], hi = ix->h_dict[2 * (size_t)col[i] + 1];
+    uint32_t n = key_decode(lo, hi, b);
+    std::string s;
+    if (n) s.assign(b, n);
+    else {
+      char hx[48];
+      snprintf(hx, sizeof hx, "#%016llx%016llx", (unsigned long long)hi, (unsigned long long)lo);
+      s = hx;
+    }
+    rows.emplace_back(std::move(s), tf[i]);
+  }
+  std::sort(rows.begin(), rows.end());
+  uint64_t need = 0;
+  for (auto &r : rows) need += r.first.size() + 1;
+  *n_out = rows.size();
+  if (need > terms_cap || rows.size() > cap) return fail(TFIDF_E_BUFFER, "buffers too small");
+  uint64_t p = 0;
+  for (size_t i = 0; i < rows.size(); i++) {
+    memcpy(terms + p, rows[i].first.c_str(), rows[i].first.size() + 1);
+    p += rows[i].first.size() + 1;
+    tfs[i] = rows[i].second;
+  }
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_term_df(tfidf_index *ix, const uint8_t *term, uint64_t len, uint64_t *df_local,
+                             uint64_t *df_effective) {
+  if (!ix || (!term && len)) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
+  std::string t((const char *)term, len);
+  uint64_t lo, hi;
+  term_key(t, &lo, &hi);
+  const uint32_t s = host_lookup(ix, lo, hi);
+  const uint64_t l = s == kInvalidSlot ? 0 : ix->h_df[s];
+  if (df_local) *df_local = l;
+  if (df_effective) *df_effective = (s != kInvalidSlot && ix->has_global) ? ix->gdf[s] : l;
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_term_key(const uint8_t *term, uint64_t len, uint64_t *lo, uint64_t *hi) {
+  if ((!term && len) || !lo || !hi) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  std::string t((const char *)term, len);
+  term_key(t, lo, hi);
+  return TFIDF_OK;
+}
+
+// ---------------------------------------------------------------------------
+// GLOBAL statistics
+
+extern "C" int tfidf_vocab_size(const tfidf_index *ix, uint64_t *n) {
+  if (!ix || !n) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  *n = ix->committed ? ix->num_terms : 0;
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_vocab_export_device(tfidf_index *ix, void *d_keys, void *d_df, uint64_t cap, uint64_t *n_out) {
+  if (!ix || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
+  DeviceGuard g(ix->cfg.device);
+  *n_out = ix->num_terms;
+  if (ix->num_terms > cap) return fail(TFIDF_E_BUFFER, "need %llu keys", (unsigned long long)ix->num_terms);
+  // sorted (hi, lo) key list of this shard + df, assembled from the host mirror
+  std::vector<std::pair<std::pair<uint64_t, uint64_t>, uint32_t>> v;
+  v.reserve(ix->num_terms);
+  for (uint32_t s = 0; s < ix->C; s++)
+    if (ix->h_dict[2 * (size_t)s])
+      v.push_back({{ix->h_dict[2 * (size_t)s + 1], ix->h_dict[2 * (size_t)s]}, ix->h_df[s]});
+  std::sort(v.begin(), v.end());
+  std::vector<uint64_t> keys(2 * v.size());
+  std::vector<uint32_t> df(v.size());
+  for (size_t i = 0; i < v.size(); i++) {
+    keys[2 * i] = v[i].first.second;
+    keys[2 * i + 1] = v[i].first.first;
+    df[i] = v[i].second;
+  }
+  if (!v.empty()) {
+    if (d_keys) HIP_TRY(hipMemcpy(d_keys, keys.data(), keys.size() * 8, hipMemcpyHostToDevice));
+    if (d_df) HIP_TRY(hipMemcpy(d_df, df.data(), df.size() * 4, hipMemcpyHostToDevice));
+  }
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_vocab_canonicalize_device(tfidf_index *ix, const void *d_all_keys, uint64_t n_all,
+                                               void *d_df_canonical, uint64_t cap, uint64_t *n_canonical) {
+  if (!ix || !n_canonical) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
+  DeviceGuard g(ix->cfg.device);
+  hipStream_t s = ix->stream;
+  DevBuf canon;
+  HIP_TRY(canon.reserve(n_all * 16 + 16));
+  uint64_t nu = 0;
+  HIP_TRY(sort_unique_keys128((const uint64_t *)d_all_keys, n_all, canon.as<uint64_t>(), &nu, s));
+  *n_canonical = nu;
+  if (nu > cap) { canon.release(); return fail(TFIDF_E_BUFFER, "need %llu canonical slots", (unsigned long long)nu); }
+  HIP_TRY(ix->canon_of_slot.reserve((size_t)ix->C * 4));
+  HIP_TRY(slot_to_canon(ix->dict.as<uint64_t>(), ix->C, canon.as<uint64_t>(), nu, ix->canon_of_slot.as<uint32_t>(), s));
+  if (d_df_canonical) {
+    HIP_TRY(hipMemsetAsync(d_df_canonical, 0, nu * 4, s));
+    HIP_TRY(scatter_df_canon(ix->blk.as<uint32_t>() + (size_t)ix->n_blocks * ix->C, ix->canon_of_slot.as<uint32_t>(),
+                             ix->C, (uint32_t *)d_df_canonical, s));
+  }
+  HIP_TRY(hipStreamSynchronize(s));
+  canon.release();
+  ix->n_canon = nu;
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_set_global_stats_device(tfidf_index *ix, const void *d_df_canonical, uint64_t n_canonical,
+                                             uint64_t doc_count, uint64_t sum_ttf) {
+  if (!ix || !d_df_canonical) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
+  if (n_canonical != ix->n_canon) return fail(TFIDF_E_STATE, "canonical vocabulary size mismatch");
+  DeviceGuard g(ix->cfg.device);
+  hipStream_t s = ix->stream;
+  DevBuf gd;
+  HIP_TRY(gd.reserve((size_t)ix->C * 4));
+  HIP_TRY(gather_df_canon((const uint32_t *)d_df_canonical, ix->canon_of_slot.as<uint32_t>(), ix->C,
+                          gd.as<uint32_t>(), s));
+  ix->gdf.resize(ix->C);
+  HIP_TRY(hipMemcpyAsync(ix->gdf.data(), gd.p, (size_t)ix->C * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  gd.release();
+  ix->has_global = true;
+  ix->g_doc_count = doc_count;
+  ix->g_sum_ttf = sum_ttf;
+  return upload_cache(ix);
+}
+
+extern "C" int tfidf_set_global_stats(tfidf_index *ix, const uint64_t *keys_lohi, const uint64_t *df, uint64_t n,
+                                      uint64_t doc_count, uint64_t sum_ttf) {
+  if (!ix || (n && (!keys_lohi || !df))) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
+  DeviceGuard g(ix->cfg.device);
+  ix->gdf.assign(ix->C, 0);
+  for (uint32_t s = 0; s < ix->C; s++) ix->gdf[s] = ix->h_df[s];  // keys not listed keep local df
+  for (uint64_t i = 0; i < n; i++) {
+    const uint32_t s = host_lookup(ix, keys_lohi[2 * i], keys_lohi[2 * i + 1]);
+    if (s != kInvalidSlot) ix->gdf[s] = (uint32_t)df[i];
+  }
+  ix->has_global = true;
+  ix->g_doc_count = doc_count;
+  ix->g_sum_ttf = sum_ttf;
+  return upload_cache(ix);
+}
+
+extern "C" int tfidf_clear_global_stats(tfidf_index *ix) {
+  if (!ix) return fail(TFIDF_E_INVALID_ARG, "NULL index");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DeviceGuard g(ix->cfg.device);
+  ix->has_global = false;
+  ix->gdf.clear();
+  return ix->committed ? upload_cache(ix) : TFIDF_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Leader.start merge (host: it merges per-worker result lists by name)
+
+extern "C" int tfidf_leader_merge(const uint8_t *names, const uint64_t *offsets, uint64_t n, const double *scores,
+                                  uint64_t *out_first, double *out_sum, uint64_t *n_out) {
+  if (!n_out || (n && (!names || !offsets || !scores || !out_first || !out_sum)))
+    return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  std::unordered_map<std::string, size_t> pos;
+  std::vector<std::pair<std::string, uint64_t>> order;
+  std::vector<double> sum;
+  for (uint64_t i = 0; i < n; i++) {
+    std::string k((const char *)names + offsets[i], offsets[i + 1] - offsets[i]);
+    auto it = pos.find(k);
+    if (it == pos.end()) {                   // HashMap.merge: first value stored as-is
+      pos.emplace(k, sum.size());
+      order.emplace_back(std::move(k), i);
+      sum.push_back(scores[i]);
+    } else {
+      sum[it->second] += scores[i];          // Double::sum in response order
+    }
+  }
+  std::vector<size_t> idx(order.size());
+  for (size_t i = 0; i < idx.size(); i++) idx[i] = i;
+  std::sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return order[a].first < order[b].first; });
+  for (size_t r = 0; r < idx.size(); r++) {
+    out_first[r] = order[idx[r]].second;
+    out_sum[r] = sum[idx[r]];
+  }
+  *n_out = idx.size();
+  return TFIDF_OK;
+}
+
+// ---------------------------------------------------------------------------
+// synthetic corpus
+
+extern "C" int tfidf_synth_corpus(int device, uint64_t seed, uint64_t n_docs, uint64_t doc_base, const double *cdf,
+                                  uint32_t V, uint32_t len_min, uint32_t len_max, void **d_text, void **d_offsets,
+                                  uint64_t *total_bytes) {
+  if (!cdf || !d_text || !d_offsets || !total_bytes || V == 0 || len_max < len_min)
+    return fail(TFIDF_E_INVALID_ARG, "bad argument");
+  if (len_max >= (1u << 20) - 1) return fail(TFIDF_E_INVALID_ARG, "len_max must be < 2^20 - 1");
+  DeviceGuard g(device);
+  hipStream_t s;
+  HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  const uint32_t G = 1u << 16;
+  std::vector<uint32_t> guide(G + 1);
+  for (uint32_t i = 0; i <= G; i++) {
+    const double u = (double)i / (double)G;
+    guide[i] = (uint32_t)(std::upper_bound(cdf, cdf + V, u) - cdf);
+    if (guide[i] > V - 1) guide[i] = V - 1;
+  }
+  DevBuf dcdf, dguide, bytes;
+  HIP_TRY(dcdf.reserve((size_t)V * 8));
+  HIP_TRY(dguide.reserve((size_t)(G + 1) * 4));
+  HIP_TRY(bytes.reserve(n_docs * 8 + 8));
+  void *off = nullptr;
+  HIP_TRY(hipMalloc(&off, (n_docs + 1) * 8));
+  HIP_TRY(hipMemcpyAsync(dcdf.p, cdf, (size_t)V * 8, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipMemcpyAsync(dguide.p, guide.data(), (size_t)(G + 1) * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(synth_doc_lengths(seed, n_docs, doc_base, dcdf.as<double>(), dguide.as<uint32_t>(), V, len_min, len_max,
+                            bytes.as<uint64_t>(), s));
+  HIP_TRY(exclusive_scan_u64(bytes.as<uint64_t>(), (uint64_t *)off, n_docs, s));
+  uint64_t tot = 0;
+  HIP_TRY(hipMemcpyAsync(&tot, (uint64_t *)off + n_docs, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  void *txt = nullptr;
+  HIP_TRY(hipMalloc(&txt, tot + 128));
+  HIP_TRY(hipMemsetAsync(txt, 0, tot + 128, s));
+  HIP_TRY(synth_doc_text(seed, n_docs, doc_base, dcdf.as<double>(), dguide.as<uint32_t>(), V, len_min, len_max,
+                         (const uint64_t *)off, (uint8_t *)txt, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  dcdf.release();
+  dguide.release();
+  bytes.release();
+  hipStreamDestroy(s);
+  *d_text = txt;
+  *d_offsets = off;
+  *total_bytes = tot;
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_device_free(int device, void *d_ptr) {
+  DeviceGuard g(device);
+  if (d_ptr) HIP_TRY(hipFree(d_ptr));
+  return TFIDF_OK;
+}

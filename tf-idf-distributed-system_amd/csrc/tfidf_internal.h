@@ -1,0 +1,122 @@
+// tfidf_internal.h — kernel parameter blocks and launch wrappers (host side).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "tfidf_common.h"
+
+namespace tfidf {
+
+// Error flags raised by kernels (device word err[0]; err[1] = first doc).
+constexpr uint32_t kErrNonAscii = 1u;
+constexpr uint32_t kErrTokenTooLong = 2u;
+constexpr uint32_t kErrCapacity = 4u;
+constexpr uint32_t kErrTfTooLarge = 8u;
+constexpr uint32_t kErrLongScratch = 16u;
+
+// Short-document path limits (workgroup per document, LDS tables).
+constexpr uint32_t kShortMaxBytes = 4096;
+constexpr uint32_t kShortMaxTokens = 1024;
+constexpr uint32_t kShortTable = 1024;
+// Long-document path: chunks of kChunk bytes, global per-document table.
+constexpr uint32_t kChunk = 2048;
+constexpr uint32_t kPreMargin = 64;
+constexpr uint32_t kPostMargin = 320;
+
+struct BuildParams {
+  const uint8_t *text;        // corpus base (device)
+  const uint64_t *offsets;    // staged doc offsets [n_staged + 1]
+  const uint32_t *live_map;   // committed doc -> staged doc (nullptr = identity)
+  uint64_t n_docs;            // committed docs
+  uint64_t *dict;             // 2*C u64: [2s] = key lo, [2s+1] = key hi
+  uint32_t cap_mask;          // C - 1
+  uint32_t range_shift;       // log2(range size)
+  uint32_t n_ranges;          // R = C >> range_shift
+  uint32_t *csr_col;          // padded CSR rows: dictionary slot per entry
+  uint32_t *csr_tf;           // tf per entry
+  uint32_t *doc_len;          // tokens per doc (field length)
+  uint32_t *doc_nuniq;        // distinct terms per doc
+  uint8_t *doc_norm;          // SmallFloat.intToByte4(len)
+  uint32_t *rsplit;           // [n_docs][R] inclusive end of each range segment in the row
+  uint32_t *long_list;        // docs deferred to the long path
+  uint32_t *long_count;
+  unsigned long long *stats;  // [0] docCount, [1] sumTotalTermFreq, [2] nnz
+  uint32_t *err;              // [0] flags, [1] first offending doc
+  // long path scratch (one table region per workgroup)
+  uint64_t *lt_keys;          // 2 * lt_slots per workgroup
+  uint32_t *lt_cnt;           // lt_slots per workgroup
+  uint32_t *lt_g;             // lt_slots per workgroup
+  uint32_t lt_slots_log2;     // table slots per workgroup (max)
+};
+
+__host__ __device__ inline uint64_t csr_row_base(const uint64_t *offsets, uint64_t src) {
+  // A document of L bytes holds at most ceil(L/2) tokens, so rows laid out at
+  // floor((offset + src) / 2) never overlap.
+  return (offsets[src] + src) >> 1;
+}
+
+struct PostingParams {
+  const uint64_t *offsets;
+  const uint32_t *live_map;
+  uint64_t n_docs;
+  uint32_t C;                 // dictionary slots
+  uint32_t range_shift, n_ranges;
+  uint32_t n_blocks;          // ceil(n_docs / kBlockDocs)
+  const uint32_t *csr_col, *csr_tf, *rsplit;
+  const uint8_t *doc_norm;
+  uint32_t *blk;              // [(n_blocks + 1) * C]: counts -> exclusive offsets; row n_blocks = df
+  uint64_t *col_ptr;          // [C + 1]
+  uint64_t *post;             // [nnz]: doc | (tf << 8 | norm) << 32
+  uint32_t *err;
+};
+
+// --- launch wrappers (kernels_index.hip) ---
+hipError_t launch_tokenize_short(const BuildParams &p, int grid, hipStream_t s);
+hipError_t launch_tokenize_long(const BuildParams &p, int grid, hipStream_t s);
+hipError_t launch_df_partial(const PostingParams &p, hipStream_t s);
+hipError_t launch_block_scan(const PostingParams &p, hipStream_t s);
+hipError_t launch_col_scan(const PostingParams &p, hipStream_t s);
+hipError_t launch_scatter(const PostingParams &p, hipStream_t s);
+
+// --- query scoring (kernels_query.hip) ---
+struct QueryParams {
+  const uint64_t *post;
+  const uint64_t *col_ptr;
+  const uint32_t *blk;        // exclusive block offsets [(n_blocks + 1) * C]
+  uint32_t C;
+  uint32_t n_blocks;
+  uint64_t n_docs;
+  const float *cache;         // 256 floats (BM25 norm cache)
+  const uint32_t *q_off;      // [n_q + 1] into q_slot / q_w
+  const uint32_t *q_slot;     // dictionary slot per query term (kInvalidSlot = absent)
+  const float *q_w;           // BM25 weight per query term (boost * idf)
+  uint32_t n_q;
+  uint32_t k;                 // top-k (1..1024); 0 = all hits
+  // outputs
+  uint64_t *cand;             // [n_q][n_blocks][k] candidate keys (score bits << 32 | ~doc)
+  uint32_t *cand_n;           // [n_q][n_blocks]
+  uint32_t *out_doc;          // [n_q][k]
+  float *out_score;           // [n_q][k]
+  uint32_t *out_n;            // [n_q]
+  // all-hits mode
+  uint64_t *hits;             // [n_blocks * kBlockDocs] keys (score bits << 32 | ~doc)
+  uint32_t *hits_n;           // [n_blocks]
+};
+hipError_t launch_score_blocks(const QueryParams &p, hipStream_t s);
+hipError_t launch_merge_topk(const QueryParams &p, hipStream_t s);
+
+// --- distributed vocabulary helpers (kernels_vocab.hip) ---
+hipError_t launch_vocab_export(const uint64_t *dict, const uint32_t *df, uint32_t C, uint64_t *keys_out,
+                               uint32_t *df_out, uint32_t *count, hipStream_t s);
+
+// --- synthetic corpus (kernels_synth.hip) ---
+hipError_t synth_doc_lengths(uint64_t seed, uint64_t n_docs, uint64_t doc_base, const double *cdf,
+                             const uint32_t *guide, uint32_t V, uint32_t len_min, uint32_t len_max,
+                             uint64_t *bytes_out, hipStream_t s);
+hipError_t synth_doc_text(uint64_t seed, uint64_t n_docs, uint64_t doc_base, const double *cdf,
+                          const uint32_t *guide, uint32_t V, uint32_t len_min, uint32_t len_max,
+                          const uint64_t *offsets, uint8_t *text, hipStream_t s);
+hipError_t exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, hipStream_t s);
+
+}  // namespace tfidf

@@ -1,0 +1,117 @@
+"""Multi-GPU orchestration: documents sharded across ranks (one process per
+GPU), exchanges over torch.distributed — backend "nccl" is RCCL over xGMI on
+MI355X; "gloo" is used by the CPU tests.
+
+Two modes:
+  * SHARD (the reference's N-worker semantics, Leader.java:39-92): every rank
+    scores with its own statistics; results are merged by document name.
+    No data-path collective.
+  * GLOBAL (the reference's 1-worker semantics on a sharded corpus):
+      1. vocabulary agreement: all-gather every shard's sorted term keys,
+         sorted union on device -> canonical term ids;
+      2. all-reduce (SUM) of the canonical DF vector + {docCount, sumTTF};
+      3. per-rank top-k with global doc ids (shard base + local), all-gather,
+         merge by (score desc, doc asc).
+
+The engine is passed in as an adapter (HipShardAdapter in production; the
+CPU tests inject an oracle-backed adapter with the same methods).
+"""
+import torch
+import torch.distributed as dist
+
+
+class HipShardAdapter:
+    """Adapter over a ShardIndex whose buffers live on ``device`` (cuda:N)."""
+
+    def __init__(self, shard, device, doc_base=0):
+        self.shard = shard
+        self.device = torch.device(device)
+        self.doc_base = doc_base
+
+    def local_stats(self):
+        s = self.shard.stats()
+        return int(s["doc_count"]), int(s["sum_ttf"]), int(s["num_docs"])
+
+    def export_vocab(self):
+        n = self.shard.vocab_size()
+        keys = torch.zeros((max(n, 1), 2), dtype=torch.int64, device=self.device)
+        df = torch.zeros(max(n, 1), dtype=torch.int32, device=self.device)
+        torch.cuda.synchronize(self.device)
+        self.shard.vocab_export_device(keys.data_ptr(), df.data_ptr(), n)
+        return keys[:n], df[:n]
+
+    def canonicalize(self, all_keys):
+        m = all_keys.shape[0]
+        dfc = torch.zeros(max(m, 1), dtype=torch.int32, device=self.device)
+        torch.cuda.synchronize(self.device)
+        n = self.shard.vocab_canonicalize_device(all_keys.data_ptr(), m, dfc.data_ptr(), max(m, 1))
+        return dfc[:n]
+
+    def import_global(self, dfc, doc_count, sum_ttf):
+        dfc = dfc.contiguous()
+        torch.cuda.synchronize(self.device)
+        self.shard.set_global_stats_device(dfc.data_ptr(), dfc.shape[0], doc_count, sum_ttf)
+
+    def search_topk(self, query, k):
+        return self.shard.search_arrays(query, k)
+
+    def doc_key(self, doc):
+        return self.shard.doc_key(doc)
+
+
+def _dev(adapter):
+    return adapter.device if isinstance(adapter.device, torch.device) else torch.device(adapter.device)
+
+
+def global_commit(adapter, group=None):
+    """Steps 1-2 of GLOBAL mode.  Call after the shard's own commit."""
+    dev = _dev(adapter)
+    ws = dist.get_world_size(group)
+    keys, df = adapter.export_vocab()
+    n = torch.tensor([keys.shape[0]], dtype=torch.int64, device=dev)
+    ns = [torch.zeros_like(n) for _ in range(ws)]
+    dist.all_gather(ns, n, group=group)
+    m = int(max(int(x.item()) for x in ns))
+    padded = torch.zeros((max(m, 1), 2), dtype=torch.int64, device=dev)   # hi == 0 rows are dropped
+    padded[:keys.shape[0]] = keys
+    gathered = [torch.zeros_like(padded) for _ in range(ws)]
+    dist.all_gather(gathered, padded, group=group)
+    all_keys = torch.cat(gathered, 0).contiguous()
+    dfc = adapter.canonicalize(all_keys)
+    dist.all_reduce(dfc, op=dist.ReduceOp.SUM, group=group)
+    dc, ttf, _ = adapter.local_stats()
+    st = torch.tensor([dc, ttf], dtype=torch.int64, device=dev)
+    dist.all_reduce(st, op=dist.ReduceOp.SUM, group=group)
+    adapter.import_global(dfc, int(st[0].item()), int(st[1].item()))
+    return int(dfc.shape[0]), int(st[0].item()), int(st[1].item())
+
+
+def global_search(adapter, query: bytes, k: int, group=None):
+    """Step 3: per-rank top-k, all-gather, merge.  Returns [(global doc, score)]."""
+    dev = _dev(adapter)
+    ws = dist.get_world_size(group)
+    docs, scores = adapter.search_topk(query, k)
+    n = len(docs)
+    keyed = torch.zeros((k, 2), dtype=torch.int64, device=dev)
+    if n:
+        keyed[:n, 0] = torch.as_tensor(docs.astype("int64") + adapter.doc_base, device=dev)
+        keyed[:n, 1] = torch.as_tensor(scores.view("int32").astype("int64"), device=dev)
+    cnt = torch.tensor([n], dtype=torch.int64, device=dev)
+    cnts = [torch.zeros_like(cnt) for _ in range(ws)]
+    dist.all_gather(cnts, cnt, group=group)
+    outs = [torch.zeros_like(keyed) for _ in range(ws)]
+    dist.all_gather(outs, keyed, group=group)
+    import numpy as np
+    cands = []
+    for c, o in zip(cnts, outs):
+        c = int(c.item())
+        arr = o[:c].cpu().numpy()
+        for d, sb in arr.tolist():
+            cands.append((np.int32(sb).view(np.float32).item(), d))
+    cands.sort(key=lambda x: (-x[0], x[1]))
+    return [(d, s) for s, d in cands[:k]]
+
+
+def shard_range(n_docs, rank, world):
+    """Contiguous document range of a rank: [rank*N/G, (rank+1)*N/G)."""
+    return rank * n_docs // world, (rank + 1) * n_docs // world

@@ -1,0 +1,199 @@
+"""ShardIndex: one GPU shard of the engine — the per-worker Lucene index of the
+reference (Worker.java:54-55 ``luceneDir`` + ``indexWriter``) behind the C ABI.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+
+
+def term_key(term: bytes):
+    """128-bit device key (lo, hi) of an analysed (lower-cased) token."""
+    lo, hi = C.c_uint64(), C.c_uint64()
+    L.check(L.load().tfidf_term_key(term, len(term), C.byref(lo), C.byref(hi)))
+    return lo.value, hi.value
+
+
+class ShardIndex:
+    def __init__(self, device=0, k1=1.2, b=0.75, vocab_capacity_log2=18, stats_mode=L.STATS_SHARD):
+        lib = L.load()
+        cfg = L.Config()
+        L.check(lib.tfidf_config_init(C.byref(cfg)))
+        cfg.k1, cfg.b, cfg.device = k1, b, device
+        cfg.vocab_capacity_log2 = vocab_capacity_log2
+        cfg.stats_mode = stats_mode
+        h = C.c_void_p()
+        L.check(lib.tfidf_create(C.byref(cfg), C.byref(h)))
+        self._h = h
+        self.device = device
+
+    # -- lifetime -----------------------------------------------------------
+    def close(self):
+        if self._h:
+            L.load().tfidf_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- indexing (Worker.addDocToIndex / IndexWriter.commit) ----------------
+    def add_documents(self, texts, keys=None):
+        """texts: list of bytes; keys: list of bytes (relative paths) or None."""
+        n = len(texts)
+        offs = np.zeros(n + 1, np.uint64)
+        if n:
+            offs[1:] = np.cumsum([len(t) for t in texts], dtype=np.uint64)
+        blob = b"".join(texts)
+        kb, koffs = None, None
+        if keys is not None:
+            assert len(keys) == n
+            koffs = np.zeros(n + 1, np.uint64)
+            if n:
+                koffs[1:] = np.cumsum([len(k) for k in keys], dtype=np.uint64)
+            kb = b"".join(keys)
+        L.check(L.load().tfidf_add_docs(self._h, blob, L.ptr(offs, C.c_uint64), n, kb,
+                                        None if koffs is None else L.ptr(koffs, C.c_uint64)))
+
+    def add_documents_device(self, d_text, d_offsets, n_docs, total_bytes):
+        L.check(L.load().tfidf_add_docs_device(self._h, C.c_void_p(d_text), C.c_void_p(d_offsets), n_docs,
+                                               total_bytes))
+
+    def commit(self):
+        L.check(L.load().tfidf_commit(self._h))
+
+    def commit_timing(self):
+        t = L.CommitTiming()
+        L.check(L.load().tfidf_get_commit_timing(self._h, C.byref(t)))
+        return {f: getattr(t, f) for f, _ in L.CommitTiming._fields_}
+
+    def stats(self):
+        s = L.IndexStats()
+        L.check(L.load().tfidf_stats(self._h, C.byref(s)))
+        return {f: getattr(s, f) for f, _ in L.IndexStats._fields_}
+
+    # -- search (Worker.searchIndex) ------------------------------------------
+    def search(self, query: bytes, k=0):
+        """[(doc, float score)] in (score desc, doc asc); k == 0 -> all hits."""
+        lib = L.load()
+        cap = max(k, 1) if k else max(self.stats()["num_docs"], 1)
+        docs = np.zeros(cap, np.uint32)
+        scores = np.zeros(cap, np.float32)
+        n = C.c_uint64()
+        rc = lib.tfidf_search(self._h, query, len(query), k, L.ptr(docs, C.c_uint32), L.ptr(scores, C.c_float),
+                              cap, C.byref(n))
+        L.check(rc)
+        m = n.value
+        return list(zip(docs[:m].tolist(), scores[:m].tolist()))
+
+    def search_arrays(self, query: bytes, k):
+        lib = L.load()
+        docs = np.zeros(max(k, 1), np.uint32)
+        scores = np.zeros(max(k, 1), np.float32)
+        n = C.c_uint64()
+        L.check(lib.tfidf_search(self._h, query, len(query), k, L.ptr(docs, C.c_uint32), L.ptr(scores, C.c_float),
+                                 max(k, 1), C.byref(n)))
+        return docs[:n.value], scores[:n.value]
+
+    def search_batch(self, queries, k):
+        """queries: list of bytes.  Returns (docs[n_q, k], scores[n_q, k], counts[n_q])."""
+        nq = len(queries)
+        offs = np.zeros(nq + 1, np.uint64)
+        offs[1:] = np.cumsum([len(q) for q in queries], dtype=np.uint64)
+        docs = np.zeros((nq, k), np.uint32)
+        scores = np.zeros((nq, k), np.float32)
+        counts = np.zeros(nq, np.uint32)
+        L.check(L.load().tfidf_search_batch(self._h, b"".join(queries), L.ptr(offs, C.c_uint64), nq, k,
+                                            L.ptr(docs, C.c_uint32), L.ptr(scores, C.c_float),
+                                            L.ptr(counts, C.c_uint32)))
+        return docs, scores, counts
+
+    def last_search_ms(self):
+        a, b = C.c_float(), C.c_float()
+        L.check(L.load().tfidf_last_search_ms(self._h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    # -- inspection -----------------------------------------------------------
+    def doc_key(self, doc):
+        buf = C.create_string_buffer(4096)
+        n = C.c_uint64()
+        L.check(L.load().tfidf_doc_key(self._h, doc, buf, 4096, C.byref(n)))
+        return buf.raw[:n.value]
+
+    def doc_len(self, doc):
+        ln, nm = C.c_uint32(), C.c_uint8()
+        L.check(L.load().tfidf_doc_len(self._h, doc, C.byref(ln), C.byref(nm)))
+        return ln.value, nm.value
+
+    def doc_terms(self, doc):
+        ln, _ = self.doc_len(doc)
+        cap = ln + 1
+        buf = C.create_string_buffer(cap * 48 + 64)
+        tfs = np.zeros(cap, np.uint32)
+        n = C.c_uint64()
+        L.check(L.load().tfidf_doc_terms(self._h, doc, buf, len(buf), L.ptr(tfs, C.c_uint32), cap, C.byref(n)))
+        terms = buf.raw.split(b"\0")[:n.value]
+        return dict(zip(terms, tfs[:n.value].tolist()))
+
+    def df(self, term: bytes):
+        a, b = C.c_uint64(), C.c_uint64()
+        L.check(L.load().tfidf_term_df(self._h, term, len(term), C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    # -- GLOBAL statistics ------------------------------------------------------
+    def vocab_size(self):
+        n = C.c_uint64()
+        L.check(L.load().tfidf_vocab_size(self._h, C.byref(n)))
+        return n.value
+
+    def vocab_export_device(self, d_keys, d_df, cap):
+        n = C.c_uint64()
+        L.check(L.load().tfidf_vocab_export_device(self._h, C.c_void_p(d_keys), C.c_void_p(d_df), cap, C.byref(n)))
+        return n.value
+
+    def vocab_canonicalize_device(self, d_all_keys, n_all, d_df_canon, cap):
+        n = C.c_uint64()
+        L.check(L.load().tfidf_vocab_canonicalize_device(self._h, C.c_void_p(d_all_keys), n_all,
+                                                         C.c_void_p(d_df_canon), cap, C.byref(n)))
+        return n.value
+
+    def set_global_stats_device(self, d_df_canon, n_canon, doc_count, sum_ttf):
+        L.check(L.load().tfidf_set_global_stats_device(self._h, C.c_void_p(d_df_canon), n_canon, doc_count,
+                                                       sum_ttf))
+
+    def set_global_stats(self, keys_lohi, df, doc_count, sum_ttf):
+        keys_lohi = np.ascontiguousarray(keys_lohi, np.uint64).reshape(-1)
+        df = np.ascontiguousarray(df, np.uint64)
+        L.check(L.load().tfidf_set_global_stats(self._h, L.ptr(keys_lohi, C.c_uint64), L.ptr(df, C.c_uint64),
+                                                len(df), doc_count, sum_ttf))
+
+    def clear_global_stats(self):
+        L.check(L.load().tfidf_clear_global_stats(self._h))
+
+
+def leader_merge(responses):
+    """Leader.start merge via the C ABI: list (worker order) of lists of
+    (name bytes, double) -> [(name, sum)] ordered by name."""
+    flat = [x for r in responses for x in r]
+    n = len(flat)
+    if n == 0:
+        return []
+    names = b"".join(nm for nm, _ in flat)
+    offs = np.zeros(n + 1, np.uint64)
+    offs[1:] = np.cumsum([len(nm) for nm, _ in flat], dtype=np.uint64)
+    sc = np.array([s for _, s in flat], np.float64)
+    first = np.zeros(n, np.uint64)
+    sums = np.zeros(n, np.float64)
+    m = C.c_uint64()
+    L.check(L.load().tfidf_leader_merge(names, L.ptr(offs, C.c_uint64), n, L.ptr(sc, C.c_double),
+                                        L.ptr(first, C.c_uint64), L.ptr(sums, C.c_double), C.byref(m)))
+    return [(flat[int(first[i])][0], float(sums[i])) for i in range(m.value)]

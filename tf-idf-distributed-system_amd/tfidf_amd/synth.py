@@ -1,0 +1,118 @@
+"""Synthetic Zipf corpus — host (NumPy) generator and the
+device generator behind tfidf_synth_corpus.  The two are bit-identical
+(tests/test_synth.py).  Synthetic data stands in for the reference's corpus:
+there is no network for real datasets.
+
+Definition (mix64 = splitmix64 step, S2 = mix64(seed)):
+  T_d   = len_min + mix64(S2 ^ (d << 20 | 0xFFFFF)) % (len_max - len_min + 1)
+  u     = (mix64(S2 ^ (d << 20 | t)) >> 11) * 2^-53
+  rank  = 1 + searchsorted(cdf, u, side="right"),  cdf = cumsum(r^-s) / H
+  word  = bijective base-26 ('a' = 1) of rank + 18278   (rank 1 -> "aaaa")
+  sep   = '\n' after every 16th token and after the last, else ' '
+Queries: 3 distinct ranks uniform in [100, 10000) from seed + 1.
+"""
+import ctypes as C
+
+import numpy as np
+
+SEED = 20251015
+M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+
+def _mix64(z):
+    z = np.asarray(z, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def mix64(x: int) -> int:
+    return int(_mix64(np.uint64(x)))
+
+
+def zipf_cdf(V, s=1.0):
+    r = np.arange(1, V + 1, dtype=np.float64)
+    w = r ** (-s)
+    cdf = np.cumsum(w / w.sum())
+    cdf[-1] = 1.0
+    return cdf
+
+
+def word(rank: int) -> bytes:
+    n = rank + 18278
+    out = []
+    while n:
+        n -= 1
+        out.append(97 + n % 26)
+        n //= 26
+    return bytes(reversed(out))
+
+
+def doc_tokens(seed, d, len_min, len_max):
+    s2 = _mix64(np.uint64(seed))
+    h = _mix64(s2 ^ np.uint64((d << 20) | 0xFFFFF))
+    return len_min + int(h % np.uint64(len_max - len_min + 1))
+
+
+def doc_ranks(seed, d, len_min, len_max, cdf):
+    s2 = _mix64(np.uint64(seed))
+    T = doc_tokens(seed, d, len_min, len_max)
+    t = np.arange(T, dtype=np.uint64)
+    h = _mix64(s2 ^ ((np.uint64(d) << np.uint64(20)) | t))
+    u = (h >> np.uint64(11)).astype(np.float64) * 2.0 ** -53
+    ranks = np.searchsorted(cdf, u, side="right") + 1
+    return np.minimum(ranks, len(cdf))
+
+
+def doc_text(seed, d, len_min, len_max, cdf) -> bytes:
+    ranks = doc_ranks(seed, d, len_min, len_max, cdf)
+    parts = []
+    T = len(ranks)
+    for t, r in enumerate(ranks.tolist()):
+        parts.append(word(r))
+        parts.append(b"\n" if (t % 16 == 15 or t == T - 1) else b" ")
+    return b"".join(parts)
+
+
+def corpus(n_docs, V=100_000, len_min=400, len_max=600, seed=SEED, s=1.0, doc_base=0):
+    """Host corpus (list of bytes) — use for small N (tests, CPU baseline sample)."""
+    cdf = zipf_cdf(V, s)
+    return [doc_text(seed, doc_base + i, len_min, len_max, cdf) for i in range(n_docs)]
+
+
+def queries(n_q, n_terms=3, lo=100, hi=10_000, seed=SEED + 1):
+    """n_q queries of n_terms distinct ranks uniform in [lo, hi)."""
+    s2 = mix64(seed)
+    out = []
+    for q in range(n_q):
+        ranks, j = [], 0
+        while len(ranks) < n_terms:
+            r = lo + mix64(s2 ^ ((q << 8) | j)) % (hi - lo)
+            j += 1
+            if r not in ranks:
+                ranks.append(r)
+        out.append(b" ".join(word(r) for r in ranks))
+    return out
+
+
+class DeviceCorpus:
+    """Corpus generated directly in HBM by the tfidf_synth_corpus kernels."""
+
+    def __init__(self, n_docs, V=100_000, len_min=400, len_max=600, seed=SEED, s=1.0, doc_base=0, device=0):
+        from . import _lib as L
+        lib = L.load()
+        cdf = np.ascontiguousarray(zipf_cdf(V, s))
+        t, o, tot = C.c_void_p(), C.c_void_p(), C.c_uint64()
+        L.check(lib.tfidf_synth_corpus(device, seed, n_docs, doc_base, L.ptr(cdf, C.c_double), V, len_min,
+                                       len_max, C.byref(t), C.byref(o), C.byref(tot)))
+        self.d_text, self.d_offsets, self.total_bytes = t.value, o.value, tot.value
+        self.n_docs, self.device = n_docs, device
+
+    def free(self):
+        from . import _lib as L
+        if self.d_text:
+            L.load().tfidf_device_free(self.device, C.c_void_p(self.d_text))
+            L.load().tfidf_device_free(self.device, C.c_void_p(self.d_offsets))
+            self.d_text = self.d_offsets = None
