@@ -20,6 +20,19 @@ from tfidf_amd._lib import UnsupportedInput, UnsupportedQuery
 pytestmark = pytest.mark.gpu
 
 
+def keyed(terms):
+    """Oracle doc_terms with long (> 18 byte) terms replaced by the engine's
+    printable 128-bit key: the device keys those terms by hash."""
+    from tfidf_amd.engine import term_key
+    out = {}
+    for t, tf in terms.items():
+        if len(t) > 18:
+            lo, hi = term_key(t)
+            t = b"#%016x%016x" % (hi, lo)
+        out[t] = tf
+    return out
+
+
 def f32bits(x):
     return np.float32(x).view(np.int32).item()
 
@@ -146,7 +159,7 @@ def test_zipf_stats(zipf):
 def test_zipf_tf_rows(zipf):
     g, o, texts = zipf
     for d in list(range(0, 3000, 97)) + [2999]:
-        assert g.doc_terms(d) == o.doc_terms(d)
+        assert g.doc_terms(d) == keyed(o.doc_terms(d))
         assert g.doc_len(d) == (o.doc_len(d), o.doc_norm(d))
 
 
@@ -204,7 +217,7 @@ def test_punctuation_corpus_parity():
     s = g.stats()
     assert (s["doc_count"], s["sum_ttf"], s["num_terms"]) == (o.doc_count, o.sum_ttf, o.num_terms)
     for d in range(len(texts)):
-        assert g.doc_terms(d) == o.doc_terms(d), d
+        assert g.doc_terms(d) == keyed(o.doc_terms(d)), d
         assert g.doc_len(d) == (o.doc_len(d), o.doc_norm(d))
     for q in [b"a", b"b.c x", b"3,14", b"abc xyz", b"_", b"y" * 19]:
         assert_hits_equal(g.search(q, 0), o.search(q, 0))
@@ -224,12 +237,12 @@ def test_long_documents_path():
     texts.insert(9, random_text(rng, 20000))        # punctuation-heavy long doc
     g, o = build_pair(texts, cap_log2=18)
     s = g.stats()
-    assert s["long_docs"] >= 7
+    assert s["long_docs"] >= 6       # 700-token doc (< 4 KB) stays on the LDS path
     assert (s["doc_count"], s["sum_ttf"], s["num_terms"], s["nnz"]) == \
         (o.doc_count, o.sum_ttf, o.num_terms, sum(o.vocab().values()))
     for d in range(len(texts)):
         if len(texts[d]) > 4096 or d % 17 == 0:
-            assert g.doc_terms(d) == o.doc_terms(d), d
+            assert g.doc_terms(d) == keyed(o.doc_terms(d)), d
             assert g.doc_len(d) == (o.doc_len(d), o.doc_norm(d))
     for q in synth.queries(15, lo=1, hi=2000) + [b"ab", b"a b c"]:
         assert_hits_equal(g.search(q, 0), o.search(q, 0))

@@ -30,6 +30,12 @@ namespace tfidf {
 // ---------------------------------------------------------------------------
 // small helpers
 
+// Workgroup barrier that orders LDS only: it does not drain outstanding
+// global loads/stores (a __syncthreads() would wait for vmcnt(0) and stall
+// every phase behind the previous document's CSR stores and the next
+// document's prefetch).  Used wherever phases communicate through LDS alone.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ uint32_t block_excl_scan_256(uint32_t v, uint32_t *sh, uint32_t *total) {
   const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   uint32_t x = v;
@@ -39,7 +45,7 @@ __device__ __forceinline__ uint32_t block_excl_scan_256(uint32_t v, uint32_t *sh
     if (lane >= (uint32_t)o) x += y;
   }
   if (lane == 63) sh[wid] = x;
-  __syncthreads();
+  lds_barrier();
   uint32_t base = 0, tot = 0;
 #pragma unroll
   for (int w = 0; w < 4; w++) {
@@ -47,7 +53,7 @@ __device__ __forceinline__ uint32_t block_excl_scan_256(uint32_t v, uint32_t *sh
     if ((uint32_t)w < wid) base += s;
     tot += s;
   }
-  __syncthreads();
+  lds_barrier();
   *total = tot;
   return base + x - v;
 }
@@ -57,53 +63,54 @@ __device__ __forceinline__ void set_err(uint32_t *err, uint32_t flag, uint32_t d
   if (old == 0) atomicExch(err + 1, doc);
 }
 
-// Global dictionary: claim by CAS on the key's lo word (lo != 0 for every
-// key), publish hi.  Plain loads may be stale but can only show an older
-// state (slots go 0 -> key once), so a stale "empty" falls through to the CAS
-// which returns the true value.  A slot claimed but not yet published is
-// re-read (agent-scope atomic load) without advancing.  SIMT-safe: the
-// publishing store precedes any re-read in program order.
-__device__ uint32_t dict_find_or_insert(uint64_t *dict, uint32_t mask, uint64_t lo, uint64_t hi) {
+// Global dictionary (open addressing, 16 B slots, key lo at [2s], hi at
+// [2s+1]).  A lane probes 4 consecutive slots per round with independent
+// 16 B loads (one memory round trip covers 4 linear probes).  Claim = CAS on
+// the lo word (lo != 0 for every key), then publish hi.  Plain loads may be
+// stale but only show an older state (slots go 0 -> key once): a stale
+// "empty" falls through to the CAS, which returns the true value.  A slot
+// claimed but not yet published is re-read with an agent-scope atomic load.
+// SIMT-safe: every claiming lane publishes before any lane re-reads.
+__device__ uint32_t dict_find_or_insert(uint64_t *dict, uint32_t mask, uint64_t lo, uint64_t hi, bool active) {
   uint32_t s = (uint32_t)key_hash(lo, hi) & mask;
   uint32_t result = kInvalidSlot;
-  bool done = false;
-  const uint32_t limit = 2 * (mask + 1) + 4096;
+  bool done = !active;
+  const uint32_t limit = (mask + 1) + 4096;
   for (uint32_t it = 0; it < limit; it++) {
-    uint64_t clo = 0, chi = 0;
-    // (1) claim block: every claiming lane publishes hi before (2) runs
+    if (__all(done)) break;
+    uint32_t js = 0;        // slot to act on this round
+    int act = 0;            // 0 advance, 1 found, 2 try claim, 3 recheck pending
     if (!done) {
-      ulonglong2 e = *reinterpret_cast<const ulonglong2 *>(dict + 2 * (size_t)s);
-      clo = e.x;
-      chi = e.y;
-      if (clo == 0) {
-        unsigned long long old = atomicCAS(reinterpret_cast<unsigned long long *>(dict + 2 * (size_t)s), 0ull,
-                                           (unsigned long long)lo);
-        if (old == 0) {
-          __hip_atomic_store(dict + 2 * (size_t)s + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          result = s;
-          done = true;
-        } else {
-          clo = old;
-          chi = 0;
-        }
+      ulonglong2 e[4];
+#pragma unroll
+      for (int j = 0; j < 4; j++) e[j] = *reinterpret_cast<const ulonglong2 *>(dict + 2 * (size_t)((s + j) & mask));
+#pragma unroll
+      for (int j = 3; j >= 0; j--) {   // earliest slot wins
+        const bool empty = e[j].x == 0;
+        const bool same = e[j].x == lo && e[j].y == hi;
+        const bool pend = e[j].x == lo && e[j].y == 0;
+        if (empty || same || pend) { js = (s + j) & mask; act = same ? 1 : (empty ? 2 : 3); }
+      }
+      if (act == 0) s = (s + 4) & mask;
+      if (act == 1) { result = js; done = true; }
+    }
+    if (act == 2) {
+      unsigned long long old = atomicCAS(reinterpret_cast<unsigned long long *>(dict + 2 * (size_t)js), 0ull,
+                                         (unsigned long long)lo);
+      if (old == 0) {
+        __hip_atomic_store(dict + 2 * (size_t)js + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        result = js;
+        done = true;
+      } else {
+        s = old == lo ? js : ((js + 1) & mask);   // recheck (pending) or move past
       }
     }
     asm volatile("" ::: "memory");
-    // (2) match block
-    if (!done) {
-      if (clo == lo) {
-        if (chi == 0) chi = __hip_atomic_load(dict + 2 * (size_t)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (chi == hi) {
-          result = s;
-          done = true;
-        } else if (chi != 0) {
-          s = (s + 1) & mask;
-        }  // chi == 0: claimed elsewhere, not yet published -> re-read this slot
-      } else {
-        s = (s + 1) & mask;
-      }
+    if (act == 3 && !done) {
+      const uint64_t chi = __hip_atomic_load(dict + 2 * (size_t)js + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (chi == hi) { result = js; done = true; }
+      else s = chi == 0 ? js : ((js + 1) & mask);
     }
-    if (__all(done)) break;
   }
   return result;
 }
@@ -154,7 +161,8 @@ __device__ uint32_t gtable_insert(uint64_t *keys, uint32_t *cnt, uint32_t mask, 
 }
 
 // ---------------------------------------------------------------------------
-// Shared tokenizer phases over a staged window of bytes in LDS.
+// Shared tokenizer phases over a staged window of bytes in LDS.  They talk
+// through LDS only and synchronise with lds_barrier().
 //   text      : LDS bytes, window byte r at text[shift + r]
 //   wlen      : window length (bytes outside the window read as class Other)
 //   wbits     : out, one bit per window position (word-segment membership)
@@ -177,7 +185,11 @@ __device__ __forceinline__ uint8_t code_at(const uint8_t *text, const uint8_t *l
   return lut[c & 127];
 }
 
-// Returns true (block-uniform) if a non-ASCII byte is present.
+// Word-segment bits, 64 positions per wave-iteration: one LDS byte read +
+// one class-LUT read per lane; neighbour classes by lane shuffle (only lanes
+// 0 and 63 read across the 64-byte boundary); the membership bits of the
+// 64 positions are one __ballot.  Returns true (block-uniform) if a
+// non-ASCII byte is present.
 __device__ bool phase_wordbits(const uint8_t *text, const uint8_t *lut, uint32_t shift, uint32_t wlen,
                                uint64_t *wbits, uint32_t *flag_lds) {
   const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -185,22 +197,24 @@ __device__ bool phase_wordbits(const uint8_t *text, const uint8_t *lut, uint32_t
   bool nonascii = false;
   for (uint32_t m = wid; m < nwords; m += 4) {
     const int64_t r = (int64_t)m * 64 + lane;
-    uint8_t cur = 0, prev = 0, next = 0;
+    uint32_t cur = 0;
     if (r < wlen) {
-      uint8_t c = text[shift + r];
+      const uint8_t c = text[shift + r];
       nonascii |= c >= 128;
       cur = lut[c & 127];
-      prev = code_at(text, lut, shift, r - 1, wlen);
-      next = code_at(text, lut, shift, r + 1, wlen);
     }
-    const bool w = (r < wlen) && wb_is_word(prev, cur, next);
+    uint32_t prev = __shfl_up(cur, 1, 64);
+    uint32_t next = __shfl_down(cur, 1, 64);
+    if (lane == 0) prev = code_at(text, lut, shift, r - 1, wlen);
+    if (lane == 63) next = code_at(text, lut, shift, r + 1, wlen);
+    const bool w = (r < wlen) && wb_is_word((uint8_t)prev, (uint8_t)cur, (uint8_t)next);
     const uint64_t mask = __ballot(w);
     if (lane == 0) wbits[m] = mask;
   }
   if (__any(nonascii) && lane == 0) atomicOr(flag_lds, 1u);
-  __syncthreads();
+  lds_barrier();
   const bool bad = (*flag_lds & 1u) != 0;
-  __syncthreads();      // every thread has read the flag before anyone resets it
+  lds_barrier();      // every thread has read the flag before anyone resets it
   return bad;
 }
 
@@ -250,23 +264,39 @@ __device__ uint32_t phase_token_spans(const uint64_t *wbits, uint32_t wlen, uint
     }
     total_all += total;
   }
-  __syncthreads();      // spans visible to every thread
+  lds_barrier();      // spans visible to every thread
   return total_all;
 }
 
-// Build the key of the token [s, e) of the window; false if the span holds
-// no letter/digit (a run of '_' is not a token) — then *valid = false.
+// Key of the token [s, e) of the window; *valid = false if the span holds no
+// letter/digit (a run of '_' is not a token).  The 7-bit packing is exact
+// for <= 18 bytes; only longer tokens pay for the two hashes.
 __device__ __forceinline__ void token_key(const uint8_t *text, const uint8_t *lut, uint32_t shift, uint32_t s,
                                           uint32_t e, uint64_t *lo, uint64_t *hi, bool *valid) {
-  KeyBuilder kb;
+  const uint32_t n = e - s;
   uint8_t any = 0;
-  for (uint32_t j = s; j < e; j++) {
-    const uint8_t c = text[shift + j];
-    any |= lut[c & 127];
-    kb.push(ascii_lower(c));
+  if (n <= kShortKeyChars) {
+    uint64_t a = 0, b = 0;
+    for (uint32_t j = 0; j < n; j++) {
+      const uint8_t c = text[shift + s + j];
+      any |= lut[c & 127];
+      const uint64_t v = ascii_lower(c);
+      const uint32_t bit = 7 * j;
+      if (bit < 64) a |= v << bit;
+      if (bit + 7 > 64) b |= bit < 64 ? (v >> (64 - bit)) : (v << (bit - 64));
+    }
+    *lo = a;
+    *hi = b | kKeyValid;
+  } else {
+    KeyBuilder kb;
+    for (uint32_t j = s; j < e; j++) {
+      const uint8_t c = text[shift + j];
+      any |= lut[c & 127];
+      kb.push(ascii_lower(c));
+    }
+    kb.finish(lo, hi);
   }
   *valid = (any & (kClsL | kClsD)) != 0;
-  kb.finish(lo, hi);
 }
 
 // ---------------------------------------------------------------------------
@@ -330,6 +360,32 @@ __device__ __forceinline__ void lds_table_insert(ShortSmem &sm, uint64_t lo, uin
   if (!done) atomicOr(&sm.flags, 2u);   // overflow -> long path
 }
 
+// Prefetch of a short document's bytes into registers: 2 x 16 B per thread
+// covers 4096 + 15 bytes of misalignment.
+struct DocPrefetch {
+  uint4 v0, v1;
+  uint64_t s0, L, src;
+  uint32_t shift;
+  bool valid;
+};
+
+__device__ __forceinline__ void prefetch_doc(const BuildParams &p, uint64_t d, DocPrefetch &pf) {
+  pf.valid = d < p.n_docs;
+  if (!pf.valid) return;
+  pf.src = p.live_map ? p.live_map[d] : d;
+  pf.s0 = p.offsets[pf.src];
+  pf.L = p.offsets[pf.src + 1] - pf.s0;
+  const uintptr_t a = reinterpret_cast<uintptr_t>(p.text + pf.s0);
+  const uintptr_t al = a & ~(uintptr_t)15;
+  pf.shift = (uint32_t)(a - al);
+  if (pf.L > kShortMaxBytes) return;
+  const uint32_t nchunks = (uint32_t)((pf.shift + pf.L + 15) >> 4);
+  const uint4 *src = reinterpret_cast<const uint4 *>(al);
+  const uint4 z = make_uint4(0, 0, 0, 0);
+  pf.v0 = threadIdx.x < nchunks ? src[threadIdx.x] : z;
+  pf.v1 = threadIdx.x + 256 < nchunks ? src[threadIdx.x + 256] : z;
+}
+
 __global__ void __launch_bounds__(256) k_tokenize_short(BuildParams p) {
   __shared__ ShortSmem sm;
   const uint32_t tid = threadIdx.x;
@@ -338,19 +394,25 @@ __global__ void __launch_bounds__(256) k_tokenize_short(BuildParams p) {
   if (tid < 64) { sm.rcnt[tid] = 0; sm.rcur[tid] = 0; }
   if (tid == 0) { sm.n_uniq = 0; sm.len = 0; sm.flags = 0; }
   unsigned long long my_doc_count = 0, my_ttf = 0, my_nnz = 0;
-  __syncthreads();
+  DocPrefetch pf;
+  prefetch_doc(p, blockIdx.x, pf);
+  lds_barrier();
 
   for (uint64_t d = blockIdx.x; d < p.n_docs; d += gridDim.x) {
-    const uint64_t src = p.live_map ? p.live_map[d] : d;
-    const uint64_t s0 = p.offsets[src], s1 = p.offsets[src + 1];
-    const uint64_t L = s1 - s0;
+    const uint64_t src = pf.src, L = pf.L;
+    const uint32_t shift = pf.shift;
     if (L > kShortMaxBytes) {
       if (tid == 0) p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
+      prefetch_doc(p, d + gridDim.x, pf);
       continue;                                           // block-uniform
     }
-    uint32_t shift;
-    stage_bytes(sm.text, p.text + s0, L, &shift);
-    __syncthreads();
+    // stage from registers, then start fetching the next document
+    uint4 *dst = reinterpret_cast<uint4 *>(sm.text);
+    const uint32_t nchunks = (uint32_t)((shift + L + 15) >> 4);
+    if (tid < nchunks) dst[tid] = pf.v0;
+    if (tid + 256 < nchunks) dst[tid + 256] = pf.v1;
+    prefetch_doc(p, d + gridDim.x, pf);
+    lds_barrier();
     const bool nonascii = phase_wordbits(sm.text, sm.lut, shift, (uint32_t)L, sm.wbits, &sm.flags);
     if (nonascii) {
       if (tid == 0) {
@@ -359,14 +421,14 @@ __global__ void __launch_bounds__(256) k_tokenize_short(BuildParams p) {
         for (uint32_t r = 0; r < p.n_ranges; r++) p.rsplit[d * p.n_ranges + r] = 0;
         sm.flags = 0;
       }
-      __syncthreads();
+      lds_barrier();
       continue;
     }
     const uint32_t ntok = phase_token_spans(sm.wbits, (uint32_t)L, 0, (uint32_t)L, sm.tok_s, sm.tok_e,
                                             kShortMaxTokens, sm.scan);
     if (ntok > kShortMaxTokens) {
       if (tid == 0) p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
-      __syncthreads();
+      lds_barrier();
       continue;
     }
     // Phase C: tokens -> per-document histogram in LDS
@@ -387,31 +449,36 @@ __global__ void __launch_bounds__(256) k_tokenize_short(BuildParams p) {
       lds_table_insert(sm, lo, hi, valid);
     }
     atomicAdd(&sm.len, my_len);
-    __syncthreads();
+    lds_barrier();
     const uint32_t nu = sm.n_uniq;
     if (sm.flags & 2u) {                                  // LDS table overflow
       for (uint32_t i = tid; i < nu; i += 256) {
         const uint32_t s = sm.claimed[i];
         sm.t_lo[s] = 0; sm.t_hi[s] = 0; sm.t_cnt[s] = 0;
       }
-      __syncthreads();
+      lds_barrier();
       if (tid == 0) {
         p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
         sm.n_uniq = 0; sm.len = 0; sm.flags = 0;
       }
-      __syncthreads();
+      lds_barrier();
       continue;
     }
-    // Phase D: dictionary slots, range partition, CSR row
+    // Phase D: dictionary slots (all lookups of a thread issued together),
+    // range partition, CSR row
     const uint64_t base = csr_row_base(p.offsets, src);
-    for (uint32_t i = tid; i < nu; i += 256) {
-      const uint32_t s = sm.claimed[i];
-      uint32_t g = dict_find_or_insert(p.dict, p.cap_mask, sm.t_lo[s], sm.t_hi[s]);
-      if (g == kInvalidSlot) { set_err(p.err, kErrCapacity, (uint32_t)d); g = 0; }
-      atomicAdd(&sm.rcnt[g >> p.range_shift], 1u);
-      sm.t_lo[s] = g;
+    for (uint32_t i0 = 0; i0 < nu; i0 += 256) {
+      const uint32_t i = i0 + tid;
+      const bool act = i < nu;
+      const uint32_t s = act ? sm.claimed[i] : 0;
+      uint32_t g = dict_find_or_insert(p.dict, p.cap_mask, act ? sm.t_lo[s] : 1, act ? sm.t_hi[s] : kKeyValid, act);
+      if (act) {
+        if (g == kInvalidSlot) { set_err(p.err, kErrCapacity, (uint32_t)d); g = 0; }
+        atomicAdd(&sm.rcnt[g >> p.range_shift], 1u);
+        sm.t_lo[s] = g;
+      }
     }
-    __syncthreads();
+    lds_barrier();
     if (tid == 0) {
       uint32_t run = 0;
       for (uint32_t r = 0; r < p.n_ranges; r++) {
@@ -429,7 +496,7 @@ __global__ void __launch_bounds__(256) k_tokenize_short(BuildParams p) {
       my_ttf += len;
       my_nnz += nu;
     }
-    __syncthreads();
+    lds_barrier();
     for (uint32_t i = tid; i < nu; i += 256) {
       const uint32_t s = sm.claimed[i];
       const uint32_t g = (uint32_t)sm.t_lo[s];
@@ -438,9 +505,9 @@ __global__ void __launch_bounds__(256) k_tokenize_short(BuildParams p) {
       p.csr_tf[base + pos] = sm.t_cnt[s];
       sm.t_lo[s] = 0; sm.t_hi[s] = 0; sm.t_cnt[s] = 0;
     }
-    __syncthreads();
+    lds_barrier();
     if (tid == 0) { sm.n_uniq = 0; sm.len = 0; sm.flags = 0; }
-    __syncthreads();
+    lds_barrier();
   }
   if (tid == 0) {
     atomicAdd(&p.stats[0], my_doc_count);
@@ -528,15 +595,21 @@ __global__ void __launch_bounds__(256) k_tokenize_long(BuildParams p) {
     atomicAdd(&sm.len, my_len);
     // emission: dictionary lookup + range counts
     uint32_t my_nu = 0;
-    for (uint32_t s = tid; s < T; s += 256) {
-      const uint64_t lo = keys[2 * s];
-      if (lo == 0) continue;
-      const uint64_t hi = keys[2 * s + 1];
-      uint32_t g = dict_find_or_insert(p.dict, p.cap_mask, lo, hi);
-      if (g == kInvalidSlot) { set_err(p.err, kErrCapacity, d); g = 0; }
-      gsl[s] = g;
-      atomicAdd(&sm.rcnt[g >> p.range_shift], 1u);
-      my_nu++;
+    for (uint32_t s0 = 0; s0 < T; s0 += 256) {
+      const uint32_t s = s0 + tid;
+      uint64_t lo = 0, hi = 0;
+      if (s < T) {
+        lo = __hip_atomic_load(keys + 2 * (size_t)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        hi = __hip_atomic_load(keys + 2 * (size_t)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      const bool act = lo != 0;
+      uint32_t g = dict_find_or_insert(p.dict, p.cap_mask, act ? lo : 1, act ? hi : kKeyValid, act);
+      if (act) {
+        if (g == kInvalidSlot) { set_err(p.err, kErrCapacity, d); g = 0; }
+        gsl[s] = g;
+        atomicAdd(&sm.rcnt[g >> p.range_shift], 1u);
+        my_nu++;
+      }
     }
     atomicAdd(&sm.nu, my_nu);
     __syncthreads();
@@ -560,11 +633,11 @@ __global__ void __launch_bounds__(256) k_tokenize_long(BuildParams p) {
     __syncthreads();
     const uint64_t base = csr_row_base(p.offsets, src);
     for (uint32_t s = tid; s < T; s += 256) {
-      if (keys[2 * s] == 0) continue;
+      if (__hip_atomic_load(keys + 2 * (size_t)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) continue;
       const uint32_t g = gsl[s];
       const uint32_t pos = atomicAdd(&sm.rcur[g >> p.range_shift], 1u);
       p.csr_col[base + pos] = g;
-      p.csr_tf[base + pos] = cnt[s];
+      p.csr_tf[base + pos] = __hip_atomic_load(cnt + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     if (tid == 0) { sm.len = 0; sm.flags = 0; sm.nu = 0; }
