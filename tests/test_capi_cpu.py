@@ -57,25 +57,30 @@ def test_create_without_device_fails_loudly():
 
 
 def _pack7(term: bytes):
-    v = 0
+    v = len(term)
     for j, c in enumerate(term):
-        v |= c << (7 * j)
+        v |= c << (5 + 7 * j)
     return v & ((1 << 64) - 1), (v >> 64) | (1 << 63)
 
 
-@pytest.mark.parametrize("term", [b"a", b"fast", b"kheder", b"wireless", b"u.s.a", b"3,14", b"abcdefghi",
-                                  b"abcdefghij", b"x" * 18])
+@pytest.mark.parametrize("term", [b"a", b"fast", b"kheder", b"wireless", b"u.s.a", b"3,14", b"abcdefgh",
+                                  b"abcdefghi", b"abcdefghij", b"x" * 17])
 def test_short_term_keys_are_exact_7bit_packing(term):
     assert term_key(term) == _pack7(term)
 
 
+def test_short_keys_up_to_8_bytes_live_in_lo():
+    for t in (b"a", b"abcdefgh", b"12345678"):
+        assert term_key(t)[1] == 1 << 63
+
+
 def test_long_term_keys_hashed_and_distinct():
-    a = term_key(b"a" * 19)
+    a = term_key(b"a" * 18)
     b = term_key(b"a" * 20)
     c = term_key(b"b" + b"a" * 18)
     assert len({a, b, c}) == 3
     for lo, hi in (a, b, c):
-        assert hi >> 62 == 3 and lo & 1 == 1       # VALID | LONG flags, lo != 0
+        assert hi >> 62 == 3 and lo & 31 == 0 and lo != 0   # VALID | LONG flags, length field 0
 
 
 def test_leader_merge_matches_oracle():

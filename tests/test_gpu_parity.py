@@ -21,12 +21,12 @@ pytestmark = pytest.mark.gpu
 
 
 def keyed(terms):
-    """Oracle doc_terms with long (> 18 byte) terms replaced by the engine's
+    """Oracle doc_terms with long (> 17 byte) terms replaced by the engine's
     printable 128-bit key: the device keys those terms by hash."""
     from tfidf_amd.engine import term_key
     out = {}
     for t, tf in terms.items():
-        if len(t) > 18:
+        if len(t) > 17:
             lo, hi = term_key(t)
             t = b"#%016x%016x" % (hi, lo)
         out[t] = tf
@@ -212,7 +212,7 @@ def random_text(rng, n):
 def test_punctuation_corpus_parity():
     rng = random.Random(7)
     texts = [random_text(rng, rng.randint(0, 3000)) for _ in range(400)]
-    texts += [b"", b"   ", b"___", b"...", b"a.b.c", b"3,14;15", b"don't", b"x" * 18, b"y" * 19, b"z" * 255]
+    texts += [b"", b"   ", b"___", b"...", b"a.b.c", b"3,14;15", b"don't", b"x" * 17, b"w" * 18, b"y" * 19, b"z" * 255]
     g, o = build_pair(texts)
     s = g.stats()
     assert (s["doc_count"], s["sum_ttf"], s["num_terms"]) == (o.doc_count, o.sum_ttf, o.num_terms)

@@ -71,8 +71,16 @@ __device__ __forceinline__ void set_err(uint32_t *err, uint32_t flag, uint32_t d
 // "empty" falls through to the CAS, which returns the true value.  A slot
 // claimed but not yet published is re-read with an agent-scope atomic load.
 // SIMT-safe: every claiming lane publishes before any lane re-reads.
+__device__ __forceinline__ void probe_pick(ulonglong2 e, uint32_t slot, uint64_t lo, uint64_t hi, uint32_t &js,
+                                           int &act) {
+  const bool empty = e.x == 0;
+  const bool same = e.x == lo && e.y == hi;
+  const bool pend = e.x == lo && e.y == 0;
+  if (act == 0 && (empty || same || pend)) { js = slot; act = same ? 1 : (empty ? 2 : 3); }
+}
+
 __device__ uint32_t dict_find_or_insert(uint64_t *dict, uint32_t mask, uint64_t lo, uint64_t hi, bool active) {
-  uint32_t s = (uint32_t)key_hash(lo, hi) & mask;
+  uint32_t s = key_hash(lo, hi) & mask;
   uint32_t result = kInvalidSlot;
   bool done = !active;
   const uint32_t limit = (mask + 1) + 4096;
@@ -81,16 +89,15 @@ __device__ uint32_t dict_find_or_insert(uint64_t *dict, uint32_t mask, uint64_t 
     uint32_t js = 0;        // slot to act on this round
     int act = 0;            // 0 advance, 1 found, 2 try claim, 3 recheck pending
     if (!done) {
-      ulonglong2 e[4];
-#pragma unroll
-      for (int j = 0; j < 4; j++) e[j] = *reinterpret_cast<const ulonglong2 *>(dict + 2 * (size_t)((s + j) & mask));
-#pragma unroll
-      for (int j = 3; j >= 0; j--) {   // earliest slot wins
-        const bool empty = e[j].x == 0;
-        const bool same = e[j].x == lo && e[j].y == hi;
-        const bool pend = e[j].x == lo && e[j].y == 0;
-        if (empty || same || pend) { js = (s + j) & mask; act = same ? 1 : (empty ? 2 : 3); }
-      }
+      const uint32_t s1 = (s + 1) & mask, s2 = (s + 2) & mask, s3 = (s + 3) & mask;
+      const ulonglong2 e0 = *reinterpret_cast<const ulonglong2 *>(dict + 2 * (size_t)s);
+      const ulonglong2 e1 = *reinterpret_cast<const ulonglong2 *>(dict + 2 * (size_t)s1);
+      const ulonglong2 e2 = *reinterpret_cast<const ulonglong2 *>(dict + 2 * (size_t)s2);
+      const ulonglong2 e3 = *reinterpret_cast<const ulonglong2 *>(dict + 2 * (size_t)s3);
+      probe_pick(e0, s, lo, hi, js, act);
+      probe_pick(e1, s1, lo, hi, js, act);
+      probe_pick(e2, s2, lo, hi, js, act);
+      probe_pick(e3, s3, lo, hi, js, act);
       if (act == 0) s = (s + 4) & mask;
       if (act == 1) { result = js; done = true; }
     }
@@ -118,7 +125,7 @@ __device__ uint32_t dict_find_or_insert(uint64_t *dict, uint32_t mask, uint64_t 
 // Per-document table in global memory (long path).  Only the owning
 // workgroup touches it, so workgroup-scope atomics are sufficient.
 __device__ uint32_t gtable_insert(uint64_t *keys, uint32_t *cnt, uint32_t mask, uint64_t lo, uint64_t hi) {
-  uint32_t s = (uint32_t)key_hash(lo, hi) & mask;
+  uint32_t s = (key_hash(lo, hi) >> 7) & mask;
   uint32_t result = kInvalidSlot;
   bool done = false;
   const uint32_t limit = 2 * (mask + 1) + 4096;
@@ -178,44 +185,102 @@ __device__ __forceinline__ void stage_bytes(uint8_t *lds, const uint8_t *gsrc, u
   *shift_out = shift;
 }
 
-__device__ __forceinline__ uint8_t code_at(const uint8_t *text, const uint8_t *lut, uint32_t shift, int64_t r,
-                                           int64_t wlen) {
-  if (r < 0 || r >= wlen) return 0;
-  uint8_t c = text[shift + r];
-  return lut[c & 127];
+// ---- SWAR word-break classification (4 ASCII bytes per 32-bit op; every
+// byte is < 0x80 once the non-ASCII check passed, so byte-wise adds never
+// carry).  Flags live in bit 7 of each byte.
+__device__ __forceinline__ uint32_t swar_eq(uint32_t x, uint32_t c4) { return ~((x ^ c4) + 0x7F7F7F7Fu) & 0x80808080u; }
+__device__ __forceinline__ uint32_t swar_letter(uint32_t x) {
+  const uint32_t lw = x | 0x20202020u;                       // fold case
+  return (lw + 0x1F1F1F1Fu) & ~(lw + 0x05050505u) & 0x80808080u;   // 'a'..'z'
+}
+__device__ __forceinline__ uint32_t swar_digit(uint32_t x) {
+  return (x + 0x50505050u) & ~(x + 0x46464646u) & 0x80808080u;     // '0'..'9'
+}
+// bit-7 flags of the 4 bytes -> 4-bit nibble (byte k -> bit k)
+__device__ __forceinline__ uint32_t swar_nib(uint32_t w) {
+  const uint32_t f = (w >> 7) & 0x01010101u;
+  const uint32_t g = f | (f >> 7);
+  return (g | (g >> 14)) & 0xFu;
+}
+// LD flags of one byte: letter -> bit 7, digit -> bit 6
+__device__ __forceinline__ uint32_t ld_byte(uint32_t c) {
+  const uint32_t l = ((c | 0x20u) - 'a') < 26u, d = (c - '0') < 10u;
+  return (l << 7) | (d << 6);
 }
 
-// Word-segment bits, 64 positions per wave-iteration: one LDS byte read +
-// one class-LUT read per lane; neighbour classes by lane shuffle (only lanes
-// 0 and 63 read across the 64-byte boundary); the membership bits of the
-// 64 positions are one __ballot.  Returns true (block-uniform) if a
-// non-ASCII byte is present.
-__device__ bool phase_wordbits(const uint8_t *text, const uint8_t *lut, uint32_t shift, uint32_t wlen,
-                               uint64_t *wbits, uint32_t *flag_lds) {
+// Word-segment bits for buffer positions [0, hi): unit u (16 bits) covers
+// bytes [16u, 16u + 16) of the LDS buffer; bytes outside [lo, hi) are blanked
+// to ' ' (class Other).  One lane classifies 16 bytes (one ds_read_b128);
+// cross-lane neighbours by shuffle.  Returns true (block-uniform) if a
+// non-ASCII byte lies in [lo, hi).
+__device__ bool phase_wordbits(const uint8_t *text, uint32_t lo, uint32_t hi, uint64_t *wbits, uint32_t *flag_lds) {
   const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const uint32_t nwords = (wlen + 63) >> 6;
-  bool nonascii = false;
-  for (uint32_t m = wid; m < nwords; m += 4) {
-    const int64_t r = (int64_t)m * 64 + lane;
-    uint32_t cur = 0;
-    if (r < wlen) {
-      const uint8_t c = text[shift + r];
-      nonascii |= c >= 128;
-      cur = lut[c & 127];
+  const uint32_t nunits = (hi + 15) >> 4;
+  const uint32_t nblocks = (nunits + 63) >> 6;
+  uint16_t *units = reinterpret_cast<uint16_t *>(wbits);
+  uint32_t bad = 0;
+  for (uint32_t k = wid; k < nblocks; k += 4) {
+    const uint32_t u = k * 64 + lane;
+    const uint32_t base = u * 16;
+    uint32_t x0 = 0x20202020u, x1 = 0x20202020u, x2 = 0x20202020u, x3 = 0x20202020u;
+    if (u < nunits) {
+      const uint4 v = *reinterpret_cast<const uint4 *>(text + base);
+      x0 = v.x; x1 = v.y; x2 = v.z; x3 = v.w;
+      if (base < lo || base + 16 > hi) {              // edge unit: blank bytes outside [lo, hi)
+        uint32_t xs[4] = {x0, x1, x2, x3};
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+#pragma unroll
+          for (int bb = 0; bb < 4; bb++) {
+            const uint32_t pos = base + 4 * i + bb;
+            if (pos < lo || pos >= hi) xs[i] = (xs[i] & ~(0xFFu << (8 * bb))) | (0x20u << (8 * bb));
+          }
+        x0 = xs[0]; x1 = xs[1]; x2 = xs[2]; x3 = xs[3];
+      }
     }
-    uint32_t prev = __shfl_up(cur, 1, 64);
-    uint32_t next = __shfl_down(cur, 1, 64);
-    if (lane == 0) prev = code_at(text, lut, shift, r - 1, wlen);
-    if (lane == 63) next = code_at(text, lut, shift, r + 1, wlen);
-    const bool w = (r < wlen) && wb_is_word((uint8_t)prev, (uint8_t)cur, (uint8_t)next);
-    const uint64_t mask = __ballot(w);
-    if (lane == 0) wbits[m] = mask;
+    bad |= (x0 | x1 | x2 | x3) & 0x80808080u;
+    const uint32_t L0 = swar_letter(x0), L1 = swar_letter(x1), L2 = swar_letter(x2), L3 = swar_letter(x3);
+    const uint32_t D0 = swar_digit(x0), D1 = swar_digit(x1), D2 = swar_digit(x2), D3 = swar_digit(x3);
+    const uint32_t C0 = L0 | D0 | swar_eq(x0, 0x5F5F5F5Fu), C1 = L1 | D1 | swar_eq(x1, 0x5F5F5F5Fu);
+    const uint32_t C2 = L2 | D2 | swar_eq(x2, 0x5F5F5F5Fu), C3 = L3 | D3 | swar_eq(x3, 0x5F5F5F5Fu);
+    const uint32_t LD0 = L0 | (D0 >> 1), LD1 = L1 | (D1 >> 1), LD2 = L2 | (D2 >> 1), LD3 = L3 | (D3 >> 1);
+    // candidate joiners: bytes in 0x27..0x3B that are not digits (' ( ) * + , - . / : ;)
+    auto punct = [](uint32_t x, uint32_t d) {
+      return (x + 0x59595959u) & ~(x + 0x44444444u) & ~d & 0x80808080u;
+    };
+    const uint32_t P = punct(x0, D0) | punct(x1, D1) | punct(x2, D2) | punct(x3, D3);
+    uint32_t ML0 = 0, ML1 = 0, ML2 = 0, ML3 = 0, MN0 = 0, MN1 = 0, MN2 = 0, MN3 = 0;
+    if (__any(P != 0)) {
+      auto mids = [](uint32_t x, uint32_t &ml, uint32_t &mn) {
+        const uint32_t both = swar_eq(x, 0x2E2E2E2Eu) | swar_eq(x, 0x27272727u);   // '.' '\''
+        ml = both | swar_eq(x, 0x3A3A3A3Au);                                       // ':'
+        mn = both | swar_eq(x, 0x2C2C2C2Cu) | swar_eq(x, 0x3B3B3B3Bu);             // ',' ';'
+      };
+      mids(x0, ML0, MN0); mids(x1, ML1, MN1); mids(x2, ML2, MN2); mids(x3, ML3, MN3);
+    }
+    // neighbour flags across lanes (byte before this unit / byte after it)
+    uint32_t ldp = __shfl_up(LD3, 1, 64);
+    uint32_t ldn = __shfl_down(LD0, 1, 64);
+    if (lane == 0) ldp = (base >= 1 && base - 1 >= lo && base - 1 < hi) ? ld_byte(text[base - 1]) << 24 : 0u;
+    if (lane == 63) ldn = (base + 16 >= lo && base + 16 < hi) ? ld_byte(text[base + 16]) : 0u;
+    auto word = [](uint32_t c, uint32_t ml, uint32_t mn, uint32_t ld_prev4, uint32_t ld, uint32_t ld_next4) {
+      const uint32_t p = __builtin_amdgcn_alignbyte(ld, ld_prev4, 3);   // flags of byte i-1
+      const uint32_t n = __builtin_amdgcn_alignbyte(ld_next4, ld, 1);   // flags of byte i+1
+      const uint32_t x = p & n;                                           // bit7 Lp&Ln, bit6 Dp&Dn
+      return (c | (ml & x) | (mn & (x << 1))) & 0x80808080u;
+    };
+    const uint32_t w0 = word(C0, ML0, MN0, ldp, LD0, LD1);
+    const uint32_t w1 = word(C1, ML1, MN1, LD0, LD1, LD2);
+    const uint32_t w2 = word(C2, ML2, MN2, LD1, LD2, LD3);
+    const uint32_t w3 = word(C3, ML3, MN3, LD2, LD3, ldn);
+    const uint32_t m16 = swar_nib(w0) | (swar_nib(w1) << 4) | (swar_nib(w2) << 8) | (swar_nib(w3) << 12);
+    if (u < nunits) units[u] = (uint16_t)m16;
   }
-  if (__any(nonascii) && lane == 0) atomicOr(flag_lds, 1u);
+  if (__any(bad != 0) && lane == 0) atomicOr(flag_lds, 1u);
   lds_barrier();
-  const bool bad = (*flag_lds & 1u) != 0;
+  const bool isbad = (*flag_lds & 1u) != 0;
   lds_barrier();      // every thread has read the flag before anyone resets it
-  return bad;
+  return isbad;
 }
 
 // Token spans starting in window positions [r0, r1).  Writes (start, end)
@@ -268,35 +333,62 @@ __device__ uint32_t phase_token_spans(const uint64_t *wbits, uint32_t wlen, uint
   return total_all;
 }
 
-// Key of the token [s, e) of the window; *valid = false if the span holds no
-// letter/digit (a run of '_' is not a token).  The 7-bit packing is exact
-// for <= 18 bytes; only longer tokens pay for the two hashes.
-__device__ __forceinline__ void token_key(const uint8_t *text, const uint8_t *lut, uint32_t shift, uint32_t s,
-                                          uint32_t e, uint64_t *lo, uint64_t *hi, bool *valid) {
+// Key of the token at LDS buffer bytes [s, e); *valid = false if the span
+// holds no letter/digit (only '_' can form such a span).  Tokens of <= 18
+// bytes are packed 4 bytes per step: funnel-shift to the token start,
+// blank the tail, SWAR lower-case, 4 x 7-bit pack; longer tokens are hashed.
+__device__ __forceinline__ uint32_t keep_bytes(uint32_t n, uint32_t i) {   // bytes 4i.. of a token of length n
+  return n >= 4 * i + 4 ? 0xFFFFFFFFu : (n <= 4 * i ? 0u : (0xFFFFFFFFu >> (8 * (4 * i + 4 - n))));
+}
+__device__ __forceinline__ uint32_t pack7(uint32_t t) {
+  return (t & 0x7Fu) | (__builtin_amdgcn_ubfe(t, 8, 7) << 7) | (__builtin_amdgcn_ubfe(t, 16, 7) << 14) |
+         (__builtin_amdgcn_ubfe(t, 24, 7) << 21);
+}
+__device__ __forceinline__ uint32_t lower4(uint32_t t) {
+  const uint32_t up = (t + 0x3F3F3F3Fu) & ~(t + 0x25252525u) & 0x80808080u;   // 'A'..'Z'
+  return t | (up >> 2);
+}
+
+__device__ __forceinline__ void token_key(const uint8_t *text, uint32_t s, uint32_t e, uint64_t *lo, uint64_t *hi,
+                                          bool *valid) {
   const uint32_t n = e - s;
-  uint8_t any = 0;
-  if (n <= kShortKeyChars) {
-    uint64_t a = 0, b = 0;
-    for (uint32_t j = 0; j < n; j++) {
-      const uint8_t c = text[shift + s + j];
-      any |= lut[c & 127];
-      const uint64_t v = ascii_lower(c);
-      const uint32_t bit = 7 * j;
-      if (bit < 64) a |= v << bit;
-      if (bit + 7 > 64) b |= bit < 64 ? (v >> (64 - bit)) : (v << (bit - 64));
-    }
-    *lo = a;
-    *hi = b | kKeyValid;
-  } else {
+  if (n > kShortKeyChars) {
     KeyBuilder kb;
+    bool any = false;
     for (uint32_t j = s; j < e; j++) {
-      const uint8_t c = text[shift + j];
-      any |= lut[c & 127];
+      const uint8_t c = text[j];
+      any |= c != '_';
       kb.push(ascii_lower(c));
     }
     kb.finish(lo, hi);
+    *valid = any;
+    return;
   }
-  *valid = (any & (kClsL | kClsD)) != 0;
+  const uint32_t *tw = reinterpret_cast<const uint32_t *>(text);
+  const uint32_t a0 = s >> 2, o = s & 3;
+  const uint32_t d0 = tw[a0], d1 = tw[a0 + 1], d2 = tw[a0 + 2];
+  uint32_t t0 = __builtin_amdgcn_alignbyte(d1, d0, o) & keep_bytes(n, 0);
+  uint32_t t1 = __builtin_amdgcn_alignbyte(d2, d1, o) & keep_bytes(n, 1);
+  uint32_t nu = ((t0 ^ 0x5F5F5F5Fu) & keep_bytes(n, 0)) | ((t1 ^ 0x5F5F5F5Fu) & keep_bytes(n, 1));
+  const uint32_t p0 = pack7(lower4(t0)), p1 = pack7(lower4(t1));
+  uint32_t p2 = 0, p3 = 0, p4 = 0;
+  if (__any(n > 8)) {
+    if (n > 8) {
+      const uint32_t d3 = tw[a0 + 3], d4 = tw[a0 + 4], d5 = tw[a0 + 5];
+      const uint32_t t2 = __builtin_amdgcn_alignbyte(d3, d2, o) & keep_bytes(n, 2);
+      const uint32_t t3 = __builtin_amdgcn_alignbyte(d4, d3, o) & keep_bytes(n, 3);
+      const uint32_t t4 = __builtin_amdgcn_alignbyte(d5, d4, o) & keep_bytes(n, 4);
+      nu |= ((t2 ^ 0x5F5F5F5Fu) & keep_bytes(n, 2)) | ((t3 ^ 0x5F5F5F5Fu) & keep_bytes(n, 3)) |
+            ((t4 ^ 0x5F5F5F5Fu) & keep_bytes(n, 4));
+      p2 = pack7(lower4(t2));
+      p3 = pack7(lower4(t3));
+      p4 = pack7(lower4(t4));
+    }
+  }
+  // char j at bit 5 + 7j; group i (4 chars) at bit 5 + 28i; length in bits 0..4
+  *lo = (uint64_t)n | ((uint64_t)p0 << 5) | ((uint64_t)p1 << 33) | ((uint64_t)p2 << 61);
+  *hi = ((uint64_t)p2 >> 3) | ((uint64_t)p3 << 25) | ((uint64_t)p4 << 53) | kKeyValid;
+  *valid = nu != 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -318,72 +410,73 @@ struct ShortSmem {
   alignas(16) uint8_t text[kShortMaxBytes + 64];
 };
 
+// Per-document TF histogram in LDS.  One returning ds_cmpst_b64 per probe
+// claims an empty slot (lo 0 -> key lo) or reports the resident lo; equal lo
+// means equal length, and for tokens of <= 8 bytes equal lo is equality (hi
+// is VALID alone), so only longer tokens read hi.  Counting is a
+// non-returning ds_add; the list of used slots is built afterwards.
 __device__ __forceinline__ void lds_table_insert(ShortSmem &sm, uint64_t lo, uint64_t hi, bool active) {
-  uint32_t s = (uint32_t)key_hash(lo, hi) & (kShortTable - 1);
+  uint32_t s = key_hash(lo, hi) >> (32 - 10);           // top 10 bits (kShortTable = 1024)
+  const bool short8 = ((uint32_t)(lo & 31) - 1u) < 8u;   // 1..8 bytes (long keys have 0)
   bool done = !active;
-  for (uint32_t it = 0; it < 2 * kShortTable + 256; it++) {
+  for (uint32_t it = 0; it < kShortTable + 64; it++) {
     if (__all(done)) return;
-    bool claimed = false;
-    uint64_t clo = 0, chi = 0;
-    if (!done) {
-      clo = *(volatile uint64_t *)&sm.t_lo[s];
-      if (clo == 0) {
-        unsigned long long old = atomicCAS((unsigned long long *)&sm.t_lo[s], 0ull, (unsigned long long)lo);
-        if (old == 0) {
-          *(volatile uint64_t *)&sm.t_hi[s] = hi;
-          atomicAdd(&sm.t_cnt[s], 1u);
-          const uint32_t idx = atomicAdd(&sm.n_uniq, 1u);
-          sm.claimed[idx] = (uint16_t)s;
-          claimed = true;
-          done = true;
-        } else {
-          clo = old;
-        }
-      }
-    }
+    uint64_t old = 0;
+    if (!done) old = atomicCAS((unsigned long long *)&sm.t_lo[s], 0ull, (unsigned long long)lo);
+    const bool claimed = !done && old == 0;
+    if (claimed) __hip_atomic_store(&sm.t_hi[s], hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     asm volatile("" ::: "memory");
-    if (!done && !claimed) {
-      if (clo == lo) {
-        chi = *(volatile uint64_t *)&sm.t_hi[s];
-        if (chi == hi) {
-          atomicAdd(&sm.t_cnt[s], 1u);
-          done = true;
-        } else if (chi != 0) {
-          s = (s + 1) & (kShortTable - 1);
-        }
-        // chi == 0: claimed by another wave, not yet published -> retry slot
-      } else {
-        s = (s + 1) & (kShortTable - 1);
-      }
+    bool hit = claimed || (!done && old == lo && short8);
+    if (!done && !hit && old == lo) {                    // same length > 8: compare hi
+      const uint64_t chi = __hip_atomic_load(&sm.t_hi[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (chi == hi) hit = true;
+      // chi == 0: claimed by another wave, hi not yet visible -> retry the same slot
+      if (chi != hi && chi != 0) s = (s + 1) & (kShortTable - 1);
+    } else if (!done && !hit) {
+      s = (s + 1) & (kShortTable - 1);
+    }
+    if (hit) {
+      atomicAdd(&sm.t_cnt[s], 1u);
+      done = true;
     }
   }
   if (!done) atomicOr(&sm.flags, 2u);   // overflow -> long path
 }
 
-// Prefetch of a short document's bytes into registers: 2 x 16 B per thread
-// covers 4096 + 15 bytes of misalignment.
-struct DocPrefetch {
-  uint4 v0, v1;
+// Next-document prefetch into registers: 2 x 16 B per thread covers 4096 +
+// 15 bytes of misalignment.  Loads go through an explicit global
+// (address_space 1) pointer so they are global_load_dwordx4 and stay in
+// flight (nothing waits on them) until the next document is staged.
+__device__ __forceinline__ uint4 gload16(const void *ptr) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  typedef __attribute__((address_space(1))) const uint32_t gu32;
+  gu32 *g = (gu32 *)ptr;
+  return make_uint4(g[0], g[1], g[2], g[3]);
+#else
+  return *reinterpret_cast<const uint4 *>(ptr);
+#endif
+}
+
+struct DocMeta {
   uint64_t s0, L, src;
   uint32_t shift;
-  bool valid;
 };
 
-__device__ __forceinline__ void prefetch_doc(const BuildParams &p, uint64_t d, DocPrefetch &pf) {
-  pf.valid = d < p.n_docs;
-  if (!pf.valid) return;
-  pf.src = p.live_map ? p.live_map[d] : d;
-  pf.s0 = p.offsets[pf.src];
-  pf.L = p.offsets[pf.src + 1] - pf.s0;
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p.text + pf.s0);
-  const uintptr_t al = a & ~(uintptr_t)15;
-  pf.shift = (uint32_t)(a - al);
-  if (pf.L > kShortMaxBytes) return;
-  const uint32_t nchunks = (uint32_t)((pf.shift + pf.L + 15) >> 4);
-  const uint4 *src = reinterpret_cast<const uint4 *>(al);
-  const uint4 z = make_uint4(0, 0, 0, 0);
-  pf.v0 = threadIdx.x < nchunks ? src[threadIdx.x] : z;
-  pf.v1 = threadIdx.x + 256 < nchunks ? src[threadIdx.x + 256] : z;
+__device__ __forceinline__ DocMeta doc_meta(const BuildParams &p, uint64_t d) {
+  DocMeta m;
+  m.src = p.live_map ? p.live_map[d] : d;
+  m.s0 = p.offsets[m.src];
+  m.L = p.offsets[m.src + 1] - m.s0;
+  m.shift = (uint32_t)(reinterpret_cast<uintptr_t>(p.text + m.s0) & 15);
+  return m;
+}
+
+__device__ __forceinline__ void prefetch_text(const BuildParams &p, const DocMeta &m, uint4 &v0, uint4 &v1) {
+  if (m.L > kShortMaxBytes) return;
+  const uint32_t nchunks = (uint32_t)((m.shift + m.L + 15) >> 4);
+  const uint4 *src = reinterpret_cast<const uint4 *>(reinterpret_cast<uintptr_t>(p.text + m.s0) & ~(uintptr_t)15);
+  if (threadIdx.x < nchunks) v0 = gload16(src + threadIdx.x);
+  if (threadIdx.x + 256 < nchunks) v1 = gload16(src + threadIdx.x + 256);
 }
 
 __global__ void __launch_bounds__(256) k_tokenize_short(BuildParams p) {
@@ -394,26 +487,33 @@ __global__ void __launch_bounds__(256) k_tokenize_short(BuildParams p) {
   if (tid < 64) { sm.rcnt[tid] = 0; sm.rcur[tid] = 0; }
   if (tid == 0) { sm.n_uniq = 0; sm.len = 0; sm.flags = 0; }
   unsigned long long my_doc_count = 0, my_ttf = 0, my_nnz = 0;
-  DocPrefetch pf;
-  prefetch_doc(p, blockIdx.x, pf);
+  uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
+  DocMeta meta;
+  if (blockIdx.x < p.n_docs) {
+    meta = doc_meta(p, blockIdx.x);
+    prefetch_text(p, meta, v0, v1);
+  }
   lds_barrier();
 
   for (uint64_t d = blockIdx.x; d < p.n_docs; d += gridDim.x) {
-    const uint64_t src = pf.src, L = pf.L;
-    const uint32_t shift = pf.shift;
+    const uint64_t src = meta.src, L = meta.L;
+    const uint32_t shift = meta.shift;
+    const uint64_t dn = d + gridDim.x;
     if (L > kShortMaxBytes) {
       if (tid == 0) p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
-      prefetch_doc(p, d + gridDim.x, pf);
+      if (dn < p.n_docs) { meta = doc_meta(p, dn); prefetch_text(p, meta, v0, v1); }
       continue;                                           // block-uniform
     }
     // stage from registers, then start fetching the next document
     uint4 *dst = reinterpret_cast<uint4 *>(sm.text);
     const uint32_t nchunks = (uint32_t)((shift + L + 15) >> 4);
-    if (tid < nchunks) dst[tid] = pf.v0;
-    if (tid + 256 < nchunks) dst[tid + 256] = pf.v1;
-    prefetch_doc(p, d + gridDim.x, pf);
+    if (tid < nchunks) dst[tid] = v0;
+    if (tid + 256 < nchunks) dst[tid + 256] = v1;
+    if (dn < p.n_docs) { meta = doc_meta(p, dn); prefetch_text(p, meta, v0, v1); }
     lds_barrier();
-    const bool nonascii = phase_wordbits(sm.text, sm.lut, shift, (uint32_t)L, sm.wbits, &sm.flags);
+    if (p.debug_stop == 1) continue;
+    const uint32_t lo_b = shift, hi_b = shift + (uint32_t)L;     // document bytes in buffer coordinates
+    const bool nonascii = phase_wordbits(sm.text, lo_b, hi_b, sm.wbits, &sm.flags);
     if (nonascii) {
       if (tid == 0) {
         set_err(p.err, kErrNonAscii, (uint32_t)d);
@@ -424,8 +524,10 @@ __global__ void __launch_bounds__(256) k_tokenize_short(BuildParams p) {
       lds_barrier();
       continue;
     }
-    const uint32_t ntok = phase_token_spans(sm.wbits, (uint32_t)L, 0, (uint32_t)L, sm.tok_s, sm.tok_e,
-                                            kShortMaxTokens, sm.scan);
+    if (p.debug_stop == 2) continue;
+    const uint32_t ntok = phase_token_spans(sm.wbits, hi_b, lo_b, hi_b, sm.tok_s, sm.tok_e, kShortMaxTokens,
+                                            sm.scan);
+    if (p.debug_stop == 3) continue;
     if (ntok > kShortMaxTokens) {
       if (tid == 0) p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
       lds_barrier();
@@ -442,7 +544,7 @@ __global__ void __launch_bounds__(256) k_tokenize_short(BuildParams p) {
         if (e - s > kMaxTokenLen) {
           set_err(p.err, kErrTokenTooLong, (uint32_t)d);
         } else {
-          token_key(sm.text, sm.lut, shift, s, e, &lo, &hi, &valid);
+          token_key(sm.text, s, e, &lo, &hi, &valid);
         }
       }
       my_len += valid;
@@ -450,7 +552,29 @@ __global__ void __launch_bounds__(256) k_tokenize_short(BuildParams p) {
     }
     atomicAdd(&sm.len, my_len);
     lds_barrier();
+    {   // list of used slots: each thread owns 4 consecutive slots
+      uint32_t used = 0;
+#pragma unroll
+      for (int q = 0; q < 4; q++) used |= (sm.t_lo[tid * 4 + q] != 0) << q;
+      uint32_t total;
+      uint32_t at = block_excl_scan_256(__popc(used), sm.scan, &total);
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        if (used & (1u << q)) sm.claimed[at++] = (uint16_t)(tid * 4 + q);
+      if (tid == 0) sm.n_uniq = total;
+      lds_barrier();
+    }
     const uint32_t nu = sm.n_uniq;
+    if (p.debug_stop == 4) {
+      for (uint32_t i = tid; i < nu; i += 256) {
+        const uint32_t s = sm.claimed[i];
+        sm.t_lo[s] = 0; sm.t_hi[s] = 0; sm.t_cnt[s] = 0;
+      }
+      lds_barrier();
+      if (tid == 0) { sm.n_uniq = 0; sm.len = 0; sm.flags = 0; }
+      lds_barrier();
+      continue;
+    }
     if (sm.flags & 2u) {                                  // LDS table overflow
       for (uint32_t i = tid; i < nu; i += 256) {
         const uint32_t s = sm.claimed[i];
@@ -479,6 +603,17 @@ __global__ void __launch_bounds__(256) k_tokenize_short(BuildParams p) {
       }
     }
     lds_barrier();
+    if (p.debug_stop == 5) {
+      for (uint32_t i = tid; i < nu; i += 256) {
+        const uint32_t s = sm.claimed[i];
+        sm.t_lo[s] = 0; sm.t_hi[s] = 0; sm.t_cnt[s] = 0;
+      }
+      if (tid < 64) sm.rcnt[tid] = 0;
+      lds_barrier();
+      if (tid == 0) { sm.n_uniq = 0; sm.len = 0; sm.flags = 0; }
+      lds_barrier();
+      continue;
+    }
     if (tid == 0) {
       uint32_t run = 0;
       for (uint32_t r = 0; r < p.n_ranges; r++) {
@@ -566,15 +701,16 @@ __global__ void __launch_bounds__(256) k_tokenize_long(BuildParams p) {
       uint32_t shift;
       stage_bytes(sm.text, p.text + s0 + wlo, wlen, &shift);
       __syncthreads();
-      if (phase_wordbits(sm.text, sm.lut, shift, wlen, sm.wbits, &sm.flags)) { bad = true; break; }
-      const uint32_t ntok = phase_token_spans(sm.wbits, wlen, (uint32_t)(cs - wlo), (uint32_t)(ce - wlo),
-                                              sm.tok_s, sm.tok_e, kChunk / 2 + 8, sm.scan);
+      const uint32_t hi_b = shift + wlen;
+      if (phase_wordbits(sm.text, shift, hi_b, sm.wbits, &sm.flags)) { bad = true; break; }
+      const uint32_t ntok = phase_token_spans(sm.wbits, hi_b, shift + (uint32_t)(cs - wlo),
+                                              shift + (uint32_t)(ce - wlo), sm.tok_s, sm.tok_e, kChunk / 2 + 8, sm.scan);
       for (uint32_t i = tid; i < ntok; i += 256) {
         const uint32_t s = sm.tok_s[i], e = sm.tok_e[i];
         if (e - s > kMaxTokenLen) { set_err(p.err, kErrTokenTooLong, d); continue; }
         uint64_t lo, hi;
         bool valid;
-        token_key(sm.text, sm.lut, shift, s, e, &lo, &hi, &valid);
+        token_key(sm.text, s, e, &lo, &hi, &valid);
         if (!valid) continue;
         my_len++;
         if (gtable_insert(keys, cnt, mask, lo, hi) == kInvalidSlot) atomicOr(&sm.flags, 4u);
@@ -697,29 +833,63 @@ __global__ void __launch_bounds__(256) k_block_scan(PostingParams p) {
   p.blk[(size_t)p.n_blocks * p.C + t] = run;
 }
 
-// single workgroup exclusive scan of df (row n_blocks of blk) -> col_ptr[C + 1]
+// single workgroup exclusive scan of df (row n_blocks of blk) -> col_ptr[C + 1].
+// Tiles of 16384 slots: each thread loads 16 consecutive df values with four
+// 16 B loads (coalesced across the workgroup), scans them in registers, and a
+// workgroup scan of the 1024 thread totals gives the offsets.
 __global__ void __launch_bounds__(1024) k_col_scan(PostingParams p) {
-  __shared__ unsigned long long part[1024];
+  __shared__ unsigned long long wsum[16];
+  __shared__ unsigned long long carry_sh;
   const uint32_t *df = p.blk + (size_t)p.n_blocks * p.C;
-  const uint32_t per = (p.C + 1023) / 1024;
-  const uint64_t a = (uint64_t)threadIdx.x * per;
-  const uint64_t z = a + per < p.C ? a + per : p.C;
-  unsigned long long s = 0;
-  for (uint64_t i = a; i < z; i++) s += df[i];
-  part[threadIdx.x] = s;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) carry_sh = 0;
   __syncthreads();
-  for (uint32_t o = 1; o < 1024; o <<= 1) {
-    unsigned long long v = threadIdx.x >= o ? part[threadIdx.x - o] : 0ull;
+  for (uint32_t t0 = 0; t0 < p.C; t0 += 16384) {
+    const uint32_t i0 = t0 + tid * 16;
+    uint32_t v[16];
+    if (i0 + 16 <= p.C) {
+      const uint4 *src = reinterpret_cast<const uint4 *>(df + i0);
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint4 x = src[q];
+        v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; q++) v[q] = (i0 + q < p.C) ? df[i0 + q] : 0u;
+    }
+    unsigned long long tot = 0;
+#pragma unroll
+    for (int q = 0; q < 16; q++) tot += v[q];
+    // workgroup exclusive scan of tot
+    unsigned long long x = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      unsigned long long y = __shfl_up(x, o, 64);
+      if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
     __syncthreads();
-    part[threadIdx.x] += v;
+    unsigned long long base = carry_sh, all = 0;
+    for (uint32_t w = 0; w < 16; w++) {
+      const unsigned long long sw = wsum[w];
+      if (w < wid) base += sw;
+      all += sw;
+    }
+    base += x - tot;
+    __syncthreads();
+    if (tid == 0) carry_sh += all;
+    unsigned long long run = base;
+    if (i0 < p.C) {
+#pragma unroll
+      for (int q = 0; q < 16; q++) {
+        if (i0 + q < p.C) p.col_ptr[i0 + q] = run;
+        run += v[q];
+      }
+    }
     __syncthreads();
   }
-  unsigned long long run = part[threadIdx.x] - s;
-  for (uint64_t i = a; i < z; i++) {
-    p.col_ptr[i] = run;
-    run += df[i];
-  }
-  if (threadIdx.x == 1023) p.col_ptr[p.C] = part[1023];
+  if (tid == 0) p.col_ptr[p.C] = carry_sh;
 }
 
 // grid (n_blocks, n_ranges), 1024 threads: LDS cursor per slot of the range.

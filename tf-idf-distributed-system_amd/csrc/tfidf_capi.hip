@@ -7,6 +7,7 @@
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -414,6 +415,7 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   bp.long_count = reinterpret_cast<uint32_t *>(ctr + 4);
   bp.stats = reinterpret_cast<unsigned long long *>(ctr);
   bp.err = reinterpret_cast<uint32_t *>(ctr + 3);
+  if (const char *ds = getenv("TFIDF_DEBUG_STOP")) bp.debug_stop = (uint32_t)atoi(ds);   // profiling only
 
   HIP_TRY(hipEventRecord(ix->ev[EV_START], s));
   if (N) {
@@ -421,6 +423,16 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
     HIP_TRY(launch_tokenize_short(bp, (int)grid, s));
   }
   HIP_TRY(hipEventRecord(ix->ev[EV_TOK], s));
+  if (bp.debug_stop) {                      // profiling only: rows are incomplete, stop here
+    HIP_TRY(hipStreamSynchronize(s));
+    ix->timing = tfidf_commit_timing{};
+    ix->timing.ms_tokenize = ev_ms(ix, EV_START, EV_TOK);
+    ix->timing.ms_total = ix->timing.ms_tokenize;
+    ix->timing.text_bytes = ix->text_bytes;
+    ix->timing.num_docs = N;
+    ix->committed = false;
+    return TFIDF_OK;
+  }
   uint32_t n_long = 0;
   HIP_TRY(hipMemcpyAsync(&n_long, ctr + 4, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));

@@ -1,13 +1,14 @@
 // tfidf_common.h — definitions shared by host and device code of libtfidf.
 //
 // Term identity.  A term is the lower-cased byte string of a StandardAnalyzer
-// token (Lucene 9.8.0).  The engine keys terms by 128 bits:
-//   * tokens of <= 18 bytes: the 7-bit ASCII codes packed little-endian,
-//     char j at bits [7j, 7j+7) of the 126-bit payload — an exact, collision
-//     free encoding (ASCII only; non-ASCII input is rejected upstream);
-//   * longer tokens (19..255 bytes): two independent 64-bit hashes with the
-//     LONG flag set.
-// Bit 127 (VALID) is set for every key so that hi == 0 marks an empty slot.
+// token (Lucene 9.8.0).  The engine keys terms by 128 bits (lo, hi):
+//   * tokens of <= 17 bytes: exact — bits 0..4 of lo = length, char j (7-bit
+//     ASCII) at bits [5 + 7j, 12 + 7j) of the 128-bit value.  Because the
+//     length sits in lo, two keys with equal lo have equal length, and a
+//     token of <= 8 bytes is fully described by lo (its hi is VALID alone);
+//   * longer tokens (18..255 bytes): two independent 64-bit hashes with the
+//     LONG flag set (bits 0..4 of lo = 0, so they never equal a short lo).
+// Bit 127 (VALID) is set for every key so that hi == 0 marks "not written".
 #pragma once
 
 #include <stdint.h>
@@ -21,7 +22,7 @@
 namespace tfidf {
 
 constexpr uint32_t kMaxTokenLen = 255;          // StandardAnalyzer.DEFAULT_MAX_TOKEN_LENGTH
-constexpr uint32_t kShortKeyChars = 18;         // 18 * 7 = 126 payload bits
+constexpr uint32_t kShortKeyChars = 17;         // 5 + 17 * 7 = 124 payload bits
 constexpr uint64_t kKeyValid = 1ull << 63;      // in hi
 constexpr uint64_t kKeyLong = 1ull << 62;       // in hi
 constexpr uint32_t kRangeBits = 15;             // 32768 dictionary slots per LDS range tile
@@ -66,17 +67,31 @@ TFIDF_HD uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
   return z ^ (z >> 31);
 }
 
-TFIDF_HD uint64_t key_hash(uint64_t lo, uint64_t hi) { return mix64(lo ^ mix64(hi)); }
+// 32-bit multiply-xorshift hash of a 128-bit key.  The global dictionary
+// uses the low bits (slot = h & (2^c - 1), c <= 21), the per-document LDS
+// table the top 10 bits, so the two probe sequences are independent.
+TFIDF_HD uint32_t key_hash(uint64_t lo, uint64_t hi) {
+  uint32_t h = (uint32_t)lo * 0x9E3779B1u;
+  h ^= (uint32_t)(lo >> 32) * 0x85EBCA77u;
+  h ^= (uint32_t)hi * 0xC2B2AE3Du;
+  h ^= (uint32_t)(hi >> 32) * 0x27D4EB2Fu;
+  h ^= h >> 15;
+  h *= 0x2C1B3C6Du;
+  h ^= h >> 12;
+  h *= 0x297A2D39u;
+  h ^= h >> 15;
+  return h;
+}
 
 // Incremental key builder over lower-cased bytes.
 struct KeyBuilder {
-  uint64_t lo = 0, hi = 0;    // packed payload (short form)
+  uint64_t lo = 0, hi = 0;    // packed payload (short form), length added in finish()
   uint64_t h1 = 0x243F6A8885A308D3ull, h2 = 0x13198A2E03707344ull;  // long-form hashes
   uint32_t n = 0;
   TFIDF_HD void push(uint8_t c) {
-    uint32_t bit = 7 * n;
     if (n < kShortKeyChars) {
-      uint64_t v = (uint64_t)c;
+      const uint32_t bit = 5 + 7 * n;
+      const uint64_t v = (uint64_t)c;
       if (bit < 64) {
         lo |= v << bit;
         if (bit > 57) hi |= v >> (64 - bit);
@@ -90,11 +105,11 @@ struct KeyBuilder {
   }
   TFIDF_HD void finish(uint64_t *klo, uint64_t *khi) const {
     if (n <= kShortKeyChars) {
-      *klo = lo;
+      *klo = lo | n;
       *khi = hi | kKeyValid;
     } else {
-      uint64_t a = mix64(h1 ^ ((uint64_t)n << 56)) | 1ull;   // lo != 0 for every key
-      uint64_t b = mix64(h2 ^ a);
+      const uint64_t a = (mix64(h1 ^ ((uint64_t)n << 56)) & ~31ull) | 32ull;   // low 5 bits 0, lo != 0
+      const uint64_t b = mix64(h2 ^ a);
       *klo = a;
       *khi = (b & ~(3ull << 62)) | kKeyValid | kKeyLong;
     }
@@ -106,15 +121,14 @@ TFIDF_HD bool key_is_long(uint64_t hi) { return (hi & kKeyLong) != 0; }
 // Decode a short key back to bytes; returns length (0 if long).
 TFIDF_HD uint32_t key_decode(uint64_t lo, uint64_t hi, char *out) {
   if (key_is_long(hi)) return 0;
-  uint32_t n = 0;
-  for (uint32_t j = 0; j < kShortKeyChars; j++) {
-    uint32_t bit = 7 * j;
+  const uint32_t n = (uint32_t)(lo & 31);
+  for (uint32_t j = 0; j < n; j++) {
+    const uint32_t bit = 5 + 7 * j;
     uint64_t v;
     if (bit + 7 <= 64) v = (lo >> bit) & 0x7F;
     else if (bit < 64) v = ((lo >> bit) | (hi << (64 - bit))) & 0x7F;
     else v = (hi >> (bit - 64)) & 0x7F;
-    if (v == 0) break;
-    out[n++] = (char)v;
+    out[j] = (char)v;
   }
   return n;
 }

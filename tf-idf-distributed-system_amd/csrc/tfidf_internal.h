@@ -48,6 +48,7 @@ struct BuildParams {
   uint32_t *lt_cnt;           // lt_slots per workgroup
   uint32_t *lt_g;             // lt_slots per workgroup
   uint32_t lt_slots_log2;     // table slots per workgroup (max)
+  uint32_t debug_stop;        // profiling only (TFIDF_DEBUG_STOP): end each document after phase N
 };
 
 __host__ __device__ inline uint64_t csr_row_base(const uint64_t *offsets, uint64_t src) {
