@@ -56,31 +56,35 @@ def test_create_without_device_fails_loudly():
     assert rc in (L.E_NO_DEVICE, L.E_HIP)
 
 
-def _pack7(term: bytes):
-    v = len(term)
-    for j, c in enumerate(term):
-        v |= c << (5 + 7 * j)
-    return v & ((1 << 64) - 1), (v >> 64) | (1 << 63)
+def _raw_key(term):
+    """tfidf_common.h key format for terms of <= 16 bytes (exact)."""
+    b = term.lower()
+    lo = int.from_bytes(b[:8].ljust(8, b"\0"), "little")
+    if len(b) <= 8:
+        return lo, 1 << 63
+    hi = int.from_bytes(b[8:16].ljust(8, b"\0"), "little")
+    return lo | (1 << 63), hi | (1 << 63)
 
 
 @pytest.mark.parametrize("term", [b"a", b"fast", b"kheder", b"wireless", b"u.s.a", b"3,14", b"abcdefgh",
-                                  b"abcdefghi", b"abcdefghij", b"x" * 17])
-def test_short_term_keys_are_exact_7bit_packing(term):
-    assert term_key(term) == _pack7(term)
+                                  b"abcdefghi", b"abcdefghij", b"x" * 16])
+def test_exact_term_keys_are_raw_bytes(term):
+    assert term_key(term) == _raw_key(term)
 
 
 def test_short_keys_up_to_8_bytes_live_in_lo():
     for t in (b"a", b"abcdefgh", b"12345678"):
-        assert term_key(t)[1] == 1 << 63
+        lo, hi = term_key(t)
+        assert hi == 1 << 63 and lo >> 63 == 0
 
 
 def test_long_term_keys_hashed_and_distinct():
-    a = term_key(b"a" * 18)
+    a = term_key(b"a" * 17)
     b = term_key(b"a" * 20)
     c = term_key(b"b" + b"a" * 18)
     assert len({a, b, c}) == 3
     for lo, hi in (a, b, c):
-        assert hi >> 62 == 3 and lo & 31 == 0 and lo != 0   # VALID | LONG flags, length field 0
+        assert lo >> 63 == 1 and (lo >> 55) & 1 == 1 and hi >> 63 == 1   # LONG | HASHED, VALID
 
 
 def test_leader_merge_matches_oracle():

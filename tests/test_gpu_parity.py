@@ -21,12 +21,12 @@ pytestmark = pytest.mark.gpu
 
 
 def keyed(terms):
-    """Oracle doc_terms with long (> 17 byte) terms replaced by the engine's
+    """Oracle doc_terms with long (> 16 byte) terms replaced by the engine's
     printable 128-bit key: the device keys those terms by hash."""
     from tfidf_amd.engine import term_key
     out = {}
     for t, tf in terms.items():
-        if len(t) > 17:
+        if len(t) > 16:
             lo, hi = term_key(t)
             t = b"#%016x%016x" % (hi, lo)
         out[t] = tf

@@ -63,69 +63,100 @@ __device__ __forceinline__ void set_err(uint32_t *err, uint32_t flag, uint32_t d
   if (old == 0) atomicExch(err + 1, doc);
 }
 
-// Global dictionary (open addressing, 16 B slots, key lo at [2s], hi at
-// [2s+1]).  A lane probes 4 consecutive slots per round with independent
-// 16 B loads (one memory round trip covers 4 linear probes).  Claim = CAS on
-// the lo word (lo != 0 for every key), then publish hi.  Plain loads may be
-// stale but only show an older state (slots go 0 -> key once): a stale
-// "empty" falls through to the CAS, which returns the true value.  A slot
-// claimed but not yet published is re-read with an agent-scope atomic load.
-// SIMT-safe: every claiming lane publishes before any lane re-reads.
-__device__ __forceinline__ void probe_pick(ulonglong2 e, uint32_t slot, uint64_t lo, uint64_t hi, uint32_t &js,
-                                           int &act) {
-  const bool empty = e.x == 0;
-  const bool same = e.x == lo && e.y == hi;
-  const bool pend = e.x == lo && e.y == 0;
-  if (act == 0 && (empty || same || pend)) { js = slot; act = same ? 1 : (empty ? 2 : 3); }
-}
+// Global dictionary: lo[C] followed by hi[C] (u64 each).  Probing is linear
+// over the slots starting at the aligned 2-slot bucket of key_hash & (C - 1);
+// one 16 B load of lo covers a bucket.  Claim = CAS lo 0 -> key lo, then
+// publish hi (agent scope).  A resident lo equal to the lo of a key of <= 8
+// bytes IS that key (lo holds every byte; bit 63 clear), so such keys never
+// read hi; other keys compare hi, re-reading a claimed-but-unpublished hi (0).
+// Slots go 0 -> key once, so a stale plain load only shows an older state: a
+// stale "empty" falls through to the CAS, which returns the true value.
+__device__ __forceinline__ bool key_lo_is_short(uint64_t lo) { return (lo >> 63) == 0; }
 
-__device__ uint32_t dict_find_or_insert(uint64_t *dict, uint32_t mask, uint64_t lo, uint64_t hi, bool active) {
-  uint32_t s = key_hash(lo, hi) & mask;
-  uint32_t result = kInvalidSlot;
-  bool done = !active;
-  const uint32_t limit = (mask + 1) + 4096;
+template <int K>
+__device__ __forceinline__ void dict_lookup_multi(uint64_t *dict, uint32_t mask, const uint64_t *lo, const uint64_t *hi,
+                                                  const bool *act, uint32_t *out) {
+  uint64_t *dlo = dict;
+  uint64_t *dhi = dict + (size_t)mask + 1;
+  uint32_t s[K];
+  bool done[K];
+#pragma unroll
+  for (int j = 0; j < K; j++) {
+    s[j] = dict_home(dict_hash(lo[j], hi[j]), mask) & ~1u;
+    done[j] = !act[j];
+    out[j] = kInvalidSlot;
+  }
+  const uint32_t limit = mask + 1 + 4096;
   for (uint32_t it = 0; it < limit; it++) {
-    if (__all(done)) break;
-    uint32_t js = 0;        // slot to act on this round
-    int act = 0;            // 0 advance, 1 found, 2 try claim, 3 recheck pending
-    if (!done) {
-      const uint32_t s1 = (s + 1) & mask, s2 = (s + 2) & mask, s3 = (s + 3) & mask;
-      const ulonglong2 e0 = *reinterpret_cast<const ulonglong2 *>(dict + 2 * (size_t)s);
-      const ulonglong2 e1 = *reinterpret_cast<const ulonglong2 *>(dict + 2 * (size_t)s1);
-      const ulonglong2 e2 = *reinterpret_cast<const ulonglong2 *>(dict + 2 * (size_t)s2);
-      const ulonglong2 e3 = *reinterpret_cast<const ulonglong2 *>(dict + 2 * (size_t)s3);
-      probe_pick(e0, s, lo, hi, js, act);
-      probe_pick(e1, s1, lo, hi, js, act);
-      probe_pick(e2, s2, lo, hi, js, act);
-      probe_pick(e3, s3, lo, hi, js, act);
-      if (act == 0) s = (s + 4) & mask;
-      if (act == 1) { result = js; done = true; }
+    bool anyp = false;
+#pragma unroll
+    for (int j = 0; j < K; j++) anyp |= !done[j];
+    if (!__any(anyp)) break;
+    ulonglong2 e[K];
+#pragma unroll
+    for (int j = 0; j < K; j++)
+      if (!done[j]) e[j] = *reinterpret_cast<const ulonglong2 *>(dlo + (s[j] & ~1u));
+    uint32_t js[K];
+    int a[K];     // 0 advance, 1 found, 2 try claim, 3 compare hi
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+      a[j] = 0;
+      js[j] = s[j];
+      if (!done[j]) {
+        const bool sh = key_lo_is_short(lo[j]);
+        const uint64_t v0 = (s[j] & 1) ? e[j].y : e[j].x;
+        if (v0 == 0) a[j] = 2;
+        else if (v0 == lo[j]) a[j] = sh ? 1 : 3;
+        else if (!(s[j] & 1)) {
+          js[j] = s[j] + 1;
+          if (e[j].y == 0) a[j] = 2;
+          else if (e[j].y == lo[j]) a[j] = sh ? 1 : 3;
+        }
+        if (a[j] == 0) s[j] = ((s[j] | 1u) + 1u) & mask;
+        if (a[j] == 1) { out[j] = js[j]; done[j] = true; }
+      }
     }
-    if (act == 2) {
-      unsigned long long old = atomicCAS(reinterpret_cast<unsigned long long *>(dict + 2 * (size_t)js), 0ull,
-                                         (unsigned long long)lo);
-      if (old == 0) {
-        __hip_atomic_store(dict + 2 * (size_t)js + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        result = js;
-        done = true;
-      } else {
-        s = old == lo ? js : ((js + 1) & mask);   // recheck (pending) or move past
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+      if (a[j] == 2) {
+        const unsigned long long old =
+            atomicCAS(reinterpret_cast<unsigned long long *>(dlo + js[j]), 0ull, (unsigned long long)lo[j]);
+        if (old == 0) {
+          __hip_atomic_store(dhi + js[j], hi[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          out[j] = js[j];
+          done[j] = true;
+        } else if (old == lo[j]) {
+          if (key_lo_is_short(lo[j])) { out[j] = js[j]; done[j] = true; }
+          else { s[j] = js[j]; a[j] = 3; }
+        } else {
+          s[j] = (js[j] + 1) & mask;
+        }
       }
     }
     asm volatile("" ::: "memory");
-    if (act == 3 && !done) {
-      const uint64_t chi = __hip_atomic_load(dict + 2 * (size_t)js + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (chi == hi) { result = js; done = true; }
-      else s = chi == 0 ? js : ((js + 1) & mask);
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+      if (a[j] == 3 && !done[j]) {
+        const uint64_t chi = __hip_atomic_load(dhi + js[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (chi == hi[j]) { out[j] = js[j]; done[j] = true; }
+        else s[j] = chi == 0 ? js[j] : ((js[j] + 1) & mask);
+      }
     }
   }
-  return result;
+}
+
+__device__ __forceinline__ uint32_t dict_find_or_insert(uint64_t *dict, uint32_t mask, uint64_t lo, uint64_t hi,
+                                                        bool active) {
+  uint32_t out;
+  dict_lookup_multi<1>(dict, mask, &lo, &hi, &active, &out);
+  return out;
 }
 
 // Per-document table in global memory (long path).  Only the owning
 // workgroup touches it, so workgroup-scope atomics are sufficient.
 __device__ uint32_t gtable_insert(uint64_t *keys, uint32_t *cnt, uint32_t mask, uint64_t lo, uint64_t hi) {
-  uint32_t s = (key_hash(lo, hi) >> 7) & mask;
+  const uint32_t h0 = dict_hash(lo, hi);
+  uint32_t s = (h0 ^ (h0 >> 16)) & mask;
   uint32_t result = kInvalidSlot;
   bool done = false;
   const uint32_t limit = 2 * (mask + 1) + 4096;
@@ -333,16 +364,12 @@ __device__ uint32_t phase_token_spans(const uint64_t *wbits, uint32_t wlen, uint
   return total_all;
 }
 
-// Key of the token at LDS buffer bytes [s, e); *valid = false if the span
-// holds no letter/digit (only '_' can form such a span).  Tokens of <= 18
-// bytes are packed 4 bytes per step: funnel-shift to the token start,
-// blank the tail, SWAR lower-case, 4 x 7-bit pack; longer tokens are hashed.
+// Key of the token at LDS buffer bytes [s, e) (tfidf_common.h format);
+// *valid = false if the span holds no letter/digit (only '_' can form such a
+// span).  Tokens of <= 16 bytes: 4 bytes per step (funnel-shift to the token
+// start, blank the tail, SWAR lower-case); longer tokens go through KeyBuilder.
 __device__ __forceinline__ uint32_t keep_bytes(uint32_t n, uint32_t i) {   // bytes 4i.. of a token of length n
   return n >= 4 * i + 4 ? 0xFFFFFFFFu : (n <= 4 * i ? 0u : (0xFFFFFFFFu >> (8 * (4 * i + 4 - n))));
-}
-__device__ __forceinline__ uint32_t pack7(uint32_t t) {
-  return (t & 0x7Fu) | (__builtin_amdgcn_ubfe(t, 8, 7) << 7) | (__builtin_amdgcn_ubfe(t, 16, 7) << 14) |
-         (__builtin_amdgcn_ubfe(t, 24, 7) << 21);
 }
 __device__ __forceinline__ uint32_t lower4(uint32_t t) {
   const uint32_t up = (t + 0x3F3F3F3Fu) & ~(t + 0x25252525u) & 0x80808080u;   // 'A'..'Z'
@@ -352,7 +379,7 @@ __device__ __forceinline__ uint32_t lower4(uint32_t t) {
 __device__ __forceinline__ void token_key(const uint8_t *text, uint32_t s, uint32_t e, uint64_t *lo, uint64_t *hi,
                                           bool *valid) {
   const uint32_t n = e - s;
-  if (n > kShortKeyChars) {
+  if (n > kExactKeyChars) {
     KeyBuilder kb;
     bool any = false;
     for (uint32_t j = s; j < e; j++) {
@@ -366,87 +393,236 @@ __device__ __forceinline__ void token_key(const uint8_t *text, uint32_t s, uint3
   }
   const uint32_t *tw = reinterpret_cast<const uint32_t *>(text);
   const uint32_t a0 = s >> 2, o = s & 3;
-  const uint32_t d0 = tw[a0], d1 = tw[a0 + 1], d2 = tw[a0 + 2];
-  uint32_t t0 = __builtin_amdgcn_alignbyte(d1, d0, o) & keep_bytes(n, 0);
-  uint32_t t1 = __builtin_amdgcn_alignbyte(d2, d1, o) & keep_bytes(n, 1);
-  uint32_t nu = ((t0 ^ 0x5F5F5F5Fu) & keep_bytes(n, 0)) | ((t1 ^ 0x5F5F5F5Fu) & keep_bytes(n, 1));
-  const uint32_t p0 = pack7(lower4(t0)), p1 = pack7(lower4(t1));
-  uint32_t p2 = 0, p3 = 0, p4 = 0;
-  if (__any(n > 8)) {
-    if (n > 8) {
-      const uint32_t d3 = tw[a0 + 3], d4 = tw[a0 + 4], d5 = tw[a0 + 5];
-      const uint32_t t2 = __builtin_amdgcn_alignbyte(d3, d2, o) & keep_bytes(n, 2);
-      const uint32_t t3 = __builtin_amdgcn_alignbyte(d4, d3, o) & keep_bytes(n, 3);
-      const uint32_t t4 = __builtin_amdgcn_alignbyte(d5, d4, o) & keep_bytes(n, 4);
-      nu |= ((t2 ^ 0x5F5F5F5Fu) & keep_bytes(n, 2)) | ((t3 ^ 0x5F5F5F5Fu) & keep_bytes(n, 3)) |
-            ((t4 ^ 0x5F5F5F5Fu) & keep_bytes(n, 4));
-      p2 = pack7(lower4(t2));
-      p3 = pack7(lower4(t3));
-      p4 = pack7(lower4(t4));
-    }
+  uint32_t d[5];
+#pragma unroll
+  for (int i = 0; i < 5; i++) d[i] = tw[a0 + i];
+  uint32_t l[4], nu = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t k = keep_bytes(n, i);
+    const uint32_t t = __builtin_amdgcn_alignbyte(d[i + 1], d[i], o) & k;
+    nu |= (t ^ 0x5F5F5F5Fu) & k;
+    l[i] = lower4(t);
   }
-  // char j at bit 5 + 7j; group i (4 chars) at bit 5 + 28i; length in bits 0..4
-  *lo = (uint64_t)n | ((uint64_t)p0 << 5) | ((uint64_t)p1 << 33) | ((uint64_t)p2 << 61);
-  *hi = ((uint64_t)p2 >> 3) | ((uint64_t)p3 << 25) | ((uint64_t)p4 << 53) | kKeyValid;
+  *lo = (uint64_t)l[0] | ((uint64_t)l[1] << 32);
+  *hi = kKeyValid;
+  if (n > 8) {
+    *lo |= kLoLong;
+    *hi |= (uint64_t)l[2] | ((uint64_t)l[3] << 32);
+  }
   *valid = nu != 0;
 }
 
 // ---------------------------------------------------------------------------
-// Short-document path.
+// Wave-per-document path.  One wavefront owns one document at a time (its
+// aligned window must fit kWaveWindow = 64 lanes x 64 B, with <= kWaveTokens
+// tokens and <= kWaveTerms distinct terms) and a private LDS arena.  No
+// workgroup barrier anywhere: every phase is wave-synchronous (DS operations
+// of a wave execute in issue order), and the hot loops are branch-free (idle
+// lanes aim their LDS atomics at a per-lane no-op slot instead of masking).
+//
+//   stage     : next document prefetched into registers (4 x 16 B per lane,
+//               coalesced) while the current one is processed; written to LDS
+//               with bytes outside the document zeroed (class Other)
+//   classify  : lane l classifies window bytes [64l, 64l + 64) with SWAR
+//               (4 bytes per op) -> 64-bit word-segment mask W
+//   spans     : token starts S = W & ~(W << 1 | prev), ends E = ~W & (W << 1 |
+//               prev); the k-th start of a lane pairs with its k-th end, a token
+//               running past the lane ends at the next lane's first end
+//               (ballot + one cross-lane read).  Spans are compacted into a
+//               dense LDS list (wave scan of per-lane counts)
+//   histogram : lane l keys tokens l + 64k (k < kWaveK, all in flight) and
+//               counts them in the LDS table with returning 64-bit CASes; after
+//               kWaveFastRounds probe rounds the few unresolved tokens move to
+//               a one-per-lane retry queue
+//   dictionary: occupied table slots are compacted into a dense list; lane l
+//               resolves terms l + 64k to global dictionary slots (all loads in
+//               flight), unresolved ones through a one-per-lane retry queue
+//   CSR row   : grouped by dictionary range (wave scans of packed 16-bit range
+//               counters), staged in LDS, copied out with coalesced stores
+//
+// Table key (64 bit): a token of <= 8 bytes is keyed by its global key lo
+// (tfidf_common.h: lower-cased bytes, zero padded, bit 63 clear).  A longer
+// token is "folded": bit 63 set, bits 0..7 = length, bits 13..25 = start of
+// its first occurrence, bits 26..62 = 37 hash bits of its lower-cased bytes.
+// Two folded keys that agree outside the position field are compared byte by
+// byte (lower-cased) in the window: table identity is exact.
 
-struct ShortSmem {
-  uint64_t t_lo[kShortTable];
-  uint64_t t_hi[kShortTable];
-  uint32_t t_cnt[kShortTable];
-  uint16_t claimed[kShortTable];
-  uint16_t tok_s[kShortMaxTokens];
-  uint16_t tok_e[kShortMaxTokens];
-  uint64_t wbits[kShortMaxBytes / 64 + 2];
-  uint32_t rcnt[64];
-  uint32_t rcur[64];
-  uint32_t scan[8];
-  uint32_t n_uniq, len, flags, pad;
-  uint8_t lut[128];
-  alignas(16) uint8_t text[kShortMaxBytes + 64];
+constexpr uint32_t kWaveWindow = 4096;            // 64 lanes x 64 B
+constexpr uint32_t kWaveSlots = 1024;             // per-document LDS table
+constexpr uint32_t kWaveSlotBits = 10;
+constexpr uint32_t kWaveTokens = 1024;            // token list capacity
+constexpr uint32_t kWaveK = 8;                    // tokens / terms per lane in flight
+constexpr uint32_t kWaveTerms = 64 * kWaveK;      // distinct terms per document (wave path)
+constexpr uint32_t kWaveQueue = 64;               // retry queues: one entry per lane
+constexpr uint32_t kWaveFastRounds = 2;
+constexpr uint64_t kFoldBit = 1ull << 63;
+constexpr uint64_t kFoldPosMask = 0x1FFFull << 13;
+constexpr uint32_t kLookupPending = 0xFFFFFFFEu;
+
+struct WaveSmem {
+  alignas(16) uint8_t text[kWaveWindow + 32];    // +32: key reads run past a token's end
+  alignas(16) uint64_t key[kWaveSlots];          // term table; then lookup queue / results; then CSR staging
+  alignas(16) uint32_t cnt[kWaveSlots / 2];      // u16 counts, two per word
+  alignas(16) uint32_t list[kWaveTokens];        // token spans (start | end << 16); then term slots (u16)
+  alignas(16) uint64_t qkey[kWaveQueue];         // histogram retry queue
+  alignas(16) uint16_t qslot[kWaveQueue];
+  alignas(16) uint64_t noop[64];                 // per-lane no-op atomic target (stays 0)
 };
 
-// Per-document TF histogram in LDS.  One returning ds_cmpst_b64 per probe
-// claims an empty slot (lo 0 -> key lo) or reports the resident lo; equal lo
-// means equal length, and for tokens of <= 8 bytes equal lo is equality (hi
-// is VALID alone), so only longer tokens read hi.  Counting is a
-// non-returning ds_add; the list of used slots is built afterwards.
-__device__ __forceinline__ void lds_table_insert(ShortSmem &sm, uint64_t lo, uint64_t hi, bool active) {
-  uint32_t s = key_hash(lo, hi) >> (32 - 10);           // top 10 bits (kShortTable = 1024)
-  const bool short8 = ((uint32_t)(lo & 31) - 1u) < 8u;   // 1..8 bytes (long keys have 0)
-  bool done = !active;
-  for (uint32_t it = 0; it < kShortTable + 64; it++) {
-    if (__all(done)) return;
-    uint64_t old = 0;
-    if (!done) old = atomicCAS((unsigned long long *)&sm.t_lo[s], 0ull, (unsigned long long)lo);
-    const bool claimed = !done && old == 0;
-    if (claimed) __hip_atomic_store(&sm.t_hi[s], hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    asm volatile("" ::: "memory");
-    bool hit = claimed || (!done && old == lo && short8);
-    if (!done && !hit && old == lo) {                    // same length > 8: compare hi
-      const uint64_t chi = __hip_atomic_load(&sm.t_hi[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (chi == hi) hit = true;
-      // chi == 0: claimed by another wave, hi not yet visible -> retry the same slot
-      if (chi != hi && chi != 0) s = (s + 1) & (kShortTable - 1);
-    } else if (!done && !hit) {
-      s = (s + 1) & (kShortTable - 1);
-    }
-    if (hit) {
-      atomicAdd(&sm.t_cnt[s], 1u);
-      done = true;
-    }
-  }
-  if (!done) atomicOr(&sm.flags, 2u);   // overflow -> long path
+// DPP wave-wide inclusive prefix sum (row shifts, then row broadcasts 15/31).
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t x) {
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);   // row_shr:1
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);   // row_shr:2
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);   // row_shr:4
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);   // row_shr:8
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);   // row_bcast:15
+  x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);   // row_bcast:31
+  return x;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_add(x), 63);
 }
 
-// Next-document prefetch into registers: 2 x 16 B per thread covers 4096 +
-// 15 bytes of misalignment.  Loads go through an explicit global
-// (address_space 1) pointer so they are global_load_dwordx4 and stay in
-// flight (nothing waits on them) until the next document is staged.
+// Word-segment mask of window bytes [64*lane, 64*lane + 64).  Bytes outside
+// the document were zeroed at staging (class Other).  Wave-uniform flags:
+// *bad = a byte >= 0x80 in the document, *under = a '_' in the document.
+__device__ __forceinline__ uint64_t lane_word_mask(const uint8_t *text, uint32_t lane, bool *bad, bool *under) {
+  uint32_t x[16];
+  {
+    const uint4 *t = reinterpret_cast<const uint4 *>(text + lane * 64);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint4 v = t[k];
+      x[4 * k] = v.x; x[4 * k + 1] = v.y; x[4 * k + 2] = v.z; x[4 * k + 3] = v.w;
+    }
+  }
+  // pass 1: letter/digit flags (neighbour context), non-ASCII, joiner presence
+  uint32_t LD[16];
+  uint32_t badacc = 0, P = 0;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const uint32_t D = swar_digit(x[i]);
+    LD[i] = swar_letter(x[i]) | (D >> 1);
+    badacc |= x[i];
+    P |= (x[i] + 0x59595959u) & ~(x[i] + 0x44444444u) & ~D;   // ' ( ) * + , - . / : ; (candidate joiners)
+  }
+  uint32_t ldp = __shfl_up(LD[15], 1, 64);
+  uint32_t ldn = __shfl_down(LD[0], 1, 64);
+  if (lane == 0) ldp = 0;
+  if (lane == 63) ldn = 0;
+  const bool mids = __any((P & 0x80808080u) != 0);
+  // pass 2: word bits
+  uint64_t W = 0;
+  uint32_t us = 0;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    const uint32_t u = swar_eq(x[i], 0x5F5F5F5Fu);
+    us |= u;
+    uint32_t c = LD[i] | (LD[i] << 1) | u;                          // letter | digit | '_' (bit 7)
+    if (mids) {
+      const uint32_t prev4 = i ? LD[i - 1] : ldp;
+      const uint32_t next4 = i < 15 ? LD[i + 1] : ldn;
+      const uint32_t pf = __builtin_amdgcn_alignbyte(LD[i], prev4, 3);   // flags of byte i-1
+      const uint32_t nf = __builtin_amdgcn_alignbyte(next4, LD[i], 1);   // flags of byte i+1
+      const uint32_t both = pf & nf;                                     // bit7 letters, bit6 digits
+      const uint32_t dq = swar_eq(x[i], 0x2E2E2E2Eu) | swar_eq(x[i], 0x27272727u);   // '.' '\''
+      const uint32_t ml = dq | swar_eq(x[i], 0x3A3A3A3Au);                            // ':'
+      const uint32_t mn = dq | swar_eq(x[i], 0x2C2C2C2Cu) | swar_eq(x[i], 0x3B3B3B3Bu);  // ',' ';'
+      c |= (ml & both) | (mn & (both << 1));
+    }
+    W |= (uint64_t)swar_nib(c & 0x80808080u) << (4 * i);
+  }
+  *bad = __any((badacc & 0x80808080u) != 0);
+  *under = __any(us != 0);
+  return W;
+}
+
+// Folded table key of a token of 9..255 bytes at tp (see above); *h slot hash.
+__device__ __noinline__ uint64_t fold_key(const uint8_t *text, uint32_t tp, uint32_t n, uint32_t *h, bool *valid) {
+  const uint32_t *tw = reinterpret_cast<const uint32_t *>(text);
+  const uint32_t a0 = tp >> 2, o = tp & 3;
+  uint32_t h1 = 0x243F6A88u ^ n, h2 = 0x85A308D3u + n, nu = 0;
+  uint32_t prev = tw[a0];
+  for (uint32_t i = 0; 4 * i < n; i++) {
+    const uint32_t nx = tw[a0 + i + 1];
+    const uint32_t k = keep_bytes(n, i);
+    const uint32_t t = __builtin_amdgcn_alignbyte(nx, prev, o) & k;
+    prev = nx;
+    nu |= (t ^ 0x5F5F5F5Fu) & k;
+    const uint32_t l = lower4(t);
+    h1 = (h1 ^ l) * 0x9E3779B1u; h1 = __builtin_rotateleft32(h1, 13);
+    h2 = (h2 ^ l) * 0x85EBCA77u; h2 = __builtin_rotateleft32(h2, 17);
+  }
+  h1 ^= h1 >> 16; h1 *= 0x2C1B3C6Du; h1 ^= h1 >> 13;
+  h2 ^= h2 >> 16; h2 *= 0x297A2D39u; h2 ^= h2 >> 13;
+  *h = h2;
+  *valid = nu != 0;
+  return kFoldBit | (uint64_t)n | ((uint64_t)tp << 13) | ((uint64_t)h1 << 26) | (((uint64_t)(h1 ^ h2) & 31ull) << 58);
+}
+
+// Lower-cased byte equality of the n-byte spans at p1 and p2.
+__device__ __noinline__ bool span_same(const uint8_t *text, uint32_t p1, uint32_t p2, uint32_t n) {
+  const uint32_t *tw = reinterpret_cast<const uint32_t *>(text);
+  const uint32_t a1 = p1 >> 2, o1 = p1 & 3, a2 = p2 >> 2, o2 = p2 & 3;
+  for (uint32_t i = 0; 4 * i < n; i++) {
+    const uint32_t x = __builtin_amdgcn_alignbyte(tw[a1 + i + 1], tw[a1 + i], o1);
+    const uint32_t y = __builtin_amdgcn_alignbyte(tw[a2 + i + 1], tw[a2 + i], o2);
+    if ((lower4(x) ^ lower4(y)) & keep_bytes(n, i)) return false;
+  }
+  return true;
+}
+
+// Does a CAS that returned `old` resolve the token keyed `tk`?  (claimed the
+// empty slot, or found the same term)
+__device__ __forceinline__ bool table_hit(const uint8_t *text, uint64_t old, uint64_t tk) {
+  if (old == 0 || old == tk) return true;
+  if ((tk & old & kFoldBit) && ((old ^ tk) & ~kFoldPosMask) == 0)
+    return span_same(text, (uint32_t)(old >> 13) & 0x1FFFu, (uint32_t)(tk >> 13) & 0x1FFFu, (uint32_t)tk & 0xFFu);
+  return false;
+}
+
+// One bucket probe of a short key (dictionary lo array, 2-slot bucket at s & ~1,
+// slots >= s considered).  Returns the found slot, or kLookupPending with
+// *claim = slot to claim (empty) or kInvalidSlot (advance to the next bucket).
+__device__ __forceinline__ uint32_t bucket_probe(ulonglong2 e, uint32_t s, uint64_t lo, uint32_t *claim) {
+  const bool odd = (s & 1u) != 0;
+  const uint64_t v0 = odd ? e.y : e.x;
+  const bool f0 = v0 == lo, z0 = v0 == 0;
+  const bool f1 = !odd && e.y == lo, z1 = !odd && e.y == 0;
+  const bool hit = f0 || (!z0 && f1);
+  const bool cl = z0 || (!f0 && !f1 && z1);
+  *claim = cl ? (z0 ? s : s + 1) : kInvalidSlot;
+  return hit ? (f0 ? s : s + 1) : kLookupPending;
+}
+
+// Claim slot cs for short key lo (CAS on lo, then publish hi).  Returns the
+// slot if it now holds lo, else kLookupPending with *s advanced past cs.
+__device__ __forceinline__ uint32_t dict_claim_short(uint64_t *dict, uint32_t mask, uint32_t cs, uint64_t lo,
+                                                     uint32_t *s) {
+  const unsigned long long old = atomicCAS(reinterpret_cast<unsigned long long *>(dict + cs), 0ull,
+                                           (unsigned long long)lo);
+  if (old == 0) __hip_atomic_store(dict + (size_t)mask + 1 + cs, kKeyValid, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+  if (old == 0 || old == lo) return cs;
+  *s = (cs + 1) & mask;
+  return kLookupPending;
+}
+
+// 16-bit field f of a packed 8-field value (two fields per word)
+__device__ __forceinline__ uint32_t field8(const uint32_t *w, uint32_t f) {
+  const uint32_t h = f >> 1;
+  const uint32_t v = h == 0 ? w[0] : (h == 1 ? w[1] : (h == 2 ? w[2] : w[3]));
+  return (v >> (16 * (f & 1))) & 0xFFFFu;
+}
+__device__ __forceinline__ void field8_add(uint32_t *w, uint32_t f, uint32_t inc16) {
+  const uint32_t h = f >> 1, inc = inc16 << (16 * (f & 1));
+  w[0] += h == 0 ? inc : 0u;
+  w[1] += h == 1 ? inc : 0u;
+  w[2] += h == 2 ? inc : 0u;
+  w[3] += h == 3 ? inc : 0u;
+}
+
 __device__ __forceinline__ uint4 gload16(const void *ptr) {
 #if defined(__HIP_DEVICE_COMPILE__)
   typedef __attribute__((address_space(1))) const uint32_t gu32;
@@ -471,159 +647,467 @@ __device__ __forceinline__ DocMeta doc_meta(const BuildParams &p, uint64_t d) {
   return m;
 }
 
-__device__ __forceinline__ void prefetch_text(const BuildParams &p, const DocMeta &m, uint4 &v0, uint4 &v1) {
-  if (m.L > kShortMaxBytes) return;
+__device__ __forceinline__ bool fits_wave(const DocMeta &m) { return m.shift + m.L <= kWaveWindow; }
+
+__device__ __forceinline__ void prefetch_wave(const BuildParams &p, const DocMeta &m, uint32_t lane, uint4 *v) {
+  if (!fits_wave(m)) return;
   const uint32_t nchunks = (uint32_t)((m.shift + m.L + 15) >> 4);
   const uint4 *src = reinterpret_cast<const uint4 *>(reinterpret_cast<uintptr_t>(p.text + m.s0) & ~(uintptr_t)15);
-  if (threadIdx.x < nchunks) v0 = gload16(src + threadIdx.x);
-  if (threadIdx.x + 256 < nchunks) v1 = gload16(src + threadIdx.x + 256);
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    if (lane + 64 * k < nchunks) v[k] = gload16(src + lane + 64 * k);
 }
 
-__global__ void __launch_bounds__(256) k_tokenize_short(BuildParams p) {
-  __shared__ ShortSmem sm;
-  const uint32_t tid = threadIdx.x;
-  for (uint32_t i = tid; i < 128; i += 256) sm.lut[i] = wb_class(i);
-  for (uint32_t i = tid; i < kShortTable; i += 256) { sm.t_lo[i] = 0; sm.t_hi[i] = 0; sm.t_cnt[i] = 0; }
-  if (tid < 64) { sm.rcnt[tid] = 0; sm.rcur[tid] = 0; }
-  if (tid == 0) { sm.n_uniq = 0; sm.len = 0; sm.flags = 0; }
+// bytes of the dword at window byte q that lie in [lo, hi)
+__device__ __forceinline__ uint32_t keep_range(uint32_t q, uint32_t lo, uint32_t hi) {
+  const uint32_t a = q >= lo ? 0xFFFFFFFFu : (lo - q >= 4 ? 0u : (0xFFFFFFFFu << (8 * (lo - q))));
+  const uint32_t b = q + 4 <= hi ? 0xFFFFFFFFu : (hi <= q ? 0u : (0xFFFFFFFFu >> (8 * (q + 4 - hi))));
+  return a & b;
+}
+
+__device__ __forceinline__ void clear_table(WaveSmem &sm, uint32_t lane) {
+  uint4 *kw = reinterpret_cast<uint4 *>(sm.key);
+  uint4 *cw = reinterpret_cast<uint4 *>(sm.cnt);
+#pragma unroll
+  for (int q = 0; q < (int)(kWaveSlots * 8 / 16 / 64); q++) kw[lane + 64 * q] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+  for (int q = 0; q < (int)(kWaveSlots * 2 / 16 / 64); q++) cw[lane + 64 * q] = make_uint4(0, 0, 0, 0);
+}
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_tokenize_wave(BuildParams p) {
+  __shared__ WaveSmem sm;
+  const uint32_t lane = threadIdx.x;
+  clear_table(sm, lane);           // table starts empty; every document leaves it empty
+  sm.noop[lane] = 0;
   unsigned long long my_doc_count = 0, my_ttf = 0, my_nnz = 0;
-  uint4 v0 = make_uint4(0, 0, 0, 0), v1 = make_uint4(0, 0, 0, 0);
+  uint4 v[4] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
   DocMeta meta;
   if (blockIdx.x < p.n_docs) {
     meta = doc_meta(p, blockIdx.x);
-    prefetch_text(p, meta, v0, v1);
+    prefetch_wave(p, meta, lane, v);
   }
-  lds_barrier();
+  const uint32_t R = p.n_ranges;
+  const uint32_t dmask = p.cap_mask;
+  uint16_t *slots = reinterpret_cast<uint16_t *>(sm.list);
+  unsigned long long *noop = reinterpret_cast<unsigned long long *>(&sm.noop[lane]);
+  const uint32_t *tw = reinterpret_cast<const uint32_t *>(sm.text);
 
   for (uint64_t d = blockIdx.x; d < p.n_docs; d += gridDim.x) {
     const uint64_t src = meta.src, L = meta.L;
     const uint32_t shift = meta.shift;
+    const bool fits = fits_wave(meta);
     const uint64_t dn = d + gridDim.x;
-    if (L > kShortMaxBytes) {
-      if (tid == 0) p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
-      if (dn < p.n_docs) { meta = doc_meta(p, dn); prefetch_text(p, meta, v0, v1); }
-      continue;                                           // block-uniform
+    if (!fits) {
+      if (lane == 0) p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
+      if (dn < p.n_docs) { meta = doc_meta(p, dn); prefetch_wave(p, meta, lane, v); }
+      continue;                                             // wave-uniform
     }
-    // stage from registers, then start fetching the next document
-    uint4 *dst = reinterpret_cast<uint4 *>(sm.text);
-    const uint32_t nchunks = (uint32_t)((shift + L + 15) >> 4);
-    if (tid < nchunks) dst[tid] = v0;
-    if (tid + 256 < nchunks) dst[tid + 256] = v1;
-    if (dn < p.n_docs) { meta = doc_meta(p, dn); prefetch_text(p, meta, v0, v1); }
-    lds_barrier();
+    // ---- stage: registers -> LDS (whole window; bytes outside the document
+    // zeroed), then fetch the next document
+    {
+      const uint32_t hi_b = shift + (uint32_t)L;
+      const uint32_t nchunks = (hi_b + 15) >> 4;
+      uint4 *dst = reinterpret_cast<uint4 *>(sm.text);
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t c = lane + 64 * k;
+        uint4 val = c < nchunks ? v[k] : make_uint4(0, 0, 0, 0);
+        if (c == 0 || c == nchunks - 1) {
+          val.x &= keep_range(16 * c, shift, hi_b);
+          val.y &= keep_range(16 * c + 4, shift, hi_b);
+          val.z &= keep_range(16 * c + 8, shift, hi_b);
+          val.w &= keep_range(16 * c + 12, shift, hi_b);
+        }
+        dst[c] = val;
+      }
+    }
+    if (dn < p.n_docs) { meta = doc_meta(p, dn); prefetch_wave(p, meta, lane, v); }
+    asm volatile("" ::: "memory");
     if (p.debug_stop == 1) continue;
-    const uint32_t lo_b = shift, hi_b = shift + (uint32_t)L;     // document bytes in buffer coordinates
-    const bool nonascii = phase_wordbits(sm.text, lo_b, hi_b, sm.wbits, &sm.flags);
-    if (nonascii) {
-      if (tid == 0) {
+
+    // ---- classify + spans -> dense token list
+    bool bad, under;
+    const uint64_t W = lane_word_mask(sm.text, lane, &bad, &under);
+    if (bad) {
+      if (lane == 0) {
         set_err(p.err, kErrNonAscii, (uint32_t)d);
         p.doc_len[d] = 0; p.doc_nuniq[d] = 0; p.doc_norm[d] = 0;
-        for (uint32_t r = 0; r < p.n_ranges; r++) p.rsplit[d * p.n_ranges + r] = 0;
-        sm.flags = 0;
       }
-      lds_barrier();
+      for (uint32_t r = lane; r < R; r += 64) p.rsplit[d * R + r] = 0;
       continue;
     }
+    const uint64_t wlast = __ballot((W >> 63) & 1ull);
+    const uint64_t prevW = lane ? (wlast >> (lane - 1)) & 1ull : 0ull;
+    uint64_t S = W & ~((W << 1) | prevW);
+    uint64_t E = ~W & ((W << 1) | prevW);
+    const uint32_t firstE = E ? lane * 64 + (uint32_t)__builtin_ctzll(E) : kWaveWindow;
+    const uint64_t hasE = __ballot(E != 0);
+    const uint64_t later = lane == 63 ? 0ull : (hasE & (~0ull << (lane + 1)));
+    const uint32_t srcl = later ? (uint32_t)__builtin_ctzll(later) : lane;
+    uint32_t nz = (uint32_t)__shfl((int)firstE, (int)srcl, 64);
+    if (!later) nz = kWaveWindow;
+    if (prevW) E &= E - 1;                                  // closes the token open from lane - 1
+    const uint32_t nts = (uint32_t)__popcll(S);
+    const uint32_t tincl = wave_incl_add(nts);
+    const uint32_t ntok = (uint32_t)__builtin_amdgcn_readlane((int)tincl, 63);
+    if (ntok > kWaveTokens) {                               // wave-uniform
+      if (lane == 0) p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
+      continue;
+    }
+    {
+      uint32_t at = tincl - nts;
+      uint32_t s0 = (uint32_t)S, s1 = (uint32_t)(S >> 32), e0 = (uint32_t)E, e1 = (uint32_t)(E >> 32);
+      while (s0 | s1) {
+        const uint32_t tp = lane * 64 + (s0 ? (uint32_t)__builtin_ctz(s0) : 32 + (uint32_t)__builtin_ctz(s1));
+        const uint32_t te = (e0 | e1) ? lane * 64 + (e0 ? (uint32_t)__builtin_ctz(e0) : 32 + (uint32_t)__builtin_ctz(e1))
+                                      : nz;
+        if (s0) s0 &= s0 - 1; else s1 &= s1 - 1;
+        if (e0) e0 &= e0 - 1; else e1 &= e1 - 1;
+        sm.list[at++] = tp | (te << 16);
+      }
+    }
+    asm volatile("" ::: "memory");
     if (p.debug_stop == 2) continue;
-    const uint32_t ntok = phase_token_spans(sm.wbits, hi_b, lo_b, hi_b, sm.tok_s, sm.tok_e, kShortMaxTokens,
-                                            sm.scan);
-    if (p.debug_stop == 3) continue;
-    if (ntok > kShortMaxTokens) {
-      if (tid == 0) p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
-      lds_barrier();
-      continue;
-    }
-    // Phase C: tokens -> per-document histogram in LDS
-    uint32_t my_len = 0;
-    for (uint32_t i0 = 0; i0 < ntok; i0 += 256) {
-      const uint32_t i = i0 + tid;
-      uint64_t lo = 0, hi = 0;
-      bool valid = false;
-      if (i < ntok) {
-        const uint32_t s = sm.tok_s[i], e = sm.tok_e[i];
-        if (e - s > kMaxTokenLen) {
-          set_err(p.err, kErrTokenTooLong, (uint32_t)d);
-        } else {
-          token_key(sm.text, s, e, &lo, &hi, &valid);
+
+    // ---- per-document histogram in LDS
+    uint32_t claims = 0, toks = 0;
+    bool overflow = false;
+    for (uint32_t tb = 0; tb < ntok && !overflow; tb += 64 * kWaveK) {
+      const uint32_t kmax = min(kWaveK, (ntok - tb + 63) >> 6);   // wave-uniform
+      uint64_t tkey[kWaveK];
+      uint32_t slot[kWaveK];
+      uint32_t pendm = 0, longm = 0;
+#pragma unroll
+      for (int k = 0; k < (int)kWaveK; k++) {          // keys of <= 8 bytes, branch-free
+        tkey[k] = 0;
+        slot[k] = 0;
+        if ((uint32_t)k < kmax) {
+          const uint32_t idx = tb + lane + 64 * k;
+          const bool in = idx < ntok;
+          const uint32_t e = sm.list[in ? idx : 0u];
+          const uint32_t tp = e & 0xFFFFu, n = (e >> 16) - tp;
+          const uint32_t a0 = tp >> 2, o = tp & 3;
+          const uint32_t d0 = tw[a0], d1 = tw[a0 + 1], d2 = tw[a0 + 2];
+          const uint64_t m64 = n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1);
+          const uint32_t t0 = __builtin_amdgcn_alignbyte(d1, d0, o) & (uint32_t)m64;
+          const uint32_t t1 = __builtin_amdgcn_alignbyte(d2, d1, o) & (uint32_t)(m64 >> 32);
+          bool valid = true;
+          if (under) valid = (((t0 ^ 0x5F5F5F5Fu) & (uint32_t)m64) | ((t1 ^ 0x5F5F5F5Fu) & (uint32_t)(m64 >> 32))) != 0;
+          const uint32_t l0 = lower4(t0), l1 = lower4(t1);
+          tkey[k] = (uint64_t)l0 | ((uint64_t)l1 << 32);
+          slot[k] = ((l0 ^ rotl32(l1, 16)) * 0x85EBCA77u) >> (32 - kWaveSlotBits);
+          pendm |= (uint32_t)(in && n <= 8 && valid) << k;
+          longm |= (uint32_t)(in && n > 8) << k;
         }
       }
-      my_len += valid;
-      lds_table_insert(sm, lo, hi, valid);
-    }
-    atomicAdd(&sm.len, my_len);
-    lds_barrier();
-    {   // list of used slots: each thread owns 4 consecutive slots
-      uint32_t used = 0;
+      const bool hasfold = __any(longm != 0);
+      if (hasfold) {                                    // tokens of 9..255 bytes: folded keys
 #pragma unroll
-      for (int q = 0; q < 4; q++) used |= (sm.t_lo[tid * 4 + q] != 0) << q;
-      uint32_t total;
-      uint32_t at = block_excl_scan_256(__popc(used), sm.scan, &total);
+        for (int k = 0; k < (int)kWaveK; k++) {
+          if ((longm >> k) & 1u) {
+            const uint32_t e = sm.list[tb + lane + 64 * k];
+            const uint32_t tp = e & 0xFFFFu, n = (e >> 16) - tp;
+            if (n > kMaxTokenLen) {
+              set_err(p.err, kErrTokenTooLong, (uint32_t)d);
+            } else {
+              uint32_t h;
+              bool valid;
+              tkey[k] = fold_key(sm.text, tp, n, &h, &valid);
+              slot[k] = h >> (32 - kWaveSlotBits);
+              pendm |= (uint32_t)valid << k;
+            }
+          }
+        }
+      }
+      toks += (uint32_t)__popc(pendm);
+      for (uint32_t round = 0;; round++) {
+        const uint32_t np = (uint32_t)__popc(pendm);
+        const uint32_t pincl = wave_incl_add(np);
+        const uint32_t P = (uint32_t)__builtin_amdgcn_readlane((int)pincl, 63);
+        if (P == 0) break;
+        if (round >= kWaveSlots) { overflow = true; break; }
+        if (round >= kWaveFastRounds && P <= kWaveQueue) {
+          // retry queue: one unresolved token per lane, probed until resolved
+          uint32_t at = pincl - np;
 #pragma unroll
-      for (int q = 0; q < 4; q++)
-        if (used & (1u << q)) sm.claimed[at++] = (uint16_t)(tid * 4 + q);
-      if (tid == 0) sm.n_uniq = total;
-      lds_barrier();
-    }
-    const uint32_t nu = sm.n_uniq;
-    if (p.debug_stop == 4) {
-      for (uint32_t i = tid; i < nu; i += 256) {
-        const uint32_t s = sm.claimed[i];
-        sm.t_lo[s] = 0; sm.t_hi[s] = 0; sm.t_cnt[s] = 0;
+          for (int k = 0; k < (int)kWaveK; k++)
+            if ((pendm >> k) & 1u) { sm.qkey[at] = tkey[k]; sm.qslot[at] = (uint16_t)slot[k]; at++; }
+          asm volatile("" ::: "memory");
+          bool qp = lane < P;
+          uint64_t qk = 0;
+          uint32_t qs = 0;
+          if (qp) { qk = sm.qkey[lane]; qs = sm.qslot[lane]; }
+          for (uint32_t it = 0; __any(qp); it++) {
+            if (it >= kWaveSlots) { overflow = true; break; }
+            if (qp) {
+              const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long *>(&sm.key[qs]), 0ull,
+                                             (unsigned long long)qk);
+              if (table_hit(sm.text, old, qk)) {
+                atomicAdd(&sm.cnt[qs >> 1], 1u << (16 * (qs & 1)));
+                claims += old == 0;
+                qp = false;
+              } else {
+                qs = (qs + 1) & (kWaveSlots - 1);
+              }
+            }
+          }
+          break;
+        }
+        // one probe round for every pending token (no-op CAS for the others)
+        uint64_t old[kWaveK];
+#pragma unroll
+        for (int k = 0; k < (int)kWaveK; k++) {
+          old[k] = 0;
+          if ((uint32_t)k < kmax) {
+            const bool pend = (pendm >> k) & 1u;
+            old[k] = atomicCAS(pend ? reinterpret_cast<unsigned long long *>(&sm.key[slot[k]]) : noop,
+                               pend ? 0ull : ~0ull, (unsigned long long)tkey[k]);
+          }
+        }
+        uint32_t foldm = 0;
+#pragma unroll
+        for (int k = 0; k < (int)kWaveK; k++) {
+          if ((uint32_t)k < kmax) {
+            const bool pend = (pendm >> k) & 1u;
+            const bool hit = pend && (old[k] == 0 || old[k] == tkey[k]);
+            atomicAdd(hit ? &sm.cnt[slot[k] >> 1] : reinterpret_cast<uint32_t *>(noop),
+                      hit ? 1u << (16 * (slot[k] & 1)) : 0u);
+            claims += hit && old[k] == 0;
+            pendm &= ~((uint32_t)hit << k);
+            bool fc = false;
+            if (hasfold)
+              fc = pend && !hit && ((old[k] & tkey[k]) >> 63) && ((old[k] ^ tkey[k]) & ~kFoldPosMask) == 0;
+            foldm |= (uint32_t)fc << k;
+            if (pend && !hit && !fc) slot[k] = (slot[k] + 1) & (kWaveSlots - 1);
+          }
+        }
+        if (hasfold && __any(foldm != 0)) {              // same length and hash: compare bytes
+#pragma unroll
+          for (int k = 0; k < (int)kWaveK; k++) {
+            if ((foldm >> k) & 1u) {
+              if (span_same(sm.text, (uint32_t)(old[k] >> 13) & 0x1FFFu, (uint32_t)(tkey[k] >> 13) & 0x1FFFu,
+                            (uint32_t)tkey[k] & 0xFFu)) {
+                atomicAdd(&sm.cnt[slot[k] >> 1], 1u << (16 * (slot[k] & 1)));
+                pendm &= ~(1u << k);
+              } else {
+                slot[k] = (slot[k] + 1) & (kWaveSlots - 1);
+              }
+            }
+          }
+        }
       }
-      lds_barrier();
-      if (tid == 0) { sm.n_uniq = 0; sm.len = 0; sm.flags = 0; }
-      lds_barrier();
+    }
+    const uint32_t len = wave_sum(toks), nu = wave_sum(claims);
+    if (overflow || nu > kWaveTerms) {                      // wave-uniform: long path
+      clear_table(sm, lane);
+      if (lane == 0) p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
       continue;
     }
-    if (sm.flags & 2u) {                                  // LDS table overflow
-      for (uint32_t i = tid; i < nu; i += 256) {
-        const uint32_t s = sm.claimed[i];
-        sm.t_lo[s] = 0; sm.t_hi[s] = 0; sm.t_cnt[s] = 0;
+    if (p.debug_stop == 3) { clear_table(sm, lane); continue; }
+
+    // ---- dense list of occupied table slots (this lane scans 16)
+    {
+      uint32_t occ = 0;
+      const uint4 *kp = reinterpret_cast<const uint4 *>(&sm.key[16 * lane]);
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        const uint4 t = kp[q];
+        occ |= (uint32_t)((t.x | t.y) != 0) << (2 * q);
+        occ |= (uint32_t)((t.z | t.w) != 0) << (2 * q + 1);
       }
-      lds_barrier();
-      if (tid == 0) {
-        p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
-        sm.n_uniq = 0; sm.len = 0; sm.flags = 0;
+      const uint32_t c = (uint32_t)__popc(occ);
+      uint32_t at = wave_incl_add(c) - c;
+      while (occ) {
+        slots[at++] = (uint16_t)(16 * lane + (uint32_t)__builtin_ctz(occ));
+        occ &= occ - 1;
       }
-      lds_barrier();
-      continue;
+      asm volatile("" ::: "memory");
     }
-    // Phase D: dictionary slots (all lookups of a thread issued together),
-    // range partition, CSR row
-    const uint64_t base = csr_row_base(p.offsets, src);
-    for (uint32_t i0 = 0; i0 < nu; i0 += 256) {
-      const uint32_t i = i0 + tid;
-      const bool act = i < nu;
-      const uint32_t s = act ? sm.claimed[i] : 0;
-      uint32_t g = dict_find_or_insert(p.dict, p.cap_mask, act ? sm.t_lo[s] : 1, act ? sm.t_hi[s] : kKeyValid, act);
-      if (act) {
-        if (g == kInvalidSlot) { set_err(p.err, kErrCapacity, (uint32_t)d); g = 0; }
-        atomicAdd(&sm.rcnt[g >> p.range_shift], 1u);
-        sm.t_lo[s] = g;
+
+    // ---- dictionary slots of terms lane + 64k
+    const uint32_t tmax = (nu + 63) >> 6;                   // wave-uniform, <= kWaveK
+    uint32_t g[kWaveK], tf[kWaveK];
+    uint32_t actm = 0;
+    {
+      uint64_t lo[kWaveK];
+      uint32_t ps[kWaveK];
+      uint32_t foldm = 0;
+#pragma unroll
+      for (int k = 0; k < (int)kWaveK; k++) {
+        lo[k] = 0;
+        tf[k] = 0;
+        g[k] = kInvalidSlot;
+        ps[k] = 0;
+        if ((uint32_t)k < tmax) {
+          const uint32_t idx = lane + 64 * k;
+          const bool in = idx < nu;
+          const uint32_t s = slots[in ? idx : 0u] & (kWaveSlots - 1);
+          const uint64_t key = sm.key[s];
+          tf[k] = (sm.cnt[s >> 1] >> (16 * (s & 1))) & 0xFFFFu;
+          const bool f = in && (key & kFoldBit);
+          lo[k] = (in && !f) ? key : 0ull;
+          foldm |= (uint32_t)f << k;
+          actm |= (uint32_t)in << k;
+          ps[k] = dict_home(dict_hash_short(lo[k]), dmask) & ~1u;
+          if (in && !f) g[k] = kLookupPending;
+        }
+      }
+      // folded (> 8 byte) terms: exact 128-bit keys, one lookup per lane at a time
+      while (__any(foldm != 0)) {
+        uint64_t flo = 1, fhi = kKeyValid;
+        uint32_t k = 0;
+        const bool fa = foldm != 0;
+        if (fa) {
+          k = (uint32_t)__builtin_ctz(foldm);
+          foldm &= foldm - 1;
+          const uint64_t key = sm.key[slots[lane + 64 * k]];
+          const uint32_t n = (uint32_t)key & 0xFFu, tp = (uint32_t)(key >> 13) & 0x1FFFu;
+          bool valid;
+          token_key(sm.text, tp, tp + n, &flo, &fhi, &valid);
+        }
+        const uint32_t gg = dict_find_or_insert(p.dict, dmask, flo, fhi, fa);
+#pragma unroll
+        for (int kk = 0; kk < (int)kWaveK; kk++)
+          if (fa && (uint32_t)kk == k) g[kk] = gg;
+      }
+      // short terms: bucket probes, all of a lane's loads in flight per round
+      for (uint32_t round = 0;; round++) {
+        uint32_t np = 0;
+#pragma unroll
+        for (int k = 0; k < (int)kWaveK; k++) np += g[k] == kLookupPending;
+        const uint32_t pincl = wave_incl_add(np);
+        const uint32_t P = (uint32_t)__builtin_amdgcn_readlane((int)pincl, 63);
+        if (P == 0) break;
+        if (round > 0 && P <= kWaveQueue) {
+          // retry queue in the (no longer needed) table: (lo, probe slot, term index)
+          uint64_t *qlo = sm.key;
+          uint2 *qmeta = reinterpret_cast<uint2 *>(sm.key + kWaveQueue);
+          uint32_t *res = reinterpret_cast<uint32_t *>(sm.key + 2 * kWaveQueue);
+          uint32_t at = pincl - np;
+#pragma unroll
+          for (int k = 0; k < (int)kWaveK; k++)
+            if (g[k] == kLookupPending) { qlo[at] = lo[k]; qmeta[at] = make_uint2(ps[k], lane + 64 * k); at++; }
+          asm volatile("" ::: "memory");
+          const bool qa = lane < P;
+          uint64_t ql = 0;
+          uint2 qm = make_uint2(0, 0);
+          if (qa) { ql = qlo[lane]; qm = qmeta[lane]; }
+          uint32_t qs = qm.x, qg = qa ? kLookupPending : kInvalidSlot;
+          for (uint32_t it = 0; it < dmask + 4096 && __any(qg == kLookupPending); it++) {
+            if (qg == kLookupPending) {
+              const ulonglong2 e = *reinterpret_cast<const ulonglong2 *>(p.dict + (qs & ~1u));
+              uint32_t cs;
+              qg = bucket_probe(e, qs, ql, &cs);
+              if (qg == kLookupPending) {
+                if (cs != kInvalidSlot) qg = dict_claim_short(p.dict, dmask, cs, ql, &qs);
+                else qs = ((qs | 1u) + 1u) & dmask;
+              }
+            }
+          }
+          if (qa) res[qm.y] = qg == kLookupPending ? kInvalidSlot : qg;
+          asm volatile("" ::: "memory");
+#pragma unroll
+          for (int k = 0; k < (int)kWaveK; k++)
+            if (g[k] == kLookupPending) g[k] = res[lane + 64 * k];
+          break;
+        }
+        if (round > dmask) break;                          // table exhausted: capacity error below
+        ulonglong2 e[kWaveK];
+#pragma unroll
+        for (int k = 0; k < (int)kWaveK; k++) {
+          e[k] = make_ulonglong2(0, 0);
+          if ((uint32_t)k < tmax)
+            e[k] = *reinterpret_cast<const ulonglong2 *>(p.dict + (g[k] == kLookupPending ? (ps[k] & ~1u) : 0u));
+        }
+        uint32_t cs[kWaveK];
+        bool anyclaim = false;
+#pragma unroll
+        for (int k = 0; k < (int)kWaveK; k++) {
+          cs[k] = kInvalidSlot;
+          if ((uint32_t)k < tmax) {
+            const bool pend = g[k] == kLookupPending;
+            uint32_t c;
+            const uint32_t r = bucket_probe(e[k], ps[k], lo[k], &c);
+            if (pend) {
+              g[k] = r;
+              cs[k] = c;
+              anyclaim |= c != kInvalidSlot;
+              if (r == kLookupPending && c == kInvalidSlot) ps[k] = ((ps[k] | 1u) + 1u) & dmask;
+            }
+          }
+        }
+        if (__any(anyclaim)) {
+#pragma unroll
+          for (int k = 0; k < (int)kWaveK; k++)
+            if (cs[k] != kInvalidSlot) g[k] = dict_claim_short(p.dict, dmask, cs[k], lo[k], &ps[k]);
+        }
+      }
+      bool caperr = false;
+#pragma unroll
+      for (int k = 0; k < (int)kWaveK; k++) {
+        const bool e = ((actm >> k) & 1u) && (g[k] == kInvalidSlot || g[k] == kLookupPending);
+        caperr |= e;
+        if (e) g[k] = 0;
+      }
+      if (caperr) set_err(p.err, kErrCapacity, (uint32_t)d);
+    }
+    if (p.debug_stop == 4) { clear_table(sm, lane); continue; }
+
+    // ---- CSR row grouped by dictionary range (8 ranges per pass), staged in LDS
+    uint32_t *st_col = reinterpret_cast<uint32_t *>(sm.key);
+    uint32_t *st_tf = st_col + kWaveSlots;
+    const uint32_t st_noop = kWaveSlots - 64 + lane;          // unused staging words (nu <= kWaveTerms)
+    uint32_t run = 0;
+    for (uint32_t rb = 0; rb < R; rb += 8) {
+      uint32_t c[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int k = 0; k < (int)kWaveK; k++) {
+        if ((uint32_t)k < tmax) {
+          const uint32_t f = (g[k] >> p.range_shift) - rb;
+          field8_add(c, f, (((actm >> k) & 1u) && f < 8) ? 1u : 0u);
+        }
+      }
+      uint32_t pk[4], tot[4];
+#pragma unroll
+      for (int w = 0; w < 4; w++) {
+        const uint32_t incl = wave_incl_add(c[w]);
+        pk[w] = incl - c[w];
+        tot[w] = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      }
+      // exclusive scan of the 8 totals (wave-uniform), packed the same way
+      uint32_t fb[4] = {0, 0, 0, 0}, acc = 0;
+#pragma unroll
+      for (int f = 0; f < 8; f++) {
+        fb[f >> 1] |= acc << (16 * (f & 1));
+        acc += (tot[f >> 1] >> (16 * (f & 1))) & 0xFFFFu;
+      }
+      if (lane < 8 && rb + lane < R)
+        p.rsplit[d * R + rb + lane] = run + field8(fb, lane) + field8(tot, lane);
+#pragma unroll
+      for (int w = 0; w < 4; w++) pk[w] += fb[w];
+#pragma unroll
+      for (int k = 0; k < (int)kWaveK; k++) {
+        if ((uint32_t)k < tmax) {
+          const uint32_t f = (g[k] >> p.range_shift) - rb;
+          const bool inr = ((actm >> k) & 1u) && f < 8;
+          const uint32_t pos = inr ? run + field8(pk, f) : st_noop;
+          field8_add(pk, f, inr ? 1u : 0u);
+          st_col[pos] = g[k];
+          st_tf[pos] = tf[k];
+        }
+      }
+      run += acc;
+    }
+    asm volatile("" ::: "memory");
+    {
+      const uint64_t row = csr_row_base(p.offsets, src);
+      for (uint32_t i = lane; i < nu; i += 64) {
+        p.csr_col[row + i] = st_col[i];
+        p.csr_tf[row + i] = st_tf[i];
       }
     }
-    lds_barrier();
-    if (p.debug_stop == 5) {
-      for (uint32_t i = tid; i < nu; i += 256) {
-        const uint32_t s = sm.claimed[i];
-        sm.t_lo[s] = 0; sm.t_hi[s] = 0; sm.t_cnt[s] = 0;
-      }
-      if (tid < 64) sm.rcnt[tid] = 0;
-      lds_barrier();
-      if (tid == 0) { sm.n_uniq = 0; sm.len = 0; sm.flags = 0; }
-      lds_barrier();
-      continue;
-    }
-    if (tid == 0) {
-      uint32_t run = 0;
-      for (uint32_t r = 0; r < p.n_ranges; r++) {
-        const uint32_t c = sm.rcnt[r];
-        sm.rcur[r] = run;
-        run += c;
-        p.rsplit[d * p.n_ranges + r] = run;
-        sm.rcnt[r] = 0;
-      }
-      const uint32_t len = sm.len;
+    clear_table(sm, lane);
+    if (lane == 0) {
       p.doc_len[d] = len;
       p.doc_nuniq[d] = nu;
       p.doc_norm[d] = (uint8_t)int_to_byte4(len);
@@ -631,20 +1115,8 @@ __global__ void __launch_bounds__(256) k_tokenize_short(BuildParams p) {
       my_ttf += len;
       my_nnz += nu;
     }
-    lds_barrier();
-    for (uint32_t i = tid; i < nu; i += 256) {
-      const uint32_t s = sm.claimed[i];
-      const uint32_t g = (uint32_t)sm.t_lo[s];
-      const uint32_t pos = atomicAdd(&sm.rcur[g >> p.range_shift], 1u);
-      p.csr_col[base + pos] = g;
-      p.csr_tf[base + pos] = sm.t_cnt[s];
-      sm.t_lo[s] = 0; sm.t_hi[s] = 0; sm.t_cnt[s] = 0;
-    }
-    lds_barrier();
-    if (tid == 0) { sm.n_uniq = 0; sm.len = 0; sm.flags = 0; }
-    lds_barrier();
   }
-  if (tid == 0) {
+  if (lane == 0) {
     atomicAdd(&p.stats[0], my_doc_count);
     atomicAdd(&p.stats[1], my_ttf);
     atomicAdd(&p.stats[2], my_nnz);
@@ -923,8 +1395,8 @@ __global__ void __launch_bounds__(1024) k_scatter(PostingParams p) {
 // ---------------------------------------------------------------------------
 // launchers
 
-hipError_t launch_tokenize_short(const BuildParams &p, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(k_tokenize_short, dim3(grid), dim3(256), 0, s, p);
+hipError_t launch_tokenize_wave(const BuildParams &p, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(k_tokenize_wave, dim3(grid), dim3(64), 0, s, p);
   return hipGetLastError();
 }
 hipError_t launch_tokenize_long(const BuildParams &p, int grid, hipStream_t s) {

@@ -169,7 +169,7 @@ __global__ void k_slot_to_canon(const uint64_t *dict, uint32_t C, const uint64_t
                                 uint32_t *canon_of_slot) {
   const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= C) return;
-  const uint64_t lo = dict[2 * s], hi = dict[2 * s + 1];
+  const uint64_t lo = dict[s], hi = dict[C + s];   // lo[C] then hi[C]
   if (lo == 0) { canon_of_slot[s] = kInvalidSlot; return; }
   uint64_t a = 0, z = n_canon;
   while (a < z) {

@@ -419,8 +419,8 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
 
   HIP_TRY(hipEventRecord(ix->ev[EV_START], s));
   if (N) {
-    const uint64_t grid = std::min<uint64_t>(N, (uint64_t)ix->num_cus * 4);
-    HIP_TRY(launch_tokenize_short(bp, (int)grid, s));
+    const uint64_t grid = std::min<uint64_t>(N, (uint64_t)ix->num_cus * kWaveWGsPerCU);
+    HIP_TRY(launch_tokenize_wave(bp, (int)grid, s));
   }
   HIP_TRY(hipEventRecord(ix->ev[EV_TOK], s));
   if (bp.debug_stop) {                      // profiling only: rows are incomplete, stop here
@@ -519,7 +519,7 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   HIP_TRY(hipStreamSynchronize(s));
   if (err2 & kErrTfTooLarge) return fail(TFIDF_E_UNSUPPORTED_INPUT, "a term frequency exceeds 2^24 - 1");
   uint64_t nt = 0;
-  for (uint32_t i = 0; i < C; i++) nt += ix->h_dict[2 * (size_t)i] != 0;
+  for (uint32_t i = 0; i < C; i++) nt += ix->h_dict[i] != 0;
   ix->num_terms = nt;
 
   tfidf_commit_timing &t = ix->timing;
@@ -569,9 +569,11 @@ extern "C" int tfidf_stats(const tfidf_index *ix, tfidf_index_stats *out) {
 static uint32_t host_lookup(const tfidf_index *ix, uint64_t lo, uint64_t hi) {
   if (ix->C == 0) return kInvalidSlot;
   const uint32_t mask = ix->C - 1;
-  uint32_t s = (uint32_t)key_hash(lo, hi) & mask;
+  // same probe order as the device (kernels_index.hip dict_lookup_multi):
+  // linear from the aligned 2-slot bucket of the hash; lo[C] then hi[C]
+  uint32_t s = dict_home(dict_hash(lo, hi), mask) & ~1u;
   for (uint32_t it = 0; it <= mask; it++) {
-    const uint64_t clo = ix->h_dict[2 * (size_t)s], chi = ix->h_dict[2 * (size_t)s + 1];
+    const uint64_t clo = ix->h_dict[s], chi = ix->h_dict[(size_t)ix->C + s];
     if (clo == 0) return kInvalidSlot;
     if (clo == lo && chi == hi) return s;
     s = (s + 1) & mask;
@@ -812,7 +814,7 @@ extern "C" int tfidf_doc_terms(tfidf_index *ix, uint64_t doc, char *terms, uint6
   std::vector<std::pair<std::string, uint32_t>> rows;
   for (uint32_t i = 0; i < nu; i++) {
     char b[32];
-    const uint64_t lo = ix->h_dict[2 * (size_t)col[i]], hi = ix->h_dict[2 * (size_t)col[i] + 1];
+    const uint64_t lo = ix->h_dict[col[i]], hi = ix->h_dict[(size_t)ix->C + col[i]];
     uint32_t n = key_decode(lo, hi, b);
     std::string s;
     if (n) s.assign(b, n);
@@ -878,8 +880,8 @@ extern "C" int tfidf_vocab_export_device(tfidf_index *ix, void *d_keys, void *d_
   std::vector<std::pair<std::pair<uint64_t, uint64_t>, uint32_t>> v;
   v.reserve(ix->num_terms);
   for (uint32_t s = 0; s < ix->C; s++)
-    if (ix->h_dict[2 * (size_t)s])
-      v.push_back({{ix->h_dict[2 * (size_t)s + 1], ix->h_dict[2 * (size_t)s]}, ix->h_df[s]});
+    if (ix->h_dict[s])
+      v.push_back({{ix->h_dict[(size_t)ix->C + s], ix->h_dict[s]}, ix->h_df[s]});
   std::sort(v.begin(), v.end());
   std::vector<uint64_t> keys(2 * v.size());
   std::vector<uint32_t> df(v.size());

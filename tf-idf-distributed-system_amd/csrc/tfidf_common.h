@@ -1,14 +1,17 @@
 // tfidf_common.h — definitions shared by host and device code of libtfidf.
 //
 // Term identity.  A term is the lower-cased byte string of a StandardAnalyzer
-// token (Lucene 9.8.0).  The engine keys terms by 128 bits (lo, hi):
-//   * tokens of <= 17 bytes: exact — bits 0..4 of lo = length, char j (7-bit
-//     ASCII) at bits [5 + 7j, 12 + 7j) of the 128-bit value.  Because the
-//     length sits in lo, two keys with equal lo have equal length, and a
-//     token of <= 8 bytes is fully described by lo (its hi is VALID alone);
-//   * longer tokens (18..255 bytes): two independent 64-bit hashes with the
-//     LONG flag set (bits 0..4 of lo = 0, so they never equal a short lo).
-// Bit 127 (VALID) is set for every key so that hi == 0 marks "not written".
+// token (Lucene 9.8.0).  The engine keys terms by 128 bits (lo, hi) built from
+// the raw bytes (ASCII, so bit 7 of every byte is free for flags; a token
+// never holds a 0 byte, so zero padding encodes the length):
+//   * 1..8 bytes : lo = bytes 0..7 (little endian, zero padded), hi = VALID.
+//                  lo alone identifies the term (bit 63 of lo clear);
+//   * 9..16 bytes: lo = bytes 0..7 | LO_LONG (bit 63), hi = bytes 8..15 |
+//                  VALID — exact;
+//   * 17..255    : lo = bytes 0..7 | LO_LONG | LO_HASHED (bit 55), hi = VALID
+//                  | 63-bit hash of all bytes and the length.
+// Bit 63 of hi (VALID) is set for every key so that hi == 0 marks "not
+// written" in the device dictionary.
 #pragma once
 
 #include <stdint.h>
@@ -22,9 +25,10 @@
 namespace tfidf {
 
 constexpr uint32_t kMaxTokenLen = 255;          // StandardAnalyzer.DEFAULT_MAX_TOKEN_LENGTH
-constexpr uint32_t kShortKeyChars = 17;         // 5 + 17 * 7 = 124 payload bits
+constexpr uint32_t kExactKeyChars = 16;         // longer keys carry a hash in hi
 constexpr uint64_t kKeyValid = 1ull << 63;      // in hi
-constexpr uint64_t kKeyLong = 1ull << 62;       // in hi
+constexpr uint64_t kLoLong = 1ull << 63;        // in lo: more than 8 bytes
+constexpr uint64_t kLoHashed = 1ull << 55;      // in lo: more than 16 bytes (hi is a hash)
 constexpr uint32_t kRangeBits = 15;             // 32768 dictionary slots per LDS range tile
 constexpr uint32_t kRangeSlots = 1u << kRangeBits;
 constexpr uint32_t kBlockDocs = 8192;           // doc block of the inverted index / scorer
@@ -67,68 +71,67 @@ TFIDF_HD uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
   return z ^ (z >> 31);
 }
 
-// 32-bit multiply-xorshift hash of a 128-bit key.  The global dictionary
-// uses the low bits (slot = h & (2^c - 1), c <= 21), the per-document LDS
-// table the top 10 bits, so the two probe sequences are independent.
-TFIDF_HD uint32_t key_hash(uint64_t lo, uint64_t hi) {
-  uint32_t h = (uint32_t)lo * 0x9E3779B1u;
-  h ^= (uint32_t)(lo >> 32) * 0x85EBCA77u;
-  h ^= (uint32_t)hi * 0xC2B2AE3Du;
-  h ^= (uint32_t)(hi >> 32) * 0x27D4EB2Fu;
+// 32-bit multiply-xorshift hash of a 64-bit word.
+TFIDF_HD uint32_t hash32_64(uint64_t k) {
+  uint32_t h = (uint32_t)k * 0x9E3779B1u ^ (uint32_t)(k >> 32) * 0x85EBCA77u;
   h ^= h >> 15;
   h *= 0x2C1B3C6Du;
   h ^= h >> 12;
-  h *= 0x297A2D39u;
-  h ^= h >> 15;
   return h;
+}
+
+// Global dictionary hash of a 128-bit key: multiplicative (Fibonacci); the
+// home slot is its TOP cap_log2 bits (dict_home).  One multiply: the wave
+// kernel computes it per distinct term of every document.
+TFIDF_HD uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+TFIDF_HD uint32_t dict_hash(uint64_t lo, uint64_t hi) {
+  const uint32_t x = (uint32_t)lo ^ rotl32((uint32_t)(lo >> 32), 16) ^ (uint32_t)hi ^ rotl32((uint32_t)(hi >> 32), 8);
+  return x * 0x9E3779B1u;
+}
+TFIDF_HD uint32_t dict_hash_short(uint64_t lo) {   // hi = VALID
+  return ((uint32_t)lo ^ rotl32((uint32_t)(lo >> 32), 16) ^ 0x80u) * 0x9E3779B1u;
+}
+TFIDF_HD uint32_t dict_home(uint32_t h, uint32_t mask) {   // mask = C - 1, C = 2^c >= 2
+  return (h >> __builtin_clz(mask)) & mask;
 }
 
 // Incremental key builder over lower-cased bytes.
 struct KeyBuilder {
-  uint64_t lo = 0, hi = 0;    // packed payload (short form), length added in finish()
-  uint64_t h1 = 0x243F6A8885A308D3ull, h2 = 0x13198A2E03707344ull;  // long-form hashes
+  uint64_t w0 = 0, w1 = 0;    // raw bytes 0..15
+  uint64_t h1 = 0x243F6A8885A308D3ull, h2 = 0x13198A2E03707344ull;  // hash of all bytes
   uint32_t n = 0;
   TFIDF_HD void push(uint8_t c) {
-    if (n < kShortKeyChars) {
-      const uint32_t bit = 5 + 7 * n;
-      const uint64_t v = (uint64_t)c;
-      if (bit < 64) {
-        lo |= v << bit;
-        if (bit > 57) hi |= v >> (64 - bit);
-      } else {
-        hi |= v << (bit - 64);
-      }
-    }
+    if (n < 8) w0 |= (uint64_t)c << (8 * n);
+    else if (n < 16) w1 |= (uint64_t)c << (8 * (n - 8));
     h1 = (h1 ^ c) * 0x100000001B3ull;
     h2 = mix64(h2 + c);
     n++;
   }
   TFIDF_HD void finish(uint64_t *klo, uint64_t *khi) const {
-    if (n <= kShortKeyChars) {
-      *klo = lo | n;
-      *khi = hi | kKeyValid;
+    if (n <= 8) {
+      *klo = w0;
+      *khi = kKeyValid;
+    } else if (n <= kExactKeyChars) {
+      *klo = w0 | kLoLong;
+      *khi = w1 | kKeyValid;
     } else {
-      const uint64_t a = (mix64(h1 ^ ((uint64_t)n << 56)) & ~31ull) | 32ull;   // low 5 bits 0, lo != 0
-      const uint64_t b = mix64(h2 ^ a);
-      *klo = a;
-      *khi = (b & ~(3ull << 62)) | kKeyValid | kKeyLong;
+      *klo = w0 | kLoLong | kLoHashed;
+      *khi = mix64(h2 ^ mix64(h1 ^ ((uint64_t)n << 56))) | kKeyValid;
     }
   }
 };
 
-TFIDF_HD bool key_is_long(uint64_t hi) { return (hi & kKeyLong) != 0; }
+TFIDF_HD bool key_is_hashed(uint64_t lo) { return (lo & kLoHashed) != 0; }
 
-// Decode a short key back to bytes; returns length (0 if long).
+// Decode an exact key back to bytes; returns length (0 if hashed).
 TFIDF_HD uint32_t key_decode(uint64_t lo, uint64_t hi, char *out) {
-  if (key_is_long(hi)) return 0;
-  const uint32_t n = (uint32_t)(lo & 31);
-  for (uint32_t j = 0; j < n; j++) {
-    const uint32_t bit = 5 + 7 * j;
-    uint64_t v;
-    if (bit + 7 <= 64) v = (lo >> bit) & 0x7F;
-    else if (bit < 64) v = ((lo >> bit) | (hi << (64 - bit))) & 0x7F;
-    else v = (hi >> (bit - 64)) & 0x7F;
-    out[j] = (char)v;
+  if (key_is_hashed(lo)) return 0;
+  const uint64_t w[2] = {lo & ~kLoLong, (lo & kLoLong) ? (hi & ~kKeyValid) : 0ull};
+  uint32_t n = 0;
+  for (int i = 0; i < 16; i++) {
+    const uint8_t c = (uint8_t)(w[i >> 3] >> (8 * (i & 7)));
+    if (!c) break;
+    out[n++] = (char)c;
   }
   return n;
 }

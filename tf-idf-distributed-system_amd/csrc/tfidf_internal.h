@@ -15,10 +15,6 @@ constexpr uint32_t kErrCapacity = 4u;
 constexpr uint32_t kErrTfTooLarge = 8u;
 constexpr uint32_t kErrLongScratch = 16u;
 
-// Short-document path limits (workgroup per document, LDS tables).
-constexpr uint32_t kShortMaxBytes = 4096;
-constexpr uint32_t kShortMaxTokens = 1024;
-constexpr uint32_t kShortTable = 1024;
 // Long-document path: chunks of kChunk bytes, global per-document table.
 constexpr uint32_t kChunk = 2048;
 constexpr uint32_t kPreMargin = 64;
@@ -29,7 +25,7 @@ struct BuildParams {
   const uint64_t *offsets;    // staged doc offsets [n_staged + 1]
   const uint32_t *live_map;   // committed doc -> staged doc (nullptr = identity)
   uint64_t n_docs;            // committed docs
-  uint64_t *dict;             // 2*C u64: [2s] = key lo, [2s+1] = key hi
+  uint64_t *dict;             // 2*C u64: lo[C] (key lo per slot) then hi[C]
   uint32_t cap_mask;          // C - 1
   uint32_t range_shift;       // log2(range size)
   uint32_t n_ranges;          // R = C >> range_shift
@@ -73,7 +69,8 @@ struct PostingParams {
 };
 
 // --- launch wrappers (kernels_index.hip) ---
-hipError_t launch_tokenize_short(const BuildParams &p, int grid, hipStream_t s);
+hipError_t launch_tokenize_wave(const BuildParams &p, int grid, hipStream_t s);
+constexpr uint32_t kWaveWGsPerCU = 8;    // 64-thread workgroups per CU (2 waves/SIMD: VGPR-bound)
 hipError_t launch_tokenize_long(const BuildParams &p, int grid, hipStream_t s);
 hipError_t launch_df_partial(const PostingParams &p, hipStream_t s);
 hipError_t launch_block_scan(const PostingParams &p, hipStream_t s);

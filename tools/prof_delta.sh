@@ -6,7 +6,7 @@ cd /tmp && export TMPDIR=/tmp
 for s in $1 $2; do
  for g in 1 2; do
   if [ $g = 1 ]; then C="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES"; else C="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS_ATOMIC SQ_LDS_ATOMIC_RETURN"; fi
-  TFIDF_DEBUG_STOP=$s timeout -s KILL 90 rocprofv3 --pmc $C --kernel-include-regex tokenize_short -d $O/s${s}g$g -o p --output-format csv -- python3 $R/bench.py --docs 200000 --steps 1 --warmup 0 --no-queries --cpu-sample 0 > $O/s${s}g$g.log 2>&1 || exit 2
+  TFIDF_DEBUG_STOP=$s timeout -s KILL 90 rocprofv3 --pmc $C --kernel-include-regex tokenize_wave -d $O/s${s}g$g -o p --output-format csv -- python3 $R/bench.py --docs 200000 --steps 1 --warmup 0 --no-queries --cpu-sample 0 > $O/s${s}g$g.log 2>&1 || exit 2
  done
 done
 python3 - $O $1 $2 <<'PY'
