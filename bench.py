@@ -152,7 +152,7 @@ def main():
         # slot column read + per-block DF partials written
         "ms_df": 4 * nnz + 4 * n_blocks * C_slots,
         # partials read + offsets written
-        "ms_blockscan": 8 * n_blocks * C_slots,
+        "ms_blockscan": 12 * n_blocks * C_slots,
         # CSR (slot + tf) read + packed postings written
         "ms_scatter": 16 * nnz + 4 * n_blocks * C_slots,
     }

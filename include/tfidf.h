@@ -89,8 +89,8 @@ typedef struct tfidf_commit_timing {
   float ms_tokenize;   /* tfidf_tokenize_count: text -> per-doc TF rows (CSR) */
   float ms_long;       /* long-document path */
   float ms_df;         /* per (doc block, term range) DF histograms */
-  float ms_blockscan;  /* DF reduction over blocks + posting offsets */
-  float ms_colscan;    /* exclusive scan of DF -> posting-list starts */
+  float ms_blockscan;  /* DF = sum over doc blocks + per-block posting offsets (scan over slots) */
+  float ms_colscan;    /* exclusive scan of block totals -> block bases */
   float ms_scatter;    /* CSR -> block-segmented inverted postings */
   uint64_t text_bytes;
   uint64_t num_docs;

@@ -15,12 +15,15 @@
 //                    per-document hash table in global memory.
 //   df_partial     : per (8192-doc block, 32768-slot range) LDS histogram of
 //                    CSR slots -> per-block DF counts (no global atomics).
-//   block_scan     : exclusive scan over blocks per slot -> posting offsets,
-//                    DF = total (docFreq), in place.
-//   col_scan       : exclusive scan of DF -> posting-list start per slot.
-//   scatter        : CSR -> block-segmented inverted postings, packed
-//                    (doc u32 | tf << 8 | norm) u64.
+//   df_sum         : DF (docFreq) per slot = sum of the per-block counts.
+//   row_scan       : per block, exclusive scan over slots -> offsets of each
+//                    term's postings inside the block; block totals.
+//   block_base     : exclusive scan of block totals -> block bases.
+//   scatter        : CSR -> block-major inverted postings (block b, slot s
+//                    at bbase[b] + offset), packed (doc u32 | tf << 8 | norm) u64.
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 
 #include "tfidf_common.h"
 #include "tfidf_internal.h"
@@ -1269,7 +1272,12 @@ __device__ __forceinline__ void doc_segment(const PostingParams &p, uint64_t d, 
   *hi = p.rsplit[d * p.n_ranges + r];
 }
 
+// Documents per wave in flight in the inversion kernels: each wave walks
+// kInvDocs documents' segments together so their loads overlap.
+constexpr int kInvDocs = 4;
+
 // grid (n_blocks, n_ranges), 1024 threads, LDS histogram of one slot range.
+// Wave w handles documents d0 + w + 16 (kInvDocs i + j), j < kInvDocs.
 __global__ void __launch_bounds__(1024) k_df_partial(PostingParams p) {
   extern __shared__ uint32_t hist[];
   const uint32_t b = blockIdx.x, r = blockIdx.y;
@@ -1280,39 +1288,49 @@ __global__ void __launch_bounds__(1024) k_df_partial(PostingParams p) {
   const uint64_t d1 = d0 + kBlockDocs < p.n_docs ? d0 + kBlockDocs : p.n_docs;
   const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const uint32_t rmask = RS - 1;
-  for (uint64_t d = d0 + wid; d < d1; d += nw) {
-    uint64_t base;
-    uint32_t lo, hi;
-    doc_segment(p, d, r, &base, &lo, &hi);
-    for (uint32_t e = lo + lane; e < hi; e += 64) atomicAdd(&hist[p.csr_col[base + e] & rmask], 1u);
+  for (uint64_t dd = d0 + wid; dd < d1; dd += (uint64_t)nw * kInvDocs) {
+    uint64_t base[kInvDocs];
+    uint32_t lo[kInvDocs], hi[kInvDocs], maxn = 0;
+#pragma unroll
+    for (int j = 0; j < kInvDocs; j++) {
+      const uint64_t d = dd + (uint64_t)nw * j;
+      lo[j] = hi[j] = 0;
+      base[j] = 0;
+      if (d < d1) doc_segment(p, d, r, &base[j], &lo[j], &hi[j]);
+      maxn = max(maxn, hi[j] - lo[j]);
+    }
+    for (uint32_t off = lane; off < maxn; off += 64) {
+      uint32_t c[kInvDocs];
+#pragma unroll
+      for (int j = 0; j < kInvDocs; j++) c[j] = lo[j] + off < hi[j] ? p.csr_col[base[j] + lo[j] + off] : kInvalidSlot;
+#pragma unroll
+      for (int j = 0; j < kInvDocs; j++)
+        if (c[j] != kInvalidSlot) atomicAdd(&hist[c[j] & rmask], 1u);
+    }
   }
   __syncthreads();
   uint32_t *out = p.blk + (size_t)b * p.C + ((size_t)r << p.range_shift);
   for (uint32_t i = threadIdx.x; i < RS; i += blockDim.x) out[i] = hist[i];
 }
 
-// per slot: exclusive scan over blocks in place; row n_blocks = df.
-__global__ void __launch_bounds__(256) k_block_scan(PostingParams p) {
+// per slot: df = sum of the per-block counts (row n_blocks).
+__global__ void __launch_bounds__(256) k_df_sum(PostingParams p) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= p.C) return;
   uint32_t run = 0;
-  for (uint32_t b = 0; b < p.n_blocks; b++) {
-    const size_t i = (size_t)b * p.C + t;
-    const uint32_t v = p.blk[i];
-    p.blk[i] = run;
-    run += v;
-  }
+  for (uint32_t b = 0; b < p.n_blocks; b++) run += p.blk[(size_t)b * p.C + t];
   p.blk[(size_t)p.n_blocks * p.C + t] = run;
 }
 
-// single workgroup exclusive scan of df (row n_blocks of blk) -> col_ptr[C + 1].
-// Tiles of 16384 slots: each thread loads 16 consecutive df values with four
+// per block row: exclusive scan over slots in place (one workgroup per row);
+// the row total goes to bbase[b + 1] (turned into bases by k_block_base).
+// Tiles of 16384 slots: each thread loads 16 consecutive counts with four
 // 16 B loads (coalesced across the workgroup), scans them in registers, and a
 // workgroup scan of the 1024 thread totals gives the offsets.
-__global__ void __launch_bounds__(1024) k_col_scan(PostingParams p) {
-  __shared__ unsigned long long wsum[16];
-  __shared__ unsigned long long carry_sh;
-  const uint32_t *df = p.blk + (size_t)p.n_blocks * p.C;
+__global__ void __launch_bounds__(1024) k_row_scan(PostingParams p) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t carry_sh;
+  uint32_t *row = p.blk + (size_t)blockIdx.x * p.C;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if (tid == 0) carry_sh = 0;
   __syncthreads();
@@ -1320,7 +1338,7 @@ __global__ void __launch_bounds__(1024) k_col_scan(PostingParams p) {
     const uint32_t i0 = t0 + tid * 16;
     uint32_t v[16];
     if (i0 + 16 <= p.C) {
-      const uint4 *src = reinterpret_cast<const uint4 *>(df + i0);
+      const uint4 *src = reinterpret_cast<const uint4 *>(row + i0);
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const uint4 x = src[q];
@@ -1328,67 +1346,115 @@ __global__ void __launch_bounds__(1024) k_col_scan(PostingParams p) {
       }
     } else {
 #pragma unroll
-      for (int q = 0; q < 16; q++) v[q] = (i0 + q < p.C) ? df[i0 + q] : 0u;
+      for (int q = 0; q < 16; q++) v[q] = (i0 + q < p.C) ? row[i0 + q] : 0u;
     }
-    unsigned long long tot = 0;
+    uint32_t tot = 0;
 #pragma unroll
     for (int q = 0; q < 16; q++) tot += v[q];
-    // workgroup exclusive scan of tot
-    unsigned long long x = tot;
+    uint32_t x = tot;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-      unsigned long long y = __shfl_up(x, o, 64);
+      const uint32_t y = __shfl_up(x, o, 64);
       if (lane >= (uint32_t)o) x += y;
     }
     if (lane == 63) wsum[wid] = x;
     __syncthreads();
-    unsigned long long base = carry_sh, all = 0;
+    uint32_t base = carry_sh, all = 0;
     for (uint32_t w = 0; w < 16; w++) {
-      const unsigned long long sw = wsum[w];
+      const uint32_t sw = wsum[w];
       if (w < wid) base += sw;
       all += sw;
     }
     base += x - tot;
     __syncthreads();
     if (tid == 0) carry_sh += all;
-    unsigned long long run = base;
-    if (i0 < p.C) {
+    uint32_t run = base;
+    uint32_t o[16];
 #pragma unroll
-      for (int q = 0; q < 16; q++) {
-        if (i0 + q < p.C) p.col_ptr[i0 + q] = run;
-        run += v[q];
-      }
+    for (int q = 0; q < 16; q++) { o[q] = run; run += v[q]; }
+    if (i0 + 16 <= p.C) {
+      uint4 *dst = reinterpret_cast<uint4 *>(row + i0);
+#pragma unroll
+      for (int q = 0; q < 4; q++) dst[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 16; q++)
+        if (i0 + q < p.C) row[i0 + q] = o[q];
     }
     __syncthreads();
   }
-  if (tid == 0) p.col_ptr[p.C] = carry_sh;
+  if (tid == 0) p.bbase[blockIdx.x + 1] = carry_sh;
 }
 
-// grid (n_blocks, n_ranges), 1024 threads: LDS cursor per slot of the range.
+// bbase[b + 1] holds block b's total: exclusive scan over blocks (tiny).
+__global__ void k_block_base(PostingParams p) {
+  if (threadIdx.x != 0) return;
+  uint64_t run = 0;
+  p.bbase[0] = 0;
+  for (uint32_t b = 0; b < p.n_blocks; b++) {
+    run += p.bbase[b + 1];
+    p.bbase[b + 1] = run;
+  }
+}
+
+// grid (n_blocks, n_ranges), 1024 threads: LDS cursor per slot of the range;
+// kInvDocs documents per wave in flight (as k_df_partial).
 __global__ void __launch_bounds__(1024) k_scatter(PostingParams p) {
   extern __shared__ uint32_t cur[];
-  const uint32_t b = blockIdx.x, r = blockIdx.y;
+  for (uint32_t tile = blockIdx.x; tile < p.n_blocks * p.n_ranges; tile += gridDim.x) {
+  const uint32_t b = tile / p.n_ranges, r = tile % p.n_ranges;
+  __syncthreads();
   const uint32_t RS = 1u << p.range_shift;
   const size_t g0 = (size_t)r << p.range_shift;
-  for (uint32_t i = threadIdx.x; i < RS; i += blockDim.x)
-    cur[i] = (uint32_t)(p.col_ptr[g0 + i] + p.blk[(size_t)b * p.C + g0 + i]);
+  const uint32_t *row = p.blk + (size_t)b * p.C + g0;
+  const uint64_t bb = p.bbase[b];
+  for (uint32_t i = threadIdx.x; i < RS; i += blockDim.x) cur[i] = row[i];
   __syncthreads();
   const uint64_t d0 = (uint64_t)b * kBlockDocs;
   const uint64_t d1 = d0 + kBlockDocs < p.n_docs ? d0 + kBlockDocs : p.n_docs;
   const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const uint32_t rmask = RS - 1;
-  for (uint64_t d = d0 + wid; d < d1; d += nw) {
-    uint64_t base;
-    uint32_t lo, hi;
-    doc_segment(p, d, r, &base, &lo, &hi);
-    const uint32_t nrm = p.doc_norm[d];
-    for (uint32_t e = lo + lane; e < hi; e += 64) {
-      const uint32_t g = p.csr_col[base + e];
-      const uint32_t tf = p.csr_tf[base + e];
-      if (tf > kMaxTf) atomicOr(p.err, kErrTfTooLarge);
-      const uint32_t pos = atomicAdd(&cur[g & rmask], 1u);
-      p.post[pos] = (uint64_t)(uint32_t)d | ((uint64_t)((tf << 8) | nrm) << 32);
+  bool tf_big = false;
+  for (uint64_t dd = d0 + wid; dd < d1; dd += (uint64_t)nw * kInvDocs) {
+    uint64_t base[kInvDocs];
+    uint32_t lo[kInvDocs], hi[kInvDocs], nrm[kInvDocs], maxn = 0;
+#pragma unroll
+    for (int j = 0; j < kInvDocs; j++) {
+      const uint64_t d = dd + (uint64_t)nw * j;
+      lo[j] = hi[j] = 0;
+      base[j] = 0;
+      nrm[j] = 0;
+      if (d < d1) {
+        doc_segment(p, d, r, &base[j], &lo[j], &hi[j]);
+        nrm[j] = p.doc_norm[d];
+      }
+      maxn = max(maxn, hi[j] - lo[j]);
     }
+    for (uint32_t off = lane; off < maxn; off += 64) {
+      uint32_t c[kInvDocs], t[kInvDocs];
+#pragma unroll
+      for (int j = 0; j < kInvDocs; j++) {
+        const bool in = lo[j] + off < hi[j];
+        c[j] = in ? p.csr_col[base[j] + lo[j] + off] : kInvalidSlot;
+        t[j] = in ? p.csr_tf[base[j] + lo[j] + off] : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < kInvDocs; j++) {
+        if (c[j] != kInvalidSlot) {
+          tf_big |= t[j] > kMaxTf;
+          const uint64_t d = dd + (uint64_t)nw * j;
+          const uint64_t val = (uint64_t)(uint32_t)d | ((uint64_t)((t[j] << 8) | nrm[j]) << 32);
+          if (p.debug_scatter == 1) {
+            p.post[(base[j] + lo[j] + off) % (p.n_docs * 4)] = val;
+          } else {
+            const uint64_t pos = bb + atomicAdd(&cur[c[j] & rmask], 1u);
+            if (p.debug_scatter != 2) p.post[pos] = val;
+          }
+        }
+      }
+    }
+  }
+  if (tf_big) atomicOr(p.err, kErrTfTooLarge);
   }
 }
 
@@ -1417,18 +1483,24 @@ hipError_t launch_df_partial(const PostingParams &p, hipStream_t s) {
   hipLaunchKernelGGL(k_df_partial, dim3(p.n_blocks, p.n_ranges), dim3(1024), lds, s, p);
   return hipGetLastError();
 }
-hipError_t launch_block_scan(const PostingParams &p, hipStream_t s) {
-  hipLaunchKernelGGL(k_block_scan, dim3((p.C + 255) / 256), dim3(256), 0, s, p);
+hipError_t launch_df_sum(const PostingParams &p, hipStream_t s) {
+  hipLaunchKernelGGL(k_df_sum, dim3((p.C + 255) / 256), dim3(256), 0, s, p);
   return hipGetLastError();
 }
-hipError_t launch_col_scan(const PostingParams &p, hipStream_t s) {
-  hipLaunchKernelGGL(k_col_scan, dim3(1), dim3(1024), 0, s, p);
+hipError_t launch_row_scan(const PostingParams &p, hipStream_t s) {
+  hipLaunchKernelGGL(k_row_scan, dim3(p.n_blocks), dim3(1024), 0, s, p);
+  return hipGetLastError();
+}
+hipError_t launch_block_base(const PostingParams &p, hipStream_t s) {
+  hipLaunchKernelGGL(k_block_base, dim3(1), dim3(64), 0, s, p);
   return hipGetLastError();
 }
 hipError_t launch_scatter(const PostingParams &p, hipStream_t s) {
   allow_big_lds();
   const size_t lds = sizeof(uint32_t) << p.range_shift;
-  hipLaunchKernelGGL(k_scatter, dim3(p.n_blocks, p.n_ranges), dim3(1024), lds, s, p);
+  const uint32_t tiles = p.n_blocks * p.n_ranges;
+  const uint32_t grid = p.scatter_wgs ? std::min(p.scatter_wgs, tiles) : tiles;
+  hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(1024), lds, s, p);
   return hipGetLastError();
 }
 

@@ -77,9 +77,10 @@ __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
     const uint32_t slot = p.q_slot[j];
     if (slot == kInvalidSlot) continue;                   // uniform
     const float w = p.q_w[j];
-    const uint64_t cp = p.col_ptr[slot];
-    const uint64_t lo = cp + p.blk[(size_t)b * p.C + slot];
-    const uint64_t hi = cp + p.blk[(size_t)(b + 1) * p.C + slot];
+    const uint64_t bb = p.bbase[b];
+    const uint32_t *row = p.blk + (size_t)b * p.C;
+    const uint64_t lo = bb + row[slot];
+    const uint64_t hi = slot + 1 < p.C ? bb + row[slot + 1] : p.bbase[b + 1];
     for (uint64_t i = lo + tid; i < hi; i += blockDim.x) {
       const uint64_t e = p.post[i];
       const uint32_t ld = (uint32_t)(e & 0xFFFFFFFFu) - (uint32_t)d0;

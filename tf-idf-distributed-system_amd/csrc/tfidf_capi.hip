@@ -118,7 +118,7 @@ struct tfidf_index {
   std::vector<uint32_t> live_map;  // committed -> staged (empty = identity)
   DevBuf d_live_map;
   uint32_t cap_log2 = 18, C = 0, range_shift = 15, R = 1, n_blocks = 0;
-  DevBuf dict, csr_col, csr_tf, doc_len, doc_nuniq, doc_norm, rsplit, long_list, counters, blk, col_ptr, post;
+  DevBuf dict, csr_col, csr_tf, doc_len, doc_nuniq, doc_norm, rsplit, long_list, counters, blk, bbase, post;
   DevBuf lt_keys, lt_cnt, lt_g;
   uint32_t lt_log2 = 0, lt_wgs = 64;
   std::vector<uint64_t> h_dict;
@@ -188,7 +188,7 @@ extern "C" int tfidf_destroy(tfidf_index *ix) {
   hipStreamSynchronize(ix->stream);
   DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->d_live_map, &ix->dict, &ix->csr_col, &ix->csr_tf, &ix->doc_len,
                     &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->long_list, &ix->counters, &ix->blk,
-                    &ix->col_ptr, &ix->post, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->canon_of_slot,
+                    &ix->bbase, &ix->post, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->canon_of_slot,
                     &ix->q_off, &ix->q_slot, &ix->q_w, &ix->cache, &ix->cand, &ix->cand_n, &ix->out_doc,
                     &ix->out_score, &ix->out_n, &ix->hits, &ix->hits_n, &ix->hits_c, &ix->hits_s, &ix->sort_tmp};
   for (DevBuf *b : bufs) b->release();
@@ -389,7 +389,7 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   HIP_TRY(ix->long_list.reserve(N * 4 + 4));
   HIP_TRY(ix->counters.reserve(64));
   HIP_TRY(ix->blk.reserve((size_t)(ix->n_blocks + 1) * C * 4));
-  HIP_TRY(ix->col_ptr.reserve((size_t)(C + 1) * 8));
+  HIP_TRY(ix->bbase.reserve((size_t)(ix->n_blocks + 2) * 8));
 
   // counters: [0..2] stats u64, [3] err flags u32 + [3].hi first doc, [4] long_count
   uint64_t *ctr = ix->counters.as<uint64_t>();
@@ -492,9 +492,11 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   pp.rsplit = bp.rsplit;
   pp.doc_norm = bp.doc_norm;
   pp.blk = ix->blk.as<uint32_t>();
-  pp.col_ptr = ix->col_ptr.as<uint64_t>();
+  pp.bbase = ix->bbase.as<uint64_t>();
   pp.post = ix->post.as<uint64_t>();
   pp.err = bp.err;
+  if (const char *ds = getenv("TFIDF_DEBUG_SCATTER")) pp.debug_scatter = (uint32_t)atoi(ds);   // profiling only
+  if (const char *sw = getenv("TFIDF_SCATTER_WGS")) pp.scatter_wgs = (uint32_t)atoi(sw);       // profiling only
   HIP_TRY(hipEventRecord(ix->ev[EV_D0], s));
   if (ix->n_blocks) {
     HIP_TRY(launch_df_partial(pp, s));
@@ -502,9 +504,10 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
     HIP_TRY(hipMemsetAsync(ix->blk.p, 0, (size_t)C * 4, s));
   }
   HIP_TRY(hipEventRecord(ix->ev[EV_DF], s));
-  HIP_TRY(launch_block_scan(pp, s));
+  HIP_TRY(launch_df_sum(pp, s));
+  if (ix->n_blocks) HIP_TRY(launch_row_scan(pp, s));
   HIP_TRY(hipEventRecord(ix->ev[EV_BSCAN], s));
-  HIP_TRY(launch_col_scan(pp, s));
+  HIP_TRY(launch_block_base(pp, s));
   HIP_TRY(hipEventRecord(ix->ev[EV_CSCAN], s));
   if (ix->n_blocks) HIP_TRY(launch_scatter(pp, s));
   HIP_TRY(hipEventRecord(ix->ev[EV_SCAT], s));
@@ -556,7 +559,7 @@ extern "C" int tfidf_stats(const tfidf_index *ix, tfidf_index_stats *out) {
   out->long_docs = ix->long_docs;
   out->text_bytes = ix->text_bytes;
   const DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->dict, &ix->csr_col, &ix->csr_tf, &ix->doc_len,
-                          &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->blk, &ix->col_ptr, &ix->post};
+                          &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->blk, &ix->bbase, &ix->post};
   uint64_t tot = 0;
   for (const DevBuf *b : bufs) tot += b->bytes;
   out->device_bytes = tot;
@@ -620,7 +623,7 @@ static int run_scoring(tfidf_index *ix, const std::vector<uint32_t> &qoff, const
   }
   QueryParams qp{};
   qp.post = ix->post.as<uint64_t>();
-  qp.col_ptr = ix->col_ptr.as<uint64_t>();
+  qp.bbase = ix->bbase.as<uint64_t>();
   qp.blk = ix->blk.as<uint32_t>();
   qp.C = ix->C;
   qp.n_blocks = ix->n_blocks;

@@ -62,10 +62,15 @@ struct PostingParams {
   uint32_t n_blocks;          // ceil(n_docs / kBlockDocs)
   const uint32_t *csr_col, *csr_tf, *rsplit;
   const uint8_t *doc_norm;
-  uint32_t *blk;              // [(n_blocks + 1) * C]: counts -> exclusive offsets; row n_blocks = df
-  uint64_t *col_ptr;          // [C + 1]
-  uint64_t *post;             // [nnz]: doc | (tf << 8 | norm) << 32
+  uint32_t *blk;              // [(n_blocks + 1) * C]: per-block term counts -> per-block exclusive
+                              // offsets over slots; row n_blocks = df
+  uint64_t *bbase;            // [n_blocks + 1]: first posting of each block (block-major postings)
+  uint64_t *post;             // [nnz]: doc | (tf << 8 | norm) << 32; block b, slot s at
+                              // bbase[b] + blk[b][s]
   uint32_t *err;
+  uint32_t scatter_wgs;       // persistent scatter grid (0 = one workgroup per tile)
+  uint32_t debug_scatter;     // profiling only (TFIDF_DEBUG_SCATTER): 1 = CSR-order stores, no
+                              // cursor atomics; 2 = cursor atomics, no stores
 };
 
 // --- launch wrappers (kernels_index.hip) ---
@@ -73,15 +78,16 @@ hipError_t launch_tokenize_wave(const BuildParams &p, int grid, hipStream_t s);
 constexpr uint32_t kWaveWGsPerCU = 8;    // 64-thread workgroups per CU (2 waves/SIMD: VGPR-bound)
 hipError_t launch_tokenize_long(const BuildParams &p, int grid, hipStream_t s);
 hipError_t launch_df_partial(const PostingParams &p, hipStream_t s);
-hipError_t launch_block_scan(const PostingParams &p, hipStream_t s);
-hipError_t launch_col_scan(const PostingParams &p, hipStream_t s);
+hipError_t launch_df_sum(const PostingParams &p, hipStream_t s);
+hipError_t launch_row_scan(const PostingParams &p, hipStream_t s);
+hipError_t launch_block_base(const PostingParams &p, hipStream_t s);
 hipError_t launch_scatter(const PostingParams &p, hipStream_t s);
 
 // --- query scoring (kernels_query.hip) ---
 struct QueryParams {
   const uint64_t *post;
-  const uint64_t *col_ptr;
-  const uint32_t *blk;        // exclusive block offsets [(n_blocks + 1) * C]
+  const uint64_t *bbase;      // [n_blocks + 1] first posting of each block
+  const uint32_t *blk;        // per-block exclusive offsets over slots [n_blocks * C]
   uint32_t C;
   uint32_t n_blocks;
   uint64_t n_docs;

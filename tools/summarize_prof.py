@@ -48,6 +48,14 @@ def main():
     ks = kernel_stats(d)
     fetch = pmc(d, "fetch", "FETCH_SIZE")
     write = pmc(d, "write", "WRITE_SIZE")
+    sq = {}
+    for sub in ("sq1", "sq2"):
+        for f in glob.glob(os.path.join(d, sub, "**", "*counter_collection.csv"), recursive=True):
+            acc = collections.defaultdict(float)
+            for r in csv.DictReader(open(f)):
+                acc[(short(r["Kernel_Name"]), r["Counter_Name"])] += float(r["Counter_Value"])
+            for (k, c), v in acc.items():
+                sq.setdefault(k, {})[c] = v
     rows = []
     for k in sorted(set(ks) | set(fetch) | set(write), key=lambda k: -ks.get(k, {}).get("total_ms", 0)):
         s = ks.get(k, {})
@@ -63,6 +71,10 @@ def main():
             r["kernel"][:28], g(r.get("calls"), "%d"), g(r.get("total_ms"), "%.3f"), g(r.get("avg_ms"), "%.4f"),
             g(r.get("pct"), "%.2f"), g(r["fetch_bytes_raw"], "%.4g"), g(r["write_bytes"], "%.4g"),
             g(r["hbm_bytes_corrected"], "%.4g")))
+    if sq:
+        print("\nSQ counters (summed over dispatches of one build; quad-cycles for *_CYCLES/WAIT/ACTIVE):")
+        for k, cs in sorted(sq.items()):
+            print("  %-26s %s" % (k[:26], " ".join("%s=%.3g" % (c.replace("SQ_", ""), v) for c, v in sorted(cs.items()))))
     if "--json" in sys.argv:
         json.dump(rows, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
 
