@@ -43,6 +43,8 @@ def parse():
     ap.add_argument("--batch-queries", type=int, default=10_000)
     ap.add_argument("--cpu-sample", type=int, default=25_000, help="docs in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-queries", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r01", "traffic.json"),
+                    help="per-kernel HBM bytes from tools/prof_round.sh (rocprofv3 PMC passes of this workload)")
     return ap.parse_args()
 
 
@@ -161,6 +163,19 @@ def main():
     achieved = alg[dom] / (dom_ms * 1e-3) / 1e9 if dom_ms > 0 else 0.0
     phase_gbs = {k: (alg[k] / (phases[k] * 1e-3) / 1e9 if phases[k] > 0 else None) for k in alg}
     b_index = text_bytes + 8 * nnz + 9 * N + 4 * args.vocab * world
+    # measured HBM traffic of the dominant kernel: a separate rocprofv3 PMC pass
+    # over the same workload (counters cannot be read from inside this run)
+    traffic, traffic_src = None, None
+    kname = {"ms_tokenize": "k_tokenize_wave", "ms_df": "k_df_partial", "ms_blockscan": "k_row_scan",
+             "ms_scatter": "k_scatter"}[dom]
+    try:
+        tj = json.load(open(args.traffic_json))
+        w = tj.get("workload") or {}
+        if (w.get("docs_per_gpu"), w.get("text_bytes_per_gpu"), w.get("nnz_per_gpu")) == (N, text_bytes, nnz):
+            traffic = tj["kernels"][kname]["hbm_bytes_corrected"]
+            traffic_src = os.path.relpath(args.traffic_json, REPO) + " (" + tj["note"] + ")"
+    except (OSError, KeyError, ValueError, TypeError):
+        pass
     result = {
         "metric": "docs indexed/sec + queries scored/sec (node) at 1/2/4/8 GPUs; % HBM roofline",
         "value": world * N * args.steps / elapsed,
@@ -180,8 +195,8 @@ def main():
             "docs_per_gpu": N, "text_bytes_per_gpu": text_bytes, "nnz_per_gpu": nnz,
             "vocab_terms": st["num_terms"], "parallelism": "dp%d (document shards)" % world},
         "roofline": {"bound": "hbm", "kernel": dom.replace("ms_", ""), "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "alg_bytes_per_launch": alg[dom], "avg_launch_ms": dom_ms},
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": traffic_src, "alg_bytes_per_launch": alg[dom], "avg_launch_ms": dom_ms},
         "phases_ms": phases,
         "phases_alg_GBs": phase_gbs,
         "index_build_alg_bytes": b_index,

@@ -18,6 +18,7 @@ SMALL="python3 $R/bench.py --steps 1 --warmup 0 --no-queries --cpu-sample 0 ${PM
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_" -d $O/fetch -o fetch --output-format csv -- $SMALL > $O/fetch.log 2>&1 || { echo "fetch failed"; tail -5 $O/fetch.log; exit 2; }
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_" -d $O/write -o write --output-format csv -- $SMALL > $O/write.log 2>&1 || { echo "write failed"; tail -5 $O/write.log; exit 3; }
 echo "traffic ok"
+grep '"metric"' $O/fetch.log | python3 -c "import json,sys; r=json.loads(sys.stdin.read()); c=r['config']; json.dump({'docs_per_gpu': c['docs_per_gpu'], 'text_bytes_per_gpu': c['text_bytes_per_gpu'], 'nnz_per_gpu': c['nnz_per_gpu']}, open('$O/workload.json','w'))" || true
 if [ -n "${SQ:-}" ]; then
   timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --kernel-include-regex "k_" -d $O/sq1 -o sq1 --output-format csv -- $SMALL > $O/sq1.log 2>&1 || { echo "sq1 failed"; exit 4; }
   timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_BUSY_CYCLES --kernel-include-regex "k_" -d $O/sq2 -o sq2 --output-format csv -- $SMALL > $O/sq2.log 2>&1 || { echo "sq2 failed"; exit 5; }
@@ -30,4 +31,4 @@ if [ -n "${ABLATE:-}" ]; then
     python3 -c "import json; r=json.loads(open('$O/ablate_$s.log').read().strip().splitlines()[-1]); print('stop=$s tokenize_ms=%.3f' % r['phases_ms']['ms_tokenize'])" 2>/dev/null || { echo "stop=$s: no json"; tail -3 $O/ablate_$s.log; }
   done
 fi
-python3 $R/tools/summarize_prof.py $O
+python3 $R/tools/summarize_prof.py $O --json $O/traffic.json

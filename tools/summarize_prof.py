@@ -76,7 +76,12 @@ def main():
         for k, cs in sorted(sq.items()):
             print("  %-26s %s" % (k[:26], " ".join("%s=%.3g" % (c.replace("SQ_", ""), v) for c, v in sorted(cs.items()))))
     if "--json" in sys.argv:
-        json.dump(rows, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
+        out = {"note": "per-launch HBM bytes from separate rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE in KiB; "
+                       "FETCH doubled for gfx950 wide streaming reads per MI355X_MICROARCH.md)",
+               "workload": json.load(open(os.path.join(d, "workload.json"))) if os.path.exists(
+                   os.path.join(d, "workload.json")) else None,
+               "kernels": {r["kernel"]: r for r in rows}}
+        json.dump(out, open(sys.argv[sys.argv.index("--json") + 1], "w"), indent=1)
 
 
 if __name__ == "__main__":
