@@ -776,32 +776,36 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     uint32_t claims = 0, toks = 0;
     bool overflow = false;
     for (uint32_t tb = 0; tb < ntok && !overflow; tb += 64 * kWaveK) {
-      const uint32_t kmax = min(kWaveK, (ntok - tb + 63) >> 6);   // wave-uniform
       uint64_t tkey[kWaveK];
       uint32_t slot[kWaveK];
       uint32_t pendm = 0, longm = 0;
+      // keys of <= 8 bytes, branch-free: all list reads, then all text reads, then the math
+      uint32_t ent[kWaveK];
 #pragma unroll
-      for (int k = 0; k < (int)kWaveK; k++) {          // keys of <= 8 bytes, branch-free
-        tkey[k] = 0;
-        slot[k] = 0;
-        if ((uint32_t)k < kmax) {
-          const uint32_t idx = tb + lane + 64 * k;
-          const bool in = idx < ntok;
-          const uint32_t e = sm.list[in ? idx : 0u];
-          const uint32_t tp = e & 0xFFFFu, n = (e >> 16) - tp;
-          const uint32_t a0 = tp >> 2, o = tp & 3;
-          const uint32_t d0 = tw[a0], d1 = tw[a0 + 1], d2 = tw[a0 + 2];
-          const uint64_t m64 = n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1);
-          const uint32_t t0 = __builtin_amdgcn_alignbyte(d1, d0, o) & (uint32_t)m64;
-          const uint32_t t1 = __builtin_amdgcn_alignbyte(d2, d1, o) & (uint32_t)(m64 >> 32);
-          bool valid = true;
-          if (under) valid = (((t0 ^ 0x5F5F5F5Fu) & (uint32_t)m64) | ((t1 ^ 0x5F5F5F5Fu) & (uint32_t)(m64 >> 32))) != 0;
-          const uint32_t l0 = lower4(t0), l1 = lower4(t1);
-          tkey[k] = (uint64_t)l0 | ((uint64_t)l1 << 32);
-          slot[k] = ((l0 ^ rotl32(l1, 16)) * 0x85EBCA77u) >> (32 - kWaveSlotBits);
-          pendm |= (uint32_t)(in && n <= 8 && valid) << k;
-          longm |= (uint32_t)(in && n > 8) << k;
-        }
+      for (int k = 0; k < (int)kWaveK; k++) {
+        const uint32_t idx = tb + lane + 64 * k;
+        ent[k] = sm.list[idx < ntok ? idx : 0u];
+      }
+      uint32_t dw[kWaveK][3];
+#pragma unroll
+      for (int k = 0; k < (int)kWaveK; k++) {
+        const uint32_t a0 = (ent[k] & 0xFFFFu) >> 2;
+        dw[k][0] = tw[a0]; dw[k][1] = tw[a0 + 1]; dw[k][2] = tw[a0 + 2];
+      }
+#pragma unroll
+      for (int k = 0; k < (int)kWaveK; k++) {
+        const bool in = tb + lane + 64 * k < ntok;
+        const uint32_t tp = ent[k] & 0xFFFFu, n = (ent[k] >> 16) - tp, o = tp & 3;
+        const uint64_t m64 = n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1);
+        const uint32_t t0 = __builtin_amdgcn_alignbyte(dw[k][1], dw[k][0], o) & (uint32_t)m64;
+        const uint32_t t1 = __builtin_amdgcn_alignbyte(dw[k][2], dw[k][1], o) & (uint32_t)(m64 >> 32);
+        bool valid = true;
+        if (under) valid = (((t0 ^ 0x5F5F5F5Fu) & (uint32_t)m64) | ((t1 ^ 0x5F5F5F5Fu) & (uint32_t)(m64 >> 32))) != 0;
+        const uint32_t l0 = lower4(t0), l1 = lower4(t1);
+        tkey[k] = (uint64_t)l0 | ((uint64_t)l1 << 32);
+        slot[k] = ((l0 ^ rotl32(l1, 16)) * 0x85EBCA77u) >> (32 - kWaveSlotBits);
+        pendm |= (uint32_t)(in && n <= 8 && valid) << k;
+        longm |= (uint32_t)(in && n > 8) << k;
       }
       const bool hasfold = __any(longm != 0);
       if (hasfold) {                                    // tokens of 9..255 bytes: folded keys
@@ -860,29 +864,24 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         uint64_t old[kWaveK];
 #pragma unroll
         for (int k = 0; k < (int)kWaveK; k++) {
-          old[k] = 0;
-          if ((uint32_t)k < kmax) {
-            const bool pend = (pendm >> k) & 1u;
-            old[k] = atomicCAS(pend ? reinterpret_cast<unsigned long long *>(&sm.key[slot[k]]) : noop,
-                               pend ? 0ull : ~0ull, (unsigned long long)tkey[k]);
-          }
+          const bool pend = (pendm >> k) & 1u;
+          old[k] = atomicCAS(pend ? reinterpret_cast<unsigned long long *>(&sm.key[slot[k]]) : noop,
+                             pend ? 0ull : ~0ull, (unsigned long long)tkey[k]);
         }
         uint32_t foldm = 0;
 #pragma unroll
         for (int k = 0; k < (int)kWaveK; k++) {
-          if ((uint32_t)k < kmax) {
-            const bool pend = (pendm >> k) & 1u;
-            const bool hit = pend && (old[k] == 0 || old[k] == tkey[k]);
-            atomicAdd(hit ? &sm.cnt[slot[k] >> 1] : reinterpret_cast<uint32_t *>(noop),
-                      hit ? 1u << (16 * (slot[k] & 1)) : 0u);
-            claims += hit && old[k] == 0;
-            pendm &= ~((uint32_t)hit << k);
-            bool fc = false;
-            if (hasfold)
-              fc = pend && !hit && ((old[k] & tkey[k]) >> 63) && ((old[k] ^ tkey[k]) & ~kFoldPosMask) == 0;
-            foldm |= (uint32_t)fc << k;
-            if (pend && !hit && !fc) slot[k] = (slot[k] + 1) & (kWaveSlots - 1);
-          }
+          const bool pend = (pendm >> k) & 1u;
+          const bool hit = pend && (old[k] == 0 || old[k] == tkey[k]);
+          atomicAdd(hit ? &sm.cnt[slot[k] >> 1] : reinterpret_cast<uint32_t *>(noop),
+                    hit ? 1u << (16 * (slot[k] & 1)) : 0u);
+          claims += hit && old[k] == 0;
+          pendm &= ~((uint32_t)hit << k);
+          bool fc = false;
+          if (hasfold)
+            fc = pend && !hit && ((old[k] & tkey[k]) >> 63) && ((old[k] ^ tkey[k]) & ~kFoldPosMask) == 0;
+          foldm |= (uint32_t)fc << k;
+          if (pend && !hit && !fc) slot[k] = (slot[k] + 1) & (kWaveSlots - 1);
         }
         if (hasfold && __any(foldm != 0)) {              // same length and hash: compare bytes
 #pragma unroll
@@ -928,7 +927,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     }
 
     // ---- dictionary slots of terms lane + 64k
-    const uint32_t tmax = (nu + 63) >> 6;                   // wave-uniform, <= kWaveK
     uint32_t g[kWaveK], tf[kWaveK];
     uint32_t actm = 0;
     {
@@ -941,7 +939,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         tf[k] = 0;
         g[k] = kInvalidSlot;
         ps[k] = 0;
-        if ((uint32_t)k < tmax) {
+        {
           const uint32_t idx = lane + 64 * k;
           const bool in = idx < nu;
           const uint32_t s = slots[in ? idx : 0u] & (kWaveSlots - 1);
@@ -1017,27 +1015,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         if (round > dmask) break;                          // table exhausted: capacity error below
         ulonglong2 e[kWaveK];
 #pragma unroll
-        for (int k = 0; k < (int)kWaveK; k++) {
-          e[k] = make_ulonglong2(0, 0);
-          if ((uint32_t)k < tmax)
-            e[k] = *reinterpret_cast<const ulonglong2 *>(p.dict + (g[k] == kLookupPending ? (ps[k] & ~1u) : 0u));
-        }
+        for (int k = 0; k < (int)kWaveK; k++)
+          e[k] = *reinterpret_cast<const ulonglong2 *>(p.dict + (g[k] == kLookupPending ? (ps[k] & ~1u) : 0u));
         uint32_t cs[kWaveK];
         bool anyclaim = false;
 #pragma unroll
         for (int k = 0; k < (int)kWaveK; k++) {
-          cs[k] = kInvalidSlot;
-          if ((uint32_t)k < tmax) {
-            const bool pend = g[k] == kLookupPending;
-            uint32_t c;
-            const uint32_t r = bucket_probe(e[k], ps[k], lo[k], &c);
-            if (pend) {
-              g[k] = r;
-              cs[k] = c;
-              anyclaim |= c != kInvalidSlot;
-              if (r == kLookupPending && c == kInvalidSlot) ps[k] = ((ps[k] | 1u) + 1u) & dmask;
-            }
-          }
+          const bool pend = g[k] == kLookupPending;
+          uint32_t c;
+          const uint32_t r = bucket_probe(e[k], ps[k], lo[k], &c);
+          cs[k] = pend ? c : kInvalidSlot;
+          anyclaim |= pend && c != kInvalidSlot;
+          if (pend && r == kLookupPending && c == kInvalidSlot) ps[k] = ((ps[k] | 1u) + 1u) & dmask;
+          if (pend) g[k] = r;
         }
         if (__any(anyclaim)) {
 #pragma unroll
@@ -1065,10 +1055,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       uint32_t c[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int k = 0; k < (int)kWaveK; k++) {
-        if ((uint32_t)k < tmax) {
-          const uint32_t f = (g[k] >> p.range_shift) - rb;
-          field8_add(c, f, (((actm >> k) & 1u) && f < 8) ? 1u : 0u);
-        }
+        const uint32_t f = (g[k] >> p.range_shift) - rb;
+        field8_add(c, f, (((actm >> k) & 1u) && f < 8) ? 1u : 0u);
       }
       uint32_t pk[4], tot[4];
 #pragma unroll
@@ -1090,14 +1078,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       for (int w = 0; w < 4; w++) pk[w] += fb[w];
 #pragma unroll
       for (int k = 0; k < (int)kWaveK; k++) {
-        if ((uint32_t)k < tmax) {
-          const uint32_t f = (g[k] >> p.range_shift) - rb;
-          const bool inr = ((actm >> k) & 1u) && f < 8;
-          const uint32_t pos = inr ? run + field8(pk, f) : st_noop;
-          field8_add(pk, f, inr ? 1u : 0u);
-          st_col[pos] = g[k];
-          st_tf[pos] = tf[k];
-        }
+        const uint32_t f = (g[k] >> p.range_shift) - rb;
+        const bool inr = ((actm >> k) & 1u) && f < 8;
+        const uint32_t pos = inr ? run + field8(pk, f) : st_noop;
+        field8_add(pk, f, inr ? 1u : 0u);
+        st_col[pos] = g[k];
+        st_tf[pos] = tf[k];
       }
       run += acc;
     }
@@ -1273,8 +1259,47 @@ __device__ __forceinline__ void doc_segment(const PostingParams &p, uint64_t d, 
 }
 
 // Documents per wave in flight in the inversion kernels: each wave walks
-// kInvDocs documents' segments together so their loads overlap.
+// kInvDocs documents' segments together so their loads overlap, and issues
+// the next group's segment loads before the current group's LDS atomics and
+// stores (gfx9 counts stores in vmcnt: waiting for loads issued after a
+// store would also wait for the store).
 constexpr int kInvDocs = 4;
+
+struct InvGroup {               // wave-uniform
+  uint64_t base[kInvDocs];
+  uint32_t lo[kInvDocs], hi[kInvDocs], nrm[kInvDocs];
+  uint32_t maxn;
+};
+
+__device__ __forceinline__ InvGroup inv_group(const PostingParams &p, uint64_t dd, uint64_t d1, uint32_t stride,
+                                              uint32_t r, bool with_norm) {
+  InvGroup g;
+  g.maxn = 0;
+#pragma unroll
+  for (int j = 0; j < kInvDocs; j++) {
+    const uint64_t d = dd + (uint64_t)stride * j;
+    g.lo[j] = g.hi[j] = 0;
+    g.base[j] = 0;
+    g.nrm[j] = 0;
+    if (d < d1) {
+      doc_segment(p, d, r, &g.base[j], &g.lo[j], &g.hi[j]);
+      if (with_norm) g.nrm[j] = p.doc_norm[d];
+    }
+    g.maxn = max(g.maxn, g.hi[j] - g.lo[j]);
+  }
+  return g;
+}
+
+// segment entries off of the group's documents (kInvalidSlot past a segment)
+__device__ __forceinline__ void inv_load(const PostingParams &p, const InvGroup &g, uint32_t off, uint32_t *c,
+                                         uint32_t *t, bool with_tf) {
+#pragma unroll
+  for (int j = 0; j < kInvDocs; j++) {
+    const bool in = g.lo[j] + off < g.hi[j];
+    c[j] = in ? p.csr_col[g.base[j] + g.lo[j] + off] : kInvalidSlot;
+    if (with_tf) t[j] = in ? p.csr_tf[g.base[j] + g.lo[j] + off] : 0u;
+  }
+}
 
 // grid (n_blocks, n_ranges), 1024 threads, LDS histogram of one slot range.
 // Wave w handles documents d0 + w + 16 (kInvDocs i + j), j < kInvDocs.
@@ -1286,27 +1311,32 @@ __global__ void __launch_bounds__(1024) k_df_partial(PostingParams p) {
   __syncthreads();
   const uint64_t d0 = (uint64_t)b * kBlockDocs;
   const uint64_t d1 = d0 + kBlockDocs < p.n_docs ? d0 + kBlockDocs : p.n_docs;
-  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const uint32_t lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const uint32_t wid = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t rmask = RS - 1;
-  for (uint64_t dd = d0 + wid; dd < d1; dd += (uint64_t)nw * kInvDocs) {
-    uint64_t base[kInvDocs];
-    uint32_t lo[kInvDocs], hi[kInvDocs], maxn = 0;
+  const uint64_t step = (uint64_t)nw * kInvDocs;
+  uint64_t dd = d0 + wid;
+  InvGroup cur = inv_group(p, dd, d1, nw, r, false);
+  uint32_t c[kInvDocs], t[kInvDocs];
+  if (dd < d1) inv_load(p, cur, lane, c, t, false);
+  while (dd < d1) {
+    const uint64_t dn = dd + step;
+    const InvGroup nxt = inv_group(p, dn, d1, nw, r, false);
+    uint32_t cn[kInvDocs], tn[kInvDocs];
+    if (dn < d1) inv_load(p, nxt, lane, cn, tn, false);            // next group in flight
 #pragma unroll
-    for (int j = 0; j < kInvDocs; j++) {
-      const uint64_t d = dd + (uint64_t)nw * j;
-      lo[j] = hi[j] = 0;
-      base[j] = 0;
-      if (d < d1) doc_segment(p, d, r, &base[j], &lo[j], &hi[j]);
-      maxn = max(maxn, hi[j] - lo[j]);
-    }
-    for (uint32_t off = lane; off < maxn; off += 64) {
-      uint32_t c[kInvDocs];
-#pragma unroll
-      for (int j = 0; j < kInvDocs; j++) c[j] = lo[j] + off < hi[j] ? p.csr_col[base[j] + lo[j] + off] : kInvalidSlot;
+    for (int j = 0; j < kInvDocs; j++)
+      if (c[j] != kInvalidSlot) atomicAdd(&hist[c[j] & rmask], 1u);
+    for (uint32_t off = lane + 64; off < cur.maxn; off += 64) {     // segments longer than 64
+      inv_load(p, cur, off, c, t, false);
 #pragma unroll
       for (int j = 0; j < kInvDocs; j++)
         if (c[j] != kInvalidSlot) atomicAdd(&hist[c[j] & rmask], 1u);
     }
+    cur = nxt;
+#pragma unroll
+    for (int j = 0; j < kInvDocs; j++) c[j] = cn[j];
+    dd = dn;
   }
   __syncthreads();
   uint32_t *out = p.blk + (size_t)b * p.C + ((size_t)r << p.range_shift);
@@ -1397,65 +1427,63 @@ __global__ void k_block_base(PostingParams p) {
   }
 }
 
-// grid (n_blocks, n_ranges), 1024 threads: LDS cursor per slot of the range;
-// kInvDocs documents per wave in flight (as k_df_partial).
+// grid: (block, range) tiles, 1024 threads: LDS cursor per slot of the range;
+// kInvDocs documents per wave in flight, next group's loads issued before the
+// current group's stores (as k_df_partial).
+__device__ __forceinline__ void scatter_entries(const PostingParams &p, uint32_t *cur, uint32_t rmask, uint64_t bb,
+                                                const InvGroup &g, uint64_t dd, uint32_t stride, const uint32_t *c,
+                                                const uint32_t *t, bool *tf_big) {
+#pragma unroll
+  for (int j = 0; j < kInvDocs; j++) {
+    if (c[j] != kInvalidSlot) {
+      *tf_big |= t[j] > kMaxTf;
+      const uint64_t d = dd + (uint64_t)stride * j;
+      const uint64_t val = (uint64_t)(uint32_t)d | ((uint64_t)((t[j] << 8) | g.nrm[j]) << 32);
+      const uint64_t pos = bb + atomicAdd(&cur[c[j] & rmask], 1u);
+      if (p.debug_scatter != 2) p.post[pos] = val;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(1024) k_scatter(PostingParams p) {
   extern __shared__ uint32_t cur[];
-  for (uint32_t tile = blockIdx.x; tile < p.n_blocks * p.n_ranges; tile += gridDim.x) {
-  const uint32_t b = tile / p.n_ranges, r = tile % p.n_ranges;
-  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const uint32_t wid = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t RS = 1u << p.range_shift;
-  const size_t g0 = (size_t)r << p.range_shift;
-  const uint32_t *row = p.blk + (size_t)b * p.C + g0;
-  const uint64_t bb = p.bbase[b];
-  for (uint32_t i = threadIdx.x; i < RS; i += blockDim.x) cur[i] = row[i];
-  __syncthreads();
-  const uint64_t d0 = (uint64_t)b * kBlockDocs;
-  const uint64_t d1 = d0 + kBlockDocs < p.n_docs ? d0 + kBlockDocs : p.n_docs;
-  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const uint32_t rmask = RS - 1;
   bool tf_big = false;
-  for (uint64_t dd = d0 + wid; dd < d1; dd += (uint64_t)nw * kInvDocs) {
-    uint64_t base[kInvDocs];
-    uint32_t lo[kInvDocs], hi[kInvDocs], nrm[kInvDocs], maxn = 0;
-#pragma unroll
-    for (int j = 0; j < kInvDocs; j++) {
-      const uint64_t d = dd + (uint64_t)nw * j;
-      lo[j] = hi[j] = 0;
-      base[j] = 0;
-      nrm[j] = 0;
-      if (d < d1) {
-        doc_segment(p, d, r, &base[j], &lo[j], &hi[j]);
-        nrm[j] = p.doc_norm[d];
+  for (uint32_t tile = blockIdx.x; tile < p.n_blocks * p.n_ranges; tile += gridDim.x) {
+    const uint32_t b = tile / p.n_ranges, r = tile % p.n_ranges;
+    __syncthreads();
+    const size_t g0 = (size_t)r << p.range_shift;
+    const uint32_t *row = p.blk + (size_t)b * p.C + g0;
+    const uint64_t bb = p.bbase[b];
+    for (uint32_t i = threadIdx.x; i < RS; i += blockDim.x) cur[i] = row[i];
+    __syncthreads();
+    const uint64_t d0 = (uint64_t)b * kBlockDocs;
+    const uint64_t d1 = d0 + kBlockDocs < p.n_docs ? d0 + kBlockDocs : p.n_docs;
+    const uint64_t step = (uint64_t)nw * kInvDocs;
+    uint64_t dd = d0 + wid;
+    InvGroup g = inv_group(p, dd, d1, nw, r, true);
+    uint32_t c[kInvDocs], t[kInvDocs];
+    if (dd < d1) inv_load(p, g, lane, c, t, true);
+    while (dd < d1) {
+      const uint64_t dn = dd + step;
+      const InvGroup gn = inv_group(p, dn, d1, nw, r, true);
+      uint32_t cn[kInvDocs], tn[kInvDocs];
+      if (dn < d1) inv_load(p, gn, lane, cn, tn, true);           // next group in flight
+      scatter_entries(p, cur, rmask, bb, g, dd, nw, c, t, &tf_big);
+      for (uint32_t off = lane + 64; off < g.maxn; off += 64) {    // segments longer than 64
+        inv_load(p, g, off, c, t, true);
+        scatter_entries(p, cur, rmask, bb, g, dd, nw, c, t, &tf_big);
       }
-      maxn = max(maxn, hi[j] - lo[j]);
-    }
-    for (uint32_t off = lane; off < maxn; off += 64) {
-      uint32_t c[kInvDocs], t[kInvDocs];
+      g = gn;
 #pragma unroll
-      for (int j = 0; j < kInvDocs; j++) {
-        const bool in = lo[j] + off < hi[j];
-        c[j] = in ? p.csr_col[base[j] + lo[j] + off] : kInvalidSlot;
-        t[j] = in ? p.csr_tf[base[j] + lo[j] + off] : 0u;
-      }
-#pragma unroll
-      for (int j = 0; j < kInvDocs; j++) {
-        if (c[j] != kInvalidSlot) {
-          tf_big |= t[j] > kMaxTf;
-          const uint64_t d = dd + (uint64_t)nw * j;
-          const uint64_t val = (uint64_t)(uint32_t)d | ((uint64_t)((t[j] << 8) | nrm[j]) << 32);
-          if (p.debug_scatter == 1) {
-            p.post[(base[j] + lo[j] + off) % (p.n_docs * 4)] = val;
-          } else {
-            const uint64_t pos = bb + atomicAdd(&cur[c[j] & rmask], 1u);
-            if (p.debug_scatter != 2) p.post[pos] = val;
-          }
-        }
-      }
+      for (int j = 0; j < kInvDocs; j++) { c[j] = cn[j]; t[j] = tn[j]; }
+      dd = dn;
     }
   }
   if (tf_big) atomicOr(p.err, kErrTfTooLarge);
-  }
 }
 
 // ---------------------------------------------------------------------------
