@@ -1263,7 +1263,7 @@ __device__ __forceinline__ void doc_segment(const PostingParams &p, uint64_t d, 
 // the next group's segment loads before the current group's LDS atomics and
 // stores (gfx9 counts stores in vmcnt: waiting for loads issued after a
 // store would also wait for the store).
-constexpr int kInvDocs = 4;
+constexpr int kInvDocs = 8;
 
 struct InvGroup {               // wave-uniform
   uint64_t base[kInvDocs];
@@ -1427,63 +1427,139 @@ __global__ void k_block_base(PostingParams p) {
   }
 }
 
-// grid: (block, range) tiles, 1024 threads: LDS cursor per slot of the range;
-// kInvDocs documents per wave in flight, next group's loads issued before the
-// current group's stores (as k_df_partial).
-__device__ __forceinline__ void scatter_entries(const PostingParams &p, uint32_t *cur, uint32_t rmask, uint64_t bb,
-                                                const InvGroup &g, uint64_t dd, uint32_t stride, const uint32_t *c,
-                                                const uint32_t *t, bool *tf_big) {
+// Inversion in two passes so that every store stream stays L2-resident.
+// A (block, range) tile's postings span ~10 k term regions: storing each
+// posting straight to its final slot keeps that many partial lines open per
+// workgroup and writes back ~3x the bytes.  Instead:
+//   k_scatter_part : per tile, each posting is appended to one of the tile's
+//                    sub-range streams (kSubSlots slots each) in a temporary
+//                    buffer laid out exactly like the postings (stream k's
+//                    region = the final region of its slots, from blk), packed
+//                    doc_local(13) | slot_low(10) | tf(24) | norm(8);
+//   k_scatter_sort : per stream (~86 KB), LDS cursor per slot, final postings
+//                    written inside the stream's own region.
+constexpr uint32_t kSubSlots = 512;
+constexpr uint32_t kSubBits = 9;
+
+// Lanes of the wave holding the same BITS-bit key (active lanes only): one
+// ballot per key bit.  Used to turn same-address LDS atomics (hot terms hit
+// one cursor from most lanes of a wave) into one atomic per distinct key.
+template <int BITS>
+__device__ __forceinline__ uint64_t peer_mask(uint32_t key) {
+  uint64_t peers = __ballot(1);
+#pragma unroll
+  for (int b = 0; b < BITS; b++) {
+    const uint64_t m = __ballot((key >> b) & 1u);
+    peers &= ((key >> b) & 1u) ? m : ~m;
+  }
+  return peers;
+}
+
+// Wave-aggregated cursor bump: returns the old cursor value + this lane's rank
+// among its peers (same result as one atomicAdd(cur + key, 1) per lane).
+template <int BITS>
+__device__ __forceinline__ uint32_t cursor_bump(uint32_t *cur, uint32_t key, uint32_t lane) {
+  const uint64_t peers = peer_mask<BITS>(key);
+  const uint32_t rank = (uint32_t)__popcll(peers & ((1ull << lane) - 1));
+  const uint32_t leader = (uint32_t)__builtin_ctzll(peers);
+  uint32_t base = 0;
+  if (rank == 0) base = atomicAdd(cur + key, (uint32_t)__popcll(peers));
+  base = (uint32_t)__shfl((int)base, (int)leader, 64);
+  return base + rank;
+}
+
+__device__ __forceinline__ void part_entries(const PostingParams &p, uint32_t *bcur, uint32_t rmask, uint64_t bb,
+                                             const InvGroup &g, uint64_t dd, uint32_t d0l, uint32_t stride,
+                                             const uint32_t *c, const uint32_t *t, bool *tf_big) {
+  const uint32_t lane = threadIdx.x & 63;
+  constexpr uint32_t kNoop = kRangeSlots / kSubSlots;       // idle lanes bump a spare cursor
 #pragma unroll
   for (int j = 0; j < kInvDocs; j++) {
-    if (c[j] != kInvalidSlot) {
-      *tf_big |= t[j] > kMaxTf;
-      const uint64_t d = dd + (uint64_t)stride * j;
-      const uint64_t val = (uint64_t)(uint32_t)d | ((uint64_t)((t[j] << 8) | g.nrm[j]) << 32);
-      const uint64_t pos = bb + atomicAdd(&cur[c[j] & rmask], 1u);
-      if (p.debug_scatter != 2) p.post[pos] = val;
-    }
+    const bool in = c[j] != kInvalidSlot;
+    if (!__any(in)) continue;                                 // wave-uniform
+    *tf_big |= in && t[j] > kMaxTf;
+    const uint32_t sl = c[j] & rmask;
+    const uint32_t dl = (uint32_t)(dd + (uint64_t)stride * j) - d0l;
+    const uint64_t val = (uint64_t)dl | ((uint64_t)(sl & (kSubSlots - 1)) << 13) |
+                         ((uint64_t)(t[j] & kMaxTf) << 23) | ((uint64_t)g.nrm[j] << 47);
+    const uint32_t pos = cursor_bump<kRangeBits - kSubBits + 1>(bcur, in ? sl >> kSubBits : kNoop, lane);
+    if (in) p.post_tmp[bb + pos] = val;
   }
 }
 
-__global__ void __launch_bounds__(1024) k_scatter(PostingParams p) {
-  extern __shared__ uint32_t cur[];
+__global__ void __launch_bounds__(1024) k_scatter_part(PostingParams p) {
+  __shared__ uint32_t bcur[kRangeSlots / kSubSlots + 1];
   const uint32_t lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   const uint32_t wid = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const uint32_t RS = 1u << p.range_shift;
-  const uint32_t rmask = RS - 1;
+  const uint32_t b = blockIdx.x, r = blockIdx.y;
+  const uint32_t RS = 1u << p.range_shift, rmask = RS - 1;
+  const uint32_t nsub = RS > kSubSlots ? RS / kSubSlots : 1u;
+  const uint32_t *row = p.blk + (size_t)b * p.C + ((size_t)r << p.range_shift);
+  if (threadIdx.x < nsub) bcur[threadIdx.x] = row[threadIdx.x * kSubSlots];
+  __syncthreads();
+  const uint64_t bb = p.bbase[b];
+  const uint64_t d0 = (uint64_t)b * kBlockDocs;
+  const uint64_t d1 = d0 + kBlockDocs < p.n_docs ? d0 + kBlockDocs : p.n_docs;
+  const uint64_t step = (uint64_t)nw * kInvDocs;
   bool tf_big = false;
-  for (uint32_t tile = blockIdx.x; tile < p.n_blocks * p.n_ranges; tile += gridDim.x) {
-    const uint32_t b = tile / p.n_ranges, r = tile % p.n_ranges;
-    __syncthreads();
-    const size_t g0 = (size_t)r << p.range_shift;
-    const uint32_t *row = p.blk + (size_t)b * p.C + g0;
-    const uint64_t bb = p.bbase[b];
-    for (uint32_t i = threadIdx.x; i < RS; i += blockDim.x) cur[i] = row[i];
-    __syncthreads();
-    const uint64_t d0 = (uint64_t)b * kBlockDocs;
-    const uint64_t d1 = d0 + kBlockDocs < p.n_docs ? d0 + kBlockDocs : p.n_docs;
-    const uint64_t step = (uint64_t)nw * kInvDocs;
-    uint64_t dd = d0 + wid;
-    InvGroup g = inv_group(p, dd, d1, nw, r, true);
-    uint32_t c[kInvDocs], t[kInvDocs];
-    if (dd < d1) inv_load(p, g, lane, c, t, true);
-    while (dd < d1) {
-      const uint64_t dn = dd + step;
-      const InvGroup gn = inv_group(p, dn, d1, nw, r, true);
-      uint32_t cn[kInvDocs], tn[kInvDocs];
-      if (dn < d1) inv_load(p, gn, lane, cn, tn, true);           // next group in flight
-      scatter_entries(p, cur, rmask, bb, g, dd, nw, c, t, &tf_big);
-      for (uint32_t off = lane + 64; off < g.maxn; off += 64) {    // segments longer than 64
-        inv_load(p, g, off, c, t, true);
-        scatter_entries(p, cur, rmask, bb, g, dd, nw, c, t, &tf_big);
-      }
-      g = gn;
-#pragma unroll
-      for (int j = 0; j < kInvDocs; j++) { c[j] = cn[j]; t[j] = tn[j]; }
-      dd = dn;
+  uint64_t dd = d0 + wid;
+  InvGroup g = inv_group(p, dd, d1, nw, r, true);
+  uint32_t c[kInvDocs], t[kInvDocs];
+  if (dd < d1) inv_load(p, g, lane, c, t, true);
+  while (dd < d1) {
+    const uint64_t dn = dd + step;
+    const InvGroup gn = inv_group(p, dn, d1, nw, r, true);
+    uint32_t cn[kInvDocs], tn[kInvDocs];
+    if (dn < d1) inv_load(p, gn, lane, cn, tn, true);           // next group in flight
+    part_entries(p, bcur, rmask, bb, g, dd, (uint32_t)d0, nw, c, t, &tf_big);
+    for (uint32_t off = lane + 64; off < g.maxn; off += 64) {    // segments longer than 64
+      inv_load(p, g, off, c, t, true);
+      part_entries(p, bcur, rmask, bb, g, dd, (uint32_t)d0, nw, c, t, &tf_big);
     }
+    g = gn;
+#pragma unroll
+    for (int j = 0; j < kInvDocs; j++) { c[j] = cn[j]; t[j] = tn[j]; }
+    dd = dn;
   }
   if (tf_big) atomicOr(p.err, kErrTfTooLarge);
+}
+
+// grid (n_blocks, n_ranges, streams per range), 1024 threads: few streams per
+// CU at a time, so the regions being written stay L2-resident
+__global__ void __launch_bounds__(1024) k_scatter_sort(PostingParams p) {
+  __shared__ uint32_t cur[kSubSlots + 1];                   // + no-op cursor for idle lanes
+  const uint32_t b = blockIdx.x, r = blockIdx.y, k = blockIdx.z;
+  const uint32_t RS = 1u << p.range_shift;
+  const uint32_t BS = RS < kSubSlots ? RS : kSubSlots;
+  const size_t s0 = ((size_t)r << p.range_shift) + (size_t)k * BS;
+  const uint32_t *row = p.blk + (size_t)b * p.C;
+  const uint64_t bb = p.bbase[b];
+  for (uint32_t i = threadIdx.x; i < BS; i += blockDim.x) cur[i] = row[s0 + i];
+  const uint32_t lo = row[s0];
+  const uint32_t hi = s0 + BS < p.C ? row[s0 + BS] : (uint32_t)(p.bbase[b + 1] - bb);
+  __syncthreads();
+  const uint32_t d0 = b * kBlockDocs;
+  const uint32_t lane = threadIdx.x & 63;
+  constexpr int U = 4;                                       // entries per thread in flight
+  for (uint32_t e0 = lo; e0 < hi; e0 += U * blockDim.x) {   // uniform trip count: all lanes ballot
+    uint64_t x[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t e = e0 + u * blockDim.x + threadIdx.x;
+      x[u] = e < hi ? p.post_tmp[bb + e] : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t e = e0 + u * blockDim.x + threadIdx.x;
+      if (__all(e >= hi)) break;
+      const bool in = e < hi;
+      const uint32_t sl = in ? (uint32_t)(x[u] >> 13) & (kSubSlots - 1) : kSubSlots;   // kSubSlots: no-op key
+      const uint32_t pos = cursor_bump<kSubBits + 1>(cur, sl, lane);
+      const uint32_t tf = (uint32_t)(x[u] >> 23) & kMaxTf, nrm = (uint32_t)(x[u] >> 47) & 0xFFu;
+      if (in)
+        p.post[bb + pos] = (uint64_t)(d0 + ((uint32_t)x[u] & (kBlockDocs - 1))) | ((uint64_t)((tf << 8) | nrm) << 32);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1501,7 +1577,6 @@ static void allow_big_lds() {
   static bool done = false;
   if (done) return;
   hipFuncSetAttribute((const void *)k_df_partial, hipFuncAttributeMaxDynamicSharedMemorySize, 4 << kRangeBits);
-  hipFuncSetAttribute((const void *)k_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, 4 << kRangeBits);
   done = true;
 }
 
@@ -1524,11 +1599,12 @@ hipError_t launch_block_base(const PostingParams &p, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t launch_scatter(const PostingParams &p, hipStream_t s) {
-  allow_big_lds();
-  const size_t lds = sizeof(uint32_t) << p.range_shift;
-  const uint32_t tiles = p.n_blocks * p.n_ranges;
-  const uint32_t grid = p.scatter_wgs ? std::min(p.scatter_wgs, tiles) : tiles;
-  hipLaunchKernelGGL(k_scatter, dim3(grid), dim3(1024), lds, s, p);
+  hipLaunchKernelGGL(k_scatter_part, dim3(p.n_blocks, p.n_ranges), dim3(1024), 0, s, p);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const uint32_t RS = 1u << p.range_shift;
+  const uint32_t nsub = RS > kSubSlots ? RS / kSubSlots : 1u;
+  hipLaunchKernelGGL(k_scatter_sort, dim3(p.n_blocks, p.n_ranges, nsub), dim3(1024), 0, s, p);
   return hipGetLastError();
 }
 

@@ -118,7 +118,7 @@ struct tfidf_index {
   std::vector<uint32_t> live_map;  // committed -> staged (empty = identity)
   DevBuf d_live_map;
   uint32_t cap_log2 = 18, C = 0, range_shift = 15, R = 1, n_blocks = 0;
-  DevBuf dict, csr_col, csr_tf, doc_len, doc_nuniq, doc_norm, rsplit, long_list, counters, blk, bbase, post;
+  DevBuf dict, csr_col, csr_tf, doc_len, doc_nuniq, doc_norm, rsplit, long_list, counters, blk, bbase, post, post_tmp;
   DevBuf lt_keys, lt_cnt, lt_g;
   uint32_t lt_log2 = 0, lt_wgs = 64;
   std::vector<uint64_t> h_dict;
@@ -188,7 +188,7 @@ extern "C" int tfidf_destroy(tfidf_index *ix) {
   hipStreamSynchronize(ix->stream);
   DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->d_live_map, &ix->dict, &ix->csr_col, &ix->csr_tf, &ix->doc_len,
                     &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->long_list, &ix->counters, &ix->blk,
-                    &ix->bbase, &ix->post, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->canon_of_slot,
+                    &ix->bbase, &ix->post, &ix->post_tmp, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->canon_of_slot,
                     &ix->q_off, &ix->q_slot, &ix->q_w, &ix->cache, &ix->cand, &ix->cand_n, &ix->out_doc,
                     &ix->out_score, &ix->out_n, &ix->hits, &ix->hits_n, &ix->hits_c, &ix->hits_s, &ix->sort_tmp};
   for (DevBuf *b : bufs) b->release();
@@ -478,6 +478,7 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   ix->nnz = hctr[2];
   if (ix->nnz >= 0xFFFFFFFFull) return fail(TFIDF_E_CAPACITY, "more than 2^32 postings per shard");
   HIP_TRY(ix->post.reserve(ix->nnz * 8 + 8));
+  HIP_TRY(ix->post_tmp.reserve(ix->nnz * 8 + 8));
 
   PostingParams pp{};
   pp.offsets = bp.offsets;
@@ -494,9 +495,8 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   pp.blk = ix->blk.as<uint32_t>();
   pp.bbase = ix->bbase.as<uint64_t>();
   pp.post = ix->post.as<uint64_t>();
+  pp.post_tmp = ix->post_tmp.as<uint64_t>();
   pp.err = bp.err;
-  if (const char *ds = getenv("TFIDF_DEBUG_SCATTER")) pp.debug_scatter = (uint32_t)atoi(ds);   // profiling only
-  if (const char *sw = getenv("TFIDF_SCATTER_WGS")) pp.scatter_wgs = (uint32_t)atoi(sw);       // profiling only
   HIP_TRY(hipEventRecord(ix->ev[EV_D0], s));
   if (ix->n_blocks) {
     HIP_TRY(launch_df_partial(pp, s));

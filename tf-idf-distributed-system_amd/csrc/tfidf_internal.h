@@ -68,9 +68,7 @@ struct PostingParams {
   uint64_t *post;             // [nnz]: doc | (tf << 8 | norm) << 32; block b, slot s at
                               // bbase[b] + blk[b][s]
   uint32_t *err;
-  uint32_t scatter_wgs;       // persistent scatter grid (0 = one workgroup per tile)
-  uint32_t debug_scatter;     // profiling only (TFIDF_DEBUG_SCATTER): 1 = CSR-order stores, no
-                              // cursor atomics; 2 = cursor atomics, no stores
+  uint64_t *post_tmp;         // [nnz] scatter pass 1 output (sub-range streams, same regions)
 };
 
 // --- launch wrappers (kernels_index.hip) ---
