@@ -2,15 +2,17 @@
 // reference, Worker.java:222-241: IndexSearcher.search(query, MAX) with
 // Lucene 9.8.0 BM25Similarity and TopScoreDocCollector), for gfx950.
 //
-//   score_blocks : grid (doc block, query).  For each query term (in query
-//                  order) the workgroup streams that term's posting segment
-//                  for the block (contiguous, coalesced u64 loads) and
-//                  computes  s = w - w / (1f + (float)tf * cache[norm])  in
-//                  float (no contraction), accumulating (double)s per doc in
-//                  LDS — the disjunction's double sum — then rounds once to
-//                  float.  Top-k within the block: 4-pass 8-bit radix select
-//                  on the float bits, ties resolved by ascending doc via a
-//                  block scan over the hit bitmap (HitQueue order).
+//   score_blocks : grid (doc block, query chunk); the workgroup scores the
+//                  chunk's queries one after another against its block,
+//                  reusing the LDS accumulator.  For each query term (in
+//                  query order) it streams that term's posting segment for
+//                  the block (contiguous, coalesced u64 loads) and computes
+//                  s = w - w / (1f + (float)tf * cache[norm])  in float (no
+//                  contraction), accumulating (double)s per doc in LDS — the
+//                  disjunction's double sum — then rounds once to float.
+//                  Top-k within the block: 4-pass 8-bit radix select on the
+//                  float bits, ties resolved by ascending doc via a block scan
+//                  over the hit bitmap (HitQueue order).
 //   merge_topk   : per query, radix select over all block candidates on the
 //                  64-bit key (score bits << 32 | ~doc), then a bitonic sort
 //                  in LDS -> (score desc, doc asc).
@@ -54,117 +56,205 @@ __device__ __forceinline__ float bm25_term(float w, uint32_t tf, float norm_inve
   return w - v;
 }
 
+// Radix-select step, run by one whole wave: over the 256-bin histogram taken
+// from the high bin down, find the bin where the running count first reaches
+// rem.  Returns the bin; *above = count in higher bins.  Lane l holds bins
+// 255-4l .. 252-4l; lane prefix by DPP-free shuffles (one wave).
+__device__ __forceinline__ uint32_t wave_select_bin(const uint32_t *hist, uint32_t rem, uint32_t *above) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t h[4], inc[4], run = 0;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    h[i] = hist[255 - (4 * lane + i)];
+    run += h[i];
+    inc[i] = run;                                   // lane-local inclusive
+  }
+  uint32_t x = run;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  const uint32_t base = x - run;                    // exclusive over lanes
+  int first = -1;
+#pragma unroll
+  for (int i = 3; i >= 0; i--)
+    if (base + inc[i] >= rem) first = i;
+  const uint64_t m = __ballot(first >= 0);
+  const uint32_t src = m ? (uint32_t)__builtin_ctzll(m) : 63u;
+  const uint32_t fi = (uint32_t)__shfl(first < 0 ? 0 : first, (int)src, 64);
+  uint32_t cum = base + (fi ? inc[fi - 1] : 0u);    // count in bins above the selected one
+  cum = (uint32_t)__shfl((int)cum, (int)src, 64);
+  *above = cum;
+  return 255u - (4u * src + fi);
+}
+
+constexpr uint32_t kQTermsFast = 4;   // query terms whose ranges / first chunk are prefetched
+
 struct ScoreSmem {
   double acc[kBlockDocs];
+  uint32_t tlo[kQTermsFast], thi[kQTermsFast];
+  float tw[kQTermsFast];
   uint32_t hitbits[kBlockDocs / 32];
-  uint16_t hitlist[kBlockDocs];
   float cache[256];
   uint32_t hist[256];
   uint32_t scan[16];
   uint32_t nhit, prefix, remaining, outn;
 };
 
+// Hits are enumerated from the bitmap: thread t owns docs [16 t, 16 t + 16)
+// (ascending doc order for ties).  The per-query set-up is a 1 KiB bitmap
+// clear, so a chunk of queries amortises the workgroup launch, and the LDS
+// footprint (66 KiB) admits two workgroups per CU.
 __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
   __shared__ ScoreSmem sm;
-  const uint32_t b = blockIdx.x, q = blockIdx.y, tid = threadIdx.x;
+  const uint32_t b = blockIdx.x, tid = threadIdx.x;
+  const uint32_t q0 = blockIdx.y * p.q_chunk;
+  const uint32_t q1 = min(p.n_q, q0 + p.q_chunk);
   const uint64_t d0 = (uint64_t)b * kBlockDocs;
-  for (uint32_t i = tid; i < kBlockDocs / 32; i += blockDim.x) sm.hitbits[i] = 0;
+  const uint64_t bb = p.bbase[b];
+  const uint64_t bend = p.bbase[b + 1];
+  const uint32_t *row = p.blk + (size_t)b * p.C;
   for (uint32_t i = tid; i < 256; i += blockDim.x) sm.cache[i] = p.cache[i];
-  if (tid == 0) { sm.nhit = 0; sm.outn = 0; }
-  __syncthreads();
-  const uint32_t t0 = p.q_off[q], t1 = p.q_off[q + 1];
-  for (uint32_t j = t0; j < t1; j++) {
-    const uint32_t slot = p.q_slot[j];
-    if (slot == kInvalidSlot) continue;                   // uniform
-    const float w = p.q_w[j];
-    const uint64_t bb = p.bbase[b];
-    const uint32_t *row = p.blk + (size_t)b * p.C;
-    const uint64_t lo = bb + row[slot];
-    const uint64_t hi = slot + 1 < p.C ? bb + row[slot + 1] : p.bbase[b + 1];
-    for (uint64_t i = lo + tid; i < hi; i += blockDim.x) {
-      const uint64_t e = p.post[i];
-      const uint32_t ld = (uint32_t)(e & 0xFFFFFFFFu) - (uint32_t)d0;
-      const uint32_t tfn = (uint32_t)(e >> 32);
-      const float s = bm25_term(w, tfn >> 8, sm.cache[tfn & 255u]);
-      const uint32_t bit = 1u << (ld & 31);
-      const uint32_t old = atomicOr(&sm.hitbits[ld >> 5], bit);
-      if (old & bit) {
-        sm.acc[ld] += (double)s;
-      } else {
-        sm.acc[ld] = (double)s;
-        sm.hitlist[atomicAdd(&sm.nhit, 1u)] = (uint16_t)ld;
-      }
-    }
-    __syncthreads();
-  }
-  const uint32_t nhit = sm.nhit;
   const uint32_t k = p.k;
-  if (k == 0) {
-    // all-hits mode: dump every hit key of the block
-    for (uint32_t i = tid; i < nhit; i += blockDim.x) {
-      const uint32_t ld = sm.hitlist[i];
-      const float sc = (float)sm.acc[ld];
-      p.hits[(size_t)b * kBlockDocs + i] =
-          ((uint64_t)__float_as_uint(sc) << 32) | (uint64_t)(~(uint32_t)(d0 + ld));
-    }
-    if (tid == 0) p.hits_n[b] = nhit;
-    return;
-  }
-  uint64_t *cand = p.cand + ((size_t)q * p.n_blocks + b) * k;
-  if (nhit <= k) {
-    for (uint32_t i = tid; i < nhit; i += blockDim.x) {
-      const uint32_t ld = sm.hitlist[i];
-      cand[i] = ((uint64_t)__float_as_uint((float)sm.acc[ld]) << 32) | (uint64_t)(~(uint32_t)(d0 + ld));
-    }
-    if (tid == 0) p.cand_n[(size_t)q * p.n_blocks + b] = nhit;
-    return;
-  }
-  // radix select: threshold T = k-th largest score bits
-  if (tid == 0) { sm.prefix = 0; sm.remaining = k; }
-  for (int pass = 0; pass < 4; pass++) {
-    const int sh = 24 - 8 * pass;
-    for (uint32_t i = tid; i < 256; i += blockDim.x) sm.hist[i] = 0;
+  for (uint32_t q = q0; q < q1; q++) {
+    for (uint32_t i = tid; i < kBlockDocs / 32; i += blockDim.x) sm.hitbits[i] = 0;
+    if (tid == 0) { sm.nhit = 0; sm.outn = 0; }
     __syncthreads();
-    const uint32_t prefix = sm.prefix;
-    const uint32_t hmask = pass == 0 ? 0u : (0xFFFFFFFFu << (sh + 8));
-    for (uint32_t i = tid; i < nhit; i += blockDim.x) {
-      const uint32_t sb = __float_as_uint((float)sm.acc[sm.hitlist[i]]);
-      if ((sb & hmask) == (prefix & hmask)) atomicAdd(&sm.hist[(sb >> sh) & 255u], 1u);
-    }
-    __syncthreads();
-    if (tid == 0) {
-      uint32_t rem = sm.remaining, cum = 0;
-      for (int bin = 255; bin >= 0; bin--) {
-        const uint32_t h = sm.hist[bin];
-        if (cum + h >= rem) {
-          sm.prefix = prefix | ((uint32_t)bin << sh);
-          sm.remaining = rem - cum;
-          break;
-        }
-        cum += h;
+    const uint32_t t0 = p.q_off[q], t1 = p.q_off[q + 1];
+    // all terms' posting ranges in one round trip (thread j fetches term j)
+    if (tid < t1 - t0 && tid < kQTermsFast) {
+      const uint32_t slot = p.q_slot[t0 + tid];
+      uint32_t a = 0, z = 0;
+      if (slot != kInvalidSlot) {
+        a = row[slot];
+        z = slot + 1 < p.C ? row[slot + 1] : (uint32_t)(bend - bb);
       }
+      sm.tlo[tid] = a;
+      sm.thi[tid] = z;
+      sm.tw[tid] = p.q_w[t0 + tid];
     }
     __syncthreads();
+    // first chunk of every term's postings in flight before any is consumed
+    uint64_t pre[kQTermsFast];
+#pragma unroll
+    for (uint32_t j = 0; j < kQTermsFast; j++) {
+      pre[j] = 0;
+      if (j < t1 - t0 && sm.tlo[j] + tid < sm.thi[j]) pre[j] = p.post[bb + sm.tlo[j] + tid];
+    }
+    uint32_t my_new = 0;
+    for (uint32_t j = t0; j < t1; j++) {
+      const uint32_t jj = j - t0;
+      uint64_t lo, hi;
+      float w;
+      if (jj < kQTermsFast) {
+        lo = bb + sm.tlo[jj];
+        hi = bb + sm.thi[jj];
+        w = sm.tw[jj];
+      } else {
+        const uint32_t slot = p.q_slot[j];
+        if (slot == kInvalidSlot) continue;               // uniform
+        w = p.q_w[j];
+        lo = bb + row[slot];
+        hi = slot + 1 < p.C ? bb + row[slot + 1] : bend;
+      }
+      for (uint64_t i = lo + tid; i < hi; i += blockDim.x) {
+        uint64_t e;
+        if (jj < kQTermsFast && i == lo + tid) {
+#pragma unroll
+          for (uint32_t u = 0; u < kQTermsFast; u++)
+            if (u == jj) e = pre[u];
+        } else {
+          e = p.post[i];
+        }
+        const uint32_t ld = (uint32_t)(e & 0xFFFFFFFFu) - (uint32_t)d0;
+        const uint32_t tfn = (uint32_t)(e >> 32);
+        const float sc = bm25_term(w, tfn >> 8, sm.cache[tfn & 255u]);
+        const uint32_t bit = 1u << (ld & 31);
+        const uint32_t old = atomicOr(&sm.hitbits[ld >> 5], bit);
+        if (old & bit) {
+          sm.acc[ld] += (double)sc;
+        } else {
+          sm.acc[ld] = (double)sc;
+          my_new++;
+        }
+      }
+      __syncthreads();                                     // term order = the disjunction's sum order
+    }
+    if (my_new) atomicAdd(&sm.nhit, my_new);
+    __syncthreads();
+    const uint32_t nhit = sm.nhit;
+    const uint32_t bits = (sm.hitbits[tid >> 1] >> (16 * (tid & 1))) & 0xFFFFu;
+    if (k == 0) {
+      // all-hits mode (single query): every hit key of the block
+      uint32_t tot;
+      uint32_t at = block_excl_scan((uint32_t)__popc(bits), sm.scan, &tot);
+      for (uint32_t x = bits; x; x &= x - 1) {
+        const uint32_t ld = tid * kDocsPerThread + (__ffs(x) - 1);
+        const float sc = (float)sm.acc[ld];
+        p.hits[(size_t)b * kBlockDocs + at++] =
+            ((uint64_t)__float_as_uint(sc) << 32) | (uint64_t)(~(uint32_t)(d0 + ld));
+      }
+      if (tid == 0) p.hits_n[b] = nhit;
+      __syncthreads();
+      continue;
+    }
+    uint64_t *cand = p.cand + ((size_t)q * p.n_blocks + b) * k;
+    if (nhit <= k) {
+      uint32_t tot;
+      uint32_t at = block_excl_scan((uint32_t)__popc(bits), sm.scan, &tot);
+      for (uint32_t x = bits; x; x &= x - 1) {
+        const uint32_t ld = tid * kDocsPerThread + (__ffs(x) - 1);
+        cand[at++] = ((uint64_t)__float_as_uint((float)sm.acc[ld]) << 32) | (uint64_t)(~(uint32_t)(d0 + ld));
+      }
+      if (tid == 0) p.cand_n[(size_t)q * p.n_blocks + b] = nhit;
+      __syncthreads();
+      continue;
+    }
+    // radix select: threshold T = k-th largest score bits
+    if (tid == 0) { sm.prefix = 0; sm.remaining = k; }
+    for (int pass = 0; pass < 4; pass++) {
+      const int sh = 24 - 8 * pass;
+      for (uint32_t i = tid; i < 256; i += blockDim.x) sm.hist[i] = 0;
+      __syncthreads();
+      const uint32_t prefix = sm.prefix;
+      const uint32_t hmask = pass == 0 ? 0u : (0xFFFFFFFFu << (sh + 8));
+      for (uint32_t x = bits; x; x &= x - 1) {
+        const uint32_t sb = __float_as_uint((float)sm.acc[tid * kDocsPerThread + (__ffs(x) - 1)]);
+        if ((sb & hmask) == (prefix & hmask)) atomicAdd(&sm.hist[(sb >> sh) & 255u], 1u);
+      }
+      __syncthreads();
+      if (tid < 64) {
+        const uint32_t rem = sm.remaining;
+        uint32_t above;
+        const uint32_t bin = wave_select_bin(sm.hist, rem, &above);
+        if (tid == 0) {
+          sm.prefix = prefix | (bin << sh);
+          sm.remaining = rem - above;
+        }
+      }
+      __syncthreads();
+    }
+    const uint32_t T = sm.prefix, take_ties = sm.remaining;
+    // collection in ascending doc order
+    uint32_t nties = 0;
+    for (uint32_t x = bits; x; x &= x - 1) {
+      const uint32_t ld = tid * kDocsPerThread + (__ffs(x) - 1);
+      nties += __float_as_uint((float)sm.acc[ld]) == T;
+    }
+    uint32_t tot;
+    uint32_t tie_rank = block_excl_scan(nties, sm.scan, &tot);
+    for (uint32_t x = bits; x; x &= x - 1) {
+      const uint32_t ld = tid * kDocsPerThread + (__ffs(x) - 1);
+      const uint32_t sb = __float_as_uint((float)sm.acc[ld]);
+      bool take = sb > T;
+      if (sb == T) take = tie_rank++ < take_ties;
+      if (take) cand[atomicAdd(&sm.outn, 1u)] = ((uint64_t)sb << 32) | (uint64_t)(~(uint32_t)(d0 + ld));
+    }
+    __syncthreads();
+    if (tid == 0) p.cand_n[(size_t)q * p.n_blocks + b] = sm.outn;
+    __syncthreads();
   }
-  const uint32_t T = sm.prefix, take_ties = sm.remaining;
-  // collection in ascending doc order: thread owns docs [16 tid, 16 tid + 16)
-  const uint32_t bits = (sm.hitbits[tid >> 1] >> (16 * (tid & 1))) & 0xFFFFu;
-  uint32_t nties = 0;
-  for (uint32_t x = bits; x; x &= x - 1) {
-    const uint32_t ld = tid * kDocsPerThread + (__ffs(x) - 1);
-    nties += __float_as_uint((float)sm.acc[ld]) == T;
-  }
-  uint32_t tot;
-  uint32_t tie_rank = block_excl_scan(nties, sm.scan, &tot);
-  for (uint32_t x = bits; x; x &= x - 1) {
-    const uint32_t ld = tid * kDocsPerThread + (__ffs(x) - 1);
-    const uint32_t sb = __float_as_uint((float)sm.acc[ld]);
-    bool take = sb > T;
-    if (sb == T) take = tie_rank++ < take_ties;
-    if (take) cand[atomicAdd(&sm.outn, 1u)] = ((uint64_t)sb << 32) | (uint64_t)(~(uint32_t)(d0 + ld));
-  }
-  __syncthreads();
-  if (tid == 0) p.cand_n[(size_t)q * p.n_blocks + b] = sm.outn;
 }
 
 // One workgroup (1024 threads) per query.
@@ -202,16 +292,13 @@ __global__ void __launch_bounds__(1024) k_merge_topk(QueryParams p) {
         }
       }
       __syncthreads();
-      if (tid == 0) {
-        uint32_t rem = sm.remaining, cum = 0;
-        for (int bin = 255; bin >= 0; bin--) {
-          const uint32_t h = sm.hist[bin];
-          if (cum + h >= rem) {
-            sm.prefix = prefix | ((uint64_t)bin << sh);
-            sm.remaining = rem - cum;
-            break;
-          }
-          cum += h;
+      if (tid < 64) {
+        const uint32_t rem = sm.remaining;
+        uint32_t above;
+        const uint32_t bin = wave_select_bin(sm.hist, rem, &above);
+        if (tid == 0) {
+          sm.prefix = prefix | ((uint64_t)bin << sh);
+          sm.remaining = rem - above;
         }
       }
       __syncthreads();
@@ -256,7 +343,8 @@ __global__ void __launch_bounds__(1024) k_merge_topk(QueryParams p) {
 }
 
 hipError_t launch_score_blocks(const QueryParams &p, hipStream_t s) {
-  hipLaunchKernelGGL(k_score_blocks, dim3(p.n_blocks, p.n_q), dim3(kScoreThreads), 0, s, p);
+  const uint32_t chunks = (p.n_q + p.q_chunk - 1) / p.q_chunk;
+  hipLaunchKernelGGL(k_score_blocks, dim3(p.n_blocks, chunks), dim3(kScoreThreads), 0, s, p);
   return hipGetLastError();
 }
 hipError_t launch_merge_topk(const QueryParams &p, hipStream_t s) {

@@ -634,6 +634,12 @@ static int run_scoring(tfidf_index *ix, const std::vector<uint32_t> &qoff, const
   qp.q_w = ix->q_w.as<float>();
   qp.n_q = n_q;
   qp.k = k;
+  {   // enough (block, chunk) workgroups to fill the chip ~4 deep; never more chunks than queries
+    const uint32_t want = (uint32_t)ix->num_cus * 4;
+    uint32_t chunks = ix->n_blocks ? (want + ix->n_blocks - 1) / ix->n_blocks : 1;
+    chunks = std::max(1u, std::min(chunks, n_q));
+    qp.q_chunk = (n_q + chunks - 1) / chunks;
+  }
   if (k) {
     HIP_TRY(ix->cand.reserve((size_t)n_q * ix->n_blocks * k * 8 + 8));
     HIP_TRY(ix->cand_n.reserve((size_t)n_q * ix->n_blocks * 4 + 4));

@@ -94,6 +94,7 @@ struct QueryParams {
   const uint32_t *q_slot;     // dictionary slot per query term (kInvalidSlot = absent)
   const float *q_w;           // BM25 weight per query term (boost * idf)
   uint32_t n_q;
+  uint32_t q_chunk;           // queries per score_blocks workgroup
   uint32_t k;                 // top-k (1..1024); 0 = all hits
   // outputs
   uint64_t *cand;             // [n_q][n_blocks][k] candidate keys (score bits << 32 | ~doc)
