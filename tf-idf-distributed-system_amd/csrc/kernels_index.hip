@@ -1271,20 +1271,32 @@ struct InvGroup {               // wave-uniform
   uint32_t maxn;
 };
 
+// Group metadata, loaded lane-parallel (lane j < kInvDocs fetches document j:
+// one round trip for the whole group instead of a dependent scalar chain per
+// document) and broadcast with readlane.
 __device__ __forceinline__ InvGroup inv_group(const PostingParams &p, uint64_t dd, uint64_t d1, uint32_t stride,
                                               uint32_t r, bool with_norm) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t d = dd + (uint64_t)stride * (lane & (kInvDocs - 1));
+  const bool ok = lane < (uint32_t)kInvDocs && d < d1;
+  uint64_t base = 0;
+  uint32_t lo = 0, hi = 0, nrm = 0;
+  if (ok) {
+    const uint64_t src = p.live_map ? p.live_map[d] : d;
+    base = csr_row_base(p.offsets, src);
+    lo = r ? p.rsplit[d * p.n_ranges + r - 1] : 0;
+    hi = p.rsplit[d * p.n_ranges + r];
+    if (with_norm) nrm = p.doc_norm[d];
+  }
   InvGroup g;
   g.maxn = 0;
 #pragma unroll
   for (int j = 0; j < kInvDocs; j++) {
-    const uint64_t d = dd + (uint64_t)stride * j;
-    g.lo[j] = g.hi[j] = 0;
-    g.base[j] = 0;
-    g.nrm[j] = 0;
-    if (d < d1) {
-      doc_segment(p, d, r, &g.base[j], &g.lo[j], &g.hi[j]);
-      if (with_norm) g.nrm[j] = p.doc_norm[d];
-    }
+    g.base[j] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(base >> 32), j) << 32) |
+                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)base, j);
+    g.lo[j] = (uint32_t)__builtin_amdgcn_readlane((int)lo, j);
+    g.hi[j] = (uint32_t)__builtin_amdgcn_readlane((int)hi, j);
+    g.nrm[j] = (uint32_t)__builtin_amdgcn_readlane((int)nrm, j);
     g.maxn = max(g.maxn, g.hi[j] - g.lo[j]);
   }
   return g;
