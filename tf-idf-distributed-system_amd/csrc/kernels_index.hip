@@ -434,10 +434,10 @@ __device__ __forceinline__ void token_key(const uint8_t *text, uint32_t s, uint3
 //               running past the lane ends at the next lane's first end
 //               (ballot + one cross-lane read).  Spans are compacted into a
 //               dense LDS list (wave scan of per-lane counts)
-//   histogram : lane l keys tokens l + 64k (k < kWaveK, all in flight) and
-//               counts them in the LDS table with returning 64-bit CASes; after
-//               kWaveFastRounds probe rounds the few unresolved tokens move to
-//               a one-per-lane retry queue
+//   histogram : batches of 64K tokens (K = 8, 4 or 2 by what is left); lane l
+//               keys tokens l + 64k (all in flight) and counts them in the LDS
+//               table with returning 64-bit CASes; once <= 128 tokens are
+//               unresolved they move to a two-per-lane retry queue
 //   dictionary: occupied table slots are compacted into a dense list; lane l
 //               resolves terms l + 64k to global dictionary slots (all loads in
 //               flight), unresolved ones through a one-per-lane retry queue
@@ -457,8 +457,8 @@ constexpr uint32_t kWaveSlotBits = 10;
 constexpr uint32_t kWaveTokens = 1024;            // token list capacity
 constexpr uint32_t kWaveK = 8;                    // tokens / terms per lane in flight
 constexpr uint32_t kWaveTerms = 64 * kWaveK;      // distinct terms per document (wave path)
-constexpr uint32_t kWaveQueue = 64;               // retry queues: one entry per lane
-constexpr uint32_t kWaveFastRounds = 2;
+constexpr uint32_t kWaveQueue = 128;              // histogram retry queue: two entries per lane
+constexpr uint32_t kDictQueue = 64;               // dictionary retry queue: one entry per lane
 constexpr uint64_t kFoldBit = 1ull << 63;
 constexpr uint64_t kFoldPosMask = 0x1FFFull << 13;
 constexpr uint32_t kLookupPending = 0xFFFFFFFEu;
@@ -592,9 +592,9 @@ __device__ __forceinline__ uint32_t bucket_probe(ulonglong2 e, uint32_t s, uint6
   const bool odd = (s & 1u) != 0;
   const uint64_t v0 = odd ? e.y : e.x;
   const bool f0 = v0 == lo, z0 = v0 == 0;
-  const bool f1 = !odd && e.y == lo, z1 = !odd && e.y == 0;
-  const bool hit = f0 || (!z0 && f1);
-  const bool cl = z0 || (!f0 && !f1 && z1);
+  const bool f1 = !odd & (e.y == lo), z1 = !odd & (e.y == 0);
+  const bool hit = f0 | (!z0 & f1);
+  const bool cl = z0 | (!f0 & !f1 & z1);
   *claim = cl ? (z0 ? s : s + 1) : kInvalidSlot;
   return hit ? (f0 ? s : s + 1) : kLookupPending;
 }
@@ -677,6 +677,156 @@ __device__ __forceinline__ void clear_table(WaveSmem &sm, uint32_t lane) {
   for (int q = 0; q < (int)(kWaveSlots * 2 / 16 / 64); q++) cw[lane + 64 * q] = make_uint4(0, 0, 0, 0);
 }
 
+// One batch of the per-document histogram: lane l keys tokens tb + l + 64k
+// (k < K) of the token list, all LDS reads in flight, then probe rounds over
+// the table (branch-free: idle lanes CAS a no-op slot), then a retry queue of
+// two entries per lane once few tokens are left.
+template <int K>
+__device__ __forceinline__ void hist_batch(WaveSmem &sm, const BuildParams &p, uint64_t d, uint32_t lane, uint32_t tb,
+                                           uint32_t ntok, bool under, unsigned long long *noop, uint32_t &claims,
+                                           uint32_t &toks, bool &overflow) {
+  const uint32_t *tw = reinterpret_cast<const uint32_t *>(sm.text);
+  uint64_t tkey[K];
+  uint32_t slot[K];
+  uint32_t pendm = 0, longm = 0;
+  // keys of <= 8 bytes: all list reads, then all text reads, then the math
+  uint32_t ent[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const uint32_t idx = tb + lane + 64 * k;
+    ent[k] = sm.list[idx < ntok ? idx : 0u];
+  }
+  uint32_t dw[K][3];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const uint32_t a0 = (ent[k] & 0xFFFFu) >> 2;
+    dw[k][0] = tw[a0]; dw[k][1] = tw[a0 + 1]; dw[k][2] = tw[a0 + 2];
+  }
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const bool in = tb + lane + 64 * k < ntok;
+    const uint32_t tp = ent[k] & 0xFFFFu, n = (ent[k] >> 16) - tp, o = tp & 3;
+    const uint64_t m64 = n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1);
+    const uint32_t t0 = __builtin_amdgcn_alignbyte(dw[k][1], dw[k][0], o) & (uint32_t)m64;
+    const uint32_t t1 = __builtin_amdgcn_alignbyte(dw[k][2], dw[k][1], o) & (uint32_t)(m64 >> 32);
+    const bool valid =
+        !under | ((((t0 ^ 0x5F5F5F5Fu) & (uint32_t)m64) | ((t1 ^ 0x5F5F5F5Fu) & (uint32_t)(m64 >> 32))) != 0);
+    const uint32_t l0 = lower4(t0), l1 = lower4(t1);
+    tkey[k] = (uint64_t)l0 | ((uint64_t)l1 << 32);
+    slot[k] = ((l0 ^ rotl32(l1, 16)) * 0x85EBCA77u) >> (32 - kWaveSlotBits);
+    pendm |= (uint32_t)(in & (n <= 8) & valid) << k;
+    longm |= (uint32_t)(in & (n > 8)) << k;
+  }
+  if (__any(longm != 0)) {                               // tokens of 9..255 bytes: folded keys
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      if ((longm >> k) & 1u) {
+        const uint32_t e = sm.list[tb + lane + 64 * k];
+        const uint32_t tp = e & 0xFFFFu, n = (e >> 16) - tp;
+        if (n > kMaxTokenLen) {
+          set_err(p.err, kErrTokenTooLong, (uint32_t)d);
+        } else {
+          uint32_t h;
+          bool valid;
+          tkey[k] = fold_key(sm.text, tp, n, &h, &valid);
+          slot[k] = h >> (32 - kWaveSlotBits);
+          pendm |= (uint32_t)valid << k;
+        }
+      }
+    }
+  }
+  toks += (uint32_t)__popc(pendm);
+  for (uint32_t round = 0;; round++) {
+    const uint32_t np = (uint32_t)__popc(pendm);
+    const uint32_t pincl = wave_incl_add(np);
+    const uint32_t P = (uint32_t)__builtin_amdgcn_readlane((int)pincl, 63);
+    if (P == 0) return;
+    if (round >= kWaveSlots) { overflow = true; return; }
+    if ((round >= 1 && P <= kWaveQueue) || K <= 2) {
+      // retry queue: two unresolved tokens per lane, probed until resolved
+      uint32_t at = pincl - np;
+#pragma unroll
+      for (int k = 0; k < K; k++)
+        if ((pendm >> k) & 1u) { sm.qkey[at] = tkey[k]; sm.qslot[at] = (uint16_t)slot[k]; at++; }
+      asm volatile("" ::: "memory");
+      if (P > kWaveQueue) { overflow = true; return; }     // cannot happen for K <= 2
+      uint64_t qk[2];
+      uint32_t qs[2];
+      bool qp[2];
+#pragma unroll
+      for (int i = 0; i < 2; i++) {
+        const uint32_t idx = lane + 64 * i;
+        qp[i] = idx < P;
+        qk[i] = qp[i] ? sm.qkey[idx] : 0ull;
+        qs[i] = qp[i] ? sm.qslot[idx] : 0u;
+      }
+      for (uint32_t it = 0; __any(qp[0] | qp[1]); it++) {
+        if (it >= kWaveSlots) { overflow = true; return; }
+        uint64_t old[2];
+#pragma unroll
+        for (int i = 0; i < 2; i++)
+          old[i] = atomicCAS(qp[i] ? reinterpret_cast<unsigned long long *>(&sm.key[qs[i]]) : noop,
+                             qp[i] ? 0ull : ~0ull, (unsigned long long)qk[i]);
+#pragma unroll
+        for (int i = 0; i < 2; i++) {
+          bool hit = qp[i] & ((old[i] == 0) | (old[i] == qk[i]));
+          const bool fc = qp[i] & !hit & (((old[i] & qk[i]) >> 63) != 0) &
+                          (((old[i] ^ qk[i]) & ~kFoldPosMask) == 0);
+          if (fc)
+            hit = span_same(sm.text, (uint32_t)(old[i] >> 13) & 0x1FFFu, (uint32_t)(qk[i] >> 13) & 0x1FFFu,
+                            (uint32_t)qk[i] & 0xFFu);
+          atomicAdd(hit ? &sm.cnt[qs[i] >> 1] : reinterpret_cast<uint32_t *>(noop),
+                    hit ? 1u << (16 * (qs[i] & 1)) : 0u);
+          claims += (uint32_t)(hit & (old[i] == 0));
+          const bool adv = qp[i] & !hit;
+          qs[i] = adv ? ((qs[i] + 1) & (kWaveSlots - 1)) : qs[i];
+          qp[i] = adv;
+        }
+      }
+      return;
+    }
+    // one probe round for every pending token (no-op CAS for the others)
+    uint64_t old[K];
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const bool pend = (pendm >> k) & 1u;
+      old[k] = atomicCAS(pend ? reinterpret_cast<unsigned long long *>(&sm.key[slot[k]]) : noop,
+                         pend ? 0ull : ~0ull, (unsigned long long)tkey[k]);
+    }
+    uint32_t foldm = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const bool pend = (pendm >> k) & 1u;
+      const bool z = old[k] == 0;
+      const bool hit = pend & (z | (old[k] == tkey[k]));
+      atomicAdd(hit ? &sm.cnt[slot[k] >> 1] : reinterpret_cast<uint32_t *>(noop),
+                hit ? 1u << (16 * (slot[k] & 1)) : 0u);
+      claims += (uint32_t)(hit & z);
+      pendm &= ~((uint32_t)hit << k);
+      // same folded hash, other position: exact compare below (always false without long tokens)
+      const bool fc = pend & !hit & (((old[k] & tkey[k]) >> 63) != 0) &
+                      (((old[k] ^ tkey[k]) & ~kFoldPosMask) == 0);
+      foldm |= (uint32_t)fc << k;
+      const bool adv = pend & !hit & !fc;
+      slot[k] = adv ? ((slot[k] + 1) & (kWaveSlots - 1)) : slot[k];
+    }
+    if (__any(foldm != 0)) {                              // same length and hash: compare bytes
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        if ((foldm >> k) & 1u) {
+          if (span_same(sm.text, (uint32_t)(old[k] >> 13) & 0x1FFFu, (uint32_t)(tkey[k] >> 13) & 0x1FFFu,
+                        (uint32_t)tkey[k] & 0xFFu)) {
+            atomicAdd(&sm.cnt[slot[k] >> 1], 1u << (16 * (slot[k] & 1)));
+            pendm &= ~(1u << k);
+          } else {
+            slot[k] = (slot[k] + 1) & (kWaveSlots - 1);
+          }
+        }
+      }
+    }
+  }
+}
+
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_tokenize_wave(BuildParams p) {
   __shared__ WaveSmem sm;
   const uint32_t lane = threadIdx.x;
@@ -693,7 +843,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   const uint32_t dmask = p.cap_mask;
   uint16_t *slots = reinterpret_cast<uint16_t *>(sm.list);
   unsigned long long *noop = reinterpret_cast<unsigned long long *>(&sm.noop[lane]);
-  const uint32_t *tw = reinterpret_cast<const uint32_t *>(sm.text);
 
   for (uint64_t d = blockIdx.x; d < p.n_docs; d += gridDim.x) {
     const uint64_t src = meta.src, L = meta.L;
@@ -775,129 +924,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     // ---- per-document histogram in LDS
     uint32_t claims = 0, toks = 0;
     bool overflow = false;
-    for (uint32_t tb = 0; tb < ntok && !overflow; tb += 64 * kWaveK) {
-      uint64_t tkey[kWaveK];
-      uint32_t slot[kWaveK];
-      uint32_t pendm = 0, longm = 0;
-      // keys of <= 8 bytes, branch-free: all list reads, then all text reads, then the math
-      uint32_t ent[kWaveK];
-#pragma unroll
-      for (int k = 0; k < (int)kWaveK; k++) {
-        const uint32_t idx = tb + lane + 64 * k;
-        ent[k] = sm.list[idx < ntok ? idx : 0u];
-      }
-      uint32_t dw[kWaveK][3];
-#pragma unroll
-      for (int k = 0; k < (int)kWaveK; k++) {
-        const uint32_t a0 = (ent[k] & 0xFFFFu) >> 2;
-        dw[k][0] = tw[a0]; dw[k][1] = tw[a0 + 1]; dw[k][2] = tw[a0 + 2];
-      }
-#pragma unroll
-      for (int k = 0; k < (int)kWaveK; k++) {
-        const bool in = tb + lane + 64 * k < ntok;
-        const uint32_t tp = ent[k] & 0xFFFFu, n = (ent[k] >> 16) - tp, o = tp & 3;
-        const uint64_t m64 = n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1);
-        const uint32_t t0 = __builtin_amdgcn_alignbyte(dw[k][1], dw[k][0], o) & (uint32_t)m64;
-        const uint32_t t1 = __builtin_amdgcn_alignbyte(dw[k][2], dw[k][1], o) & (uint32_t)(m64 >> 32);
-        bool valid = true;
-        if (under) valid = (((t0 ^ 0x5F5F5F5Fu) & (uint32_t)m64) | ((t1 ^ 0x5F5F5F5Fu) & (uint32_t)(m64 >> 32))) != 0;
-        const uint32_t l0 = lower4(t0), l1 = lower4(t1);
-        tkey[k] = (uint64_t)l0 | ((uint64_t)l1 << 32);
-        slot[k] = ((l0 ^ rotl32(l1, 16)) * 0x85EBCA77u) >> (32 - kWaveSlotBits);
-        pendm |= (uint32_t)(in && n <= 8 && valid) << k;
-        longm |= (uint32_t)(in && n > 8) << k;
-      }
-      const bool hasfold = __any(longm != 0);
-      if (hasfold) {                                    // tokens of 9..255 bytes: folded keys
-#pragma unroll
-        for (int k = 0; k < (int)kWaveK; k++) {
-          if ((longm >> k) & 1u) {
-            const uint32_t e = sm.list[tb + lane + 64 * k];
-            const uint32_t tp = e & 0xFFFFu, n = (e >> 16) - tp;
-            if (n > kMaxTokenLen) {
-              set_err(p.err, kErrTokenTooLong, (uint32_t)d);
-            } else {
-              uint32_t h;
-              bool valid;
-              tkey[k] = fold_key(sm.text, tp, n, &h, &valid);
-              slot[k] = h >> (32 - kWaveSlotBits);
-              pendm |= (uint32_t)valid << k;
-            }
-          }
-        }
-      }
-      toks += (uint32_t)__popc(pendm);
-      for (uint32_t round = 0;; round++) {
-        const uint32_t np = (uint32_t)__popc(pendm);
-        const uint32_t pincl = wave_incl_add(np);
-        const uint32_t P = (uint32_t)__builtin_amdgcn_readlane((int)pincl, 63);
-        if (P == 0) break;
-        if (round >= kWaveSlots) { overflow = true; break; }
-        if (round >= kWaveFastRounds && P <= kWaveQueue) {
-          // retry queue: one unresolved token per lane, probed until resolved
-          uint32_t at = pincl - np;
-#pragma unroll
-          for (int k = 0; k < (int)kWaveK; k++)
-            if ((pendm >> k) & 1u) { sm.qkey[at] = tkey[k]; sm.qslot[at] = (uint16_t)slot[k]; at++; }
-          asm volatile("" ::: "memory");
-          bool qp = lane < P;
-          uint64_t qk = 0;
-          uint32_t qs = 0;
-          if (qp) { qk = sm.qkey[lane]; qs = sm.qslot[lane]; }
-          for (uint32_t it = 0; __any(qp); it++) {
-            if (it >= kWaveSlots) { overflow = true; break; }
-            if (qp) {
-              const uint64_t old = atomicCAS(reinterpret_cast<unsigned long long *>(&sm.key[qs]), 0ull,
-                                             (unsigned long long)qk);
-              if (table_hit(sm.text, old, qk)) {
-                atomicAdd(&sm.cnt[qs >> 1], 1u << (16 * (qs & 1)));
-                claims += old == 0;
-                qp = false;
-              } else {
-                qs = (qs + 1) & (kWaveSlots - 1);
-              }
-            }
-          }
-          break;
-        }
-        // one probe round for every pending token (no-op CAS for the others)
-        uint64_t old[kWaveK];
-#pragma unroll
-        for (int k = 0; k < (int)kWaveK; k++) {
-          const bool pend = (pendm >> k) & 1u;
-          old[k] = atomicCAS(pend ? reinterpret_cast<unsigned long long *>(&sm.key[slot[k]]) : noop,
-                             pend ? 0ull : ~0ull, (unsigned long long)tkey[k]);
-        }
-        uint32_t foldm = 0;
-#pragma unroll
-        for (int k = 0; k < (int)kWaveK; k++) {
-          const bool pend = (pendm >> k) & 1u;
-          const bool hit = pend && (old[k] == 0 || old[k] == tkey[k]);
-          atomicAdd(hit ? &sm.cnt[slot[k] >> 1] : reinterpret_cast<uint32_t *>(noop),
-                    hit ? 1u << (16 * (slot[k] & 1)) : 0u);
-          claims += hit && old[k] == 0;
-          pendm &= ~((uint32_t)hit << k);
-          bool fc = false;
-          if (hasfold)
-            fc = pend && !hit && ((old[k] & tkey[k]) >> 63) && ((old[k] ^ tkey[k]) & ~kFoldPosMask) == 0;
-          foldm |= (uint32_t)fc << k;
-          if (pend && !hit && !fc) slot[k] = (slot[k] + 1) & (kWaveSlots - 1);
-        }
-        if (hasfold && __any(foldm != 0)) {              // same length and hash: compare bytes
-#pragma unroll
-          for (int k = 0; k < (int)kWaveK; k++) {
-            if ((foldm >> k) & 1u) {
-              if (span_same(sm.text, (uint32_t)(old[k] >> 13) & 0x1FFFu, (uint32_t)(tkey[k] >> 13) & 0x1FFFu,
-                            (uint32_t)tkey[k] & 0xFFu)) {
-                atomicAdd(&sm.cnt[slot[k] >> 1], 1u << (16 * (slot[k] & 1)));
-                pendm &= ~(1u << k);
-              } else {
-                slot[k] = (slot[k] + 1) & (kWaveSlots - 1);
-              }
-            }
-          }
-        }
-      }
+    for (uint32_t tb = 0; tb < ntok && !overflow;) {       // batch width by what is left
+      const uint32_t rem = ntok - tb;
+      if (rem > 256) { hist_batch<8>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 512; }
+      else if (rem > 128) { hist_batch<4>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 256; }
+      else { hist_batch<2>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 128; }
     }
     const uint32_t len = wave_sum(toks), nu = wave_sum(claims);
     if (overflow || nu > kWaveTerms) {                      // wave-uniform: long path
@@ -945,12 +976,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
           const uint32_t s = slots[in ? idx : 0u] & (kWaveSlots - 1);
           const uint64_t key = sm.key[s];
           tf[k] = (sm.cnt[s >> 1] >> (16 * (s & 1))) & 0xFFFFu;
-          const bool f = in && (key & kFoldBit);
-          lo[k] = (in && !f) ? key : 0ull;
+          const bool f = in & ((key & kFoldBit) != 0);
+          const bool sh = in & !f;
+          lo[k] = sh ? key : 0ull;
           foldm |= (uint32_t)f << k;
           actm |= (uint32_t)in << k;
           ps[k] = dict_home(dict_hash_short(lo[k]), dmask) & ~1u;
-          if (in && !f) g[k] = kLookupPending;
+          g[k] = sh ? kLookupPending : g[k];
         }
       }
       // folded (> 8 byte) terms: exact 128-bit keys, one lookup per lane at a time
@@ -979,11 +1011,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         const uint32_t pincl = wave_incl_add(np);
         const uint32_t P = (uint32_t)__builtin_amdgcn_readlane((int)pincl, 63);
         if (P == 0) break;
-        if (round > 0 && P <= kWaveQueue) {
+        if (round > 0 && P <= kDictQueue) {
           // retry queue in the (no longer needed) table: (lo, probe slot, term index)
           uint64_t *qlo = sm.key;
-          uint2 *qmeta = reinterpret_cast<uint2 *>(sm.key + kWaveQueue);
-          uint32_t *res = reinterpret_cast<uint32_t *>(sm.key + 2 * kWaveQueue);
+          uint2 *qmeta = reinterpret_cast<uint2 *>(sm.key + kDictQueue);
+          uint32_t *res = reinterpret_cast<uint32_t *>(sm.key + 2 * kDictQueue);
           uint32_t at = pincl - np;
 #pragma unroll
           for (int k = 0; k < (int)kWaveK; k++)
@@ -1025,9 +1057,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
           uint32_t c;
           const uint32_t r = bucket_probe(e[k], ps[k], lo[k], &c);
           cs[k] = pend ? c : kInvalidSlot;
-          anyclaim |= pend && c != kInvalidSlot;
-          if (pend && r == kLookupPending && c == kInvalidSlot) ps[k] = ((ps[k] | 1u) + 1u) & dmask;
-          if (pend) g[k] = r;
+          anyclaim |= pend & (c != kInvalidSlot);
+          const bool adv = pend & (r == kLookupPending) & (c == kInvalidSlot);
+          ps[k] = adv ? (((ps[k] | 1u) + 1u) & dmask) : ps[k];
+          g[k] = pend ? r : g[k];
         }
         if (__any(anyclaim)) {
 #pragma unroll
@@ -1038,7 +1071,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       bool caperr = false;
 #pragma unroll
       for (int k = 0; k < (int)kWaveK; k++) {
-        const bool e = ((actm >> k) & 1u) && (g[k] == kInvalidSlot || g[k] == kLookupPending);
+        const bool e = (((actm >> k) & 1u) != 0) & ((g[k] == kInvalidSlot) | (g[k] == kLookupPending));
         caperr |= e;
         if (e) g[k] = 0;
       }
@@ -1046,42 +1079,57 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     }
     if (p.debug_stop == 4) { clear_table(sm, lane); continue; }
 
-    // ---- CSR row grouped by dictionary range (8 ranges per pass), staged in LDS
+    // ---- CSR row grouped by dictionary range (8 ranges per pass), staged in LDS.
+    // Eight 16-bit range counters per lane live in two u64 words (ranges 0-3,
+    // 4-7): field access is one 64-bit select + shift, no branches.
     uint32_t *st_col = reinterpret_cast<uint32_t *>(sm.key);
     uint32_t *st_tf = st_col + kWaveSlots;
     const uint32_t st_noop = kWaveSlots - 64 + lane;          // unused staging words (nu <= kWaveTerms)
     uint32_t run = 0;
     for (uint32_t rb = 0; rb < R; rb += 8) {
-      uint32_t c[4] = {0, 0, 0, 0};
-#pragma unroll
-      for (int k = 0; k < (int)kWaveK; k++) {
-        const uint32_t f = (g[k] >> p.range_shift) - rb;
-        field8_add(c, f, (((actm >> k) & 1u) && f < 8) ? 1u : 0u);
-      }
-      uint32_t pk[4], tot[4];
-#pragma unroll
-      for (int w = 0; w < 4; w++) {
-        const uint32_t incl = wave_incl_add(c[w]);
-        pk[w] = incl - c[w];
-        tot[w] = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-      }
-      // exclusive scan of the 8 totals (wave-uniform), packed the same way
-      uint32_t fb[4] = {0, 0, 0, 0}, acc = 0;
-#pragma unroll
-      for (int f = 0; f < 8; f++) {
-        fb[f >> 1] |= acc << (16 * (f & 1));
-        acc += (tot[f >> 1] >> (16 * (f & 1))) & 0xFFFFu;
-      }
-      if (lane < 8 && rb + lane < R)
-        p.rsplit[d * R + rb + lane] = run + field8(fb, lane) + field8(tot, lane);
-#pragma unroll
-      for (int w = 0; w < 4; w++) pk[w] += fb[w];
+      uint64_t c0 = 0, c1 = 0;
+      uint32_t fk[kWaveK];
 #pragma unroll
       for (int k = 0; k < (int)kWaveK; k++) {
         const uint32_t f = (g[k] >> p.range_shift) - rb;
         const bool inr = ((actm >> k) & 1u) && f < 8;
-        const uint32_t pos = inr ? run + field8(pk, f) : st_noop;
-        field8_add(pk, f, inr ? 1u : 0u);
+        fk[k] = inr ? f : 8u;                                  // 8 = not in this pass
+        const uint64_t inc = inr ? (1ull << (16 * (f & 3))) : 0ull;
+        c0 += (f & 4) ? 0ull : inc;
+        c1 += (f & 4) ? inc : 0ull;
+      }
+      // wave exclusive scan of the 8 fields (4 u32 words) + totals
+      uint32_t w[4] = {(uint32_t)c0, (uint32_t)(c0 >> 32), (uint32_t)c1, (uint32_t)(c1 >> 32)};
+      uint32_t tot[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const uint32_t incl = wave_incl_add(w[i]);
+        tot[i] = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        w[i] = incl - w[i];
+      }
+      // exclusive scan of the 8 totals (wave-uniform), packed the same way
+      uint64_t fb0 = 0, fb1 = 0;
+      uint32_t acc = 0, lane_base = 0, lane_tot = 0;
+#pragma unroll
+      for (int f = 0; f < 8; f++) {
+        const uint32_t t = (tot[f >> 1] >> (16 * (f & 1))) & 0xFFFFu;
+        if (f < 4) fb0 |= (uint64_t)acc << (16 * f); else fb1 |= (uint64_t)acc << (16 * (f - 4));
+        if ((uint32_t)f == lane) { lane_base = acc; lane_tot = t; }
+        acc += t;
+      }
+      if (lane < 8 && rb + lane < R) p.rsplit[d * R + rb + lane] = run + lane_base + lane_tot;
+      uint64_t pk0 = ((uint64_t)w[0] | ((uint64_t)w[1] << 32)) + fb0;
+      uint64_t pk1 = ((uint64_t)w[2] | ((uint64_t)w[3] << 32)) + fb1;
+#pragma unroll
+      for (int k = 0; k < (int)kWaveK; k++) {
+        const uint32_t f = fk[k];
+        const bool inr = f < 8;
+        const uint64_t wsel = (f & 4) ? pk1 : pk0;
+        const uint32_t sh = 16 * (f & 3);
+        const uint32_t pos = inr ? run + ((uint32_t)(wsel >> sh) & 0xFFFFu) : st_noop;
+        const uint64_t inc = inr ? (1ull << sh) : 0ull;
+        pk0 += (f & 4) ? 0ull : inc;
+        pk1 += (f & 4) ? inc : 0ull;
         st_col[pos] = g[k];
         st_tf[pos] = tf[k];
       }
