@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--batch-queries", type=int, default=10_000)
     ap.add_argument("--cpu-sample", type=int, default=25_000, help="docs in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-queries", action="store_true")
+    ap.add_argument("--cap-log2", type=int, default=0,
+                    help="dictionary slots 2^x (0 = smallest power of two >= 1.6 x vocab, at least 2^18)")
+    ap.add_argument("--inversion", choices=("auto", "block", "term"), default="auto")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r01", "traffic.json"),
                     help="per-kernel HBM bytes from tools/prof_round.sh (rocprofv3 PMC passes of this workload)")
     return ap.parse_args()
@@ -117,7 +120,13 @@ def main():
     doc_base = rank * n_docs
     corpus = synth.DeviceCorpus(n_docs, V=args.vocab, len_min=args.len_min, len_max=args.len_max,
                                 doc_base=doc_base, device=local)
-    idx = ShardIndex(device=local, vocab_capacity_log2=18,
+    cap = args.cap_log2
+    if not cap:
+        cap = 18
+        while (1 << cap) < 1.6 * args.vocab:
+            cap += 1
+    inv = {"auto": 0, "block": 1, "term": 2}[args.inversion]
+    idx = ShardIndex(device=local, vocab_capacity_log2=cap, inversion=inv,
                      stats_mode=STATS_GLOBAL if world > 1 else 0)
     idx.add_documents_device(corpus.d_text, corpus.d_offsets, n_docs, corpus.total_bytes)
     adapter = D.HipShardAdapter(idx, dev, doc_base=doc_base) if world > 1 else None
@@ -153,8 +162,10 @@ def main():
     text_bytes, nnz, N = st["text_bytes"], st["nnz"], st["num_docs"]
 
     # ---- roofline of the dominant kernel (algorithmic bytes) ----
-    C_slots = 1 << 18
+    C_slots = 1 << cap
     n_blocks = (N + 8191) // 8192
+    if st["term_major"]:
+        n_blocks = 0        # no per-block count table: the sort-based inversion reads CSR, writes postings
     alg = {
         # text read once + CSR (slot u32 + tf u32) written once + row metadata (SURVEY: 9 B/doc)
         "ms_tokenize": text_bytes + 8 * nnz + 9 * N,
@@ -196,11 +207,14 @@ def main():
         "vs_baseline": None,
         "dtype": "u8/u32 (integer inversion), f32 BM25 with f64 accumulation",
         "data": "synthetic (Zipf s=1.0 corpus generated in HBM by tfidf_synth_corpus, seed 20251015)",
-        "config": {"workload": "cfg2: %d docs/GPU x U[%d,%d] tokens, V=%d, full index build per step%s" % (
+        "config": {"workload": "%s: %d docs/GPU x U[%d,%d] tokens, V=%d, full index build per step%s" % (
+            "cfg2" if (args.vocab, args.len_min, args.len_max) == (100_000, 400, 600) else
+            "cfg5-shape" if args.vocab >= 1_000_000 else "custom",
             N, args.len_min, args.len_max, args.vocab,
             "; GLOBAL stats exchange (vocab all-gather + DF all-reduce, RCCL)" if world > 1 else ""),
             "docs_per_gpu": N, "text_bytes_per_gpu": text_bytes, "nnz_per_gpu": nnz,
-            "vocab_terms": st["num_terms"], "parallelism": "dp%d (document shards)" % world},
+            "vocab_terms": st["num_terms"], "dict_slots_log2": cap, "inversion": "term-major" if st["term_major"] else "block-major",
+            "parallelism": "dp%d (document shards)" % world},
         "roofline": {"bound": "hbm", "kernel": dom.replace("ms_", ""), "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "traffic_source": traffic_src, "alg_bytes_per_launch": alg[dom], "avg_launch_ms": dom_ms},

@@ -60,6 +60,12 @@ extern "C" {
 #define TFIDF_STATS_SHARD 0  /* per-shard statistics: the reference's N-worker semantics */
 #define TFIDF_STATS_GLOBAL 1 /* statistics imported from all shards: 1-worker semantics */
 
+/* Inverted-index layout built by tfidf_commit (results are identical). */
+#define TFIDF_INVERSION_AUTO 0  /* block-major unless its (docs/8192 + 1) x 2^vocab_capacity_log2 count table
+                                   outgrows the CSR, or vocab_capacity_log2 > 21 (huge vocabularies) */
+#define TFIDF_INVERSION_BLOCK 1 /* block-major: postings grouped by 8192-doc block, then term */
+#define TFIDF_INVERSION_TERM 2  /* term-major: postings grouped by term, docs ascending (sort-based) */
+
 typedef struct tfidf_index tfidf_index;
 
 typedef struct tfidf_config {
@@ -67,8 +73,10 @@ typedef struct tfidf_config {
   float b;                      /* BM25 b,  default 0.75f */
   int32_t stats_mode;           /* TFIDF_STATS_SHARD (default) or TFIDF_STATS_GLOBAL */
   int32_t device;               /* HIP device ordinal */
-  uint32_t vocab_capacity_log2; /* dictionary slots = 2^x; default 18 (<= ~200k terms) */
+  uint32_t vocab_capacity_log2; /* dictionary slots = 2^x, x in [10, 26]; default 18 (<= ~200k terms);
+                                   x > 21 implies the term-major inversion */
   uint32_t max_token_len;       /* StandardAnalyzer.DEFAULT_MAX_TOKEN_LENGTH = 255 (only value supported) */
+  int32_t inversion;            /* TFIDF_INVERSION_AUTO (default), _BLOCK or _TERM */
 } tfidf_config;
 
 typedef struct tfidf_index_stats {
@@ -80,6 +88,7 @@ typedef struct tfidf_index_stats {
   uint64_t device_bytes;  /* HBM held by the index (feeds /worker/index-size) */
   uint64_t long_docs;     /* documents indexed by the long-document path */
   uint64_t text_bytes;    /* corpus bytes resident on the device */
+  uint64_t term_major;    /* 1 if the last commit built the term-major layout (TFIDF_INVERSION_TERM) */
 } tfidf_index_stats;
 
 /* Per-phase device times of the last commit, measured with HIP events on the

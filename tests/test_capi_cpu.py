@@ -37,6 +37,7 @@ def test_version_and_config_defaults():
     assert lib.tfidf_config_init(C.byref(cfg)) == 0
     assert abs(cfg.k1 - 1.2) < 1e-7 and abs(cfg.b - 0.75) < 1e-7
     assert cfg.max_token_len == 255 and cfg.vocab_capacity_log2 == 18
+    assert cfg.inversion == 0   # TFIDF_INVERSION_AUTO
 
 
 def test_create_without_device_fails_loudly():

@@ -89,11 +89,42 @@ __device__ __forceinline__ uint32_t wave_select_bin(const uint32_t *hist, uint32
   return 255u - (4u * src + fi);
 }
 
+// Wave-cooperative lower bound over one term's doc-ascending postings
+// (term-major layout): first i in [lo, hi) with doc(post[i]) >= x.  Each step
+// samples 64 evenly spaced postings, so a list of df entries takes
+// ceil(log64(df)) + 1 dependent loads instead of log2(df).
+__device__ __forceinline__ uint64_t wave_lower_bound(const uint64_t *post, uint64_t lo, uint64_t hi, uint32_t x) {
+  const uint32_t lane = threadIdx.x & 63;
+  while (hi - lo > 64) {
+    const uint64_t step = (hi - lo + 63) >> 6;
+    const uint64_t i = lo + lane * step;
+    const bool less = i < hi && (uint32_t)post[i] < x;
+    const uint32_t c = (uint32_t)__popcll(__ballot(less));   // samples are sorted: lanes [0, c) are below x
+    if (c == 0) return lo;
+    const uint64_t nlo = lo + (uint64_t)(c - 1) * step + 1;
+    hi = min(hi, lo + (uint64_t)c * step);
+    lo = nlo;
+  }
+  const uint64_t i = lo + lane;
+  const bool less = i < hi && (uint32_t)post[i] < x;
+  return lo + (uint64_t)__popcll(__ballot(less));
+}
+
+// Segment of doc block [d0, d0 + kBlockDocs) in slot's postings (whole wave).
+__device__ __forceinline__ void term_block_range(const QueryParams &p, uint32_t slot, uint32_t d0, uint64_t *a,
+                                                 uint64_t *z) {
+  const uint64_t t0 = p.toff[slot], t1 = p.toff[slot + 1];
+  const uint64_t lo = wave_lower_bound(p.post, t0, t1, d0);
+  *a = lo;
+  *z = wave_lower_bound(p.post, lo, t1, d0 + kBlockDocs);
+}
+
 constexpr uint32_t kQTermsFast = 4;   // query terms whose ranges / first chunk are prefetched
 
 struct ScoreSmem {
   double acc[kBlockDocs];
-  uint32_t tlo[kQTermsFast], thi[kQTermsFast];
+  uint64_t tlo[kQTermsFast], thi[kQTermsFast];     // absolute posting ranges of the block's segments
+  uint64_t xlo, xhi;                               // range of a query term beyond the first kQTermsFast
   float tw[kQTermsFast];
   uint32_t hitbits[kBlockDocs / 32];
   float cache[256];
@@ -112,9 +143,9 @@ __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
   const uint32_t q0 = blockIdx.y * p.q_chunk;
   const uint32_t q1 = min(p.n_q, q0 + p.q_chunk);
   const uint64_t d0 = (uint64_t)b * kBlockDocs;
-  const uint64_t bb = p.bbase[b];
-  const uint64_t bend = p.bbase[b + 1];
-  const uint32_t *row = p.blk + (size_t)b * p.C;
+  const uint64_t bb = p.toff ? 0 : p.bbase[b];
+  const uint64_t bend = p.toff ? 0 : p.bbase[b + 1];
+  const uint32_t *row = p.toff ? nullptr : p.blk + (size_t)b * p.C;
   for (uint32_t i = tid; i < 256; i += blockDim.x) sm.cache[i] = p.cache[i];
   const uint32_t k = p.k;
   for (uint32_t q = q0; q < q1; q++) {
@@ -122,13 +153,23 @@ __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
     if (tid == 0) { sm.nhit = 0; sm.outn = 0; }
     __syncthreads();
     const uint32_t t0 = p.q_off[q], t1 = p.q_off[q + 1];
-    // all terms' posting ranges in one round trip (thread j fetches term j)
-    if (tid < t1 - t0 && tid < kQTermsFast) {
+    if (p.toff) {
+      // term-major layout: wave j finds term j's segment for this block in the
+      // term's doc-sorted list (two 64-ary searches)
+      const uint32_t wv = tid >> 6;
+      if (wv < t1 - t0 && wv < kQTermsFast) {
+        const uint32_t slot = p.q_slot[t0 + wv];
+        uint64_t a = 0, z = 0;
+        if (slot != kInvalidSlot) term_block_range(p, slot, (uint32_t)d0, &a, &z);
+        if ((tid & 63) == 0) { sm.tlo[wv] = a; sm.thi[wv] = z; sm.tw[wv] = p.q_w[t0 + wv]; }
+      }
+    } else if (tid < t1 - t0 && tid < kQTermsFast) {
+      // block-major layout: all terms' ranges in one round trip (thread j fetches term j)
       const uint32_t slot = p.q_slot[t0 + tid];
-      uint32_t a = 0, z = 0;
+      uint64_t a = 0, z = 0;
       if (slot != kInvalidSlot) {
-        a = row[slot];
-        z = slot + 1 < p.C ? row[slot + 1] : (uint32_t)(bend - bb);
+        a = bb + row[slot];
+        z = slot + 1 < p.C ? bb + row[slot + 1] : bend;
       }
       sm.tlo[tid] = a;
       sm.thi[tid] = z;
@@ -140,7 +181,7 @@ __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
 #pragma unroll
     for (uint32_t j = 0; j < kQTermsFast; j++) {
       pre[j] = 0;
-      if (j < t1 - t0 && sm.tlo[j] + tid < sm.thi[j]) pre[j] = p.post[bb + sm.tlo[j] + tid];
+      if (j < t1 - t0 && sm.tlo[j] + tid < sm.thi[j]) pre[j] = p.post[sm.tlo[j] + tid];
     }
     uint32_t my_new = 0;
     for (uint32_t j = t0; j < t1; j++) {
@@ -148,15 +189,26 @@ __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
       uint64_t lo, hi;
       float w;
       if (jj < kQTermsFast) {
-        lo = bb + sm.tlo[jj];
-        hi = bb + sm.thi[jj];
+        lo = sm.tlo[jj];
+        hi = sm.thi[jj];
         w = sm.tw[jj];
       } else {
         const uint32_t slot = p.q_slot[j];
         if (slot == kInvalidSlot) continue;               // uniform
         w = p.q_w[j];
-        lo = bb + row[slot];
-        hi = slot + 1 < p.C ? bb + row[slot + 1] : bend;
+        if (p.toff) {
+          if (tid < 64) {
+            uint64_t a, z;
+            term_block_range(p, slot, (uint32_t)d0, &a, &z);
+            if (tid == 0) { sm.xlo = a; sm.xhi = z; }
+          }
+          __syncthreads();
+          lo = sm.xlo;
+          hi = sm.xhi;
+        } else {
+          lo = bb + row[slot];
+          hi = slot + 1 < p.C ? bb + row[slot + 1] : bend;
+        }
       }
       for (uint64_t i = lo + tid; i < hi; i += blockDim.x) {
         uint64_t e;

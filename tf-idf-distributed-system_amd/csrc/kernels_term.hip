@@ -1,0 +1,114 @@
+// kernels_term.hip — term-major inversion for large vocabularies.
+//
+// The block-major inversion (kernels_index.hip) keeps a dense per-block count
+// table of (N / 8192 + 1) x C words.  With SURVEY §8 cfg 5 (5 M-term vocabulary,
+// millions of short documents per GPU) that table alone would be tens of GB, so
+// above a size threshold the index is inverted term-major instead:
+//
+//   1. (slot, doc) pairs: every CSR entry becomes key = slot << dbits | doc,
+//      value = tf << 8 | norm, written at the document's compact row offset
+//      (exclusive sum of distinct-term counts);
+//   2. radix sort of the pairs on the key bits only (rocPRIM onesweep);
+//   3. term bounds: toff[s] = first posting of slot s (C + 1 entries, one
+//      binary search per slot), df[s] = toff[s + 1] - toff[s];
+//   4. pack: post[i] = doc | (tf << 8 | norm) << 32 — the same posting word as
+//      the block-major layout, so the scoring kernels only differ in how they
+//      find a (doc block, term) segment (a wave-parallel search of the term's
+//      doc-sorted list, kernels_query.hip).
+//
+// The result is what Lucene's postings hold for the field (per term, docs in
+// ascending order with freq and the doc's norm byte) — reference: inversion
+// inside IndexWriter.updateDocument, J/worker/Worker.java:218; read back by
+// searcher.search at :230.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include "tfidf_common.h"
+#include "tfidf_internal.h"
+
+namespace tfidf {
+
+// One wave per document (grid-stride): the row is contiguous, so lanes write
+// consecutive pair slots.
+__global__ void __launch_bounds__(256) k_term_pairs(TermParams p) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  for (uint64_t d = wave; d < p.n_docs; d += nw) {
+    const uint64_t src = p.live_map ? p.live_map[d] : d;
+    const uint64_t base = csr_row_base(p.offsets, src);
+    const uint32_t n = p.doc_nuniq[d], o = p.row_off[d], nrm = p.doc_norm[d];
+    for (uint32_t j = lane; j < n; j += 64) {
+      const uint32_t c = p.csr_col[base + j], t = p.csr_tf[base + j];
+      if (t >= (1u << 24)) atomicOr(p.err, kErrTfTooLarge);
+      p.keys[o + j] = ((uint64_t)c << p.dbits) | d;
+      p.vals[o + j] = (t << 8) | nrm;
+    }
+  }
+}
+
+// toff[s] = first index i with slot(key[i]) >= s, for s in [0, C]: one thread
+// per slot, binary search of the sorted keys (empty slots cost the same as
+// full ones, so sparse tables over a huge C stay parallel).
+__global__ void k_term_bounds(const uint64_t *keys, uint64_t nnz, uint32_t dbits, uint32_t C, uint64_t *toff) {
+  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s > C) return;
+  uint64_t a = 0, z = nnz;
+  while (a < z) {
+    const uint64_t m = (a + z) >> 1;
+    if ((keys[m] >> dbits) < s) a = m + 1; else z = m;
+  }
+  toff[s] = a;
+}
+
+__global__ void k_term_df(const uint64_t *toff, uint32_t C, uint32_t *df) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < C) df[s] = (uint32_t)(toff[s + 1] - toff[s]);
+}
+
+__global__ void k_term_pack(const uint64_t *keys, const uint32_t *vals, uint64_t nnz, uint64_t dmask,
+                            uint64_t *post) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nnz) post[i] = (keys[i] & dmask) | ((uint64_t)vals[i] << 32);
+}
+
+hipError_t term_invert_tmp_bytes(uint64_t n_docs, uint64_t nnz, uint32_t key_bits, size_t *bytes) {
+  size_t a = 0, b = 0;
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, a, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                  n_docs ? n_docs : 1);
+  if (e != hipSuccess) return e;
+  hipcub::DoubleBuffer<uint64_t> k(nullptr, nullptr);
+  hipcub::DoubleBuffer<uint32_t> v(nullptr, nullptr);
+  e = hipcub::DeviceRadixSort::SortPairs(nullptr, b, k, v, nnz ? nnz : 1, 0, (int)key_bits);
+  *bytes = (a > b ? a : b) + 256;
+  return e;
+}
+
+hipError_t launch_term_invert(TermParams p, void *tmp, size_t tmp_bytes, hipStream_t s) {
+  hipError_t e;
+  if (p.n_docs == 0) {
+    hipLaunchKernelGGL(k_term_bounds, dim3(p.C / 256 + 1), dim3(256), 0, s, p.keys, (uint64_t)0, p.dbits, p.C,
+                       p.toff);
+    hipLaunchKernelGGL(k_term_df, dim3((p.C + 255) / 256), dim3(256), 0, s, p.toff, p.C, p.df);
+    return hipGetLastError();
+  }
+  e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, p.doc_nuniq, p.row_off, p.n_docs, s);
+  if (e != hipSuccess) return e;
+  {
+    const uint64_t waves = p.n_docs < (1ull << 20) ? p.n_docs : (1ull << 20);
+    hipLaunchKernelGGL(k_term_pairs, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, p);
+  }
+  hipcub::DoubleBuffer<uint64_t> k(p.keys, p.keys_alt);
+  hipcub::DoubleBuffer<uint32_t> v(p.vals, p.vals_alt);
+  e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, k, v, p.nnz, 0, (int)(p.dbits + p.slot_bits), s);
+  if (e != hipSuccess) return e;
+  const unsigned g = (unsigned)((p.nnz + 256) / 256);
+  hipLaunchKernelGGL(k_term_bounds, dim3(p.C / 256 + 1), dim3(256), 0, s, k.Current(), p.nnz, p.dbits, p.C,
+                     p.toff);
+  hipLaunchKernelGGL(k_term_df, dim3((p.C + 255) / 256), dim3(256), 0, s, p.toff, p.C, p.df);
+  hipLaunchKernelGGL(k_term_pack, dim3(g), dim3(256), 0, s, k.Current(), v.Current(), p.nnz,
+                     (1ull << p.dbits) - 1, p.post);
+  return hipGetLastError();
+}
+
+}  // namespace tfidf

@@ -92,6 +92,10 @@ struct DeviceGuard {
   }
 };
 
+// block-major rows are grouped into at most 64 dictionary ranges (the long
+// path's per-range counters), i.e. C <= 64 x 32768
+constexpr uint32_t kMaxBlockCapLog2 = 21;
+
 enum { EV_START, EV_TOK, EV_L0, EV_LONG, EV_D0, EV_DF, EV_BSCAN, EV_CSCAN, EV_SCAT, EV_Q0, EV_Q1, EV_Q2, EV_N };
 
 struct tfidf_index {
@@ -119,6 +123,12 @@ struct tfidf_index {
   DevBuf d_live_map;
   uint32_t cap_log2 = 18, C = 0, range_shift = 15, R = 1, n_blocks = 0;
   DevBuf dict, csr_col, csr_tf, doc_len, doc_nuniq, doc_norm, rsplit, long_list, counters, blk, bbase, post, post_tmp;
+  // term-major inversion (large vocabularies): compact row offsets, sort values (x2), term offsets, df
+  bool term_major = false;
+  DevBuf row_off, tvals, toff, tdf, term_tmp;
+  const uint32_t *df_dev() const {
+    return term_major ? tdf.as<uint32_t>() : blk.as<uint32_t>() + (size_t)n_blocks * C;
+  }
   DevBuf lt_keys, lt_cnt, lt_g;
   uint32_t lt_log2 = 0, lt_wgs = 64;
   std::vector<uint64_t> h_dict;
@@ -151,6 +161,7 @@ extern "C" int tfidf_config_init(tfidf_config *cfg) {
   cfg->device = 0;
   cfg->vocab_capacity_log2 = 18;
   cfg->max_token_len = 255;
+  cfg->inversion = TFIDF_INVERSION_AUTO;
   return TFIDF_OK;
 }
 
@@ -158,7 +169,9 @@ extern "C" int tfidf_create(const tfidf_config *cfg, tfidf_index **out) {
   if (!cfg || !out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
   if (cfg->max_token_len != 255) return fail(TFIDF_E_INVALID_ARG, "only max_token_len = 255 is supported");
   uint32_t lg = cfg->vocab_capacity_log2 ? cfg->vocab_capacity_log2 : 18;
-  if (lg < 10 || lg > 21) return fail(TFIDF_E_INVALID_ARG, "vocab_capacity_log2 must be in [10, 21]");
+  if (lg < 10 || lg > 26) return fail(TFIDF_E_INVALID_ARG, "vocab_capacity_log2 must be in [10, 26]");
+  if (lg > kMaxBlockCapLog2 && cfg->inversion == TFIDF_INVERSION_BLOCK)
+    return fail(TFIDF_E_INVALID_ARG, "block-major inversion supports vocab_capacity_log2 <= %u", kMaxBlockCapLog2);
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(TFIDF_E_NO_DEVICE, "no HIP device");
   if (cfg->device < 0 || cfg->device >= ndev) return fail(TFIDF_E_NO_DEVICE, "device %d out of range", cfg->device);
@@ -190,7 +203,8 @@ extern "C" int tfidf_destroy(tfidf_index *ix) {
                     &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->long_list, &ix->counters, &ix->blk,
                     &ix->bbase, &ix->post, &ix->post_tmp, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->canon_of_slot,
                     &ix->q_off, &ix->q_slot, &ix->q_w, &ix->cache, &ix->cand, &ix->cand_n, &ix->out_doc,
-                    &ix->out_score, &ix->out_n, &ix->hits, &ix->hits_n, &ix->hits_c, &ix->hits_s, &ix->sort_tmp};
+                    &ix->out_score, &ix->out_n, &ix->hits, &ix->hits_n, &ix->hits_c, &ix->hits_s, &ix->sort_tmp,
+                    &ix->row_off, &ix->tvals, &ix->toff, &ix->tdf, &ix->term_tmp};
   for (DevBuf *b : bufs) b->release();
   for (int i = 0; i < EV_N; i++) hipEventDestroy(ix->ev[i]);
   hipStreamDestroy(ix->stream);
@@ -372,12 +386,22 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   const uint64_t N = ix->n_docs;
   ix->C = 1u << ix->cap_log2;
   const uint32_t C = ix->C;
-  const uint32_t RS = C < kRangeSlots ? C : kRangeSlots;
+  ix->n_blocks = (uint32_t)((N + kBlockDocs - 1) / kBlockDocs);
+  const uint64_t row_cap = (ix->text_bytes + ix->n_staged) / 2 + 2;
+  // Inversion layout: block-major needs a dense (blocks + 1) x C count table;
+  // when that outgrows the CSR itself (huge vocabularies, SURVEY §8 cfg 5) the
+  // postings are built term-major by a sort instead (kernels_term.hip).
+  {
+    const uint64_t blk_bytes = (uint64_t)(ix->n_blocks + 1) * C * 4;
+    if (ix->cfg.inversion == TFIDF_INVERSION_TERM) ix->term_major = true;
+    else if (ix->cfg.inversion == TFIDF_INVERSION_BLOCK) ix->term_major = false;
+    else ix->term_major = ix->cap_log2 > kMaxBlockCapLog2 || (blk_bytes > (1ull << 31) && blk_bytes > row_cap * 4);
+  }
+  // CSR rows are grouped by dictionary range for the block-major passes only
+  const uint32_t RS = ix->term_major ? C : (C < kRangeSlots ? C : kRangeSlots);
   ix->range_shift = 0;
   while ((1u << ix->range_shift) < RS) ix->range_shift++;
   ix->R = C >> ix->range_shift;
-  ix->n_blocks = (uint32_t)((N + kBlockDocs - 1) / kBlockDocs);
-  const uint64_t row_cap = (ix->text_bytes + ix->n_staged) / 2 + 2;
 
   HIP_TRY(ix->dict.reserve((size_t)2 * C * 8));
   HIP_TRY(ix->csr_col.reserve(row_cap * 4));
@@ -388,8 +412,14 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   HIP_TRY(ix->rsplit.reserve(N * ix->R * 4 + 4));
   HIP_TRY(ix->long_list.reserve(N * 4 + 4));
   HIP_TRY(ix->counters.reserve(64));
-  HIP_TRY(ix->blk.reserve((size_t)(ix->n_blocks + 1) * C * 4));
-  HIP_TRY(ix->bbase.reserve((size_t)(ix->n_blocks + 2) * 8));
+  if (ix->term_major) {
+    HIP_TRY(ix->row_off.reserve(N * 4 + 4));
+    HIP_TRY(ix->toff.reserve(((size_t)C + 1) * 8));
+    HIP_TRY(ix->tdf.reserve((size_t)C * 4));
+  } else {
+    HIP_TRY(ix->blk.reserve((size_t)(ix->n_blocks + 1) * C * 4));
+    HIP_TRY(ix->bbase.reserve((size_t)(ix->n_blocks + 2) * 8));
+  }
 
   // counters: [0..2] stats u64, [3] err flags u32 + [3].hi first doc, [4] long_count
   uint64_t *ctr = ix->counters.as<uint64_t>();
@@ -498,24 +528,59 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   pp.post_tmp = ix->post_tmp.as<uint64_t>();
   pp.err = bp.err;
   HIP_TRY(hipEventRecord(ix->ev[EV_D0], s));
-  if (ix->n_blocks) {
-    HIP_TRY(launch_df_partial(pp, s));
+  if (ix->term_major) {
+    TermParams tp{};
+    tp.offsets = bp.offsets;
+    tp.live_map = bp.live_map;
+    tp.n_docs = N;
+    tp.nnz = ix->nnz;
+    tp.C = C;
+    tp.slot_bits = ix->cap_log2;
+    tp.dbits = 1;
+    while ((1ull << tp.dbits) < N) tp.dbits++;
+    tp.csr_col = bp.csr_col;
+    tp.csr_tf = bp.csr_tf;
+    tp.doc_nuniq = bp.doc_nuniq;
+    tp.doc_norm = bp.doc_norm;
+    tp.row_off = ix->row_off.as<uint32_t>();
+    HIP_TRY(ix->tvals.reserve(ix->nnz * 8 + 16));
+    tp.keys = ix->post_tmp.as<uint64_t>();
+    tp.keys_alt = ix->post.as<uint64_t>();
+    tp.vals = ix->tvals.as<uint32_t>();
+    tp.vals_alt = tp.vals + ix->nnz + 1;
+    tp.post = ix->post.as<uint64_t>();
+    tp.toff = ix->toff.as<uint64_t>();
+    tp.df = ix->tdf.as<uint32_t>();
+    tp.err = bp.err;
+    size_t tb = 0;
+    HIP_TRY(term_invert_tmp_bytes(N, ix->nnz, tp.dbits + tp.slot_bits, &tb));
+    HIP_TRY(ix->term_tmp.reserve(tb));
+    // the whole inversion is reported under ms_scatter
+    HIP_TRY(hipEventRecord(ix->ev[EV_DF], s));
+    HIP_TRY(hipEventRecord(ix->ev[EV_BSCAN], s));
+    HIP_TRY(hipEventRecord(ix->ev[EV_CSCAN], s));
+    HIP_TRY(launch_term_invert(tp, ix->term_tmp.p, tb, s));
+    HIP_TRY(hipEventRecord(ix->ev[EV_SCAT], s));
   } else {
-    HIP_TRY(hipMemsetAsync(ix->blk.p, 0, (size_t)C * 4, s));
+    if (ix->n_blocks) {
+      HIP_TRY(launch_df_partial(pp, s));
+    } else {
+      HIP_TRY(hipMemsetAsync(ix->blk.p, 0, (size_t)C * 4, s));
+    }
+    HIP_TRY(hipEventRecord(ix->ev[EV_DF], s));
+    HIP_TRY(launch_df_sum(pp, s));
+    if (ix->n_blocks) HIP_TRY(launch_row_scan(pp, s));
+    HIP_TRY(hipEventRecord(ix->ev[EV_BSCAN], s));
+    HIP_TRY(launch_block_base(pp, s));
+    HIP_TRY(hipEventRecord(ix->ev[EV_CSCAN], s));
+    if (ix->n_blocks) HIP_TRY(launch_scatter(pp, s));
+    HIP_TRY(hipEventRecord(ix->ev[EV_SCAT], s));
   }
-  HIP_TRY(hipEventRecord(ix->ev[EV_DF], s));
-  HIP_TRY(launch_df_sum(pp, s));
-  if (ix->n_blocks) HIP_TRY(launch_row_scan(pp, s));
-  HIP_TRY(hipEventRecord(ix->ev[EV_BSCAN], s));
-  HIP_TRY(launch_block_base(pp, s));
-  HIP_TRY(hipEventRecord(ix->ev[EV_CSCAN], s));
-  if (ix->n_blocks) HIP_TRY(launch_scatter(pp, s));
-  HIP_TRY(hipEventRecord(ix->ev[EV_SCAT], s));
   // host mirrors for query analysis: dictionary keys + df
   ix->h_dict.resize((size_t)2 * C);
   ix->h_df.resize(C);
   HIP_TRY(hipMemcpyAsync(ix->h_dict.data(), ix->dict.p, (size_t)2 * C * 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(ix->h_df.data(), ix->blk.as<uint32_t>() + (size_t)ix->n_blocks * C, (size_t)C * 4,
+  HIP_TRY(hipMemcpyAsync(ix->h_df.data(), ix->df_dev(), (size_t)C * 4,
                          hipMemcpyDeviceToHost, s));
   uint32_t err2 = 0;
   HIP_TRY(hipMemcpyAsync(&err2, ctr + 3, 4, hipMemcpyDeviceToHost, s));
@@ -558,8 +623,10 @@ extern "C" int tfidf_stats(const tfidf_index *ix, tfidf_index_stats *out) {
   out->nnz = ix->nnz;
   out->long_docs = ix->long_docs;
   out->text_bytes = ix->text_bytes;
+  out->term_major = ix->committed && ix->term_major;
   const DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->dict, &ix->csr_col, &ix->csr_tf, &ix->doc_len,
-                          &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->blk, &ix->bbase, &ix->post};
+                          &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->blk, &ix->bbase, &ix->post,
+                          &ix->toff, &ix->tdf};
   uint64_t tot = 0;
   for (const DevBuf *b : bufs) tot += b->bytes;
   out->device_bytes = tot;
@@ -625,6 +692,7 @@ static int run_scoring(tfidf_index *ix, const std::vector<uint32_t> &qoff, const
   qp.post = ix->post.as<uint64_t>();
   qp.bbase = ix->bbase.as<uint64_t>();
   qp.blk = ix->blk.as<uint32_t>();
+  qp.toff = ix->term_major ? ix->toff.as<uint64_t>() : nullptr;
   qp.C = ix->C;
   qp.n_blocks = ix->n_blocks;
   qp.n_docs = ix->n_docs;
@@ -923,7 +991,7 @@ extern "C" int tfidf_vocab_canonicalize_device(tfidf_index *ix, const void *d_al
   HIP_TRY(slot_to_canon(ix->dict.as<uint64_t>(), ix->C, canon.as<uint64_t>(), nu, ix->canon_of_slot.as<uint32_t>(), s));
   if (d_df_canonical) {
     HIP_TRY(hipMemsetAsync(d_df_canonical, 0, nu * 4, s));
-    HIP_TRY(scatter_df_canon(ix->blk.as<uint32_t>() + (size_t)ix->n_blocks * ix->C, ix->canon_of_slot.as<uint32_t>(),
+    HIP_TRY(scatter_df_canon(ix->df_dev(), ix->canon_of_slot.as<uint32_t>(),
                              ix->C, (uint32_t *)d_df_canonical, s));
   }
   HIP_TRY(hipStreamSynchronize(s));

@@ -81,11 +81,32 @@ hipError_t launch_row_scan(const PostingParams &p, hipStream_t s);
 hipError_t launch_block_base(const PostingParams &p, hipStream_t s);
 hipError_t launch_scatter(const PostingParams &p, hipStream_t s);
 
+// --- term-major inversion for large vocabularies (kernels_term.hip) ---
+struct TermParams {
+  const uint64_t *offsets;
+  const uint32_t *live_map;
+  uint64_t n_docs, nnz;
+  uint32_t C, slot_bits;      // C = 2^slot_bits
+  uint32_t dbits;             // doc bits in a sort key (2^dbits >= n_docs)
+  const uint32_t *csr_col, *csr_tf, *doc_nuniq;
+  const uint8_t *doc_norm;
+  uint32_t *row_off;          // [n_docs] compact row offsets (exclusive sum of doc_nuniq)
+  uint64_t *keys, *keys_alt;  // [nnz] each: sort keys slot << dbits | doc (double buffer)
+  uint32_t *vals, *vals_alt;  // [nnz] each: tf << 8 | norm
+  uint64_t *post;             // [nnz] out: doc | (tf << 8 | norm) << 32, term-major, docs ascending
+  uint64_t *toff;             // [C + 1] out: first posting of each slot
+  uint32_t *df;               // [C] out
+  uint32_t *err;
+};
+hipError_t term_invert_tmp_bytes(uint64_t n_docs, uint64_t nnz, uint32_t key_bits, size_t *bytes);
+hipError_t launch_term_invert(TermParams p, void *tmp, size_t tmp_bytes, hipStream_t s);
+
 // --- query scoring (kernels_query.hip) ---
 struct QueryParams {
   const uint64_t *post;
   const uint64_t *bbase;      // [n_blocks + 1] first posting of each block
   const uint32_t *blk;        // per-block exclusive offsets over slots [n_blocks * C]
+  const uint64_t *toff;       // term-major layout: [C + 1] first posting per slot (nullptr = block-major)
   uint32_t C;
   uint32_t n_blocks;
   uint64_t n_docs;

@@ -25,15 +25,19 @@ E_NO_DEVICE = 9
 STATS_SHARD = 0
 STATS_GLOBAL = 1
 
+INVERSION_AUTO = 0
+INVERSION_BLOCK = 1
+INVERSION_TERM = 2
+
 
 class Config(C.Structure):
     _fields_ = [("k1", C.c_float), ("b", C.c_float), ("stats_mode", C.c_int32), ("device", C.c_int32),
-                ("vocab_capacity_log2", C.c_uint32), ("max_token_len", C.c_uint32)]
+                ("vocab_capacity_log2", C.c_uint32), ("max_token_len", C.c_uint32), ("inversion", C.c_int32)]
 
 
 class IndexStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("num_docs", "doc_count", "sum_ttf", "num_terms", "nnz",
-                                          "device_bytes", "long_docs", "text_bytes")]
+                                          "device_bytes", "long_docs", "text_bytes", "term_major")]
 
 
 class CommitTiming(C.Structure):

@@ -16,13 +16,15 @@ def term_key(term: bytes):
 
 
 class ShardIndex:
-    def __init__(self, device=0, k1=1.2, b=0.75, vocab_capacity_log2=18, stats_mode=L.STATS_SHARD):
+    def __init__(self, device=0, k1=1.2, b=0.75, vocab_capacity_log2=18, stats_mode=L.STATS_SHARD,
+                 inversion=L.INVERSION_AUTO):
         lib = L.load()
         cfg = L.Config()
         L.check(lib.tfidf_config_init(C.byref(cfg)))
         cfg.k1, cfg.b, cfg.device = k1, b, device
         cfg.vocab_capacity_log2 = vocab_capacity_log2
         cfg.stats_mode = stats_mode
+        cfg.inversion = inversion
         h = C.c_void_p()
         L.check(lib.tfidf_create(C.byref(cfg), C.byref(h)))
         self._h = h
