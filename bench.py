@@ -46,17 +46,11 @@ def parse():
     ap.add_argument("--cap-log2", type=int, default=0,
                     help="dictionary slots 2^x (0 = smallest power of two >= 1.6 x vocab, at least 2^18)")
     ap.add_argument("--inversion", choices=("auto", "block", "term"), default="auto")
+    ap.add_argument("--no-e2e", dest="e2e", action="store_false",
+                    help="skip the PCIe-inclusive (host corpus -> HBM -> index) measurement")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r01", "traffic.json"),
                     help="per-kernel HBM bytes from tools/prof_round.sh (rocprofv3 PMC passes of this workload)")
     return ap.parse_args()
-
-
-def hip_d2h(dst_np, src_ptr, nbytes):
-    hip = C.CDLL("libamdhip64.so")
-    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-    rc = hip.hipMemcpy(dst_np.ctypes.data, C.c_void_p(src_ptr), nbytes, 2)
-    if rc != 0:
-        raise RuntimeError("hipMemcpy D2H failed: %d" % rc)
 
 
 def cpu_baseline(corpus, args, n_docs):
@@ -64,10 +58,7 @@ def cpu_baseline(corpus, args, n_docs):
     first n_docs of the same corpus: docs indexed/sec (+ top-10 queries/sec)."""
     from oracle import oracle as O
     n = min(n_docs, corpus.n_docs)
-    offs = np.zeros(n + 1, np.uint64)
-    hip_d2h(offs, corpus.d_offsets, (n + 1) * 8)
-    text = np.zeros(int(offs[n]), np.uint8)
-    hip_d2h(text, corpus.d_text, int(offs[n]))
+    text, offs = corpus.to_host(n)
     raw = text.tobytes()
     o = O.OracleIndex()
     t0 = time.perf_counter()
@@ -87,6 +78,24 @@ def cpu_baseline(corpus, args, n_docs):
                       "Lucene 9.8 analysis+inversion+stats, 1 thread; no JDK/Lucene in the image" % (n, len(raw) / 1e6),
             "seconds": t_idx, "queries_per_sec_top10": len(qs) / t_q,
             "queries_sample": "50 cfg-2 queries over the %d-doc sample" % n}
+
+
+def measured_copy_GBs(dev, nbytes=1 << 30, reps=5):
+    """Device-to-device copy bandwidth (read + write bytes / time): the
+    achievable-HBM reference the roofline is also quoted against."""
+    import torch
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    del a, b
+    return 2 * nbytes / (ms * 1e-3) / 1e9
 
 
 def main():
@@ -162,6 +171,7 @@ def main():
     text_bytes, nnz, N = st["text_bytes"], st["nnz"], st["num_docs"]
 
     # ---- roofline of the dominant kernel (algorithmic bytes) ----
+    copy_gbs = measured_copy_GBs(dev)
     C_slots = 1 << cap
     n_blocks = (N + 8191) // 8192
     if st["term_major"]:
@@ -217,6 +227,7 @@ def main():
             "parallelism": "dp%d (document shards)" % world},
         "roofline": {"bound": "hbm", "kernel": dom.replace("ms_", ""), "achieved": achieved, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "measured_copy_GBs": copy_gbs, "frac_of_measured_copy": achieved / copy_gbs,
                      "traffic_source": traffic_src, "alg_bytes_per_launch": alg[dom], "avg_launch_ms": dom_ms},
         "phases_ms": phases,
         "phases_alg_GBs": phase_gbs,
@@ -227,14 +238,15 @@ def main():
 
     # ---- queries (outside the timed region) ----
     if not args.no_queries and world == 1:
-        if world > 1:
-            D.global_commit(adapter)
         qs = synth.queries(max(args.queries, 1))
         idx.search(qs[0], 10)
-        t0 = time.perf_counter()
+        lat = []
         dev_ms = 0.0
+        t0 = time.perf_counter()
         for q in qs:
+            t1 = time.perf_counter()
             idx.search_arrays(q, 10)
+            lat.append(time.perf_counter() - t1)
             dev_ms += idx.last_search_ms()[1]
         t_top = time.perf_counter() - t0
         t0 = time.perf_counter()
@@ -250,11 +262,60 @@ def main():
         sc_ms, tot_ms = idx.last_search_ms()
         result["queries"] = {
             "single_top10_qps": len(qs) / t_top,
+            "single_top10_p50_ms": float(np.percentile(lat, 50)) * 1e3,
+            "single_top10_p99_ms": float(np.percentile(lat, 99)) * 1e3,
             "single_top10_device_ms_avg": dev_ms / len(qs),
             "single_all_hits_qps": 20 / t_all, "avg_hits": nh / 20,
             "batch10k_top10_qps": len(bq) / t_b,
             "batch10k_device_ms": tot_ms, "batch10k_scoring_ms": sc_ms,
         }
+    elif not args.no_queries:
+        # node-level queries over the sharded corpus with GLOBAL statistics:
+        # each rank scores every query on its shard, per-rank top-k keys are
+        # all-gathered over RCCL and merged on device (distributed.py)
+        bq = synth.queries(args.batch_queries)
+        D.global_search_batch(adapter, bq[:100], 10)
+        out = {}
+        for k in (10, 100):
+            barrier()
+            t0 = time.perf_counter()
+            D.global_search_batch(adapter, bq, k)
+            barrier()
+            out["batch%dk_top%d_qps" % (len(bq) // 1000, k)] = len(bq) / (time.perf_counter() - t0)
+        qs = synth.queries(max(args.queries, 1) // 4 or 1)
+        lat = []
+        for q in qs:
+            barrier()
+            t1 = time.perf_counter()
+            D.global_search(adapter, q, 100)
+            lat.append(time.perf_counter() - t1)
+        out["single_top100_p50_ms"] = float(np.percentile(lat, 50)) * 1e3
+        out["single_top100_qps"] = 1.0 / float(np.mean(lat))
+        out["note"] = "node-level: %d ranks, GLOBAL stats, per-rank top-k all-gather + device merge" % world
+        result["queries"] = out
+
+    # ---- corpus loader: PCIe-inclusive end-to-end build (not `value`) ----
+    if args.e2e and world == 1:
+        text, offs = corpus.to_host()
+        best_add, best_tot = None, None
+        for _ in range(2):
+            idx.clear()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            idx.add_documents_buffer(text, offs)
+            t1 = time.perf_counter()
+            idx.commit()
+            torch.cuda.synchronize()
+            t2 = time.perf_counter()
+            if best_tot is None or t2 - t0 < best_tot:
+                best_add, best_tot = t1 - t0, t2 - t0
+        result["end_to_end"] = {
+            "docs_per_s": N / best_tot, "ms": best_tot * 1e3, "h2d_ms": best_add * 1e3,
+            "h2d_GBs": len(text) / best_add / 1e9,
+            "note": "host corpus (pageable numpy) -> pinned double-buffered staging -> HBM, then tfidf_commit; "
+                    "best of 2"}
+        del text, offs
+
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         result["cpu_baseline"] = cpu_baseline(corpus, args, args.cpu_sample)
     corpus.free()

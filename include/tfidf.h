@@ -116,9 +116,14 @@ int tfidf_destroy(tfidf_index *ix);
 /* Host corpus: n_docs documents, document i = utf8[offsets[i] .. offsets[i+1]).
  * keys (may be NULL) = relative paths, key i = keys[key_offsets[i] .. key_offsets[i+1]);
  * a key already present replaces that document (updateDocument by Term("path", key)).
- * With keys == NULL the key of a document is its decimal ordinal in this index. */
+ * With keys == NULL the key of a document is its decimal ordinal in this index.
+ * Bytes reach HBM through two pinned staging buffers (host copy of one overlapped
+ * with the DMA of the other); the call returns once they are resident. */
 int tfidf_add_docs(tfidf_index *ix, const uint8_t *utf8, const uint64_t *offsets, uint64_t n_docs,
                    const uint8_t *keys, const uint64_t *key_offsets);
+/* Drop every staged and committed document (the index is empty, as after
+ * tfidf_create); device and pinned staging buffers are kept for reuse. */
+int tfidf_clear(tfidf_index *ix);
 /* Device-resident corpus (e.g. produced by tfidf_synth_corpus): copied device-to-device. */
 int tfidf_add_docs_device(tfidf_index *ix, const void *d_utf8, const void *d_offsets, uint64_t n_docs,
                           uint64_t total_bytes);

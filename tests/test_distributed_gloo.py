@@ -73,6 +73,15 @@ class OracleShardAdapter:
         hits = self.o.search(q, k)
         return np.array([d for d, _ in hits], np.uint32), np.array([s for _, s in hits], np.float32)
 
+    def search_batch(self, queries, k):
+        docs = np.zeros((len(queries), k), np.uint32)
+        scores = np.zeros((len(queries), k), np.float32)
+        counts = np.zeros(len(queries), np.uint32)
+        for i, q in enumerate(queries):
+            d, s = self.search_topk(q, k)
+            docs[i, :len(d)], scores[i, :len(s)], counts[i] = d, s, len(d)
+        return docs, scores, counts
+
 
 def _free_port():
     s = socket.socket()
@@ -91,10 +100,12 @@ def _worker(rank, world, port, queries, k, out_path):
     ad = OracleShardAdapter(texts[lo:hi], lo)
     n_canon, dc, ttf = D.global_commit(ad)
     results = [D.global_search(ad, q, k) for q in queries]
+    bd, bs, bc = D.global_search_batch(ad, queries, k)
+    batch = [[[int(bd[i, j]), float(bs[i, j])] for j in range(int(bc[i]))] for i in range(len(queries))]
     if rank == 0:
         import json
         with open(out_path, "w") as f:
-            json.dump({"n_canon": n_canon, "dc": dc, "ttf": ttf,
+            json.dump({"n_canon": n_canon, "dc": dc, "ttf": ttf, "batch": batch,
                        "results": [[[d, float(s)] for d, s in r] for r in results]}, f)
     dist.barrier()
     dist.destroy_process_group()
@@ -115,7 +126,9 @@ def test_global_mode_equals_single_index(tmp_path, world):
     o.commit()
     assert res["dc"] == o.doc_count and res["ttf"] == o.sum_ttf
     assert res["n_canon"] == o.num_terms
-    for q, got in zip(queries, res["results"]):
+    for q, got, gotb in zip(queries, res["results"], res["batch"]):
         want = o.search(q, k)
         assert [d for d, _ in got] == [d for d, _ in want]
         assert [np.float32(s) for _, s in got] == [np.float32(s) for _, s in want]
+        assert [d for d, _ in gotb] == [d for d, _ in want]
+        assert [np.float32(s) for _, s in gotb] == [np.float32(s) for _, s in want]

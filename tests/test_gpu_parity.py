@@ -281,6 +281,42 @@ def test_incremental_add_then_recommit():
     o.close()
 
 
+def test_host_loader_pinned_staging_and_clear():
+    """Host corpus of > 2 staging buffers (32 MiB each) through the pinned
+    loader = the same corpus added device-to-device; clear() empties the index
+    and a re-add reproduces it."""
+    dc = synth.DeviceCorpus(40000, V=50000, len_min=300, len_max=500)
+    text, offs = dc.to_host()
+    assert len(text) > 70 << 20
+    a = ShardIndex()
+    a.add_documents_buffer(text, offs)
+    a.commit()
+    b = ShardIndex()
+    b.add_documents_device(dc.d_text, dc.d_offsets, dc.n_docs, dc.total_bytes)
+    b.commit()
+    sa = a.stats()
+    assert sa == b.stats()
+    qs = synth.queries(10)
+    want = [b.search(q, 10) for q in qs]
+    assert [a.search(q, 10) for q in qs] == want
+    a.clear()
+    assert a.stats()["num_docs"] == 0
+    a.add_documents_buffer(text, offs)
+    a.commit()
+    assert a.stats() == sa
+    assert [a.search(q, 10) for q in qs] == want
+    # spot-check a few documents against the oracle
+    o = O.OracleIndex()
+    for d in (0, 17, 39999):
+        o.add_doc(str(d).encode(), text[int(offs[d]):int(offs[d + 1])].tobytes())
+    o.commit()
+    for i, d in enumerate((0, 17, 39999)):
+        assert a.doc_terms(d) == keyed(o.doc_terms(i))
+    for x in (a, b, o):
+        x.close()
+    dc.free()
+
+
 def test_non_ascii_document_rejected():
     g = ShardIndex()
     g.add_documents([b"fine text", "café".encode()])

@@ -55,6 +55,9 @@ class HipShardAdapter:
     def search_topk(self, query, k):
         return self.shard.search_arrays(query, k)
 
+    def search_batch(self, queries, k):
+        return self.shard.search_batch(queries, k)
+
     def doc_key(self, doc):
         return self.shard.doc_key(doc)
 
@@ -110,6 +113,42 @@ def global_search(adapter, query: bytes, k: int, group=None):
             cands.append((np.int32(sb).view(np.float32).item(), d))
     cands.sort(key=lambda x: (-x[0], x[1]))
     return [(d, s) for s, d in cands[:k]]
+
+
+def merge_keys(docs, scores, counts, doc_base, device):
+    """Per-rank batch top-k -> int64 merge keys [n_q, k] on ``device``:
+    (float32 score bits << 32) | ~global_doc.  BM25 scores are > 0, so the
+    integer order of the keys is (score desc, doc asc) descending, the
+    reference's HitQueue order; empty slots are 0."""
+    import numpy as np
+    nq, k = docs.shape
+    valid = np.arange(k)[None, :] < counts.astype(np.int64)[:, None]
+    g = (docs.astype(np.uint64) + np.uint64(doc_base)) & np.uint64(0xFFFFFFFF)
+    key = (scores.view(np.uint32).astype(np.uint64) << np.uint64(32)) | (~g & np.uint64(0xFFFFFFFF))
+    key = np.where(valid, key, np.uint64(0)).view(np.int64)
+    return torch.from_numpy(np.ascontiguousarray(key)).to(device)
+
+
+def global_search_batch(adapter, queries, k: int, group=None):
+    """Batched step 3 (cfg 3/4): every rank scores the whole batch on its
+    shard, the [n_q, k] merge keys are all-gathered once (one RCCL
+    collective for the batch) and the global top-k of each query is a device
+    top-k over the ws*k candidates.  Returns (docs int64[n_q, k], scores
+    float32[n_q, k], counts int64[n_q]) as numpy arrays (global doc ids)."""
+    import numpy as np
+    dev = _dev(adapter)
+    ws = dist.get_world_size(group)
+    docs, scores, counts = adapter.search_batch(queries, k)
+    mine = merge_keys(docs, scores, counts, adapter.doc_base, dev)
+    outs = [torch.empty_like(mine) for _ in range(ws)]
+    dist.all_gather(outs, mine, group=group)
+    allk = torch.cat(outs, dim=1)                                   # [n_q, ws * k]
+    top = torch.topk(allk, k, dim=1, largest=True, sorted=True).values
+    top = top.cpu().numpy().view(np.uint64)
+    cnt = (top != 0).sum(axis=1)
+    gdoc = (~top & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    sc = (top >> np.uint64(32)).astype(np.uint32).view(np.float32)
+    return gdoc, sc, cnt
 
 
 def shard_range(n_docs, rank, world):

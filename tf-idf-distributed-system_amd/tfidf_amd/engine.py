@@ -66,6 +66,18 @@ class ShardIndex:
         L.check(L.load().tfidf_add_docs(self._h, blob, L.ptr(offs, C.c_uint64), n, kb,
                                         None if koffs is None else L.ptr(koffs, C.c_uint64)))
 
+    def add_documents_buffer(self, text, offsets):
+        """Host corpus as one uint8 buffer + uint64 offsets[n + 1] (no per-doc
+        Python objects): the loader path the reference's Worker.init feeds."""
+        text = np.ascontiguousarray(text, dtype=np.uint8)
+        offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
+        L.check(L.load().tfidf_add_docs(self._h, C.c_void_p(text.ctypes.data), L.ptr(offsets, C.c_uint64),
+                                        len(offsets) - 1, None, None))
+
+    def clear(self):
+        """Drop all staged/committed documents; device buffers are kept for reuse."""
+        L.check(L.load().tfidf_clear(self._h))
+
     def add_documents_device(self, d_text, d_offsets, n_docs, total_bytes):
         L.check(L.load().tfidf_add_docs_device(self._h, C.c_void_p(d_text), C.c_void_p(d_offsets), n_docs,
                                                total_bytes))

@@ -97,6 +97,14 @@ def queries(n_q, n_terms=3, lo=100, hi=10_000, seed=SEED + 1):
     return out
 
 
+def _d2h(dst_np, src_ptr, nbytes):
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    rc = hip.hipMemcpy(dst_np.ctypes.data, C.c_void_p(src_ptr), nbytes, 2)     # hipMemcpyDeviceToHost
+    if rc != 0:
+        raise RuntimeError("hipMemcpy D2H failed: %d" % rc)
+
+
 class DeviceCorpus:
     """Corpus generated directly in HBM by the tfidf_synth_corpus kernels."""
 
@@ -109,6 +117,15 @@ class DeviceCorpus:
                                        len_max, C.byref(t), C.byref(o), C.byref(tot)))
         self.d_text, self.d_offsets, self.total_bytes = t.value, o.value, tot.value
         self.n_docs, self.device = n_docs, device
+
+    def to_host(self, n_docs=None):
+        """(text uint8[], offsets uint64[n + 1]) of the first n_docs documents."""
+        n = self.n_docs if n_docs is None else min(n_docs, self.n_docs)
+        offs = np.zeros(n + 1, np.uint64)
+        _d2h(offs, self.d_offsets, (n + 1) * 8)
+        text = np.zeros(int(offs[n]), np.uint8)
+        _d2h(text, self.d_text, int(offs[n]))
+        return text, offs
 
     def free(self):
         from . import _lib as L

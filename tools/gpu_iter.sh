@@ -14,4 +14,5 @@ print("value %.4g docs/s  ms/step %.2f" % (r["value"], r["ms_per_step"]))
 print("roofline", {k: r["roofline"][k] for k in ("kernel", "achieved", "frac", "avg_launch_ms")})
 print("phases", {k: round(v, 3) for k, v in r["phases_ms"].items()})
 print("queries", r.get("queries"))
+print("e2e", r.get("end_to_end"), "copyGBs", r["roofline"].get("measured_copy_GBs"))
 PY
