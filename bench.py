@@ -257,7 +257,7 @@ def main():
             "cfg2" if (args.vocab, args.len_min, args.len_max) == (100_000, 400, 600) else
             "cfg5-shape" if args.vocab >= 1_000_000 else "custom",
             N, args.len_min, args.len_max, args.vocab,
-            "; GLOBAL stats exchange (vocab all-gather + DF all-reduce, RCCL)" if world > 1 else ""),
+            "; GLOBAL stats exchange (term-ownership all-to-all of (term, df) records + stats all-reduce, RCCL)" if world > 1 else ""),
             "docs_per_gpu": N, "text_bytes_per_gpu": text_bytes, "nnz_per_gpu": nnz,
             "vocab_terms": st["num_terms"], "dict_slots_log2": cap, "inversion": "term-major" if st["term_major"] else "block-major",
             "parallelism": "dp%d (document shards)" % world},

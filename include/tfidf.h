@@ -152,6 +152,19 @@ int tfidf_term_df(tfidf_index *ix, const uint8_t *term, uint64_t len, uint64_t *
                   uint64_t *df_effective);
 
 /* ---- GLOBAL statistics across shards (no reference counterpart) ----
+ * Term-ownership exchange (used by the multi-GPU orchestration; O(vocabulary)
+ * per rank, no sort):
+ * 1. tfidf_vocab_partition_device: this shard's vocabulary as records
+ *    (lo, hi, df: 3 x u64 each) grouped by owner rank (a hash of the term key
+ *    mod n_ranks); counts[r] (host, n_ranks entries) = records for rank r.
+ * 2. caller all-to-alls the records to their owners (RCCL), then the owner
+ *    calls tfidf_vocab_reduce_device on everything it received: d_df_out
+ *    (u32 per record, same order) = df summed over identical terms;
+ *    *n_unique = distinct terms this rank owns.
+ * 3. caller all-to-alls the answers back (reverse split sizes), all-reduces
+ *    {doc_count, sum_ttf}, and tfidf_set_global_df_device imports the answers
+ *    (in the record order step 1 produced).
+ * Canonical-vocabulary form (sorted union; kept for tools and tests):
  * 1. tfidf_vocab_export_device: this shard's term keys (16 B each, sorted
  *    ascending as (hi, lo)) and local df into caller device buffers.
  * 2. caller all-gathers the key lists (RCCL), then
@@ -160,6 +173,12 @@ int tfidf_term_df(tfidf_index *ix, const uint8_t *term, uint64_t len, uint64_t *
  *    shard's df in canonical order (zero elsewhere).
  * 3. caller all-reduces d_df_canonical and {doc_count, sum_ttf} (RCCL SUM), then
  *    tfidf_set_global_stats_device imports them. */
+int tfidf_vocab_partition_device(tfidf_index *ix, uint32_t n_ranks, void *d_records, uint64_t cap,
+                                 uint64_t *counts, uint64_t *n_out);
+int tfidf_vocab_reduce_device(tfidf_index *ix, const void *d_records, uint64_t n, void *d_df_out,
+                              uint64_t *n_unique);
+int tfidf_set_global_df_device(tfidf_index *ix, const void *d_df, uint64_t n, uint64_t doc_count,
+                               uint64_t sum_ttf);
 int tfidf_vocab_size(const tfidf_index *ix, uint64_t *n);
 int tfidf_vocab_export_device(tfidf_index *ix, void *d_keys, void *d_df, uint64_t cap, uint64_t *n_out);
 int tfidf_vocab_canonicalize_device(tfidf_index *ix, const void *d_all_keys, uint64_t n_all,

@@ -64,6 +64,38 @@ class OracleShardAdapter:
             dfc[self.canon_index[key]] = d
         return torch.from_numpy(dfc)
 
+    # term-ownership exchange (distributed.global_commit)
+    @staticmethod
+    def _owner(lo, hi, G):
+        return ((lo * 0x9E3779B97F4A7C15 ^ hi) & 0xFFFFFFFFFFFFFFFF) % G
+
+    def vocab_partition(self, n_ranks):
+        groups = [[] for _ in range(n_ranks)]
+        self.sent_terms = []
+        by_owner = [[] for _ in range(n_ranks)]
+        for t, df in sorted(self.o.vocab().items()):
+            lo, hi = term_key(t)
+            r = self._owner(lo, hi, n_ranks)
+            groups[r].append((lo, hi, df))
+            by_owner[r].append(t)
+        for r in range(n_ranks):
+            self.sent_terms += by_owner[r]
+        rows = [x for g in groups for x in g]
+        rec = np.array(rows, np.uint64).reshape(-1, 3).view(np.int64)
+        return torch.from_numpy(rec.copy()), [len(g) for g in groups]
+
+    def vocab_reduce(self, records):
+        r = records.numpy().view(np.uint64)
+        tot = {}
+        for lo, hi, df in r.tolist():
+            tot[(lo, hi)] = tot.get((lo, hi), 0) + df
+        ans = np.array([tot[(lo, hi)] for lo, hi, _ in r.tolist()], np.int32)
+        return torch.from_numpy(ans), len(tot)
+
+    def import_global_df(self, gdf, doc_count, sum_ttf):
+        g = gdf.numpy().tolist()
+        self.o.set_global_stats(doc_count, sum_ttf, {t: int(d) for t, d in zip(self.sent_terms, g)})
+
     def import_global(self, dfc, doc_count, sum_ttf):
         dfc = dfc.numpy()
         df_by_term = {t: int(dfc[self.canon_index[key]]) for key, t in self.terms.items()}
@@ -100,6 +132,11 @@ def _worker(rank, world, port, queries, k, out_path):
     ad = OracleShardAdapter(texts[lo:hi], lo)
     n_canon, dc, ttf = D.global_commit(ad)
     results = [D.global_search(ad, q, k) for q in queries]
+    # the canonical (all-gather + sorted union) form must agree
+    n2, dc2, ttf2 = D.global_commit_canonical(ad)
+    assert (n2, dc2, ttf2) == (n_canon, dc, ttf)
+    assert [D.global_search(ad, q, k) for q in queries] == results
+    D.global_commit(ad)
     bd, bs, bc = D.global_search_batch(ad, queries, k)
     batch = [[[int(bd[i, j]), float(bs[i, j])] for j in range(int(bc[i]))] for i in range(len(queries))]
     if rank == 0:

@@ -384,3 +384,66 @@ def test_global_stats_two_shards_equal_single_index():
     for s in shards:
         s.close()
     o.close()
+
+
+def test_global_stats_term_ownership_three_shards():
+    """The ownership exchange (vocab_partition -> all-to-all -> owner reduce ->
+    all-to-all back -> import), with the all-to-alls done by hand between three
+    shards on one GPU, equals the single index."""
+    import torch
+    texts = synth.corpus(5000, V=8000, len_min=20, len_max=120)
+    cuts = [0, 1200, 3100, 5000]
+    G = 3
+    dev = torch.device("cuda:0")
+    shards, recs, counts = [], [], []
+    for r in range(G):
+        s = ShardIndex()
+        s.add_documents(texts[cuts[r]:cuts[r + 1]])
+        s.commit()
+        n = s.vocab_size()
+        rec = torch.zeros((n, 3), dtype=torch.int64, device=dev)
+        torch.cuda.synchronize()
+        n2, c = s.vocab_partition_device(G, rec.data_ptr(), n)
+        assert n2 == n and int(c.sum()) == n
+        shards.append(s)
+        recs.append(rec)
+        counts.append([int(x) for x in c])
+    starts = [[sum(counts[r][:o]) for o in range(G)] for r in range(G)]
+    answers = [[None] * G for _ in range(G)]          # answers[sender][owner]
+    n_unique = 0
+    for o in range(G):                                # owner o receives from every rank, in rank order
+        parts = [recs[r][starts[r][o]:starts[r][o] + counts[r][o]] for r in range(G)]
+        recv = torch.cat(parts).contiguous()
+        out = torch.zeros(max(recv.shape[0], 1), dtype=torch.int32, device=dev)
+        torch.cuda.synchronize()
+        n_unique += shards[o].vocab_reduce_device(recv.data_ptr(), recv.shape[0], out.data_ptr())
+        at = 0
+        for r in range(G):
+            answers[r][o] = out[at:at + counts[r][o]]
+            at += counts[r][o]
+    st = [s.stats() for s in shards]
+    dc, ttf = sum(x["doc_count"] for x in st), sum(x["sum_ttf"] for x in st)
+    for r in range(G):
+        back = torch.cat(answers[r]).contiguous()
+        torch.cuda.synchronize()
+        shards[r].set_global_df_device(back.data_ptr(), back.shape[0], dc, ttf)
+    o = O.OracleIndex()
+    for i, t in enumerate(texts):
+        o.add_doc(str(i).encode(), t)
+    o.commit()
+    assert n_unique == o.num_terms
+    vocab = o.vocab()
+    for t in list(vocab)[:200]:
+        for s in shards:
+            loc, eff = s.df(t)
+            assert eff == vocab[t] or loc == 0
+    for q in synth.queries(20, lo=1, hi=2000):
+        want = o.search(q, 0)
+        got = []
+        for base, s in zip(cuts, shards):
+            got += [(d + base, sc) for d, sc in s.search(q, 0)]
+        got.sort(key=lambda x: (-x[1], x[0]))
+        assert_hits_equal(got, want)
+    for s in shards:
+        s.close()
+    o.close()

@@ -1,0 +1,113 @@
+// kernels_vocab.hip — GLOBAL statistics by term ownership.
+//
+// The reference's single worker sees one docFreq per term (Lucene
+// CollectionStatistics/TermStatistics at J/worker/Worker.java:230).  With the
+// corpus sharded over G GPUs every shard counts its own docFreq; the global
+// value is the sum over shards of the same term.  Each term has an owner rank
+// (hash of its 128-bit key mod G):
+//   1. partition : every shard groups its (key, df) records by owner;
+//   2. all-to-all (RCCL, host orchestration) sends each group to its owner;
+//   3. reduce    : the owner sums df over identical keys in a device hash table
+//                  (the dictionary's own find-or-insert) and answers, record by
+//                  record, with the summed df;
+//   4. all-to-all back, then each shard scatters the answers into a per-slot
+//      global-df vector.
+// Work per rank is O(vocabulary / G x G) = O(vocabulary), independent of G, and
+// nothing is sorted.
+#include <hip/hip_runtime.h>
+
+#include "dict_device.h"
+#include "tfidf_common.h"
+#include "tfidf_internal.h"
+
+namespace tfidf {
+
+__device__ __forceinline__ uint32_t owner_of(uint64_t lo, uint64_t hi, uint32_t G) {
+  uint32_t x = dict_hash(lo, hi) * 0x85EBCA6Bu;     // bits independent of the dictionary's home slot
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return (uint32_t)(((uint64_t)x * G) >> 32);
+}
+
+__global__ void k_vocab_count(const uint64_t *dict, uint32_t C, uint32_t G, uint32_t *counts) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= C) return;
+  const uint64_t lo = dict[s];
+  if (lo == 0) return;
+  atomicAdd(&counts[owner_of(lo, dict[(size_t)C + s], G)], 1u);
+}
+
+__global__ void k_vocab_scatter(const uint64_t *dict, const uint32_t *df, uint32_t C, uint32_t G, uint32_t *cursor,
+                                uint64_t *records, uint32_t *sent_slot) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= C) return;
+  const uint64_t lo = dict[s];
+  if (lo == 0) return;
+  const uint64_t hi = dict[(size_t)C + s];
+  const uint32_t at = atomicAdd(&cursor[owner_of(lo, hi, G)], 1u);
+  records[3 * (size_t)at] = lo;
+  records[3 * (size_t)at + 1] = hi;
+  records[3 * (size_t)at + 2] = df[s];
+  sent_slot[at] = s;
+}
+
+__global__ void k_vocab_insert(const uint64_t *records, uint64_t n, uint64_t *table, uint32_t tmask, uint32_t *sums,
+                               uint32_t *rslot) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool act = i < n;
+  const uint64_t lo = act ? records[3 * i] : 1, hi = act ? records[3 * i + 1] : kKeyValid;
+  const uint32_t slot = dict_find_or_insert(table, tmask, lo, hi, act);
+  if (act) {
+    atomicAdd(&sums[slot], (uint32_t)records[3 * i + 2]);
+    rslot[i] = slot;
+  }
+}
+
+__global__ void k_vocab_answer(const uint32_t *sums, const uint32_t *rslot, uint64_t n, uint32_t *out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = sums[rslot[i]];
+}
+
+__global__ void k_vocab_occupied(const uint64_t *table, uint64_t T, unsigned long long *n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool occ = i < T && table[i] != 0;
+  const uint64_t m = __ballot(occ);
+  if ((threadIdx.x & 63) == 0 && m) atomicAdd(n, (unsigned long long)__popcll(m));
+}
+
+__global__ void k_vocab_import(const uint32_t *sent_slot, const uint32_t *gdf_in, uint64_t n, uint32_t *gdf) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) gdf[sent_slot[i]] = gdf_in[i];
+}
+
+static unsigned blocks(uint64_t n) { return (unsigned)((n + 255) / 256 ? (n + 255) / 256 : 1); }
+
+hipError_t vocab_count(const uint64_t *dict, uint32_t C, uint32_t G, uint32_t *counts, hipStream_t s) {
+  hipLaunchKernelGGL(k_vocab_count, dim3(blocks(C)), dim3(256), 0, s, dict, C, G, counts);
+  return hipGetLastError();
+}
+
+hipError_t vocab_scatter(const uint64_t *dict, const uint32_t *df, uint32_t C, uint32_t G, uint32_t *cursor,
+                         uint64_t *records, uint32_t *sent_slot, hipStream_t s) {
+  hipLaunchKernelGGL(k_vocab_scatter, dim3(blocks(C)), dim3(256), 0, s, dict, df, C, G, cursor, records, sent_slot);
+  return hipGetLastError();
+}
+
+hipError_t vocab_reduce(const uint64_t *records, uint64_t n, uint64_t *table, uint32_t tmask, uint32_t *sums,
+                        uint32_t *rslot, uint32_t *out, unsigned long long *n_unique, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_vocab_insert, dim3(blocks(n)), dim3(256), 0, s, records, n, table, tmask, sums, rslot);
+  hipLaunchKernelGGL(k_vocab_answer, dim3(blocks(n)), dim3(256), 0, s, sums, rslot, n, out);
+  hipLaunchKernelGGL(k_vocab_occupied, dim3(blocks((uint64_t)tmask + 1)), dim3(256), 0, s, table,
+                     (uint64_t)tmask + 1, n_unique);
+  return hipGetLastError();
+}
+
+hipError_t vocab_import(const uint32_t *sent_slot, const uint32_t *gdf_in, uint64_t n, uint32_t *gdf, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_vocab_import, dim3(blocks(n)), dim3(256), 0, s, sent_slot, gdf_in, n, gdf);
+  return hipGetLastError();
+}
+
+}  // namespace tfidf

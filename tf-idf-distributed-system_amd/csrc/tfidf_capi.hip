@@ -146,6 +146,9 @@ struct tfidf_index {
   uint64_t g_doc_count = 0, g_sum_ttf = 0;
   DevBuf canon_of_slot;
   uint64_t n_canon = 0;
+  // term-ownership exchange: record order -> slot, owner-side scratch table
+  DevBuf sent_slot, vcounts, vt_table, vt_sum, vt_rslot, gdf_dev;
+  uint64_t n_sent = 0;
 
   // query scratch
   DevBuf q_off, q_slot, q_w, cache, cand, cand_n, out_doc, out_score, out_n, hits, hits_n, hits_c, hits_s, sort_tmp;
@@ -209,7 +212,8 @@ extern "C" int tfidf_destroy(tfidf_index *ix) {
                     &ix->bbase, &ix->post, &ix->post_tmp, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->canon_of_slot,
                     &ix->q_off, &ix->q_slot, &ix->q_w, &ix->cache, &ix->cand, &ix->cand_n, &ix->out_doc,
                     &ix->out_score, &ix->out_n, &ix->hits, &ix->hits_n, &ix->hits_c, &ix->hits_s, &ix->sort_tmp,
-                    &ix->row_off, &ix->tvals, &ix->toff, &ix->tdf, &ix->term_tmp};
+                    &ix->row_off, &ix->tvals, &ix->toff, &ix->tdf, &ix->term_tmp, &ix->sent_slot, &ix->vcounts,
+                    &ix->vt_table, &ix->vt_sum, &ix->vt_rslot, &ix->gdf_dev};
   for (DevBuf *b : bufs) b->release();
   for (int i = 0; i < EV_N; i++) hipEventDestroy(ix->ev[i]);
   for (int i = 0; i < 2; i++) {
@@ -1071,6 +1075,82 @@ extern "C" int tfidf_vocab_canonicalize_device(tfidf_index *ix, const void *d_al
   canon.release();
   ix->n_canon = nu;
   return TFIDF_OK;
+}
+
+extern "C" int tfidf_vocab_partition_device(tfidf_index *ix, uint32_t n_ranks, void *d_records, uint64_t cap,
+                                            uint64_t *counts, uint64_t *n_out) {
+  if (!ix || !n_out || !counts || n_ranks == 0) return fail(TFIDF_E_INVALID_ARG, "NULL argument or n_ranks == 0");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
+  DeviceGuard g(ix->cfg.device);
+  *n_out = ix->num_terms;
+  if (ix->num_terms > cap) return fail(TFIDF_E_BUFFER, "need %llu records", (unsigned long long)ix->num_terms);
+  if (ix->num_terms && !d_records) return fail(TFIDF_E_INVALID_ARG, "NULL records");
+  hipStream_t s = ix->stream;
+  HIP_TRY(ix->vcounts.reserve((size_t)n_ranks * 8));
+  HIP_TRY(ix->sent_slot.reserve(ix->num_terms * 4 + 4));
+  uint32_t *cnt = ix->vcounts.as<uint32_t>(), *cur = cnt + n_ranks;
+  HIP_TRY(hipMemsetAsync(cnt, 0, (size_t)n_ranks * 4, s));
+  HIP_TRY(vocab_count(ix->dict.as<uint64_t>(), ix->C, n_ranks, cnt, s));
+  std::vector<uint32_t> hc(n_ranks), start(n_ranks);
+  HIP_TRY(hipMemcpyAsync(hc.data(), cnt, (size_t)n_ranks * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  uint64_t acc = 0;
+  for (uint32_t r = 0; r < n_ranks; r++) { start[r] = (uint32_t)acc; counts[r] = hc[r]; acc += hc[r]; }
+  if (acc != ix->num_terms) return fail(TFIDF_E_STATE, "vocabulary count mismatch");
+  HIP_TRY(hipMemcpyAsync(cur, start.data(), (size_t)n_ranks * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(vocab_scatter(ix->dict.as<uint64_t>(), ix->df_dev(), ix->C, n_ranks, cur, (uint64_t *)d_records,
+                        ix->sent_slot.as<uint32_t>(), s));
+  HIP_TRY(hipStreamSynchronize(s));
+  ix->n_sent = acc;
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_vocab_reduce_device(tfidf_index *ix, const void *d_records, uint64_t n, void *d_df_out,
+                                         uint64_t *n_unique) {
+  if (!ix || !n_unique || (n && (!d_records || !d_df_out))) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DeviceGuard g(ix->cfg.device);
+  *n_unique = 0;
+  if (n == 0) return TFIDF_OK;
+  if (n >= (1ull << 30)) return fail(TFIDF_E_CAPACITY, "too many vocabulary records");
+  hipStream_t s = ix->stream;
+  uint64_t T = 1024;
+  while (T < 2 * n) T <<= 1;
+  HIP_TRY(ix->vt_table.reserve(T * 16));
+  HIP_TRY(ix->vt_sum.reserve(T * 4));
+  HIP_TRY(ix->vt_rslot.reserve(n * 4));
+  HIP_TRY(hipMemsetAsync(ix->vt_table.p, 0, T * 16, s));
+  HIP_TRY(hipMemsetAsync(ix->vt_sum.p, 0, T * 4, s));
+  HIP_TRY(ix->vcounts.reserve(64));
+  unsigned long long *nu = reinterpret_cast<unsigned long long *>(ix->vcounts.p);
+  HIP_TRY(hipMemsetAsync(nu, 0, 8, s));
+  HIP_TRY(vocab_reduce((const uint64_t *)d_records, n, ix->vt_table.as<uint64_t>(), (uint32_t)(T - 1),
+                       ix->vt_sum.as<uint32_t>(), ix->vt_rslot.as<uint32_t>(), (uint32_t *)d_df_out, nu, s));
+  HIP_TRY(hipMemcpyAsync(n_unique, nu, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_set_global_df_device(tfidf_index *ix, const void *d_df, uint64_t n, uint64_t doc_count,
+                                          uint64_t sum_ttf) {
+  if (!ix || (n && !d_df)) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
+  if (n != ix->n_sent) return fail(TFIDF_E_STATE, "expected %llu records (tfidf_vocab_partition_device)",
+                                   (unsigned long long)ix->n_sent);
+  DeviceGuard g(ix->cfg.device);
+  hipStream_t s = ix->stream;
+  HIP_TRY(ix->gdf_dev.reserve((size_t)ix->C * 4));
+  HIP_TRY(hipMemsetAsync(ix->gdf_dev.p, 0, (size_t)ix->C * 4, s));
+  HIP_TRY(vocab_import(ix->sent_slot.as<uint32_t>(), (const uint32_t *)d_df, n, ix->gdf_dev.as<uint32_t>(), s));
+  ix->gdf.resize(ix->C);
+  HIP_TRY(hipMemcpyAsync(ix->gdf.data(), ix->gdf_dev.p, (size_t)ix->C * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  ix->has_global = true;
+  ix->g_doc_count = doc_count;
+  ix->g_sum_ttf = sum_ttf;
+  return upload_cache(ix);
 }
 
 extern "C" int tfidf_set_global_stats_device(tfidf_index *ix, const void *d_df_canonical, uint64_t n_canonical,

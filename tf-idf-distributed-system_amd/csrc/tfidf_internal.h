@@ -130,9 +130,13 @@ struct QueryParams {
 hipError_t launch_score_blocks(const QueryParams &p, hipStream_t s);
 hipError_t launch_merge_topk(const QueryParams &p, hipStream_t s);
 
-// --- distributed vocabulary helpers (kernels_vocab.hip) ---
-hipError_t launch_vocab_export(const uint64_t *dict, const uint32_t *df, uint32_t C, uint64_t *keys_out,
-                               uint32_t *df_out, uint32_t *count, hipStream_t s);
+// --- GLOBAL statistics by term ownership (kernels_vocab.hip) ---
+hipError_t vocab_count(const uint64_t *dict, uint32_t C, uint32_t G, uint32_t *counts, hipStream_t s);
+hipError_t vocab_scatter(const uint64_t *dict, const uint32_t *df, uint32_t C, uint32_t G, uint32_t *cursor,
+                         uint64_t *records, uint32_t *sent_slot, hipStream_t s);
+hipError_t vocab_reduce(const uint64_t *records, uint64_t n, uint64_t *table, uint32_t tmask, uint32_t *sums,
+                        uint32_t *rslot, uint32_t *out, unsigned long long *n_unique, hipStream_t s);
+hipError_t vocab_import(const uint32_t *sent_slot, const uint32_t *gdf_in, uint64_t n, uint32_t *gdf, hipStream_t s);
 
 // --- synthetic corpus (kernels_synth.hip) ---
 hipError_t synth_doc_lengths(uint64_t seed, uint64_t n_docs, uint64_t doc_base, const double *cdf,

@@ -90,6 +90,9 @@ SIGNATURES = {
     "tfidf_vocab_export_device": (C.c_int, [VP, VP, VP, C.c_uint64, U64P]),
     "tfidf_vocab_canonicalize_device": (C.c_int, [VP, VP, C.c_uint64, VP, C.c_uint64, U64P]),
     "tfidf_set_global_stats_device": (C.c_int, [VP, VP, C.c_uint64, C.c_uint64, C.c_uint64]),
+    "tfidf_vocab_partition_device": (C.c_int, [VP, C.c_uint32, VP, C.c_uint64, U64P, U64P]),
+    "tfidf_vocab_reduce_device": (C.c_int, [VP, VP, C.c_uint64, VP, U64P]),
+    "tfidf_set_global_df_device": (C.c_int, [VP, VP, C.c_uint64, C.c_uint64, C.c_uint64]),
     "tfidf_set_global_stats": (C.c_int, [VP, U64P, U64P, C.c_uint64, C.c_uint64, C.c_uint64]),
     "tfidf_clear_global_stats": (C.c_int, [VP]),
     "tfidf_term_key": (C.c_int, [C.c_char_p, C.c_uint64, U64P, U64P]),

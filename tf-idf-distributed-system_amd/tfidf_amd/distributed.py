@@ -7,10 +7,12 @@ Two modes:
     scores with its own statistics; results are merged by document name.
     No data-path collective.
   * GLOBAL (the reference's 1-worker semantics on a sharded corpus):
-      1. vocabulary agreement: all-gather every shard's sorted term keys,
-         sorted union on device -> canonical term ids;
-      2. all-reduce (SUM) of the canonical DF vector + {docCount, sumTTF};
-      3. per-rank top-k with global doc ids (shard base + local), all-gather,
+      1. term ownership: every shard sends its (term key, df) records to the
+         term's owner rank (all-to-all); the owner sums df over identical keys
+         on device and answers record by record (all-to-all back);
+         {docCount, sumTTF} are all-reduced (SUM).  O(vocabulary) per rank.
+         (global_commit_canonical is the older all-gather + sorted-union form.)
+      2. per-rank top-k with global doc ids (shard base + local), all-gather,
          merge by (score desc, doc asc).
 
 The engine is passed in as an adapter (HipShardAdapter in production; the
@@ -47,6 +49,27 @@ class HipShardAdapter:
         n = self.shard.vocab_canonicalize_device(all_keys.data_ptr(), m, dfc.data_ptr(), max(m, 1))
         return dfc[:n]
 
+    def vocab_partition(self, n_ranks):
+        """-> (records int64 [n, 3] (lo, hi, df) grouped by owner, counts list)."""
+        n = self.shard.vocab_size()
+        rec = torch.zeros((max(n, 1), 3), dtype=torch.int64, device=self.device)
+        torch.cuda.synchronize(self.device)
+        n2, counts = self.shard.vocab_partition_device(n_ranks, rec.data_ptr(), max(n, 1))
+        return rec[:n2], [int(c) for c in counts]
+
+    def vocab_reduce(self, records):
+        """Owner side: (summed df int32 for every received record, distinct terms)."""
+        records = records.contiguous()
+        out = torch.zeros(max(records.shape[0], 1), dtype=torch.int32, device=self.device)
+        torch.cuda.synchronize(self.device)
+        nu = self.shard.vocab_reduce_device(records.data_ptr(), records.shape[0], out.data_ptr())
+        return out[:records.shape[0]], nu
+
+    def import_global_df(self, gdf, doc_count, sum_ttf):
+        gdf = gdf.contiguous()
+        torch.cuda.synchronize(self.device)
+        self.shard.set_global_df_device(gdf.data_ptr(), gdf.shape[0], doc_count, sum_ttf)
+
     def import_global(self, dfc, doc_count, sum_ttf):
         dfc = dfc.contiguous()
         torch.cuda.synchronize(self.device)
@@ -66,8 +89,42 @@ def _dev(adapter):
     return adapter.device if isinstance(adapter.device, torch.device) else torch.device(adapter.device)
 
 
+def _a2a(out, inp, out_splits, in_splits, group):
+    """all_to_all_single; gloo (CPU rehearsal) needs host tensors."""
+    if dist.get_backend(group) == "gloo" and inp.is_cuda:
+        o = out.cpu()
+        dist.all_to_all_single(o, inp.cpu(), output_split_sizes=out_splits, input_split_sizes=in_splits,
+                               group=group)
+        out.copy_(o)
+    else:
+        dist.all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits, group=group)
+
+
 def global_commit(adapter, group=None):
-    """Steps 1-2 of GLOBAL mode.  Call after the shard's own commit."""
+    """Step 1 of GLOBAL mode (term ownership).  Call after the shard's own
+    commit.  Returns (global vocabulary size, docCount, sumTTF)."""
+    dev = _dev(adapter)
+    ws = dist.get_world_size(group)
+    rec, counts = adapter.vocab_partition(ws)
+    cnt = torch.tensor(counts, dtype=torch.int64, device=dev)
+    rcnt = torch.empty_like(cnt)
+    _a2a(rcnt, cnt, None, None, group)
+    rcounts = [int(x) for x in rcnt.tolist()]
+    recv = torch.empty((sum(rcounts), 3), dtype=torch.int64, device=dev)
+    _a2a(recv, rec.contiguous(), rcounts, counts, group)
+    ans, n_own = adapter.vocab_reduce(recv)
+    back = torch.empty(sum(counts), dtype=torch.int32, device=dev)
+    _a2a(back, ans.contiguous(), counts, rcounts, group)
+    dc, ttf, _ = adapter.local_stats()
+    st = torch.tensor([dc, ttf, n_own], dtype=torch.int64, device=dev)
+    dist.all_reduce(st, op=dist.ReduceOp.SUM, group=group)
+    adapter.import_global_df(back, int(st[0].item()), int(st[1].item()))
+    return int(st[2].item()), int(st[0].item()), int(st[1].item())
+
+
+def global_commit_canonical(adapter, group=None):
+    """All-gather + sorted-union form of GLOBAL statistics (canonical term
+    ids; O(G x vocabulary) per rank).  Same results as global_commit."""
     dev = _dev(adapter)
     ws = dist.get_world_size(group)
     keys, df = adapter.export_vocab()

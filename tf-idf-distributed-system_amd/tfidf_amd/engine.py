@@ -184,6 +184,24 @@ class ShardIndex:
         L.check(L.load().tfidf_set_global_stats_device(self._h, C.c_void_p(d_df_canon), n_canon, doc_count,
                                                        sum_ttf))
 
+    def vocab_partition_device(self, n_ranks, d_records, cap):
+        """Records (lo, hi, df) grouped by owner rank -> (n, counts[n_ranks])."""
+        counts = np.zeros(n_ranks, np.uint64)
+        n = C.c_uint64()
+        L.check(L.load().tfidf_vocab_partition_device(self._h, n_ranks, C.c_void_p(d_records), cap,
+                                                      L.ptr(counts, C.c_uint64), C.byref(n)))
+        return n.value, counts
+
+    def vocab_reduce_device(self, d_records, n, d_df_out):
+        """-> distinct terms among the records."""
+        u = C.c_uint64()
+        L.check(L.load().tfidf_vocab_reduce_device(self._h, C.c_void_p(d_records), n, C.c_void_p(d_df_out),
+                                                   C.byref(u)))
+        return u.value
+
+    def set_global_df_device(self, d_df, n, doc_count, sum_ttf):
+        L.check(L.load().tfidf_set_global_df_device(self._h, C.c_void_p(d_df), n, doc_count, sum_ttf))
+
     def set_global_stats(self, keys_lohi, df, doc_count, sum_ttf):
         keys_lohi = np.ascontiguousarray(keys_lohi, np.uint64).reshape(-1)
         df = np.ascontiguousarray(df, np.uint64)
