@@ -654,7 +654,7 @@ __device__ __forceinline__ void hist_batch(WaveSmem &sm, const BuildParams &p, u
     const uint32_t P = (uint32_t)__builtin_amdgcn_readlane((int)pincl, 63);
     if (P == 0) return;
     if (round >= kWaveSlots) { overflow = true; return; }
-    if ((round >= 1 && P <= kWaveQueue) || K <= 2) {
+    if (P <= kWaveQueue) {                                // few left: two-per-lane queue
       // retry queue: two unresolved tokens per lane, probed until resolved
       uint32_t at = pincl - np;
 #pragma unroll
@@ -679,6 +679,7 @@ __device__ __forceinline__ void hist_batch(WaveSmem &sm, const BuildParams &p, u
         for (int i = 0; i < 2; i++)
           old[i] = atomicCAS(qp[i] ? reinterpret_cast<unsigned long long *>(&sm.key[qs[i]]) : noop,
                              qp[i] ? 0ull : ~0ull, (unsigned long long)qk[i]);
+        __builtin_amdgcn_sched_barrier(0);     // every CAS issued before the first result is waited on
 #pragma unroll
         for (int i = 0; i < 2; i++) {
           bool hit = qp[i] & ((old[i] == 0) | (old[i] == qk[i]));
@@ -705,6 +706,10 @@ __device__ __forceinline__ void hist_batch(WaveSmem &sm, const BuildParams &p, u
       old[k] = atomicCAS(pend ? reinterpret_cast<unsigned long long *>(&sm.key[slot[k]]) : noop,
                          pend ? 0ull : ~0ull, (unsigned long long)tkey[k]);
     }
+    // keep all K returning CASes in flight together: without this barrier the
+    // scheduler interleaves each result's compare and so waits out every round
+    // trip in turn (measured: K serialized LDS latencies per probe round)
+    __builtin_amdgcn_sched_barrier(0);
     uint32_t foldm = 0;
 #pragma unroll
     for (int k = 0; k < K; k++) {
