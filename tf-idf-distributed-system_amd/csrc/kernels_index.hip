@@ -27,6 +27,7 @@
 
 #include "dict_device.h"
 #include "tfidf_common.h"
+#include "wave_ops.h"
 #include "tfidf_internal.h"
 
 namespace tfidf {
@@ -1417,33 +1418,6 @@ __global__ void k_block_base(PostingParams p) {
 //                    written inside the stream's own region.
 constexpr uint32_t kSubSlots = 512;
 constexpr uint32_t kSubBits = 9;
-
-// Lanes of the wave holding the same BITS-bit key (active lanes only): one
-// ballot per key bit.  Used to turn same-address LDS atomics (hot terms hit
-// one cursor from most lanes of a wave) into one atomic per distinct key.
-template <int BITS>
-__device__ __forceinline__ uint64_t peer_mask(uint32_t key) {
-  uint64_t peers = __ballot(1);
-#pragma unroll
-  for (int b = 0; b < BITS; b++) {
-    const uint64_t m = __ballot((key >> b) & 1u);
-    peers &= ((key >> b) & 1u) ? m : ~m;
-  }
-  return peers;
-}
-
-// Wave-aggregated cursor bump: returns the old cursor value + this lane's rank
-// among its peers (same result as one atomicAdd(cur + key, 1) per lane).
-template <int BITS>
-__device__ __forceinline__ uint32_t cursor_bump(uint32_t *cur, uint32_t key, uint32_t lane) {
-  const uint64_t peers = peer_mask<BITS>(key);
-  const uint32_t rank = (uint32_t)__popcll(peers & ((1ull << lane) - 1));
-  const uint32_t leader = (uint32_t)__builtin_ctzll(peers);
-  uint32_t base = 0;
-  if (rank == 0) base = atomicAdd(cur + key, (uint32_t)__popcll(peers));
-  base = (uint32_t)__shfl((int)base, (int)leader, 64);
-  return base + rank;
-}
 
 __device__ __forceinline__ void part_entries(const PostingParams &p, uint32_t *bcur, uint32_t rmask, uint64_t bb,
                                              const InvGroup &g, uint64_t dd, uint32_t d0l, uint32_t stride,

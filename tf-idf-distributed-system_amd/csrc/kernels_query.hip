@@ -130,7 +130,7 @@ struct ScoreSmem {
   float cache[256];
   uint32_t hist[256];
   uint32_t scan[16];
-  uint32_t nhit, prefix, remaining, outn;
+  uint32_t nhit, prefix, remaining, outn, smin, smax, flag;
 };
 
 // Hits are enumerated from the bitmap: thread t owns docs [16 t, 16 t + 16)
@@ -150,7 +150,8 @@ __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
   const uint32_t k = p.k;
   for (uint32_t q = q0; q < q1; q++) {
     for (uint32_t i = tid; i < kBlockDocs / 32; i += blockDim.x) sm.hitbits[i] = 0;
-    if (tid == 0) { sm.nhit = 0; sm.outn = 0; }
+    for (uint32_t i = tid; i < 256; i += blockDim.x) sm.hist[i] = 0;
+    if (tid == 0) { sm.nhit = 0; sm.outn = 0; sm.smin = 0xFFFFFFFFu; sm.smax = 0; }
     __syncthreads();
     const uint32_t t0 = p.q_off[q], t1 = p.q_off[q + 1];
     if (p.toff) {
@@ -263,44 +264,79 @@ __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
       __syncthreads();
       continue;
     }
-    // radix select: threshold T = k-th largest score bits
-    if (tid == 0) { sm.prefix = 0; sm.remaining = k; }
-    for (int pass = 0; pass < 4; pass++) {
-      const int sh = 24 - 8 * pass;
-      for (uint32_t i = tid; i < 256; i += blockDim.x) sm.hist[i] = 0;
-      __syncthreads();
-      const uint32_t prefix = sm.prefix;
-      const uint32_t hmask = pass == 0 ? 0u : (0xFFFFFFFFu << (sh + 8));
+    // Radix select of the k-th largest score bits, starting at the byte of the
+    // highest bit on which the block's hits differ (scores share sign and
+    // most exponent bits) and stopping as soon as the boundary bin holds
+    // exactly the entries still needed.  Scores are converted to float bits
+    // once, in place (low word of acc[ld]).
+    uint32_t mn = 0xFFFFFFFFu, mx = 0;
+    for (uint32_t x = bits; x; x &= x - 1) {
+      const uint32_t ld = tid * kDocsPerThread + (__ffs(x) - 1);
+      const uint32_t sb = __float_as_uint((float)sm.acc[ld]);
+      reinterpret_cast<uint32_t *>(&sm.acc[ld])[0] = sb;
+      mn = min(mn, sb);
+      mx = max(mx, sb);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {                     // wave min/max, then one LDS atomic per wave
+      mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, 64));
+      mx = max(mx, (uint32_t)__shfl_xor((int)mx, o, 64));
+    }
+    if ((tid & 63) == 0 && mx) { atomicMin(&sm.smin, mn); atomicMax(&sm.smax, mx); }
+    __syncthreads();
+    // bits [r, 32) are common to all hits / resolved; each pass takes the next
+    // (up to) 8 bits below r as the digit, so the first digit is the top 8
+    // bits on which the hits differ
+    const uint32_t diff = sm.smin ^ sm.smax;
+    int r = diff ? 32 - __builtin_clz(diff) : 0;
+    uint32_t prefix = r < 32 ? sm.smax & (0xFFFFFFFFu << r) : 0u;
+    uint32_t rem = k;
+    bool all_bin = false;                                  // boundary bin entirely taken
+    // hist is zero here (cleared at the query start, and by wave 0 after each
+    // selection), so a pass costs two barriers: histogram, selection
+    while (r > 0) {
+      const int w = r < 8 ? r : 8, sh = r - w;
+      const uint32_t hmask = r < 32 ? (0xFFFFFFFFu << r) : 0u;
       for (uint32_t x = bits; x; x &= x - 1) {
-        const uint32_t sb = __float_as_uint((float)sm.acc[tid * kDocsPerThread + (__ffs(x) - 1)]);
-        if ((sb & hmask) == (prefix & hmask)) atomicAdd(&sm.hist[(sb >> sh) & 255u], 1u);
+        const uint32_t sb = reinterpret_cast<const uint32_t *>(&sm.acc[tid * kDocsPerThread + (__ffs(x) - 1)])[0];
+        if ((sb & hmask) == prefix) atomicAdd(&sm.hist[(sb >> sh) & ((1u << w) - 1)], 1u);
       }
       __syncthreads();
       if (tid < 64) {
-        const uint32_t rem = sm.remaining;
         uint32_t above;
         const uint32_t bin = wave_select_bin(sm.hist, rem, &above);
+        const uint32_t inbin = sm.hist[bin];
+#pragma unroll
+        for (int i = 0; i < 4; i++) sm.hist[tid + 64 * i] = 0;
         if (tid == 0) {
           sm.prefix = prefix | (bin << sh);
           sm.remaining = rem - above;
+          sm.flag = inbin == rem - above;
         }
       }
       __syncthreads();
+      prefix = sm.prefix;
+      rem = sm.remaining;
+      all_bin = sm.flag != 0;
+      r = sh;
+      if (all_bin) break;
     }
-    const uint32_t T = sm.prefix, take_ties = sm.remaining;
-    // collection in ascending doc order
+    // T = prefix over bits [r, 32): keys above it are taken, keys in it are all
+    // taken (all_bin) or, fully resolved (r = 0), ties in doc order
+    const uint32_t tmask = 0xFFFFFFFFu << r;
+    const uint32_t T = prefix, take_ties = all_bin ? 0xFFFFFFFFu : rem;
     uint32_t nties = 0;
     for (uint32_t x = bits; x; x &= x - 1) {
       const uint32_t ld = tid * kDocsPerThread + (__ffs(x) - 1);
-      nties += __float_as_uint((float)sm.acc[ld]) == T;
+      nties += (reinterpret_cast<const uint32_t *>(&sm.acc[ld])[0] & tmask) == T;
     }
     uint32_t tot;
     uint32_t tie_rank = block_excl_scan(nties, sm.scan, &tot);
     for (uint32_t x = bits; x; x &= x - 1) {
       const uint32_t ld = tid * kDocsPerThread + (__ffs(x) - 1);
-      const uint32_t sb = __float_as_uint((float)sm.acc[ld]);
-      bool take = sb > T;
-      if (sb == T) take = tie_rank++ < take_ties;
+      const uint32_t sb = reinterpret_cast<const uint32_t *>(&sm.acc[ld])[0];
+      bool take = (sb & tmask) > T;
+      if ((sb & tmask) == T) take = tie_rank++ < take_ties;
       if (take) cand[atomicAdd(&sm.outn, 1u)] = ((uint64_t)sb << 32) | (uint64_t)(~(uint32_t)(d0 + ld));
     }
     __syncthreads();
@@ -309,13 +345,19 @@ __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
   }
 }
 
-// One workgroup (1024 threads) per query.
+// One workgroup (1024 threads) per query.  Candidates are read flat (thread t
+// takes slots t, t + 1024, ... of the [block][k] candidate array) and kept in
+// registers when there are at most 4 per thread; radix select from the first
+// byte on which the candidates differ, stopping once the boundary bin is
+// entirely needed.  Keys (score bits << 32 | ~doc) are unique.
 struct MergeSmem {
   uint64_t keys[1024];
   uint32_t hist[256];
-  uint64_t prefix;
-  uint32_t remaining, outn;
+  uint64_t prefix, kmin, kmax;
+  uint32_t remaining, outn, total, all_bin;
 };
+
+constexpr int kMergeRegs = 4;
 
 __global__ void __launch_bounds__(1024) k_merge_topk(QueryParams p) {
   __shared__ MergeSmem sm;
@@ -323,45 +365,91 @@ __global__ void __launch_bounds__(1024) k_merge_topk(QueryParams p) {
   const uint32_t nb = p.n_blocks;
   const uint64_t *cand = p.cand + (size_t)q * nb * k;
   const uint32_t *cn = p.cand_n + (size_t)q * nb;
-  // total candidates
-  uint32_t M = 0;
-  for (uint32_t b = 0; b < nb; b++) M += cn[b];
-  const uint32_t kk = M < k ? M : k;
-  if (tid == 0) { sm.prefix = 0; sm.remaining = kk; sm.outn = 0; }
+  const uint32_t nflat = nb * k;
+  if (tid == 0) { sm.total = 0; sm.outn = 0; sm.kmin = ~0ull; sm.kmax = 0; sm.all_bin = 0; }
+  for (uint32_t i = tid; i < 256; i += blockDim.x) sm.hist[i] = 0;
   __syncthreads();
+  uint32_t part = 0;
+  for (uint32_t b = tid; b < nb; b += blockDim.x) part += cn[b];
+  if (part) atomicAdd(&sm.total, part);
+  auto key_at = [&](uint32_t f) -> uint64_t {
+    const uint32_t b = f / k, i = f - b * k;
+    return i < cn[b] ? cand[f] : 0ull;                     // 0 = empty (real keys have score bits > 0)
+  };
+  const bool inreg = nflat <= kMergeRegs * blockDim.x;
+  uint64_t kr[kMergeRegs];
+  uint64_t lmin = ~0ull, lmax = 0;
+#pragma unroll
+  for (int r = 0; r < kMergeRegs; r++) {
+    const uint32_t f = tid + r * blockDim.x;
+    kr[r] = inreg && f < nflat ? key_at(f) : 0ull;
+    if (kr[r]) { lmin = min(lmin, kr[r]); lmax = max(lmax, kr[r]); }
+  }
+  if (!inreg)
+    for (uint32_t f = tid; f < nflat; f += blockDim.x) {
+      const uint64_t key = key_at(f);
+      if (key) { lmin = min(lmin, key); lmax = max(lmax, key); }
+    }
+  if (lmax) {
+    atomicMin(reinterpret_cast<unsigned long long *>(&sm.kmin), (unsigned long long)lmin);
+    atomicMax(reinterpret_cast<unsigned long long *>(&sm.kmax), (unsigned long long)lmax);
+  }
+  __syncthreads();
+  const uint32_t M = sm.total;
+  const uint32_t kk = M < k ? M : k;
+  uint64_t T = 0, tmask = ~0ull;                          // take (key & tmask) >= T
   if (M > k) {
-    for (int pass = 0; pass < 8; pass++) {
-      const int sh = 56 - 8 * pass;
-      for (uint32_t i = tid; i < 256; i += blockDim.x) sm.hist[i] = 0;
-      __syncthreads();
-      const uint64_t prefix = sm.prefix;
-      const uint64_t hmask = pass == 0 ? 0ull : (~0ull << (sh + 8));
-      for (uint32_t b = 0; b < nb; b++) {
-        const uint32_t n = cn[b];
-        for (uint32_t i = tid; i < n; i += blockDim.x) {
-          const uint64_t key = cand[(size_t)b * k + i];
-          if ((key & hmask) == (prefix & hmask)) atomicAdd(&sm.hist[(key >> sh) & 255u], 1u);
+    const uint64_t diff = sm.kmin ^ sm.kmax;                // != 0: keys are unique
+    int rb = 64 - __builtin_clzll(diff);                    // bits [rb, 64) common / resolved
+    uint64_t prefix = rb < 64 ? sm.kmax & (~0ull << rb) : 0ull;
+    uint32_t rem = kk;
+    while (rb > 0) {                                        // hist is zero (cleared at start / by wave 0)
+      const int w = rb < 8 ? rb : 8, sh = rb - w;
+      const uint64_t hmask = rb < 64 ? (~0ull << rb) : 0ull;
+      const uint32_t dmask = (1u << w) - 1;
+      if (inreg) {
+#pragma unroll
+        for (int r = 0; r < kMergeRegs; r++)
+          if (kr[r] && (kr[r] & hmask) == prefix) atomicAdd(&sm.hist[(uint32_t)(kr[r] >> sh) & dmask], 1u);
+      } else {
+        for (uint32_t f = tid; f < nflat; f += blockDim.x) {
+          const uint64_t key = key_at(f);
+          if (key && (key & hmask) == prefix) atomicAdd(&sm.hist[(uint32_t)(key >> sh) & dmask], 1u);
         }
       }
       __syncthreads();
       if (tid < 64) {
-        const uint32_t rem = sm.remaining;
         uint32_t above;
         const uint32_t bin = wave_select_bin(sm.hist, rem, &above);
+        const uint32_t inbin = sm.hist[bin];
+#pragma unroll
+        for (int i = 0; i < 4; i++) sm.hist[tid + 64 * i] = 0;
         if (tid == 0) {
           sm.prefix = prefix | ((uint64_t)bin << sh);
           sm.remaining = rem - above;
+          sm.all_bin = inbin == rem - above;
         }
       }
       __syncthreads();
+      prefix = sm.prefix;
+      rem = sm.remaining;
+      rb = sh;
+      if (sm.all_bin != 0) break;
     }
+    tmask = ~0ull << rb;
+    T = prefix;
   }
-  const uint64_t T = (M > k) ? sm.prefix : 0ull;   // keys are unique: take key >= T
-  for (uint32_t b = 0; b < nb; b++) {
-    const uint32_t n = cn[b];
-    for (uint32_t i = tid; i < n; i += blockDim.x) {
-      const uint64_t key = cand[(size_t)b * k + i];
-      if (key >= T) {
+  if (inreg) {
+#pragma unroll
+    for (int r = 0; r < kMergeRegs; r++)
+      if (kr[r] && (kr[r] & tmask) >= T) {
+        const uint32_t pos = atomicAdd(&sm.outn, 1u);
+        if (pos < 1024) sm.keys[pos] = kr[r];
+      }
+  } else {
+    for (uint32_t f = tid; f < nflat; f += blockDim.x) {
+      const uint64_t key = key_at(f);
+      if (key && (key & tmask) >= T) {
         const uint32_t pos = atomicAdd(&sm.outn, 1u);
         if (pos < 1024) sm.keys[pos] = key;
       }

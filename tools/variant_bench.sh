@@ -7,7 +7,7 @@ L=tf-idf-distributed-system_amd/lib/libtfidf.so
 cp $L /tmp/libtfidf_base.so
 for v in base tools/variants/*.so; do
   if [ "$v" = base ]; then cp /tmp/libtfidf_base.so $L; else cp $v $L; fi
-  timeout -k 10 200 python -u bench.py --steps 3 --warmup 1 --no-queries --cpu-sample 0 > gpurun_out/var.log 2>&1 || { echo "$v failed"; tail -3 gpurun_out/var.log; cp /tmp/libtfidf_base.so $L; exit 1; }
-  python3 -c "import json; r=json.loads(open('gpurun_out/var.log').read().strip().splitlines()[-1]); print('%-40s' % '$v', {k: round(v, 3) for k, v in r['phases_ms'].items()})"
+  timeout -k 10 200 python -u bench.py --steps 3 --warmup 1 ${VAR_QUERIES:---no-queries} --no-e2e --cpu-sample 0 > gpurun_out/var.log 2>&1 || { echo "$v failed"; tail -3 gpurun_out/var.log; cp /tmp/libtfidf_base.so $L; exit 1; }
+  python3 -c "import json; r=json.loads(open('gpurun_out/var.log').read().strip().splitlines()[-1]); print('%-40s' % '$v', {k: round(v, 3) for k, v in r['phases_ms'].items()}, r.get('queries'))"
 done
 cp /tmp/libtfidf_base.so $L
