@@ -139,16 +139,31 @@ struct ScoreSmem {
 // footprint (66 KiB) admits two workgroups per CU.
 __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
   __shared__ ScoreSmem sm;
-  const uint32_t b = blockIdx.x, tid = threadIdx.x;
+  const uint32_t tid = threadIdx.x;
   const uint32_t q0 = blockIdx.y * p.q_chunk;
   const uint32_t q1 = min(p.n_q, q0 + p.q_chunk);
-  const uint64_t d0 = (uint64_t)b * kBlockDocs;
-  const uint64_t bb = p.toff ? 0 : p.bbase[b];
-  const uint64_t bend = p.toff ? 0 : p.bbase[b + 1];
-  const uint32_t *row = p.toff ? nullptr : p.blk + (size_t)b * p.C;
   for (uint32_t i = tid; i < 256; i += blockDim.x) sm.cache[i] = p.cache[i];
   const uint32_t k = p.k;
-  for (uint32_t q = q0; q < q1; q++) {
+  // grid mode: workgroup (block, query chunk); list mode (ovf_list): persistent
+  // workgroups over the pairs k_score_pairs left (too many postings)
+  const bool listmode = p.ovf_list != nullptr;
+  const uint32_t n_it = listmode ? 0xFFFFFFFFu : (q1 > q0 ? q1 - q0 : 0u);
+  for (uint32_t it = 0; it < n_it; it++) {
+    uint32_t q, b;
+    if (listmode) {
+      const uint32_t idx = blockIdx.x + it * gridDim.x;
+      if (idx >= *p.ovf_count) break;                                 // uniform
+      const uint32_t pr = p.ovf_list[idx];
+      q = pr / p.n_blocks;
+      b = pr - q * p.n_blocks;
+    } else {
+      q = q0 + it;
+      b = blockIdx.x;
+    }
+    const uint64_t d0 = (uint64_t)b * kBlockDocs;
+    const uint64_t bb = p.toff ? 0 : p.bbase[b];
+    const uint64_t bend = p.toff ? 0 : p.bbase[b + 1];
+    const uint32_t *row = p.toff ? nullptr : p.blk + (size_t)b * p.C;
     for (uint32_t i = tid; i < kBlockDocs / 32; i += blockDim.x) sm.hitbits[i] = 0;
     for (uint32_t i = tid; i < 256; i += blockDim.x) sm.hist[i] = 0;
     if (tid == 0) { sm.nhit = 0; sm.outn = 0; sm.smin = 0xFFFFFFFFu; sm.smax = 0; }
@@ -482,7 +497,218 @@ __global__ void __launch_bounds__(1024) k_merge_topk(QueryParams p) {
   if (tid == 0) p.out_n[q] = kk;
 }
 
+// ---------------------------------------------------------------------------
+// Wave per (doc block, query) pair — the batched path.  A query's postings in
+// one 8192-doc block are few (cfg 4: ~500), so instead of a dense 64 KiB
+// accumulator and ~14 workgroup barriers per pair, one wavefront scores the
+// pair into a private 1024-slot LDS hash table (doc -> double) and selects the
+// block's top-k with wave-level radix passes over unique 64-bit keys
+// (score bits << 32 | ~doc: (score desc, doc asc) is plain key order, so ties
+// need no extra pass).  No workgroup barrier after the set-up; 12 waves per
+// CU hide the LDS/HBM latencies.  Pairs with more than kPairMaxPost postings
+// are appended to ovf_list and left to k_score_blocks (list mode).  Term order per document is
+// the query order (the wave processes terms in sequence), so each score is the
+// same double sum as the dense path.
+constexpr uint32_t kPairSlots = 1024;
+constexpr uint32_t kPairMaxPost = 768;
+constexpr uint32_t kPairWaves = kPairWavesPerWG;
+constexpr uint32_t kPairEmpty = 0xFFFFFFFFu;
+
+struct PairSmem {
+  uint32_t key[kPairWaves][kPairSlots];           // doc - d0 per slot (kPairEmpty = free)
+  double val[kPairWaves][kPairSlots];             // score sum per slot
+  uint32_t hist[kPairWaves][256];
+  uint32_t list[kPairWaves][kPairMaxPost / 2];    // claimed slots (u16), in claim order
+  float cache[256];
+};
+
+__global__ void __launch_bounds__(kPairWaves * 64) k_score_pairs(QueryParams p) {
+  __shared__ PairSmem sm;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) sm.cache[i] = p.cache[i];
+  for (uint32_t i = lane; i < 256; i += 64) sm.hist[w][i] = 0;
+  __syncthreads();
+  uint32_t *key = sm.key[w];
+  double *val = sm.val[w];
+  uint32_t *hist = sm.hist[w];
+  const uint32_t nb = p.n_blocks, k = p.k;
+  const uint64_t npairs = (uint64_t)p.n_q * nb;
+  for (uint64_t pr = (uint64_t)blockIdx.x * kPairWaves + w; pr < npairs; pr += (uint64_t)gridDim.x * kPairWaves) {
+    const uint32_t q = (uint32_t)(pr / nb), b = (uint32_t)(pr - (uint64_t)q * nb);
+    const uint32_t d0 = b * kBlockDocs;
+    const uint32_t t0 = p.q_off[q], t1 = p.q_off[q + 1];
+    // ranges of the first 64 terms (lane j holds term j); longer queries go dense
+    uint64_t a = 0, z = 0;
+    float tw = 0.f;
+    const uint32_t nt = t1 - t0;
+    if (nt > 64) { if (lane == 0) p.ovf_list[atomicAdd(p.ovf_count, 1u)] = (uint32_t)pr; continue; }
+    if (p.toff) {
+      for (uint32_t j = 0; j < nt; j++) {
+        const uint32_t slot = p.q_slot[t0 + j];
+        uint64_t ja = 0, jz = 0;
+        if (slot != kInvalidSlot) term_block_range(p, slot, d0, &ja, &jz);
+        if (lane == j) { a = ja; z = jz; }
+      }
+    } else if (lane < nt) {
+      const uint32_t slot = p.q_slot[t0 + lane];
+      if (slot != kInvalidSlot) {
+        const uint32_t *row = p.blk + (size_t)b * p.C;
+        const uint64_t bb = p.bbase[b];
+        a = bb + row[slot];
+        z = slot + 1 < p.C ? bb + row[slot + 1] : p.bbase[b + 1];
+      }
+    }
+    if (lane < nt) tw = p.q_w[t0 + lane];
+    uint32_t P = (uint32_t)(z - a);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) P += (uint32_t)__shfl_xor((int)P, o, 64);
+    uint64_t *cand = p.cand + pr * k;
+    if (P > kPairMaxPost) { if (lane == 0) p.ovf_list[atomicAdd(p.ovf_count, 1u)] = (uint32_t)pr; continue; }
+    if (P == 0) { if (lane == 0) p.cand_n[pr] = 0; continue; }
+    // the first two 64-posting chunks of the first kQTermsFast terms: all in
+    // flight before the table is cleared (one HBM latency for a typical pair)
+    uint64_t pre[kQTermsFast][2];
+#pragma unroll
+    for (uint32_t j = 0; j < kQTermsFast; j++) {
+      const uint64_t ja = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(a >> 32), j) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a, j);
+      const uint64_t jz = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(z >> 32), j) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)z, j);
+#pragma unroll
+      for (uint32_t c = 0; c < 2; c++) {
+        const uint64_t i = ja + lane + 64 * c;
+        pre[j][c] = (j < nt && i < jz) ? p.post[i] : 0ull;
+      }
+    }
+    {
+      uint4 *kw = reinterpret_cast<uint4 *>(key);
+#pragma unroll
+      for (int i = 0; i < (int)(kPairSlots / 4 / 64); i++)
+        kw[lane + 64 * i] = make_uint4(kPairEmpty, kPairEmpty, kPairEmpty, kPairEmpty);
+    }
+    uint32_t nhit = 0;
+    uint32_t nlist = 0;                                          // wave-uniform count of claimed slots
+    uint16_t *list = reinterpret_cast<uint16_t *>(sm.list[w]);
+    // insert one posting per lane (inactive lanes: e = 0 and act = false);
+    // claimed slots are appended to the wave's hit list
+    auto insert = [&](uint64_t e, bool act, float wj) {
+      uint32_t claimed = kPairEmpty;
+      if (act) {
+        const uint32_t ld = (uint32_t)e - d0;
+        const uint32_t tfn = (uint32_t)(e >> 32);
+        const float sc = bm25_term(wj, tfn >> 8, sm.cache[tfn & 255u]);
+        uint32_t slot = (ld * 0x9E3779B1u) >> 22;
+        for (;;) {
+          const uint32_t old = atomicCAS(&key[slot], kPairEmpty, ld);
+          if (old == kPairEmpty) { val[slot] = (double)sc; claimed = slot; break; }
+          if (old == ld) { val[slot] += (double)sc; break; }
+          slot = (slot + 1) & (kPairSlots - 1);
+        }
+      }
+      const bool c = claimed != kPairEmpty;
+      const uint64_t m = __ballot(c);
+      if (c) list[nlist + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint16_t)claimed;
+      nlist += (uint32_t)__popcll(m);
+    };
+    for (uint32_t j = 0; j < nt; j++) {
+      const uint64_t ja = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(a >> 32), j) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a, j);
+      const uint64_t jz = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(z >> 32), j) << 32) |
+                          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)z, j);
+      const float wj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tw), j));
+      uint64_t i0 = ja;
+      if (j < kQTermsFast) {
+        uint64_t e0 = 0, e1 = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < kQTermsFast; u++)
+          if (u == j) { e0 = pre[u][0]; e1 = pre[u][1]; }
+        insert(e0, ja + lane < jz, wj);
+        if (ja + 64 < jz) insert(e1, ja + 64 + lane < jz, wj);     // uniform
+        i0 = ja + 128;
+      }
+      // remaining chunks, four loads in flight per step
+      for (; i0 < jz; i0 += 256) {
+        uint64_t e[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const uint64_t i = i0 + 64 * u + lane;
+          e[u] = i < jz ? p.post[i] : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+          if (i0 + 64 * u < jz) insert(e[u], i0 + 64 * u + lane < jz, wj);
+      }
+    }
+    nhit = nlist;
+    // this lane's hits as selection keys, in registers
+    constexpr int kPer = (int)((kPairMaxPost + 63) / 64);
+    uint64_t kv[kPer];
+    uint64_t kmin = ~0ull, kmax = 0;
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+      const uint32_t idx = lane + 64 * u;
+      kv[u] = 0;
+      if (idx < nhit) {
+        const uint32_t slot = list[idx];
+        kv[u] = ((uint64_t)__float_as_uint((float)val[slot]) << 32) | (uint64_t)(~(d0 + key[slot]));
+        kmin = min(kmin, kv[u]);
+        kmax = max(kmax, kv[u]);
+      }
+    }
+    uint64_t T = 0, tmask = ~0ull;                         // take (key & tmask) >= T
+    if (nhit > k) {
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        kmin = min(kmin, (uint64_t)__shfl_xor((long long)kmin, o, 64));
+        kmax = max(kmax, (uint64_t)__shfl_xor((long long)kmax, o, 64));
+      }
+      int rb = 64 - __builtin_clzll(kmin ^ kmax);          // keys unique and nhit > k >= 1: kmin != kmax
+      uint64_t prefix = rb < 64 ? kmax & (~0ull << rb) : 0ull;
+      uint32_t rem = k;
+      while (rb > 0) {
+        const int wd = rb < 8 ? rb : 8, sh = rb - wd;
+        const uint64_t hmask = rb < 64 ? (~0ull << rb) : 0ull;
+        const uint32_t dmask = (1u << wd) - 1;
+#pragma unroll
+        for (int u = 0; u < kPer; u++)
+          if (kv[u] && (kv[u] & hmask) == prefix) atomicAdd(&hist[(uint32_t)(kv[u] >> sh) & dmask], 1u);
+        uint32_t above;
+        const uint32_t bin = wave_select_bin(hist, rem, &above);
+        const uint32_t inbin = hist[bin];
+#pragma unroll
+        for (int i = 0; i < 4; i++) hist[lane + 64 * i] = 0;
+        prefix |= (uint64_t)bin << sh;
+        rem -= above;
+        rb = sh;
+        if (inbin == rem) break;
+      }
+      tmask = ~0ull << rb;
+      T = prefix;
+    }
+    // write the taken keys (wave-compacted)
+    uint32_t base = 0;
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+      const bool take = kv[u] && (kv[u] & tmask) >= T;
+      const uint64_t m = __ballot(take);
+      if (take) cand[base + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = kv[u];
+      base += (uint32_t)__popcll(m);
+    }
+    if (lane == 0) p.cand_n[pr] = base;
+  }
+}
+
+hipError_t launch_score_pairs(const QueryParams &p, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(k_score_pairs, dim3(grid), dim3(kPairWaves * 64), 0, s, p);
+  return hipGetLastError();
+}
+
 hipError_t launch_score_blocks(const QueryParams &p, hipStream_t s) {
+  if (p.ovf_list) {
+    hipLaunchKernelGGL(k_score_blocks, dim3(p.list_grid), dim3(kScoreThreads), 0, s, p);
+    return hipGetLastError();
+  }
   const uint32_t chunks = (p.n_q + p.q_chunk - 1) / p.q_chunk;
   hipLaunchKernelGGL(k_score_blocks, dim3(p.n_blocks, chunks), dim3(kScoreThreads), 0, s, p);
   return hipGetLastError();

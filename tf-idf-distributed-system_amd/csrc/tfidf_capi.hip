@@ -147,7 +147,7 @@ struct tfidf_index {
   DevBuf canon_of_slot;
   uint64_t n_canon = 0;
   // term-ownership exchange: record order -> slot, owner-side scratch table
-  DevBuf sent_slot, vcounts, vt_table, vt_sum, vt_rslot, gdf_dev;
+  DevBuf sent_slot, vcounts, vt_table, vt_sum, vt_rslot, gdf_dev, ovf;
   uint64_t n_sent = 0;
 
   // query scratch
@@ -213,7 +213,7 @@ extern "C" int tfidf_destroy(tfidf_index *ix) {
                     &ix->q_off, &ix->q_slot, &ix->q_w, &ix->cache, &ix->cand, &ix->cand_n, &ix->out_doc,
                     &ix->out_score, &ix->out_n, &ix->hits, &ix->hits_n, &ix->hits_c, &ix->hits_s, &ix->sort_tmp,
                     &ix->row_off, &ix->tvals, &ix->toff, &ix->tdf, &ix->term_tmp, &ix->sent_slot, &ix->vcounts,
-                    &ix->vt_table, &ix->vt_sum, &ix->vt_rslot, &ix->gdf_dev};
+                    &ix->vt_table, &ix->vt_sum, &ix->vt_rslot, &ix->gdf_dev, &ix->ovf};
   for (DevBuf *b : bufs) b->release();
   for (int i = 0; i < EV_N; i++) hipEventDestroy(ix->ev[i]);
   for (int i = 0; i < 2; i++) {
@@ -803,6 +803,21 @@ static int run_scoring(tfidf_index *ix, const std::vector<uint32_t> &qoff, const
     qp.hits_n = ix->hits_n.as<uint32_t>();
   }
   HIP_TRY(hipEventRecord(ix->ev[EV_Q0], s));
+  const size_t npairs = (size_t)n_q * ix->n_blocks;
+  if (k && npairs >= (size_t)ix->num_cus * 16 && npairs < (1ull << 32)) {
+    // batches: wave per (block, query) pair; pairs with many postings are
+    // listed for the dense per-block kernel (list mode, persistent grid).
+    // Single queries keep the dense kernel: a few hundred pairs cannot fill
+    // the chip one wave each.
+    HIP_TRY(ix->ovf.reserve(npairs * 4 + 64));
+    qp.ovf_count = ix->ovf.as<uint32_t>();
+    qp.ovf_list = qp.ovf_count + 16;
+    qp.list_grid = (uint32_t)ix->num_cus * 2;
+    HIP_TRY(hipMemsetAsync(qp.ovf_count, 0, 4, s));
+    const uint64_t want = (npairs + kPairWavesPerWG - 1) / kPairWavesPerWG;
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)ix->num_cus * 40));
+    HIP_TRY(launch_score_pairs(qp, grid, s));
+  }
   HIP_TRY(launch_score_blocks(qp, s));
   HIP_TRY(hipEventRecord(ix->ev[EV_Q1], s));
   if (k) HIP_TRY(launch_merge_topk(qp, s));

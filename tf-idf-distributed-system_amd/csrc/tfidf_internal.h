@@ -126,7 +126,13 @@ struct QueryParams {
   // all-hits mode
   uint64_t *hits;             // [n_blocks * kBlockDocs] keys (score bits << 32 | ~doc)
   uint32_t *hits_n;           // [n_blocks]
+  // wave-per-pair path (k > 0): pairs it leaves to k_score_blocks (nullptr = dense grid mode)
+  uint32_t *ovf_list;         // pair ids q * n_blocks + b
+  uint32_t *ovf_count;        // zeroed before k_score_pairs
+  uint32_t list_grid;         // k_score_blocks workgroups in list mode
 };
+hipError_t launch_score_pairs(const QueryParams &p, int grid, hipStream_t s);
+constexpr uint32_t kPairWavesPerWG = 2;   // k_score_pairs workgroup = 2 waves (30 KB LDS: 5 per CU)
 hipError_t launch_score_blocks(const QueryParams &p, hipStream_t s);
 hipError_t launch_merge_topk(const QueryParams &p, hipStream_t s);
 
