@@ -129,6 +129,15 @@ int tfidf_add_docs_device(tfidf_index *ix, const void *d_utf8, const void *d_off
                           uint64_t total_bytes);
 
 int tfidf_commit(tfidf_index *ix);
+
+/* Persistence (the reference's FSDirectory index, Worker.java:67-73).  tfidf_save
+ * writes the staged corpus (text, offsets, document keys, replace-by-key
+ * liveness) to `path` (atomically: path.tmp, then rename).  tfidf_load stages a
+ * saved file into an EMPTY index (same vocab_capacity_log2); call tfidf_commit
+ * afterwards (more documents may be added first, replacing by key as usual).
+ * The inverted index itself is rebuilt by the commit rather than stored. */
+int tfidf_save(tfidf_index *ix, const char *path);
+int tfidf_load(tfidf_index *ix, const char *path);
 int tfidf_get_commit_timing(const tfidf_index *ix, tfidf_commit_timing *out);
 int tfidf_stats(const tfidf_index *ix, tfidf_index_stats *out);
 

@@ -341,6 +341,151 @@ extern "C" int tfidf_clear(tfidf_index *ix) {
   return TFIDF_OK;
 }
 
+// ---------------------------------------------------------------------------
+// Persistence (the reference keeps a Lucene index in
+// FSDirectory(lucene.index.path) and reopens it at start-up,
+// J/worker/Worker.java:67-73).  What is stored is the staged corpus (text,
+// offsets, document keys, liveness after replace-by-key) — the index
+// structures are rebuilt by tfidf_commit on load: on MI355X the rebuild runs
+// at tens of GB/s of corpus, faster than reading the derived structures
+// (≈ 2x the corpus size) back from storage.
+static const char kFileMagic[8] = {'T', 'F', 'I', 'D', 'F', 'I', 'X', '1'};
+
+struct FileHeader {
+  char magic[8];
+  uint32_t version, reserved;
+  float k1, b;
+  int32_t stats_mode, inversion;
+  uint32_t vocab_capacity_log2, pad;
+  uint64_t n_staged, text_bytes, key_bytes, n_dead, meta_hash;
+};
+
+static uint64_t fnv1a(uint64_t h, const void *p, size_t n) {
+  const uint8_t *c = static_cast<const uint8_t *>(p);
+  for (size_t i = 0; i < n; i++) { h ^= c[i]; h *= 0x100000001B3ull; }
+  return h;
+}
+
+static uint64_t meta_hash(const tfidf_index *ix) {
+  uint64_t h = 0xCBF29CE484222325ull;
+  h = fnv1a(h, ix->h_offsets.data(), ix->h_offsets.size() * 8);
+  h = fnv1a(h, ix->key_off.data(), ix->key_off.size() * 8);
+  h = fnv1a(h, ix->key_arena.data(), ix->key_arena.size());
+  h = fnv1a(h, ix->key_synth.data(), ix->key_synth.size());
+  h = fnv1a(h, ix->staged_live.data(), ix->staged_live.size());
+  return h;
+}
+
+extern "C" int tfidf_save(tfidf_index *ix, const char *path) {
+  if (!ix || !path) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DeviceGuard g(ix->cfg.device);
+  HIP_TRY(hipStreamSynchronize(ix->stream));
+  FileHeader h{};
+  memcpy(h.magic, kFileMagic, 8);
+  h.version = 1;
+  h.k1 = ix->cfg.k1;
+  h.b = ix->cfg.b;
+  h.stats_mode = ix->cfg.stats_mode;
+  h.inversion = ix->cfg.inversion;
+  h.vocab_capacity_log2 = ix->cap_log2;
+  h.n_staged = ix->n_staged;
+  h.text_bytes = ix->text_bytes;
+  h.key_bytes = ix->key_arena.size();
+  h.n_dead = ix->n_dead;
+  h.meta_hash = meta_hash(ix);
+  const std::string tmp = std::string(path) + ".tmp";
+  FILE *f = fopen(tmp.c_str(), "wb");
+  if (!f) return fail(TFIDF_E_INVALID_ARG, "cannot open %s for writing", tmp.c_str());
+  bool ok = fwrite(&h, sizeof h, 1, f) == 1;
+  ok = ok && fwrite(ix->h_offsets.data(), 8, ix->h_offsets.size(), f) == ix->h_offsets.size();
+  ok = ok && fwrite(ix->key_off.data(), 8, ix->key_off.size(), f) == ix->key_off.size();
+  ok = ok && (ix->key_arena.empty() || fwrite(ix->key_arena.data(), 1, ix->key_arena.size(), f) == ix->key_arena.size());
+  ok = ok && (ix->n_staged == 0 || fwrite(ix->key_synth.data(), 1, ix->n_staged, f) == ix->n_staged);
+  ok = ok && (ix->n_staged == 0 || fwrite(ix->staged_live.data(), 1, ix->n_staged, f) == ix->n_staged);
+  // corpus text: device -> pinned staging buffer -> file, chunk by chunk
+  if (ok && ix->text_bytes) {
+    if (!ix->stage[0]) {
+      if (hipHostMalloc(&ix->stage[0], kStageBytes, hipHostMallocDefault) != hipSuccess) ix->stage[0] = nullptr;
+    }
+    if (!ix->stage[0]) { fclose(f); remove(tmp.c_str()); return fail(TFIDF_E_OOM, "pinned staging buffer"); }
+    for (uint64_t off = 0; ok && off < ix->text_bytes; off += kStageBytes) {
+      const size_t n = (size_t)std::min<uint64_t>(kStageBytes, ix->text_bytes - off);
+      if (hipMemcpy(ix->stage[0], ix->text.as<uint8_t>() + off, n, hipMemcpyDeviceToHost) != hipSuccess) {
+        fclose(f);
+        remove(tmp.c_str());
+        return fail(TFIDF_E_HIP, "copy of the corpus from the device failed");
+      }
+      ok = fwrite(ix->stage[0], 1, n, f) == n;
+    }
+  }
+  ok = (fclose(f) == 0) && ok;
+  if (!ok || rename(tmp.c_str(), path) != 0) {
+    remove(tmp.c_str());
+    return fail(TFIDF_E_INVALID_ARG, "write of %s failed", path);
+  }
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_add_docs(tfidf_index *ix, const uint8_t *utf8, const uint64_t *offsets, uint64_t n_docs,
+                              const uint8_t *keys, const uint64_t *key_offsets);
+
+extern "C" int tfidf_load(tfidf_index *ix, const char *path) {
+  if (!ix || !path) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  {
+    std::lock_guard<std::mutex> lk(ix->mu);
+    if (ix->n_staged) return fail(TFIDF_E_STATE, "tfidf_load needs an empty index (tfidf_create / tfidf_clear)");
+  }
+  FILE *f = fopen(path, "rb");
+  if (!f) return fail(TFIDF_E_INVALID_ARG, "cannot open %s", path);
+  FileHeader h{};
+  if (fread(&h, sizeof h, 1, f) != 1 || memcmp(h.magic, kFileMagic, 8) != 0 || h.version != 1) {
+    fclose(f);
+    return fail(TFIDF_E_INVALID_ARG, "%s is not a tfidf index file (version 1)", path);
+  }
+  if (h.vocab_capacity_log2 != ix->cap_log2) {
+    fclose(f);
+    return fail(TFIDF_E_INVALID_ARG, "index file has vocab_capacity_log2 %u, this index %u", h.vocab_capacity_log2,
+                ix->cap_log2);
+  }
+  const uint64_t n = h.n_staged;
+  std::vector<uint64_t> offs(n + 1), koff(n + 1);
+  std::string arena(h.key_bytes, '\0');
+  std::vector<uint8_t> synth(n), live(n);
+  bool ok = fread(offs.data(), 8, n + 1, f) == n + 1 && fread(koff.data(), 8, n + 1, f) == n + 1;
+  ok = ok && (h.key_bytes == 0 || fread(&arena[0], 1, h.key_bytes, f) == h.key_bytes);
+  ok = ok && (n == 0 || (fread(synth.data(), 1, n, f) == n && fread(live.data(), 1, n, f) == n));
+  ok = ok && offs[0] == 0 && offs[n] == h.text_bytes && koff[0] == 0 && koff[n] == h.key_bytes;
+  for (uint64_t i = 0; ok && i < n; i++) ok = offs[i + 1] >= offs[i] && koff[i + 1] >= koff[i];
+  std::vector<uint8_t> text;
+  if (ok) {
+    text.resize(h.text_bytes);
+    ok = h.text_bytes == 0 || fread(text.data(), 1, h.text_bytes, f) == h.text_bytes;
+  }
+  fclose(f);
+  if (!ok) return fail(TFIDF_E_INVALID_ARG, "%s is truncated or corrupt", path);
+  // stage every stored document (as if keyless), then restore keys and
+  // liveness exactly as saved
+  int rc = tfidf_add_docs(ix, n ? text.data() : nullptr, offs.data(), n, nullptr, nullptr);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(ix->mu);
+  ix->key_arena = arena;
+  ix->key_off.assign(koff.begin(), koff.end());
+  ix->key_synth = synth;
+  ix->staged_live = live;
+  ix->key_to_staged.clear();
+  ix->n_dead = 0;
+  for (uint64_t i = 0; i < n; i++) {
+    if (!live[i]) { ix->n_dead++; continue; }
+    if (!synth[i]) ix->key_to_staged[std::string(arena, koff[i], koff[i + 1] - koff[i])] = i;
+  }
+  if (ix->n_dead != h.n_dead || meta_hash(ix) != h.meta_hash) {
+    ix->committed = false;
+    return fail(TFIDF_E_INVALID_ARG, "%s: metadata checksum mismatch", path);
+  }
+  return TFIDF_OK;
+}
+
 extern "C" int tfidf_add_docs(tfidf_index *ix, const uint8_t *utf8, const uint64_t *offsets, uint64_t n_docs,
                               const uint8_t *keys, const uint64_t *key_offsets) {
   if (!ix || (!utf8 && n_docs) || !offsets) return fail(TFIDF_E_INVALID_ARG, "NULL argument");

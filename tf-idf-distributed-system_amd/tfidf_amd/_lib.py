@@ -75,6 +75,8 @@ SIGNATURES = {
     "tfidf_destroy": (C.c_int, [VP]),
     "tfidf_add_docs": (C.c_int, [VP, VP, U64P, C.c_uint64, C.c_char_p, U64P]),
     "tfidf_clear": (C.c_int, [VP]),
+    "tfidf_save": (C.c_int, [VP, C.c_char_p]),
+    "tfidf_load": (C.c_int, [VP, C.c_char_p]),
     "tfidf_add_docs_device": (C.c_int, [VP, VP, VP, C.c_uint64, C.c_uint64]),
     "tfidf_commit": (C.c_int, [VP]),
     "tfidf_get_commit_timing": (C.c_int, [VP, C.POINTER(CommitTiming)]),

@@ -2,6 +2,7 @@
 reference (Worker.java:54-55 ``luceneDir`` + ``indexWriter``) behind the C ABI.
 """
 import ctypes as C
+import os
 
 import numpy as np
 
@@ -73,6 +74,14 @@ class ShardIndex:
         offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
         L.check(L.load().tfidf_add_docs(self._h, C.c_void_p(text.ctypes.data), L.ptr(offsets, C.c_uint64),
                                         len(offsets) - 1, None, None))
+
+    def save(self, path):
+        """Persist the staged corpus + keys (tfidf_save); the index is rebuilt by commit() after load()."""
+        L.check(L.load().tfidf_save(self._h, os.fsencode(path)))
+
+    def load(self, path):
+        """Stage a saved index file into this (empty) index; call commit() next."""
+        L.check(L.load().tfidf_load(self._h, os.fsencode(path)))
 
     def clear(self):
         """Drop all staged/committed documents; device buffers are kept for reuse."""

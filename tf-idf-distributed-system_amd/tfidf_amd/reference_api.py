@@ -33,11 +33,23 @@ class Worker:
         self.index = ShardIndex(device=device, vocab_capacity_log2=vocab_capacity_log2)
         self._committed = False
 
-    # Worker.java:57-94 @PostConstruct init: walk the documents directory,
-    # skipping the index directory, addDocToIndex per regular file, commit.
+    INDEX_FILE = "tfidf.idx"
+
+    def _index_file(self):
+        return os.path.join(self.INDEX_PATH, self.INDEX_FILE) if self.INDEX_PATH else None
+
+    # Worker.java:57-94 @PostConstruct init: open the index directory
+    # (IndexWriterConfig default OpenMode CREATE_OR_APPEND: a saved index is
+    # reopened), walk the documents directory skipping the index directory,
+    # addDocToIndex per regular file (replacing by relative path), commit.
     def init(self):
+        idx_file = self._index_file()
+        if idx_file and os.path.isfile(idx_file):
+            self.index.load(idx_file)
         docs_path = os.path.normpath(self.DOCUMENTS_PATH)
         if not os.path.isdir(docs_path):
+            if idx_file and os.path.isfile(idx_file):
+                self.commit()
             return
         idx_path = os.path.normpath(self.INDEX_PATH) if self.INDEX_PATH else None
         paths = []
@@ -59,8 +71,7 @@ class Worker:
             keys.append(k)
             texts.append(t)
         self.index.add_documents(texts, keys)
-        self.index.commit()
-        self._committed = True
+        self.commit()
 
     def _read(self, path):
         base = os.path.normpath(self.DOCUMENTS_PATH)
@@ -77,9 +88,14 @@ class Worker:
         k, t = self._read(path)
         self.index.add_documents([t], [k])
 
+    # Worker.java:88,138 indexWriter.commit(): the index becomes durable
     def commit(self):
         self.index.commit()
         self._committed = True
+        idx_file = self._index_file()
+        if idx_file:
+            os.makedirs(self.INDEX_PATH, exist_ok=True)
+            self.index.save(idx_file)
 
     # Worker.java:125-146 upload: copy the file, then add + commit under the writer lock
     def upload(self, filename, data: bytes):
