@@ -1416,8 +1416,13 @@ __global__ void k_block_base(PostingParams p) {
 //                    doc_local(13) | slot_low(10) | tf(24) | norm(8);
 //   k_scatter_sort : per stream (~86 KB), LDS cursor per slot, final postings
 //                    written inside the stream's own region.
-constexpr uint32_t kSubSlots = 512;
-constexpr uint32_t kSubBits = 9;
+#ifndef TFIDF_SUB_BITS
+#define TFIDF_SUB_BITS 9
+#endif
+constexpr uint32_t kSubBits = TFIDF_SUB_BITS;
+constexpr uint32_t kSubSlots = 1u << kSubBits;
+constexpr uint32_t kTmpTfShift = 13 + kSubBits;              // temp word: doc_local(13) | slot_low | tf(24) | norm(8)
+constexpr uint32_t kTmpNormShift = kTmpTfShift + 24;
 
 __device__ __forceinline__ void part_entries(const PostingParams &p, uint32_t *bcur, uint32_t rmask, uint64_t bb,
                                              const InvGroup &g, uint64_t dd, uint32_t d0l, uint32_t stride,
@@ -1432,7 +1437,7 @@ __device__ __forceinline__ void part_entries(const PostingParams &p, uint32_t *b
     const uint32_t sl = c[j] & rmask;
     const uint32_t dl = (uint32_t)(dd + (uint64_t)stride * j) - d0l;
     const uint64_t val = (uint64_t)dl | ((uint64_t)(sl & (kSubSlots - 1)) << 13) |
-                         ((uint64_t)(t[j] & kMaxTf) << 23) | ((uint64_t)g.nrm[j] << 47);
+                         ((uint64_t)(t[j] & kMaxTf) << kTmpTfShift) | ((uint64_t)g.nrm[j] << kTmpNormShift);
     const uint32_t pos = cursor_bump<kRangeBits - kSubBits + 1>(bcur, in ? sl >> kSubBits : kNoop, lane);
     if (in) p.post_tmp[bb + pos] = val;
   }
@@ -1506,7 +1511,7 @@ __global__ void __launch_bounds__(1024) k_scatter_sort(PostingParams p) {
       const bool in = e < hi;
       const uint32_t sl = in ? (uint32_t)(x[u] >> 13) & (kSubSlots - 1) : kSubSlots;   // kSubSlots: no-op key
       const uint32_t pos = cursor_bump<kSubBits + 1>(cur, sl, lane);
-      const uint32_t tf = (uint32_t)(x[u] >> 23) & kMaxTf, nrm = (uint32_t)(x[u] >> 47) & 0xFFu;
+      const uint32_t tf = (uint32_t)(x[u] >> kTmpTfShift) & kMaxTf, nrm = (uint32_t)(x[u] >> kTmpNormShift) & 0xFFu;
       if (in)
         p.post[bb + pos] = (uint64_t)(d0 + ((uint32_t)x[u] & (kBlockDocs - 1))) | ((uint64_t)((tf << 8) | nrm) << 32);
     }
