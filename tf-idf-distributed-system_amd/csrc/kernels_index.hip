@@ -1443,8 +1443,63 @@ __device__ __forceinline__ void part_entries(const PostingParams &p, uint32_t *b
   }
 }
 
+// Wave-local staging of one document group's entries (first 64 of each
+// segment): entries are counting-sorted by sub-range stream in the wave's LDS
+// area, then stored stream run by stream run, so consecutive lanes write
+// consecutive addresses (one store request per line instead of one per
+// entry).  The stream id rides in bits 56..61 of the temp word (pass 2 ignores
+// them).
+constexpr uint32_t kPartStreams = kRangeSlots / kSubSlots;  // 64
+static_assert(kTmpNormShift + 8 <= 56 && kPartStreams <= 64, "temp word layout");
+struct PartWave {
+  uint64_t stage[kInvDocs * 64];
+  uint32_t cnt[64], soff[64], gb[64];
+};
+
+__device__ __forceinline__ void part_group_staged(const PostingParams &p, uint32_t *bcur, PartWave &w, uint32_t rmask,
+                                                  uint64_t bb, const InvGroup &g, uint64_t dd, uint32_t d0l,
+                                                  uint32_t stride, const uint32_t *c, const uint32_t *t,
+                                                  bool *tf_big) {
+  const uint32_t lane = threadIdx.x & 63;
+  uint64_t val[kInvDocs];
+  uint32_t rank[kInvDocs], sj[kInvDocs];
+#pragma unroll
+  for (int j = 0; j < kInvDocs; j++) {
+    const bool in = c[j] != kInvalidSlot;
+    const uint32_t sl = c[j] & rmask;
+    sj[j] = sl >> kSubBits;
+    rank[j] = 0;
+    val[j] = 0;
+    if (in) {
+      *tf_big |= t[j] > kMaxTf;
+      const uint32_t dl = (uint32_t)(dd + (uint64_t)stride * j) - d0l;
+      val[j] = (uint64_t)dl | ((uint64_t)(sl & (kSubSlots - 1)) << 13) | ((uint64_t)(t[j] & kMaxTf) << kTmpTfShift) |
+               ((uint64_t)g.nrm[j] << kTmpNormShift) | ((uint64_t)sj[j] << 56);
+      rank[j] = atomicAdd(&w.cnt[sj[j]], 1u);
+    }
+  }
+  const uint32_t n = w.cnt[lane];
+  const uint32_t incl = wave_incl_add(n);
+  const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  w.soff[lane] = incl - n;
+  w.gb[lane] = n ? atomicAdd(&bcur[lane], n) : 0u;
+  w.cnt[lane] = 0;
+#pragma unroll
+  for (int j = 0; j < kInvDocs; j++)
+    if (c[j] != kInvalidSlot) w.stage[w.soff[sj[j]] + rank[j]] = val[j];
+  for (uint32_t t0 = 0; t0 < T; t0 += 64) {
+    const uint32_t ti = t0 + lane;
+    if (ti < T) {
+      const uint64_t v = w.stage[ti];
+      const uint32_t st = (uint32_t)(v >> 56);
+      p.post_tmp[bb + w.gb[st] + (ti - w.soff[st])] = v;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(1024) k_scatter_part(PostingParams p) {
   __shared__ uint32_t bcur[kRangeSlots / kSubSlots + 1];
+  __shared__ PartWave pwave[16];
   const uint32_t lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   const uint32_t wid = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const uint32_t b = blockIdx.x, r = blockIdx.y;
@@ -1452,6 +1507,7 @@ __global__ void __launch_bounds__(1024) k_scatter_part(PostingParams p) {
   const uint32_t nsub = RS > kSubSlots ? RS / kSubSlots : 1u;
   const uint32_t *row = p.blk + (size_t)b * p.C + ((size_t)r << p.range_shift);
   if (threadIdx.x < nsub) bcur[threadIdx.x] = row[threadIdx.x * kSubSlots];
+  if (threadIdx.x < 16 * 64) pwave[threadIdx.x >> 6].cnt[threadIdx.x & 63] = 0;
   __syncthreads();
   const uint64_t bb = p.bbase[b];
   const uint64_t d0 = (uint64_t)b * kBlockDocs;
@@ -1467,7 +1523,7 @@ __global__ void __launch_bounds__(1024) k_scatter_part(PostingParams p) {
     const InvGroup gn = inv_group(p, dn, d1, nw, r, true);
     uint32_t cn[kInvDocs], tn[kInvDocs];
     if (dn < d1) inv_load(p, gn, lane, cn, tn, true);           // next group in flight
-    part_entries(p, bcur, rmask, bb, g, dd, (uint32_t)d0, nw, c, t, &tf_big);
+    part_group_staged(p, bcur, pwave[wid], rmask, bb, g, dd, (uint32_t)d0, nw, c, t, &tf_big);
     for (uint32_t off = lane + 64; off < g.maxn; off += 64) {    // segments longer than 64
       inv_load(p, g, off, c, t, true);
       part_entries(p, bcur, rmask, bb, g, dd, (uint32_t)d0, nw, c, t, &tf_big);
