@@ -5,16 +5,18 @@
 // millions of short documents per GPU) that table alone would be tens of GB, so
 // above a size threshold the index is inverted term-major instead:
 //
-//   1. (slot, doc) pairs: every CSR entry becomes key = slot << dbits | doc,
-//      value = tf << 8 | norm, written at the document's compact row offset
-//      (exclusive sum of distinct-term counts);
-//   2. radix sort of the pairs on the key bits only (rocPRIM onesweep);
+//   1. (slot, posting) pairs: every CSR entry becomes key = slot (u32),
+//      value = doc | (tf << 8 | norm) << 32 (the block-major posting word),
+//      written at the document's compact row offset (exclusive sum of
+//      distinct-term counts), i.e. in document order;
+//   2. stable radix sort on the log2(C) slot bits only (rocPRIM onesweep):
+//      documents stay ascending within each term, so the sorted values ARE
+//      the postings;
 //   3. term bounds: toff[s] = first posting of slot s (C + 1 entries, one
-//      binary search per slot), df[s] = toff[s + 1] - toff[s];
-//   4. pack: post[i] = doc | (tf << 8 | norm) << 32 — the same posting word as
-//      the block-major layout, so the scoring kernels only differ in how they
-//      find a (doc block, term) segment (a wave-parallel search of the term's
-//      doc-sorted list, kernels_query.hip).
+//      binary search per slot), df[s] = toff[s + 1] - toff[s].
+// The scoring kernels only differ from the block-major case in how they find
+// a (doc block, term) segment (a wave-parallel search of the term's
+// doc-sorted list, kernels_query.hip).
 //
 // The result is what Lucene's postings hold for the field (per term, docs in
 // ascending order with freq and the doc's norm byte) — reference: inversion
@@ -41,22 +43,22 @@ __global__ void __launch_bounds__(256) k_term_pairs(TermParams p) {
     for (uint32_t j = lane; j < n; j += 64) {
       const uint32_t c = p.csr_col[base + j], t = p.csr_tf[base + j];
       if (t >= (1u << 24)) atomicOr(p.err, kErrTfTooLarge);
-      p.keys[o + j] = ((uint64_t)c << p.dbits) | d;
-      p.vals[o + j] = (t << 8) | nrm;
+      p.keys[o + j] = c;
+      p.vals[o + j] = d | ((uint64_t)((t << 8) | nrm) << 32);
     }
   }
 }
 
-// toff[s] = first index i with slot(key[i]) >= s, for s in [0, C]: one thread
-// per slot, binary search of the sorted keys (empty slots cost the same as
-// full ones, so sparse tables over a huge C stay parallel).
-__global__ void k_term_bounds(const uint64_t *keys, uint64_t nnz, uint32_t dbits, uint32_t C, uint64_t *toff) {
+// toff[s] = first index i with key[i] >= s, for s in [0, C]: one thread per
+// slot, binary search of the sorted keys (empty slots cost the same as full
+// ones, so sparse tables over a huge C stay parallel).
+__global__ void k_term_bounds(const uint32_t *keys, uint64_t nnz, uint32_t C, uint64_t *toff) {
   const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s > C) return;
   uint64_t a = 0, z = nnz;
   while (a < z) {
     const uint64_t m = (a + z) >> 1;
-    if ((keys[m] >> dbits) < s) a = m + 1; else z = m;
+    if (keys[m] < s) a = m + 1; else z = m;
   }
   toff[s] = a;
 }
@@ -66,19 +68,13 @@ __global__ void k_term_df(const uint64_t *toff, uint32_t C, uint32_t *df) {
   if (s < C) df[s] = (uint32_t)(toff[s + 1] - toff[s]);
 }
 
-__global__ void k_term_pack(const uint64_t *keys, const uint32_t *vals, uint64_t nnz, uint64_t dmask,
-                            uint64_t *post) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < nnz) post[i] = (keys[i] & dmask) | ((uint64_t)vals[i] << 32);
-}
-
 hipError_t term_invert_tmp_bytes(uint64_t n_docs, uint64_t nnz, uint32_t key_bits, size_t *bytes) {
   size_t a = 0, b = 0;
   hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, a, (const uint32_t *)nullptr, (uint32_t *)nullptr,
                                                   n_docs ? n_docs : 1);
   if (e != hipSuccess) return e;
-  hipcub::DoubleBuffer<uint64_t> k(nullptr, nullptr);
-  hipcub::DoubleBuffer<uint32_t> v(nullptr, nullptr);
+  hipcub::DoubleBuffer<uint32_t> k(nullptr, nullptr);
+  hipcub::DoubleBuffer<uint64_t> v(nullptr, nullptr);
   e = hipcub::DeviceRadixSort::SortPairs(nullptr, b, k, v, nnz ? nnz : 1, 0, (int)key_bits);
   *bytes = (a > b ? a : b) + 256;
   return e;
@@ -86,9 +82,8 @@ hipError_t term_invert_tmp_bytes(uint64_t n_docs, uint64_t nnz, uint32_t key_bit
 
 hipError_t launch_term_invert(TermParams p, void *tmp, size_t tmp_bytes, hipStream_t s) {
   hipError_t e;
-  if (p.n_docs == 0) {
-    hipLaunchKernelGGL(k_term_bounds, dim3(p.C / 256 + 1), dim3(256), 0, s, p.keys, (uint64_t)0, p.dbits, p.C,
-                       p.toff);
+  if (p.n_docs == 0 || p.nnz == 0) {
+    hipLaunchKernelGGL(k_term_bounds, dim3(p.C / 256 + 1), dim3(256), 0, s, p.keys, (uint64_t)0, p.C, p.toff);
     hipLaunchKernelGGL(k_term_df, dim3((p.C + 255) / 256), dim3(256), 0, s, p.toff, p.C, p.df);
     return hipGetLastError();
   }
@@ -98,16 +93,16 @@ hipError_t launch_term_invert(TermParams p, void *tmp, size_t tmp_bytes, hipStre
     const uint64_t waves = p.n_docs < (1ull << 20) ? p.n_docs : (1ull << 20);
     hipLaunchKernelGGL(k_term_pairs, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, p);
   }
-  hipcub::DoubleBuffer<uint64_t> k(p.keys, p.keys_alt);
-  hipcub::DoubleBuffer<uint32_t> v(p.vals, p.vals_alt);
-  e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, k, v, p.nnz, 0, (int)(p.dbits + p.slot_bits), s);
+  hipcub::DoubleBuffer<uint32_t> k(p.keys, p.keys_alt);
+  hipcub::DoubleBuffer<uint64_t> v(p.vals, p.vals_alt);
+  e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, k, v, p.nnz, 0, (int)p.slot_bits, s);
   if (e != hipSuccess) return e;
-  const unsigned g = (unsigned)((p.nnz + 256) / 256);
-  hipLaunchKernelGGL(k_term_bounds, dim3(p.C / 256 + 1), dim3(256), 0, s, k.Current(), p.nnz, p.dbits, p.C,
-                     p.toff);
+  if (v.Current() != p.post) {
+    e = hipMemcpyAsync(p.post, v.Current(), p.nnz * 8, hipMemcpyDeviceToDevice, s);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_term_bounds, dim3(p.C / 256 + 1), dim3(256), 0, s, k.Current(), p.nnz, p.C, p.toff);
   hipLaunchKernelGGL(k_term_df, dim3((p.C + 255) / 256), dim3(256), 0, s, p.toff, p.C, p.df);
-  hipLaunchKernelGGL(k_term_pack, dim3(g), dim3(256), 0, s, k.Current(), v.Current(), p.nnz,
-                     (1ull << p.dbits) - 1, p.post);
   return hipGetLastError();
 }
 

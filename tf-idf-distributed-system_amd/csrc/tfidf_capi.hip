@@ -758,24 +758,22 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
     tp.nnz = ix->nnz;
     tp.C = C;
     tp.slot_bits = ix->cap_log2;
-    tp.dbits = 1;
-    while ((1ull << tp.dbits) < N) tp.dbits++;
     tp.csr_col = bp.csr_col;
     tp.csr_tf = bp.csr_tf;
     tp.doc_nuniq = bp.doc_nuniq;
     tp.doc_norm = bp.doc_norm;
     tp.row_off = ix->row_off.as<uint32_t>();
     HIP_TRY(ix->tvals.reserve(ix->nnz * 8 + 16));
-    tp.keys = ix->post_tmp.as<uint64_t>();
-    tp.keys_alt = ix->post.as<uint64_t>();
-    tp.vals = ix->tvals.as<uint32_t>();
-    tp.vals_alt = tp.vals + ix->nnz + 1;
+    tp.keys = ix->tvals.as<uint32_t>();
+    tp.keys_alt = tp.keys + ix->nnz + 1;
+    tp.vals = ix->post_tmp.as<uint64_t>();
+    tp.vals_alt = ix->post.as<uint64_t>();
     tp.post = ix->post.as<uint64_t>();
     tp.toff = ix->toff.as<uint64_t>();
     tp.df = ix->tdf.as<uint32_t>();
     tp.err = bp.err;
     size_t tb = 0;
-    HIP_TRY(term_invert_tmp_bytes(N, ix->nnz, tp.dbits + tp.slot_bits, &tb));
+    HIP_TRY(term_invert_tmp_bytes(N, ix->nnz, tp.slot_bits, &tb));
     HIP_TRY(ix->term_tmp.reserve(tb));
     // the whole inversion is reported under ms_scatter
     HIP_TRY(hipEventRecord(ix->ev[EV_DF], s));

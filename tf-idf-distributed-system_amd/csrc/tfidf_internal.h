@@ -87,12 +87,11 @@ struct TermParams {
   const uint32_t *live_map;
   uint64_t n_docs, nnz;
   uint32_t C, slot_bits;      // C = 2^slot_bits
-  uint32_t dbits;             // doc bits in a sort key (2^dbits >= n_docs)
   const uint32_t *csr_col, *csr_tf, *doc_nuniq;
   const uint8_t *doc_norm;
   uint32_t *row_off;          // [n_docs] compact row offsets (exclusive sum of doc_nuniq)
-  uint64_t *keys, *keys_alt;  // [nnz] each: sort keys slot << dbits | doc (double buffer)
-  uint32_t *vals, *vals_alt;  // [nnz] each: tf << 8 | norm
+  uint32_t *keys, *keys_alt;  // [nnz] each: sort keys = slot (double buffer)
+  uint64_t *vals, *vals_alt;  // [nnz] each: posting words (double buffer; one of them is post)
   uint64_t *post;             // [nnz] out: doc | (tf << 8 | norm) << 32, term-major, docs ascending
   uint64_t *toff;             // [C + 1] out: first posting of each slot
   uint32_t *df;               // [C] out
