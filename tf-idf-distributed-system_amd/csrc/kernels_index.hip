@@ -594,7 +594,7 @@ __device__ __forceinline__ void clear_table(WaveSmem &sm, uint32_t lane) {
 // (k < K) of the token list, all LDS reads in flight, then probe rounds over
 // the table (branch-free: idle lanes CAS a no-op slot), then a retry queue of
 // two entries per lane once few tokens are left.
-template <int K>
+template <int K, bool FOLD>
 __device__ __forceinline__ void hist_batch(WaveSmem &sm, const BuildParams &p, uint64_t d, uint32_t lane, uint32_t tb,
                                            uint32_t ntok, bool under, unsigned long long *noop, uint32_t &claims,
                                            uint32_t &toks, bool &overflow) {
@@ -630,7 +630,7 @@ __device__ __forceinline__ void hist_batch(WaveSmem &sm, const BuildParams &p, u
     pendm |= (uint32_t)(in & (n <= 8) & valid) << k;
     longm |= (uint32_t)(in & (n > 8)) << k;
   }
-  if (__any(longm != 0)) {                               // tokens of 9..255 bytes: folded keys
+  if (FOLD && __any(longm != 0)) {                      // tokens of 9..255 bytes: folded keys
 #pragma unroll
     for (int k = 0; k < K; k++) {
       if ((longm >> k) & 1u) {
@@ -684,7 +684,7 @@ __device__ __forceinline__ void hist_batch(WaveSmem &sm, const BuildParams &p, u
 #pragma unroll
         for (int i = 0; i < 2; i++) {
           bool hit = qp[i] & ((old[i] == 0) | (old[i] == qk[i]));
-          const bool fc = qp[i] & !hit & (((old[i] & qk[i]) >> 63) != 0) &
+          const bool fc = FOLD && qp[i] & !hit & (((old[i] & qk[i]) >> 63) != 0) &
                           (((old[i] ^ qk[i]) & ~kFoldPosMask) == 0);
           if (fc)
             hit = span_same(sm.text, (uint32_t)(old[i] >> 13) & 0x1FFFu, (uint32_t)(qk[i] >> 13) & 0x1FFFu,
@@ -722,13 +722,13 @@ __device__ __forceinline__ void hist_batch(WaveSmem &sm, const BuildParams &p, u
       claims += (uint32_t)(hit & z);
       pendm &= ~((uint32_t)hit << k);
       // same folded hash, other position: exact compare below (always false without long tokens)
-      const bool fc = pend & !hit & (((old[k] & tkey[k]) >> 63) != 0) &
+      const bool fc = FOLD && pend & !hit & (((old[k] & tkey[k]) >> 63) != 0) &
                       (((old[k] ^ tkey[k]) & ~kFoldPosMask) == 0);
       foldm |= (uint32_t)fc << k;
       const bool adv = pend & !hit & !fc;
       slot[k] = adv ? ((slot[k] + 1) & (kWaveSlots - 1)) : slot[k];
     }
-    if (__any(foldm != 0)) {                              // same length and hash: compare bytes
+    if (FOLD && __any(foldm != 0)) {                      // same length and hash: compare bytes
 #pragma unroll
       for (int k = 0; k < K; k++) {
         if ((foldm >> k) & 1u) {
@@ -824,6 +824,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       if (lane == 0) p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
       continue;
     }
+    bool longtok = false;
     {
       uint32_t at = tincl - nts;
       uint32_t s0 = (uint32_t)S, s1 = (uint32_t)(S >> 32), e0 = (uint32_t)E, e1 = (uint32_t)(E >> 32);
@@ -833,20 +834,29 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
                                       : nz;
         if (s0) s0 &= s0 - 1; else s1 &= s1 - 1;
         if (e0) e0 &= e0 - 1; else e1 &= e1 - 1;
+        longtok |= te - tp > 8;
         sm.list[at++] = tp | (te << 16);
       }
     }
     asm volatile("" ::: "memory");
     if (p.debug_stop == 2) continue;
 
-    // ---- per-document histogram in LDS
+    // ---- per-document histogram in LDS (folded-key checks only when the
+    // document holds a token of more than 8 bytes)
+    const bool anylong = __any(longtok);
     uint32_t claims = 0, toks = 0;
     bool overflow = false;
     for (uint32_t tb = 0; tb < ntok && !overflow;) {       // batch width by what is left
       const uint32_t rem = ntok - tb;
-      if (rem > 256) { hist_batch<8>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 512; }
-      else if (rem > 128) { hist_batch<4>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 256; }
-      else { hist_batch<2>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 128; }
+      if (anylong) {
+        if (rem > 256) { hist_batch<8, true>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 512; }
+        else if (rem > 128) { hist_batch<4, true>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 256; }
+        else { hist_batch<2, true>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 128; }
+      } else {
+        if (rem > 256) { hist_batch<8, false>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 512; }
+        else if (rem > 128) { hist_batch<4, false>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 256; }
+        else { hist_batch<2, false>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 128; }
+      }
     }
     const uint32_t len = wave_sum(toks), nu = wave_sum(claims);
     if (overflow || nu > kWaveTerms) {                      // wave-uniform: long path
