@@ -270,6 +270,8 @@ def main():
         "index_build_alg_bytes": b_index,
         "index_build_GBs_end_to_end": b_index / (elapsed / args.steps) / 1e9,
         "long_docs": st["long_docs"],
+        "tokenizer_docs_per_window": st["pack_docs"],
+        "pack_retried_docs": st["pack_retried"],
     }
 
     # ---- queries (outside the timed region) ----

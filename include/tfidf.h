@@ -89,6 +89,8 @@ typedef struct tfidf_index_stats {
   uint64_t long_docs;     /* documents indexed by the long-document path */
   uint64_t text_bytes;    /* corpus bytes resident on the device */
   uint64_t term_major;    /* 1 if the last commit built the term-major layout (TFIDF_INVERSION_TERM) */
+  uint64_t pack_docs;     /* documents per tokenizer window in the last commit (1 = one per window) */
+  uint64_t pack_retried;  /* documents the packed windows handed to the one-per-window pass */
 } tfidf_index_stats;
 
 /* Per-phase device times of the last commit, measured with HIP events on the

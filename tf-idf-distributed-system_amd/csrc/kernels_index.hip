@@ -376,6 +376,30 @@ constexpr uint64_t kFoldBit = 1ull << 63;
 constexpr uint64_t kFoldPosMask = 0x1FFFull << 13;
 constexpr uint32_t kLookupPending = 0xFFFFFFFEu;
 
+// Packed documents (PACK instantiation, short-document corpora): a wave
+// indexes up to kPackMax consecutive documents of one contiguous window at a
+// time.  Token list entries carry the pack-local document index j in their
+// spare bits (start | end << 16, both < 2^13: j bits 0-2 at 13-15, bit 3 at
+// 29).  Table keys are made document-distinct: a key of <= 8 bytes carries j
+// in the free bit 7 of its first four bytes (ASCII), a folded key in bits
+// 8..12; the dictionary sees the key with those bits cleared.
+constexpr uint32_t kPackMax = 16;
+static_assert(kPackMaxDocs <= kPackMax, "pack size");
+constexpr uint32_t kSpanMask = 0x1FFFu;
+constexpr uint64_t kPackTagMask = 0x80808080ull;
+__device__ __forceinline__ uint32_t span_entry(uint32_t tp, uint32_t te, uint32_t j) {
+  return tp | (te << 16) | ((j & 7u) << 13) | ((j >> 3) << 29);
+}
+__device__ __forceinline__ uint32_t span_doc(uint32_t e) { return ((e >> 13) & 7u) | (((e >> 29) & 1u) << 3); }
+__device__ __forceinline__ uint32_t pack_tag(uint32_t j) {
+  return ((j & 1u) << 7) | ((j & 2u) << 14) | ((j & 4u) << 21) | ((j & 8u) << 28);
+}
+__device__ __forceinline__ uint32_t key_doc(uint64_t key) {
+  if (key & kFoldBit) return (uint32_t)(key >> 8) & 31u;
+  const uint32_t l = (uint32_t)key;
+  return ((l >> 7) & 1u) | ((l >> 14) & 2u) | ((l >> 21) & 4u) | ((l >> 28) & 8u);
+}
+
 struct WaveSmem {
   alignas(16) uint8_t text[kWaveWindow + 32];    // +32: key reads run past a token's end
   alignas(16) uint64_t key[kWaveSlots];          // term table; then lookup queue / results; then CSR staging
@@ -403,7 +427,10 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 // Word-segment mask of window bytes [64*lane, 64*lane + 64).  Bytes outside
 // the document were zeroed at staging (class Other).  Wave-uniform flags:
 // *bad = a byte >= 0x80 in the document, *under = a '_' in the document.
-__device__ __forceinline__ uint64_t lane_word_mask(const uint8_t *text, uint32_t lane, bool *bad, bool *under) {
+// PACK: *wbase = the same mask before the joiner rules (letters, digits, '_').
+template <bool PACK>
+__device__ __forceinline__ uint64_t lane_word_mask(const uint8_t *text, uint32_t lane, bool *bad, bool *under,
+                                                   uint64_t *wbase) {
   uint32_t x[16];
   {
     const uint4 *t = reinterpret_cast<const uint4 *>(text + lane * 64);
@@ -429,13 +456,14 @@ __device__ __forceinline__ uint64_t lane_word_mask(const uint8_t *text, uint32_t
   if (lane == 63) ldn = 0;
   const bool mids = __any((P & 0x80808080u) != 0);
   // pass 2: word bits
-  uint64_t W = 0;
+  uint64_t W = 0, WB = 0;
   uint32_t us = 0;
 #pragma unroll
   for (int i = 0; i < 16; i++) {
     const uint32_t u = swar_eq(x[i], 0x5F5F5F5Fu);
     us |= u;
     uint32_t c = LD[i] | (LD[i] << 1) | u;                          // letter | digit | '_' (bit 7)
+    if (PACK) WB |= (uint64_t)swar_nib(c & 0x80808080u) << (4 * i);
     if (mids) {
       const uint32_t prev4 = i ? LD[i - 1] : ldp;
       const uint32_t next4 = i < 15 ? LD[i + 1] : ldn;
@@ -451,6 +479,7 @@ __device__ __forceinline__ uint64_t lane_word_mask(const uint8_t *text, uint32_t
   }
   *bad = __any((badacc & 0x80808080u) != 0);
   *under = __any(us != 0);
+  if (PACK) *wbase = WB;
   return W;
 }
 
@@ -549,21 +578,62 @@ __device__ __forceinline__ uint4 gload16(const void *ptr) {
 #endif
 }
 
+// One unit of the wave path: d = first (committed) document, src = its
+// staged source, [s0, s0 + L) = the window's corpus bytes.  PACK: np documents
+// d .. d + np - 1 with sources src .. src + np - 1; lane j <= np holds pofs =
+// the corpus offset of document j (lane np: the end); ok = the sources are
+// contiguous and no document is empty (the boundaries are distinct).
 struct DocMeta {
-  uint64_t s0, L, src;
-  uint32_t shift;
+  uint64_t d, s0, L, src, pofs;
+  uint32_t shift, np;
+  bool ok;
 };
 
-__device__ __forceinline__ DocMeta doc_meta(const BuildParams &p, uint64_t d) {
+template <bool PACK>
+__device__ __forceinline__ DocMeta unit_meta(const BuildParams &p, uint64_t u, uint32_t lane) {
   DocMeta m;
-  m.src = p.live_map ? p.live_map[d] : d;
-  m.s0 = p.offsets[m.src];
-  m.L = p.offsets[m.src + 1] - m.s0;
+  if (!PACK) {
+    m.d = p.doc_list ? p.doc_list[u] : u;
+    m.src = p.live_map ? p.live_map[m.d] : m.d;
+    m.s0 = p.offsets[m.src];
+    m.L = p.offsets[m.src + 1] - m.s0;
+    m.pofs = 0;
+    m.np = 1;
+    m.ok = true;
+  } else {
+    m.d = u * p.pack;
+    const uint32_t np = (uint32_t)min((uint64_t)p.pack, p.n_docs - m.d);
+    const uint32_t j = lane < np ? lane : np - 1;
+    // lane j < np: source of document d + j; lanes >= np: one past the last source
+    const uint64_t sj = (p.live_map ? (uint64_t)p.live_map[m.d + j] : m.d + j) + (lane < np ? 0u : 1u);
+    m.src = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(sj >> 32), 0) << 32) |
+            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sj, 0);
+    const bool contig = __all(lane > np || sj == m.src + lane);
+    m.pofs = p.offsets[sj];
+    const uint64_t nxt = ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(m.pofs >> 32), 1, 64) << 32) |
+                         (uint32_t)__shfl_down((int)(uint32_t)m.pofs, 1, 64);
+    const bool nonempty = __all(lane >= np || nxt > m.pofs);
+    m.s0 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(m.pofs >> 32), 0) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m.pofs, 0);
+    const uint64_t end = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(m.pofs >> 32), (int)np) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m.pofs, (int)np);
+    m.L = end - m.s0;
+    m.np = np;
+    m.ok = contig && nonempty;
+  }
   m.shift = (uint32_t)(reinterpret_cast<uintptr_t>(p.text + m.s0) & 15);
   return m;
 }
 
-__device__ __forceinline__ bool fits_wave(const DocMeta &m) { return m.shift + m.L <= kWaveWindow; }
+__device__ __forceinline__ bool fits_wave(const DocMeta &m) { return m.ok && m.shift + m.L <= kWaveWindow; }
+
+// PACK: documents d .. d + np - 1 go to the single-document pass.
+__device__ __forceinline__ void defer_pack(const BuildParams &p, uint64_t d, uint32_t np, uint32_t lane) {
+  uint32_t base = 0;
+  if (lane == 0) base = atomicAdd(p.retry_count, np);
+  base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
+  if (lane < np) p.retry_list[base + lane] = (uint32_t)(d + lane);
+}
 
 __device__ __forceinline__ void prefetch_wave(const BuildParams &p, const DocMeta &m, uint32_t lane, uint4 *v) {
   if (!fits_wave(m)) return;
@@ -594,7 +664,7 @@ __device__ __forceinline__ void clear_table(WaveSmem &sm, uint32_t lane) {
 // (k < K) of the token list, all LDS reads in flight, then probe rounds over
 // the table (branch-free: idle lanes CAS a no-op slot), then a retry queue of
 // two entries per lane once few tokens are left.
-template <int K, bool FOLD>
+template <int K, bool FOLD, bool PACK>
 __device__ __forceinline__ void hist_batch(WaveSmem &sm, const BuildParams &p, uint64_t d, uint32_t lane, uint32_t tb,
                                            uint32_t ntok, bool under, unsigned long long *noop, uint32_t &claims,
                                            uint32_t &toks, bool &overflow) {
@@ -612,19 +682,19 @@ __device__ __forceinline__ void hist_batch(WaveSmem &sm, const BuildParams &p, u
   uint32_t dw[K][3];
 #pragma unroll
   for (int k = 0; k < K; k++) {
-    const uint32_t a0 = (ent[k] & 0xFFFFu) >> 2;
+    const uint32_t a0 = (ent[k] & kSpanMask) >> 2;
     dw[k][0] = tw[a0]; dw[k][1] = tw[a0 + 1]; dw[k][2] = tw[a0 + 2];
   }
 #pragma unroll
   for (int k = 0; k < K; k++) {
     const bool in = tb + lane + 64 * k < ntok;
-    const uint32_t tp = ent[k] & 0xFFFFu, n = (ent[k] >> 16) - tp, o = tp & 3;
+    const uint32_t tp = ent[k] & kSpanMask, n = ((ent[k] >> 16) & kSpanMask) - tp, o = tp & 3;
     const uint64_t m64 = n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1);
     const uint32_t t0 = __builtin_amdgcn_alignbyte(dw[k][1], dw[k][0], o) & (uint32_t)m64;
     const uint32_t t1 = __builtin_amdgcn_alignbyte(dw[k][2], dw[k][1], o) & (uint32_t)(m64 >> 32);
     const bool valid =
         !under | ((((t0 ^ 0x5F5F5F5Fu) & (uint32_t)m64) | ((t1 ^ 0x5F5F5F5Fu) & (uint32_t)(m64 >> 32))) != 0);
-    const uint32_t l0 = lower4(t0), l1 = lower4(t1);
+    const uint32_t l0 = lower4(t0) | (PACK ? pack_tag(span_doc(ent[k])) : 0u), l1 = lower4(t1);
     tkey[k] = (uint64_t)l0 | ((uint64_t)l1 << 32);
     slot[k] = ((l0 ^ rotl32(l1, 16)) * 0x85EBCA77u) >> (32 - kWaveSlotBits);
     pendm |= (uint32_t)(in & (n <= 8) & valid) << k;
@@ -635,13 +705,17 @@ __device__ __forceinline__ void hist_batch(WaveSmem &sm, const BuildParams &p, u
     for (int k = 0; k < K; k++) {
       if ((longm >> k) & 1u) {
         const uint32_t e = sm.list[tb + lane + 64 * k];
-        const uint32_t tp = e & 0xFFFFu, n = (e >> 16) - tp;
+        const uint32_t tp = e & kSpanMask, n = ((e >> 16) & kSpanMask) - tp;
         if (n > kMaxTokenLen) {
           set_err(p.err, kErrTokenTooLong, (uint32_t)d);
         } else {
           uint32_t h;
           bool valid;
           tkey[k] = fold_key(sm.text, tp, n, &h, &valid);
+          if (PACK) {
+            tkey[k] |= (uint64_t)span_doc(e) << 8;
+            h ^= span_doc(e) * 0x9E3779B1u;
+          }
           slot[k] = h >> (32 - kWaveSlotBits);
           pendm |= (uint32_t)valid << k;
         }
@@ -745,6 +819,12 @@ __device__ __forceinline__ void hist_batch(WaveSmem &sm, const BuildParams &p, u
   }
 }
 
+// Units: PACK = false, one document per unit (documents 0..n_docs-1, or the
+// doc_list entries); PACK = true, unit u = documents [u * pack, u * pack + pack)
+// sharing one window.  A pack that cannot take the packed path (window or
+// token/term capacity, non-contiguous sources, an empty or non-ASCII document)
+// sends its documents to retry_list for a PACK = false pass.
+template <bool PACK>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_tokenize_wave(BuildParams p) {
   __shared__ WaveSmem sm;
   const uint32_t lane = threadIdx.x;
@@ -752,24 +832,31 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   sm.noop[lane] = 0;
   unsigned long long my_doc_count = 0, my_ttf = 0, my_nnz = 0;
   uint4 v[4] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+  const uint64_t n_units = PACK ? (p.n_docs + p.pack - 1) / p.pack : (p.doc_list ? *p.doc_list_count : p.n_docs);
   DocMeta meta;
-  if (blockIdx.x < p.n_docs) {
-    meta = doc_meta(p, blockIdx.x);
+  if (blockIdx.x < n_units) {
+    meta = unit_meta<PACK>(p, blockIdx.x, lane);
     prefetch_wave(p, meta, lane, v);
   }
   const uint32_t R = p.n_ranges;
   const uint32_t dmask = p.cap_mask;
   uint16_t *slots = reinterpret_cast<uint16_t *>(sm.list);
   unsigned long long *noop = reinterpret_cast<unsigned long long *>(&sm.noop[lane]);
+  // PACK per-document scratch in the histogram queue area (free after the histogram)
+  uint32_t *pk_len = reinterpret_cast<uint32_t *>(sm.qkey), *pk_nu = pk_len + kPackMax,
+           *pk_start = pk_len + 2 * kPackMax;
+  uint64_t *pk_row = sm.qkey + 2 * kPackMax;
 
-  for (uint64_t d = blockIdx.x; d < p.n_docs; d += gridDim.x) {
-    const uint64_t src = meta.src, L = meta.L;
-    const uint32_t shift = meta.shift;
+  for (uint64_t u = blockIdx.x; u < n_units; u += gridDim.x) {
+    const uint64_t d = meta.d, src = meta.src, L = meta.L, s0 = meta.s0;
+    const uint32_t shift = meta.shift, np = meta.np;
+    const uint64_t pofs = meta.pofs;
     const bool fits = fits_wave(meta);
-    const uint64_t dn = d + gridDim.x;
+    const uint64_t un = u + gridDim.x;
     if (!fits) {
-      if (lane == 0) p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
-      if (dn < p.n_docs) { meta = doc_meta(p, dn); prefetch_wave(p, meta, lane, v); }
+      if (PACK) defer_pack(p, d, np, lane);
+      else if (lane == 0) p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
+      if (un < n_units) { meta = unit_meta<PACK>(p, un, lane); prefetch_wave(p, meta, lane, v); }
       continue;                                             // wave-uniform
     }
     // ---- stage: registers -> LDS (whole window; bytes outside the document
@@ -791,14 +878,37 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         dst[c] = val;
       }
     }
-    if (dn < p.n_docs) { meta = doc_meta(p, dn); prefetch_wave(p, meta, lane, v); }
+    if (un < n_units) { meta = unit_meta<PACK>(p, un, lane); prefetch_wave(p, meta, lane, v); }
     asm volatile("" ::: "memory");
     if (p.debug_stop == 1) continue;
 
     // ---- classify + spans -> dense token list
     bool bad, under;
-    const uint64_t W = lane_word_mask(sm.text, lane, &bad, &under);
+    uint64_t wbase = 0;
+    uint64_t W = lane_word_mask<PACK>(sm.text, lane, &bad, &under, &wbase);
+    // PACK: document boundaries q_j (window position of document j's first
+    // byte, j >= 1).  No token spans one: a joiner next to q_j that is a word
+    // byte only through its neighbour across q_j is dropped, and a token is
+    // ended / started at q_j.  Token -> document: dbase = #{q_j <= 64 lane} plus
+    // the boundaries inside the lane below the token start (bm).
+    uint64_t bq = 0, bm = 0;
+    uint32_t dbase = 0;
+    if (PACK && !bad) {
+      const uint32_t qv = shift + (uint32_t)(pofs - s0);
+      uint64_t jm = 0;
+      const uint32_t l0 = 64 * lane;
+      for (uint32_t j = 1; j < np; j++) {
+        const uint32_t q = (uint32_t)__builtin_amdgcn_readlane((int)qv, (int)j);
+        dbase += q <= l0;
+        const uint32_t r = q - l0;                           // wraps for q < l0
+        if (r < 64) { bq |= 1ull << r; if (r) bm |= 1ull << r; }
+        if (r - 1 < 64) jm |= 1ull << (r - 1);
+        if (r < 64) jm |= 1ull << r;
+      }
+      W &= ~(jm & ~wbase);
+    }
     if (bad) {
+      if (PACK) { defer_pack(p, d, np, lane); continue; }
       if (lane == 0) {
         set_err(p.err, kErrNonAscii, (uint32_t)d);
         p.doc_len[d] = 0; p.doc_nuniq[d] = 0; p.doc_norm[d] = 0;
@@ -810,6 +920,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     const uint64_t prevW = lane ? (wlast >> (lane - 1)) & 1ull : 0ull;
     uint64_t S = W & ~((W << 1) | prevW);
     uint64_t E = ~W & ((W << 1) | prevW);
+    if (PACK) {
+      S |= bq & W;
+      E |= bq & ((W << 1) | prevW);
+    }
     const uint32_t firstE = E ? lane * 64 + (uint32_t)__builtin_ctzll(E) : kWaveWindow;
     const uint64_t hasE = __ballot(E != 0);
     const uint64_t later = lane == 63 ? 0ull : (hasE & (~0ull << (lane + 1)));
@@ -821,7 +935,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     const uint32_t tincl = wave_incl_add(nts);
     const uint32_t ntok = (uint32_t)__builtin_amdgcn_readlane((int)tincl, 63);
     if (ntok > kWaveTokens) {                               // wave-uniform
-      if (lane == 0) p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
+      if (PACK) defer_pack(p, d, np, lane);
+      else if (lane == 0) p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
       continue;
     }
     bool longtok = false;
@@ -835,7 +950,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         if (s0) s0 &= s0 - 1; else s1 &= s1 - 1;
         if (e0) e0 &= e0 - 1; else e1 &= e1 - 1;
         longtok |= te - tp > 8;
-        sm.list[at++] = tp | (te << 16);
+        const uint32_t j = PACK ? dbase + (uint32_t)__popcll(bm & ((2ull << (tp - 64 * lane)) - 1)) : 0u;
+        sm.list[at++] = span_entry(tp, te, j);
       }
     }
     asm volatile("" ::: "memory");
@@ -849,19 +965,20 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     for (uint32_t tb = 0; tb < ntok && !overflow;) {       // batch width by what is left
       const uint32_t rem = ntok - tb;
       if (anylong) {
-        if (rem > 256) { hist_batch<8, true>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 512; }
-        else if (rem > 128) { hist_batch<4, true>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 256; }
-        else { hist_batch<2, true>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 128; }
+        if (rem > 256) { hist_batch<8, true, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 512; }
+        else if (rem > 128) { hist_batch<4, true, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 256; }
+        else { hist_batch<2, true, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 128; }
       } else {
-        if (rem > 256) { hist_batch<8, false>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 512; }
-        else if (rem > 128) { hist_batch<4, false>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 256; }
-        else { hist_batch<2, false>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 128; }
+        if (rem > 256) { hist_batch<8, false, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 512; }
+        else if (rem > 128) { hist_batch<4, false, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 256; }
+        else { hist_batch<2, false, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 128; }
       }
     }
     const uint32_t len = wave_sum(toks), nu = wave_sum(claims);
     if (overflow || nu > kWaveTerms) {                      // wave-uniform: long path
       clear_table(sm, lane);
-      if (lane == 0) p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
+      if (PACK) defer_pack(p, d, np, lane);
+      else if (lane == 0) p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
       continue;
     }
     if (p.debug_stop == 3) { clear_table(sm, lane); continue; }
@@ -886,8 +1003,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     }
 
     // ---- dictionary slots of terms lane + 64k
-    uint32_t g[kWaveK], tf[kWaveK];
+    uint32_t g[kWaveK], tf[kWaveK], tdoc[kWaveK];
     uint32_t actm = 0;
+    if (PACK && lane < kPackMax) { pk_len[lane] = 0; pk_nu[lane] = 0; }
     {
       uint64_t lo[kWaveK];
       uint32_t ps[kWaveK];
@@ -906,7 +1024,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
           tf[k] = (sm.cnt[s >> 1] >> (16 * (s & 1))) & 0xFFFFu;
           const bool f = in & ((key & kFoldBit) != 0);
           const bool sh = in & !f;
-          lo[k] = sh ? key : 0ull;
+          tdoc[k] = PACK ? key_doc(key) : 0u;
+          if (PACK && in) { atomicAdd(&pk_len[tdoc[k]], tf[k]); atomicAdd(&pk_nu[tdoc[k]], 1u); }
+          lo[k] = sh ? (PACK ? key & ~kPackTagMask : key) : 0ull;
           foldm |= (uint32_t)f << k;
           actm |= (uint32_t)in << k;
           ps[k] = dict_home(dict_hash_short(lo[k]), dmask) & ~1u;
@@ -1013,13 +1133,25 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     uint32_t *st_col = reinterpret_cast<uint32_t *>(sm.key);
     uint32_t *st_tf = st_col + kWaveSlots;
     const uint32_t st_noop = kWaveSlots - 64 + lane;          // unused staging words (nu <= kWaveTerms)
+    // PACK: groups are (document, range) in that order, so each document's row
+    // is one contiguous run of the staging area starting at pk_start[j]
+    const uint32_t rbits = (uint32_t)__builtin_ctz(R);
+    const uint32_t G = PACK ? np << rbits : R;
+    if (PACK) {
+      const uint32_t nuj = lane < np ? pk_nu[lane] : 0u;
+      const uint32_t incl = wave_incl_add(nuj);
+      if (lane < np) {
+        pk_start[lane] = incl - nuj;
+        pk_row[lane] = (pofs + src + lane) >> 1;             // csr_row_base of document src + lane
+      }
+    }
     uint32_t run = 0;
-    for (uint32_t rb = 0; rb < R; rb += 8) {
+    for (uint32_t rb = 0; rb < G; rb += 8) {
       uint64_t c0 = 0, c1 = 0;
       uint32_t fk[kWaveK];
 #pragma unroll
       for (int k = 0; k < (int)kWaveK; k++) {
-        const uint32_t f = (g[k] >> p.range_shift) - rb;
+        const uint32_t f = (PACK ? (tdoc[k] << rbits) + (g[k] >> p.range_shift) : (g[k] >> p.range_shift)) - rb;
         const bool inr = ((actm >> k) & 1u) && f < 8;
         fk[k] = inr ? f : 8u;                                  // 8 = not in this pass
         const uint64_t inc = inr ? (1ull << (16 * (f & 3))) : 0ull;
@@ -1045,7 +1177,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         if ((uint32_t)f == lane) { lane_base = acc; lane_tot = t; }
         acc += t;
       }
-      if (lane < 8 && rb + lane < R) p.rsplit[d * R + rb + lane] = run + lane_base + lane_tot;
+      if (!PACK && lane < 8 && rb + lane < R) p.rsplit[d * R + rb + lane] = run + lane_base + lane_tot;
+      if (PACK && lane < 8 && rb + lane < G) {
+        const uint32_t gg = rb + lane, j = gg >> rbits;
+        p.rsplit[(d + j) * R + (gg & (R - 1))] = run + lane_base + lane_tot - pk_start[j];
+      }
       uint64_t pk0 = ((uint64_t)w[0] | ((uint64_t)w[1] << 32)) + fb0;
       uint64_t pk1 = ((uint64_t)w[2] | ((uint64_t)w[3] << 32)) + fb1;
 #pragma unroll
@@ -1059,11 +1195,30 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         pk0 += (f & 4) ? 0ull : inc;
         pk1 += (f & 4) ? inc : 0ull;
         st_col[pos] = g[k];
-        st_tf[pos] = tf[k];
+        st_tf[pos] = PACK ? tf[k] | (tdoc[k] << 24) : tf[k];
       }
       run += acc;
     }
     asm volatile("" ::: "memory");
+    if (PACK) {
+      for (uint32_t i = lane; i < nu; i += 64) {
+        const uint32_t t = st_tf[i], j = t >> 24;
+        const uint64_t row = pk_row[j] + i - pk_start[j];
+        p.csr_col[row] = st_col[i];
+        p.csr_tf[row] = t & 0xFFFFFFu;
+      }
+      if (lane < np) {
+        const uint32_t lj = pk_len[lane], nj = pk_nu[lane];
+        p.doc_len[d + lane] = lj;
+        p.doc_nuniq[d + lane] = nj;
+        p.doc_norm[d + lane] = (uint8_t)int_to_byte4(lj);
+        my_doc_count += lj > 0;
+        my_ttf += lj;
+        my_nnz += nj;
+      }
+      clear_table(sm, lane);
+      continue;
+    }
     {
       const uint64_t row = csr_row_base(p.offsets, src);
       for (uint32_t i = lane; i < nu; i += 64) {
@@ -1081,7 +1236,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       my_nnz += nu;
     }
   }
-  if (lane == 0) {
+  if (my_ttf | my_nnz | my_doc_count) {                    // lane 0 (PACK: lanes < pack)
     atomicAdd(&p.stats[0], my_doc_count);
     atomicAdd(&p.stats[1], my_ttf);
     atomicAdd(&p.stats[2], my_nnz);
@@ -1588,7 +1743,8 @@ __global__ void __launch_bounds__(1024) k_scatter_sort(PostingParams p) {
 // launchers
 
 hipError_t launch_tokenize_wave(const BuildParams &p, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(k_tokenize_wave, dim3(grid), dim3(64), 0, s, p);
+  if (p.pack > 1) hipLaunchKernelGGL(k_tokenize_wave<true>, dim3(grid), dim3(64), 0, s, p);
+  else hipLaunchKernelGGL(k_tokenize_wave<false>, dim3(grid), dim3(64), 0, s, p);
   return hipGetLastError();
 }
 hipError_t launch_tokenize_long(const BuildParams &p, int grid, hipStream_t s) {

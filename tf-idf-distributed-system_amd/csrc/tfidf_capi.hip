@@ -127,6 +127,9 @@ struct tfidf_index {
   DevBuf d_live_map;
   uint32_t cap_log2 = 18, C = 0, range_shift = 15, R = 1, n_blocks = 0;
   DevBuf dict, csr_col, csr_tf, doc_len, doc_nuniq, doc_norm, rsplit, long_list, counters, blk, bbase, post, post_tmp;
+  DevBuf retry_list;                   // packed wave path: documents deferred to the single-document pass
+  uint32_t pack_docs = 1;              // documents per wave window in the last commit
+  uint64_t pack_retried = 0;           // documents the packs deferred in the last commit
   // term-major inversion (large vocabularies): compact row offsets, sort values (x2), term offsets, df
   bool term_major = false;
   DevBuf row_off, tvals, toff, tdf, term_tmp;
@@ -209,7 +212,7 @@ extern "C" int tfidf_destroy(tfidf_index *ix) {
   hipStreamSynchronize(ix->stream);
   DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->d_live_map, &ix->dict, &ix->csr_col, &ix->csr_tf, &ix->doc_len,
                     &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->long_list, &ix->counters, &ix->blk,
-                    &ix->bbase, &ix->post, &ix->post_tmp, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->canon_of_slot,
+                    &ix->retry_list, &ix->bbase, &ix->post, &ix->post_tmp, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->canon_of_slot,
                     &ix->q_off, &ix->q_slot, &ix->q_w, &ix->cache, &ix->cand, &ix->cand_n, &ix->out_doc,
                     &ix->out_score, &ix->out_n, &ix->hits, &ix->hits_n, &ix->hits_c, &ix->hits_s, &ix->sort_tmp,
                     &ix->row_off, &ix->tvals, &ix->toff, &ix->tdf, &ix->term_tmp, &ix->sent_slot, &ix->vcounts,
@@ -634,6 +637,16 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   HIP_TRY(ix->rsplit.reserve(N * ix->R * 4 + 4));
   HIP_TRY(ix->long_list.reserve(N * 4 + 4));
   HIP_TRY(ix->counters.reserve(64));
+  // Short-document corpora: the wave path indexes packs of consecutive
+  // documents per window (about kPackBytes of text per pack; SURVEY cfg 5
+  // shape: 6 documents of ~330 B).  TFIDF_PACK_DOCS overrides (tests).
+  uint32_t pack = 1;
+  {
+    const uint64_t avg = ix->n_staged ? ix->text_bytes / ix->n_staged : 0;
+    if (avg) pack = (uint32_t)std::min<uint64_t>(kPackMaxDocs, std::max<uint64_t>(1, kPackBytes / avg));
+    if (const char *e = getenv("TFIDF_PACK_DOCS")) pack = (uint32_t)std::max(1, std::min(atoi(e), (int)kPackMaxDocs));
+  }
+  if (pack > 1) HIP_TRY(ix->retry_list.reserve(N * 4 + 4));
   if (ix->term_major) {
     HIP_TRY(ix->row_off.reserve(N * 4 + 4));
     HIP_TRY(ix->toff.reserve(((size_t)C + 1) * 8));
@@ -643,7 +656,7 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
     HIP_TRY(ix->bbase.reserve((size_t)(ix->n_blocks + 2) * 8));
   }
 
-  // counters: [0..2] stats u64, [3] err flags u32 + [3].hi first doc, [4] long_count
+  // counters: [0..2] stats u64, [3] err flags u32 + [3].hi first doc, [4] long_count, [5] retry_count
   uint64_t *ctr = ix->counters.as<uint64_t>();
   HIP_TRY(hipMemsetAsync(ix->counters.p, 0, 64, s));
   HIP_TRY(hipMemsetAsync(ix->dict.p, 0, (size_t)2 * C * 8, s));
@@ -668,11 +681,31 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   bp.stats = reinterpret_cast<unsigned long long *>(ctr);
   bp.err = reinterpret_cast<uint32_t *>(ctr + 3);
   if (const char *ds = getenv("TFIDF_DEBUG_STOP")) bp.debug_stop = (uint32_t)atoi(ds);   // profiling only
+  bp.pack = pack;
+  bp.retry_list = pack > 1 ? ix->retry_list.as<uint32_t>() : nullptr;
+  bp.retry_count = reinterpret_cast<uint32_t *>(ctr + 5);
+  ix->pack_docs = pack;
+  ix->pack_retried = 0;
 
   HIP_TRY(hipEventRecord(ix->ev[EV_START], s));
   if (N) {
-    const uint64_t grid = std::min<uint64_t>(N, (uint64_t)ix->num_cus * kWaveWGsPerCU);
+    const uint64_t units = (N + pack - 1) / pack;
+    const uint64_t grid = std::min<uint64_t>(units, (uint64_t)ix->num_cus * kWaveWGsPerCU);
     HIP_TRY(launch_tokenize_wave(bp, (int)grid, s));
+    if (pack > 1 && !bp.debug_stop) {       // documents the packs could not take: one per wave
+      uint32_t n_retry = 0;
+      HIP_TRY(hipMemcpyAsync(&n_retry, ctr + 5, 4, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      ix->pack_retried = n_retry;
+      if (n_retry) {
+        BuildParams rp = bp;
+        rp.pack = 1;
+        rp.doc_list = bp.retry_list;
+        rp.doc_list_count = bp.retry_count;
+        const uint64_t rgrid = std::min<uint64_t>(n_retry, (uint64_t)ix->num_cus * kWaveWGsPerCU);
+        HIP_TRY(launch_tokenize_wave(rp, (int)rgrid, s));
+      }
+    }
   }
   HIP_TRY(hipEventRecord(ix->ev[EV_TOK], s));
   if (bp.debug_stop) {                      // profiling only: rows are incomplete, stop here
@@ -844,6 +877,8 @@ extern "C" int tfidf_stats(const tfidf_index *ix, tfidf_index_stats *out) {
   out->long_docs = ix->long_docs;
   out->text_bytes = ix->text_bytes;
   out->term_major = ix->committed && ix->term_major;
+  out->pack_docs = ix->pack_docs;
+  out->pack_retried = ix->pack_retried;
   const DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->dict, &ix->csr_col, &ix->csr_tf, &ix->doc_len,
                           &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->blk, &ix->bbase, &ix->post,
                           &ix->toff, &ix->tdf};

@@ -45,6 +45,15 @@ struct BuildParams {
   uint32_t *lt_g;             // lt_slots per workgroup
   uint32_t lt_slots_log2;     // table slots per workgroup (max)
   uint32_t debug_stop;        // profiling only (TFIDF_DEBUG_STOP): end each document after phase N
+  // wave path units: pack > 1 = packs of `pack` consecutive documents per
+  // window (short-document corpora); documents a pack cannot take go to
+  // retry_list.  doc_list (pack <= 1): process these documents only
+  // (*doc_list_count of them) instead of 0..n_docs-1.
+  uint32_t pack;
+  uint32_t *retry_list;
+  uint32_t *retry_count;
+  const uint32_t *doc_list;
+  const uint32_t *doc_list_count;
 };
 
 __host__ __device__ inline uint64_t csr_row_base(const uint64_t *offsets, uint64_t src) {
@@ -73,7 +82,9 @@ struct PostingParams {
 
 // --- launch wrappers (kernels_index.hip) ---
 hipError_t launch_tokenize_wave(const BuildParams &p, int grid, hipStream_t s);
-constexpr uint32_t kWaveWGsPerCU = 8;    // 64-thread workgroups per CU (2 waves/SIMD: VGPR-bound)
+constexpr uint32_t kWaveWGsPerCU = 8;
+constexpr uint32_t kPackMaxDocs = 16;     // documents per packed window (<= kPackMax, kernels_index.hip)
+constexpr uint64_t kPackBytes = 2048;     // text per packed window (auto pack size)    // 64-thread workgroups per CU (2 waves/SIMD: VGPR-bound)
 hipError_t launch_tokenize_long(const BuildParams &p, int grid, hipStream_t s);
 hipError_t launch_df_partial(const PostingParams &p, hipStream_t s);
 hipError_t launch_df_sum(const PostingParams &p, hipStream_t s);
