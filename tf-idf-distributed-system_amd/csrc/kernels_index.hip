@@ -1717,7 +1717,7 @@ __global__ void __launch_bounds__(1024) k_scatter_sort(PostingParams p) {
   __syncthreads();
   const uint32_t d0 = b * kBlockDocs;
   const uint32_t lane = threadIdx.x & 63;
-  constexpr int U = 4;                                       // entries per thread in flight
+  constexpr int U = 8;              // entries per thread in flight (8: a ~5 k-entry stream in one round; 4 was 3.4% slower)
   for (uint32_t e0 = lo; e0 < hi; e0 += U * blockDim.x) {   // uniform trip count: all lanes ballot
     uint64_t x[U];
 #pragma unroll
