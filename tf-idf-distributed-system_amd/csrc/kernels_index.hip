@@ -1577,8 +1577,10 @@ __global__ void k_block_base(PostingParams p) {
 //   k_scatter_part : per tile, each posting is appended to one of the tile's
 //                    sub-range streams (kSubSlots slots each) in a temporary
 //                    buffer laid out exactly like the postings (stream k's
-//                    region = the final region of its slots, from blk), packed
-//                    doc_local(13) | slot_low(10) | tf(24) | norm(8);
+//                    region = the final region of its slots, from blk), one
+//                    32-bit word doc_local(13) | slot_low(9) | tf(10); tf >=
+//                    1023 is stored as 1023 and re-read from the CSR row in
+//                    pass 2, the norm is re-read from doc_norm there;
 //   k_scatter_sort : per stream (~86 KB), LDS cursor per slot, final postings
 //                    written inside the stream's own region.
 #ifndef TFIDF_SUB_BITS
@@ -1586,8 +1588,9 @@ __global__ void k_block_base(PostingParams p) {
 #endif
 constexpr uint32_t kSubBits = TFIDF_SUB_BITS;
 constexpr uint32_t kSubSlots = 1u << kSubBits;
-constexpr uint32_t kTmpTfShift = 13 + kSubBits;              // temp word: doc_local(13) | slot_low | tf(24) | norm(8)
-constexpr uint32_t kTmpNormShift = kTmpTfShift + 24;
+constexpr uint32_t kTmpTfShift = 13 + kSubBits;              // temp word: doc_local(13) | slot_low | tf(10)
+constexpr uint32_t kTmpTfEsc = (1u << (32 - kTmpTfShift)) - 1; // tf field value meaning "tf >= this: see the CSR"
+static_assert(kTmpTfShift <= 22, "temp word layout");
 
 __device__ __forceinline__ void part_entries(const PostingParams &p, uint32_t *bcur, uint32_t rmask, uint64_t bb,
                                              const InvGroup &g, uint64_t dd, uint32_t d0l, uint32_t stride,
@@ -1601,8 +1604,7 @@ __device__ __forceinline__ void part_entries(const PostingParams &p, uint32_t *b
     *tf_big |= in && t[j] > kMaxTf;
     const uint32_t sl = c[j] & rmask;
     const uint32_t dl = (uint32_t)(dd + (uint64_t)stride * j) - d0l;
-    const uint64_t val = (uint64_t)dl | ((uint64_t)(sl & (kSubSlots - 1)) << 13) |
-                         ((uint64_t)(t[j] & kMaxTf) << kTmpTfShift) | ((uint64_t)g.nrm[j] << kTmpNormShift);
+    const uint32_t val = dl | ((sl & (kSubSlots - 1)) << 13) | (min(t[j], kTmpTfEsc) << kTmpTfShift);
     const uint32_t pos = cursor_bump<kRangeBits - kSubBits + 1>(bcur, in ? sl >> kSubBits : kNoop, lane);
     if (in) p.post_tmp[bb + pos] = val;
   }
@@ -1615,7 +1617,7 @@ __device__ __forceinline__ void part_entries(const PostingParams &p, uint32_t *b
 // entry).  The stream id rides in bits 56..61 of the temp word (pass 2 ignores
 // them).
 constexpr uint32_t kPartStreams = kRangeSlots / kSubSlots;  // 64
-static_assert(kTmpNormShift + 8 <= 56 && kPartStreams <= 64, "temp word layout");
+static_assert(kPartStreams <= 64, "temp word layout");
 struct PartWave {
   uint64_t stage[kInvDocs * 64];
   uint32_t cnt[64], soff[64], gb[64];
@@ -1638,8 +1640,8 @@ __device__ __forceinline__ void part_group_staged(const PostingParams &p, uint32
     if (in) {
       *tf_big |= t[j] > kMaxTf;
       const uint32_t dl = (uint32_t)(dd + (uint64_t)stride * j) - d0l;
-      val[j] = (uint64_t)dl | ((uint64_t)(sl & (kSubSlots - 1)) << 13) | ((uint64_t)(t[j] & kMaxTf) << kTmpTfShift) |
-               ((uint64_t)g.nrm[j] << kTmpNormShift) | ((uint64_t)sj[j] << 56);
+      val[j] = (uint64_t)(dl | ((sl & (kSubSlots - 1)) << 13) | (min(t[j], kTmpTfEsc) << kTmpTfShift)) |
+               ((uint64_t)sj[j] << 56);
       rank[j] = atomicAdd(&w.cnt[sj[j]], 1u);
     }
   }
@@ -1657,7 +1659,7 @@ __device__ __forceinline__ void part_group_staged(const PostingParams &p, uint32
     if (ti < T) {
       const uint64_t v = w.stage[ti];
       const uint32_t st = (uint32_t)(v >> 56);
-      p.post_tmp[bb + w.gb[st] + (ti - w.soff[st])] = v;
+      p.post_tmp[bb + w.gb[st] + (ti - w.soff[st])] = (uint32_t)v;
     }
   }
 }
@@ -1680,12 +1682,12 @@ __global__ void __launch_bounds__(1024) k_scatter_part(PostingParams p) {
   const uint64_t step = (uint64_t)nw * kInvDocs;
   bool tf_big = false;
   uint64_t dd = d0 + wid;
-  InvGroup g = inv_group(p, dd, d1, nw, r, true);
+  InvGroup g = inv_group(p, dd, d1, nw, r, false);
   uint32_t c[kInvDocs], t[kInvDocs];
   if (dd < d1) inv_load(p, g, lane, c, t, true);
   while (dd < d1) {
     const uint64_t dn = dd + step;
-    const InvGroup gn = inv_group(p, dn, d1, nw, r, true);
+    const InvGroup gn = inv_group(p, dn, d1, nw, r, false);
     uint32_t cn[kInvDocs], tn[kInvDocs];
     if (dn < d1) inv_load(p, gn, lane, cn, tn, true);           // next group in flight
     part_group_staged(p, bcur, pwave[wid], rmask, bb, g, dd, (uint32_t)d0, nw, c, t, &tf_big);
@@ -1699,6 +1701,17 @@ __global__ void __launch_bounds__(1024) k_scatter_part(PostingParams p) {
     dd = dn;
   }
   if (tf_big) atomicOr(p.err, kErrTfTooLarge);
+}
+
+// tf of (doc, slot) from the document's CSR row segment of range r (the
+// escape path of the 10-bit temp tf field)
+__device__ uint32_t csr_tf_of(const PostingParams &p, uint64_t d, uint32_t r, uint32_t slot) {
+  uint64_t base;
+  uint32_t lo, hi;
+  doc_segment(p, d, r, &base, &lo, &hi);
+  for (uint32_t i = lo; i < hi; i++)
+    if (p.csr_col[base + i] == slot) return p.csr_tf[base + i];
+  return 0;
 }
 
 // grid (n_blocks, n_ranges, streams per range), 1024 threads: few streams per
@@ -1719,22 +1732,28 @@ __global__ void __launch_bounds__(1024) k_scatter_sort(PostingParams p) {
   const uint32_t lane = threadIdx.x & 63;
   constexpr int U = 8;              // entries per thread in flight (8: a ~5 k-entry stream in one round; 4 was 3.4% slower)
   for (uint32_t e0 = lo; e0 < hi; e0 += U * blockDim.x) {   // uniform trip count: all lanes ballot
-    uint64_t x[U];
+    uint32_t x[U], nrm[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t e = e0 + u * blockDim.x + threadIdx.x;
-      x[u] = e < hi ? p.post_tmp[bb + e] : 0ull;
+      x[u] = e < hi ? p.post_tmp[bb + e] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t e = e0 + u * blockDim.x + threadIdx.x;
+      nrm[u] = e < hi ? p.doc_norm[d0 + (x[u] & (kBlockDocs - 1))] : 0u;
     }
 #pragma unroll
     for (int u = 0; u < U; u++) {
       const uint32_t e = e0 + u * blockDim.x + threadIdx.x;
       if (__all(e >= hi)) break;
       const bool in = e < hi;
-      const uint32_t sl = in ? (uint32_t)(x[u] >> 13) & (kSubSlots - 1) : kSubSlots;   // kSubSlots: no-op key
+      const uint32_t sl = in ? (x[u] >> 13) & (kSubSlots - 1) : kSubSlots;   // kSubSlots: no-op key
       const uint32_t pos = cursor_bump<kSubBits + 1>(cur, sl, lane);
-      const uint32_t tf = (uint32_t)(x[u] >> kTmpTfShift) & kMaxTf, nrm = (uint32_t)(x[u] >> kTmpNormShift) & 0xFFu;
-      if (in)
-        p.post[bb + pos] = (uint64_t)(d0 + ((uint32_t)x[u] & (kBlockDocs - 1))) | ((uint64_t)((tf << 8) | nrm) << 32);
+      const uint32_t doc = d0 + (x[u] & (kBlockDocs - 1));
+      uint32_t tf = x[u] >> kTmpTfShift;
+      if (in && tf == kTmpTfEsc) tf = csr_tf_of(p, doc, r, (uint32_t)s0 + sl);      // rare: tf >= 1023
+      if (in) p.post[bb + pos] = (uint64_t)doc | ((uint64_t)((tf << 8) | nrm[u]) << 32);
     }
   }
 }

@@ -780,7 +780,7 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   pp.blk = ix->blk.as<uint32_t>();
   pp.bbase = ix->bbase.as<uint64_t>();
   pp.post = ix->post.as<uint64_t>();
-  pp.post_tmp = ix->post_tmp.as<uint64_t>();
+  pp.post_tmp = ix->post_tmp.as<uint32_t>();
   pp.err = bp.err;
   HIP_TRY(hipEventRecord(ix->ev[EV_D0], s));
   if (ix->term_major) {

@@ -77,7 +77,7 @@ struct PostingParams {
   uint64_t *post;             // [nnz]: doc | (tf << 8 | norm) << 32; block b, slot s at
                               // bbase[b] + blk[b][s]
   uint32_t *err;
-  uint64_t *post_tmp;         // [nnz] scatter pass 1 output (sub-range streams, same regions)
+  uint32_t *post_tmp;         // [nnz] scatter pass 1 output (sub-range streams, same regions)
 };
 
 // --- launch wrappers (kernels_index.hip) ---
