@@ -692,8 +692,8 @@ __device__ __forceinline__ void hist_batch(WaveSmem &sm, const BuildParams &p, u
     const uint64_t m64 = n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1);
     const uint32_t t0 = __builtin_amdgcn_alignbyte(dw[k][1], dw[k][0], o) & (uint32_t)m64;
     const uint32_t t1 = __builtin_amdgcn_alignbyte(dw[k][2], dw[k][1], o) & (uint32_t)(m64 >> 32);
-    const bool valid =
-        !under | ((((t0 ^ 0x5F5F5F5Fu) & (uint32_t)m64) | ((t1 ^ 0x5F5F5F5Fu) & (uint32_t)(m64 >> 32))) != 0);
+    const bool valid = !(FOLD && under) |
+                       ((((t0 ^ 0x5F5F5F5Fu) & (uint32_t)m64) | ((t1 ^ 0x5F5F5F5Fu) & (uint32_t)(m64 >> 32))) != 0);
     const uint32_t l0 = lower4(t0) | (PACK ? pack_tag(span_doc(ent[k])) : 0u), l1 = lower4(t1);
     tkey[k] = (uint64_t)l0 | ((uint64_t)l1 << 32);
     slot[k] = ((l0 ^ rotl32(l1, 16)) * 0x85EBCA77u) >> (32 - kWaveSlotBits);
@@ -957,9 +957,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     asm volatile("" ::: "memory");
     if (p.debug_stop == 2) continue;
 
-    // ---- per-document histogram in LDS (folded-key checks only when the
-    // document holds a token of more than 8 bytes)
-    const bool anylong = __any(longtok);
+    // ---- per-document histogram in LDS (folded-key and '_'-only checks only
+    // when the document holds a token of more than 8 bytes or a '_')
+    const bool anylong = __any(longtok) || under;
     uint32_t claims = 0, toks = 0;
     bool overflow = false;
     for (uint32_t tb = 0; tb < ntok && !overflow;) {       // batch width by what is left
@@ -1749,7 +1749,7 @@ __global__ void __launch_bounds__(1024) k_scatter_sort(PostingParams p) {
       if (__all(e >= hi)) break;
       const bool in = e < hi;
       const uint32_t sl = in ? (x[u] >> 13) & (kSubSlots - 1) : kSubSlots;   // kSubSlots: no-op key
-      const uint32_t pos = cursor_bump<kSubBits + 1>(cur, sl, lane);
+      const uint32_t pos = cursor_bump<kSubBits + 1>(cur, sl, lane);   // (plain LDS atomics: 4% slower)
       const uint32_t doc = d0 + (x[u] & (kBlockDocs - 1));
       uint32_t tf = x[u] >> kTmpTfShift;
       if (in && tf == kTmpTfEsc) tf = csr_tf_of(p, doc, r, (uint32_t)s0 + sl);      // rare: tf >= 1023
