@@ -50,8 +50,8 @@ extern "C" {
 #define TFIDF_E_INVALID_ARG 1
 #define TFIDF_E_HIP 2
 #define TFIDF_E_OOM 3
-#define TFIDF_E_UNSUPPORTED_INPUT 4 /* non-ASCII document, token > 255 chars, tf >= 2^24 */
-#define TFIDF_E_UNSUPPORTED_QUERY 5 /* non-ASCII query, AND/OR/NOT operator words */
+#define TFIDF_E_UNSUPPORTED_INPUT 4 /* malformed UTF-8 document (Files.readString throws), tf >= 2^24 */
+#define TFIDF_E_UNSUPPORTED_QUERY 5 /* malformed UTF-8 query, AND/OR/NOT operator words */
 #define TFIDF_E_CAPACITY 6          /* vocabulary capacity exceeded */
 #define TFIDF_E_STATE 7             /* e.g. search before commit */
 #define TFIDF_E_BUFFER 8            /* caller buffer too small; *n_out holds the size needed */
@@ -203,6 +203,14 @@ int tfidf_clear_global_stats(tfidf_index *ix);
 
 /* Term key of an analysed (lower-cased) token, as the device computes it. */
 int tfidf_term_key(const uint8_t *term, uint64_t len, uint64_t *lo, uint64_t *hi);
+
+/* StandardAnalyzer (Worker.java:71,225: StandardTokenizer + LowerCaseFilter,
+ * full Unicode, maxTokenLength 255) on the host, the same scanner the index
+ * build runs on the device: NUL-terminated lower-cased UTF-8 tokens in order.
+ * TFIDF_E_BUFFER with *n_bytes = size needed when cap is too small;
+ * TFIDF_E_UNSUPPORTED_INPUT for malformed UTF-8. */
+int tfidf_analyze(const uint8_t *text, uint64_t len, char *out, uint64_t cap, uint64_t *n_tokens,
+                  uint64_t *n_bytes);
 
 /* Leader.start merge (Leader.java:73-88): names (concatenated, offsets[n+1])
  * with double scores in worker-response order -> distinct names sorted by

@@ -30,6 +30,8 @@ def _load():
                                    C.POINTER(C.c_double))
     sig = {
         "orc_tokenize": (C.c_int64, [C.c_char_p, C.c_uint64, C.c_uint32, u32p, u32p, C.c_uint64]),
+        "orc_tokenize_unicode": (C.c_int64, [C.c_char_p, C.c_uint64, C.c_uint32, u32p, u32p, C.c_uint64]),
+        "orc_lower_utf8": (C.c_uint64, [C.c_char_p, C.c_uint64, C.c_char_p]),
         "orc_int_to_byte4": (C.c_uint8, [C.c_int32]),
         "orc_byte4_to_int": (C.c_int32, [C.c_uint8]),
         "orc_create": (C.c_void_p, [C.c_float, C.c_float]),
@@ -77,15 +79,24 @@ def _p(a, ct):
     return a.ctypes.data_as(C.POINTER(ct))
 
 
-def tokenize(text: bytes, max_len=255):
-    """Token byte strings (lower-cased) of ``text``; raises on non-ASCII."""
+def lower_utf8(tok: bytes) -> bytes:
+    """LowerCaseFilter of one token (JDK 17 Character.toLowerCase per code point)."""
+    out = C.create_string_buffer(2 * len(tok) + 8)
+    n = lib().orc_lower_utf8(tok, len(tok), out)
+    return out.raw[:n]
+
+
+def tokenize(text: bytes, max_len=255, force_unicode=False):
+    """Token byte strings (lower-cased) of ``text``; raises on malformed UTF-8.
+    ASCII text takes the oracle's byte-rule path unless force_unicode."""
     cap = len(text) // 2 + 2
     st = np.zeros(cap, np.uint32)
     ln = np.zeros(cap, np.uint32)
-    n = lib().orc_tokenize(text, len(text), max_len, _p(st, C.c_uint32), _p(ln, C.c_uint32), cap)
+    f = lib().orc_tokenize_unicode if force_unicode else lib().orc_tokenize
+    n = f(text, len(text), max_len, _p(st, C.c_uint32), _p(ln, C.c_uint32), cap)
     if n < 0:
-        raise ValueError("unsupported input (non-ASCII)")
-    return [text[s:s + l].lower() for s, l in zip(st[:n], ln[:n])]
+        raise ValueError("unsupported input (malformed UTF-8)")
+    return [lower_utf8(text[s:s + l]) for s, l in zip(st[:n], ln[:n])]
 
 
 def int_to_byte4(i):

@@ -2,9 +2,12 @@
  * tfidf_oracle.c — CPU ORACLE (test infrastructure; see tfidf_oracle.h).
  *
  * Restates, single-threaded and in Java's float/double operation order:
- *  - Lucene 9.8.0 StandardTokenizer (JFlex UAX#29 word-break grammar), ASCII
- *    subset, maxTokenLength 255 (longer tokens are chopped and scanning
- *    restarts at the chop point), LowerCaseFilter, empty StopFilter
+ *  - Lucene 9.8.0 StandardTokenizer (JFlex UAX#29 word-break grammar, full
+ *    Unicode: letters, digits, Katakana, Hebrew quotes, Complex_Context runs,
+ *    Han / Hiragana single chars, emoji; ASCII text takes a byte-rule fast
+ *    path that tests check against the Unicode rules), maxTokenLength 255
+ *    (UTF-16 units; longer tokens are chopped and scanning restarts at the
+ *    chop point), LowerCaseFilter (JDK 17 Character.toLowerCase), empty StopFilter
  *    (StandardAnalyzer, constructed at Worker.java:71 and :225).
  *  - IndexingChain inversion per doc (Worker.java:218): TF per term, field
  *    length = #tokens, norm = SmallFloat.intToByte4(length) (0 when empty).
@@ -55,10 +58,13 @@ static int is_word(const uint8_t *s, uint64_t lo, uint64_t n, uint64_t i) {
   return 0;
 }
 
+int64_t orc_tokenize_unicode(const uint8_t *s, uint64_t n, uint32_t max_len, uint32_t *starts, uint32_t *lens,
+                             uint64_t cap);
+
 int64_t orc_tokenize(const uint8_t *s, uint64_t n, uint32_t max_len,
                      uint32_t *starts, uint32_t *lens, uint64_t cap) {
   for (uint64_t i = 0; i < n; i++)
-    if (s[i] >= 0x80) return ORC_E_UNSUPPORTED;
+    if (s[i] >= 0x80) return orc_tokenize_unicode(s, n, max_len, starts, lens, cap);
   if (max_len == 0) max_len = 255;
   uint64_t lo = 0, i = 0;
   int64_t cnt = 0;
@@ -84,6 +90,199 @@ int64_t orc_tokenize(const uint8_t *s, uint64_t n, uint32_t max_len,
     i = j;
   }
   return cnt;
+}
+
+/* ------------------------------------------------------------------ */
+/* Full-Unicode StandardTokenizer (Lucene 9.8.0 StandardTokenizerImpl, JFlex
+ * `%unicode 9.0`), restated by LOCAL JOIN RULES between adjacent units (the
+ * product scans with a longest-match DFA instead, unicode_scan.h; the Python
+ * transcription of the JFlex grammar in tests/ pins both).  A unit is a head
+ * char plus its trailing Extend/Format/ZWJ chars (WB4); a head of class OTHER
+ * does not take extenders (JFlex's [^] rule consumes one char), so an
+ * extender after it is its own unit, skipped — or, if it is a Complex_Context
+ * (Line_Break SA) mark, the start of an SA run. */
+#include "unicode_props.h"
+
+enum { UC_OTHER = 0, UC_AL, UC_HL, UC_NU, UC_KA, UC_EX, UC_ML, UC_MNL, UC_MN, UC_SQ, UC_DQ, UC_EXT, UC_EXT_SA,
+       UC_ZWJ, UC_SA, UC_HAN, UC_HIRA, UC_RI, UC_EMO };
+
+static int uc_cls(uint32_t cp) {
+  int lo = 0, hi = UC_NRANGES - 1;
+  while (lo <= hi) {
+    int mid = (lo + hi) / 2;
+    if (cp < uc_ranges[mid][0]) hi = mid - 1;
+    else if (cp > uc_ranges[mid][1]) lo = mid + 1;
+    else return (int)uc_ranges[mid][2];
+  }
+  return UC_OTHER;
+}
+static uint32_t uc_tolower(uint32_t cp) {   /* JDK 17 Character.toLowerCase(int) */
+  int lo = 0, hi = UC_NLOWER - 1;
+  while (lo <= hi) {
+    int mid = (lo + hi) / 2;
+    if (cp < uc_lower[mid][0]) hi = mid - 1;
+    else if (cp > uc_lower[mid][0]) lo = mid + 1;
+    else return uc_lower[mid][1];
+  }
+  return cp;
+}
+static int is_ext(int c) { return c == UC_EXT || c == UC_EXT_SA || c == UC_ZWJ; }
+static int is_ahl(int c) { return c == UC_AL || c == UC_HL; }
+static int is_midlet(int c) { return c == UC_ML || c == UC_MNL || c == UC_SQ; }
+static int is_midnum(int c) { return c == UC_MN || c == UC_MNL || c == UC_SQ; }
+static int is_wordish(int c) { return c == UC_AL || c == UC_HL || c == UC_NU || c == UC_KA || c == UC_EX; }
+
+/* RFC 3629 strict decode of the whole text; -1 on malformed input. */
+static int64_t utf8_all(const uint8_t *s, uint64_t n, uint32_t *cps, uint32_t *offs) {
+  uint64_t i = 0, k = 0;
+  while (i < n) {
+    uint32_t b = s[i], cp, need, min;
+    if (b < 0x80) { cp = b; need = 0; min = 0; }
+    else if ((b & 0xE0) == 0xC0) { cp = b & 0x1F; need = 1; min = 0x80; }
+    else if ((b & 0xF0) == 0xE0) { cp = b & 0x0F; need = 2; min = 0x800; }
+    else if ((b & 0xF8) == 0xF0) { cp = b & 0x07; need = 3; min = 0x10000; }
+    else return -1;
+    if (i + need >= n && need) return -1;
+    for (uint32_t t = 1; t <= need; t++) {
+      uint32_t c = s[i + t];
+      if ((c & 0xC0) != 0x80) return -1;
+      cp = (cp << 6) | (c & 0x3F);
+    }
+    if (cp < min || cp > 0x10FFFF || (cp >= 0xD800 && cp <= 0xDFFF)) return -1;
+    cps[k] = cp;
+    offs[k] = (uint32_t)i;
+    k++;
+    i += need + 1;
+  }
+  offs[k] = (uint32_t)n;
+  return (int64_t)k;
+}
+
+typedef struct { uint64_t a, b; int c; int zwj; } uc_unit_t;   /* cp range [a, b), head class */
+
+/* unit at code point index i (head never an absorbed extender) */
+static uc_unit_t unit_at(const int *cls, uint64_t m, uint64_t i) {
+  uc_unit_t u;
+  u.a = i; u.c = cls[i]; u.zwj = 0;
+  uint64_t j = i + 1;
+  if (u.c == UC_EXT_SA) u.c = UC_SA;                 /* orphan SA mark: an SA head */
+  if (u.c != UC_OTHER && u.c != UC_EXT && u.c != UC_ZWJ)
+    while (j < m && is_ext(cls[j])) { u.zwj = cls[j] == UC_ZWJ; j++; }
+  u.b = j;
+  return u;
+}
+
+/* do units x (with predecessor w, or w.c = -1) and y (successor z, or -1) join in one WORD token? */
+static int word_join(int w, int x, int y, int z) {
+  if (x == UC_EX && is_wordish(y)) return 1;                         /* WB13b + ENL runs */
+  if (is_wordish(x) && y == UC_EX) return 1;                         /* WB13a */
+  if ((is_ahl(x) || x == UC_NU) && (is_ahl(y) || y == UC_NU)) return 1;  /* WB5, WB8, WB9, WB10 */
+  if (x == UC_KA && y == UC_KA) return 1;                            /* WB13 */
+  if (x == UC_HL && y == UC_SQ) return 1;                            /* WB7a */
+  if (x == UC_SQ && w == UC_HL && (is_ahl(y) || y == UC_NU || y == UC_EX)) return 1;  /* Hgrp then a group */
+  if (is_ahl(x) && is_midlet(y) && is_ahl(z)) return 1;              /* WB6 */
+  if (is_midlet(x) && is_ahl(w) && is_ahl(y)) return 1;              /* WB7 */
+  if (x == UC_NU && is_midnum(y) && z == UC_NU) return 1;            /* WB12 */
+  if (is_midnum(x) && w == UC_NU && y == UC_NU) return 1;            /* WB11 */
+  if (x == UC_HL && y == UC_DQ && z == UC_HL) return 1;              /* WB7b */
+  if (x == UC_DQ && w == UC_HL && y == UC_HL) return 1;              /* WB7c */
+  return 0;
+}
+
+int64_t orc_tokenize_unicode(const uint8_t *s, uint64_t n, uint32_t max_len, uint32_t *starts, uint32_t *lens,
+                             uint64_t cap) {
+  if (max_len == 0) max_len = 255;
+  uint32_t *cps = (uint32_t *)malloc((n + 1) * 4), *offs = (uint32_t *)malloc((n + 1) * 4);
+  int *cls = (int *)malloc((n + 1) * sizeof(int));
+  if (!cps || !offs || !cls) { free(cps); free(offs); free(cls); return ORC_E_NOMEM; }
+  int64_t m = utf8_all(s, n, cps, offs);
+  if (m < 0) { free(cps); free(offs); free(cls); return ORC_E_UNSUPPORTED; }
+  for (int64_t i = 0; i < m; i++) cls[i] = uc_cls(cps[i]);
+  int64_t cnt = 0;
+  uint64_t i = 0;
+#define EMIT(A, B)                                                                    \
+  do {                                                                                \
+    uint64_t a_ = (A), b_ = (B), u16_ = 0, e_ = a_;                                   \
+    while (e_ < b_ && u16_ + (cps[e_] >= 0x10000 ? 2 : 1) <= max_len) u16_ += (cps[e_++] >= 0x10000 ? 2 : 1); \
+    if ((uint64_t)cnt < cap) { starts[cnt] = offs[a_]; lens[cnt] = offs[e_] - offs[a_]; } \
+    cnt++;                                                                            \
+    i = e_;                                                                           \
+  } while (0)
+  while (i < (uint64_t)m) {
+    uc_unit_t u = unit_at(cls, (uint64_t)m, i);
+    if (is_wordish(u.c)) {
+      /* maximal run of joined units */
+      uc_unit_t w = {0, 0, -1, 0}, x = u;
+      int core = x.c != UC_EX;
+      uint64_t end = x.b;
+      while (x.b < (uint64_t)m) {
+        uc_unit_t y = unit_at(cls, (uint64_t)m, x.b);
+        int z = -1;
+        if (y.b < (uint64_t)m) z = unit_at(cls, (uint64_t)m, y.b).c;
+        if (!word_join(w.c, x.c, y.c, z)) break;
+        w = x; x = y;
+        core |= x.c != UC_EX;
+        end = x.b;
+      }
+      if (core) { EMIT(u.a, end); continue; }
+      /* ENL-only run: JFlex skips char by char; an absorbed SA mark starts an SA run */
+      uint64_t k = u.a + 1;
+      while (k < end && cls[k] != UC_EXT_SA) k++;
+      i = k;
+      continue;
+    }
+    if (u.c == UC_SA) {
+      uint64_t e = u.b;
+      while (e < (uint64_t)m && (cls[e] == UC_SA || is_ext(cls[e]))) e++;
+      EMIT(u.a, e);
+      continue;
+    }
+    if (u.c == UC_HAN || u.c == UC_HIRA) { EMIT(u.a, u.b); continue; }
+    if (u.c == UC_EMO) {
+      uc_unit_t x = u;
+      while (x.zwj && x.b < (uint64_t)m) {
+        uc_unit_t y = unit_at(cls, (uint64_t)m, x.b);
+        if (y.c != UC_EMO) break;
+        x = y;
+      }
+      EMIT(u.a, x.b);
+      continue;
+    }
+    if (u.c == UC_RI && u.b < (uint64_t)m) {
+      uc_unit_t y = unit_at(cls, (uint64_t)m, u.b);
+      if (y.c == UC_RI) { EMIT(u.a, y.b); continue; }
+    }
+    i = i + 1;                                        /* [^] */
+  }
+#undef EMIT
+  free(cps); free(offs); free(cls);
+  return cnt;
+}
+
+/* LowerCaseFilter on one token: UTF-8 -> UTF-8 of Character.toLowerCase per
+ * code point.  dst needs 2 * len bytes.  Returns the output length. */
+uint64_t orc_lower_utf8(const uint8_t *src, uint64_t len, uint8_t *dst) {
+  uint64_t i = 0, o = 0;
+  while (i < len) {
+    uint32_t b = src[i], cp, need;
+    if (b < 0x80) { cp = b; need = 0; }
+    else if ((b & 0xE0) == 0xC0) { cp = b & 0x1F; need = 1; }
+    else if ((b & 0xF0) == 0xE0) { cp = b & 0x0F; need = 2; }
+    else { cp = b & 0x07; need = 3; }
+    for (uint32_t t = 1; t <= need; t++) cp = (cp << 6) | (src[i + t] & 0x3F);
+    i += need + 1;
+    uint32_t lc = cp < 0x80 ? ((cp >= 'A' && cp <= 'Z') ? cp + 32 : cp) : uc_tolower(cp);
+    if (lc < 0x80) dst[o++] = (uint8_t)lc;
+    else if (lc < 0x800) { dst[o++] = (uint8_t)(0xC0 | (lc >> 6)); dst[o++] = (uint8_t)(0x80 | (lc & 0x3F)); }
+    else if (lc < 0x10000) {
+      dst[o++] = (uint8_t)(0xE0 | (lc >> 12)); dst[o++] = (uint8_t)(0x80 | ((lc >> 6) & 0x3F));
+      dst[o++] = (uint8_t)(0x80 | (lc & 0x3F));
+    } else {
+      dst[o++] = (uint8_t)(0xF0 | (lc >> 18)); dst[o++] = (uint8_t)(0x80 | ((lc >> 12) & 0x3F));
+      dst[o++] = (uint8_t)(0x80 | ((lc >> 6) & 0x3F)); dst[o++] = (uint8_t)(0x80 | (lc & 0x3F));
+    }
+  }
+  return o;
 }
 
 /* ------------------------------------------------------------------ */
@@ -316,7 +515,6 @@ int orc_add_doc(orc_index *ix, const uint8_t *key, uint64_t key_len,
   return ORC_OK;
 }
 
-static uint8_t lower(uint8_t c) { return (c >= 'A' && c <= 'Z') ? (uint8_t)(c + 32) : c; }
 
 static int cmp_term_ids(const void *a, const void *b, void *ctx) {
   const strtab *t = (const strtab *)ctx;
@@ -357,7 +555,7 @@ int orc_commit(orc_index *ix) {
   uint32_t *st = (uint32_t *)malloc(tok_cap * 4), *ln = (uint32_t *)malloc(tok_cap * 4);
   uint64_t last_cap = 0;
   int64_t *last_doc = NULL; uint64_t *slot_of = NULL;
-  uint8_t *lbuf = (uint8_t *)malloc(256);
+  uint8_t *lbuf = (uint8_t *)malloc(2048);
   if (!ix->dt_term || !ix->dt_tf || !st || !ln || !lbuf) return ORC_E_NOMEM;
   ix->doc_count = 0; ix->sum_ttf = 0;
 
@@ -374,8 +572,8 @@ int orc_commit(orc_index *ix) {
     uint64_t row0 = dt_n;
     ix->dt_off[d] = row0;
     for (int64_t t = 0; t < nt; t++) {
-      for (uint32_t c = 0; c < ln[t]; c++) lbuf[c] = lower(sd->text[st[t] + c]);
-      int64_t id = st_insert(&ix->terms, lbuf, ln[t]);
+      const uint64_t ll = orc_lower_utf8(sd->text + st[t], ln[t], lbuf);
+      int64_t id = st_insert(&ix->terms, lbuf, ll);
       if (id < 0) return ORC_E_NOMEM;
       if ((uint64_t)id >= last_cap) {
         uint64_t nc = last_cap ? last_cap * 2 : 1024;
@@ -504,17 +702,21 @@ int orc_set_global_df(orc_index *ix, const uint8_t *term, uint64_t len, uint64_t
  * characters, the parse is the multiset of analysed tokens (whitespace is a
  * break character for the analyzer as well), de-duplicated by
  * BooleanQuery.rewrite with boost = occurrence count. */
-static int is_qp_ws(uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; }
+/* classic QueryParser _WHITESPACE: " " | "\t" | "\n" | "\r" | "\u3000"; length in bytes or 0 */
+static int qp_ws(const uint8_t *q, uint64_t n, uint64_t i) {
+  if (q[i] == ' ' || q[i] == '\t' || q[i] == '\n' || q[i] == '\r') return 1;
+  if (q[i] == 0xE3 && i + 2 < n && q[i + 1] == 0x80 && q[i + 2] == 0x80) return 3;
+  return 0;
+}
 
 int64_t orc_query_terms(const uint8_t *q, uint64_t n, char *buf, uint64_t buf_cap,
                         float *boosts, uint64_t cap) {
-  for (uint64_t i = 0; i < n; i++) if (q[i] >= 0x80) return ORC_E_UNSUPPORTED;
   /* operator words */
   uint64_t i = 0;
   while (i < n) {
-    while (i < n && is_qp_ws(q[i])) i++;
+    while (i < n && qp_ws(q, n, i)) i += (uint64_t)qp_ws(q, n, i);
     uint64_t j = i;
-    while (j < n && !is_qp_ws(q[j])) j++;
+    while (j < n && !qp_ws(q, n, j)) j++;
     uint64_t w = j - i;
     if ((w == 3 && (memcmp(q + i, "AND", 3) == 0 || memcmp(q + i, "NOT", 3) == 0)) ||
         (w == 2 && memcmp(q + i, "OR", 2) == 0))
@@ -527,16 +729,17 @@ int64_t orc_query_terms(const uint8_t *q, uint64_t n, char *buf, uint64_t buf_ca
   /* analyse chunk by chunk (restart context at each chunk, as QueryParser does) */
   strtab qt; st_init(&qt);
   float *cnt = (float *)calloc(tok_cap + 1, sizeof(float));
-  uint8_t lb[256];
+  uint8_t lb[2048];
   i = 0;
   while (i < n) {
-    while (i < n && is_qp_ws(q[i])) i++;
+    while (i < n && qp_ws(q, n, i)) i += (uint64_t)qp_ws(q, n, i);
     uint64_t j = i;
-    while (j < n && !is_qp_ws(q[j])) j++;
+    while (j < n && !qp_ws(q, n, j)) j++;
     int64_t nt = orc_tokenize(q + i, j - i, 255, st, ln, tok_cap);
+    if (nt < 0) { st_free(&qt); free(cnt); free(st); free(ln); return nt; }
     for (int64_t t = 0; t < nt; t++) {
-      for (uint32_t c = 0; c < ln[t]; c++) lb[c] = lower(q[i + st[t] + c]);
-      int64_t id = st_insert(&qt, lb, ln[t]);
+      const uint64_t ll = orc_lower_utf8(q + i + st[t], ln[t], lb);
+      int64_t id = st_insert(&qt, lb, ll);
       cnt[id] += 1.0f;
     }
     i = j;

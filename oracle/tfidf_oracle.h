@@ -30,17 +30,24 @@ extern "C" {
 
 #define ORC_OK 0
 #define ORC_E_ARG (-1)
-#define ORC_E_UNSUPPORTED (-2) /* non-ASCII byte, or AND/OR/NOT operator word */
+#define ORC_E_UNSUPPORTED (-2) /* malformed UTF-8, or AND/OR/NOT operator word */
 #define ORC_E_NOMEM (-3)
 #define ORC_E_CAP (-4)         /* caller buffer too small; *n_out = needed */
 
-/* StandardTokenizer (ASCII subset of UAX#29) + LowerCaseFilter.
+/* StandardTokenizer (UAX#29 JFlex grammar of Lucene 9.8).
  * Writes token start offsets / lengths (into the ORIGINAL bytes; lower-case
- * folding is ASCII A-Z -> a-z and is applied by callers).  Returns the number
+ * folding, orc_lower_utf8, is applied by callers).  Returns the number
  * of tokens (may exceed cap: only the first cap are written), or
- * ORC_E_UNSUPPORTED when a byte >= 0x80 is present. */
+ * ORC_E_UNSUPPORTED for malformed UTF-8. */
 int64_t orc_tokenize(const uint8_t *s, uint64_t n, uint32_t max_token_len,
                      uint32_t *starts, uint32_t *lens, uint64_t cap);
+/* The full-Unicode rules (orc_tokenize uses them when a byte >= 0x80 is
+ * present; exported so tests can run them on ASCII too).  Spans are in bytes;
+ * max_token_len counts UTF-16 units.  ORC_E_UNSUPPORTED = malformed UTF-8. */
+int64_t orc_tokenize_unicode(const uint8_t *s, uint64_t n, uint32_t max_token_len,
+                             uint32_t *starts, uint32_t *lens, uint64_t cap);
+/* LowerCaseFilter on one token's UTF-8 (dst >= 2 * len bytes); returns length. */
+uint64_t orc_lower_utf8(const uint8_t *src, uint64_t len, uint8_t *dst);
 
 /* SmallFloat.intToByte4 / byte4ToInt (BM25Similarity.computeNorm, LENGTH_TABLE). */
 uint8_t orc_int_to_byte4(int32_t i);

@@ -21,12 +21,12 @@ pytestmark = pytest.mark.gpu
 
 
 def keyed(terms):
-    """Oracle doc_terms with long (> 16 byte) terms replaced by the engine's
-    printable 128-bit key: the device keys those terms by hash."""
+    """Oracle doc_terms with long (> 16 byte) and non-ASCII terms replaced by
+    the engine's printable 128-bit key: the device keys those terms by hash."""
     from tfidf_amd.engine import term_key
     out = {}
     for t, tf in terms.items():
-        if len(t) > 16:
+        if len(t) > 16 or max(t, default=0) >= 0x80:
             lo, hi = term_key(t)
             t = b"#%016x%016x" % (hi, lo)
         out[t] = tf
@@ -317,9 +317,9 @@ def test_host_loader_pinned_staging_and_clear():
     dc.free()
 
 
-def test_non_ascii_document_rejected():
+def test_malformed_utf8_document_rejected():
     g = ShardIndex()
-    g.add_documents([b"fine text", "café".encode()])
+    g.add_documents([b"fine text", "café".encode(), b"caf\xe9"])
     with pytest.raises(UnsupportedInput):
         g.commit()
     g.close()

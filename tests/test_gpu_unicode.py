@@ -1,0 +1,128 @@
+"""GPU parity of the full-Unicode tokenizer path.
+
+Documents with a non-ASCII byte or a token of more than 255 chars leave the
+ASCII wave path (and packed windows) for k_tokenize_long's general phase,
+which rescans them with the device DFA of unicode_scan.h, thread slices cut
+after ASCII class-OTHER bytes.  Checked against the CPU oracle
+(oracle/tfidf_oracle.c: local join rules), itself pinned to a transcription of
+the JFlex grammar (test_unicode_tokenizer.py).  Non-ASCII results are "parity
+unpinned" against Lucene itself (no JDK here).  Bar: TF / DF / lengths / norms
+/ hit ids bit-exact, scores as float32 bit patterns.
+"""
+import random
+
+import pytest
+
+from oracle import oracle as O
+from tfidf_amd import synth
+from tfidf_amd.engine import ShardIndex
+
+from test_gpu_parity import assert_hits_equal, keyed
+from test_unicode_tokenizer import ALPHA
+
+pytestmark = pytest.mark.gpu
+
+WORDS = ["café", "Café", "naïve", "it’s", "don't", "élan", "ÉCOLE", "straße", "İstanbul", "ΣΟΦΙΑ", "σοφία",
+         "москва", "Москва", "中文", "分词器", "ひらがな", "カタカナ", "ภาษาไทย", "שָׁלוֹם", "א\"ב", "١٢٫٣", "１２３",
+         "😀", "👍🏽", "👨‍👩‍👧", "🇺🇸", "été", "abc", "xyz", "42", "u.s.a", "q_1"]
+
+
+def uni_doc(rng, n):
+    parts = []
+    for _ in range(n):
+        r = rng.random()
+        if r < 0.6:
+            parts.append(rng.choice(WORDS))
+        elif r < 0.8:
+            parts.append("".join(rng.choice(ALPHA) for _ in range(rng.randint(1, 8))))
+        else:
+            parts.append(synth.word(rng.randint(1, 3000)).decode())
+        parts.append(rng.choice([" ", " ", " ", "\n", ", ", " — ", "　", "\t"]))
+    return "".join(parts).encode()
+
+
+def build_pair(texts, cap_log2=18):
+    g = ShardIndex(vocab_capacity_log2=cap_log2)
+    g.add_documents(texts)
+    g.commit()
+    o = O.OracleIndex()
+    for i, t in enumerate(texts):
+        o.add_doc(str(i).encode(), t)
+    o.commit()
+    return g, o
+
+
+def check(g, o, texts, every=1):
+    s = g.stats()
+    assert (s["doc_count"], s["sum_ttf"], s["num_terms"], s["nnz"]) == \
+        (o.doc_count, o.sum_ttf, o.num_terms, sum(o.vocab().values()))
+    for d in range(0, len(texts), every):
+        assert g.doc_terms(d) == keyed(o.doc_terms(d)), (d, texts[d][:200])
+        assert g.doc_len(d) == (o.doc_len(d), o.doc_norm(d)), d
+
+
+QUERIES = ["café", "CAFÉ naïve", "it’s", "中文 分词器", "ภาษาไทย", "😀 🇺🇸", "σοφία ΣΟΦΙΑ", "москва abc",
+           "straße　42", "été", "א\"ב", "１２３ u.s.a"]
+
+
+def test_mixed_corpus_short_and_long_docs():
+    rng = random.Random(5)
+    texts = [uni_doc(rng, rng.randint(0, 300)) for _ in range(600)]
+    texts += synth.corpus(400, V=3000, len_min=20, len_max=300)          # ASCII docs stay on the wave path
+    texts += [uni_doc(rng, n) for n in (2000, 9000, 30000)]             # long Unicode docs (> 4 KB)
+    rng.shuffle(texts)
+    texts += [b"", "　".encode(), "﻿".encode(), "ั".encode(), "_ั".encode()]
+    g, o = build_pair(texts)
+    assert g.stats()["long_docs"] >= 600
+    check(g, o, texts)
+    for q in QUERIES:
+        qb = q.encode()
+        assert_hits_equal(g.search(qb, 0), o.search(qb, 0))
+        assert_hits_equal(g.search(qb, 10), o.search(qb, 10))
+    docs, scores, counts = g.search_batch([q.encode() for q in QUERIES], 10)
+    for i, q in enumerate(QUERIES):
+        hits = list(zip(docs[i, :counts[i]].tolist(), scores[i, :counts[i]].tolist()))
+        assert_hits_equal(hits, o.search(q.encode(), 10))
+    g.close()
+    o.close()
+
+
+@pytest.mark.parametrize("pack", [4, 16])
+def test_packed_windows_defer_unicode_docs(monkeypatch, pack):
+    monkeypatch.setenv("TFIDF_PACK_DOCS", str(pack))
+    rng = random.Random(pack)
+    texts = []
+    for i in range(1500):
+        texts.append(uni_doc(rng, rng.randint(1, 12)) if i % 7 == 3 else
+                     b" ".join(synth.word(rng.randint(1, 500)) for _ in range(rng.randint(1, 12))))
+    g, o = build_pair(texts)
+    assert g.stats()["pack_docs"] == pack
+    check(g, o, texts)
+    g.close()
+    o.close()
+
+
+def test_tokens_longer_than_255_chars_are_cut():
+    rng = random.Random(9)
+    texts = [b"x" * 256, b"ab " + b"y" * 600 + b" cd", ("é" * 300).encode(), (b"q" * 254 + "\U00010400".encode() * 3),
+             b"a.b" * 120, b"_" * 300 + b"z", b"k" * 255, b"fine text only"]
+    texts += [b" ".join([b"w" * rng.randint(200, 700)] * 3) for _ in range(20)]
+    texts += synth.corpus(300, V=500, len_min=5, len_max=50)
+    g, o = build_pair(texts)
+    check(g, o, texts)
+    for q in [b"x" * 255, b"y" * 255, "é" * 255, b"k" * 255, b"fine"]:
+        qb = q if isinstance(q, bytes) else q.encode()
+        assert_hits_equal(g.search(qb, 0), o.search(qb, 0))
+    g.close()
+    o.close()
+
+
+def test_whitespace_free_unicode_document():
+    # no ASCII split byte at all: the first thread slice scans the whole document
+    rng = random.Random(2)
+    t = "".join(rng.choice("中文字ひらがなカタカナภาษา") for _ in range(20000)).encode()
+    texts = [t, "東京タワー".encode() * 500, b"plain words here"]
+    g, o = build_pair(texts)
+    check(g, o, texts)
+    g.close()
+    o.close()

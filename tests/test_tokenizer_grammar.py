@@ -72,6 +72,7 @@ def test_long_token_chopped_at_255():
     assert [len(t) for t in toks] == [255, 255, 90]
 
 
-def test_non_ascii_rejected():
+def test_malformed_utf8_rejected():
     with pytest.raises(ValueError):
-        O.tokenize("café".encode())
+        O.tokenize(b"caf\xe9")          # Latin-1, not UTF-8: Files.readString would throw
+    assert O.tokenize("café".encode()) == ["café".encode()]

@@ -6,7 +6,7 @@
 // a flat OR of per-chunk analysed tokens — except for the operator WORDS
 // AND / OR / NOT, which escape() leaves alone.  Those are rejected
 // (TFIDF_E_UNSUPPORTED_QUERY) rather than silently mis-scored.  Chunks are
-// split on the classic QueryParser's whitespace (space, \t, \n, \r);
+// split on the classic QueryParser's whitespace (space, \t, \n, \r, U+3000);
 // BooleanQuery.rewrite de-duplicates SHOULD clauses with boost = count.
 #pragma once
 
@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "tfidf_common.h"
+#include "unicode_scan.h"
 
 namespace tfidf {
 
@@ -27,47 +28,46 @@ struct QueryTerm {
   float boost;        // occurrence count
 };
 
-// StandardTokenizer (ASCII UAX#29) over [s, s + n), tokens chopped at 255 with
-// scanning restarted at the cut.  Emits lower-cased token strings.
-inline void analyze_ascii(const uint8_t *s, uint64_t n, std::vector<std::string> *out) {
-  auto cls = [&](uint64_t i) -> uint8_t { return wb_class(s[i]); };
-  uint64_t lo = 0, i = 0;
-  auto is_word = [&](uint64_t k) -> bool {
-    uint8_t p = (k > lo) ? cls(k - 1) : 0;
-    uint8_t x = (k + 1 < n) ? cls(k + 1) : 0;
-    return wb_is_word(p, cls(k), x);
+// StandardAnalyzer over [s, s + n) (unicode_scan.h: the same scanner the
+// device runs): lower-cased token strings.  Returns false on malformed UTF-8.
+inline bool analyze(const uint8_t *s, uint64_t n, std::vector<std::string> *out) {
+  struct StrSink {
+    std::string *t;
+    void push(uint8_t c) { t->push_back((char)c); }
   };
-  while (i < n) {
-    if (!is_word(i)) { i++; continue; }
-    uint64_t j = i;
-    bool has_ld = false;
-    while (j < n && is_word(j)) { has_ld |= (cls(j) & (kClsL | kClsD)) != 0; j++; }
-    if (!has_ld) { i = j; continue; }
-    uint64_t len = j - i;
-    if (len > kMaxTokenLen) len = kMaxTokenLen;
-    std::string t(len, '\0');
-    for (uint64_t c = 0; c < len; c++) t[c] = (char)ascii_lower(s[i + c]);
+  uint64_t pos = 0, ts, te;
+  bool bad = false;
+  while (uc_next_span(s, n, &pos, n, &ts, &te, &bad)) {
+    std::string t;
+    StrSink sink{&t};
+    const uint64_t cut = uc_token_bytes(s, n, ts, te, sink);
+    if (cut < te) pos = cut;
     out->push_back(std::move(t));
-    if (j - i > kMaxTokenLen) { lo = i + kMaxTokenLen; i = lo; continue; }
-    i = j;
   }
+  return !bad;
 }
 
-// Returns 0 on success, 1 for non-ASCII, 2 for an operator word.
+// classic QueryParser whitespace: ' ' '\t' '\n' '\r' and U+3000 (E3 80 80)
+inline uint32_t qp_ws_len(const uint8_t *q, uint64_t n, uint64_t i) {
+  const uint8_t c = q[i];
+  if (c == ' ' || c == '\t' || c == '\n' || c == '\r') return 1;
+  if (c == 0xE3 && i + 2 < n && q[i + 1] == 0x80 && q[i + 2] == 0x80) return 3;
+  return 0;
+}
+
+// Returns 0 on success, 1 for malformed UTF-8, 2 for an operator word.
 inline int parse_query(const uint8_t *q, uint64_t n, std::vector<QueryTerm> *terms) {
-  for (uint64_t i = 0; i < n; i++)
-    if (q[i] >= 0x80) return 1;
-  auto ws = [](uint8_t c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r'; };
   std::vector<std::string> toks;
   uint64_t i = 0;
   while (i < n) {
-    while (i < n && ws(q[i])) i++;
+    uint32_t w;
+    while (i < n && (w = qp_ws_len(q, n, i))) i += w;
     uint64_t j = i;
-    while (j < n && !ws(q[j])) j++;
-    const uint64_t w = j - i;
-    if ((w == 3 && (!memcmp(q + i, "AND", 3) || !memcmp(q + i, "NOT", 3))) || (w == 2 && !memcmp(q + i, "OR", 2)))
+    while (j < n && !qp_ws_len(q, n, j)) j++;
+    const uint64_t len = j - i;
+    if ((len == 3 && (!memcmp(q + i, "AND", 3) || !memcmp(q + i, "NOT", 3))) || (len == 2 && !memcmp(q + i, "OR", 2)))
       return 2;
-    if (w) analyze_ascii(q + i, w, &toks);
+    if (len && !analyze(q + i, len, &toks)) return 1;
     i = j;
   }
   std::unordered_map<std::string, size_t> pos;

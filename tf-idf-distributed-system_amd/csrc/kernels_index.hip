@@ -27,6 +27,7 @@
 
 #include "dict_device.h"
 #include "tfidf_common.h"
+#include "unicode_scan.h"
 #include "wave_ops.h"
 #include "tfidf_internal.h"
 
@@ -701,13 +702,14 @@ __device__ __forceinline__ void hist_batch(WaveSmem &sm, const BuildParams &p, u
     longm |= (uint32_t)(in & (n > 8)) << k;
   }
   if (FOLD && __any(longm != 0)) {                      // tokens of 9..255 bytes: folded keys
+    bool toolong = false;
 #pragma unroll
     for (int k = 0; k < K; k++) {
       if ((longm >> k) & 1u) {
         const uint32_t e = sm.list[tb + lane + 64 * k];
         const uint32_t tp = e & kSpanMask, n = ((e >> 16) & kSpanMask) - tp;
         if (n > kMaxTokenLen) {
-          set_err(p.err, kErrTokenTooLong, (uint32_t)d);
+          toolong = true;
         } else {
           uint32_t h;
           bool valid;
@@ -721,6 +723,7 @@ __device__ __forceinline__ void hist_batch(WaveSmem &sm, const BuildParams &p, u
         }
       }
     }
+    if (__any(toolong)) { overflow = true; return; }    // > 255 chars: the long path cuts it
   }
   toks += (uint32_t)__popc(pendm);
   for (uint32_t round = 0;; round++) {
@@ -907,13 +910,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       }
       W &= ~(jm & ~wbase);
     }
-    if (bad) {
-      if (PACK) { defer_pack(p, d, np, lane); continue; }
-      if (lane == 0) {
-        set_err(p.err, kErrNonAscii, (uint32_t)d);
-        p.doc_len[d] = 0; p.doc_nuniq[d] = 0; p.doc_norm[d] = 0;
-      }
-      for (uint32_t r = lane; r < R; r += 64) p.rsplit[d * R + r] = 0;
+    if (bad) {                                              // non-ASCII: the long path's Unicode scanner
+      if (PACK) defer_pack(p, d, np, lane);
+      else if (lane == 0) p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
       continue;
     }
     const uint64_t wlast = __ballot((W >> 63) & 1ull);
@@ -1299,7 +1298,7 @@ __global__ void __launch_bounds__(256) k_tokenize_long(BuildParams p) {
                                               shift + (uint32_t)(ce - wlo), sm.tok_s, sm.tok_e, kChunk / 2 + 8, sm.scan);
       for (uint32_t i = tid; i < ntok; i += 256) {
         const uint32_t s = sm.tok_s[i], e = sm.tok_e[i];
-        if (e - s > kMaxTokenLen) { set_err(p.err, kErrTokenTooLong, d); continue; }
+        if (e - s > kMaxTokenLen) { atomicOr(&sm.flags, 8u); continue; }   // cut by the Unicode scanner
         uint64_t lo, hi;
         bool valid;
         token_key(sm.text, s, e, &lo, &hi, &valid);
@@ -1309,9 +1308,39 @@ __global__ void __launch_bounds__(256) k_tokenize_long(BuildParams p) {
       }
       __syncthreads();
     }
-    if (bad) {
+    if (bad || (sm.flags & 8u)) {
+      // General phase (unicode_scan.h): a non-ASCII byte or a token of more
+      // than 255 chars.  Reset the table and rescan the whole document with
+      // the full-Unicode scanner: thread t takes the tokens starting in its
+      // slice of the document, slices cut just after ASCII class-OTHER bytes
+      // (the scan restarts there in the start state).
+      for (uint32_t i = tid; i < T; i += 256) { keys[2 * i] = 0; keys[2 * i + 1] = 0; cnt[i] = 0; }
+      __syncthreads();
+      my_len = 0;
+      const uint8_t *doc = p.text + s0;
+      const uint64_t seg = L / 256 + 64;
+      auto slice = [&](uint64_t t) -> uint64_t {
+        if (t == 0) return 0;
+        uint64_t q = t * seg;
+        if (q >= L) return L;
+        while (q < L && !uc_split_byte(doc[q - 1])) q++;
+        return q;
+      };
+      uint64_t pos = slice(tid);
+      const uint64_t stop = slice(tid + 1);
+      uint64_t ts, te, lo, hi;
+      bool ubad = false;
+      while (uc_next_token(doc, L, &pos, stop, &ts, &te, &lo, &hi, &ubad)) {
+        my_len++;
+        if (gtable_insert(keys, cnt, mask, lo, hi) == kInvalidSlot) atomicOr(&sm.flags, 4u);
+      }
+      if (ubad) atomicOr(&sm.flags, 16u);
+      __syncthreads();
+      bad = (sm.flags & 16u) != 0;
+    }
+    if (bad) {                                   // malformed UTF-8
       if (tid == 0) {
-        set_err(p.err, kErrNonAscii, d);
+        set_err(p.err, kErrBadUtf8, d);
         p.doc_len[d] = 0; p.doc_nuniq[d] = 0; p.doc_norm[d] = 0;
         for (uint32_t r = 0; r < p.n_ranges; r++) p.rsplit[(uint64_t)d * p.n_ranges + r] = 0;
         sm.flags = 0;

@@ -752,10 +752,8 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
     if (err & kErrCapacity)
       return fail(TFIDF_E_CAPACITY, "vocabulary exceeds 2^%u dictionary slots (raise vocab_capacity_log2)",
                   ix->cap_log2);
-    if (err & kErrNonAscii)
-      return fail(TFIDF_E_UNSUPPORTED_INPUT, "document %u contains non-ASCII bytes (ASCII analyzer only)", err_doc);
-    if (err & kErrTokenTooLong)
-      return fail(TFIDF_E_UNSUPPORTED_INPUT, "document %u has a token longer than 255 chars", err_doc);
+    if (err & kErrBadUtf8)
+      return fail(TFIDF_E_UNSUPPORTED_INPUT, "document %u is not valid UTF-8", err_doc);
     return fail(TFIDF_E_UNSUPPORTED_INPUT, "index build error flags 0x%x (doc %u)", err, err_doc);
   }
   ix->doc_count = hctr[0];
@@ -914,7 +912,7 @@ struct PreparedQuery {
 static int prepare_query(tfidf_index *ix, const uint8_t *q, uint64_t n, PreparedQuery *pq) {
   std::vector<QueryTerm> terms;
   const int rc = parse_query(q, n, &terms);
-  if (rc == 1) return fail(TFIDF_E_UNSUPPORTED_QUERY, "non-ASCII query");
+  if (rc == 1) return fail(TFIDF_E_UNSUPPORTED_QUERY, "query is not valid UTF-8");
   if (rc == 2) return fail(TFIDF_E_UNSUPPORTED_QUERY, "AND/OR/NOT operator words are not supported");
   const uint64_t dc = eff_doc_count(ix);
   for (const QueryTerm &t : terms) {
@@ -1204,6 +1202,25 @@ extern "C" int tfidf_term_key(const uint8_t *term, uint64_t len, uint64_t *lo, u
   if ((!term && len) || !lo || !hi) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
   std::string t((const char *)term, len);
   term_key(t, lo, hi);
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_analyze(const uint8_t *text, uint64_t len, char *out, uint64_t cap, uint64_t *n_tokens,
+                             uint64_t *n_bytes) {
+  if ((!text && len) || !n_tokens || !n_bytes || (!out && cap)) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  std::vector<std::string> toks;
+  if (!analyze(text, len, &toks)) return fail(TFIDF_E_UNSUPPORTED_INPUT, "text is not valid UTF-8");
+  uint64_t need = 0;
+  for (auto &t : toks) need += t.size() + 1;
+  *n_tokens = toks.size();
+  *n_bytes = need;
+  if (need > cap) return fail(TFIDF_E_BUFFER, "buffer too small");
+  uint64_t p = 0;
+  for (auto &t : toks) {
+    memcpy(out + p, t.data(), t.size());
+    out[p + t.size()] = 0;
+    p += t.size() + 1;
+  }
   return TFIDF_OK;
 }
 

@@ -10,6 +10,9 @@
 //                  VALID — exact;
 //   * 17..255    : lo = bytes 0..7 | LO_LONG | LO_HASHED (bit 55), hi = VALID
 //                  | 63-bit hash of all bytes and the length.
+//   * any token holding a non-ASCII byte (UTF-8 of the lower-cased code
+//     points; unicode_scan.h): lo = 56 hash bits | LO_LONG | LO_HASHED, hi =
+//     VALID | 63-bit hash — 119 hash bits, no exact form.
 // Bit 63 of hi (VALID) is set for every key so that hi == 0 marks "not
 // written" in the device dictionary.
 #pragma once
@@ -100,7 +103,9 @@ struct KeyBuilder {
   uint64_t w0 = 0, w1 = 0;    // raw bytes 0..15
   uint64_t h1 = 0x243F6A8885A308D3ull, h2 = 0x13198A2E03707344ull;  // hash of all bytes
   uint32_t n = 0;
+  uint32_t na = 0;            // a byte >= 0x80 was pushed
   TFIDF_HD void push(uint8_t c) {
+    na |= c >> 7;
     if (n < 8) w0 |= (uint64_t)c << (8 * n);
     else if (n < 16) w1 |= (uint64_t)c << (8 * (n - 8));
     h1 = (h1 ^ c) * 0x100000001B3ull;
@@ -108,7 +113,10 @@ struct KeyBuilder {
     n++;
   }
   TFIDF_HD void finish(uint64_t *klo, uint64_t *khi) const {
-    if (n <= 8) {
+    if (na) {
+      *klo = (mix64(h1 ^ 0xA5A5A5A5A5A5A5A5ull ^ n) & 0x7F7F7F7F7F7F7F7Full) | kLoLong | kLoHashed;
+      *khi = mix64(h2 ^ mix64(h1 ^ ((uint64_t)n << 56))) | kKeyValid;
+    } else if (n <= 8) {
       *klo = w0;
       *khi = kKeyValid;
     } else if (n <= kExactKeyChars) {

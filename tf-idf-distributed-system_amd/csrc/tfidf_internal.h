@@ -9,8 +9,7 @@
 namespace tfidf {
 
 // Error flags raised by kernels (device word err[0]; err[1] = first doc).
-constexpr uint32_t kErrNonAscii = 1u;
-constexpr uint32_t kErrTokenTooLong = 2u;
+constexpr uint32_t kErrBadUtf8 = 1u;          // malformed UTF-8 (Files.readString would throw)
 constexpr uint32_t kErrCapacity = 4u;
 constexpr uint32_t kErrTfTooLarge = 8u;
 constexpr uint32_t kErrLongScratch = 16u;

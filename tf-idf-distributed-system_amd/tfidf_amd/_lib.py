@@ -99,6 +99,7 @@ SIGNATURES = {
     "tfidf_set_global_stats": (C.c_int, [VP, U64P, U64P, C.c_uint64, C.c_uint64, C.c_uint64]),
     "tfidf_clear_global_stats": (C.c_int, [VP]),
     "tfidf_term_key": (C.c_int, [C.c_char_p, C.c_uint64, U64P, U64P]),
+    "tfidf_analyze": (C.c_int, [C.c_char_p, C.c_uint64, C.c_char_p, C.c_uint64, U64P, U64P]),
     "tfidf_leader_merge": (C.c_int, [C.c_char_p, U64P, C.c_uint64, F64P, U64P, F64P, U64P]),
     "tfidf_synth_corpus": (C.c_int, [C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, F64P, C.c_uint32, C.c_uint32,
                                      C.c_uint32, C.POINTER(VP), C.POINTER(VP), U64P]),

@@ -9,6 +9,16 @@ import numpy as np
 from . import _lib as L
 
 
+def analyze(text: bytes):
+    """StandardAnalyzer (Worker.java:71,225) as the engine runs it: lower-cased
+    UTF-8 tokens of ``text`` (host side of the device scanner, unicode_scan.h)."""
+    cap = 2 * len(text) + 64
+    buf = C.create_string_buffer(cap)
+    nt, nb = C.c_uint64(), C.c_uint64()
+    L.check(L.load().tfidf_analyze(text, len(text), buf, cap, C.byref(nt), C.byref(nb)))
+    return buf.raw[:nb.value].split(b"\0")[:nt.value]
+
+
 def term_key(term: bytes):
     """128-bit device key (lo, hi) of an analysed (lower-cased) token."""
     lo, hi = C.c_uint64(), C.c_uint64()
