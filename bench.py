@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--cap-log2", type=int, default=0,
                     help="dictionary slots 2^x (0 = smallest power of two >= 1.6 x vocab, at least 2^18)")
     ap.add_argument("--inversion", choices=("auto", "block", "term"), default="auto")
+    ap.add_argument("--unicode-frac", type=float, default=0.0,
+                    help="fraction of documents made non-ASCII (Unicode tokenizer path); 0 = the cfg-2 corpus")
     ap.add_argument("--no-e2e", dest="e2e", action="store_false",
                     help="skip the PCIe-inclusive (host corpus -> HBM -> index) measurement")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r01", "traffic.json"),
@@ -165,6 +167,7 @@ def main():
     doc_base = rank * n_docs
     corpus = synth.DeviceCorpus(n_docs, V=args.vocab, len_min=args.len_min, len_max=args.len_max,
                                 doc_base=doc_base, device=local)
+    n_unicode = corpus.inject_unicode(args.unicode_frac)
     cap = args.cap_log2
     if not cap:
         cap = 18
@@ -270,6 +273,7 @@ def main():
         "index_build_alg_bytes": b_index,
         "index_build_GBs_end_to_end": b_index / (elapsed / args.steps) / 1e9,
         "long_docs": st["long_docs"],
+        "unicode_docs": n_unicode,
         "tokenizer_docs_per_window": st["pack_docs"],
         "pack_retried_docs": st["pack_retried"],
     }

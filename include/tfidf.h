@@ -91,6 +91,7 @@ typedef struct tfidf_index_stats {
   uint64_t term_major;    /* 1 if the last commit built the term-major layout (TFIDF_INVERSION_TERM) */
   uint64_t pack_docs;     /* documents per tokenizer window in the last commit (1 = one per window) */
   uint64_t pack_retried;  /* documents the packed windows handed to the one-per-window pass */
+  uint64_t unicode_docs;  /* documents (window <= 4 KB) the ASCII wave path handed to the Unicode wave path */
 } tfidf_index_stats;
 
 /* Per-phase device times of the last commit, measured with HIP events on the

@@ -910,9 +910,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       }
       W &= ~(jm & ~wbase);
     }
-    if (bad) {                                              // non-ASCII: the long path's Unicode scanner
+    if (bad) {                                              // non-ASCII: the Unicode wave path
       if (PACK) defer_pack(p, d, np, lane);
-      else if (lane == 0) p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
+      else if (lane == 0) p.uni_list[atomicAdd(p.uni_count, 1u)] = (uint32_t)d;
       continue;
     }
     const uint64_t wlast = __ballot((W >> 63) & 1ull);

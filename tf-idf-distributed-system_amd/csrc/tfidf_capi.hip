@@ -126,10 +126,11 @@ struct tfidf_index {
   std::vector<uint32_t> live_map;  // committed -> staged (empty = identity)
   DevBuf d_live_map;
   uint32_t cap_log2 = 18, C = 0, range_shift = 15, R = 1, n_blocks = 0;
-  DevBuf dict, csr_col, csr_tf, doc_len, doc_nuniq, doc_norm, rsplit, long_list, counters, blk, bbase, post, post_tmp;
+  DevBuf dict, csr_col, csr_tf, doc_len, doc_nuniq, doc_norm, rsplit, long_list, uni_list, counters, blk, bbase, post, post_tmp;
   DevBuf retry_list;                   // packed wave path: documents deferred to the single-document pass
   uint32_t pack_docs = 1;              // documents per wave window in the last commit
   uint64_t pack_retried = 0;           // documents the packs deferred in the last commit
+  uint64_t unicode_docs = 0;           // documents with non-ASCII text in the last commit
   // term-major inversion (large vocabularies): compact row offsets, sort values (x2), term offsets, df
   bool term_major = false;
   DevBuf row_off, tvals, toff, tdf, term_tmp;
@@ -211,7 +212,7 @@ extern "C" int tfidf_destroy(tfidf_index *ix) {
   DeviceGuard g(ix->cfg.device);
   hipStreamSynchronize(ix->stream);
   DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->d_live_map, &ix->dict, &ix->csr_col, &ix->csr_tf, &ix->doc_len,
-                    &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->long_list, &ix->counters, &ix->blk,
+                    &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->long_list, &ix->uni_list, &ix->counters, &ix->blk,
                     &ix->retry_list, &ix->bbase, &ix->post, &ix->post_tmp, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->canon_of_slot,
                     &ix->q_off, &ix->q_slot, &ix->q_w, &ix->cache, &ix->cand, &ix->cand_n, &ix->out_doc,
                     &ix->out_score, &ix->out_n, &ix->hits, &ix->hits_n, &ix->hits_c, &ix->hits_s, &ix->sort_tmp,
@@ -636,6 +637,7 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   HIP_TRY(ix->doc_norm.reserve(N + 16));
   HIP_TRY(ix->rsplit.reserve(N * ix->R * 4 + 4));
   HIP_TRY(ix->long_list.reserve(N * 4 + 4));
+  HIP_TRY(ix->uni_list.reserve(N * 4 + 4));
   HIP_TRY(ix->counters.reserve(64));
   // Short-document corpora: the wave path indexes packs of consecutive
   // documents per window (about kPackBytes of text per pack; SURVEY cfg 5
@@ -656,7 +658,8 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
     HIP_TRY(ix->bbase.reserve((size_t)(ix->n_blocks + 2) * 8));
   }
 
-  // counters: [0..2] stats u64, [3] err flags u32 + [3].hi first doc, [4] long_count, [5] retry_count
+  // counters: [0..2] stats u64, [3] err flags u32 + [3].hi first doc, [4] long_count, [5] retry_count,
+  // [6] uni_count
   uint64_t *ctr = ix->counters.as<uint64_t>();
   HIP_TRY(hipMemsetAsync(ix->counters.p, 0, 64, s));
   HIP_TRY(hipMemsetAsync(ix->dict.p, 0, (size_t)2 * C * 8, s));
@@ -678,6 +681,8 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   bp.rsplit = ix->rsplit.as<uint32_t>();
   bp.long_list = ix->long_list.as<uint32_t>();
   bp.long_count = reinterpret_cast<uint32_t *>(ctr + 4);
+  bp.uni_list = ix->uni_list.as<uint32_t>();
+  bp.uni_count = reinterpret_cast<uint32_t *>(ctr + 6);
   bp.stats = reinterpret_cast<unsigned long long *>(ctr);
   bp.err = reinterpret_cast<uint32_t *>(ctr + 3);
   if (const char *ds = getenv("TFIDF_DEBUG_STOP")) bp.debug_stop = (uint32_t)atoi(ds);   // profiling only
@@ -706,6 +711,9 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
         HIP_TRY(launch_tokenize_wave(rp, (int)rgrid, s));
       }
     }
+    // documents with non-ASCII text (count read on the device; exits at once when none)
+    if (!bp.debug_stop)
+      HIP_TRY(launch_tokenize_uwave(bp, (int)std::min<uint64_t>(N, (uint64_t)ix->num_cus * kUwaveWGsPerCU), s));
   }
   HIP_TRY(hipEventRecord(ix->ev[EV_TOK], s));
   if (bp.debug_stop) {                      // profiling only: rows are incomplete, stop here
@@ -718,10 +726,12 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
     ix->committed = false;
     return TFIDF_OK;
   }
-  uint32_t n_long = 0;
+  uint32_t n_long = 0, n_uni = 0;
   HIP_TRY(hipMemcpyAsync(&n_long, ctr + 4, 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(&n_uni, ctr + 6, 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   ix->long_docs = n_long;
+  ix->unicode_docs = n_uni;
   if (n_long) {
     uint32_t lg = ix->cap_log2 + 1;
     // table size needed by the longest long document (2x its token bound)
@@ -877,6 +887,7 @@ extern "C" int tfidf_stats(const tfidf_index *ix, tfidf_index_stats *out) {
   out->term_major = ix->committed && ix->term_major;
   out->pack_docs = ix->pack_docs;
   out->pack_retried = ix->pack_retried;
+  out->unicode_docs = ix->unicode_docs;
   const DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->dict, &ix->csr_col, &ix->csr_tf, &ix->doc_len,
                           &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->blk, &ix->bbase, &ix->post,
                           &ix->toff, &ix->tdf};

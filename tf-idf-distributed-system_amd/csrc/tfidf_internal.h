@@ -36,6 +36,8 @@ struct BuildParams {
   uint32_t *rsplit;           // [n_docs][R] inclusive end of each range segment in the row
   uint32_t *long_list;        // docs deferred to the long path
   uint32_t *long_count;
+  uint32_t *uni_list;         // docs the ASCII wave path found non-ASCII bytes in (Unicode wave path)
+  uint32_t *uni_count;
   unsigned long long *stats;  // [0] docCount, [1] sumTotalTermFreq, [2] nnz
   uint32_t *err;              // [0] flags, [1] first offending doc
   // long path scratch (one table region per workgroup)
@@ -85,6 +87,8 @@ constexpr uint32_t kWaveWGsPerCU = 8;
 constexpr uint32_t kPackMaxDocs = 16;     // documents per packed window (<= kPackMax, kernels_index.hip)
 constexpr uint64_t kPackBytes = 2048;     // text per packed window (auto pack size)    // 64-thread workgroups per CU (2 waves/SIMD: VGPR-bound)
 hipError_t launch_tokenize_long(const BuildParams &p, int grid, hipStream_t s);
+hipError_t launch_tokenize_uwave(const BuildParams &p, int grid, hipStream_t s);   // kernels_unicode.hip
+constexpr uint32_t kUwaveWGsPerCU = 6;    // 64-thread workgroups, ~25 KB LDS each
 hipError_t launch_df_partial(const PostingParams &p, hipStream_t s);
 hipError_t launch_df_sum(const PostingParams &p, hipStream_t s);
 hipError_t launch_row_scan(const PostingParams &p, hipStream_t s);

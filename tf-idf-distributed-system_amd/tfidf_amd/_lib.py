@@ -38,7 +38,7 @@ class Config(C.Structure):
 class IndexStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("num_docs", "doc_count", "sum_ttf", "num_terms", "nnz",
                                           "device_bytes", "long_docs", "text_bytes", "term_major",
-                                          "pack_docs", "pack_retried")]
+                                          "pack_docs", "pack_retried", "unicode_docs")]
 
 
 class CommitTiming(C.Structure):

@@ -105,6 +105,14 @@ def _d2h(dst_np, src_ptr, nbytes):
         raise RuntimeError("hipMemcpy D2H failed: %d" % rc)
 
 
+def _h2d(dst_ptr, src_np, nbytes):
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    rc = hip.hipMemcpy(C.c_void_p(dst_ptr), src_np.ctypes.data, nbytes, 1)     # hipMemcpyHostToDevice
+    if rc != 0:
+        raise RuntimeError("hipMemcpy H2D failed: %d" % rc)
+
+
 class DeviceCorpus:
     """Corpus generated directly in HBM by the tfidf_synth_corpus kernels."""
 
@@ -126,6 +134,22 @@ class DeviceCorpus:
         text = np.zeros(int(offs[n]), np.uint8)
         _d2h(text, self.d_text, int(offs[n]))
         return text, offs
+
+    def inject_unicode(self, frac, seed=SEED + 7):
+        """Make a fraction of the documents non-ASCII in place (same byte
+        length): the first two letters of the chosen documents' first word
+        become U+00E9 (C3 A9).  Those documents take the Unicode tokenizer
+        path.  Returns the number of documents changed."""
+        if frac <= 0:
+            return 0
+        text, offs = self.to_host()
+        rng = np.random.default_rng(seed)
+        pick = np.nonzero(rng.random(self.n_docs) < frac)[0]
+        starts = offs[pick][(offs[pick + 1] - offs[pick]) >= 4].astype(np.int64)
+        text[starts] = 0xC3
+        text[starts + 1] = 0xA9
+        _h2d(self.d_text, text, text.nbytes)
+        return int(starts.size)
 
     def free(self):
         from . import _lib as L
