@@ -37,7 +37,7 @@ inline bool analyze(const uint8_t *s, uint64_t n, std::vector<std::string> *out)
   };
   uint64_t pos = 0, ts, te;
   bool bad = false;
-  while (uc_next_span(s, n, &pos, n, &ts, &te, &bad)) {
+  while (uc_next_span(UcDecodeSrc{s, n}, n, &pos, n, &ts, &te, &bad)) {
     std::string t;
     StrSink sink{&t};
     const uint64_t cut = uc_token_bytes(s, n, ts, te, sink);

@@ -32,12 +32,83 @@ constexpr uint32_t kUwSlotBits = 10;
 constexpr uint32_t kUwMaxTerms = 768;
 constexpr uint32_t kUwMaxRanges = 64;
 
+// Scanner class source over classes precomputed in LDS: per byte, the class
+// of the char starting there | (length - 1) << 5, or 0xFF (malformed, or a
+// continuation byte: a scan never lands on one of a well-formed char).
+struct UwClassSrcRef {
+  const uint8_t *cls;
+  __device__ __forceinline__ uint32_t at(uint64_t i, uint32_t *len) const {
+    const uint32_t v = cls[i];
+    if (v == 0xFFu) return kUcBad;
+    *len = (v >> 5) + 1;
+    return v & 31u;
+  }
+};
+
+constexpr uint32_t kUwClasses = 19;     // kUc* classes
+constexpr uint32_t kUwStates = 12;      // kW* states (incl. kWDead)
+
+// WORD-rule scan over chars (not units): an extender keeps the DFA state (it
+// belongs to the unit of the preceding head), any other class takes a
+// transition of the LDS table built from uc_word_next.  Same spans as
+// uc_next_span (unicode_scan.h), with one LDS read per char for the class and
+// one for the transition instead of the branchy unit walk.
+__device__ __forceinline__ bool uw_next_span(const uint8_t *cls, const uint8_t *tr, uint32_t n, uint32_t *pos,
+                                             uint32_t stop, uint32_t *ts, uint32_t *te, bool *bad) {
+  while (*pos < stop) {
+    const uint32_t i = *pos;
+    const uint32_t v = cls[i];
+    if (v == 0xFFu) { *bad = true; return false; }
+    const uint32_t c = v & 31u, l = (v >> 5) + 1;
+    const uint32_t st0 = tr[kWStart * kUwClasses + c];
+    if (st0 != kWDead) {                                  // ALetter / Hebrew / Numeric / Katakana / ENL
+      uint32_t st = st0, p = i + l, last = uc_word_accepting(st) ? p : i, erun = p;
+      while (p < n) {
+        const uint32_t w = cls[p];
+        if (w == 0xFFu) { *bad = true; return false; }
+        const uint32_t cw = w & 31u;
+        if (!uc_is_extender(cw)) {
+          const uint32_t ns = tr[st * kUwClasses + cw];
+          if (ns == kWDead) break;
+          st = ns;
+        }
+        p += (w >> 5) + 1;
+        if (uc_word_accepting(st)) last = p;
+        else if (st == kWELead) erun = p;
+      }
+      if (last > i) { *ts = i; *te = last; *pos = last; return true; }
+      uint32_t q = i + l;                                 // ENL run, no core: see uc_next_span
+      while (q < erun && (cls[q] & 31u) != kUcExtendSA) q += (cls[q] >> 5) + 1;
+      *pos = q;
+      continue;
+    }
+    if (c == kUcOther || c == kUcExtend || c == kUcZWJ || c == kUcMidLetter || c == kUcMidNumLet ||
+        c == kUcMidNum || c == kUcSQuote || c == kUcDQuote) {
+      *pos = i + l;                                       // [^]
+      continue;
+    }
+    // SA runs, Han / Hiragana / emoji / Regional_Indicator units: the shared scanner
+    const UwClassSrcRef src{cls};
+    uint64_t p64 = i, ts64, te64;
+    if (!uc_next_span(src, n, &p64, (uint64_t)i + 1, &ts64, &te64, bad)) {
+      *pos = (uint32_t)p64;
+      if (*bad) return false;
+      continue;
+    }
+    *ts = (uint32_t)ts64; *te = (uint32_t)te64; *pos = (uint32_t)p64;
+    return true;
+  }
+  return false;
+}
+
 struct UwSmem {
   alignas(16) uint8_t text[kUwWindow + 16];
+  alignas(16) uint8_t cls[kUwWindow];
   unsigned long long klo[kUwSlots];   // key lo; after the lookup: dictionary slot
   unsigned long long khi[kUwSlots];   // key hi (VALID bit set: occupied)
   uint32_t cnt[kUwSlots];             // tf
   uint32_t rcnt[kUwMaxRanges];        // per-range counts, then cursors
+  uint8_t tr[kUwStates * kUwClasses]; // WORD DFA transitions
 };
 
 __device__ __forceinline__ uint32_t uw_incl_add(uint32_t x, uint32_t lane) {
@@ -55,6 +126,9 @@ __global__ void __launch_bounds__(64) k_tokenize_uwave(BuildParams p) {
   const uint32_t n_uni = *p.uni_count;
   const uint32_t R = p.n_ranges;
   unsigned long long my_dc = 0, my_ttf = 0, my_nnz = 0;
+  for (uint32_t e = lane; e < kUwStates * kUwClasses; e += 64)
+    sm.tr[e] = (uint8_t)uc_word_next(e / kUwClasses, e % kUwClasses);
+  __syncthreads();
 
   for (uint32_t it = blockIdx.x; it < n_uni; it += gridDim.x) {
     const uint32_t d = p.uni_list[it];
@@ -76,6 +150,39 @@ __global__ void __launch_bounds__(64) k_tokenize_uwave(BuildParams p) {
     sm.rcnt[lane] = 0;
     __syncthreads();
     const uint8_t *doc = sm.text + shift;
+    // ---- classes: lane l decodes bytes [64 l, 64 l + 64); ASCII words take no table read
+    for (uint32_t j = 0; j < 64; j += 4) {
+      const uint32_t i0 = 64 * lane + j;
+      if (i0 >= L) break;
+      uint32_t w = 0;
+#pragma unroll
+      for (int b = 0; b < 4; b++) w |= (i0 + b < L ? (uint32_t)doc[i0 + b] : 0x20u) << (8 * b);
+      uint32_t out = 0;
+      if ((w & 0x80808080u) == 0) {
+#pragma unroll
+        for (int b = 0; b < 4; b++) out |= uc_ascii_class((w >> (8 * b)) & 0xFFu) << (8 * b);
+      } else {
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const uint32_t x = (w >> (8 * b)) & 0xFFu;
+          uint32_t v;
+          if (x < 0x80u) v = uc_ascii_class(x);
+          else if ((x & 0xC0u) == 0x80u || i0 + b >= L) v = 0xFFu;
+          else {
+            uint32_t l;
+            const uint32_t cp = utf8_decode(doc, L, i0 + b, &l);
+            v = cp == kUcBad ? 0xFFu : (uc_class(cp) | ((l - 1) << 5));
+          }
+          out |= v << (8 * b);
+        }
+      }
+      const uint32_t keep = L - i0 >= 4 ? 4u : (uint32_t)(L - i0);
+#pragma unroll
+      for (int b = 0; b < 4; b++)
+        if ((uint32_t)b < keep) sm.cls[i0 + b] = (uint8_t)(out >> (8 * b));
+    }
+    __syncthreads();
+
 
     // ---- slices: lane l scans tokens starting in [cut(l), cut(l + 1))
     const uint64_t seg = (L + 63) >> 6;
@@ -94,7 +201,13 @@ __global__ void __launch_bounds__(64) k_tokenize_uwave(BuildParams p) {
       uint64_t ts, te, lo = 0, hi = 0;
       bool have = false;
       if (active) {
-        have = uc_next_token(doc, L, &pos, stop, &ts, &te, &lo, &hi, &ubad);
+        uint32_t p32 = (uint32_t)pos, ts32, te32;
+        have = uw_next_span(sm.cls, sm.tr, (uint32_t)L, &p32, (uint32_t)stop, &ts32, &te32, &ubad);
+        if (have) {
+          const uint64_t cutp = uc_token_key(doc, L, ts32, te32, &lo, &hi);
+          if (cutp < te32) p32 = (uint32_t)cutp;                   // 255-unit cut: rescan from the cut
+        }
+        pos = p32;
         active = have;
       }
       ntok += have;

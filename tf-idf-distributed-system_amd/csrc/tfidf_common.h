@@ -9,10 +9,10 @@
 //   * 9..16 bytes: lo = bytes 0..7 | LO_LONG (bit 63), hi = bytes 8..15 |
 //                  VALID — exact;
 //   * 17..255    : lo = bytes 0..7 | LO_LONG | LO_HASHED (bit 55), hi = VALID
-//                  | 63-bit hash of all bytes and the length.
+//                  | 63-bit hash of all bytes and the length (KeyBuilder).
 //   * any token holding a non-ASCII byte (UTF-8 of the lower-cased code
-//     points; unicode_scan.h): lo = 56 hash bits | LO_LONG | LO_HASHED, hi =
-//     VALID | 63-bit hash — 119 hash bits, no exact form.
+//     points; unicode_scan.h): lo = 56 bits of one hash chain | LO_LONG |
+//     LO_HASHED, hi = VALID | 63 bits of a second chain — no exact form.
 // Bit 63 of hi (VALID) is set for every key so that hi == 0 marks "not
 // written" in the device dictionary.
 #pragma once
@@ -98,24 +98,32 @@ TFIDF_HD uint32_t dict_home(uint32_t h, uint32_t mask) {   // mask = C - 1, C = 
   return (h >> __builtin_clz(mask)) & mask;
 }
 
-// Incremental key builder over lower-cased bytes.
+// Incremental key builder over lower-cased bytes.  The hash of the hashed
+// forms runs over 8-byte blocks (two independent 64-bit chains, one mix64 each
+// per block), so long and non-ASCII tokens cost a few ALU ops per byte.
 struct KeyBuilder {
   uint64_t w0 = 0, w1 = 0;    // raw bytes 0..15
-  uint64_t h1 = 0x243F6A8885A308D3ull, h2 = 0x13198A2E03707344ull;  // hash of all bytes
+  uint64_t cur = 0;           // current 8-byte block
+  uint64_t hb = 0x243F6A8885A308D3ull, hc = 0x13198A2E03707344ull;
   uint32_t n = 0;
   uint32_t na = 0;            // a byte >= 0x80 was pushed
   TFIDF_HD void push(uint8_t c) {
     na |= c >> 7;
     if (n < 8) w0 |= (uint64_t)c << (8 * n);
     else if (n < 16) w1 |= (uint64_t)c << (8 * (n - 8));
-    h1 = (h1 ^ c) * 0x100000001B3ull;
-    h2 = mix64(h2 + c);
+    cur |= (uint64_t)c << (8 * (n & 7));
     n++;
+    if ((n & 7) == 0) {
+      hb = mix64(hb ^ cur);
+      hc = mix64(hc + cur * 0x9E3779B97F4A7C15ull);
+      cur = 0;
+    }
   }
   TFIDF_HD void finish(uint64_t *klo, uint64_t *khi) const {
     if (na) {
-      *klo = (mix64(h1 ^ 0xA5A5A5A5A5A5A5A5ull ^ n) & 0x7F7F7F7F7F7F7F7Full) | kLoLong | kLoHashed;
-      *khi = mix64(h2 ^ mix64(h1 ^ ((uint64_t)n << 56))) | kKeyValid;
+      const uint64_t t = (uint64_t)n << 56;
+      *klo = (mix64(hb ^ cur ^ t) & 0x7F7F7F7F7F7F7F7Full) | kLoLong | kLoHashed;
+      *khi = mix64(hc + (cur ^ t) * 0x9E3779B97F4A7C15ull) | kKeyValid;
     } else if (n <= 8) {
       *klo = w0;
       *khi = kKeyValid;
@@ -124,7 +132,7 @@ struct KeyBuilder {
       *khi = w1 | kKeyValid;
     } else {
       *klo = w0 | kLoLong | kLoHashed;
-      *khi = mix64(h2 ^ mix64(h1 ^ ((uint64_t)n << 56))) | kKeyValid;
+      *khi = mix64(hb ^ mix64(hc ^ cur ^ ((uint64_t)n << 56))) | kKeyValid;
     }
   }
 };

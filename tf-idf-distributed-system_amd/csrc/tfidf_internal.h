@@ -88,7 +88,7 @@ constexpr uint32_t kPackMaxDocs = 16;     // documents per packed window (<= kPa
 constexpr uint64_t kPackBytes = 2048;     // text per packed window (auto pack size)    // 64-thread workgroups per CU (2 waves/SIMD: VGPR-bound)
 hipError_t launch_tokenize_long(const BuildParams &p, int grid, hipStream_t s);
 hipError_t launch_tokenize_uwave(const BuildParams &p, int grid, hipStream_t s);   // kernels_unicode.hip
-constexpr uint32_t kUwaveWGsPerCU = 6;    // 64-thread workgroups, ~25 KB LDS each
+constexpr uint32_t kUwaveWGsPerCU = 5;    // 64-thread workgroups, ~29 KB LDS each
 hipError_t launch_df_partial(const PostingParams &p, hipStream_t s);
 hipError_t launch_df_sum(const PostingParams &p, hipStream_t s);
 hipError_t launch_row_scan(const PostingParams &p, hipStream_t s);

@@ -62,9 +62,24 @@ TFIDF_HD uint32_t uc_class(uint32_t cp) {
 TFIDF_HD uint32_t uc_lower(uint32_t cp) {
   return (uint32_t)((int32_t)cp + kUcLowerData[(uint32_t)kUcLowerIndex[cp >> 8] * 256u + (cp & 255u)]);
 }
+// ASCII classes without a table read (the generated table agrees: every
+// ASCII class lookup of the host scanner goes through this function).
+TFIDF_HD uint32_t uc_ascii_class(uint32_t c) {
+  if ((c | 0x20u) - 'a' < 26u) return kUcALetter;
+  if (c - '0' < 10u) return kUcNumeric;
+  switch (c) {
+    case '_': return kUcExtNumLet;
+    case ':': return kUcMidLetter;
+    case '.': return kUcMidNumLet;
+    case ',': case ';': return kUcMidNum;
+    case '\'': return kUcSQuote;
+    case '"': return kUcDQuote;
+    default: return kUcOther;
+  }
+}
 TFIDF_HD bool uc_is_extender(uint32_t c) { return c == kUcExtend || c == kUcExtendSA || c == kUcZWJ; }
 // ASCII byte after which the scan state is the start state (see header).
-TFIDF_HD bool uc_split_byte(uint8_t b) { return b < 0x80 && uc_class(b) == kUcOther; }
+TFIDF_HD bool uc_split_byte(uint8_t b) { return b < 0x80 && uc_ascii_class(b) == kUcOther; }
 
 // Strict UTF-8 (what Files.readString's decoder accepts, Worker.java:198):
 // code point at byte i, *len bytes; kUcBad for a malformed, overlong,
@@ -99,6 +114,21 @@ TFIDF_HD uint32_t utf8_decode(const uint8_t *s, uint64_t n, uint64_t i, uint32_t
   }
   return kUcBad;
 }
+
+// Class source of the scanner: class of the char starting at byte i and its
+// byte length, kUcBad for malformed UTF-8.  This one decodes and reads the
+// tables (host; device fallback); the Unicode wave kernel reads classes
+// precomputed in LDS instead (kernels_unicode.hip).
+struct UcDecodeSrc {
+  const uint8_t *s;
+  uint64_t n;
+  TFIDF_HD uint32_t at(uint64_t i, uint32_t *len) const {
+    const uint32_t b = s[i];
+    if (b < 0x80u) { *len = 1; return uc_ascii_class(b); }
+    const uint32_t cp = utf8_decode(s, n, i, len);
+    return cp == kUcBad ? kUcBad : uc_class(cp);
+  }
+};
 
 // WORD rule DFA states (accepting: A, H, N, K, EAFTER, HSQ).
 enum : uint32_t { kWStart = 0, kWELead, kWA, kWH, kWN, kWK, kWEAfter, kWHSq, kWHDq, kWAMid, kWNMid, kWDead };
@@ -155,17 +185,16 @@ TFIDF_HD uint32_t uc_word_next(uint32_t st, uint32_t c) {
 
 // One unit (head + extenders) starting at byte i: returns the head class and
 // the byte after the unit in *end; *zwj_last = the unit ends with a ZWJ.
-TFIDF_HD uint32_t uc_unit(const uint8_t *s, uint64_t n, uint64_t i, uint64_t *end, bool *zwj_last, bool *bad) {
+template <class Src>
+TFIDF_HD uint32_t uc_unit(const Src &src, uint64_t n, uint64_t i, uint64_t *end, bool *zwj_last, bool *bad) {
   uint32_t l;
-  const uint32_t cp = utf8_decode(s, n, i, &l);
-  if (cp == kUcBad) { *bad = true; *end = n; return kUcOther; }
-  const uint32_t c = uc_class(cp);
+  const uint32_t c = src.at(i, &l);
+  if (c == kUcBad) { *bad = true; *end = n; return kUcOther; }
   uint64_t p = i + l;
   bool z = false;
   while (p < n) {
-    const uint32_t cp2 = utf8_decode(s, n, p, &l);
-    if (cp2 == kUcBad) { *bad = true; *end = n; return kUcOther; }
-    const uint32_t c2 = uc_class(cp2);
+    const uint32_t c2 = src.at(p, &l);
+    if (c2 == kUcBad) { *bad = true; *end = n; return kUcOther; }
     if (!uc_is_extender(c2)) break;
     z = c2 == kUcZWJ;
     p += l;
@@ -178,21 +207,21 @@ TFIDF_HD uint32_t uc_unit(const uint8_t *s, uint64_t n, uint64_t i, uint64_t *en
 // Next token starting in [*pos, stop) (a scan position); its extent is
 // [*ts, *te) (not yet chopped).  Returns false when none is left or the text
 // is malformed (*bad).  *pos is advanced past the token / skipped chars.
-TFIDF_HD bool uc_next_span(const uint8_t *s, uint64_t n, uint64_t *pos, uint64_t stop, uint64_t *ts, uint64_t *te,
+template <class Src>
+TFIDF_HD bool uc_next_span(const Src &src, uint64_t n, uint64_t *pos, uint64_t stop, uint64_t *ts, uint64_t *te,
                            bool *bad) {
   while (*pos < stop && !*bad) {
     const uint64_t i = *pos;
     uint32_t l;
-    const uint32_t cp = utf8_decode(s, n, i, &l);
-    if (cp == kUcBad) { *bad = true; return false; }
-    const uint32_t c = uc_class(cp);
+    const uint32_t c = src.at(i, &l);
+    if (c == kUcBad) { *bad = true; return false; }
     if (c == kUcALetter || c == kUcHebrew || c == kUcNumeric || c == kUcKatakana || c == kUcExtNumLet) {
       uint32_t st = kWStart;
       uint64_t p = i, last = i, erun = i;
       while (p < n) {
         uint64_t e;
         bool z;
-        const uint32_t uc = uc_unit(s, n, p, &e, &z, bad);
+        const uint32_t uc = uc_unit(src, n, p, &e, &z, bad);
         if (*bad) return false;
         const uint32_t ns = uc_word_next(st, uc);
         if (ns == kWDead) break;
@@ -207,8 +236,7 @@ TFIDF_HD bool uc_next_span(const uint8_t *s, uint64_t n, uint64_t *pos, uint64_t
       // starts an SA run there.
       uint64_t q = i + l;
       while (q < erun) {
-        const uint32_t cq = utf8_decode(s, n, q, &l);
-        if (uc_class(cq) == kUcExtendSA) break;
+        if (src.at(q, &l) == kUcExtendSA) break;
         q += l;
       }
       *pos = q;
@@ -217,9 +245,8 @@ TFIDF_HD bool uc_next_span(const uint8_t *s, uint64_t n, uint64_t *pos, uint64_t
     if (c == kUcSA || c == kUcExtendSA) {            // SEA: run of Complex_Context chars (+ extenders)
       uint64_t p = i + l;
       while (p < n) {
-        const uint32_t cp2 = utf8_decode(s, n, p, &l);
-        if (cp2 == kUcBad) { *bad = true; return false; }
-        const uint32_t c2 = uc_class(cp2);
+        const uint32_t c2 = src.at(p, &l);
+        if (c2 == kUcBad) { *bad = true; return false; }
         if (c2 != kUcSA && !uc_is_extender(c2)) break;
         p += l;
       }
@@ -229,13 +256,13 @@ TFIDF_HD bool uc_next_span(const uint8_t *s, uint64_t n, uint64_t *pos, uint64_t
     if (c == kUcHan || c == kUcHiragana || c == kUcEmoji || c == kUcRI) {
       uint64_t e;
       bool z;
-      uc_unit(s, n, i, &e, &z, bad);
+      uc_unit(src, n, i, &e, &z, bad);
       if (*bad) return false;
       if (c == kUcEmoji) {                           // ZWJ sequences
         while (z && e < n) {
           uint64_t e2;
           bool z2;
-          const uint32_t c2 = uc_unit(s, n, e, &e2, &z2, bad);
+          const uint32_t c2 = uc_unit(src, n, e, &e2, &z2, bad);
           if (*bad) return false;
           if (c2 != kUcEmoji) break;
           e = e2;
@@ -244,7 +271,7 @@ TFIDF_HD bool uc_next_span(const uint8_t *s, uint64_t n, uint64_t *pos, uint64_t
       } else if (c == kUcRI) {                       // flag = Regional_Indicator pair
         uint64_t e2 = e;
         bool z2;
-        const uint32_t c2 = e < n ? uc_unit(s, n, e, &e2, &z2, bad) : kUcOther;
+        const uint32_t c2 = e < n ? uc_unit(src, n, e, &e2, &z2, bad) : kUcOther;
         if (*bad) return false;
         if (c2 != kUcRI) { *pos = i + l; continue; }
         e = e2;
@@ -300,12 +327,18 @@ TFIDF_HD uint64_t uc_token_key(const uint8_t *s, uint64_t n, uint64_t ts, uint64
 
 // Host/device loop body: next token in [*pos, stop) with its key; handles the
 // 255-unit cut (scanning restarts at the cut).
-TFIDF_HD bool uc_next_token(const uint8_t *s, uint64_t n, uint64_t *pos, uint64_t stop, uint64_t *ts, uint64_t *te,
-                            uint64_t *lo, uint64_t *hi, bool *bad) {
-  if (!uc_next_span(s, n, pos, stop, ts, te, bad)) return false;
+template <class Src>
+TFIDF_HD bool uc_next_token(const Src &src, const uint8_t *s, uint64_t n, uint64_t *pos, uint64_t stop, uint64_t *ts,
+                            uint64_t *te, uint64_t *lo, uint64_t *hi, bool *bad) {
+  if (!uc_next_span(src, n, pos, stop, ts, te, bad)) return false;
   const uint64_t cut = uc_token_key(s, n, *ts, *te, lo, hi);
   if (cut < *te) { *te = cut; *pos = cut; }
   return true;
+}
+
+TFIDF_HD bool uc_next_token(const uint8_t *s, uint64_t n, uint64_t *pos, uint64_t stop, uint64_t *ts, uint64_t *te,
+                            uint64_t *lo, uint64_t *hi, bool *bad) {
+  return uc_next_token(UcDecodeSrc{s, n}, s, n, pos, stop, ts, te, lo, hi, bad);
 }
 
 }  // namespace tfidf
