@@ -62,7 +62,9 @@ extern "C" {
 
 /* Inverted-index layout built by tfidf_commit (results are identical). */
 #define TFIDF_INVERSION_AUTO 0  /* block-major unless its (docs/8192 + 1) x 2^vocab_capacity_log2 count table
-                                   outgrows the CSR, or vocab_capacity_log2 > 21 (huge vocabularies) */
+                                   outgrows the CSR, or vocab_capacity_log2 > 21 (huge vocabularies), or the
+                                   corpus is a few very long documents (fewer (block, range) tiles than CUs,
+                                   >= 64 KB per document: books) */
 #define TFIDF_INVERSION_BLOCK 1 /* block-major: postings grouped by 8192-doc block, then term */
 #define TFIDF_INVERSION_TERM 2  /* term-major: postings grouped by term, docs ascending (sort-based) */
 

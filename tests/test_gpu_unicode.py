@@ -127,3 +127,22 @@ def test_whitespace_free_unicode_document():
     check(g, o, texts)
     g.close()
     o.close()
+
+
+def test_book_corpus_long_unicode_docs():
+    # SURVEY cfg 1 shape (a few hundred books; here 12 of ~240 KB): every
+    # document takes the long path's general phase; AUTO builds term-major
+    # (too few (block, range) tiles for the block-major passes).
+    rng = random.Random(12)
+    texts = [uni_doc(rng, rng.randint(20000, 40000)) for _ in range(10)]
+    texts += [b" ".join(synth.word(rng.randint(1, 20000)) for _ in range(30000))] * 2
+    g, o = build_pair(texts)
+    st = g.stats()
+    assert st["long_docs"] == len(texts) and st["term_major"] == 1
+    check(g, o, texts)
+    for q in QUERIES + [synth.word(5).decode() + " " + synth.word(77).decode()]:
+        qb = q.encode()
+        assert_hits_equal(g.search(qb, 0), o.search(qb, 0))
+        assert_hits_equal(g.search(qb, 3), o.search(qb, 3))
+    g.close()
+    o.close()

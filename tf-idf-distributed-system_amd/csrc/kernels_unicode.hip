@@ -126,6 +126,7 @@ __global__ void __launch_bounds__(64) k_tokenize_uwave(BuildParams p) {
   const uint32_t n_uni = *p.uni_count;
   const uint32_t R = p.n_ranges;
   unsigned long long my_dc = 0, my_ttf = 0, my_nnz = 0;
+  if (blockIdx.x >= n_uni) return;                          // block-uniform
   for (uint32_t e = lane; e < kUwStates * kUwClasses; e += 64)
     sm.tr[e] = (uint8_t)uc_word_next(e / kUwClasses, e % kUwClasses);
   __syncthreads();

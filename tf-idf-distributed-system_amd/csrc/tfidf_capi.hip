@@ -138,7 +138,7 @@ struct tfidf_index {
     return term_major ? tdf.as<uint32_t>() : blk.as<uint32_t>() + (size_t)n_blocks * C;
   }
   DevBuf lt_keys, lt_cnt, lt_g;
-  uint32_t lt_log2 = 0, lt_wgs = 64;
+  uint32_t lt_log2 = 0, lt_wgs = 64;   // lt_wgs: long-path workgroups always allowed
   std::vector<uint64_t> h_dict;
   std::vector<uint32_t> h_df;
   uint64_t doc_count = 0, sum_ttf = 0, nnz = 0, num_terms = 0, long_docs = 0;
@@ -621,7 +621,15 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
     const uint64_t blk_bytes = (uint64_t)(ix->n_blocks + 1) * C * 4;
     if (ix->cfg.inversion == TFIDF_INVERSION_TERM) ix->term_major = true;
     else if (ix->cfg.inversion == TFIDF_INVERSION_BLOCK) ix->term_major = false;
-    else ix->term_major = ix->cap_log2 > kMaxBlockCapLog2 || (blk_bytes > (1ull << 31) && blk_bytes > row_cap * 4);
+    else {
+      // Few (block, range) tiles of very long documents (a few hundred books,
+      // SURVEY cfg 1): the block-major passes run one workgroup per tile and
+      // starve; the sort-based term-major build is parallel in the postings.
+      const uint64_t tiles = (uint64_t)ix->n_blocks * (C < kRangeSlots ? 1u : C / kRangeSlots);
+      const bool starved = tiles < ix->num_cus && ix->n_staged && ix->text_bytes / ix->n_staged >= (64u << 10);
+      ix->term_major = ix->cap_log2 > kMaxBlockCapLog2 || (blk_bytes > (1ull << 31) && blk_bytes > row_cap * 4) ||
+                       starved;
+    }
   }
   // CSR rows are grouped by dictionary range for the block-major passes only
   const uint32_t RS = ix->term_major ? C : (C < kRangeSlots ? C : kRangeSlots);
@@ -741,7 +749,11 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
     while (need < 22 && (1ull << need) < maxlen + 2) need++;
     lg = std::min(lg, need);
     ix->lt_log2 = lg;
-    const uint32_t wgs = std::min<uint32_t>(n_long, ix->lt_wgs);
+    // one workgroup per long document, up to 2 per CU, within a scratch budget
+    // (24 B per table slot per workgroup: key lo/hi, count, dictionary slot)
+    const uint64_t per_wg = 24ull << lg;
+    const uint64_t by_budget = std::max<uint64_t>(ix->lt_wgs, kLongScratchBudget / per_wg);
+    const uint32_t wgs = (uint32_t)std::min<uint64_t>({(uint64_t)n_long, (uint64_t)ix->num_cus * 2, by_budget});
     HIP_TRY(ix->lt_keys.reserve((size_t)wgs * 2 * (1ull << lg) * 8));
     HIP_TRY(ix->lt_cnt.reserve((size_t)wgs * (1ull << lg) * 4));
     HIP_TRY(ix->lt_g.reserve((size_t)wgs * (1ull << lg) * 4));

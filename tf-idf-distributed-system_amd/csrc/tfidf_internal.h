@@ -18,6 +18,7 @@ constexpr uint32_t kErrLongScratch = 16u;
 constexpr uint32_t kChunk = 2048;
 constexpr uint32_t kPreMargin = 64;
 constexpr uint32_t kPostMargin = 320;
+constexpr uint64_t kLongScratchBudget = 8ull << 30;   // per-document tables of the concurrent long-path workgroups
 
 struct BuildParams {
   const uint8_t *text;        // corpus base (device)
