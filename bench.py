@@ -239,7 +239,11 @@ def main():
         tj = json.load(open(args.traffic_json))
         w = tj.get("workload") or {}
         if (w.get("docs_per_gpu"), w.get("text_bytes_per_gpu"), w.get("nnz_per_gpu")) == (N, text_bytes, nnz):
-            traffic = tj["kernels"][kname]["hbm_bytes_corrected"]
+            # rocprof names carry template arguments (k_tokenize_wave<false>); a
+            # phase of several kernels (k_scatter_part + k_scatter_sort) sums them
+            hits = [v["hbm_bytes_corrected"] for n, v in tj["kernels"].items()
+                    if n.split("<")[0] == kname or n.startswith(kname + "_")]
+            traffic = sum(hits) if hits else None
             traffic_src = os.path.relpath(args.traffic_json, REPO) + " (" + tj["note"] + ")"
     except (OSError, KeyError, ValueError, TypeError):
         pass

@@ -199,7 +199,7 @@ __global__ void __launch_bounds__(64) k_tokenize_uwave(BuildParams p) {
     bool active = pos < stop, ubad = false, overflow = false;
     uint32_t ntok = 0;
     while (__any(active)) {
-      uint64_t ts, te, lo = 0, hi = 0;
+      uint64_t lo = 0, hi = 0;
       bool have = false;
       if (active) {
         uint32_t p32 = (uint32_t)pos, ts32, te32;
