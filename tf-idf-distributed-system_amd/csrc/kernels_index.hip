@@ -986,11 +986,15 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     {
       uint32_t occ = 0;
       const uint4 *kp = reinterpret_cast<const uint4 *>(&sm.key[16 * lane]);
+      // lanes are 128 B apart: visiting the 16-B pieces in an order rotated by
+      // (lane >> 1) & 7 gives every ds_read_b128 lane group 16 distinct bank
+      // slots (unrotated: 8-way conflicts, most of the kernel's conflict cycles)
+      const uint32_t rot = (lane >> 1) & 7;
 #pragma unroll
       for (int q = 0; q < 8; q++) {
-        const uint4 t = kp[q];
-        occ |= (uint32_t)((t.x | t.y) != 0) << (2 * q);
-        occ |= (uint32_t)((t.z | t.w) != 0) << (2 * q + 1);
+        const uint32_t qq = (q + rot) & 7;
+        const uint4 t = kp[qq];
+        occ |= ((uint32_t)((t.x | t.y) != 0) | ((uint32_t)((t.z | t.w) != 0) << 1)) << (2 * qq);
       }
       const uint32_t c = (uint32_t)__popc(occ);
       uint32_t at = wave_incl_add(c) - c;
