@@ -1824,6 +1824,21 @@ hipError_t launch_row_scan(const PostingParams &p, hipStream_t s) {
   hipLaunchKernelGGL(k_row_scan, dim3(p.n_blocks), dim3(1024), 0, s, p);
   return hipGetLastError();
 }
+// number of nonzero entries of a[0, n) (occupied dictionary slots): one
+// ballot per wave, one atomic per wave
+__global__ void __launch_bounds__(256) k_count_nonzero(const uint64_t *a, uint32_t n, unsigned long long *out) {
+  uint32_t c = 0;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint64_t m = __ballot(a[i] != 0);
+    c += (uint32_t)__popcll(m);
+  }
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(out, (unsigned long long)c);
+}
+hipError_t launch_count_nonzero(const uint64_t *a, uint32_t n, unsigned long long *out, hipStream_t s) {
+  const uint32_t grid = std::max(1u, std::min((n + 255) / 256, 2048u));
+  hipLaunchKernelGGL(k_count_nonzero, dim3(grid), dim3(256), 0, s, a, n, out);
+  return hipGetLastError();
+}
 hipError_t launch_block_base(const PostingParams &p, hipStream_t s) {
   hipLaunchKernelGGL(k_block_base, dim3(1), dim3(64), 0, s, p);
   return hipGetLastError();

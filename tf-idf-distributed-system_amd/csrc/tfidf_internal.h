@@ -94,6 +94,7 @@ hipError_t launch_df_partial(const PostingParams &p, hipStream_t s);
 hipError_t launch_df_sum(const PostingParams &p, hipStream_t s);
 hipError_t launch_row_scan(const PostingParams &p, hipStream_t s);
 hipError_t launch_block_base(const PostingParams &p, hipStream_t s);
+hipError_t launch_count_nonzero(const uint64_t *a, uint32_t n, unsigned long long *out, hipStream_t s);
 hipError_t launch_scatter(const PostingParams &p, hipStream_t s);
 
 // --- term-major inversion for large vocabularies (kernels_term.hip) ---
