@@ -218,6 +218,8 @@ def main():
     alg = {
         # text read once + CSR (slot u32 + tf u32) written once + row metadata (SURVEY: 9 B/doc)
         "ms_tokenize": text_bytes + 8 * nnz + 9 * N,
+        # long-document path (book-sized documents): the same formula over the documents it takes
+        "ms_long": text_bytes + 8 * nnz + 9 * N,
         # slot column read + per-block DF partials written
         "ms_df": 4 * nnz + 4 * n_blocks * C_slots,
         # partials read + offsets written
@@ -233,8 +235,8 @@ def main():
     # measured HBM traffic of the dominant kernel: a separate rocprofv3 PMC pass
     # over the same workload (counters cannot be read from inside this run)
     traffic, traffic_src = None, None
-    kname = {"ms_tokenize": "k_tokenize_wave", "ms_df": "k_df_partial", "ms_blockscan": "k_row_scan",
-             "ms_scatter": "k_scatter"}[dom]
+    kname = {"ms_tokenize": "k_tokenize_wave", "ms_long": "k_tokenize_long", "ms_df": "k_df_partial",
+             "ms_blockscan": "k_row_scan", "ms_scatter": "k_scatter"}[dom]
     try:
         tj = json.load(open(args.traffic_json))
         w = tj.get("workload") or {}
@@ -284,10 +286,23 @@ def main():
 
     # ---- queries (outside the timed region) ----
     if not args.no_queries and world == 1:
+        from tfidf_amd.engine import analyze
         qs = synth.queries(max(args.queries, 1))
+        # algorithmic bytes: 9 B per posting read (doc u32 + tf u32 + norm u8)
+        df_cache = {}
+
+        def post_bytes(q):
+            tot = 0
+            for t in set(analyze(q)):
+                if t not in df_cache:
+                    df_cache[t] = idx.df(t)[0]
+                tot += 9 * df_cache[t]
+            return tot
+
         idx.search(qs[0], 10)
         lat = []
         dev_ms = 0.0
+        b_q = 0
         t0 = time.perf_counter()
         for q in qs:
             t1 = time.perf_counter()
@@ -295,25 +310,50 @@ def main():
             lat.append(time.perf_counter() - t1)
             dev_ms += idx.last_search_ms()[1]
         t_top = time.perf_counter() - t0
+        for q in qs:
+            b_q += post_bytes(q) + 8 * 10
+        # all hits (searcher.search(q, Integer.MAX_VALUE)): ordered on the device, copied to host arrays
+        n_all = min(len(qs), 50)
+        idx.search_all_arrays(qs[0])
+        nh, all_dev, b_all = 0, 0.0, 0
         t0 = time.perf_counter()
-        nh = 0
-        for q in qs[:20]:
-            nh += len(idx.search(q, 0))
+        for q in qs[:n_all]:
+            d, _ = idx.search_all_arrays(q)
+            nh += len(d)
+            all_dev += idx.last_search_ms()[1]
         t_all = time.perf_counter() - t0
+        for q in qs[:n_all]:
+            b_all += post_bytes(q)
+        b_all += 8 * nh
         bq = synth.queries(args.batch_queries)
         idx.search_batch(bq[:100], 10)
         t0 = time.perf_counter()
         idx.search_batch(bq, 10)
         t_b = time.perf_counter() - t0
         sc_ms, tot_ms = idx.last_search_ms()
+        b_batch = min(sum(post_bytes(q) for q in bq), 8 * nnz + 9 * N) + 8 * 10 * len(bq)
+
+        def roof(alg_bytes, ms):
+            gbs = alg_bytes / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+            return {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": gbs / HBM_PEAK_GBS, "alg_bytes": alg_bytes, "device_ms": ms}
+
         result["queries"] = {
             "single_top10_qps": len(qs) / t_top,
             "single_top10_p50_ms": float(np.percentile(lat, 50)) * 1e3,
             "single_top10_p99_ms": float(np.percentile(lat, 99)) * 1e3,
             "single_top10_device_ms_avg": dev_ms / len(qs),
-            "single_all_hits_qps": 20 / t_all, "avg_hits": nh / 20,
+            "single_all_hits_qps": n_all / t_all, "avg_hits": nh / n_all,
+            "single_all_hits_device_ms_avg": all_dev / n_all,
             "batch10k_top10_qps": len(bq) / t_b,
             "batch10k_device_ms": tot_ms, "batch10k_scoring_ms": sc_ms,
+            "roofline": {
+                "single_top10": roof(b_q / len(qs), dev_ms / len(qs)),
+                "all_hits": roof(b_all / n_all, all_dev / n_all),
+                "batch10k_top10": roof(b_batch, tot_ms),
+                "note": "B_q = sum 9 df(t) + 8 k per query; all hits: sum 9 df(t) + 8 hits; "
+                        "B_batch = min(sum_q sum_t 9 df(t), 8 nnz + 9 N) + 8 k Q (SURVEY §8(d)); "
+                        "device time = HIP events on the index stream (scoring + ordering)"},
         }
     elif not args.no_queries:
         # node-level queries over the sharded corpus with GLOBAL statistics:

@@ -51,11 +51,13 @@ extern "C" {
 #define TFIDF_E_HIP 2
 #define TFIDF_E_OOM 3
 #define TFIDF_E_UNSUPPORTED_INPUT 4 /* malformed UTF-8 document (Files.readString throws), tf >= 2^24 */
-#define TFIDF_E_UNSUPPORTED_QUERY 5 /* malformed UTF-8 query, AND/OR/NOT operator words */
+#define TFIDF_E_UNSUPPORTED_QUERY 5 /* malformed UTF-8 query */
 #define TFIDF_E_CAPACITY 6          /* vocabulary capacity exceeded */
 #define TFIDF_E_STATE 7             /* e.g. search before commit */
 #define TFIDF_E_BUFFER 8            /* caller buffer too small; *n_out holds the size needed */
 #define TFIDF_E_NO_DEVICE 9
+#define TFIDF_E_QUERY_SYNTAX 10     /* QueryParser ParseException / TooManyClauses (Worker.java:182-185 -> []):
+                                       empty query, leading AND/OR, trailing or doubled operator word */
 
 #define TFIDF_STATS_SHARD 0  /* per-shard statistics: the reference's N-worker semantics */
 #define TFIDF_STATS_GLOBAL 1 /* statistics imported from all shards: 1-worker semantics */
@@ -157,7 +159,31 @@ int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const uint64_t *q
 /* Per-query device time of the last search call (HIP events, index stream). */
 int tfidf_last_search_ms(const tfidf_index *ix, float *ms_scoring, float *ms_total);
 
+/* ---- device-resident results (multi-GPU orchestration; no reference
+ * counterpart: they feed the RCCL all-gather that replaces Leader.java:51-70) ----
+ * Merge keys: (float32 score bits << 32) | ~(doc_base + doc) as u64 — BM25
+ * scores are > 0, so descending key order is (score desc, doc asc); 0 = empty.
+ * tfidf_search_batch_keys_device: n_q x k keys into caller device memory
+ *   (a query that does not parse has none).
+ * tfidf_search_all_keys_device: every hit of one query, ordered, into caller
+ *   device memory of cap >= num_docs keys; *n_out = hits.
+ * Both return after the keys are written (the index's stream is synchronised). */
+int tfidf_search_batch_keys_device(tfidf_index *ix, const uint8_t *q_utf8, const uint64_t *q_offsets, uint32_t n_q,
+                                   uint32_t k, uint64_t doc_base, void *d_keys);
+int tfidf_search_all_keys_device(tfidf_index *ix, const uint8_t *q, uint64_t q_len, uint64_t doc_base, void *d_keys,
+                                 uint64_t cap, uint64_t *n_out);
+/* Issue the index's device work on the caller's stream (a hipStream_t, e.g.
+ * torch.cuda.current_stream().cuda_stream; NULL = the legacy default stream),
+ * or back on the index's own stream with TFIDF_OWN_STREAM.  Pending work on
+ * the previous stream is finished first. */
+#define TFIDF_OWN_STREAM ((void *)-1)
+int tfidf_set_stream(tfidf_index *ix, void *stream);
+
 int tfidf_doc_key(const tfidf_index *ix, uint64_t doc, uint8_t *buf, uint64_t cap, uint64_t *n_out);
+/* Every committed document's key (Worker.java:214 StringField "path"), in doc
+ * order: bytes concatenated into buf, offsets[num_docs + 1]; TFIDF_E_BUFFER with
+ * *n_bytes = size needed when cap is too small. */
+int tfidf_doc_keys(const tfidf_index *ix, uint8_t *buf, uint64_t cap, uint64_t *offsets, uint64_t *n_bytes);
 int tfidf_doc_len(tfidf_index *ix, uint64_t doc, uint32_t *len, uint8_t *norm);
 /* Distinct terms of one document: NUL-separated strings (sorted by bytes) + tf. */
 int tfidf_doc_terms(tfidf_index *ix, uint64_t doc, char *terms, uint64_t terms_cap, uint32_t *tfs,
@@ -167,17 +193,21 @@ int tfidf_term_df(tfidf_index *ix, const uint8_t *term, uint64_t len, uint64_t *
 
 /* ---- GLOBAL statistics across shards (no reference counterpart) ----
  * Term-ownership exchange (used by the multi-GPU orchestration; O(vocabulary)
- * per rank, no sort):
+ * per rank, no sort).  The three device calls are ASYNCHRONOUS on the index's
+ * stream (tfidf_set_stream: the caller's collective stream), so the exchange
+ * needs one host read — the split sizes:
  * 1. tfidf_vocab_partition_device: this shard's vocabulary as records
  *    (lo, hi, df: 3 x u64 each) grouped by owner rank (a hash of the term key
- *    mod n_ranks); counts[r] (host, n_ranks entries) = records for rank r.
+ *    mod n_ranks) into d_records; d_counts (device, n_ranks x u64) = records
+ *    per owner; *n_out = records (the shard's vocabulary size, host-known).
  * 2. caller all-to-alls the records to their owners (RCCL), then the owner
  *    calls tfidf_vocab_reduce_device on everything it received: d_df_out
  *    (u32 per record, same order) = df summed over identical terms;
- *    *n_unique = distinct terms this rank owns.
- * 3. caller all-to-alls the answers back (reverse split sizes), all-reduces
- *    {doc_count, sum_ttf}, and tfidf_set_global_df_device imports the answers
- *    (in the record order step 1 produced).
+ *    d_n_unique (device u64, may be NULL) = distinct terms this rank owns.
+ * 3. caller all-to-alls the answers back (reverse split sizes), sums
+ *    {doc_count, sum_ttf} over ranks, and tfidf_set_global_df_device imports
+ *    the answers (in the record order step 1 produced); its host mirror is
+ *    copied in the background and waited for by the next search.
  * Canonical-vocabulary form (sorted union; kept for tools and tests):
  * 1. tfidf_vocab_export_device: this shard's term keys (16 B each, sorted
  *    ascending as (hi, lo)) and local df into caller device buffers.
@@ -187,10 +217,9 @@ int tfidf_term_df(tfidf_index *ix, const uint8_t *term, uint64_t len, uint64_t *
  *    shard's df in canonical order (zero elsewhere).
  * 3. caller all-reduces d_df_canonical and {doc_count, sum_ttf} (RCCL SUM), then
  *    tfidf_set_global_stats_device imports them. */
-int tfidf_vocab_partition_device(tfidf_index *ix, uint32_t n_ranks, void *d_records, uint64_t cap,
-                                 uint64_t *counts, uint64_t *n_out);
-int tfidf_vocab_reduce_device(tfidf_index *ix, const void *d_records, uint64_t n, void *d_df_out,
-                              uint64_t *n_unique);
+int tfidf_vocab_partition_device(tfidf_index *ix, uint32_t n_ranks, void *d_records, uint64_t cap, void *d_counts,
+                                 uint64_t *n_out);
+int tfidf_vocab_reduce_device(tfidf_index *ix, const void *d_records, uint64_t n, void *d_df_out, void *d_n_unique);
 int tfidf_set_global_df_device(tfidf_index *ix, const void *d_df, uint64_t n, uint64_t doc_count,
                                uint64_t sum_ttf);
 int tfidf_vocab_size(const tfidf_index *ix, uint64_t *n);
@@ -217,10 +246,13 @@ int tfidf_analyze(const uint8_t *text, uint64_t len, char *out, uint64_t cap, ui
 
 /* Leader.start merge (Leader.java:73-88): names (concatenated, offsets[n+1])
  * with double scores in worker-response order -> distinct names sorted by
- * String.compareTo with Double::sum totals.  out_first[i] = index of the
- * first occurrence of the i-th distinct name.  n_out = #distinct. */
+ * String.compareTo (UTF-16 code units) with Double::sum totals.  out_first[i]
+ * = index of the first occurrence of the i-th distinct name.  n_out = #distinct. */
 int tfidf_leader_merge(const uint8_t *names, const uint64_t *offsets, uint64_t n, const double *scores,
                        uint64_t *out_first, double *out_sum, uint64_t *n_out);
+/* Stable permutation of n UTF-8 names in String.compareTo (UTF-16) order (the
+ * TreeMap order of Leader.java:80-88; the multi-GPU name table). */
+int tfidf_sort_names(const uint8_t *names, const uint64_t *offsets, uint64_t n, uint64_t *perm);
 
 /* ---- synthetic corpus (bench/test input generator, device side) ----
  * Zipf(s) over V ranks, rank r -> bijective base-26 word of

@@ -14,7 +14,11 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "liboracle.so")
 
-OK, E_ARG, E_UNSUPPORTED, E_NOMEM, E_CAP = 0, -1, -2, -3, -4
+OK, E_ARG, E_UNSUPPORTED, E_NOMEM, E_CAP, E_SYNTAX = 0, -1, -2, -3, -4, -5
+
+
+class QuerySyntaxError(ValueError):
+    """QueryParser ParseException / TooManyClauses (the reference answers [])."""
 
 
 def build():
@@ -112,6 +116,8 @@ def query_terms(q: bytes):
     buf = C.create_string_buffer(len(q) + cap + 16)
     boosts = np.zeros(cap, np.float32)
     n = lib().orc_query_terms(q, len(q), buf, len(buf), _p(boosts, C.c_float), cap)
+    if n == E_SYNTAX:
+        raise QuerySyntaxError("query does not parse")
     if n < 0:
         raise ValueError("query rejected: %d" % n)
     terms = buf.raw.split(b"\0")[:n]
@@ -214,6 +220,8 @@ class OracleIndex:
                               cap, C.byref(n))
         if rc == E_UNSUPPORTED:
             raise ValueError("query rejected (unsupported)")
+        if rc == E_SYNTAX:
+            raise QuerySyntaxError("query does not parse")
         if rc != OK:
             raise RuntimeError("orc_search rc=%d" % rc)
         return list(zip(docs[:n.value].tolist(), scores[:n.value].tolist()))

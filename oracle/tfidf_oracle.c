@@ -695,64 +695,242 @@ int orc_set_global_df(orc_index *ix, const uint8_t *term, uint64_t len, uint64_t
 }
 
 /* ------------------------------------------------------------------ */
-/* Query analysis: QueryParser.escape + classic QueryParser (default OR,
- * splitOnWhitespace) + StandardAnalyzer per chunk.  escape() neutralises
- * every special character except the operator WORDS AND/OR/NOT, which stay
- * operators; those are reported as ORC_E_UNSUPPORTED.  With only escaped
- * characters, the parse is the multiset of analysed tokens (whitespace is a
- * break character for the analyzer as well), de-duplicated by
- * BooleanQuery.rewrite with boost = occurrence count. */
-/* classic QueryParser _WHITESPACE: " " | "\t" | "\n" | "\r" | "\u3000"; length in bytes or 0 */
+/* Query: Worker.searchIndex (Worker.java:225-230) =
+ *   new QueryParser("contents", new StandardAnalyzer()).parse(QueryParser.escape(q))
+ *   searcher.search(query, Integer.MAX_VALUE)
+ * restated from Lucene 9.8.0:
+ *  - QueryParser.escape backslash-escapes  \ + - ! ( ) : ^ [ ] " { } ~ * ? | & /
+ *    so the classic grammar (queryparser/classic/QueryParser.jj) only sees
+ *    whitespace-separated TERM chunks and the operator words AND / OR / NOT:
+ *      Query := Modifiers Clause (Conjunction Modifiers Clause)*
+ *      Conjunction := [AND | OR], Modifiers := [NOT], Clause := TERM
+ *    anything else (empty query, leading AND/OR, trailing or doubled
+ *    operator) is a ParseException, which Worker turns into [] (:182-185);
+ *  - QueryParserBase.addClause, default operator OR: AND marks the previous
+ *    clause MUST unless it is MUST_NOT and the new clause MUST; NOT marks it
+ *    MUST_NOT; else SHOULD.  A chunk the analyzer empties adds no clause;
+ *  - QueryBuilder.createFieldQuery (not quoted, autoGeneratePhraseQueries
+ *    false): one token -> TermQuery, several -> BooleanQuery of SHOULD
+ *    TermQuerys (analyzeMultiBoolean);
+ *  - BooleanQuery.Builder.add: more than IndexSearcher.maxClauseCount (1024)
+ *    clauses in one node -> TooManyClauses (-> ParseException / exception);
+ *  - BooleanQuery.rewrite to its fixpoint: nested clauses rewritten first
+ *    (their duplicate SHOULD terms merged, a one-term result is
+ *    BoostQuery(term, n)); duplicate SHOULD clauses and duplicate MUST
+ *    clauses merged by summing their (unwrapped) boosts in double; nested
+ *    pure disjunctions in SHOULD position flattened [verify: restated, no
+ *    Lucene artefact in this image];
+ *  - scoring (Boolean2ScorerSupplier): no MUST -> SHOULD disjunction
+ *    (float)(double sum); MUST only -> conjunction (float)(double sum of the
+ *    clause scores; a nested clause scores (float)(double sum of its terms));
+ *    MUST + SHOULD -> ReqOptSumScorer: required float + optional float (float
+ *    addition) when a SHOULD matches; MUST_NOT removes documents; no positive
+ *    clause -> no hits.  TermQuery weight = boost * idf (BM25Scorer). */
+#define OQ_SHOULD 0
+#define OQ_MUST 1
+#define OQ_MUST_NOT 2
+#define OQ_MAX_CLAUSES 1024
+
+/* classic QueryParser _WHITESPACE: " " | "\t" | "\n" | "\r" | "　"; length in bytes or 0 */
 static int qp_ws(const uint8_t *q, uint64_t n, uint64_t i) {
   if (q[i] == ' ' || q[i] == '\t' || q[i] == '\n' || q[i] == '\r') return 1;
   if (q[i] == 0xE3 && i + 2 < n && q[i + 1] == 0x80 && q[i + 2] == 0x80) return 3;
   return 0;
 }
 
+typedef struct {
+  int occur;
+  uint32_t t0, nt;      /* distinct tokens: entries [t0, t0 + nt) of the token table */
+  double boost;         /* clause boost after MUST de-duplication */
+  int dead;             /* merged into an earlier identical clause */
+} oq_clause;
+
+typedef struct {
+  strtab toks;                     /* distinct token strings of the whole query */
+  uint32_t *tid; float *tcnt;      /* token table: token id + count inside its clause */
+  uint32_t nt, tcap;
+  oq_clause *cl; uint32_t ncl, clcap;
+} oq_query;
+
+static void oq_free(oq_query *Q) {
+  st_free(&Q->toks); free(Q->tid); free(Q->tcnt); free(Q->cl);
+}
+
+static int oq_push_tok(oq_query *Q, uint32_t id) {
+  if (Q->nt == Q->tcap) {
+    uint32_t nc = Q->tcap ? Q->tcap * 2 : 64;
+    uint32_t *a = (uint32_t *)realloc(Q->tid, nc * 4);
+    if (!a) return ORC_E_NOMEM;
+    Q->tid = a;
+    float *c = (float *)realloc(Q->tcnt, nc * 4);
+    if (!c) return ORC_E_NOMEM;
+    Q->tcnt = c; Q->tcap = nc;
+  }
+  Q->tid[Q->nt] = id; Q->tcnt[Q->nt] = 1.0f; Q->nt++;
+  return ORC_OK;
+}
+
+/* addClause for one TERM chunk [s, s + len) */
+static int oq_add_clause(oq_query *Q, int conj_and, int mod_not, const uint8_t *s, uint64_t len) {
+  if (Q->ncl > 0 && conj_and && Q->cl[Q->ncl - 1].occur != OQ_MUST_NOT) Q->cl[Q->ncl - 1].occur = OQ_MUST;
+  uint64_t cap = len / 2 + 2;
+  uint32_t *st = (uint32_t *)malloc(cap * 4), *ln = (uint32_t *)malloc(cap * 4);
+  uint8_t lb[2048];
+  if (!st || !ln) { free(st); free(ln); return ORC_E_NOMEM; }
+  int64_t nt = orc_tokenize(s, len, 255, st, ln, cap);
+  if (nt < 0) { free(st); free(ln); return ORC_E_UNSUPPORTED; }
+  if (nt == 0) { free(st); free(ln); return ORC_OK; }
+  if (nt > OQ_MAX_CLAUSES) { free(st); free(ln); return ORC_E_SYNTAX; }
+  if (Q->ncl == Q->clcap) {
+    uint32_t nc = Q->clcap ? Q->clcap * 2 : 16;
+    oq_clause *c = (oq_clause *)realloc(Q->cl, nc * sizeof(oq_clause));
+    if (!c) { free(st); free(ln); return ORC_E_NOMEM; }
+    Q->cl = c; Q->clcap = nc;
+  }
+  oq_clause *c = &Q->cl[Q->ncl++];
+  c->occur = mod_not ? OQ_MUST_NOT : (conj_and ? OQ_MUST : OQ_SHOULD);
+  c->t0 = Q->nt; c->nt = 0; c->boost = 1.0; c->dead = 0;
+  for (int64_t t = 0; t < nt; t++) {
+    const uint64_t ll = orc_lower_utf8(s + st[t], ln[t], lb);
+    int64_t id = st_insert(&Q->toks, lb, ll);
+    if (id < 0) { free(st); free(ln); return ORC_E_NOMEM; }
+    uint32_t k = c->t0;
+    while (k < c->t0 + c->nt && Q->tid[k] != (uint32_t)id) k++;
+    if (k < c->t0 + c->nt) { Q->tcnt[k] += 1.0f; continue; }   /* the nested query's SHOULD dedupe */
+    if (oq_push_tok(Q, (uint32_t)id) != ORC_OK) { free(st); free(ln); return ORC_E_NOMEM; }
+    c->nt++;
+  }
+  free(st); free(ln);
+  return ORC_OK;
+}
+
+/* clause equality after rewrite: a one-token clause is its term (its count
+ * is a BoostQuery boost, unwrapped by the dedupe); a nested clause equals a
+ * nested clause with the same (token, count) multiset */
+static int oq_same(const oq_query *Q, const oq_clause *a, const oq_clause *b) {
+  if (a->nt != b->nt) return 0;
+  if (a->nt == 1) return Q->tid[a->t0] == Q->tid[b->t0];
+  for (uint32_t i = 0; i < a->nt; i++) {
+    uint32_t j = 0;
+    while (j < b->nt && Q->tid[b->t0 + j] != Q->tid[a->t0 + i]) j++;
+    if (j == b->nt || Q->tcnt[b->t0 + j] != Q->tcnt[a->t0 + i]) return 0;
+  }
+  return 1;
+}
+
+static int oq_parse(const uint8_t *q, uint64_t n, oq_query *Q) {
+  memset(Q, 0, sizeof *Q);
+  if (st_init(&Q->toks) != ORC_OK) return ORC_E_NOMEM;
+  /* lexer: whitespace-separated chunks, AND / OR / NOT exactly -> operators */
+  enum { K_TERM, K_AND, K_OR, K_NOT };
+  uint64_t m = 0, cap = 16;
+  uint64_t *sa = (uint64_t *)malloc(cap * 8), *sl = (uint64_t *)malloc(cap * 8);
+  int *kd = (int *)malloc(cap * sizeof(int));
+  if (!sa || !sl || !kd) { free(sa); free(sl); free(kd); return ORC_E_NOMEM; }
+  for (uint64_t i = 0; i < n;) {
+    while (i < n && qp_ws(q, n, i)) i += (uint64_t)qp_ws(q, n, i);
+    if (i >= n) break;
+    uint64_t j = i;
+    while (j < n && !qp_ws(q, n, j)) j++;
+    if (m == cap) {
+      cap *= 2;
+      sa = (uint64_t *)realloc(sa, cap * 8); sl = (uint64_t *)realloc(sl, cap * 8);
+      kd = (int *)realloc(kd, cap * sizeof(int));
+      if (!sa || !sl || !kd) return ORC_E_NOMEM;
+    }
+    const uint64_t w = j - i;
+    sa[m] = i; sl[m] = w;
+    kd[m] = (w == 3 && !memcmp(q + i, "AND", 3)) ? K_AND
+          : (w == 2 && !memcmp(q + i, "OR", 2)) ? K_OR
+          : (w == 3 && !memcmp(q + i, "NOT", 3)) ? K_NOT : K_TERM;
+    m++;
+    i = j;
+  }
+  int rc = ORC_OK;
+  uint64_t p = 0;
+  int first = 1;
+  while (rc == ORC_OK && (first || p < m)) {
+    int conj_and = 0, mod_not = 0;
+    if (!first && (kd[p] == K_AND || kd[p] == K_OR)) { conj_and = kd[p] == K_AND; p++; }
+    if (p < m && kd[p] == K_NOT) { mod_not = 1; p++; }
+    if (p >= m || kd[p] != K_TERM) { rc = ORC_E_SYNTAX; break; }
+    rc = oq_add_clause(Q, conj_and, mod_not, q + sa[p], sl[p]);
+    p++;
+    first = 0;
+  }
+  free(sa); free(sl); free(kd);
+  if (rc != ORC_OK) return rc;
+  if (Q->ncl > OQ_MAX_CLAUSES) return ORC_E_SYNTAX;
+  /* MUST de-duplication (boosts summed in double on the first occurrence) */
+  for (uint32_t i = 0; i < Q->ncl; i++) {
+    oq_clause *a = &Q->cl[i];
+    if (a->occur != OQ_MUST || a->dead) continue;
+    a->boost = a->nt == 1 ? (double)Q->tcnt[a->t0] : 1.0;
+    for (uint32_t j = i + 1; j < Q->ncl; j++) {
+      oq_clause *b = &Q->cl[j];
+      if (b->occur == OQ_MUST && !b->dead && oq_same(Q, a, b)) {
+        a->boost += b->nt == 1 ? (double)Q->tcnt[b->t0] : 1.0;
+        b->dead = 1;
+      }
+    }
+  }
+  /* the flattening builder: every distinct SHOULD clause's terms + the other
+   * distinct clauses must fit maxClauseCount */
+  int nested = 0;
+  uint64_t flat = 0;
+  for (uint32_t i = 0; i < Q->ncl; i++) {
+    const oq_clause *a = &Q->cl[i];
+    if (a->dead) continue;
+    int dup = 0;
+    for (uint32_t j = 0; j < i && !dup; j++)
+      dup = Q->cl[j].occur == a->occur && !Q->cl[j].dead && a->occur != OQ_MUST && oq_same(Q, &Q->cl[j], a);
+    if (dup) continue;
+    if (a->occur == OQ_SHOULD) { flat += a->nt; nested |= a->nt > 1; }
+    else flat += 1;
+  }
+  if (nested && flat > OQ_MAX_CLAUSES) return ORC_E_SYNTAX;
+  return ORC_OK;
+}
+
+/* SHOULD terms of the rewritten query: flattened, duplicates merged
+ * (first appearance order), boost = summed count */
+static uint32_t oq_should(const oq_query *Q, uint32_t *ids, double *boost) {
+  uint32_t ns = 0;
+  for (uint32_t i = 0; i < Q->ncl; i++) {
+    const oq_clause *c = &Q->cl[i];
+    if (c->occur != OQ_SHOULD) continue;
+    for (uint32_t k = c->t0; k < c->t0 + c->nt; k++) {
+      uint32_t j = 0;
+      while (j < ns && ids[j] != Q->tid[k]) j++;
+      if (j == ns) { ids[ns] = Q->tid[k]; boost[ns] = 0.0; ns++; }
+      boost[j] += (double)Q->tcnt[k];
+    }
+  }
+  return ns;
+}
+
 int64_t orc_query_terms(const uint8_t *q, uint64_t n, char *buf, uint64_t buf_cap,
                         float *boosts, uint64_t cap) {
-  /* operator words */
-  uint64_t i = 0;
-  while (i < n) {
-    while (i < n && qp_ws(q, n, i)) i += (uint64_t)qp_ws(q, n, i);
-    uint64_t j = i;
-    while (j < n && !qp_ws(q, n, j)) j++;
-    uint64_t w = j - i;
-    if ((w == 3 && (memcmp(q + i, "AND", 3) == 0 || memcmp(q + i, "NOT", 3) == 0)) ||
-        (w == 2 && memcmp(q + i, "OR", 2) == 0))
-      return ORC_E_UNSUPPORTED;
-    i = j;
-  }
-  uint64_t tok_cap = n / 2 + 2;
-  uint32_t *st = (uint32_t *)malloc(tok_cap * 4), *ln = (uint32_t *)malloc(tok_cap * 4);
-  if (!st || !ln) return ORC_E_NOMEM;
-  /* analyse chunk by chunk (restart context at each chunk, as QueryParser does) */
-  strtab qt; st_init(&qt);
-  float *cnt = (float *)calloc(tok_cap + 1, sizeof(float));
-  uint8_t lb[2048];
-  i = 0;
-  while (i < n) {
-    while (i < n && qp_ws(q, n, i)) i += (uint64_t)qp_ws(q, n, i);
-    uint64_t j = i;
-    while (j < n && !qp_ws(q, n, j)) j++;
-    int64_t nt = orc_tokenize(q + i, j - i, 255, st, ln, tok_cap);
-    if (nt < 0) { st_free(&qt); free(cnt); free(st); free(ln); return nt; }
-    for (int64_t t = 0; t < nt; t++) {
-      const uint64_t ll = orc_lower_utf8(q + i + st[t], ln[t], lb);
-      int64_t id = st_insert(&qt, lb, ll);
-      cnt[id] += 1.0f;
-    }
-    i = j;
-  }
+  oq_query Q;
+  int rc = oq_parse(q, n, &Q);
+  if (rc != ORC_OK) { oq_free(&Q); return rc; }
+  uint32_t *ids = (uint32_t *)malloc((Q.nt + 1) * 4);
+  double *bs = (double *)malloc((Q.nt + 1) * 8);
+  if (!ids || !bs) { free(ids); free(bs); oq_free(&Q); return ORC_E_NOMEM; }
+  uint32_t ns = oq_should(&Q, ids, bs);
   uint64_t need = 0;
-  for (uint64_t t = 0; t < qt.n; t++) need += qt.len[t] + 1;
-  int64_t ret = (int64_t)qt.n;
-  if (need > buf_cap || qt.n > cap) ret = ORC_E_CAP;
+  for (uint32_t t = 0; t < ns; t++) need += Q.toks.len[ids[t]] + 1;
+  int64_t ret = (int64_t)ns;
+  if (need > buf_cap || ns > cap) ret = ORC_E_CAP;
   else {
-    memcpy(buf, qt.arena, need);
-    for (uint64_t t = 0; t < qt.n; t++) boosts[t] = cnt[t];
+    uint64_t off = 0;
+    for (uint32_t t = 0; t < ns; t++) {
+      memcpy(buf + off, st_str(&Q.toks, ids[t]), Q.toks.len[ids[t]] + 1);
+      off += Q.toks.len[ids[t]] + 1;
+      boosts[t] = (float)bs[t];
+    }
   }
-  st_free(&qt); free(cnt); free(st); free(ln);
+  free(ids); free(bs); oq_free(&Q);
   return ret;
 }
 
@@ -764,105 +942,204 @@ static int hit_cmp(const void *a, const void *b) {
   return x->doc < y->doc ? -1 : (x->doc > y->doc);
 }
 
+/* BM25 weight of query token id under the statistics in force; returns the
+ * index term id or -1 (absent: TermWeight.scorer == null) */
+static int64_t oq_term(const orc_index *ix, const oq_query *Q, uint32_t id, uint64_t doc_count, float boost,
+                       float *w) {
+  const char *p = st_str(&Q->toks, id);
+  const uint64_t len = Q->toks.len[id];
+  int64_t t = st_find(&ix->terms, (const uint8_t *)p, len);
+  if (t < 0 || doc_count == 0) return -1;
+  uint64_t df = ix->df[t];
+  if (ix->g_doc_count) {
+    int64_t gid = st_find(&ix->g_terms, (const uint8_t *)p, len);
+    df = gid >= 0 ? ix->g_df[gid] : df;
+  }
+  *w = boost * orc_idf(df, doc_count);
+  return t;
+}
+
 int orc_search(const orc_index *ix, const uint8_t *q, uint64_t q_len, uint32_t k,
                uint32_t *docs, float *scores, uint64_t cap, uint64_t *n_out) {
   *n_out = 0;
   if (!ix->committed) return ORC_E_ARG;
-  uint64_t tcap = q_len / 2 + 2;
-  char *tb = (char *)malloc(q_len + tcap + 16);
-  float *boost = (float *)malloc(tcap * sizeof(float));
-  int64_t nq = orc_query_terms(q, q_len, tb, q_len + tcap + 16, boost, tcap);
-  if (nq < 0) { free(tb); free(boost); return (int)nq; }
-  uint64_t N = ix->nlive;
-  uint64_t doc_count = ix->g_doc_count ? ix->g_doc_count : ix->doc_count;
-  uint64_t sum_ttf = ix->g_doc_count ? ix->g_sum_ttf : ix->sum_ttf;
-  double *acc = (double *)calloc(N + 1, sizeof(double));
-  uint8_t *hitm = (uint8_t *)calloc(N + 1, 1);
+  oq_query Q;
+  int rc = oq_parse(q, q_len, &Q);
+  if (rc != ORC_OK) { oq_free(&Q); return rc; }
+  const uint64_t N = ix->nlive;
+  const uint64_t doc_count = ix->g_doc_count ? ix->g_doc_count : ix->doc_count;
+  const uint64_t sum_ttf = ix->g_doc_count ? ix->g_sum_ttf : ix->sum_ttf;
   float cache[256];
   if (doc_count > 0) orc_norm_cache(ix->k1, ix->b, orc_avgdl(sum_ttf, doc_count), cache);
-  const char *p = tb;
-  for (int64_t t = 0; t < nq; t++) {
-    uint64_t len = strlen(p);
-    int64_t id = st_find(&ix->terms, (const uint8_t *)p, len);
-    if (id >= 0 && doc_count > 0) {
-      uint64_t df = ix->df[id];
-      if (ix->g_doc_count) {
-        int64_t gid = st_find(&ix->g_terms, (const uint8_t *)p, len);
-        df = gid >= 0 ? ix->g_df[gid] : df;
-      }
-      float w = boost[t] * orc_idf(df, doc_count);
-      for (uint64_t e = 0; e < ix->plen[id]; e++) {
-        const posting *ps = &ix->plist[id][e];
-        acc[ps->doc] += (double)orc_bm25(w, ps->tf, cache[ix->doc_norm[ps->doc]]);
-        hitm[ps->doc] = 1;
+  double *sacc = (double *)calloc(N + 1, sizeof(double));   /* SHOULD double sum */
+  double *racc = (double *)calloc(N + 1, sizeof(double));   /* MUST: double sum of clause floats */
+  double *cacc = (double *)calloc(N + 1, sizeof(double));   /* current MUST clause */
+  uint8_t *smatch = (uint8_t *)calloc(N + 1, 1), *cmatch = (uint8_t *)calloc(N + 1, 1);
+  uint8_t *excl = (uint8_t *)calloc(N + 1, 1);
+  uint32_t *rcount = (uint32_t *)calloc(N + 1, 4);
+  uint32_t *ids = (uint32_t *)malloc((Q.nt + 1) * 4);
+  double *bs = (double *)malloc((Q.nt + 1) * 8);
+  if (!sacc || !racc || !cacc || !smatch || !cmatch || !excl || !rcount || !ids || !bs) rc = ORC_E_NOMEM;
+  uint32_t n_must = 0, ns = 0;
+  if (rc == ORC_OK) {
+    /* SHOULD (flattened, merged) */
+    ns = oq_should(&Q, ids, bs);
+    for (uint32_t s = 0; s < ns; s++) {
+      float w;
+      int64_t t = oq_term(ix, &Q, ids[s], doc_count, (float)bs[s], &w);
+      if (t < 0) continue;
+      for (uint64_t e = 0; e < ix->plen[t]; e++) {
+        const posting *ps = &ix->plist[t][e];
+        sacc[ps->doc] += (double)orc_bm25(w, ps->tf, cache[ix->doc_norm[ps->doc]]);
+        smatch[ps->doc] = 1;
       }
     }
-    p += len + 1;
+    /* MUST clauses, in order: clause score, then the conjunction's double sum */
+    for (uint32_t c = 0; c < Q.ncl; c++) {
+      const oq_clause *cl = &Q.cl[c];
+      if (cl->occur != OQ_MUST || cl->dead) continue;
+      n_must++;
+      memset(cmatch, 0, N + 1);
+      const float cb = (float)cl->boost;
+      for (uint32_t i = cl->t0; i < cl->t0 + cl->nt; i++) {
+        float tb = cl->nt == 1 ? cb : cb * Q.tcnt[i];
+        float w;
+        int64_t t = oq_term(ix, &Q, Q.tid[i], doc_count, tb, &w);
+        if (t < 0) continue;
+        for (uint64_t e = 0; e < ix->plen[t]; e++) {
+          const posting *ps = &ix->plist[t][e];
+          const double sc = (double)orc_bm25(w, ps->tf, cache[ix->doc_norm[ps->doc]]);
+          cacc[ps->doc] = cmatch[ps->doc] ? cacc[ps->doc] + sc : sc;
+          cmatch[ps->doc] = 1;
+        }
+      }
+      for (uint64_t d = 0; d < N; d++)
+        if (cmatch[d]) { racc[d] += (double)(float)cacc[d]; rcount[d]++; }
+    }
+    /* MUST_NOT */
+    for (uint32_t c = 0; c < Q.ncl; c++) {
+      const oq_clause *cl = &Q.cl[c];
+      if (cl->occur != OQ_MUST_NOT) continue;
+      for (uint32_t i = cl->t0; i < cl->t0 + cl->nt; i++) {
+        float w;
+        int64_t t = oq_term(ix, &Q, Q.tid[i], doc_count, 1.0f, &w);
+        if (t < 0) continue;
+        for (uint64_t e = 0; e < ix->plen[t]; e++) excl[ix->plist[t][e].doc] = 1;
+      }
+    }
   }
+  hit *h = rc == ORC_OK ? (hit *)malloc((N + 1) * sizeof(hit)) : NULL;
+  if (rc == ORC_OK && !h) rc = ORC_E_NOMEM;
   uint64_t nh = 0;
-  for (uint64_t d = 0; d < N; d++) nh += hitm[d];
-  hit *h = (hit *)malloc((nh + 1) * sizeof(hit));
-  uint64_t j = 0;
-  for (uint64_t d = 0; d < N; d++)
-    if (hitm[d]) { h[j].score = (float)acc[d]; h[j].doc = (uint32_t)d; j++; }
-  qsort(h, nh, sizeof(hit), hit_cmp);
-  uint64_t out = (k == 0 || k > nh) ? nh : k;
-  int rc = ORC_OK;
-  *n_out = out;
-  if (out > cap) rc = ORC_E_CAP;
-  else
-    for (uint64_t i = 0; i < out; i++) { docs[i] = h[i].doc; scores[i] = h[i].score; }
-  free(h); free(acc); free(hitm); free(tb); free(boost);
+  if (rc == ORC_OK) {
+    for (uint64_t d = 0; d < N; d++) {
+      if (excl[d]) continue;
+      float sc;
+      if (n_must) {
+        if (rcount[d] != n_must) continue;
+        const float req = (float)racc[d];
+        if (smatch[d]) { const float opt = (float)sacc[d]; sc = req + opt; }
+        else sc = req;
+      } else {
+        if (!smatch[d]) continue;
+        sc = (float)sacc[d];
+      }
+      h[nh].score = sc; h[nh].doc = (uint32_t)d; nh++;
+    }
+    qsort(h, nh, sizeof(hit), hit_cmp);
+    uint64_t out = (k == 0 || k > nh) ? nh : k;
+    *n_out = out;
+    if (out > cap) rc = ORC_E_CAP;
+    else
+      for (uint64_t i = 0; i < out; i++) { docs[i] = h[i].doc; scores[i] = h[i].score; }
+  }
+  free(h); free(sacc); free(racc); free(cacc); free(smatch); free(cmatch); free(excl); free(rcount);
+  free(ids); free(bs); oq_free(&Q);
   return rc;
 }
 
 /* ------------------------------------------------------------------ */
-static const uint8_t *g_names;
-static const uint64_t *g_offs;
+/* Leader.start merge (Leader.java:73-88): HashMap.merge(name, score,
+ * Double::sum) in response order, then TreeMap<String, Double> order =
+ * String.compareTo = lexicographic over UTF-16 code units.  Each name is
+ * transcoded UTF-8 -> UTF-16 (surrogate pairs for code points >= 0x10000;
+ * an invalid byte maps to the unit 0xFFFD + byte, keeping distinct names
+ * distinct) and the unit arrays are compared. */
+typedef struct { uint16_t *u; uint64_t n; } u16name;
+
+static u16name to_utf16(const uint8_t *s, uint64_t n) {
+  u16name r;
+  r.u = (uint16_t *)malloc((2 * n + 1) * sizeof(uint16_t));
+  r.n = 0;
+  uint64_t i = 0;
+  while (i < n) {
+    uint8_t c = s[i];
+    uint32_t len = c < 0x80 ? 1 : (c & 0xE0) == 0xC0 ? 2 : (c & 0xF0) == 0xE0 ? 3 : (c & 0xF8) == 0xF0 ? 4 : 0;
+    uint32_t cp = 0, ok = len && i + len <= n;
+    if (ok) {
+      cp = len == 1 ? c : (uint32_t)(c & (0x7F >> len));
+      for (uint32_t k = 1; k < len; k++) {
+        if ((s[i + k] & 0xC0) != 0x80) { ok = 0; break; }
+        cp = (cp << 6) | (s[i + k] & 0x3F);
+      }
+    }
+    if (!ok) { r.u[r.n++] = 0xFFFD; r.u[r.n++] = c; i++; continue; }
+    if (cp >= 0x10000) {
+      cp -= 0x10000;
+      r.u[r.n++] = (uint16_t)(0xD800 + (cp >> 10));
+      r.u[r.n++] = (uint16_t)(0xDC00 + (cp & 0x3FF));
+    } else {
+      r.u[r.n++] = (uint16_t)cp;
+    }
+    i += len;
+  }
+  return r;
+}
+
+static int u16_cmp(const u16name *x, const u16name *y) {
+  uint64_t m = x->n < y->n ? x->n : y->n;
+  for (uint64_t i = 0; i < m; i++)
+    if (x->u[i] != y->u[i]) return x->u[i] < y->u[i] ? -1 : 1;
+  return x->n == y->n ? 0 : (x->n < y->n ? -1 : 1);
+}
+
+static const u16name *g_u16;
 static int name_cmp_idx(const void *a, const void *b) {
   uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
-  uint64_t lx = g_offs[x + 1] - g_offs[x], ly = g_offs[y + 1] - g_offs[y];
-  uint64_t m = lx < ly ? lx : ly;
-  int c = memcmp(g_names + g_offs[x], g_names + g_offs[y], m);
+  int c = u16_cmp(&g_u16[x], &g_u16[y]);
   if (c) return c;
-  if (lx != ly) return lx < ly ? -1 : 1;
   return x < y ? -1 : (x > y);                   /* stable: first occurrence first */
 }
 
 int64_t orc_leader_merge(const uint8_t *names, const uint64_t *offsets, uint64_t n,
                          const double *scores, uint64_t *out_first, double *out_sum) {
   uint64_t *idx = (uint64_t *)malloc((n + 1) * sizeof(uint64_t));
-  if (!idx) return ORC_E_NOMEM;
-  for (uint64_t i = 0; i < n; i++) idx[i] = i;
-  g_names = names; g_offs = offsets;
+  u16name *u = (u16name *)malloc((n + 1) * sizeof(u16name));
+  if (!idx || !u) { free(idx); free(u); return ORC_E_NOMEM; }
+  for (uint64_t i = 0; i < n; i++) {
+    idx[i] = i;
+    u[i] = to_utf16(names + offsets[i], offsets[i + 1] - offsets[i]);
+  }
+  g_u16 = u;
   qsort(idx, n, sizeof(uint64_t), name_cmp_idx);
   int64_t m = -1;
   uint64_t prev = 0;
   for (uint64_t r = 0; r < n; r++) {
     uint64_t i = idx[r];
-    int same = 0;
-    if (m >= 0) {
-      uint64_t lp = offsets[prev + 1] - offsets[prev], li = offsets[i + 1] - offsets[i];
-      same = lp == li && memcmp(names + offsets[prev], names + offsets[i], li) == 0;
-    }
-    if (!same) { m++; out_first[m] = i; out_sum[m] = 0.0; prev = i; }
+    if (m < 0 || u16_cmp(&u[prev], &u[i]) != 0) { m++; out_first[m] = i; prev = i; }
   }
   /* Double::sum in response order (HashMap.merge is applied in list order) */
   for (uint64_t r = 0; r <= (uint64_t)m && m >= 0; r++) out_sum[r] = 0.0;
   for (uint64_t i = 0; i < n; i++) {
-    /* binary search distinct index for name i */
     int64_t lo = 0, hi = m;
     while (lo <= hi) {
       int64_t mid = (lo + hi) / 2;
-      uint64_t f = out_first[mid];
-      uint64_t lf = offsets[f + 1] - offsets[f], li = offsets[i + 1] - offsets[i];
-      uint64_t mm = lf < li ? lf : li;
-      int c = memcmp(names + offsets[f], names + offsets[i], mm);
-      if (!c) c = lf == li ? 0 : (lf < li ? -1 : 1);
+      int c = u16_cmp(&u[out_first[mid]], &u[i]);
       if (c == 0) { out_sum[mid] += scores[i]; break; }
       if (c < 0) lo = mid + 1; else hi = mid - 1;
     }
   }
-  free(idx);
+  for (uint64_t i = 0; i < n; i++) free(u[i].u);
+  free(u); free(idx);
   return m + 1;
 }

@@ -30,9 +30,10 @@ extern "C" {
 
 #define ORC_OK 0
 #define ORC_E_ARG (-1)
-#define ORC_E_UNSUPPORTED (-2) /* malformed UTF-8, or AND/OR/NOT operator word */
+#define ORC_E_UNSUPPORTED (-2) /* malformed UTF-8 */
 #define ORC_E_NOMEM (-3)
 #define ORC_E_CAP (-4)         /* caller buffer too small; *n_out = needed */
+#define ORC_E_SYNTAX (-5)      /* QueryParser ParseException / TooManyClauses (Worker answers []) */
 
 /* StandardTokenizer (UAX#29 JFlex grammar of Lucene 9.8).
  * Writes token start offsets / lengths (into the ORIGINAL bytes; lower-case
@@ -84,14 +85,16 @@ int64_t orc_vocab(const orc_index *ix, char *buf, uint64_t buf_cap, uint32_t *df
 int orc_set_global_stats(orc_index *ix, uint64_t doc_count, uint64_t sum_ttf);
 int orc_set_global_df(orc_index *ix, const uint8_t *term, uint64_t len, uint64_t df);
 
-/* Worker.searchIndex: parse(escape(q)) -> BM25 disjunction -> hits ordered
- * (score desc, doc asc).  k == 0 returns all hits (searcher.search(q, MAX)).
- * Returns ORC_OK / ORC_E_UNSUPPORTED / ORC_E_CAP (n_out = needed). */
+/* Worker.searchIndex: parse(escape(q)) (operator words AND / OR / NOT kept)
+ * -> rewritten BooleanQuery -> BM25 scores -> hits ordered (score desc, doc
+ * asc).  k == 0 returns all hits (searcher.search(q, MAX)).  Returns ORC_OK /
+ * ORC_E_UNSUPPORTED / ORC_E_SYNTAX / ORC_E_CAP (n_out = needed). */
 int orc_search(const orc_index *ix, const uint8_t *q, uint64_t q_len, uint32_t k,
                uint32_t *docs, float *scores, uint64_t cap, uint64_t *n_out);
 
-/* Query analysis used by orc_search: distinct terms (first appearance order)
- * NUL-separated + boost (occurrence count).  Returns #terms or error. */
+/* SHOULD terms of the parsed + rewritten query (nested disjunctions
+ * flattened, duplicates merged, first appearance order) NUL-separated + boost
+ * (occurrence count).  Returns #terms or error. */
 int64_t orc_query_terms(const uint8_t *q, uint64_t q_len, char *buf, uint64_t buf_cap,
                         float *boosts, uint64_t cap);
 
@@ -102,8 +105,8 @@ void orc_norm_cache(float k1, float b, float avgdl, float cache[256]);
 float orc_bm25(float weight, uint32_t tf, float norm_inverse);
 
 /* Leader.start merge: names (concatenated, offsets[n+1]) with double scores in
- * worker-response order -> distinct names sorted by String.compareTo (ASCII
- * byte order) with Double::sum totals.  Output: index of first occurrence of
+ * worker-response order -> distinct names sorted by String.compareTo (UTF-16
+ * code units) with Double::sum totals.  Output: index of first occurrence of
  * each distinct name in sorted order + sums.  Returns #distinct. */
 int64_t orc_leader_merge(const uint8_t *names, const uint64_t *offsets, uint64_t n,
                          const double *scores, uint64_t *out_first, double *out_sum);

@@ -15,7 +15,12 @@ properties that do not depend on an oracle index of the whole corpus:
   Appendix A.3) with the engine's df / docCount / sumTTF and the hit's TF row
   and norm — bit-exact as float32;
 * ranking: an all-hits query returns exactly df(t) hits for one term, ordered
-  (score desc, doc asc); top-k is that order's prefix; batched = single.
+  (score desc, doc asc); top-k is that order's prefix; batched = single;
+* document frequencies of the WHOLE vocabulary against an independent count:
+  the host copy of the corpus is re-tokenised with plain torch tensor ops on
+  the device (word spans between separator bytes, little-endian byte keys,
+  unique (term, doc) pairs) — none of the engine's kernels — and every term's
+  df, the vocabulary size and sumDocFreq must equal the engine's.
 """
 import numpy as np
 import pytest
@@ -54,8 +59,76 @@ def expected_score(g, st, q_terms, d, cache):
     return float(np.float32(acc))
 
 
+def independent_df(dc, n):
+    """{term key lo: df} of the synthetic corpus (lower-case ASCII words of
+    <= 8 bytes separated by ' ' / '\\n'), counted with torch ops on cuda:0."""
+    import torch
+    text, offs = dc.to_host(n)
+    t = torch.from_numpy(text).cuda()
+    del text
+    o = torch.from_numpy(offs.astype(np.int64)).cuda()
+    sep = (t == 32) | (t == 10)
+    assert bool(((t >= 97) & (t <= 122) | sep).all())          # the generator's alphabet
+    # word starts / ends in 1 GiB chunks (torch.nonzero sizes in 32 bits)
+    st, en = [], []
+    n_b = t.numel()
+    for a in range(0, n_b, 1 << 30):
+        b = min(n_b, a + (1 << 30))
+        word = ~sep[a:b]
+        prev = torch.ones_like(word)
+        prev[1:] = sep[a:b - 1]
+        if a:
+            prev[0] = sep[a - 1]
+        st.append(torch.nonzero(word & prev).squeeze(1) + a)
+        nxt = torch.ones_like(word)
+        nxt[:-1] = sep[a + 1:b]
+        if b < n_b:
+            nxt[-1] = sep[b]
+        en.append(torch.nonzero(word & nxt).squeeze(1) + a)
+        del word, prev, nxt
+    starts, ends = torch.cat(st), torch.cat(en)
+    del st, en, sep
+    ln = ends - starts + 1
+    del ends
+    assert int(ln.max()) <= 8
+    key = torch.zeros_like(starts)
+    for j in range(int(ln.max())):
+        b = t[(starts + j).clamp(max=t.numel() - 1)].to(torch.int64)
+        key |= torch.where(ln > j, b, torch.zeros_like(b)) << (8 * j)
+    del ln, t
+    doc = torch.searchsorted(o[1:].contiguous(), starts, right=True)
+    del starts
+    bits = max(1, (n - 1).bit_length())
+    assert int(key.max()).bit_length() + bits <= 63
+    pairs = torch.unique((key << bits) | doc)
+    del key, doc
+    terms, df = torch.unique_consecutive(pairs >> bits, return_counts=True)
+    out = dict(zip(terms.cpu().numpy().tolist(), df.cpu().numpy().tolist()))
+    del pairs, terms, df
+    torch.cuda.empty_cache()
+    return out
+
+
+def engine_df(g):
+    """{term key lo: df} exported from the engine (tfidf_vocab_export_device)."""
+    import torch
+    n = g.vocab_size()
+    keys = torch.zeros((n, 2), dtype=torch.int64, device="cuda:0")
+    df = torch.zeros(n, dtype=torch.int32, device="cuda:0")
+    torch.cuda.synchronize()
+    assert g.vocab_export_device(keys.data_ptr(), df.data_ptr(), n) == n
+    k = keys.cpu().numpy().view(np.uint64)
+    assert (k[:, 1] == np.uint64(1 << 63)).all()                # <= 8-byte exact keys
+    return dict(zip(k[:, 0].tolist(), df.cpu().numpy().tolist()))
+
+
 def check_corpus(g, dc, n, len_min, len_max, queries, rng):
     st = g.stats()
+    want_df = independent_df(dc, n)
+    got_df = engine_df(g)
+    assert len(got_df) == len(want_df) == st["num_terms"]
+    assert got_df == want_df
+    assert sum(want_df.values()) == st["nnz"]
     lens = doc_lengths(n, len_min, len_max)
     assert st["num_docs"] == n and st["doc_count"] == n
     assert st["sum_ttf"] == int(lens.sum())

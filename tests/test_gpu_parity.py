@@ -15,7 +15,7 @@ import pytest
 from oracle import oracle as O
 from tfidf_amd import synth
 from tfidf_amd.engine import ShardIndex
-from tfidf_amd._lib import UnsupportedInput, UnsupportedQuery
+from tfidf_amd._lib import QuerySyntaxError, UnsupportedInput
 
 pytestmark = pytest.mark.gpu
 
@@ -91,7 +91,7 @@ def test_fixture_tf_df_norms(fx):
 
 
 @pytest.mark.parametrize("q", [b"fast food", b"cat", b"best wireless earbuds", b"kheder", b"at night",
-                               b"fast fast food", b"FAST Food!", b"2024 helo", b"nothing here", b"",
+                               b"fast fast food", b"FAST Food!", b"2024 helo", b"nothing here",
                                b"+fast -(food)", b"e-mail kheder:helo"])
 def test_fixture_search_all_hits(fx, q):
     g, o, _ = fx
@@ -105,10 +105,12 @@ def test_fixture_search_topk(fx, k):
         assert_hits_equal(g.search(q, k=k), o.search(q, k=k))
 
 
-def test_operator_words_rejected(fx):
-    g, _, _ = fx
-    with pytest.raises(UnsupportedQuery):
-        g.search(b"fast AND food")
+def test_operator_words_are_operators(fx):
+    # the operator-word parity suite is tests/test_gpu_operators.py
+    g, o, _ = fx
+    assert_hits_equal(g.search(b"fast AND food", 0), o.search(b"fast AND food", 0))
+    with pytest.raises(QuerySyntaxError):
+        g.search(b"")
 
 
 def test_reference_worker_and_leader(tmp_path, lucene_fixture):
@@ -127,7 +129,10 @@ def test_reference_worker_and_leader(tmp_path, lucene_fixture):
         got = w.process_documents(q)
         want = [{"document": {"name": o.doc_key(d).decode()}, "score": s} for d, s in o.search(q.encode())]
         assert got == want
-    assert w.process_documents("fast AND food") == []          # Worker.java:182-185
+    got = w.process_documents("fast AND NOT best")              # operator words stay operators
+    assert got == [{"document": {"name": o.doc_key(d).decode()}, "score": s}
+                   for d, s in o.search(b"fast AND NOT best")] and got
+    assert w.process_documents("fast AND") == []                # ParseException: Worker.java:182-185
     out = Leader([w]).start("fast food")
     assert list(out) == sorted(out)                              # TreeMap order
     assert list(out) == ["file.txt", "file3.txt", "file5.txt", "file6.txt", "file7.txt", "file8.txt"]
@@ -402,8 +407,11 @@ def test_global_stats_term_ownership_three_shards():
         s.commit()
         n = s.vocab_size()
         rec = torch.zeros((n, 3), dtype=torch.int64, device=dev)
+        cnt = torch.zeros(G, dtype=torch.int64, device=dev)
         torch.cuda.synchronize()
-        n2, c = s.vocab_partition_device(G, rec.data_ptr(), n)
+        n2 = s.vocab_partition_device(G, rec.data_ptr(), n, cnt.data_ptr())
+        s.set_stream(None)                            # (asynchronous: finish the index's stream)
+        c = cnt.cpu()
         assert n2 == n and int(c.sum()) == n
         shards.append(s)
         recs.append(rec)
@@ -415,8 +423,11 @@ def test_global_stats_term_ownership_three_shards():
         parts = [recs[r][starts[r][o]:starts[r][o] + counts[r][o]] for r in range(G)]
         recv = torch.cat(parts).contiguous()
         out = torch.zeros(max(recv.shape[0], 1), dtype=torch.int32, device=dev)
+        nu = torch.zeros(1, dtype=torch.int64, device=dev)
         torch.cuda.synchronize()
-        n_unique += shards[o].vocab_reduce_device(recv.data_ptr(), recv.shape[0], out.data_ptr())
+        shards[o].vocab_reduce_device(recv.data_ptr(), recv.shape[0], out.data_ptr(), nu.data_ptr())
+        shards[o].set_stream(None)
+        n_unique += int(nu.item())
         at = 0
         for r in range(G):
             answers[r][o] = out[at:at + counts[r][o]]
@@ -427,6 +438,7 @@ def test_global_stats_term_ownership_three_shards():
         back = torch.cat(answers[r]).contiguous()
         torch.cuda.synchronize()
         shards[r].set_global_df_device(back.data_ptr(), back.shape[0], dc, ttf)
+        shards[r].set_stream(None)
     o = O.OracleIndex()
     for i, t in enumerate(texts):
         o.add_doc(str(i).encode(), t)

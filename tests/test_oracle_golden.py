@@ -136,20 +136,28 @@ def _np_bm25_scores(ix, terms_boosts):
 
 
 @pytest.mark.parametrize("q", [b"fast food", b"fast fast food", b"kheder helo 2024", b"night at night",
-                               b"wireless best earbuds cat", b"zzz", b""])
+                               b"wireless best earbuds cat", b"zzz"])
 def test_bm25_numpy_restatement(ix, q):
-    want = _np_bm25_scores(ix, O.query_terms(q)) if q.strip() else []
+    want = _np_bm25_scores(ix, O.query_terms(q))
     assert ix.search(q) == want
+
+
+def test_empty_query_is_parse_exception(ix):
+    # QueryParser.parse("") throws ParseException (Encountered <EOF>); Worker answers []
+    for q in (b"", b"  \t "):
+        with pytest.raises(O.QuerySyntaxError):
+            ix.search(q)
 
 
 def test_duplicate_query_terms_boost():
     assert O.query_terms(b"fast Fast food fast") == [(b"fast", 3.0), (b"food", 1.0)]
 
 
-@pytest.mark.parametrize("q", [b"fast AND food", b"NOT cat", b"a OR b"])
-def test_operator_words_rejected(ix, q):
-    with pytest.raises(ValueError):
-        ix.search(q)
+def test_operator_words_parse(ix):
+    # escape() leaves AND / OR / NOT: they stay operators (tests/test_query_operators.py)
+    assert {d for d, _ in ix.search(b"fast AND food")} == {d for d, _ in ix.search(b"fast")}
+    assert ix.search(b"NOT cat") == []
+    assert ix.search(b"cat OR night") == ix.search(b"cat night")
 
 
 def test_escaped_specials_are_plain_text(ix):

@@ -121,8 +121,16 @@ __device__ __forceinline__ void term_block_range(const QueryParams &p, uint32_t 
 
 constexpr uint32_t kQTermsFast = 4;   // query terms whose ranges / first chunk are prefetched
 
-struct ScoreSmem {
+// kOps: queries with MUST / MUST_NOT clauses (QueryParser operator words,
+// analysis.h).  Per document: acc = the current MUST clause's double sum, then
+// the SHOULD double sum; req = double sum of the MUST clauses' float scores;
+// bitmaps of the current clause, of every MUST clause so far and of MUST_NOT.
+template <bool kOps> struct ScoreSmem {
   double acc[kBlockDocs];
+  double req[kOps ? kBlockDocs : 1];
+  uint32_t grpbits[kOps ? kBlockDocs / 32 : 1];
+  uint32_t reqbits[kOps ? kBlockDocs / 32 : 1];
+  uint32_t notbits[kOps ? kBlockDocs / 32 : 1];
   uint64_t tlo[kQTermsFast], thi[kQTermsFast];     // absolute posting ranges of the block's segments
   uint64_t xlo, xhi;                               // range of a query term beyond the first kQTermsFast
   float tw[kQTermsFast];
@@ -136,9 +144,18 @@ struct ScoreSmem {
 // Hits are enumerated from the bitmap: thread t owns docs [16 t, 16 t + 16)
 // (ascending doc order for ties).  The per-query set-up is a 1 KiB bitmap
 // clear, so a chunk of queries amortises the workgroup launch, and the LDS
-// footprint (66 KiB) admits two workgroups per CU.
+// footprint (66 KiB) admits two workgroups per CU (kOps: 134 KiB, one).
+//
+// Operator queries (kOps) follow Lucene 9.8.0's scorer shapes for the
+// rewritten BooleanQuery (Boolean2ScorerSupplier): a MUST clause's score is
+// its float score ((float) double sum for a nested disjunction); the required
+// part is (float) of the double sum of the MUST clauses (ConjunctionScorer /
+// BlockMaxConjunctionScorer); SHOULD terms add (float) of their double sum in
+// float (ReqOptSumScorer) when one matches; MUST_NOT excludes (ReqExclScorer).
+// Without MUST clauses a document needs a SHOULD match: the plain disjunction.
+template <bool kOps>
 __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
-  __shared__ ScoreSmem sm;
+  __shared__ ScoreSmem<kOps> sm;
   const uint32_t tid = threadIdx.x;
   const uint32_t q0 = blockIdx.y * p.q_chunk;
   const uint32_t q1 = min(p.n_q, q0 + p.q_chunk);
@@ -164,11 +181,16 @@ __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
     const uint64_t bb = p.toff ? 0 : p.bbase[b];
     const uint64_t bend = p.toff ? 0 : p.bbase[b + 1];
     const uint32_t *row = p.toff ? nullptr : p.blk + (size_t)b * p.C;
-    for (uint32_t i = tid; i < kBlockDocs / 32; i += blockDim.x) sm.hitbits[i] = 0;
+    for (uint32_t i = tid; i < kBlockDocs / 32; i += blockDim.x) {
+      sm.hitbits[i] = 0;
+      if (kOps) { sm.grpbits[i] = 0; sm.reqbits[i] = 0; sm.notbits[i] = 0; }
+    }
     for (uint32_t i = tid; i < 256; i += blockDim.x) sm.hist[i] = 0;
     if (tid == 0) { sm.nhit = 0; sm.outn = 0; sm.smin = 0xFFFFFFFFu; sm.smax = 0; }
     __syncthreads();
     const uint32_t t0 = p.q_off[q], t1 = p.q_off[q + 1];
+    const uint32_t ngroups = kOps ? (p.q_meta[q] & 0xFFFFu) : 0u;
+    bool alive = true;                                     // kOps: a document still meets every MUST clause
     if (p.toff) {
       // term-major layout: wave j finds term j's segment for this block in the
       // term's doc-sorted list (two 64-ary searches)
@@ -201,7 +223,9 @@ __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
     }
     uint32_t my_new = 0;
     for (uint32_t j = t0; j < t1; j++) {
+      if (kOps && !alive) break;                           // uniform: no document can match any more
       const uint32_t jj = j - t0;
+      const uint32_t role = kOps ? p.q_role[j] >> 24 : kRoleShould;
       uint64_t lo, hi;
       float w;
       if (jj < kQTermsFast) {
@@ -210,9 +234,10 @@ __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
         w = sm.tw[jj];
       } else {
         const uint32_t slot = p.q_slot[j];
-        if (slot == kInvalidSlot) continue;               // uniform
         w = p.q_w[j];
-        if (p.toff) {
+        if (slot == kInvalidSlot) {                        // uniform
+          lo = hi = 0;
+        } else if (p.toff) {
           if (tid < 64) {
             uint64_t a, z;
             term_block_range(p, slot, (uint32_t)d0, &a, &z);
@@ -236,10 +261,15 @@ __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
           e = p.post[i];
         }
         const uint32_t ld = (uint32_t)(e & 0xFFFFFFFFu) - (uint32_t)d0;
+        const uint32_t bit = 1u << (ld & 31);
+        if (kOps && role == kRoleNot) {
+          atomicOr(&sm.notbits[ld >> 5], bit);
+          continue;
+        }
         const uint32_t tfn = (uint32_t)(e >> 32);
         const float sc = bm25_term(w, tfn >> 8, sm.cache[tfn & 255u]);
-        const uint32_t bit = 1u << (ld & 31);
-        const uint32_t old = atomicOr(&sm.hitbits[ld >> 5], bit);
+        uint32_t *bm = (kOps && role == kRoleMust) ? sm.grpbits : sm.hitbits;
+        const uint32_t old = atomicOr(&bm[ld >> 5], bit);
         if (old & bit) {
           sm.acc[ld] += (double)sc;
         } else {
@@ -248,21 +278,86 @@ __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
         }
       }
       __syncthreads();                                     // term order = the disjunction's sum order
+      if (kOps && role == kRoleMust && (j + 1 == t1 || p.q_role[j + 1] != p.q_role[j])) {
+        // end of MUST clause g: fold its float score into req for the documents
+        // that met every MUST clause so far (one 32-doc word per thread)
+        const uint32_t g = p.q_role[j] & 0xFFFFFFu;
+        uint32_t rb = 0;
+        if (tid < kBlockDocs / 32) {
+          const uint32_t gb = sm.grpbits[tid];
+          rb = g == 0 ? gb : (sm.reqbits[tid] & gb);
+          for (uint32_t x = rb; x; x &= x - 1) {
+            const uint32_t ld = tid * 32 + (__ffs(x) - 1);
+            const double cs = (double)(float)sm.acc[ld];
+            sm.req[ld] = g == 0 ? cs : sm.req[ld] + cs;
+          }
+          sm.reqbits[tid] = rb;
+          sm.grpbits[tid] = 0;
+        }
+        alive = __syncthreads_or(rb != 0) != 0;
+      }
     }
-    if (my_new) atomicAdd(&sm.nhit, my_new);
+    if (kOps) {
+      // final match set and score per document: required part, plus the
+      // SHOULD part in float when one matched; MUST_NOT documents dropped
+      uint32_t cnt = 0;
+      if (tid < kBlockDocs / 32) {
+        const uint32_t sb = sm.hitbits[tid];
+        const uint32_t mb = (ngroups ? (alive ? sm.reqbits[tid] : 0u) : sb) & ~sm.notbits[tid];
+        for (uint32_t x = mb; x; x &= x - 1) {
+          const uint32_t b = __ffs(x) - 1, ld = tid * 32 + b;
+          float sc;
+          if (ngroups) {
+            const float r = (float)sm.req[ld];
+            sc = (sb >> b) & 1u ? r + (float)sm.acc[ld] : r;
+          } else {
+            sc = (float)sm.acc[ld];
+          }
+          sm.acc[ld] = (double)sc;
+        }
+        sm.hitbits[tid] = mb;
+        cnt = (uint32_t)__popc(mb);
+      }
+      if (cnt) atomicAdd(&sm.nhit, cnt);
+    } else if (my_new) {
+      atomicAdd(&sm.nhit, my_new);
+    }
     __syncthreads();
     const uint32_t nhit = sm.nhit;
     const uint32_t bits = (sm.hitbits[tid >> 1] >> (16 * (tid & 1))) & 0xFFFFu;
     if (k == 0) {
-      // all-hits mode (single query): every hit key of the block
-      uint32_t tot;
-      uint32_t at = block_excl_scan((uint32_t)__popc(bits), sm.scan, &tot);
-      for (uint32_t x = bits; x; x &= x - 1) {
-        const uint32_t ld = tid * kDocsPerThread + (__ffs(x) - 1);
-        const float sc = (float)sm.acc[ld];
-        p.hits[(size_t)b * kBlockDocs + at++] =
-            ((uint64_t)__float_as_uint(sc) << 32) | (uint64_t)(~(uint32_t)(d0 + ld));
+      // all-hits mode (single query): the block's hit keys (score bits << 32 |
+      // ~doc), compacted and sorted descending in LDS (bitonic over the
+      // accumulator's 64 KiB) -> one sorted run per block for k_merge_runs
+      uint64_t kv[kDocsPerThread];
+#pragma unroll
+      for (uint32_t i = 0; i < kDocsPerThread; i++) {
+        const uint32_t ld = tid * kDocsPerThread + i;
+        kv[i] = ((bits >> i) & 1u)
+                    ? ((uint64_t)__float_as_uint((float)sm.acc[ld]) << 32) | (uint64_t)(~(uint32_t)(d0 + ld))
+                    : 0ull;
       }
+      uint32_t tot;
+      uint32_t at = block_excl_scan((uint32_t)__popc(bits), sm.scan, &tot);   // barriers: reads of acc done
+      uint64_t *keys = reinterpret_cast<uint64_t *>(sm.acc);
+#pragma unroll
+      for (uint32_t i = 0; i < kDocsPerThread; i++)
+        if ((bits >> i) & 1u) keys[at++] = kv[i];
+      uint32_t P = 2;
+      while (P < nhit) P <<= 1;
+      for (uint32_t i = nhit + tid; i < P; i += blockDim.x) keys[i] = 0ull;
+      __syncthreads();
+      for (uint32_t size = 2; size <= P; size <<= 1) {
+        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+          for (uint32_t i = tid; i < P / 2; i += blockDim.x) {
+            const uint32_t lo = 2 * i - (i & (stride - 1)), hi = lo + stride;
+            const uint64_t a = keys[lo], c = keys[hi];
+            if ((lo & size) == 0 ? a < c : a > c) { keys[lo] = c; keys[hi] = a; }
+          }
+          __syncthreads();
+        }
+      }
+      for (uint32_t i = tid; i < nhit; i += blockDim.x) p.hits[(size_t)b * kBlockDocs + i] = keys[i];
       if (tid == 0) p.hits_n[b] = nhit;
       __syncthreads();
       continue;
@@ -538,6 +633,10 @@ __global__ void __launch_bounds__(kPairWaves * 64) k_score_pairs(QueryParams p) 
     const uint32_t q = (uint32_t)(pr / nb), b = (uint32_t)(pr - (uint64_t)q * nb);
     const uint32_t d0 = b * kBlockDocs;
     const uint32_t t0 = p.q_off[q], t1 = p.q_off[q + 1];
+    if (p.q_meta && p.q_meta[q]) {                        // MUST / MUST_NOT clauses: k_score_blocks<true>
+      if (lane == 0) p.ovf2_list[atomicAdd(p.ovf2_count, 1u)] = (uint32_t)pr;
+      continue;
+    }
     // ranges of the first 64 terms (lane j holds term j); longer queries go dense
     uint64_t a = 0, z = 0;
     float tw = 0.f;
@@ -699,18 +798,161 @@ __global__ void __launch_bounds__(kPairWaves * 64) k_score_pairs(QueryParams p) 
   }
 }
 
+// ---------------------------------------------------------------------------
+// All hits in (score desc, doc asc) order = searcher.search(q, Integer.MAX_VALUE)
+// (Worker.java:230).  k_score_blocks leaves one sorted run per doc block
+// (hits[b * kBlockDocs ...], hits_n[b] keys); k_hits_prefix turns the run
+// lengths into output offsets P[0..R]; k_merge_runs merges pairs of runs
+// level by level (merge path: each thread co-ranks the start of its 8-output
+// chunk by binary search, then merges sequentially).  Keys are unique, so the
+// result is the deterministic descending key order.  The last level writes
+// (doc, score) split, or packed keys with a caller doc base (multi-GPU).
+__global__ void __launch_bounds__(1024) k_hits_prefix(const uint32_t *hits_n, uint32_t R, uint64_t *P) {
+  __shared__ uint64_t wsum[16];
+  __shared__ uint64_t carry;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t base = 0; base < R; base += 1024) {
+    const uint32_t i = base + tid;
+    const uint64_t v = i < R ? hits_n[i] : 0u;
+    uint64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(x, o, 64);
+      if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) wsum[wv] = x;
+    __syncthreads();
+    uint64_t pre = carry;
+    for (uint32_t w = 0; w < wv; w++) pre += wsum[w];
+    if (i < R) P[i] = pre + x - v;
+    __syncthreads();
+    if (tid == 1023) carry = pre + x;
+    __syncthreads();
+  }
+  if (tid == 0) P[R] = carry;
+}
+
+struct MergeRunsParams {
+  const uint64_t *src;
+  uint64_t *dst;            // packed keys out (non-final levels, or final with keys_out)
+  const uint64_t *P;        // [R + 1] output offsets of the block runs
+  uint32_t R, level;
+  uint32_t gapped;          // level 0: run r starts at src + r * kBlockDocs
+  uint32_t final;           // last level: write out_doc / out_score (or keys with doc_base into dst)
+  uint32_t *out_doc;
+  float *out_score;
+  uint64_t doc_base;
+};
+
+__global__ void __launch_bounds__(256) k_merge_runs(MergeRunsParams p) {
+  const uint64_t H = p.P[p.R];
+  const uint32_t span = 1u << (p.level + 1), half = 1u << p.level;
+  const uint32_t npairs = (p.R + span - 1) / span;
+  const uint64_t nchunks = (H + 7) / 8;
+  for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunks;
+       c += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t o = c * 8;
+    const uint64_t oend = min(o + 8, H);
+    while (o < oend) {
+      // pair holding output o: the last pair whose first offset is <= o
+      uint32_t lo = 0, hi = npairs - 1;
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi + 1) >> 1;
+        if (p.P[min((uint64_t)mid * span, (uint64_t)p.R)] <= o) lo = mid; else hi = mid - 1;
+      }
+      const uint32_t a0 = lo * span, a1 = min(a0 + half, p.R), b1 = min(a0 + span, p.R);
+      const uint64_t ps = p.P[a0], pm = p.P[a1], pe = p.P[b1];
+      const uint64_t la = pm - ps, lb = pe - pm;
+      const uint64_t *A = p.src + (p.gapped ? (uint64_t)a0 * kBlockDocs : ps);
+      const uint64_t *Bv = p.src + (p.gapped ? (uint64_t)a1 * kBlockDocs : pm);
+      // co-rank: ia = outputs of [ps, o) taken from A
+      const uint64_t j = o - ps;
+      uint64_t ia_lo = j > lb ? j - lb : 0, ia_hi = min(j, la);
+      while (ia_lo < ia_hi) {
+        const uint64_t mid = (ia_lo + ia_hi) >> 1;
+        if (A[mid] > Bv[j - mid - 1]) ia_lo = mid + 1; else ia_hi = mid;
+      }
+      uint64_t ia = ia_lo, ib = j - ia_lo;
+      const uint64_t stop = min(oend, pe);
+      for (; o < stop; o++) {
+        uint64_t key;
+        if (ib >= lb || (ia < la && A[ia] > Bv[ib])) key = A[ia++];
+        else key = Bv[ib++];
+        if (!p.final) {
+          p.dst[o] = key;
+        } else {
+          const uint32_t doc = ~(uint32_t)(key & 0xFFFFFFFFull);
+          if (p.out_doc) {
+            p.out_doc[o] = doc;
+            p.out_score[o] = __uint_as_float((uint32_t)(key >> 32));
+          } else {
+            p.dst[o] = (key & 0xFFFFFFFF00000000ull) | (uint64_t)(~(uint32_t)(doc + p.doc_base));
+          }
+        }
+      }
+    }
+  }
+}
+
+hipError_t launch_hits_order(const uint64_t *hits, const uint32_t *hits_n, uint32_t R, uint64_t *P, uint64_t *tmp0,
+                             uint64_t *tmp1, uint32_t *out_doc, float *out_score, uint64_t *keys_out,
+                             uint64_t doc_base, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(k_hits_prefix, dim3(1), dim3(1024), 0, s, hits_n, R, P);
+  uint32_t levels = 1;
+  while ((1u << levels) < R) levels++;
+  MergeRunsParams mp{};
+  mp.P = P;
+  mp.R = R;
+  mp.doc_base = doc_base;
+  const uint64_t *src = hits;
+  uint64_t *bufs[2] = {tmp0, tmp1};
+  for (uint32_t L = 0; L < levels; L++) {
+    mp.src = src;
+    mp.level = L;
+    mp.gapped = L == 0;
+    mp.final = L + 1 == levels;
+    mp.dst = mp.final && keys_out ? keys_out : bufs[L & 1];
+    mp.out_doc = mp.final && !keys_out ? out_doc : nullptr;
+    mp.out_score = mp.final && !keys_out ? out_score : nullptr;
+    hipLaunchKernelGGL(k_merge_runs, dim3(grid), dim3(256), 0, s, mp);
+    src = bufs[L & 1];
+  }
+  return hipGetLastError();
+}
+
+// top-k results of n_q queries -> packed merge keys with a doc base (the
+// multi-GPU all-gather form: score bits << 32 | ~global doc; 0 = empty slot)
+__global__ void k_pack_keys(const uint32_t *out_doc, const float *out_score, const uint32_t *out_n, uint32_t n_q,
+                            uint32_t k, uint64_t doc_base, uint64_t *keys) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (uint64_t)n_q * k) return;
+  const uint32_t q = (uint32_t)(i / k), j = (uint32_t)(i - (uint64_t)q * k);
+  keys[i] = j < out_n[q] ? ((uint64_t)__float_as_uint(out_score[i]) << 32) |
+                               (uint64_t)(~(uint32_t)(out_doc[i] + doc_base))
+                         : 0ull;
+}
+
+hipError_t launch_pack_keys(const uint32_t *out_doc, const float *out_score, const uint32_t *out_n, uint32_t n_q,
+                            uint32_t k, uint64_t doc_base, uint64_t *keys, hipStream_t s) {
+  const uint64_t n = (uint64_t)n_q * k;
+  if (n) hipLaunchKernelGGL(k_pack_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, out_doc, out_score, out_n, n_q,
+                            k, doc_base, keys);
+  return hipGetLastError();
+}
+
 hipError_t launch_score_pairs(const QueryParams &p, int grid, hipStream_t s) {
   hipLaunchKernelGGL(k_score_pairs, dim3(grid), dim3(kPairWaves * 64), 0, s, p);
   return hipGetLastError();
 }
 
 hipError_t launch_score_blocks(const QueryParams &p, hipStream_t s) {
-  if (p.ovf_list) {
-    hipLaunchKernelGGL(k_score_blocks, dim3(p.list_grid), dim3(kScoreThreads), 0, s, p);
-    return hipGetLastError();
-  }
-  const uint32_t chunks = (p.n_q + p.q_chunk - 1) / p.q_chunk;
-  hipLaunchKernelGGL(k_score_blocks, dim3(p.n_blocks, chunks), dim3(kScoreThreads), 0, s, p);
+  const dim3 grid = p.ovf_list ? dim3(p.list_grid) : dim3(p.n_blocks, (p.n_q + p.q_chunk - 1) / p.q_chunk);
+  if (p.ops)
+    hipLaunchKernelGGL(k_score_blocks<true>, grid, dim3(kScoreThreads), 0, s, p);
+  else
+    hipLaunchKernelGGL(k_score_blocks<false>, grid, dim3(kScoreThreads), 0, s, p);
   return hipGetLastError();
 }
 hipError_t launch_merge_topk(const QueryParams &p, hipStream_t s) {

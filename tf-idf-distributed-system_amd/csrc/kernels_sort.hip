@@ -1,6 +1,5 @@
-// kernels_sort.hip — device sorts built on rocPRIM/hipCUB radix sort:
-//   * all-hits ordering (searcher.search(q, Integer.MAX_VALUE)): keys
-//     (score bits << 32 | ~doc) sorted descending = (score desc, doc asc);
+// kernels_sort.hip — device sorts built on rocPRIM/hipCUB radix sort (tools
+// and tests only; the all-hits order is kernels_query.hip's merge passes):
 //   * canonical vocabulary for GLOBAL statistics: sorted union of 128-bit
 //     term keys, ordered by (hi, lo), de-duplicated.
 #include <hip/hip_runtime.h>
@@ -12,11 +11,6 @@
 namespace tfidf {
 
 hipError_t exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, hipStream_t s);
-
-hipError_t sort_u64_desc(const uint64_t *in, uint64_t *out, uint64_t n, void *tmp, size_t *tmp_bytes,
-                         hipStream_t s) {
-  return hipcub::DeviceRadixSort::SortKeysDescending(tmp, *tmp_bytes, in, out, (int)n, 0, 64, s);
-}
 
 __global__ void k_split128(const uint64_t *keys, uint64_t n, uint64_t *lo, uint64_t *hi, uint32_t *idx) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;

@@ -81,10 +81,28 @@ __global__ void k_vocab_import(const uint32_t *sent_slot, const uint32_t *gdf_in
   if (i < n) gdf[sent_slot[i]] = gdf_in[i];
 }
 
+// per-owner record counts -> exclusive start cursors (u32) and the caller's
+// u64 counts; G <= 1024, one workgroup
+__global__ void k_vocab_starts(const uint32_t *counts, uint32_t G, uint32_t *cursor, uint64_t *counts_out) {
+  __shared__ uint32_t c[1024];
+  for (uint32_t r = threadIdx.x; r < G; r += blockDim.x) c[r] = counts[r];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    for (uint32_t r = 0; r < G; r++) { cursor[r] = acc; acc += c[r]; }
+  }
+  for (uint32_t r = threadIdx.x; r < G; r += blockDim.x) counts_out[r] = c[r];
+}
+
 static unsigned blocks(uint64_t n) { return (unsigned)((n + 255) / 256 ? (n + 255) / 256 : 1); }
 
 hipError_t vocab_count(const uint64_t *dict, uint32_t C, uint32_t G, uint32_t *counts, hipStream_t s) {
   hipLaunchKernelGGL(k_vocab_count, dim3(blocks(C)), dim3(256), 0, s, dict, C, G, counts);
+  return hipGetLastError();
+}
+
+hipError_t vocab_starts(const uint32_t *counts, uint32_t G, uint32_t *cursor, uint64_t *counts_out, hipStream_t s) {
+  hipLaunchKernelGGL(k_vocab_starts, dim3(1), dim3(256), 0, s, counts, G, cursor, counts_out);
   return hipGetLastError();
 }
 

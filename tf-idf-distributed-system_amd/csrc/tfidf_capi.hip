@@ -24,7 +24,6 @@
 
 namespace tfidf {
 hipError_t add_u64(uint64_t *v, uint64_t n, uint64_t delta, hipStream_t s);
-hipError_t sort_u64_desc(const uint64_t *in, uint64_t *out, uint64_t n, void *tmp, size_t *tmp_bytes, hipStream_t s);
 hipError_t sort_unique_keys128(const uint64_t *keys, uint64_t n, uint64_t *out, uint64_t *n_unique, hipStream_t s);
 hipError_t slot_to_canon(const uint64_t *dict, uint32_t C, const uint64_t *canon, uint64_t n_canon,
                          uint32_t *canon_of_slot, hipStream_t s);
@@ -101,6 +100,12 @@ template <class T> struct PinnedVec {
     n = m;
     return hipSuccess;
   }
+  void clear() { n = 0; }
+  hipError_t assign(size_t m, T v) {
+    hipError_t e = resize(m);
+    if (e == hipSuccess) for (size_t i = 0; i < m; i++) p[i] = v;
+    return e;
+  }
   T *data() { return p; }
   const T *data() const { return p; }
   size_t size() const { return n; }
@@ -130,7 +135,8 @@ enum { EV_START, EV_TOK, EV_L0, EV_LONG, EV_D0, EV_DF, EV_BSCAN, EV_CSCAN, EV_SC
 struct tfidf_index {
   tfidf_config cfg;
   std::mutex mu;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;      // stream all work is issued on (own_stream unless tfidf_set_stream)
+  hipStream_t own_stream = nullptr;
   hipEvent_t ev[EV_N];
   // side stream for the dictionary's host mirror: its D2H copy overlaps the inversion
   hipStream_t copy_stream = nullptr;
@@ -177,16 +183,19 @@ struct tfidf_index {
 
   // statistics in force
   bool has_global = false;
-  std::vector<uint32_t> gdf;       // per slot (GLOBAL)
+  PinnedVec<uint32_t> gdf;         // per slot (GLOBAL), host mirror
+  hipEvent_t gdf_ev = nullptr;     // gdf mirror copied (tfidf_set_global_df_device is asynchronous)
+  bool gdf_pending = false;
+  PinnedVec<float> h_cache;        // BM25 norm cache staging (pinned: asynchronous upload)
   uint64_t g_doc_count = 0, g_sum_ttf = 0;
   DevBuf canon_of_slot;
   uint64_t n_canon = 0;
   // term-ownership exchange: record order -> slot, owner-side scratch table
-  DevBuf sent_slot, vcounts, vt_table, vt_sum, vt_rslot, gdf_dev, ovf;
+  DevBuf sent_slot, vcounts, vnu, vt_table, vt_sum, vt_rslot, gdf_dev, ovf;
   uint64_t n_sent = 0;
 
   // query scratch
-  DevBuf q_off, q_slot, q_w, cache, cand, cand_n, out_doc, out_score, out_n, hits, hits_n, hits_c, hits_s, sort_tmp;
+  DevBuf q_off, q_slot, q_w, q_role, q_meta, cache, cand, cand_n, out_doc, out_score, out_n, hits, hits_n, hits_c, hits_s, hits_P, sort_tmp;
   float last_ms_scoring = 0, last_ms_total = 0;
 };
 
@@ -224,18 +233,20 @@ extern "C" int tfidf_create(const tfidf_config *cfg, tfidf_index **out) {
   ix->cap_log2 = lg;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, cfg->device) == hipSuccess) ix->num_cus = prop.multiProcessorCount;
-  if (hipStreamCreateWithFlags(&ix->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&ix->own_stream, hipStreamNonBlocking) != hipSuccess) {
     delete ix;
     return fail(TFIDF_E_HIP, "hipStreamCreate failed");
   }
+  ix->stream = ix->own_stream;
   if (hipStreamCreateWithFlags(&ix->copy_stream, hipStreamNonBlocking) != hipSuccess) {
-    hipStreamDestroy(ix->stream);
+    hipStreamDestroy(ix->own_stream);
     delete ix;
     return fail(TFIDF_E_HIP, "hipStreamCreate failed");
   }
   for (int i = 0; i < EV_N; i++) hipEventCreate(&ix->ev[i]);
   for (int i = 0; i < 2; i++) hipEventCreateWithFlags(&ix->stage_ev[i], hipEventDisableTiming);
   for (int i = 0; i < 2; i++) hipEventCreateWithFlags(&ix->mir_ev[i], hipEventDisableTiming);
+  hipEventCreateWithFlags(&ix->gdf_ev, hipEventDisableTiming);
   hipError_t e = ix->offsets.reserve(64);
   if (e != hipSuccess) { delete ix; return fail(TFIDF_E_OOM, "hipMalloc offsets"); }
   uint64_t zero = 0;
@@ -252,9 +263,9 @@ extern "C" int tfidf_destroy(tfidf_index *ix) {
   DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->d_live_map, &ix->dict, &ix->csr_col, &ix->csr_tf, &ix->doc_len,
                     &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->long_list, &ix->uni_list, &ix->counters, &ix->blk,
                     &ix->retry_list, &ix->bbase, &ix->post, &ix->post_tmp, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->canon_of_slot,
-                    &ix->q_off, &ix->q_slot, &ix->q_w, &ix->cache, &ix->cand, &ix->cand_n, &ix->out_doc,
-                    &ix->out_score, &ix->out_n, &ix->hits, &ix->hits_n, &ix->hits_c, &ix->hits_s, &ix->sort_tmp,
-                    &ix->row_off, &ix->tvals, &ix->toff, &ix->tdf, &ix->term_tmp, &ix->sent_slot, &ix->vcounts,
+                    &ix->q_off, &ix->q_slot, &ix->q_w, &ix->q_role, &ix->q_meta, &ix->cache, &ix->cand, &ix->cand_n, &ix->out_doc,
+                    &ix->out_score, &ix->out_n, &ix->hits, &ix->hits_n, &ix->hits_c, &ix->hits_s, &ix->hits_P, &ix->sort_tmp,
+                    &ix->row_off, &ix->tvals, &ix->toff, &ix->tdf, &ix->term_tmp, &ix->sent_slot, &ix->vcounts, &ix->vnu,
                     &ix->vt_table, &ix->vt_sum, &ix->vt_rslot, &ix->gdf_dev, &ix->ovf};
   for (DevBuf *b : bufs) b->release();
   for (int i = 0; i < EV_N; i++) hipEventDestroy(ix->ev[i]);
@@ -263,9 +274,20 @@ extern "C" int tfidf_destroy(tfidf_index *ix) {
     hipEventDestroy(ix->stage_ev[i]);
   }
   for (int i = 0; i < 2; i++) hipEventDestroy(ix->mir_ev[i]);
+  hipEventDestroy(ix->gdf_ev);
+  hipStreamSynchronize(ix->own_stream);
   hipStreamDestroy(ix->copy_stream);
-  hipStreamDestroy(ix->stream);
+  hipStreamDestroy(ix->own_stream);
   delete ix;
+  return TFIDF_OK;
+}
+
+// GLOBAL df host mirror: wait for its asynchronous copy before the first use
+static int wait_gdf(tfidf_index *ix) {
+  if (ix->gdf_pending) {
+    HIP_TRY(hipEventSynchronize(ix->gdf_ev));
+    ix->gdf_pending = false;
+  }
   return TFIDF_OK;
 }
 
@@ -380,6 +402,7 @@ extern "C" int tfidf_clear(tfidf_index *ix) {
   ix->n_dead = 0;
   ix->committed = false;
   ix->n_docs = 0;
+  wait_gdf(ix);
   ix->has_global = false;
   ix->gdf.clear();
   return TFIDF_OK;
@@ -613,8 +636,11 @@ static float bm25_idf(uint64_t df, uint64_t doc_count) {
 static uint64_t eff_doc_count(const tfidf_index *ix) { return ix->has_global ? ix->g_doc_count : ix->doc_count; }
 static uint64_t eff_sum_ttf(const tfidf_index *ix) { return ix->has_global ? ix->g_sum_ttf : ix->sum_ttf; }
 
-static int upload_cache(tfidf_index *ix) {
-  float c[256];
+static int upload_cache(tfidf_index *ix, bool sync = true) {
+  HIP_TRY(ix->h_cache.resize(256));
+  // the previous upload from the staging array must be done before it is rewritten
+  HIP_TRY(hipStreamSynchronize(ix->stream));
+  float *c = ix->h_cache.data();
   const uint64_t dc = eff_doc_count(ix);
   if (dc == 0) {
     for (int i = 0; i < 256; i++) c[i] = 0.0f;
@@ -623,8 +649,8 @@ static int upload_cache(tfidf_index *ix) {
     norm_cache(ix->cfg.k1, ix->cfg.b, avgdl, c);
   }
   HIP_TRY(ix->cache.reserve(256 * 4));
-  HIP_TRY(hipMemcpyAsync(ix->cache.p, c, sizeof c, hipMemcpyHostToDevice, ix->stream));
-  HIP_TRY(hipStreamSynchronize(ix->stream));
+  HIP_TRY(hipMemcpyAsync(ix->cache.p, c, 256 * 4, hipMemcpyHostToDevice, ix->stream));
+  if (sync) HIP_TRY(hipStreamSynchronize(ix->stream));
   return TFIDF_OK;
 }
 
@@ -935,6 +961,7 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   t.num_docs = N;
   t.nnz = ix->nnz;
 
+  if (int rc = wait_gdf(ix)) return rc;
   ix->has_global = false;
   ix->gdf.clear();
   ix->committed = true;
@@ -990,32 +1017,77 @@ static uint32_t host_lookup(const tfidf_index *ix, uint64_t lo, uint64_t hi) {
 struct PreparedQuery {
   std::vector<uint32_t> slot;
   std::vector<float> w;
+  std::vector<uint32_t> role;    // role << 24 | MUST clause index
+  uint32_t meta = 0;             // MUST clause count | has MUST_NOT << 31
 };
 
+// Query plan (analysis.h) -> dictionary slots + BM25 weights.  A term absent
+// from this shard's dictionary has no scorer (TermWeight.scorer == null): a
+// SHOULD or MUST_NOT term is dropped, a MUST clause without any present term
+// leaves the query without hits (BooleanWeight: required scorer missing), and
+// a query with neither MUST clauses nor a present SHOULD term has no hits.
 static int prepare_query(tfidf_index *ix, const uint8_t *q, uint64_t n, PreparedQuery *pq) {
-  std::vector<QueryTerm> terms;
-  const int rc = parse_query(q, n, &terms);
-  if (rc == 1) return fail(TFIDF_E_UNSUPPORTED_QUERY, "query is not valid UTF-8");
-  if (rc == 2) return fail(TFIDF_E_UNSUPPORTED_QUERY, "AND/OR/NOT operator words are not supported");
+  QueryPlan plan;
+  const int rc = parse_query(q, n, &plan);
+  if (rc == kQBadUtf8) return fail(TFIDF_E_UNSUPPORTED_QUERY, "query is not valid UTF-8");
+  if (rc == kQSyntax)
+    return fail(TFIDF_E_QUERY_SYNTAX, "query does not parse (QueryParser ParseException / TooManyClauses)");
+  if (int e = wait_gdf(ix)) return e;
   const uint64_t dc = eff_doc_count(ix);
-  for (const QueryTerm &t : terms) {
+  if (dc == 0) return TFIDF_OK;                        // no document holds a token
+  std::vector<uint32_t> present(plan.n_groups, 0);
+  uint32_t n_should = 0;
+  bool has_not = false;
+  for (const PlanTerm &t : plan.terms) {
     uint64_t lo, hi;
     term_key(t.term, &lo, &hi);
     const uint32_t s = host_lookup(ix, lo, hi);
-    if (s == kInvalidSlot || dc == 0) continue;        // absent term contributes nothing
-    const uint64_t df = ix->has_global ? ix->gdf[s] : ix->h_df[s];
-    const float idf = bm25_idf(df, dc);
-    volatile float w = t.boost * idf;                  // BM25Scorer: weight = boost * idf
-    const float wv = w;
+    if (s == kInvalidSlot) continue;                   // absent term contributes nothing
+    float wv = 0.0f;
+    if (t.role != kRoleNot) {
+      const uint64_t df = ix->has_global ? ix->gdf[s] : ix->h_df[s];
+      const float idf = bm25_idf(df, dc);
+      volatile float w = t.boost * idf;                // BM25Scorer: weight = boost * idf
+      wv = w;
+    }
+    if (t.role == kRoleMust) present[t.group]++;
+    if (t.role == kRoleShould) n_should++;
+    if (t.role == kRoleNot) has_not = true;
     pq->slot.push_back(s);
     pq->w.push_back(wv);
+    pq->role.push_back(t.role << 24 | t.group);
   }
+  bool empty = plan.n_groups == 0 && n_should == 0;
+  for (uint32_t c : present) empty |= c == 0;
+  if (empty) {
+    pq->slot.clear();
+    pq->w.clear();
+    pq->role.clear();
+    return TFIDF_OK;
+  }
+  pq->meta = plan.n_groups | (has_not ? 1u << 31 : 0u);
   return TFIDF_OK;
 }
 
-static int run_scoring(tfidf_index *ix, const std::vector<uint32_t> &qoff, const std::vector<uint32_t> &slots,
-                       const std::vector<float> &ws, uint32_t n_q, uint32_t k) {
+// Batch of prepared queries in device layout.
+struct QueryBatch {
+  std::vector<uint32_t> off{0}, slot, role, meta;
+  std::vector<float> w;
+  bool ops = false;                // some query has MUST / MUST_NOT clauses
+  void add(const PreparedQuery &pq) {
+    slot.insert(slot.end(), pq.slot.begin(), pq.slot.end());
+    w.insert(w.end(), pq.w.begin(), pq.w.end());
+    role.insert(role.end(), pq.role.begin(), pq.role.end());
+    off.push_back((uint32_t)slot.size());
+    meta.push_back(pq.slot.empty() ? 0u : pq.meta);
+    ops |= !pq.slot.empty() && pq.meta != 0;
+  }
+};
+
+static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint32_t k) {
   hipStream_t s = ix->stream;
+  const std::vector<uint32_t> &qoff = qb.off, &slots = qb.slot;
+  const std::vector<float> &ws = qb.w;
   HIP_TRY(ix->q_off.reserve(qoff.size() * 4));
   HIP_TRY(ix->q_slot.reserve(slots.size() * 4 + 4));
   HIP_TRY(ix->q_w.reserve(ws.size() * 4 + 4));
@@ -1023,6 +1095,12 @@ static int run_scoring(tfidf_index *ix, const std::vector<uint32_t> &qoff, const
   if (!slots.empty()) {
     HIP_TRY(hipMemcpyAsync(ix->q_slot.p, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(ix->q_w.p, ws.data(), ws.size() * 4, hipMemcpyHostToDevice, s));
+  }
+  if (qb.ops) {
+    HIP_TRY(ix->q_role.reserve(qb.role.size() * 4 + 4));
+    HIP_TRY(ix->q_meta.reserve(qb.meta.size() * 4 + 4));
+    HIP_TRY(hipMemcpyAsync(ix->q_role.p, qb.role.data(), qb.role.size() * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(ix->q_meta.p, qb.meta.data(), qb.meta.size() * 4, hipMemcpyHostToDevice, s));
   }
   QueryParams qp{};
   qp.post = ix->post.as<uint64_t>();
@@ -1036,6 +1114,9 @@ static int run_scoring(tfidf_index *ix, const std::vector<uint32_t> &qoff, const
   qp.q_off = ix->q_off.as<uint32_t>();
   qp.q_slot = ix->q_slot.as<uint32_t>();
   qp.q_w = ix->q_w.as<float>();
+  qp.q_role = qb.ops ? ix->q_role.as<uint32_t>() : nullptr;
+  qp.q_meta = qb.ops ? ix->q_meta.as<uint32_t>() : nullptr;
+  qp.ops = qb.ops ? 1u : 0u;
   qp.n_q = n_q;
   qp.k = k;
   {   // enough (block, chunk) workgroups to fill the chip ~4 deep; never more chunks than queries
@@ -1068,14 +1149,27 @@ static int run_scoring(tfidf_index *ix, const std::vector<uint32_t> &qoff, const
     // listed for the dense per-block kernel (list mode, persistent grid).
     // Single queries keep the dense kernel: a few hundred pairs cannot fill
     // the chip one wave each.
-    HIP_TRY(ix->ovf.reserve(npairs * 4 + 64));
+    // plain heavy pairs -> ovf list (k_score_blocks<false>); pairs of operator
+    // queries -> ovf2 list (k_score_blocks<true>)
+    HIP_TRY(ix->ovf.reserve(npairs * 8 + 64));
     qp.ovf_count = ix->ovf.as<uint32_t>();
+    qp.ovf2_count = qp.ovf_count + 1;
     qp.ovf_list = qp.ovf_count + 16;
+    qp.ovf2_list = qp.ovf_list + npairs;
     qp.list_grid = (uint32_t)ix->num_cus * 2;
-    HIP_TRY(hipMemsetAsync(qp.ovf_count, 0, 4, s));
+    HIP_TRY(hipMemsetAsync(qp.ovf_count, 0, 8, s));
     const uint64_t want = (npairs + kPairWavesPerWG - 1) / kPairWavesPerWG;
     const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)ix->num_cus * 40));
     HIP_TRY(launch_score_pairs(qp, grid, s));
+    qp.ops = 0;
+    if (qb.ops) {
+      QueryParams q2 = qp;
+      q2.ovf_list = qp.ovf2_list;
+      q2.ovf_count = qp.ovf2_count;
+      q2.ops = 1;
+      q2.list_grid = (uint32_t)ix->num_cus;          // one 134 KiB workgroup per CU
+      HIP_TRY(launch_score_blocks(q2, s));
+    }
   }
   HIP_TRY(launch_score_blocks(qp, s));
   HIP_TRY(hipEventRecord(ix->ev[EV_Q1], s));
@@ -1096,8 +1190,9 @@ extern "C" int tfidf_search(tfidf_index *ix, const uint8_t *q, uint64_t q_len, u
   int rc = prepare_query(ix, q, q_len, &pq);
   if (rc) return rc;
   if (pq.slot.empty() || ix->n_docs == 0) { ix->last_ms_scoring = ix->last_ms_total = 0; return TFIDF_OK; }
-  std::vector<uint32_t> qoff{0, (uint32_t)pq.slot.size()};
-  rc = run_scoring(ix, qoff, pq.slot, pq.w, 1, k);
+  QueryBatch qb;
+  qb.add(pq);
+  rc = run_scoring(ix, qb, 1, k);
   if (rc) return rc;
   hipStream_t s = ix->stream;
   if (k) {
@@ -1115,36 +1210,25 @@ extern "C" int tfidf_search(tfidf_index *ix, const uint8_t *q, uint64_t q_len, u
     ix->last_ms_total = ev_ms(ix, EV_Q0, EV_Q2);
     return TFIDF_OK;
   }
-  // all hits: compact the per-block hit keys, radix-sort descending
-  std::vector<uint32_t> hn(ix->n_blocks);
-  HIP_TRY(hipMemcpyAsync(hn.data(), ix->hits_n.p, hn.size() * 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  // all hits: per-block sorted runs -> merge passes on the device -> (doc, score)
+  const uint32_t R = ix->n_blocks;
+  HIP_TRY(ix->hits_c.reserve((size_t)R * kBlockDocs * 8 + 8));
+  HIP_TRY(ix->hits_P.reserve(((size_t)R + 1) * 8));
+  HIP_TRY(ix->out_doc.reserve((size_t)R * kBlockDocs * 4 + 4));
+  HIP_TRY(ix->out_score.reserve((size_t)R * kBlockDocs * 4 + 4));
+  HIP_TRY(launch_hits_order(ix->hits.as<uint64_t>(), ix->hits_n.as<uint32_t>(), R, ix->hits_P.as<uint64_t>(),
+                            ix->hits_c.as<uint64_t>(), ix->hits.as<uint64_t>(), ix->out_doc.as<uint32_t>(),
+                            ix->out_score.as<float>(), nullptr, 0, ix->num_cus * 4, s));
+  HIP_TRY(hipEventRecord(ix->ev[EV_Q2], s));
   uint64_t H = 0;
-  for (uint32_t v : hn) H += v;
+  HIP_TRY(hipMemcpyAsync(&H, ix->hits_P.as<uint64_t>() + R, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
   *n_out = H;
   if (H > cap) return fail(TFIDF_E_BUFFER, "need %llu result slots", (unsigned long long)H);
-  if (H == 0) return TFIDF_OK;
-  HIP_TRY(ix->hits_c.reserve(H * 8));
-  HIP_TRY(ix->hits_s.reserve(H * 8));
-  uint64_t off = 0;
-  for (uint32_t b = 0; b < ix->n_blocks; b++) {
-    if (hn[b])
-      HIP_TRY(hipMemcpyAsync(ix->hits_c.as<uint64_t>() + off, ix->hits.as<uint64_t>() + (size_t)b * kBlockDocs,
-                             (size_t)hn[b] * 8, hipMemcpyDeviceToDevice, s));
-    off += hn[b];
-  }
-  size_t tb = 0;
-  HIP_TRY(sort_u64_desc(ix->hits_c.as<uint64_t>(), ix->hits_s.as<uint64_t>(), H, nullptr, &tb, s));
-  HIP_TRY(ix->sort_tmp.reserve(tb));
-  HIP_TRY(sort_u64_desc(ix->hits_c.as<uint64_t>(), ix->hits_s.as<uint64_t>(), H, ix->sort_tmp.p, &tb, s));
-  std::vector<uint64_t> keys(H);
-  HIP_TRY(hipMemcpyAsync(keys.data(), ix->hits_s.p, H * 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipEventRecord(ix->ev[EV_Q2], s));
-  HIP_TRY(hipStreamSynchronize(s));
-  for (uint64_t i = 0; i < H; i++) {
-    doc_ids[i] = ~(uint32_t)(keys[i] & 0xFFFFFFFFu);
-    uint32_t sb = (uint32_t)(keys[i] >> 32);
-    memcpy(&scores[i], &sb, 4);
+  if (H) {
+    HIP_TRY(hipMemcpyAsync(doc_ids, ix->out_doc.p, H * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(scores, ix->out_score.p, H * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
   }
   ix->last_ms_scoring = ev_ms(ix, EV_Q0, EV_Q1);
   ix->last_ms_total = ev_ms(ix, EV_Q0, EV_Q2);
@@ -1158,22 +1242,21 @@ extern "C" int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const 
   std::lock_guard<std::mutex> lk(ix->mu);
   if (!ix->committed) return fail(TFIDF_E_STATE, "search before commit");
   DeviceGuard g(ix->cfg.device);
-  std::vector<uint32_t> qoff{0}, slots;
-  std::vector<float> ws;
+  // a query that does not parse (or is not UTF-8) has no hits, as the
+  // reference answers [] for it (Worker.java:182-185); the batch goes on
+  QueryBatch qb;
   for (uint32_t i = 0; i < n_q; i++) {
     PreparedQuery pq;
-    int rc = prepare_query(ix, q_utf8 + q_offsets[i], q_offsets[i + 1] - q_offsets[i], &pq);
-    if (rc) return rc;
-    slots.insert(slots.end(), pq.slot.begin(), pq.slot.end());
-    ws.insert(ws.end(), pq.w.begin(), pq.w.end());
-    qoff.push_back((uint32_t)slots.size());
+    if (prepare_query(ix, q_utf8 + q_offsets[i], q_offsets[i + 1] - q_offsets[i], &pq) != TFIDF_OK)
+      pq = PreparedQuery();
+    qb.add(pq);
   }
   if (n_q == 0) return TFIDF_OK;
-  if (ix->n_docs == 0) {
+  if (ix->n_docs == 0 || qb.slot.empty()) {
     memset(counts, 0, n_q * 4);
     return TFIDF_OK;
   }
-  int rc = run_scoring(ix, qoff, slots, ws, n_q, k);
+  int rc = run_scoring(ix, qb, n_q, k);
   if (rc) return rc;
   hipStream_t s = ix->stream;
   HIP_TRY(hipMemcpyAsync(counts, ix->out_n.p, (size_t)n_q * 4, hipMemcpyDeviceToHost, s));
@@ -1189,6 +1272,78 @@ extern "C" int tfidf_last_search_ms(const tfidf_index *ix, float *ms_scoring, fl
   if (!ix) return fail(TFIDF_E_INVALID_ARG, "NULL index");
   if (ms_scoring) *ms_scoring = ix->last_ms_scoring;
   if (ms_total) *ms_total = ix->last_ms_total;
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_set_stream(tfidf_index *ix, void *stream) {
+  if (!ix) return fail(TFIDF_E_INVALID_ARG, "NULL index");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DeviceGuard g(ix->cfg.device);
+  HIP_TRY(hipStreamSynchronize(ix->stream));
+  ix->stream = stream == TFIDF_OWN_STREAM ? ix->own_stream : static_cast<hipStream_t>(stream);
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_search_batch_keys_device(tfidf_index *ix, const uint8_t *q_utf8, const uint64_t *q_offsets,
+                                              uint32_t n_q, uint32_t k, uint64_t doc_base, void *d_keys) {
+  if (!ix || !q_offsets || (n_q && !d_keys)) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  if (k == 0 || k > 1024) return fail(TFIDF_E_INVALID_ARG, "1 <= k <= 1024");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  if (!ix->committed) return fail(TFIDF_E_STATE, "search before commit");
+  DeviceGuard g(ix->cfg.device);
+  if (n_q == 0) return TFIDF_OK;
+  hipStream_t s = ix->stream;
+  QueryBatch qb;
+  for (uint32_t i = 0; i < n_q; i++) {
+    PreparedQuery pq;
+    if (prepare_query(ix, q_utf8 + q_offsets[i], q_offsets[i + 1] - q_offsets[i], &pq) != TFIDF_OK)
+      pq = PreparedQuery();                            // does not parse -> no hits (Worker.java:182-185)
+    qb.add(pq);
+  }
+  if (ix->n_docs == 0 || qb.slot.empty()) {
+    HIP_TRY(hipMemsetAsync(d_keys, 0, (size_t)n_q * k * 8, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    return TFIDF_OK;
+  }
+  int rc = run_scoring(ix, qb, n_q, k);
+  if (rc) return rc;
+  HIP_TRY(launch_pack_keys(ix->out_doc.as<uint32_t>(), ix->out_score.as<float>(), ix->out_n.as<uint32_t>(), n_q, k,
+                           doc_base, static_cast<uint64_t *>(d_keys), s));
+  HIP_TRY(hipStreamSynchronize(s));
+  ix->last_ms_scoring = ev_ms(ix, EV_Q0, EV_Q1);
+  ix->last_ms_total = ev_ms(ix, EV_Q0, EV_Q2);
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_search_all_keys_device(tfidf_index *ix, const uint8_t *q, uint64_t q_len, uint64_t doc_base,
+                                            void *d_keys, uint64_t cap, uint64_t *n_out) {
+  if (!ix || (!q && q_len) || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  *n_out = 0;
+  std::lock_guard<std::mutex> lk(ix->mu);
+  if (!ix->committed) return fail(TFIDF_E_STATE, "search before commit");
+  if (cap < ix->n_docs || (ix->n_docs && !d_keys))
+    return fail(TFIDF_E_BUFFER, "the key buffer needs num_docs = %llu entries", (unsigned long long)ix->n_docs);
+  DeviceGuard g(ix->cfg.device);
+  PreparedQuery pq;
+  int rc = prepare_query(ix, q, q_len, &pq);
+  if (rc) return rc;
+  if (pq.slot.empty() || ix->n_docs == 0) return TFIDF_OK;
+  QueryBatch qb;
+  qb.add(pq);
+  rc = run_scoring(ix, qb, 1, 0);
+  if (rc) return rc;
+  hipStream_t s = ix->stream;
+  const uint32_t R = ix->n_blocks;
+  HIP_TRY(ix->hits_c.reserve((size_t)R * kBlockDocs * 8 + 8));
+  HIP_TRY(ix->hits_P.reserve(((size_t)R + 1) * 8));
+  HIP_TRY(launch_hits_order(ix->hits.as<uint64_t>(), ix->hits_n.as<uint32_t>(), R, ix->hits_P.as<uint64_t>(),
+                            ix->hits_c.as<uint64_t>(), ix->hits.as<uint64_t>(), nullptr, nullptr,
+                            static_cast<uint64_t *>(d_keys), doc_base, ix->num_cus * 4, s));
+  HIP_TRY(hipEventRecord(ix->ev[EV_Q2], s));
+  HIP_TRY(hipMemcpyAsync(n_out, ix->hits_P.as<uint64_t>() + R, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  ix->last_ms_scoring = ev_ms(ix, EV_Q0, EV_Q1);
+  ix->last_ms_total = ev_ms(ix, EV_Q0, EV_Q2);
   return TFIDF_OK;
 }
 
@@ -1209,6 +1364,36 @@ extern "C" int tfidf_doc_key(const tfidf_index *ix, uint64_t doc, uint8_t *buf, 
   *n_out = k.size();
   if (k.size() > cap) return fail(TFIDF_E_BUFFER, "key needs %zu bytes", k.size());
   if (buf && !k.empty()) memcpy(buf, k.data(), k.size());
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_doc_keys(const tfidf_index *ix, uint8_t *buf, uint64_t cap, uint64_t *offsets,
+                              uint64_t *n_bytes) {
+  if (!ix || !n_bytes || !offsets) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
+  std::string k;
+  uint64_t need = 0;
+  for (uint64_t d = 0; d < ix->n_docs; d++) {
+    const uint64_t st = staged_of(ix, d);
+    need += ix->key_synth[st] ? std::to_string(st).size() : ix->key_off[st + 1] - ix->key_off[st];
+  }
+  *n_bytes = need;
+  if (need > cap || (need && !buf)) return fail(TFIDF_E_BUFFER, "keys need %llu bytes", (unsigned long long)need);
+  uint64_t p = 0;
+  offsets[0] = 0;
+  for (uint64_t d = 0; d < ix->n_docs; d++) {
+    const uint64_t st = staged_of(ix, d);
+    if (ix->key_synth[st]) {
+      k = std::to_string(st);
+      memcpy(buf + p, k.data(), k.size());
+      p += k.size();
+    } else {
+      const uint64_t n = ix->key_off[st + 1] - ix->key_off[st];
+      memcpy(buf + p, ix->key_arena.data() + ix->key_off[st], n);
+      p += n;
+    }
+    offsets[d + 1] = p;
+  }
   return TFIDF_OK;
 }
 
@@ -1271,6 +1456,7 @@ extern "C" int tfidf_term_df(tfidf_index *ix, const uint8_t *term, uint64_t len,
                              uint64_t *df_effective) {
   if (!ix || (!term && len)) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
   if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
+  if (int e = wait_gdf(ix)) return e;
   std::string t((const char *)term, len);
   uint64_t lo, hi;
   term_key(t, &lo, &hi);
@@ -1371,8 +1557,9 @@ extern "C" int tfidf_vocab_canonicalize_device(tfidf_index *ix, const void *d_al
 }
 
 extern "C" int tfidf_vocab_partition_device(tfidf_index *ix, uint32_t n_ranks, void *d_records, uint64_t cap,
-                                            uint64_t *counts, uint64_t *n_out) {
-  if (!ix || !n_out || !counts || n_ranks == 0) return fail(TFIDF_E_INVALID_ARG, "NULL argument or n_ranks == 0");
+                                            void *d_counts, uint64_t *n_out) {
+  if (!ix || !n_out || !d_counts || n_ranks == 0 || n_ranks > 1024)
+    return fail(TFIDF_E_INVALID_ARG, "NULL argument or n_ranks not in [1, 1024]");
   std::lock_guard<std::mutex> lk(ix->mu);
   if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
   DeviceGuard g(ix->cfg.device);
@@ -1380,34 +1567,29 @@ extern "C" int tfidf_vocab_partition_device(tfidf_index *ix, uint32_t n_ranks, v
   if (ix->num_terms > cap) return fail(TFIDF_E_BUFFER, "need %llu records", (unsigned long long)ix->num_terms);
   if (ix->num_terms && !d_records) return fail(TFIDF_E_INVALID_ARG, "NULL records");
   hipStream_t s = ix->stream;
-  HIP_TRY(ix->vcounts.reserve((size_t)n_ranks * 8));
+  HIP_TRY(ix->vcounts.reserve((size_t)n_ranks * 8 + 64));
   HIP_TRY(ix->sent_slot.reserve(ix->num_terms * 4 + 4));
   uint32_t *cnt = ix->vcounts.as<uint32_t>(), *cur = cnt + n_ranks;
   HIP_TRY(hipMemsetAsync(cnt, 0, (size_t)n_ranks * 4, s));
   HIP_TRY(vocab_count(ix->dict.as<uint64_t>(), ix->C, n_ranks, cnt, s));
-  std::vector<uint32_t> hc(n_ranks), start(n_ranks);
-  HIP_TRY(hipMemcpyAsync(hc.data(), cnt, (size_t)n_ranks * 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  uint64_t acc = 0;
-  for (uint32_t r = 0; r < n_ranks; r++) { start[r] = (uint32_t)acc; counts[r] = hc[r]; acc += hc[r]; }
-  if (acc != ix->num_terms) return fail(TFIDF_E_STATE, "vocabulary count mismatch");
-  HIP_TRY(hipMemcpyAsync(cur, start.data(), (size_t)n_ranks * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(vocab_starts(cnt, n_ranks, cur, static_cast<uint64_t *>(d_counts), s));
   HIP_TRY(vocab_scatter(ix->dict.as<uint64_t>(), ix->df_dev(), ix->C, n_ranks, cur, (uint64_t *)d_records,
                         ix->sent_slot.as<uint32_t>(), s));
-  HIP_TRY(hipStreamSynchronize(s));
-  ix->n_sent = acc;
-  return TFIDF_OK;
+  ix->n_sent = ix->num_terms;
+  return TFIDF_OK;                                     // asynchronous on the index's stream
 }
 
 extern "C" int tfidf_vocab_reduce_device(tfidf_index *ix, const void *d_records, uint64_t n, void *d_df_out,
-                                         uint64_t *n_unique) {
-  if (!ix || !n_unique || (n && (!d_records || !d_df_out))) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+                                         void *d_n_unique) {
+  if (!ix || (n && (!d_records || !d_df_out))) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
   std::lock_guard<std::mutex> lk(ix->mu);
   DeviceGuard g(ix->cfg.device);
-  *n_unique = 0;
-  if (n == 0) return TFIDF_OK;
-  if (n >= (1ull << 30)) return fail(TFIDF_E_CAPACITY, "too many vocabulary records");
   hipStream_t s = ix->stream;
+  if (n >= (1ull << 30)) return fail(TFIDF_E_CAPACITY, "too many vocabulary records");
+  if (n == 0) {
+    if (d_n_unique) HIP_TRY(hipMemsetAsync(d_n_unique, 0, 8, s));
+    return TFIDF_OK;
+  }
   uint64_t T = 1024;
   while (T < 2 * n) T <<= 1;
   HIP_TRY(ix->vt_table.reserve(T * 16));
@@ -1415,14 +1597,13 @@ extern "C" int tfidf_vocab_reduce_device(tfidf_index *ix, const void *d_records,
   HIP_TRY(ix->vt_rslot.reserve(n * 4));
   HIP_TRY(hipMemsetAsync(ix->vt_table.p, 0, T * 16, s));
   HIP_TRY(hipMemsetAsync(ix->vt_sum.p, 0, T * 4, s));
-  HIP_TRY(ix->vcounts.reserve(64));
-  unsigned long long *nu = reinterpret_cast<unsigned long long *>(ix->vcounts.p);
+  HIP_TRY(ix->vnu.reserve(64));
+  unsigned long long *nu = reinterpret_cast<unsigned long long *>(ix->vnu.p);
   HIP_TRY(hipMemsetAsync(nu, 0, 8, s));
   HIP_TRY(vocab_reduce((const uint64_t *)d_records, n, ix->vt_table.as<uint64_t>(), (uint32_t)(T - 1),
                        ix->vt_sum.as<uint32_t>(), ix->vt_rslot.as<uint32_t>(), (uint32_t *)d_df_out, nu, s));
-  HIP_TRY(hipMemcpyAsync(n_unique, nu, 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
-  return TFIDF_OK;
+  if (d_n_unique) HIP_TRY(hipMemcpyAsync(d_n_unique, nu, 8, hipMemcpyDeviceToDevice, s));
+  return TFIDF_OK;                                     // asynchronous on the index's stream
 }
 
 extern "C" int tfidf_set_global_df_device(tfidf_index *ix, const void *d_df, uint64_t n, uint64_t doc_count,
@@ -1434,16 +1615,20 @@ extern "C" int tfidf_set_global_df_device(tfidf_index *ix, const void *d_df, uin
                                    (unsigned long long)ix->n_sent);
   DeviceGuard g(ix->cfg.device);
   hipStream_t s = ix->stream;
+  if (int e = wait_gdf(ix)) return e;                  // the mirror buffer is about to be rewritten
   HIP_TRY(ix->gdf_dev.reserve((size_t)ix->C * 4));
   HIP_TRY(hipMemsetAsync(ix->gdf_dev.p, 0, (size_t)ix->C * 4, s));
   HIP_TRY(vocab_import(ix->sent_slot.as<uint32_t>(), (const uint32_t *)d_df, n, ix->gdf_dev.as<uint32_t>(), s));
-  ix->gdf.resize(ix->C);
+  // host mirror for query analysis: copied asynchronously, waited for by the
+  // first query (prepare_query) — the exchange itself needs no host sync
+  HIP_TRY(ix->gdf.resize(ix->C));
   HIP_TRY(hipMemcpyAsync(ix->gdf.data(), ix->gdf_dev.p, (size_t)ix->C * 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipStreamSynchronize(s));
+  HIP_TRY(hipEventRecord(ix->gdf_ev, s));
+  ix->gdf_pending = true;
   ix->has_global = true;
   ix->g_doc_count = doc_count;
   ix->g_sum_ttf = sum_ttf;
-  return upload_cache(ix);
+  return upload_cache(ix, false);
 }
 
 extern "C" int tfidf_set_global_stats_device(tfidf_index *ix, const void *d_df_canonical, uint64_t n_canonical,
@@ -1458,7 +1643,8 @@ extern "C" int tfidf_set_global_stats_device(tfidf_index *ix, const void *d_df_c
   HIP_TRY(gd.reserve((size_t)ix->C * 4));
   HIP_TRY(gather_df_canon((const uint32_t *)d_df_canonical, ix->canon_of_slot.as<uint32_t>(), ix->C,
                           gd.as<uint32_t>(), s));
-  ix->gdf.resize(ix->C);
+  HIP_TRY(wait_gdf(ix) == TFIDF_OK ? hipSuccess : hipErrorUnknown);
+  HIP_TRY(ix->gdf.resize(ix->C));
   HIP_TRY(hipMemcpyAsync(ix->gdf.data(), gd.p, (size_t)ix->C * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   gd.release();
@@ -1474,7 +1660,8 @@ extern "C" int tfidf_set_global_stats(tfidf_index *ix, const uint64_t *keys_lohi
   std::lock_guard<std::mutex> lk(ix->mu);
   if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
   DeviceGuard g(ix->cfg.device);
-  ix->gdf.assign(ix->C, 0);
+  if (int e = wait_gdf(ix)) return e;
+  HIP_TRY(ix->gdf.assign(ix->C, 0));
   for (uint32_t s = 0; s < ix->C; s++) ix->gdf[s] = ix->h_df[s];  // keys not listed keep local df
   for (uint64_t i = 0; i < n; i++) {
     const uint32_t s = host_lookup(ix, keys_lohi[2 * i], keys_lohi[2 * i + 1]);
@@ -1490,6 +1677,7 @@ extern "C" int tfidf_clear_global_stats(tfidf_index *ix) {
   if (!ix) return fail(TFIDF_E_INVALID_ARG, "NULL index");
   std::lock_guard<std::mutex> lk(ix->mu);
   DeviceGuard g(ix->cfg.device);
+  if (int e = wait_gdf(ix)) return e;
   ix->has_global = false;
   ix->gdf.clear();
   return ix->committed ? upload_cache(ix) : TFIDF_OK;
@@ -1498,29 +1686,79 @@ extern "C" int tfidf_clear_global_stats(tfidf_index *ix) {
 // ---------------------------------------------------------------------------
 // Leader.start merge (host: it merges per-worker result lists by name)
 
+// String.compareTo order of two UTF-8 names: Java compares UTF-16 code units,
+// so a supplementary code point (a surrogate pair, lead 0xD800..0xDBFF)
+// sorts below U+E000..U+FFFF although its code point is larger.  Code points
+// are compared with U+E000..U+FFFF lifted above the supplementary planes; a
+// malformed sequence compares by its bytes.
+static bool utf8_next(const uint8_t *s, uint64_t n, uint64_t *i, uint32_t *cp) {
+  const uint8_t c = s[*i];
+  uint32_t len = c < 0x80 ? 1 : (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : (c >> 3) == 30 ? 4 : 0;
+  if (!len || *i + len > n) return false;
+  uint32_t v = len == 1 ? c : c & (0x7Fu >> len);
+  for (uint32_t k = 1; k < len; k++) {
+    if ((s[*i + k] & 0xC0) != 0x80) return false;
+    v = (v << 6) | (s[*i + k] & 0x3F);
+  }
+  *i += len;
+  *cp = v;
+  return true;
+}
+
+static int utf16_compare(const uint8_t *a, uint64_t na, const uint8_t *b, uint64_t nb) {
+  uint64_t i = 0, j = 0;
+  while (i < na && j < nb) {
+    const uint64_t i0 = i, j0 = j;
+    uint32_t x, y;
+    if (!utf8_next(a, na, &i, &x) || !utf8_next(b, nb, &j, &y)) {   // malformed: bytes from here on
+      const uint64_t ra = na - i0, rb = nb - j0;
+      const int c = memcmp(a + i0, b + j0, std::min(ra, rb));
+      return c ? c : (ra < rb ? -1 : ra > rb);
+    }
+    if (x >= 0xE000 && x <= 0xFFFF) x += 0x100000;
+    if (y >= 0xE000 && y <= 0xFFFF) y += 0x100000;
+    if (x != y) return x < y ? -1 : 1;
+  }
+  return (na - i) == 0 && (nb - j) == 0 ? 0 : ((na - i) == 0 ? -1 : 1);
+}
+
+extern "C" int tfidf_sort_names(const uint8_t *names, const uint64_t *offsets, uint64_t n, uint64_t *perm) {
+  if (n && (!names || !offsets || !perm)) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  for (uint64_t i = 0; i < n; i++) perm[i] = i;
+  std::stable_sort(perm, perm + n, [&](uint64_t x, uint64_t y) {
+    return utf16_compare(names + offsets[x], offsets[x + 1] - offsets[x], names + offsets[y],
+                         offsets[y + 1] - offsets[y]) < 0;
+  });
+  return TFIDF_OK;
+}
+
 extern "C" int tfidf_leader_merge(const uint8_t *names, const uint64_t *offsets, uint64_t n, const double *scores,
                                   uint64_t *out_first, double *out_sum, uint64_t *n_out) {
   if (!n_out || (n && (!names || !offsets || !scores || !out_first || !out_sum)))
     return fail(TFIDF_E_INVALID_ARG, "NULL argument");
   std::unordered_map<std::string, size_t> pos;
-  std::vector<std::pair<std::string, uint64_t>> order;
+  std::vector<uint64_t> first;
   std::vector<double> sum;
   for (uint64_t i = 0; i < n; i++) {
     std::string k((const char *)names + offsets[i], offsets[i + 1] - offsets[i]);
     auto it = pos.find(k);
     if (it == pos.end()) {                   // HashMap.merge: first value stored as-is
-      pos.emplace(k, sum.size());
-      order.emplace_back(std::move(k), i);
+      pos.emplace(std::move(k), sum.size());
+      first.push_back(i);
       sum.push_back(scores[i]);
     } else {
       sum[it->second] += scores[i];          // Double::sum in response order
     }
   }
-  std::vector<size_t> idx(order.size());
+  std::vector<size_t> idx(first.size());
   for (size_t i = 0; i < idx.size(); i++) idx[i] = i;
-  std::sort(idx.begin(), idx.end(), [&](size_t a, size_t b) { return order[a].first < order[b].first; });
+  std::sort(idx.begin(), idx.end(), [&](size_t a, size_t b) {   // TreeMap<String, Double>: String.compareTo
+    const uint64_t x = first[a], y = first[b];
+    return utf16_compare(names + offsets[x], offsets[x + 1] - offsets[x], names + offsets[y],
+                         offsets[y + 1] - offsets[y]) < 0;
+  });
   for (size_t r = 0; r < idx.size(); r++) {
-    out_first[r] = order[idx[r]].second;
+    out_first[r] = first[idx[r]];
     out_sum[r] = sum[idx[r]];
   }
   *n_out = idx.size();

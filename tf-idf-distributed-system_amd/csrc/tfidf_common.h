@@ -36,6 +36,9 @@ constexpr uint32_t kRangeBits = 15;             // 32768 dictionary slots per LD
 constexpr uint32_t kRangeSlots = 1u << kRangeBits;
 constexpr uint32_t kBlockDocs = 8192;           // doc block of the inverted index / scorer
 constexpr uint32_t kInvalidSlot = 0xFFFFFFFFu;
+// query term roles after QueryParser + BooleanQuery.rewrite (analysis.h);
+// the scorer reads role << 24 | MUST clause index per term
+constexpr uint32_t kRoleShould = 0, kRoleMust = 1, kRoleNot = 2;
 constexpr uint32_t kMaxTf = (1u << 24) - 1;     // tf packs into 24 bits of a posting
 
 // Word_Break classes (ASCII) used by the tokenizer, one bit each.

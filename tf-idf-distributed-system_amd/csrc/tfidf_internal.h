@@ -129,6 +129,9 @@ struct QueryParams {
   const uint32_t *q_off;      // [n_q + 1] into q_slot / q_w
   const uint32_t *q_slot;     // dictionary slot per query term (kInvalidSlot = absent)
   const float *q_w;           // BM25 weight per query term (boost * idf)
+  const uint32_t *q_role;     // per query term: role << 24 | MUST clause index (kRole*, tfidf_common.h)
+  const uint32_t *q_meta;     // per query: MUST clause count | has MUST_NOT << 31 (0 = plain disjunction)
+  uint32_t ops;               // k_score_blocks: the operator-query variant (MUST / MUST_NOT clauses)
   uint32_t n_q;
   uint32_t q_chunk;           // queries per score_blocks workgroup
   uint32_t k;                 // top-k (1..1024); 0 = all hits
@@ -144,15 +147,27 @@ struct QueryParams {
   // wave-per-pair path (k > 0): pairs it leaves to k_score_blocks (nullptr = dense grid mode)
   uint32_t *ovf_list;         // pair ids q * n_blocks + b
   uint32_t *ovf_count;        // zeroed before k_score_pairs
+  uint32_t *ovf2_list;        // pairs of operator queries (q_meta != 0), for k_score_blocks<true>
+  uint32_t *ovf2_count;
   uint32_t list_grid;         // k_score_blocks workgroups in list mode
 };
 hipError_t launch_score_pairs(const QueryParams &p, int grid, hipStream_t s);
 constexpr uint32_t kPairWavesPerWG = 2;   // k_score_pairs workgroup = 2 waves (30 KB LDS: 5 per CU)
 hipError_t launch_score_blocks(const QueryParams &p, hipStream_t s);
 hipError_t launch_merge_topk(const QueryParams &p, hipStream_t s);
+// all hits: per-block sorted runs (k_score_blocks, k == 0) -> one ordered list:
+// (doc, score) split into out_doc / out_score, or packed keys with doc_base
+// added into keys_out (when non-null).  P: R + 1 u64; tmp0 / tmp1: n_blocks *
+// kBlockDocs u64 each (tmp1 may alias hits).
+hipError_t launch_pack_keys(const uint32_t *out_doc, const float *out_score, const uint32_t *out_n, uint32_t n_q,
+                            uint32_t k, uint64_t doc_base, uint64_t *keys, hipStream_t s);
+hipError_t launch_hits_order(const uint64_t *hits, const uint32_t *hits_n, uint32_t R, uint64_t *P, uint64_t *tmp0,
+                             uint64_t *tmp1, uint32_t *out_doc, float *out_score, uint64_t *keys_out,
+                             uint64_t doc_base, int grid, hipStream_t s);
 
 // --- GLOBAL statistics by term ownership (kernels_vocab.hip) ---
 hipError_t vocab_count(const uint64_t *dict, uint32_t C, uint32_t G, uint32_t *counts, hipStream_t s);
+hipError_t vocab_starts(const uint32_t *counts, uint32_t G, uint32_t *cursor, uint64_t *counts_out, hipStream_t s);
 hipError_t vocab_scatter(const uint64_t *dict, const uint32_t *df, uint32_t C, uint32_t G, uint32_t *cursor,
                          uint64_t *records, uint32_t *sent_slot, hipStream_t s);
 hipError_t vocab_reduce(const uint64_t *records, uint64_t n, uint64_t *table, uint32_t tmask, uint32_t *sums,

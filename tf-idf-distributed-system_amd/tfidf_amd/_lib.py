@@ -21,9 +21,12 @@ E_CAPACITY = 6
 E_STATE = 7
 E_BUFFER = 8
 E_NO_DEVICE = 9
+E_QUERY_SYNTAX = 10
 
 STATS_SHARD = 0
 STATS_GLOBAL = 1
+
+OWN_STREAM = C.c_void_p(-1 & ((1 << 64) - 1))   # TFIDF_OWN_STREAM
 
 INVERSION_AUTO = 0
 INVERSION_BLOCK = 1
@@ -61,6 +64,10 @@ class UnsupportedInput(TfidfError):
     pass
 
 
+class QuerySyntaxError(TfidfError):
+    """QueryParser ParseException / TooManyClauses: Worker.processDocuments answers []."""
+
+
 VP = C.c_void_p
 U8P = C.POINTER(C.c_uint8)
 U32P = C.POINTER(C.c_uint32)
@@ -85,6 +92,11 @@ SIGNATURES = {
     "tfidf_search": (C.c_int, [VP, C.c_char_p, C.c_uint64, C.c_uint32, U32P, F32P, C.c_uint64, U64P]),
     "tfidf_search_batch": (C.c_int, [VP, C.c_char_p, U64P, C.c_uint32, C.c_uint32, U32P, F32P, U32P]),
     "tfidf_last_search_ms": (C.c_int, [VP, F32P, F32P]),
+    "tfidf_search_batch_keys_device": (C.c_int, [VP, C.c_char_p, U64P, C.c_uint32, C.c_uint32, C.c_uint64, VP]),
+    "tfidf_search_all_keys_device": (C.c_int, [VP, C.c_char_p, C.c_uint64, C.c_uint64, VP, C.c_uint64, U64P]),
+    "tfidf_set_stream": (C.c_int, [VP, VP]),
+    "tfidf_doc_keys": (C.c_int, [VP, C.c_char_p, C.c_uint64, U64P, U64P]),
+    "tfidf_sort_names": (C.c_int, [C.c_char_p, U64P, C.c_uint64, U64P]),
     "tfidf_doc_key": (C.c_int, [VP, C.c_uint64, C.c_char_p, C.c_uint64, U64P]),
     "tfidf_doc_len": (C.c_int, [VP, C.c_uint64, U32P, U8P]),
     "tfidf_doc_terms": (C.c_int, [VP, C.c_uint64, C.c_char_p, C.c_uint64, U32P, C.c_uint64, U64P]),
@@ -93,8 +105,8 @@ SIGNATURES = {
     "tfidf_vocab_export_device": (C.c_int, [VP, VP, VP, C.c_uint64, U64P]),
     "tfidf_vocab_canonicalize_device": (C.c_int, [VP, VP, C.c_uint64, VP, C.c_uint64, U64P]),
     "tfidf_set_global_stats_device": (C.c_int, [VP, VP, C.c_uint64, C.c_uint64, C.c_uint64]),
-    "tfidf_vocab_partition_device": (C.c_int, [VP, C.c_uint32, VP, C.c_uint64, U64P, U64P]),
-    "tfidf_vocab_reduce_device": (C.c_int, [VP, VP, C.c_uint64, VP, U64P]),
+    "tfidf_vocab_partition_device": (C.c_int, [VP, C.c_uint32, VP, C.c_uint64, VP, U64P]),
+    "tfidf_vocab_reduce_device": (C.c_int, [VP, VP, C.c_uint64, VP, VP]),
     "tfidf_set_global_df_device": (C.c_int, [VP, VP, C.c_uint64, C.c_uint64, C.c_uint64]),
     "tfidf_set_global_stats": (C.c_int, [VP, U64P, U64P, C.c_uint64, C.c_uint64, C.c_uint64]),
     "tfidf_clear_global_stats": (C.c_int, [VP]),
@@ -136,6 +148,8 @@ def check(rc):
         raise UnsupportedQuery(rc, msg)
     if rc == E_UNSUPPORTED_INPUT:
         raise UnsupportedInput(rc, msg)
+    if rc == E_QUERY_SYNTAX:
+        raise QuerySyntaxError(rc, msg)
     raise TfidfError(rc, msg)
 
 

@@ -1,80 +1,107 @@
 """Multi-GPU orchestration: documents sharded across ranks (one process per
 GPU), exchanges over torch.distributed — backend "nccl" is RCCL over xGMI on
-MI355X; "gloo" is used by the CPU tests.
+MI355X; "gloo" is used by the CPU tests and one-GPU rehearsals.
 
 Two modes:
   * SHARD (the reference's N-worker semantics, Leader.java:39-92): every rank
-    scores with its own statistics; results are merged by document name.
-    No data-path collective.
+    scores with its own statistics and returns ALL its hits
+    (Worker.java:230, Integer.MAX_VALUE); the hits are summed by document
+    name in double, in rank (= worker response) order, and ordered by name
+    (TreeMap, String.compareTo).  shard_commit builds the name table once per
+    commit; shard_search does the per-query exchange and a device merge.
   * GLOBAL (the reference's 1-worker semantics on a sharded corpus):
       1. term ownership: every shard sends its (term key, df) records to the
          term's owner rank (all-to-all); the owner sums df over identical keys
          on device and answers record by record (all-to-all back);
-         {docCount, sumTTF} are all-reduced (SUM).  O(vocabulary) per rank.
-         (global_commit_canonical is the older all-gather + sorted-union form.)
-      2. per-rank top-k with global doc ids (shard base + local), all-gather,
-         merge by (score desc, doc asc).
+         {docCount, sumTTF} are summed.  O(vocabulary) per rank, one host
+         sync (the split sizes).  (global_commit_canonical is the older
+         all-gather + sorted-union form.)
+      2. per-rank top-k (or all hits) with global doc ids as packed merge keys
+         (score bits << 32 | ~doc) written by the engine into device memory,
+         all-gathered, merged on device by (score desc, doc asc).
 
 The engine is passed in as an adapter (HipShardAdapter in production; the
 CPU tests inject an oracle-backed adapter with the same methods).
 """
+import numpy as np
 import torch
 import torch.distributed as dist
 
 
 class HipShardAdapter:
-    """Adapter over a ShardIndex whose buffers live on ``device`` (cuda:N)."""
+    """Adapter over a ShardIndex whose buffers live on ``device`` (cuda:N).
+    The index issues its device work on torch's current stream of that device,
+    so library calls and collectives are stream-ordered without host syncs."""
 
     def __init__(self, shard, device, doc_base=0):
         self.shard = shard
         self.device = torch.device(device)
         self.doc_base = doc_base
+        self.shard.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
 
     def local_stats(self):
         s = self.shard.stats()
         return int(s["doc_count"]), int(s["sum_ttf"]), int(s["num_docs"])
 
+    # -- GLOBAL statistics (term ownership) --------------------------------
+    def vocab_partition(self, n_ranks):
+        """-> (records int64 [n, 3] (lo, hi, df) grouped by owner, counts int64 [n_ranks]), on device."""
+        n = self.shard.vocab_size()
+        rec = torch.empty((max(n, 1), 3), dtype=torch.int64, device=self.device)
+        cnt = torch.empty(n_ranks, dtype=torch.int64, device=self.device)
+        n2 = self.shard.vocab_partition_device(n_ranks, rec.data_ptr(), max(n, 1), cnt.data_ptr())
+        return rec[:n2], cnt
+
+    def vocab_reduce(self, records):
+        """Owner side: (summed df int32 per received record, distinct terms int64 [1]), on device."""
+        records = records.contiguous()
+        out = torch.empty(max(records.shape[0], 1), dtype=torch.int32, device=self.device)
+        nu = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.shard.vocab_reduce_device(records.data_ptr(), records.shape[0], out.data_ptr(), nu.data_ptr())
+        return out[:records.shape[0]], nu
+
+    def import_global_df(self, gdf, doc_count, sum_ttf):
+        gdf = gdf.contiguous()
+        self.shard.set_global_df_device(gdf.data_ptr(), gdf.shape[0], doc_count, sum_ttf)
+
+    # canonical (all-gather + sorted union) form
     def export_vocab(self):
         n = self.shard.vocab_size()
         keys = torch.zeros((max(n, 1), 2), dtype=torch.int64, device=self.device)
         df = torch.zeros(max(n, 1), dtype=torch.int32, device=self.device)
-        torch.cuda.synchronize(self.device)
         self.shard.vocab_export_device(keys.data_ptr(), df.data_ptr(), n)
         return keys[:n], df[:n]
 
     def canonicalize(self, all_keys):
         m = all_keys.shape[0]
         dfc = torch.zeros(max(m, 1), dtype=torch.int32, device=self.device)
-        torch.cuda.synchronize(self.device)
         n = self.shard.vocab_canonicalize_device(all_keys.data_ptr(), m, dfc.data_ptr(), max(m, 1))
         return dfc[:n]
 
-    def vocab_partition(self, n_ranks):
-        """-> (records int64 [n, 3] (lo, hi, df) grouped by owner, counts list)."""
-        n = self.shard.vocab_size()
-        rec = torch.zeros((max(n, 1), 3), dtype=torch.int64, device=self.device)
-        torch.cuda.synchronize(self.device)
-        n2, counts = self.shard.vocab_partition_device(n_ranks, rec.data_ptr(), max(n, 1))
-        return rec[:n2], [int(c) for c in counts]
-
-    def vocab_reduce(self, records):
-        """Owner side: (summed df int32 for every received record, distinct terms)."""
-        records = records.contiguous()
-        out = torch.zeros(max(records.shape[0], 1), dtype=torch.int32, device=self.device)
-        torch.cuda.synchronize(self.device)
-        nu = self.shard.vocab_reduce_device(records.data_ptr(), records.shape[0], out.data_ptr())
-        return out[:records.shape[0]], nu
-
-    def import_global_df(self, gdf, doc_count, sum_ttf):
-        gdf = gdf.contiguous()
-        torch.cuda.synchronize(self.device)
-        self.shard.set_global_df_device(gdf.data_ptr(), gdf.shape[0], doc_count, sum_ttf)
-
     def import_global(self, dfc, doc_count, sum_ttf):
         dfc = dfc.contiguous()
-        torch.cuda.synchronize(self.device)
         self.shard.set_global_stats_device(dfc.data_ptr(), dfc.shape[0], doc_count, sum_ttf)
 
+    # -- search: packed merge keys in device memory ----------------------------
+    def topk_keys(self, queries, k):
+        """int64 [n_q, k] merge keys (global doc ids), 0 = empty slot."""
+        keys = torch.empty((len(queries), k), dtype=torch.int64, device=self.device)
+        self.shard.search_batch_keys_device(queries, k, self.doc_base, keys.data_ptr())
+        return keys
+
+    def all_keys(self, query, doc_base=None):
+        """int64 [H] merge keys of every hit, ordered (score desc, doc asc)."""
+        n = max(self.shard.stats()["num_docs"], 1)
+        keys = torch.empty(n, dtype=torch.int64, device=self.device)
+        h = self.shard.search_all_keys_device(query, self.doc_base if doc_base is None else doc_base,
+                                              keys.data_ptr(), n)
+        return keys[:h]
+
+    def doc_names(self):
+        """(uint8 blob, uint64 offsets[num_docs + 1]) of the shard's document keys."""
+        return self.shard.doc_keys()
+
+    # host-array forms (tools)
     def search_topk(self, query, k):
         return self.shard.search_arrays(query, k)
 
@@ -89,9 +116,13 @@ def _dev(adapter):
     return adapter.device if isinstance(adapter.device, torch.device) else torch.device(adapter.device)
 
 
+def _host_coll(group):
+    """gloo collectives run on host tensors here (the CPU tests and the one-GPU rehearsal)."""
+    return dist.get_backend(group) == "gloo"
+
+
 def _a2a(out, inp, out_splits, in_splits, group):
-    """all_to_all_single; gloo (CPU rehearsal) needs host tensors."""
-    if dist.get_backend(group) == "gloo" and inp.is_cuda:
+    if _host_coll(group) and inp.is_cuda:
         o = out.cpu()
         dist.all_to_all_single(o, inp.cpu(), output_split_sizes=out_splits, input_split_sizes=in_splits,
                                group=group)
@@ -100,84 +131,113 @@ def _a2a(out, inp, out_splits, in_splits, group):
         dist.all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits, group=group)
 
 
-def global_commit(adapter, group=None):
-    """Step 1 of GLOBAL mode (term ownership).  Call after the shard's own
-    commit.  Returns (global vocabulary size, docCount, sumTTF)."""
+def _all_gather(t, group):
+    """-> tensor [world, *t.shape] (same device as t)."""
+    ws = dist.get_world_size(group)
+    if _host_coll(group):
+        src = t.detach().cpu().contiguous()
+        parts = [torch.empty_like(src) for _ in range(ws)]
+        dist.all_gather(parts, src, group=group)
+        return torch.stack(parts).to(t.device)
+    out = torch.empty((ws,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(out, t.contiguous(), group=group)
+    return out
+
+
+def _all_gather_var(t, n, group):
+    """Rows [0, n) of t from every rank -> (tensor [sum n_r, ...] in rank order, [n_r]).
+    One host read (the counts)."""
+    ns = _all_gather(torch.tensor([n], dtype=torch.int64, device=t.device), group).view(-1).tolist()
+    m = max(max(ns), 1)
+    pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+    pad[:n] = t[:n]
+    g = _all_gather(pad, group)
+    return torch.cat([g[r, :ns[r]] for r in range(len(ns))], 0), ns
+
+
+def global_commit(adapter, group=None, vocab_size=False):
+    """GLOBAL statistics by term ownership; call after the shard's own commit.
+    Returns (global vocabulary size or None, docCount, sumTTF).  Host syncs:
+    one read of the gathered [per-owner counts | docCount | sumTTF] rows (the
+    all-to-all split sizes), plus one more only when vocab_size is asked for."""
     dev = _dev(adapter)
     ws = dist.get_world_size(group)
-    rec, counts = adapter.vocab_partition(ws)
-    cnt = torch.tensor(counts, dtype=torch.int64, device=dev)
-    rcnt = torch.empty_like(cnt)
-    _a2a(rcnt, cnt, None, None, group)
-    rcounts = [int(x) for x in rcnt.tolist()]
-    recv = torch.empty((sum(rcounts), 3), dtype=torch.int64, device=dev)
-    _a2a(recv, rec.contiguous(), rcounts, counts, group)
-    ans, n_own = adapter.vocab_reduce(recv)
-    back = torch.empty(sum(counts), dtype=torch.int32, device=dev)
-    _a2a(back, ans.contiguous(), counts, rcounts, group)
-    dc, ttf, _ = adapter.local_stats()
-    st = torch.tensor([dc, ttf, n_own], dtype=torch.int64, device=dev)
-    dist.all_reduce(st, op=dist.ReduceOp.SUM, group=group)
-    adapter.import_global_df(back, int(st[0].item()), int(st[1].item()))
-    return int(st[2].item()), int(st[0].item()), int(st[1].item())
+    me = dist.get_rank(group)
+    dc, ttf, _ = adapter.local_stats()                      # host values of the shard's commit
+    rec, cnt = adapter.vocab_partition(ws)                  # device, asynchronous
+    meta = torch.cat([cnt.to(torch.int64), torch.tensor([dc, ttf], dtype=torch.int64, device=dev)])
+    M = _all_gather(meta, group).cpu().tolist()             # the host sync
+    send = [int(x) for x in M[me][:ws]]
+    recv = [int(M[r][me]) for r in range(ws)]
+    gdc = sum(int(M[r][ws]) for r in range(ws))
+    gttf = sum(int(M[r][ws + 1]) for r in range(ws))
+    got = torch.empty((sum(recv), 3), dtype=torch.int64, device=dev)
+    _a2a(got, rec.contiguous(), recv, send, group)
+    ans, nu = adapter.vocab_reduce(got)
+    back = torch.empty(sum(send), dtype=torch.int32, device=dev)
+    _a2a(back, ans.contiguous(), send, recv, group)
+    adapter.import_global_df(back, gdc, gttf)
+    n_vocab = None
+    if vocab_size:
+        nu = nu.clone()
+        if _host_coll(group) and nu.is_cuda:
+            h = nu.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+            n_vocab = int(h.item())
+        else:
+            dist.all_reduce(nu, op=dist.ReduceOp.SUM, group=group)
+            n_vocab = int(nu.item())
+    return n_vocab, gdc, gttf
 
 
 def global_commit_canonical(adapter, group=None):
     """All-gather + sorted-union form of GLOBAL statistics (canonical term
     ids; O(G x vocabulary) per rank).  Same results as global_commit."""
     dev = _dev(adapter)
-    ws = dist.get_world_size(group)
     keys, df = adapter.export_vocab()
-    n = torch.tensor([keys.shape[0]], dtype=torch.int64, device=dev)
-    ns = [torch.zeros_like(n) for _ in range(ws)]
-    dist.all_gather(ns, n, group=group)
-    m = int(max(int(x.item()) for x in ns))
-    padded = torch.zeros((max(m, 1), 2), dtype=torch.int64, device=dev)   # hi == 0 rows are dropped
-    padded[:keys.shape[0]] = keys
-    gathered = [torch.zeros_like(padded) for _ in range(ws)]
-    dist.all_gather(gathered, padded, group=group)
-    all_keys = torch.cat(gathered, 0).contiguous()
+    padded, ns = _all_gather_var(keys, keys.shape[0], group)
+    all_keys = padded.contiguous()
     dfc = adapter.canonicalize(all_keys)
-    dist.all_reduce(dfc, op=dist.ReduceOp.SUM, group=group)
+    if _host_coll(group) and dfc.is_cuda:
+        h = dfc.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+        dfc.copy_(h)
+    else:
+        dist.all_reduce(dfc, op=dist.ReduceOp.SUM, group=group)
     dc, ttf, _ = adapter.local_stats()
     st = torch.tensor([dc, ttf], dtype=torch.int64, device=dev)
-    dist.all_reduce(st, op=dist.ReduceOp.SUM, group=group)
-    adapter.import_global(dfc, int(st[0].item()), int(st[1].item()))
-    return int(dfc.shape[0]), int(st[0].item()), int(st[1].item())
+    st = _all_gather(st, group).sum(0).tolist()
+    adapter.import_global(dfc, int(st[0]), int(st[1]))
+    return int(dfc.shape[0]), int(st[0]), int(st[1])
+
+
+def _keys_to_hits(keys):
+    """Descending merge keys (int64, > 0) -> [(global doc, float score)]."""
+    k = keys.cpu().numpy().view(np.uint64)
+    doc = (~k & np.uint64(0xFFFFFFFF)).astype(np.int64)
+    sc = (k >> np.uint64(32)).astype(np.uint32).view(np.float32)
+    return list(zip(doc.tolist(), sc.tolist()))
 
 
 def global_search(adapter, query: bytes, k: int, group=None):
-    """Step 3: per-rank top-k, all-gather, merge.  Returns [(global doc, score)]."""
-    dev = _dev(adapter)
-    ws = dist.get_world_size(group)
-    docs, scores = adapter.search_topk(query, k)
-    n = len(docs)
-    keyed = torch.zeros((k, 2), dtype=torch.int64, device=dev)
-    if n:
-        keyed[:n, 0] = torch.as_tensor(docs.astype("int64") + adapter.doc_base, device=dev)
-        keyed[:n, 1] = torch.as_tensor(scores.view("int32").astype("int64"), device=dev)
-    cnt = torch.tensor([n], dtype=torch.int64, device=dev)
-    cnts = [torch.zeros_like(cnt) for _ in range(ws)]
-    dist.all_gather(cnts, cnt, group=group)
-    outs = [torch.zeros_like(keyed) for _ in range(ws)]
-    dist.all_gather(outs, keyed, group=group)
-    import numpy as np
-    cands = []
-    for c, o in zip(cnts, outs):
-        c = int(c.item())
-        arr = o[:c].cpu().numpy()
-        for d, sb in arr.tolist():
-            cands.append((np.int32(sb).view(np.float32).item(), d))
-    cands.sort(key=lambda x: (-x[0], x[1]))
-    return [(d, s) for s, d in cands[:k]]
+    """Per-rank top-k (k >= 1) or every hit (k == 0, searcher.search(q,
+    Integer.MAX_VALUE)) with global doc ids; all-gather of the packed keys;
+    device merge.  Returns [(global doc, score)] in (score desc, doc asc)."""
+    if k == 0:
+        mine = adapter.all_keys(query)
+        allk, _ = _all_gather_var(mine, mine.shape[0], group)
+        allk = torch.sort(allk, descending=True).values
+        return _keys_to_hits(allk)
+    mine = adapter.topk_keys([query], k)[0]
+    allk = _all_gather(mine, group).view(-1)
+    top = torch.topk(allk, min(k, allk.numel()), largest=True, sorted=True).values
+    return _keys_to_hits(top[top != 0])
 
 
 def merge_keys(docs, scores, counts, doc_base, device):
-    """Per-rank batch top-k -> int64 merge keys [n_q, k] on ``device``:
-    (float32 score bits << 32) | ~global_doc.  BM25 scores are > 0, so the
-    integer order of the keys is (score desc, doc asc) descending, the
-    reference's HitQueue order; empty slots are 0."""
-    import numpy as np
+    """Per-rank batch top-k host arrays -> int64 merge keys [n_q, k] on
+    ``device``: (float32 score bits << 32) | ~global_doc; empty slots 0
+    (adapters without device key output)."""
     nq, k = docs.shape
     valid = np.arange(k)[None, :] < counts.astype(np.int64)[:, None]
     g = (docs.astype(np.uint64) + np.uint64(doc_base)) & np.uint64(0xFFFFFFFF)
@@ -187,25 +247,93 @@ def merge_keys(docs, scores, counts, doc_base, device):
 
 
 def global_search_batch(adapter, queries, k: int, group=None):
-    """Batched step 3 (cfg 3/4): every rank scores the whole batch on its
-    shard, the [n_q, k] merge keys are all-gathered once (one RCCL
-    collective for the batch) and the global top-k of each query is a device
-    top-k over the ws*k candidates.  Returns (docs int64[n_q, k], scores
-    float32[n_q, k], counts int64[n_q]) as numpy arrays (global doc ids)."""
-    import numpy as np
-    dev = _dev(adapter)
-    ws = dist.get_world_size(group)
-    docs, scores, counts = adapter.search_batch(queries, k)
-    mine = merge_keys(docs, scores, counts, adapter.doc_base, dev)
-    outs = [torch.empty_like(mine) for _ in range(ws)]
-    dist.all_gather(outs, mine, group=group)
-    allk = torch.cat(outs, dim=1)                                   # [n_q, ws * k]
+    """Batched step 2 (cfg 3/4): every rank scores the whole batch on its
+    shard into device merge keys, the [n_q, k] keys are all-gathered once (one
+    RCCL collective for the batch) and the global top-k of each query is a
+    device top-k over the ws*k candidates.  Returns (docs int64[n_q, k],
+    scores float32[n_q, k], counts int64[n_q]) as numpy arrays (global doc ids)."""
+    mine = adapter.topk_keys(queries, k)                            # [n_q, k] on device
+    allk = _all_gather(mine, group)                                 # [ws, n_q, k]
+    allk = allk.permute(1, 0, 2).reshape(len(queries), -1)          # [n_q, ws * k]
     top = torch.topk(allk, k, dim=1, largest=True, sorted=True).values
     top = top.cpu().numpy().view(np.uint64)
     cnt = (top != 0).sum(axis=1)
     gdoc = (~top & np.uint64(0xFFFFFFFF)).astype(np.int64)
     sc = (top >> np.uint64(32)).astype(np.uint32).view(np.float32)
     return gdoc, sc, cnt
+
+
+# ---------------------------------------------------------------------------
+# SHARD mode: the reference's N workers (Leader.java:39-92)
+
+class ShardNames:
+    """Global document-name table of SHARD mode: every distinct name of every
+    rank, sorted by String.compareTo (TreeMap order); ``local_ids`` maps this
+    rank's local doc ids to name ids (device int64)."""
+
+    def __init__(self, names, local_ids):
+        self.names = names
+        self.local_ids = local_ids
+
+
+def shard_commit(adapter, group=None):
+    """Once per commit (SHARD mode): all-gather the document names, sort their
+    union by String.compareTo (tfidf_sort_names), map local docs to name ids."""
+    from .engine import sort_names
+    dev = _dev(adapter)
+    blob, offs = adapter.doc_names()
+    n = len(offs) - 1
+    lens = torch.from_numpy((offs[1:] - offs[:-1]).astype(np.int64))
+    all_lens, ns = _all_gather_var(lens.to(dev), n, group)
+    all_blob, _ = _all_gather_var(torch.from_numpy(np.ascontiguousarray(blob, np.uint8)).to(dev), len(blob), group)
+    all_lens = all_lens.cpu().numpy()
+    all_blob = all_blob.cpu().numpy()
+    aoffs = np.zeros(len(all_lens) + 1, np.uint64)
+    aoffs[1:] = np.cumsum(all_lens, dtype=np.uint64)
+    perm = sort_names(all_blob, aoffs)
+    names, nid = [], np.zeros(len(all_lens), np.int64)
+    prev = None
+    for p in perm.tolist():
+        nm = all_blob[int(aoffs[p]):int(aoffs[p + 1])].tobytes()
+        if nm != prev:
+            names.append(nm)
+            prev = nm
+        nid[p] = len(names) - 1
+    me = dist.get_rank(group)
+    lo = int(sum(ns[:me]))
+    return ShardNames(names, torch.from_numpy(nid[lo:lo + n]).to(dev))
+
+
+def shard_search(adapter, names: ShardNames, query: bytes, group=None):
+    """Leader.start over the ranks: each rank's every hit under its own
+    statistics, all-gathered; per name the scores ((double) of the float) are
+    summed in rank order (HashMap.merge Double::sum, Leader.java:73-77) and the
+    result is ordered by name (TreeMap, :80-88).  Returns [(name, score)]."""
+    ws = dist.get_world_size(group)
+    keys = adapter.all_keys(query, doc_base=0)                      # local doc ids
+    doc = (~keys) & 0xFFFFFFFF
+    rec = torch.stack([names.local_ids[doc], keys >> 32], 1)        # (name id, score bits)
+    allr, ns = _all_gather_var(rec, rec.shape[0], group)            # rank order
+    if allr.shape[0] == 0:
+        return []
+    nid = allr[:, 0]
+    val = allr[:, 1].to(torch.int32).view(torch.float32).to(torch.float64)
+    nid_s, order = torch.sort(nid, stable=True)                     # rank order kept within a name
+    val_s = val[order]
+    first = torch.ones_like(nid_s, dtype=torch.bool)
+    first[1:] = nid_s[1:] != nid_s[:-1]
+    seg = torch.cumsum(first.to(torch.int64), 0) - 1
+    pos = torch.arange(nid_s.numel(), device=nid_s.device)
+    start = torch.zeros(int(seg[-1]) + 1, dtype=torch.int64, device=nid_s.device)
+    start[seg[first]] = pos[first]
+    occ = pos - start[seg]                                          # 0 .. ws-1 within a name
+    sums = torch.zeros(start.numel(), dtype=torch.float64, device=nid_s.device)
+    for j in range(ws):                                             # Double::sum in response order
+        m = occ == j
+        if bool(m.any()):
+            sums.index_add_(0, seg[m], val_s[m])
+    uid = nid_s[first].cpu().tolist()
+    return [(names.names[u], float(s)) for u, s in zip(uid, sums.cpu().tolist())]
 
 
 def shard_range(n_docs, rank, world):

@@ -128,6 +128,18 @@ class ShardIndex:
         m = n.value
         return list(zip(docs[:m].tolist(), scores[:m].tolist()))
 
+    def search_all_arrays(self, query: bytes):
+        """All hits as (doc uint32[], score float32[]) in (score desc, doc asc)
+        — searcher.search(q, Integer.MAX_VALUE) without per-hit Python objects."""
+        lib = L.load()
+        cap = max(self.stats()["num_docs"], 1)
+        docs = np.empty(cap, np.uint32)
+        scores = np.empty(cap, np.float32)
+        n = C.c_uint64()
+        L.check(lib.tfidf_search(self._h, query, len(query), 0, L.ptr(docs, C.c_uint32), L.ptr(scores, C.c_float),
+                                 cap, C.byref(n)))
+        return docs[:n.value], scores[:n.value]
+
     def search_arrays(self, query: bytes, k):
         lib = L.load()
         docs = np.zeros(max(k, 1), np.uint32)
@@ -150,6 +162,25 @@ class ShardIndex:
                                             L.ptr(counts, C.c_uint32)))
         return docs, scores, counts
 
+    def search_batch_keys_device(self, queries, k, doc_base, d_keys):
+        """n_q x k merge keys (score bits << 32 | ~(doc_base + doc)) into device memory d_keys."""
+        nq = len(queries)
+        offs = np.zeros(nq + 1, np.uint64)
+        offs[1:] = np.cumsum([len(q) for q in queries], dtype=np.uint64)
+        L.check(L.load().tfidf_search_batch_keys_device(self._h, b"".join(queries), L.ptr(offs, C.c_uint64), nq, k,
+                                                        doc_base, C.c_void_p(d_keys)))
+
+    def search_all_keys_device(self, query: bytes, doc_base, d_keys, cap):
+        """Every hit's merge key, ordered, into device memory (cap >= num_docs); -> #hits."""
+        n = C.c_uint64()
+        L.check(L.load().tfidf_search_all_keys_device(self._h, query, len(query), doc_base, C.c_void_p(d_keys), cap,
+                                                      C.byref(n)))
+        return n.value
+
+    def set_stream(self, stream):
+        """Issue device work on the caller's HIP stream (int handle); None = the index's own stream."""
+        L.check(L.load().tfidf_set_stream(self._h, L.OWN_STREAM if stream is None else C.c_void_p(stream)))
+
     def last_search_ms(self):
         a, b = C.c_float(), C.c_float()
         L.check(L.load().tfidf_last_search_ms(self._h, C.byref(a), C.byref(b)))
@@ -161,6 +192,19 @@ class ShardIndex:
         n = C.c_uint64()
         L.check(L.load().tfidf_doc_key(self._h, doc, buf, 4096, C.byref(n)))
         return buf.raw[:n.value]
+
+    def doc_keys(self):
+        """Every committed document's key: (uint8 blob, uint64 offsets[num_docs + 1])."""
+        lib = L.load()
+        n = self.stats()["num_docs"]
+        offs = np.zeros(n + 1, np.uint64)
+        need = C.c_uint64()
+        rc = lib.tfidf_doc_keys(self._h, None, 0, L.ptr(offs, C.c_uint64), C.byref(need))
+        if rc not in (L.OK, L.E_BUFFER):
+            L.check(rc)
+        buf = C.create_string_buffer(max(need.value, 1))
+        L.check(lib.tfidf_doc_keys(self._h, buf, need.value, L.ptr(offs, C.c_uint64), C.byref(need)))
+        return np.frombuffer(buf.raw[:need.value], np.uint8).copy(), offs
 
     def doc_len(self, doc):
         ln, nm = C.c_uint32(), C.c_uint8()
@@ -203,20 +247,18 @@ class ShardIndex:
         L.check(L.load().tfidf_set_global_stats_device(self._h, C.c_void_p(d_df_canon), n_canon, doc_count,
                                                        sum_ttf))
 
-    def vocab_partition_device(self, n_ranks, d_records, cap):
-        """Records (lo, hi, df) grouped by owner rank -> (n, counts[n_ranks])."""
-        counts = np.zeros(n_ranks, np.uint64)
+    def vocab_partition_device(self, n_ranks, d_records, cap, d_counts):
+        """Records (lo, hi, df) grouped by owner rank into d_records, per-owner
+        counts (u64) into d_counts; asynchronous on the index's stream -> n records."""
         n = C.c_uint64()
         L.check(L.load().tfidf_vocab_partition_device(self._h, n_ranks, C.c_void_p(d_records), cap,
-                                                      L.ptr(counts, C.c_uint64), C.byref(n)))
-        return n.value, counts
+                                                      C.c_void_p(d_counts), C.byref(n)))
+        return n.value
 
-    def vocab_reduce_device(self, d_records, n, d_df_out):
-        """-> distinct terms among the records."""
-        u = C.c_uint64()
+    def vocab_reduce_device(self, d_records, n, d_df_out, d_n_unique=None):
+        """Owner side: summed df per received record (asynchronous)."""
         L.check(L.load().tfidf_vocab_reduce_device(self._h, C.c_void_p(d_records), n, C.c_void_p(d_df_out),
-                                                   C.byref(u)))
-        return u.value
+                                                   C.c_void_p(d_n_unique) if d_n_unique else None))
 
     def set_global_df_device(self, d_df, n, doc_count, sum_ttf):
         L.check(L.load().tfidf_set_global_df_device(self._h, C.c_void_p(d_df), n, doc_count, sum_ttf))
@@ -229,6 +271,16 @@ class ShardIndex:
 
     def clear_global_stats(self):
         L.check(L.load().tfidf_clear_global_stats(self._h))
+
+
+def sort_names(blob, offsets):
+    """Permutation of the names blob[offsets[i]:offsets[i+1]] in String.compareTo order."""
+    n = len(offsets) - 1
+    blob = np.ascontiguousarray(blob, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    perm = np.zeros(max(n, 1), np.uint64)
+    L.check(L.load().tfidf_sort_names(blob.tobytes(), L.ptr(offsets, C.c_uint64), n, L.ptr(perm, C.c_uint64)))
+    return perm[:n]
 
 
 def leader_merge(responses):
