@@ -153,7 +153,11 @@ template <bool kOps> struct ScoreSmem {
 // BlockMaxConjunctionScorer); SHOULD terms add (float) of their double sum in
 // float (ReqOptSumScorer) when one matches; MUST_NOT excludes (ReqExclScorer).
 // Without MUST clauses a document needs a SHOULD match: the plain disjunction.
-template <bool kOps>
+//
+// kAll: all-hits mode (k == 0) as its own instantiation — its LDS sort code
+// made the compiler schedule the top-k instantiation's loops worse (10 k-query
+// batch: 12.4 -> 16.0 ms when they shared one kernel).
+template <bool kOps, bool kAll>
 __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
   __shared__ ScoreSmem<kOps> sm;
   const uint32_t tid = threadIdx.x;
@@ -325,7 +329,7 @@ __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
     __syncthreads();
     const uint32_t nhit = sm.nhit;
     const uint32_t bits = (sm.hitbits[tid >> 1] >> (16 * (tid & 1))) & 0xFFFFu;
-    if (k == 0) {
+    if (kAll) {
       // all-hits mode (single query): the block's hit keys (score bits << 32 |
       // ~doc), compacted and sorted descending in LDS (bitonic over the
       // accumulator's 64 KiB) -> one sorted run per block for k_merge_runs
@@ -949,10 +953,13 @@ hipError_t launch_score_pairs(const QueryParams &p, int grid, hipStream_t s) {
 
 hipError_t launch_score_blocks(const QueryParams &p, hipStream_t s) {
   const dim3 grid = p.ovf_list ? dim3(p.list_grid) : dim3(p.n_blocks, (p.n_q + p.q_chunk - 1) / p.q_chunk);
-  if (p.ops)
-    hipLaunchKernelGGL(k_score_blocks<true>, grid, dim3(kScoreThreads), 0, s, p);
-  else
-    hipLaunchKernelGGL(k_score_blocks<false>, grid, dim3(kScoreThreads), 0, s, p);
+  if (p.k == 0) {
+    if (p.ops) hipLaunchKernelGGL((k_score_blocks<true, true>), grid, dim3(kScoreThreads), 0, s, p);
+    else hipLaunchKernelGGL((k_score_blocks<false, true>), grid, dim3(kScoreThreads), 0, s, p);
+  } else {
+    if (p.ops) hipLaunchKernelGGL((k_score_blocks<true, false>), grid, dim3(kScoreThreads), 0, s, p);
+    else hipLaunchKernelGGL((k_score_blocks<false, false>), grid, dim3(kScoreThreads), 0, s, p);
+  }
   return hipGetLastError();
 }
 hipError_t launch_merge_topk(const QueryParams &p, hipStream_t s) {
