@@ -96,6 +96,7 @@ typedef struct tfidf_index_stats {
   uint64_t pack_docs;     /* documents per tokenizer window in the last commit (1 = one per window) */
   uint64_t pack_retried;  /* documents the packed windows handed to the one-per-window pass */
   uint64_t unicode_docs;  /* documents (window <= 4 KB) the ASCII wave path handed to the Unicode wave path */
+  uint64_t long_chunked;  /* long documents indexed chunk-parallel (the rest of long_docs: k_tokenize_long) */
 } tfidf_index_stats;
 
 /* Per-phase device times of the last commit, measured with HIP events on the

@@ -522,16 +522,40 @@ static int cmp_term_ids(const void *a, const void *b, void *ctx) {
   return strcmp(st_str(t, x), st_str(t, y));
 }
 
-/* qsort_r is a GNU extension; keep a small insertion+merge sort instead. */
+/* Per-document term order (bytes): bottom-up merge sort of (term id, tf)
+ * pairs keyed by the term strings (qsort_r is a GNU extension; the context
+ * is passed explicitly so concurrent indexes on several threads are safe). */
 static void sort_terms(uint32_t *ids, uint32_t *tfs, uint64_t n, const strtab *t) {
-  for (uint64_t i = 1; i < n; i++) {
-    uint32_t a = ids[i], f = tfs[i];
-    uint64_t j = i;
-    while (j > 0 && cmp_term_ids(&ids[j - 1], &a, (void *)t) > 0) {
-      ids[j] = ids[j - 1]; tfs[j] = tfs[j - 1]; j--;
+  if (n < 2) return;
+  uint32_t *bi = (uint32_t *)malloc(n * 4), *bt = (uint32_t *)malloc(n * 4);
+  if (!bi || !bt) {                                  /* out of memory: insertion sort in place */
+    free(bi); free(bt);
+    for (uint64_t i = 1; i < n; i++) {
+      uint32_t a = ids[i], f = tfs[i];
+      uint64_t j = i;
+      while (j > 0 && cmp_term_ids(&ids[j - 1], &a, (void *)t) > 0) { ids[j] = ids[j - 1]; tfs[j] = tfs[j - 1]; j--; }
+      ids[j] = a; tfs[j] = f;
     }
-    ids[j] = a; tfs[j] = f;
+    return;
   }
+  uint32_t *si = ids, *st = tfs, *di = bi, *dt = bt;
+  for (uint64_t w = 1; w < n; w *= 2) {
+    for (uint64_t lo = 0; lo < n; lo += 2 * w) {
+      uint64_t mid = lo + w < n ? lo + w : n, hi = lo + 2 * w < n ? lo + 2 * w : n;
+      uint64_t a = lo, b = mid, o = lo;
+      while (a < mid && b < hi) {
+        if (cmp_term_ids(&si[b], &si[a], (void *)t) < 0) { di[o] = si[b]; dt[o] = st[b]; b++; }
+        else { di[o] = si[a]; dt[o] = st[a]; a++; }
+        o++;
+      }
+      while (a < mid) { di[o] = si[a]; dt[o] = st[a]; a++; o++; }
+      while (b < hi) { di[o] = si[b]; dt[o] = st[b]; b++; o++; }
+    }
+    uint32_t *x = si; si = di; di = x;
+    x = st; st = dt; dt = x;
+  }
+  if (si != ids) { memcpy(ids, si, n * 4); memcpy(tfs, st, n * 4); }
+  free(bi); free(bt);
 }
 
 int orc_commit(orc_index *ix) {

@@ -822,6 +822,140 @@ __device__ __forceinline__ void hist_batch(WaveSmem &sm, const BuildParams &p, u
   }
 }
 
+// Dictionary slots of the document's distinct terms (table entries listed in
+// slots[0, nu)): lane l resolves terms l + 64k (k < kWaveK) -> g[k], with
+// their counts tf[k] (and, PACK, the pack-local document tdoc[k]; per-document
+// lengths / term counts accumulated into pk_len / pk_nu).  Short keys by
+// bucket probes with all of a lane's loads in flight, unresolved ones through
+// a one-per-lane retry queue; folded (> 8 byte) keys one per lane at a time.
+template <bool PACK>
+__device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p, uint32_t lane, uint32_t nu,
+                                              uint32_t doc, uint32_t *g, uint32_t *tf, uint32_t *tdoc,
+                                              uint32_t &actm, uint32_t *pk_len, uint32_t *pk_nu) {
+  const uint32_t dmask = p.cap_mask;
+  const uint16_t *slots = reinterpret_cast<const uint16_t *>(sm.list);
+  if (PACK && lane < kPackMax) { pk_len[lane] = 0; pk_nu[lane] = 0; }
+  {
+    uint64_t lo[kWaveK];
+    uint32_t ps[kWaveK];
+    uint32_t foldm = 0;
+#pragma unroll
+    for (int k = 0; k < (int)kWaveK; k++) {
+      lo[k] = 0;
+      tf[k] = 0;
+      g[k] = kInvalidSlot;
+      ps[k] = 0;
+      {
+        const uint32_t idx = lane + 64 * k;
+        const bool in = idx < nu;
+        const uint32_t s = slots[in ? idx : 0u] & (kWaveSlots - 1);
+        const uint64_t key = sm.key[s];
+        tf[k] = (sm.cnt[s >> 1] >> (16 * (s & 1))) & 0xFFFFu;
+        const bool f = in & ((key & kFoldBit) != 0);
+        const bool sh = in & !f;
+        tdoc[k] = PACK ? key_doc(key) : 0u;
+        if (PACK && in) { atomicAdd(&pk_len[tdoc[k]], tf[k]); atomicAdd(&pk_nu[tdoc[k]], 1u); }
+        lo[k] = sh ? (PACK ? key & ~kPackTagMask : key) : 0ull;
+        foldm |= (uint32_t)f << k;
+        actm |= (uint32_t)in << k;
+        ps[k] = dict_home(dict_hash_short(lo[k]), dmask) & ~1u;
+        g[k] = sh ? kLookupPending : g[k];
+      }
+    }
+    // folded (> 8 byte) terms: exact 128-bit keys, one lookup per lane at a time
+    while (__any(foldm != 0)) {
+      uint64_t flo = 1, fhi = kKeyValid;
+      uint32_t k = 0;
+      const bool fa = foldm != 0;
+      if (fa) {
+        k = (uint32_t)__builtin_ctz(foldm);
+        foldm &= foldm - 1;
+        const uint64_t key = sm.key[slots[lane + 64 * k]];
+        const uint32_t n = (uint32_t)key & 0xFFu, tp = (uint32_t)(key >> 13) & 0x1FFFu;
+        bool valid;
+        token_key(sm.text, tp, tp + n, &flo, &fhi, &valid);
+      }
+      const uint32_t gg = dict_find_or_insert(p.dict, dmask, flo, fhi, fa);
+#pragma unroll
+      for (int kk = 0; kk < (int)kWaveK; kk++)
+        if (fa && (uint32_t)kk == k) g[kk] = gg;
+    }
+    // short terms: bucket probes, all of a lane's loads in flight per round
+    for (uint32_t round = 0;; round++) {
+      uint32_t np = 0;
+#pragma unroll
+      for (int k = 0; k < (int)kWaveK; k++) np += g[k] == kLookupPending;
+      const uint32_t pincl = wave_incl_add(np);
+      const uint32_t P = (uint32_t)__builtin_amdgcn_readlane((int)pincl, 63);
+      if (P == 0) break;
+      if (round > 0 && P <= kDictQueue) {
+        // retry queue in the (no longer needed) table: (lo, probe slot, term index)
+        uint64_t *qlo = sm.key;
+        uint2 *qmeta = reinterpret_cast<uint2 *>(sm.key + kDictQueue);
+        uint32_t *res = reinterpret_cast<uint32_t *>(sm.key + 2 * kDictQueue);
+        uint32_t at = pincl - np;
+#pragma unroll
+        for (int k = 0; k < (int)kWaveK; k++)
+          if (g[k] == kLookupPending) { qlo[at] = lo[k]; qmeta[at] = make_uint2(ps[k], lane + 64 * k); at++; }
+        asm volatile("" ::: "memory");
+        const bool qa = lane < P;
+        uint64_t ql = 0;
+        uint2 qm = make_uint2(0, 0);
+        if (qa) { ql = qlo[lane]; qm = qmeta[lane]; }
+        uint32_t qs = qm.x, qg = qa ? kLookupPending : kInvalidSlot;
+        for (uint32_t it = 0; it < dmask + 4096 && __any(qg == kLookupPending); it++) {
+          if (qg == kLookupPending) {
+            const ulonglong2 e = *reinterpret_cast<const ulonglong2 *>(p.dict + (qs & ~1u));
+            uint32_t cs;
+            qg = bucket_probe(e, qs, ql, &cs);
+            if (qg == kLookupPending) {
+              if (cs != kInvalidSlot) qg = dict_claim_short(p.dict, dmask, cs, ql, &qs);
+              else qs = ((qs | 1u) + 1u) & dmask;
+            }
+          }
+        }
+        if (qa) res[qm.y] = qg == kLookupPending ? kInvalidSlot : qg;
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < (int)kWaveK; k++)
+          if (g[k] == kLookupPending) g[k] = res[lane + 64 * k];
+        break;
+      }
+      if (round > dmask) break;                          // table exhausted: capacity error below
+      ulonglong2 e[kWaveK];
+#pragma unroll
+      for (int k = 0; k < (int)kWaveK; k++)
+        e[k] = *reinterpret_cast<const ulonglong2 *>(p.dict + (g[k] == kLookupPending ? (ps[k] & ~1u) : 0u));
+      uint32_t cs[kWaveK];
+      bool anyclaim = false;
+#pragma unroll
+      for (int k = 0; k < (int)kWaveK; k++) {
+        const bool pend = g[k] == kLookupPending;
+        uint32_t c;
+        const uint32_t r = bucket_probe(e[k], ps[k], lo[k], &c);
+        cs[k] = pend ? c : kInvalidSlot;
+        anyclaim |= pend & (c != kInvalidSlot);
+        const bool adv = pend & (r == kLookupPending) & (c == kInvalidSlot);
+        ps[k] = adv ? (((ps[k] | 1u) + 1u) & dmask) : ps[k];
+        g[k] = pend ? r : g[k];
+      }
+      if (__any(anyclaim)) {
+#pragma unroll
+        for (int k = 0; k < (int)kWaveK; k++)
+          if (cs[k] != kInvalidSlot) g[k] = dict_claim_short(p.dict, dmask, cs[k], lo[k], &ps[k]);
+      }
+    }
+    bool caperr = false;
+#pragma unroll
+    for (int k = 0; k < (int)kWaveK; k++) {
+      const bool e = (((actm >> k) & 1u) != 0) & ((g[k] == kInvalidSlot) | (g[k] == kLookupPending));
+      caperr |= e;
+      if (e) g[k] = 0;
+    }
+    if (caperr) set_err(p.err, kErrCapacity, doc);
+  }
+}
+
 // Units: PACK = false, one document per unit (documents 0..n_docs-1, or the
 // doc_list entries); PACK = true, unit u = documents [u * pack, u * pack + pack)
 // sharing one window.  A pack that cannot take the packed path (window or
@@ -1008,126 +1142,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     // ---- dictionary slots of terms lane + 64k
     uint32_t g[kWaveK], tf[kWaveK], tdoc[kWaveK];
     uint32_t actm = 0;
-    if (PACK && lane < kPackMax) { pk_len[lane] = 0; pk_nu[lane] = 0; }
-    {
-      uint64_t lo[kWaveK];
-      uint32_t ps[kWaveK];
-      uint32_t foldm = 0;
-#pragma unroll
-      for (int k = 0; k < (int)kWaveK; k++) {
-        lo[k] = 0;
-        tf[k] = 0;
-        g[k] = kInvalidSlot;
-        ps[k] = 0;
-        {
-          const uint32_t idx = lane + 64 * k;
-          const bool in = idx < nu;
-          const uint32_t s = slots[in ? idx : 0u] & (kWaveSlots - 1);
-          const uint64_t key = sm.key[s];
-          tf[k] = (sm.cnt[s >> 1] >> (16 * (s & 1))) & 0xFFFFu;
-          const bool f = in & ((key & kFoldBit) != 0);
-          const bool sh = in & !f;
-          tdoc[k] = PACK ? key_doc(key) : 0u;
-          if (PACK && in) { atomicAdd(&pk_len[tdoc[k]], tf[k]); atomicAdd(&pk_nu[tdoc[k]], 1u); }
-          lo[k] = sh ? (PACK ? key & ~kPackTagMask : key) : 0ull;
-          foldm |= (uint32_t)f << k;
-          actm |= (uint32_t)in << k;
-          ps[k] = dict_home(dict_hash_short(lo[k]), dmask) & ~1u;
-          g[k] = sh ? kLookupPending : g[k];
-        }
-      }
-      // folded (> 8 byte) terms: exact 128-bit keys, one lookup per lane at a time
-      while (__any(foldm != 0)) {
-        uint64_t flo = 1, fhi = kKeyValid;
-        uint32_t k = 0;
-        const bool fa = foldm != 0;
-        if (fa) {
-          k = (uint32_t)__builtin_ctz(foldm);
-          foldm &= foldm - 1;
-          const uint64_t key = sm.key[slots[lane + 64 * k]];
-          const uint32_t n = (uint32_t)key & 0xFFu, tp = (uint32_t)(key >> 13) & 0x1FFFu;
-          bool valid;
-          token_key(sm.text, tp, tp + n, &flo, &fhi, &valid);
-        }
-        const uint32_t gg = dict_find_or_insert(p.dict, dmask, flo, fhi, fa);
-#pragma unroll
-        for (int kk = 0; kk < (int)kWaveK; kk++)
-          if (fa && (uint32_t)kk == k) g[kk] = gg;
-      }
-      // short terms: bucket probes, all of a lane's loads in flight per round
-      for (uint32_t round = 0;; round++) {
-        uint32_t np = 0;
-#pragma unroll
-        for (int k = 0; k < (int)kWaveK; k++) np += g[k] == kLookupPending;
-        const uint32_t pincl = wave_incl_add(np);
-        const uint32_t P = (uint32_t)__builtin_amdgcn_readlane((int)pincl, 63);
-        if (P == 0) break;
-        if (round > 0 && P <= kDictQueue) {
-          // retry queue in the (no longer needed) table: (lo, probe slot, term index)
-          uint64_t *qlo = sm.key;
-          uint2 *qmeta = reinterpret_cast<uint2 *>(sm.key + kDictQueue);
-          uint32_t *res = reinterpret_cast<uint32_t *>(sm.key + 2 * kDictQueue);
-          uint32_t at = pincl - np;
-#pragma unroll
-          for (int k = 0; k < (int)kWaveK; k++)
-            if (g[k] == kLookupPending) { qlo[at] = lo[k]; qmeta[at] = make_uint2(ps[k], lane + 64 * k); at++; }
-          asm volatile("" ::: "memory");
-          const bool qa = lane < P;
-          uint64_t ql = 0;
-          uint2 qm = make_uint2(0, 0);
-          if (qa) { ql = qlo[lane]; qm = qmeta[lane]; }
-          uint32_t qs = qm.x, qg = qa ? kLookupPending : kInvalidSlot;
-          for (uint32_t it = 0; it < dmask + 4096 && __any(qg == kLookupPending); it++) {
-            if (qg == kLookupPending) {
-              const ulonglong2 e = *reinterpret_cast<const ulonglong2 *>(p.dict + (qs & ~1u));
-              uint32_t cs;
-              qg = bucket_probe(e, qs, ql, &cs);
-              if (qg == kLookupPending) {
-                if (cs != kInvalidSlot) qg = dict_claim_short(p.dict, dmask, cs, ql, &qs);
-                else qs = ((qs | 1u) + 1u) & dmask;
-              }
-            }
-          }
-          if (qa) res[qm.y] = qg == kLookupPending ? kInvalidSlot : qg;
-          asm volatile("" ::: "memory");
-#pragma unroll
-          for (int k = 0; k < (int)kWaveK; k++)
-            if (g[k] == kLookupPending) g[k] = res[lane + 64 * k];
-          break;
-        }
-        if (round > dmask) break;                          // table exhausted: capacity error below
-        ulonglong2 e[kWaveK];
-#pragma unroll
-        for (int k = 0; k < (int)kWaveK; k++)
-          e[k] = *reinterpret_cast<const ulonglong2 *>(p.dict + (g[k] == kLookupPending ? (ps[k] & ~1u) : 0u));
-        uint32_t cs[kWaveK];
-        bool anyclaim = false;
-#pragma unroll
-        for (int k = 0; k < (int)kWaveK; k++) {
-          const bool pend = g[k] == kLookupPending;
-          uint32_t c;
-          const uint32_t r = bucket_probe(e[k], ps[k], lo[k], &c);
-          cs[k] = pend ? c : kInvalidSlot;
-          anyclaim |= pend & (c != kInvalidSlot);
-          const bool adv = pend & (r == kLookupPending) & (c == kInvalidSlot);
-          ps[k] = adv ? (((ps[k] | 1u) + 1u) & dmask) : ps[k];
-          g[k] = pend ? r : g[k];
-        }
-        if (__any(anyclaim)) {
-#pragma unroll
-          for (int k = 0; k < (int)kWaveK; k++)
-            if (cs[k] != kInvalidSlot) g[k] = dict_claim_short(p.dict, dmask, cs[k], lo[k], &ps[k]);
-        }
-      }
-      bool caperr = false;
-#pragma unroll
-      for (int k = 0; k < (int)kWaveK; k++) {
-        const bool e = (((actm >> k) & 1u) != 0) & ((g[k] == kInvalidSlot) | (g[k] == kLookupPending));
-        caperr |= e;
-        if (e) g[k] = 0;
-      }
-      if (caperr) set_err(p.err, kErrCapacity, (uint32_t)d);
-    }
+    resolve_terms<PACK>(sm, p, lane, nu, (uint32_t)d, g, tf, tdoc, actm, pk_len, pk_nu);
     if (p.debug_stop == 4) { clear_table(sm, lane); continue; }
 
     // ---- CSR row grouped by dictionary range (8 ranges per pass), staged in LDS.
@@ -1243,6 +1258,258 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     atomicAdd(&p.stats[0], my_doc_count);
     atomicAdd(&p.stats[1], my_ttf);
     atomicAdd(&p.stats[2], my_nnz);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Book-sized documents (SURVEY cfg 1), ASCII: chunk-parallel.  A long
+// document is cut into kCoreBytes cores; unit = (document, core).  A wave
+// stages the core with kPreBytes of context before it and kPostBytes after it
+// (UAX#29 decisions look at most two characters around a position; a token
+// that runs past the post margin is longer than 255 characters), keeps the
+// tokens STARTING in its core, counts them in its LDS table, resolves the
+// distinct terms in the global dictionary (resolve_terms) and adds the counts
+// into the document's dense per-slot array (global atomics).  k_long_rows then
+// turns each document's dense array into its CSR row (slot order, so grouped
+// by range) and zeroes it.  A chunk that cannot take this path (non-ASCII
+// text, a token of more than 255 characters, more than 512 distinct terms)
+// marks its document, which then goes to k_tokenize_long as a whole.
+constexpr uint32_t kCoreBytes = kLongCoreBytes;
+constexpr uint32_t kPreBytes = 64;
+constexpr uint32_t kPostBytes = 320;
+static_assert(kPreBytes + kCoreBytes + kPostBytes + 16 <= kWaveWindow, "chunk window");
+
+struct ChunkMeta {
+  uint64_t s0, L;                 // window: corpus bytes [s0, s0 + L)
+  uint32_t shift, core_lo, core_hi, gi;
+  uint64_t d;
+};
+
+__device__ __forceinline__ ChunkMeta chunk_meta(const BuildParams &p, uint64_t u) {
+  const uint2 e = p.chunk_list[u];
+  ChunkMeta m;
+  m.gi = e.x;
+  m.d = p.chunk_docs[e.x];
+  const uint64_t src = p.live_map ? p.live_map[m.d] : m.d;
+  const uint64_t dlo = p.offsets[src], dl = p.offsets[src + 1] - dlo;
+  const uint64_t clo = (uint64_t)e.y * kCoreBytes, chi = min(dl, clo + kCoreBytes);
+  const uint64_t ws = clo > kPreBytes ? clo - kPreBytes : 0, we = min(dl, chi + kPostBytes);
+  m.s0 = dlo + ws;
+  m.L = we - ws;
+  m.core_lo = (uint32_t)(clo - ws);
+  m.core_hi = (uint32_t)(chi - ws);
+  m.shift = (uint32_t)(reinterpret_cast<uintptr_t>(p.text + m.s0) & 15);
+  return m;
+}
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_tokenize_chunk(BuildParams p) {
+  __shared__ WaveSmem sm;
+  const uint32_t lane = threadIdx.x;
+  clear_table(sm, lane);
+  sm.noop[lane] = 0;
+  uint4 v[4] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
+  const uint64_t n_units = p.n_chunks;
+  const uint64_t C = (uint64_t)p.cap_mask + 1;
+  unsigned long long *noop = reinterpret_cast<unsigned long long *>(&sm.noop[lane]);
+  uint16_t *slots = reinterpret_cast<uint16_t *>(sm.list);
+  ChunkMeta meta;
+  auto prefetch = [&](const ChunkMeta &m) {
+    const uint32_t nchunks = (uint32_t)((m.shift + m.L + 15) >> 4);
+    const uint4 *src = reinterpret_cast<const uint4 *>(reinterpret_cast<uintptr_t>(p.text + m.s0) & ~(uintptr_t)15);
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (lane + 64 * k < nchunks) v[k] = gload16(src + lane + 64 * k);
+  };
+  if (blockIdx.x < n_units) { meta = chunk_meta(p, blockIdx.x); prefetch(meta); }
+  for (uint64_t u = blockIdx.x; u < n_units; u += gridDim.x) {
+    const ChunkMeta m = meta;
+    const uint64_t un = u + gridDim.x;
+    {   // stage (bytes outside the window zeroed), then fetch the next unit
+      const uint32_t hi_b = m.shift + (uint32_t)m.L;
+      const uint32_t nchunks = (hi_b + 15) >> 4;
+      uint4 *dst = reinterpret_cast<uint4 *>(sm.text);
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t c = lane + 64 * k;
+        uint4 val = c < nchunks ? v[k] : make_uint4(0, 0, 0, 0);
+        if (c == 0 || c == nchunks - 1) {
+          val.x &= keep_range(16 * c, m.shift, hi_b);
+          val.y &= keep_range(16 * c + 4, m.shift, hi_b);
+          val.z &= keep_range(16 * c + 8, m.shift, hi_b);
+          val.w &= keep_range(16 * c + 12, m.shift, hi_b);
+        }
+        dst[c] = val;
+      }
+    }
+    if (un < n_units) { meta = chunk_meta(p, un); prefetch(meta); }
+    asm volatile("" ::: "memory");
+    const uint32_t fail_at = m.gi;
+    bool bad, under;
+    uint64_t wbase = 0;
+    const uint64_t W = lane_word_mask<false>(sm.text, lane, &bad, &under, &wbase);
+    if (bad) {                                               // non-ASCII: the whole document -> long path
+      if (lane == 0) p.chunk_fail[fail_at] = 1u;
+      continue;
+    }
+    const uint64_t wlast = __ballot((W >> 63) & 1ull);
+    const uint64_t prevW = lane ? (wlast >> (lane - 1)) & 1ull : 0ull;
+    const uint64_t S = W & ~((W << 1) | prevW);
+    uint64_t E = ~W & ((W << 1) | prevW);
+    const uint32_t firstE = E ? lane * 64 + (uint32_t)__builtin_ctzll(E) : kWaveWindow;
+    const uint64_t hasE = __ballot(E != 0);
+    const uint64_t later = lane == 63 ? 0ull : (hasE & (~0ull << (lane + 1)));
+    const uint32_t srcl = later ? (uint32_t)__builtin_ctzll(later) : lane;
+    uint32_t nz = (uint32_t)__shfl((int)firstE, (int)srcl, 64);
+    if (!later) nz = kWaveWindow;
+    if (prevW) E &= E - 1;
+    // tokens starting in the core only: buffer positions [A, B)
+    const uint32_t A = m.shift + m.core_lo, B = m.shift + m.core_hi, l0 = 64 * lane;
+    const uint64_t below_b = B <= l0 ? 0ull : (B - l0 >= 64 ? ~0ull : ((1ull << (B - l0)) - 1));
+    const uint64_t below_a = A <= l0 ? 0ull : (A - l0 >= 64 ? ~0ull : ((1ull << (A - l0)) - 1));
+    const uint64_t core = below_b & ~below_a;
+    const uint32_t nts = (uint32_t)__popcll(S & core);
+    const uint32_t tincl = wave_incl_add(nts);
+    const uint32_t ntok = (uint32_t)__builtin_amdgcn_readlane((int)tincl, 63);
+    bool longtok = false;
+    {
+      uint32_t at = tincl - nts;
+      uint32_t s0 = (uint32_t)S, s1 = (uint32_t)(S >> 32), e0 = (uint32_t)E, e1 = (uint32_t)(E >> 32);
+      while (s0 | s1) {
+        const uint32_t tp = lane * 64 + (s0 ? (uint32_t)__builtin_ctz(s0) : 32 + (uint32_t)__builtin_ctz(s1));
+        const uint32_t te = (e0 | e1) ? lane * 64 + (e0 ? (uint32_t)__builtin_ctz(e0) : 32 + (uint32_t)__builtin_ctz(e1))
+                                      : nz;
+        if (s0) s0 &= s0 - 1; else s1 &= s1 - 1;
+        if (e0) e0 &= e0 - 1; else e1 &= e1 - 1;
+        if (tp >= A && tp < B) {
+          longtok |= te - tp > 8;
+          sm.list[at++] = span_entry(tp, te, 0);
+        }
+      }
+    }
+    asm volatile("" ::: "memory");
+    const bool anylong = __any(longtok) || under;
+    uint32_t claims = 0, toks = 0;
+    bool overflow = false;
+    for (uint32_t tb = 0; tb < ntok && !overflow;) {
+      const uint32_t rem = ntok - tb;
+      if (anylong) {
+        if (rem > 256) { hist_batch<8, true, false>(sm, p, m.d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 512; }
+        else if (rem > 128) { hist_batch<4, true, false>(sm, p, m.d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 256; }
+        else { hist_batch<2, true, false>(sm, p, m.d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 128; }
+      } else {
+        if (rem > 256) { hist_batch<8, false, false>(sm, p, m.d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 512; }
+        else if (rem > 128) { hist_batch<4, false, false>(sm, p, m.d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 256; }
+        else { hist_batch<2, false, false>(sm, p, m.d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 128; }
+      }
+    }
+    const uint32_t nu = wave_sum(claims);
+    if (overflow || nu > kWaveTerms) {
+      clear_table(sm, lane);
+      if (lane == 0) p.chunk_fail[fail_at] = 1u;
+      continue;
+    }
+    {   // dense list of occupied table slots
+      uint32_t occ = 0;
+      const uint4 *kp = reinterpret_cast<const uint4 *>(&sm.key[16 * lane]);
+      const uint32_t rot = (lane >> 1) & 7;
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        const uint32_t qq = (q + rot) & 7;
+        const uint4 t = kp[qq];
+        occ |= ((uint32_t)((t.x | t.y) != 0) | ((uint32_t)((t.z | t.w) != 0) << 1)) << (2 * qq);
+      }
+      const uint32_t c = (uint32_t)__popc(occ);
+      uint32_t at = wave_incl_add(c) - c;
+      while (occ) {
+        slots[at++] = (uint16_t)(16 * lane + (uint32_t)__builtin_ctz(occ));
+        occ &= occ - 1;
+      }
+      asm volatile("" ::: "memory");
+    }
+    uint32_t g[kWaveK], tf[kWaveK], tdoc[kWaveK];
+    uint32_t actm = 0;
+    resolve_terms<false>(sm, p, lane, nu, (uint32_t)m.d, g, tf, tdoc, actm, nullptr, nullptr);
+    uint32_t *dense = p.dense + (uint64_t)m.gi * C;
+#pragma unroll
+    for (int k = 0; k < (int)kWaveK; k++)
+      if ((actm >> k) & 1u) atomicAdd(&dense[g[k]], tf[k]);
+    clear_table(sm, lane);
+  }
+}
+
+// One workgroup per long document of the group: dense per-slot counts ->
+// CSR row in slot order (col = slot, tf = count), range splits, length,
+// norm, statistics; the dense array is zeroed for the next group.  A
+// document some chunk could not take goes to long_list (k_tokenize_long).
+__global__ void __launch_bounds__(1024) k_long_rows(BuildParams p) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t carry;
+  __shared__ unsigned long long lsum;
+  const uint32_t gi = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint64_t d = p.chunk_docs[gi];
+  const uint32_t C = p.cap_mask + 1;
+  uint32_t *dense = p.dense + (uint64_t)gi * C;
+  const bool failed = p.chunk_fail[gi] != 0;
+  if (failed) {
+    for (uint32_t i = tid; i < C / 4; i += blockDim.x) reinterpret_cast<uint4 *>(dense)[i] = make_uint4(0, 0, 0, 0);
+    if (tid == 0) p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
+    return;
+  }
+  const uint64_t src = p.live_map ? p.live_map[d] : d;
+  const uint64_t row = csr_row_base(p.offsets, src);
+  const uint32_t RS = 1u << p.range_shift;
+  if (tid == 0) { carry = 0; lsum = 0; }
+  __syncthreads();
+  unsigned long long my_len = 0;
+  for (uint32_t t0 = 0; t0 < C; t0 += 4 * 1024) {
+    const uint32_t i0 = t0 + 4 * tid;
+    uint4 x = make_uint4(0, 0, 0, 0);
+    if (i0 < C) {
+      x = reinterpret_cast<const uint4 *>(dense)[i0 >> 2];
+      reinterpret_cast<uint4 *>(dense)[i0 >> 2] = make_uint4(0, 0, 0, 0);
+    }
+    const uint32_t nz = (x.x != 0) + (x.y != 0) + (x.z != 0) + (x.w != 0);
+    my_len += (unsigned long long)x.x + x.y + x.z + x.w;
+    uint32_t incl = nz;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(incl, o, 64);
+      if (lane >= (uint32_t)o) incl += y;
+    }
+    if (lane == 63) wsum[wid] = incl;
+    __syncthreads();
+    uint32_t base = carry, all = 0;
+    for (uint32_t w = 0; w < 16; w++) {
+      const uint32_t sw = wsum[w];
+      if (w < wid) base += sw;
+      all += sw;
+    }
+    uint32_t at = base + incl - nz;
+    const uint32_t vals[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      if (vals[q]) { p.csr_col[row + at] = i0 + q; p.csr_tf[row + at] = vals[q]; at++; }
+    __syncthreads();
+    if (tid == 0) {
+      carry += all;
+      const uint32_t t1 = min(t0 + 4 * 1024, C);
+      // a range ends inside [t0, t1): its split = entries below its end
+      if ((t1 & (RS - 1)) == 0 || t1 == C) p.rsplit[d * p.n_ranges + ((t1 - 1) >> p.range_shift)] = carry;
+    }
+    __syncthreads();
+  }
+  if (my_len) atomicAdd(&lsum, my_len);
+  __syncthreads();
+  if (tid == 0) {
+    const uint64_t len = lsum;
+    const uint32_t nu = carry;
+    if (len > 0xFFFFFFFFull) set_err(p.err, kErrTfTooLarge, (uint32_t)d);
+    p.doc_len[d] = (uint32_t)len;
+    p.doc_nuniq[d] = nu;
+    p.doc_norm[d] = (uint8_t)int_to_byte4((uint32_t)len);
+    atomicAdd(&p.stats[0], (unsigned long long)(len > 0));
+    atomicAdd(&p.stats[1], len);
+    atomicAdd(&p.stats[2], (unsigned long long)nu);
   }
 }
 
@@ -1797,6 +2064,14 @@ __global__ void __launch_bounds__(1024) k_scatter_sort(PostingParams p) {
 hipError_t launch_tokenize_wave(const BuildParams &p, int grid, hipStream_t s) {
   if (p.pack > 1) hipLaunchKernelGGL(k_tokenize_wave<true>, dim3(grid), dim3(64), 0, s, p);
   else hipLaunchKernelGGL(k_tokenize_wave<false>, dim3(grid), dim3(64), 0, s, p);
+  return hipGetLastError();
+}
+hipError_t launch_tokenize_chunks(const BuildParams &p, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(k_tokenize_chunk, dim3(grid), dim3(64), 0, s, p);
+  return hipGetLastError();
+}
+hipError_t launch_long_rows(const BuildParams &p, uint32_t n_docs, hipStream_t s) {
+  hipLaunchKernelGGL(k_long_rows, dim3(n_docs), dim3(1024), 0, s, p);
   return hipGetLastError();
 }
 hipError_t launch_tokenize_long(const BuildParams &p, int grid, hipStream_t s) {

@@ -175,6 +175,8 @@ struct tfidf_index {
     return term_major ? tdf.as<uint32_t>() : blk.as<uint32_t>() + (size_t)n_blocks * C;
   }
   DevBuf lt_keys, lt_cnt, lt_g;
+  DevBuf dense, chunk_list, chunk_docs, chunk_fail;   // book-sized documents (chunk-parallel)
+  uint64_t long_chunked = 0;           // long documents the chunk path took in the last commit
   uint32_t lt_log2 = 0, lt_wgs = 64;   // lt_wgs: long-path workgroups always allowed
   PinnedVec<uint64_t> h_dict;        // host mirrors for query analysis (pinned)
   PinnedVec<uint32_t> h_df;
@@ -262,7 +264,7 @@ extern "C" int tfidf_destroy(tfidf_index *ix) {
   hipStreamSynchronize(ix->copy_stream);
   DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->d_live_map, &ix->dict, &ix->csr_col, &ix->csr_tf, &ix->doc_len,
                     &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->long_list, &ix->uni_list, &ix->counters, &ix->blk,
-                    &ix->retry_list, &ix->bbase, &ix->post, &ix->post_tmp, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->canon_of_slot,
+                    &ix->retry_list, &ix->bbase, &ix->post, &ix->post_tmp, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->dense, &ix->chunk_list, &ix->chunk_docs, &ix->chunk_fail, &ix->canon_of_slot,
                     &ix->q_off, &ix->q_slot, &ix->q_w, &ix->q_role, &ix->q_meta, &ix->cache, &ix->cand, &ix->cand_n, &ix->out_doc,
                     &ix->out_score, &ix->out_n, &ix->hits, &ix->hits_n, &ix->hits_c, &ix->hits_s, &ix->hits_P, &ix->sort_tmp,
                     &ix->row_off, &ix->tvals, &ix->toff, &ix->tdf, &ix->term_tmp, &ix->sent_slot, &ix->vcounts, &ix->vnu,
@@ -807,31 +809,80 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   HIP_TRY(hipMemcpyAsync(hctr, ctr, sizeof hctr, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   const uint32_t n_long = (uint32_t)hctr[4], n_uni = (uint32_t)hctr[6];
+  ix->long_chunked = 0;
   ix->long_docs = n_long;
   ix->unicode_docs = n_uni;
   if (n_long) {
-    uint32_t lg = ix->cap_log2 + 1;
-    // table size needed by the longest long document (2x its token bound)
-    uint64_t maxlen = 0;
-    for (uint64_t d = 0; d < ix->n_staged; d++) maxlen = std::max(maxlen, ix->h_offsets[d + 1] - ix->h_offsets[d]);
-    uint32_t need = 10;
-    while (need < 22 && (1ull << need) < maxlen + 2) need++;
-    lg = std::min(lg, need);
-    ix->lt_log2 = lg;
-    // one workgroup per long document, up to 2 per CU, within a scratch budget
-    // (24 B per table slot per workgroup: key lo/hi, count, dictionary slot)
-    const uint64_t per_wg = 24ull << lg;
-    const uint64_t by_budget = std::max<uint64_t>(ix->lt_wgs, kLongScratchBudget / per_wg);
-    const uint32_t wgs = (uint32_t)std::min<uint64_t>({(uint64_t)n_long, (uint64_t)ix->num_cus * 2, by_budget});
-    HIP_TRY(ix->lt_keys.reserve((size_t)wgs * 2 * (1ull << lg) * 8));
-    HIP_TRY(ix->lt_cnt.reserve((size_t)wgs * (1ull << lg) * 4));
-    HIP_TRY(ix->lt_g.reserve((size_t)wgs * (1ull << lg) * 4));
-    bp.lt_keys = ix->lt_keys.as<uint64_t>();
-    bp.lt_cnt = ix->lt_cnt.as<uint32_t>();
-    bp.lt_g = ix->lt_g.as<uint32_t>();
-    bp.lt_slots_log2 = lg;
     HIP_TRY(hipEventRecord(ix->ev[EV_L0], s));
-    HIP_TRY(launch_tokenize_long(bp, (int)wgs, s));
+    // book-sized documents: chunk-parallel (k_tokenize_chunk + k_long_rows),
+    // in groups whose dense per-slot count arrays fit kDenseBudget; documents
+    // a chunk could not take come back in long_list for k_tokenize_long
+    std::vector<uint32_t> ldocs(n_long);
+    HIP_TRY(hipMemcpyAsync(ldocs.data(), ix->long_list.p, (size_t)n_long * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    const uint64_t group_max = std::max<uint64_t>(1, kDenseBudget / ((uint64_t)C * 4));
+    const uint64_t gsz = std::min<uint64_t>(n_long, group_max);
+    if (ix->dense.bytes < gsz * C * 4) {
+      HIP_TRY(ix->dense.reserve(gsz * C * 4));
+      HIP_TRY(hipMemsetAsync(ix->dense.p, 0, ix->dense.bytes, s));     // k_long_rows leaves it zeroed
+    }
+    std::vector<uint2> chunks;
+    std::vector<uint64_t> gstart;                   // first chunk of each group
+    for (uint64_t g0 = 0; g0 < n_long; g0 += gsz) {
+      gstart.push_back(chunks.size());
+      for (uint64_t i = g0; i < std::min<uint64_t>(n_long, g0 + gsz); i++) {
+        const uint64_t st = ix->live_map.empty() ? ldocs[i] : ix->live_map[ldocs[i]];
+        const uint64_t L = ix->h_offsets[st + 1] - ix->h_offsets[st];
+        for (uint64_t c = 0; c * kLongCoreBytes < L; c++) chunks.push_back(make_uint2((uint32_t)(i - g0), (uint32_t)c));
+      }
+    }
+    gstart.push_back(chunks.size());
+    HIP_TRY(ix->chunk_list.reserve(chunks.size() * 8 + 8));
+    HIP_TRY(ix->chunk_docs.reserve((size_t)n_long * 4));
+    HIP_TRY(ix->chunk_fail.reserve((size_t)n_long * 4));
+    HIP_TRY(hipMemcpyAsync(ix->chunk_list.p, chunks.data(), chunks.size() * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(ix->chunk_docs.p, ldocs.data(), (size_t)n_long * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemsetAsync(ix->chunk_fail.p, 0, (size_t)n_long * 4, s));
+    HIP_TRY(hipMemsetAsync(bp.long_count, 0, 4, s));                   // the fallback list restarts
+    for (size_t gi = 0; gi + 1 < gstart.size(); gi++) {
+      const uint64_t g0 = gi * gsz, n = std::min<uint64_t>(gsz, n_long - g0);
+      BuildParams cp = bp;
+      cp.chunk_list = ix->chunk_list.as<uint2>() + gstart[gi];
+      cp.n_chunks = gstart[gi + 1] - gstart[gi];
+      cp.chunk_docs = ix->chunk_docs.as<uint32_t>() + g0;
+      cp.chunk_fail = ix->chunk_fail.as<uint32_t>() + g0;
+      cp.dense = ix->dense.as<uint32_t>();
+      const uint64_t grid = std::min<uint64_t>(cp.n_chunks, (uint64_t)ix->num_cus * kWaveWGsPerCU);
+      HIP_TRY(launch_tokenize_chunks(cp, (int)grid, s));
+      HIP_TRY(launch_long_rows(cp, (uint32_t)n, s));
+    }
+    uint32_t n_fb = 0;
+    HIP_TRY(hipMemcpyAsync(&n_fb, bp.long_count, 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipStreamSynchronize(s));
+    ix->long_chunked = n_long - n_fb;
+    if (n_fb) {
+      uint32_t lg = ix->cap_log2 + 1;
+      // table size needed by the longest long document (2x its token bound)
+      uint64_t maxlen = 0;
+      for (uint64_t d = 0; d < ix->n_staged; d++) maxlen = std::max(maxlen, ix->h_offsets[d + 1] - ix->h_offsets[d]);
+      uint32_t need = 10;
+      while (need < 22 && (1ull << need) < maxlen + 2) need++;
+      lg = std::min(lg, need);
+      ix->lt_log2 = lg;
+      // one workgroup per long document, up to 2 per CU, within a scratch budget
+      // (24 B per table slot per workgroup: key lo/hi, count, dictionary slot)
+      const uint64_t per_wg = 24ull << lg;
+      const uint64_t by_budget = std::max<uint64_t>(ix->lt_wgs, kLongScratchBudget / per_wg);
+      const uint32_t wgs = (uint32_t)std::min<uint64_t>({(uint64_t)n_fb, (uint64_t)ix->num_cus * 2, by_budget});
+      HIP_TRY(ix->lt_keys.reserve((size_t)wgs * 2 * (1ull << lg) * 8));
+      HIP_TRY(ix->lt_cnt.reserve((size_t)wgs * (1ull << lg) * 4));
+      HIP_TRY(ix->lt_g.reserve((size_t)wgs * (1ull << lg) * 4));
+      bp.lt_keys = ix->lt_keys.as<uint64_t>();
+      bp.lt_cnt = ix->lt_cnt.as<uint32_t>();
+      bp.lt_g = ix->lt_g.as<uint32_t>();
+      bp.lt_slots_log2 = lg;
+      HIP_TRY(launch_tokenize_long(bp, (int)wgs, s));
+    }
     HIP_TRY(hipEventRecord(ix->ev[EV_LONG], s));
     HIP_TRY(hipMemcpyAsync(hctr, ctr, 5 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
@@ -987,6 +1038,7 @@ extern "C" int tfidf_stats(const tfidf_index *ix, tfidf_index_stats *out) {
   out->pack_docs = ix->pack_docs;
   out->pack_retried = ix->pack_retried;
   out->unicode_docs = ix->unicode_docs;
+  out->long_chunked = ix->long_chunked;
   const DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->dict, &ix->csr_col, &ix->csr_tf, &ix->doc_len,
                           &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->blk, &ix->bbase, &ix->post,
                           &ix->toff, &ix->tdf};

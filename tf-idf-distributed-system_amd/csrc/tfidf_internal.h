@@ -56,6 +56,14 @@ struct BuildParams {
   uint32_t *retry_count;
   const uint32_t *doc_list;
   const uint32_t *doc_list_count;
+  // book-sized documents, chunk-parallel (k_tokenize_chunk / k_long_rows):
+  // units (group document index, core index), the group's documents, their
+  // dense per-slot counts (group x C u32, zero between uses), failure flags
+  const uint2 *chunk_list;
+  uint64_t n_chunks;
+  const uint32_t *chunk_docs;
+  uint32_t *dense;
+  uint32_t *chunk_fail;
 };
 
 __host__ __device__ inline uint64_t csr_row_base(const uint64_t *offsets, uint64_t src) {
@@ -88,6 +96,10 @@ constexpr uint32_t kWaveWGsPerCU = 8;
 constexpr uint32_t kPackMaxDocs = 16;     // documents per packed window (<= kPackMax, kernels_index.hip)
 constexpr uint64_t kPackBytes = 2048;     // text per packed window (auto pack size)    // 64-thread workgroups per CU (2 waves/SIMD: VGPR-bound)
 hipError_t launch_tokenize_long(const BuildParams &p, int grid, hipStream_t s);
+constexpr uint32_t kLongCoreBytes = 2048;              // = kCoreBytes (kernels_index.hip)
+constexpr uint64_t kDenseBudget = 2ull << 30;          // per-group dense count arrays (book-sized documents)
+hipError_t launch_tokenize_chunks(const BuildParams &p, int grid, hipStream_t s);
+hipError_t launch_long_rows(const BuildParams &p, uint32_t n_docs, hipStream_t s);
 hipError_t launch_tokenize_uwave(const BuildParams &p, int grid, hipStream_t s);   // kernels_unicode.hip
 constexpr uint32_t kUwaveWGsPerCU = 5;    // 64-thread workgroups, ~29 KB LDS each
 hipError_t launch_df_partial(const PostingParams &p, hipStream_t s);

@@ -41,7 +41,7 @@ class Config(C.Structure):
 class IndexStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("num_docs", "doc_count", "sum_ttf", "num_terms", "nnz",
                                           "device_bytes", "long_docs", "text_bytes", "term_major",
-                                          "pack_docs", "pack_retried", "unicode_docs")]
+                                          "pack_docs", "pack_retried", "unicode_docs", "long_chunked")]
 
 
 class CommitTiming(C.Structure):
