@@ -363,6 +363,7 @@ def test_global_stats_two_shards_equal_single_index():
         s.vocab_export_device(k.data_ptr(), df.data_ptr(), n)
         keys.append(k)
     all_keys = torch.cat(keys).contiguous()
+    torch.cuda.synchronize()                      # the shards run on their own streams
     dfcs = []
     for s in shards:
         dfc = torch.zeros(all_keys.shape[0], dtype=torch.int32, device=dev)
@@ -370,6 +371,7 @@ def test_global_stats_two_shards_equal_single_index():
         dfcs.append(dfc[:n])
     assert dfcs[0].shape == dfcs[1].shape
     total = (dfcs[0] + dfcs[1]).contiguous()
+    torch.cuda.synchronize()
     st = [s.stats() for s in shards]
     dc = sum(x["doc_count"] for x in st)
     ttf = sum(x["sum_ttf"] for x in st)

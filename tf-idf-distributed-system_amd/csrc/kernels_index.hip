@@ -1286,7 +1286,13 @@ struct ChunkMeta {
 };
 
 __device__ __forceinline__ ChunkMeta chunk_meta(const BuildParams &p, uint64_t u) {
-  const uint2 e = p.chunk_list[u];
+  // group document holding unit u: chunk_pre[gi] <= u < chunk_pre[gi + 1] (binary search, scalar loads)
+  uint32_t lo = 0, hi = p.n_group_docs;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (p.chunk_pre[mid] <= u) lo = mid; else hi = mid;
+  }
+  const uint2 e = make_uint2(lo, (uint32_t)(u - p.chunk_pre[lo]));
   ChunkMeta m;
   m.gi = e.x;
   m.d = p.chunk_docs[e.x];

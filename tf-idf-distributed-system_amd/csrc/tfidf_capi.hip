@@ -826,29 +826,34 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
       HIP_TRY(ix->dense.reserve(gsz * C * 4));
       HIP_TRY(hipMemsetAsync(ix->dense.p, 0, ix->dense.bytes, s));     // k_long_rows leaves it zeroed
     }
-    std::vector<uint2> chunks;
-    std::vector<uint64_t> gstart;                   // first chunk of each group
+    // per group: the first unit (document, core) of each document, prefix form
+    std::vector<uint32_t> pre;
+    std::vector<uint64_t> gpre;                      // offset of each group's prefix array
     for (uint64_t g0 = 0; g0 < n_long; g0 += gsz) {
-      gstart.push_back(chunks.size());
+      gpre.push_back(pre.size());
+      uint64_t acc = 0;
       for (uint64_t i = g0; i < std::min<uint64_t>(n_long, g0 + gsz); i++) {
         const uint64_t st = ix->live_map.empty() ? ldocs[i] : ix->live_map[ldocs[i]];
         const uint64_t L = ix->h_offsets[st + 1] - ix->h_offsets[st];
-        for (uint64_t c = 0; c * kLongCoreBytes < L; c++) chunks.push_back(make_uint2((uint32_t)(i - g0), (uint32_t)c));
+        pre.push_back((uint32_t)acc);
+        acc += (L + kLongCoreBytes - 1) / kLongCoreBytes;
       }
+      if (acc >= 0xFFFFFFFFull) return fail(TFIDF_E_CAPACITY, "too many document chunks");
+      pre.push_back((uint32_t)acc);
     }
-    gstart.push_back(chunks.size());
-    HIP_TRY(ix->chunk_list.reserve(chunks.size() * 8 + 8));
+    HIP_TRY(ix->chunk_list.reserve(pre.size() * 4 + 8));
     HIP_TRY(ix->chunk_docs.reserve((size_t)n_long * 4));
     HIP_TRY(ix->chunk_fail.reserve((size_t)n_long * 4));
-    HIP_TRY(hipMemcpyAsync(ix->chunk_list.p, chunks.data(), chunks.size() * 8, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(ix->chunk_list.p, pre.data(), pre.size() * 4, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemcpyAsync(ix->chunk_docs.p, ldocs.data(), (size_t)n_long * 4, hipMemcpyHostToDevice, s));
     HIP_TRY(hipMemsetAsync(ix->chunk_fail.p, 0, (size_t)n_long * 4, s));
     HIP_TRY(hipMemsetAsync(bp.long_count, 0, 4, s));                   // the fallback list restarts
-    for (size_t gi = 0; gi + 1 < gstart.size(); gi++) {
+    for (size_t gi = 0; gi < gpre.size(); gi++) {
       const uint64_t g0 = gi * gsz, n = std::min<uint64_t>(gsz, n_long - g0);
       BuildParams cp = bp;
-      cp.chunk_list = ix->chunk_list.as<uint2>() + gstart[gi];
-      cp.n_chunks = gstart[gi + 1] - gstart[gi];
+      cp.chunk_pre = ix->chunk_list.as<uint32_t>() + gpre[gi];
+      cp.n_group_docs = (uint32_t)n;
+      cp.n_chunks = pre[gpre[gi] + n];
       cp.chunk_docs = ix->chunk_docs.as<uint32_t>() + g0;
       cp.chunk_fail = ix->chunk_fail.as<uint32_t>() + g0;
       cp.dense = ix->dense.as<uint32_t>();

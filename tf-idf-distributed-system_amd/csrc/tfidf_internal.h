@@ -57,9 +57,11 @@ struct BuildParams {
   const uint32_t *doc_list;
   const uint32_t *doc_list_count;
   // book-sized documents, chunk-parallel (k_tokenize_chunk / k_long_rows):
-  // units (group document index, core index), the group's documents, their
-  // dense per-slot counts (group x C u32, zero between uses), failure flags
-  const uint2 *chunk_list;
+  // the group's documents, their first unit (chunk_pre[n_group_docs + 1],
+  // unit = (document, core)), dense per-slot counts (group x C u32, zero
+  // between uses), failure flags
+  const uint32_t *chunk_pre;
+  uint32_t n_group_docs;
   uint64_t n_chunks;
   const uint32_t *chunk_docs;
   uint32_t *dense;
