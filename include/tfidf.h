@@ -50,7 +50,8 @@ extern "C" {
 #define TFIDF_E_INVALID_ARG 1
 #define TFIDF_E_HIP 2
 #define TFIDF_E_OOM 3
-#define TFIDF_E_UNSUPPORTED_INPUT 4 /* malformed UTF-8 document (Files.readString throws), tf >= 2^24 */
+#define TFIDF_E_UNSUPPORTED_INPUT 4 /* tf >= 2^24 (a malformed UTF-8 document is indexed empty, see
+                                       tfidf_malformed_docs) */
 #define TFIDF_E_UNSUPPORTED_QUERY 5 /* malformed UTF-8 query */
 #define TFIDF_E_CAPACITY 6          /* vocabulary capacity exceeded */
 #define TFIDF_E_STATE 7             /* e.g. search before commit */
@@ -97,6 +98,7 @@ typedef struct tfidf_index_stats {
   uint64_t pack_retried;  /* documents the packed windows handed to the one-per-window pass */
   uint64_t unicode_docs;  /* documents (window <= 4 KB) the ASCII wave path handed to the Unicode wave path */
   uint64_t long_chunked;  /* long documents indexed chunk-parallel (the rest of long_docs: k_tokenize_long) */
+  uint64_t malformed_docs;/* documents that are not valid UTF-8, indexed empty (tfidf_malformed_docs) */
 } tfidf_index_stats;
 
 /* Per-phase device times of the last commit, measured with HIP events on the
@@ -186,6 +188,14 @@ int tfidf_doc_key(const tfidf_index *ix, uint64_t doc, uint8_t *buf, uint64_t ca
  * *n_bytes = size needed when cap is too small. */
 int tfidf_doc_keys(const tfidf_index *ix, uint8_t *buf, uint64_t cap, uint64_t *offsets, uint64_t *n_bytes);
 int tfidf_doc_len(tfidf_index *ix, uint64_t doc, uint32_t *len, uint8_t *norm);
+/* Documents of the last commit whose bytes are not valid UTF-8 (where the
+ * reference's Files.readString throws MalformedInputException and Tika
+ * extracts the text instead, Worker.java:199-211): they are indexed as empty
+ * documents (no tokens, norm 0) rather than failing the commit.  Committed doc
+ * ids, ascending; *n_out = count (TFIDF_E_BUFFER if cap is too small).  A
+ * caller with a text extractor re-adds the extracted text under the same key
+ * (replace-by-key) and commits again. */
+int tfidf_malformed_docs(const tfidf_index *ix, uint64_t *docs, uint64_t cap, uint64_t *n_out);
 /* Distinct terms of one document: NUL-separated strings (sorted by bytes) + tf. */
 int tfidf_doc_terms(tfidf_index *ix, uint64_t doc, char *terms, uint64_t terms_cap, uint32_t *tfs,
                     uint64_t cap, uint64_t *n_out);

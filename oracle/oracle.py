@@ -47,6 +47,7 @@ def _load():
         "orc_sum_ttf": (C.c_uint64, [C.c_void_p]),
         "orc_num_terms": (C.c_uint64, [C.c_void_p]),
         "orc_doc_len": (C.c_uint32, [C.c_void_p, C.c_uint64]),
+        "orc_malformed_docs": (C.c_uint64, [C.c_void_p, u64p, C.c_uint64]),
         "orc_doc_norm": (C.c_uint8, [C.c_void_p, C.c_uint64]),
         "orc_doc_key": (C.c_uint64, [C.c_void_p, C.c_uint64, C.c_char_p, C.c_uint64]),
         "orc_doc_terms": (C.c_int64, [C.c_void_p, C.c_uint64, C.c_char_p, C.c_uint64, u32p, C.c_uint64]),
@@ -170,6 +171,12 @@ class OracleIndex:
 
     def doc_len(self, d):
         return lib().orc_doc_len(self._ix, d)
+
+    def malformed_docs(self):
+        n = lib().orc_malformed_docs(self._ix, None, 0)
+        out = np.zeros(max(n, 1), np.uint64)
+        lib().orc_malformed_docs(self._ix, _p(out, C.c_uint64), n)
+        return out[:n].tolist()
 
     def doc_norm(self, d):
         return lib().orc_doc_norm(self._ix, d)

@@ -453,6 +453,7 @@ struct orc_index {
   uint64_t *df;                                   /* per term */
   posting **plist; uint64_t *plen;                /* postings in doc order */
   uint64_t doc_count, sum_ttf;
+  uint64_t *malformed; uint64_t n_malformed;      /* committed docs not valid UTF-8 */
   /* global override */
   uint64_t g_doc_count, g_sum_ttf;
   strtab g_terms; uint64_t *g_df; uint64_t g_df_cap;
@@ -469,7 +470,8 @@ orc_index *orc_create(float k1, float b) {
 }
 
 static void free_committed(orc_index *ix) {
-  free(ix->live); free(ix->doc_len); free(ix->doc_norm);
+  free(ix->live); free(ix->doc_len); free(ix->doc_norm); free(ix->malformed);
+  ix->malformed = NULL; ix->n_malformed = 0;
   free(ix->dt_off); free(ix->dt_term); free(ix->dt_tf);
   if (ix->plist) for (uint64_t t = 0; t < ix->terms.n; t++) free(ix->plist[t]);
   free(ix->plist); free(ix->plen); free(ix->df);
@@ -586,6 +588,15 @@ int orc_commit(orc_index *ix) {
   for (uint64_t d = 0; d < nlive; d++) {
     const stored_doc *sd = &ix->docs[ix->live[d]];
     int64_t nt = orc_tokenize(sd->text, sd->text_len, 255, st, ln, tok_cap);
+    if (nt == ORC_E_UNSUPPORTED) {
+      /* Files.readString throws MalformedInputException (Worker.java:199-201);
+       * the text then comes from Tika (text = "" when Tika fails), which is not rebuilt: the
+       * document is indexed with an empty field and listed. */
+      if (!ix->malformed) ix->malformed = (uint64_t *)malloc(nlive * sizeof(uint64_t));
+      if (!ix->malformed) return ORC_E_NOMEM;
+      ix->malformed[ix->n_malformed++] = d;
+      nt = 0;
+    }
     if (nt < 0) return (int)nt;
     if ((uint64_t)nt > tok_cap) {
       tok_cap = (uint64_t)nt;
@@ -657,6 +668,10 @@ uint64_t orc_num_docs(const orc_index *ix) { return ix->nlive; }
 uint64_t orc_doc_count(const orc_index *ix) { return ix->doc_count; }
 uint64_t orc_sum_ttf(const orc_index *ix) { return ix->sum_ttf; }
 uint64_t orc_num_terms(const orc_index *ix) { return ix->terms.n; }
+uint64_t orc_malformed_docs(const orc_index *ix, uint64_t *docs, uint64_t cap) {
+  for (uint64_t i = 0; i < ix->n_malformed && i < cap; i++) docs[i] = ix->malformed[i];
+  return ix->n_malformed;
+}
 uint32_t orc_doc_len(const orc_index *ix, uint64_t d) { return d < ix->nlive ? ix->doc_len[d] : 0; }
 uint8_t orc_doc_norm(const orc_index *ix, uint64_t d) { return d < ix->nlive ? ix->doc_norm[d] : 0; }
 

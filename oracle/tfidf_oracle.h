@@ -68,6 +68,8 @@ uint64_t orc_doc_count(const orc_index *ix);     /* docs with >= 1 token */
 uint64_t orc_sum_ttf(const orc_index *ix);
 uint64_t orc_num_terms(const orc_index *ix);
 uint32_t orc_doc_len(const orc_index *ix, uint64_t doc);
+/* Committed docs whose text is not valid UTF-8 (indexed empty); returns the count. */
+uint64_t orc_malformed_docs(const orc_index *ix, uint64_t *docs, uint64_t cap);
 uint8_t orc_doc_norm(const orc_index *ix, uint64_t doc);
 /* key of doc; returns length, copies up to cap bytes */
 uint64_t orc_doc_key(const orc_index *ix, uint64_t doc, uint8_t *buf, uint64_t cap);

@@ -140,6 +140,21 @@ def test_reference_worker_and_leader(tmp_path, lucene_fixture):
     w.close()
 
 
+def test_worker_latin1_file_goes_through_extractor(tmp_path):
+    """A windows-1252 file (not UTF-8): Worker.java:199-211 hands it to Tika;
+    the mirror's extractor decodes it and the index sees the UTF-8 text."""
+    from tfidf_amd.reference_api import Worker
+    docs = tmp_path / "documents"
+    docs.mkdir()
+    (docs / "a.txt").write_bytes(b"caf\xe9 cr\xe8me br\xfbl\xe9e")
+    (docs / "b.txt").write_bytes("café noir".encode())
+    w = Worker(str(docs), str(docs / ".luceneIndex"))
+    w.init()
+    assert [r["document"]["name"] for r in w.process_documents("café")] in (["a.txt", "b.txt"], ["b.txt", "a.txt"])
+    assert [r["document"]["name"] for r in w.process_documents("crème")] == ["a.txt"]
+    w.close()
+
+
 # ---------------------------------------------------------------------------
 # synthetic Zipf corpora
 
@@ -322,12 +337,29 @@ def test_host_loader_pinned_staging_and_clear():
     dc.free()
 
 
-def test_malformed_utf8_document_rejected():
-    g = ShardIndex()
-    g.add_documents([b"fine text", "café".encode(), b"caf\xe9"])
-    with pytest.raises(UnsupportedInput):
-        g.commit()
+def test_malformed_utf8_document_indexed_empty():
+    """A document that is not valid UTF-8 (Files.readString throws,
+    Worker.java:199-211) is indexed with an empty field and listed — it does
+    not fail the commit; the other documents are unaffected."""
+    texts = [b"fine text", "caf\u00e9 au lait".encode(), b"caf\xe9 fine", b"ok \xff\xfe text", b"text again"]
+    g, o = build_pair(texts, keys=[b"%d" % i for i in range(5)])
+    assert g.malformed_docs() == o.malformed_docs() == [2, 3]
+    s = g.stats()
+    assert s["malformed_docs"] == 2 and s["num_docs"] == 5
+    assert (s["doc_count"], s["sum_ttf"], s["num_terms"]) == (o.doc_count, o.sum_ttf, o.num_terms) == (3, 7, 6)
+    for d in range(5):
+        assert g.doc_terms(d) == keyed(o.doc_terms(d))
+        assert g.doc_len(d) == (o.doc_len(d), o.doc_norm(d))
+    for q in (b"fine", b"text", b"caf\xc3\xa9"):
+        assert_hits_equal(g.search(q, 0), o.search(q, 0))
+    # replace-by-key with the extracted text, then commit again
+    g.add_documents([b"caf\xc3\xa9 fine"], [b"2"])
+    g.commit()
+    m = g.malformed_docs()                    # updateDocument: doc "3" is now id 2, "2" moved to the end
+    assert [g.doc_key(d) for d in m] == [b"3"] and g.stats()["malformed_docs"] == 1
+    assert g.doc_key(4) == b"2" and g.doc_len(4)[0] == 2
     g.close()
+    o.close()
 
 
 def test_empty_index_and_empty_docs():

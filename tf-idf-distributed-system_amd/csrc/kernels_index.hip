@@ -976,7 +976,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     prefetch_wave(p, meta, lane, v);
   }
   const uint32_t R = p.n_ranges;
-  const uint32_t dmask = p.cap_mask;
   uint16_t *slots = reinterpret_cast<uint16_t *>(sm.list);
   unsigned long long *noop = reinterpret_cast<unsigned long long *>(&sm.noop[lane]);
   // PACK per-document scratch in the histogram queue area (free after the histogram)
@@ -1615,9 +1614,9 @@ __global__ void __launch_bounds__(256) k_tokenize_long(BuildParams p) {
       __syncthreads();
       bad = (sm.flags & 16u) != 0;
     }
-    if (bad) {                                   // malformed UTF-8
-      if (tid == 0) {
-        set_err(p.err, kErrBadUtf8, d);
+    if (bad) {                                   // malformed UTF-8: indexed empty and listed
+      if (tid == 0) {                            // (Files.readString throws; the host supplies the
+        p.bad_list[atomicAdd(p.bad_count, 1u)] = d;   // extracted text, Worker.java:199-211)
         p.doc_len[d] = 0; p.doc_nuniq[d] = 0; p.doc_norm[d] = 0;
         for (uint32_t r = 0; r < p.n_ranges; r++) p.rsplit[(uint64_t)d * p.n_ranges + r] = 0;
         sm.flags = 0;

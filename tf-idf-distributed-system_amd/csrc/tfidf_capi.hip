@@ -165,6 +165,8 @@ struct tfidf_index {
   uint32_t cap_log2 = 18, C = 0, range_shift = 15, R = 1, n_blocks = 0;
   DevBuf dict, csr_col, csr_tf, doc_len, doc_nuniq, doc_norm, rsplit, long_list, uni_list, counters, blk, bbase, post, post_tmp;
   DevBuf retry_list;                   // packed wave path: documents deferred to the single-document pass
+  DevBuf bad_list;                     // documents that are not valid UTF-8 (indexed empty)
+  std::vector<uint32_t> malformed;     // ... of the last commit, ascending committed ids
   uint32_t pack_docs = 1;              // documents per wave window in the last commit
   uint64_t pack_retried = 0;           // documents the packs deferred in the last commit
   uint64_t unicode_docs = 0;           // documents with non-ASCII text in the last commit
@@ -264,7 +266,7 @@ extern "C" int tfidf_destroy(tfidf_index *ix) {
   hipStreamSynchronize(ix->copy_stream);
   DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->d_live_map, &ix->dict, &ix->csr_col, &ix->csr_tf, &ix->doc_len,
                     &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->long_list, &ix->uni_list, &ix->counters, &ix->blk,
-                    &ix->retry_list, &ix->bbase, &ix->post, &ix->post_tmp, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->dense, &ix->chunk_list, &ix->chunk_docs, &ix->chunk_fail, &ix->canon_of_slot,
+                    &ix->retry_list, &ix->bad_list, &ix->bbase, &ix->post, &ix->post_tmp, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->dense, &ix->chunk_list, &ix->chunk_docs, &ix->chunk_fail, &ix->canon_of_slot,
                     &ix->q_off, &ix->q_slot, &ix->q_w, &ix->q_role, &ix->q_meta, &ix->cache, &ix->cand, &ix->cand_n, &ix->out_doc,
                     &ix->out_score, &ix->out_n, &ix->hits, &ix->hits_n, &ix->hits_c, &ix->hits_s, &ix->hits_P, &ix->sort_tmp,
                     &ix->row_off, &ix->tvals, &ix->toff, &ix->tdf, &ix->term_tmp, &ix->sent_slot, &ix->vcounts, &ix->vnu,
@@ -714,7 +716,8 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   HIP_TRY(ix->rsplit.reserve(N * ix->R * 4 + 4));
   HIP_TRY(ix->long_list.reserve(N * 4 + 4));
   HIP_TRY(ix->uni_list.reserve(N * 4 + 4));
-  HIP_TRY(ix->counters.reserve(64));
+  HIP_TRY(ix->counters.reserve(128));
+  HIP_TRY(ix->bad_list.reserve(N * 4 + 4));
   // Short-document corpora: the wave path indexes packs of consecutive
   // documents per window (about kPackBytes of text per pack; SURVEY cfg 5
   // shape: 6 documents of ~330 B).  TFIDF_PACK_DOCS overrides (tests).
@@ -735,9 +738,9 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   }
 
   // counters: [0..2] stats u64, [3] err flags u32 + [3].hi first doc, [4] long_count, [5] retry_count,
-  // [6] uni_count
+  // [6] uni_count, [7] occupied dictionary slots, [8] bad_count
   uint64_t *ctr = ix->counters.as<uint64_t>();
-  HIP_TRY(hipMemsetAsync(ix->counters.p, 0, 64, s));
+  HIP_TRY(hipMemsetAsync(ix->counters.p, 0, 128, s));
   HIP_TRY(hipMemsetAsync(ix->dict.p, 0, (size_t)2 * C * 8, s));
 
   BuildParams bp{};
@@ -759,6 +762,8 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   bp.long_count = reinterpret_cast<uint32_t *>(ctr + 4);
   bp.uni_list = ix->uni_list.as<uint32_t>();
   bp.uni_count = reinterpret_cast<uint32_t *>(ctr + 6);
+  bp.bad_list = ix->bad_list.as<uint32_t>();
+  bp.bad_count = reinterpret_cast<uint32_t *>(ctr + 8);
   bp.stats = reinterpret_cast<unsigned long long *>(ctr);
   bp.err = reinterpret_cast<uint32_t *>(ctr + 3);
   if (const char *ds = getenv("TFIDF_DEBUG_STOP")) bp.debug_stop = (uint32_t)atoi(ds);   // profiling only
@@ -898,8 +903,6 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
     if (err & kErrCapacity)
       return fail(TFIDF_E_CAPACITY, "vocabulary exceeds 2^%u dictionary slots (raise vocab_capacity_log2)",
                   ix->cap_log2);
-    if (err & kErrBadUtf8)
-      return fail(TFIDF_E_UNSUPPORTED_INPUT, "document %u is not valid UTF-8", err_doc);
     return fail(TFIDF_E_UNSUPPORTED_INPUT, "index build error flags 0x%x (doc %u)", err, err_doc);
   }
   ix->doc_count = hctr[0];
@@ -998,9 +1001,14 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   // occupied dictionary slots counted on the device (ctr[7]) instead of a host
   // pass over the mirror (8 M slots at 2^23 took milliseconds)
   HIP_TRY(launch_count_nonzero(ix->dict.as<uint64_t>(), C, reinterpret_cast<unsigned long long *>(ctr + 7), s));
-  uint64_t tail[5];                         // ctr[3] error flags .. ctr[7] occupied slots
+  uint64_t tail[6];                         // ctr[3] error flags .. ctr[7] occupied slots, ctr[8] malformed
   HIP_TRY(hipMemcpyAsync(tail, ctr + 3, sizeof tail, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  ix->malformed.resize((uint32_t)tail[5]);
+  if (!ix->malformed.empty()) {
+    HIP_TRY(hipMemcpy(ix->malformed.data(), ix->bad_list.p, ix->malformed.size() * 4, hipMemcpyDeviceToHost));
+    std::sort(ix->malformed.begin(), ix->malformed.end());
+  }
   const uint32_t err2 = (uint32_t)tail[0];
   if (err2 & kErrTfTooLarge) return fail(TFIDF_E_UNSUPPORTED_INPUT, "a term frequency exceeds 2^24 - 1");
   ix->num_terms = tail[4];
@@ -1044,6 +1052,7 @@ extern "C" int tfidf_stats(const tfidf_index *ix, tfidf_index_stats *out) {
   out->pack_retried = ix->pack_retried;
   out->unicode_docs = ix->unicode_docs;
   out->long_chunked = ix->long_chunked;
+  out->malformed_docs = ix->committed ? ix->malformed.size() : 0;
   const DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->dict, &ix->csr_col, &ix->csr_tf, &ix->doc_len,
                           &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->blk, &ix->bbase, &ix->post,
                           &ix->toff, &ix->tdf};
@@ -1451,6 +1460,16 @@ extern "C" int tfidf_doc_keys(const tfidf_index *ix, uint8_t *buf, uint64_t cap,
     }
     offsets[d + 1] = p;
   }
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_malformed_docs(const tfidf_index *ix, uint64_t *docs, uint64_t cap, uint64_t *n_out) {
+  if (!ix || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
+  *n_out = ix->malformed.size();
+  if (ix->malformed.size() > cap || (cap && !docs && !ix->malformed.empty()))
+    return fail(TFIDF_E_BUFFER, "need %zu entries", ix->malformed.size());
+  for (size_t i = 0; i < ix->malformed.size(); i++) docs[i] = ix->malformed[i];
   return TFIDF_OK;
 }
 

@@ -9,7 +9,6 @@
 namespace tfidf {
 
 // Error flags raised by kernels (device word err[0]; err[1] = first doc).
-constexpr uint32_t kErrBadUtf8 = 1u;          // malformed UTF-8 (Files.readString would throw)
 constexpr uint32_t kErrCapacity = 4u;
 constexpr uint32_t kErrTfTooLarge = 8u;
 constexpr uint32_t kErrLongScratch = 16u;
@@ -39,6 +38,8 @@ struct BuildParams {
   uint32_t *long_count;
   uint32_t *uni_list;         // docs the ASCII wave path found non-ASCII bytes in (Unicode wave path)
   uint32_t *uni_count;
+  uint32_t *bad_list;         // docs that are not valid UTF-8 (indexed empty; tfidf_malformed_docs)
+  uint32_t *bad_count;
   unsigned long long *stats;  // [0] docCount, [1] sumTotalTermFreq, [2] nnz
   uint32_t *err;              // [0] flags, [1] first offending doc
   // long path scratch (one table region per workgroup)

@@ -41,7 +41,8 @@ class Config(C.Structure):
 class IndexStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("num_docs", "doc_count", "sum_ttf", "num_terms", "nnz",
                                           "device_bytes", "long_docs", "text_bytes", "term_major",
-                                          "pack_docs", "pack_retried", "unicode_docs", "long_chunked")]
+                                          "pack_docs", "pack_retried", "unicode_docs", "long_chunked",
+                                          "malformed_docs")]
 
 
 class CommitTiming(C.Structure):
@@ -99,6 +100,7 @@ SIGNATURES = {
     "tfidf_sort_names": (C.c_int, [C.c_char_p, U64P, C.c_uint64, U64P]),
     "tfidf_doc_key": (C.c_int, [VP, C.c_uint64, C.c_char_p, C.c_uint64, U64P]),
     "tfidf_doc_len": (C.c_int, [VP, C.c_uint64, U32P, U8P]),
+    "tfidf_malformed_docs": (C.c_int, [VP, U64P, C.c_uint64, U64P]),
     "tfidf_doc_terms": (C.c_int, [VP, C.c_uint64, C.c_char_p, C.c_uint64, U32P, C.c_uint64, U64P]),
     "tfidf_term_df": (C.c_int, [VP, C.c_char_p, C.c_uint64, U64P, U64P]),
     "tfidf_vocab_size": (C.c_int, [VP, U64P]),

@@ -206,6 +206,14 @@ class ShardIndex:
         L.check(lib.tfidf_doc_keys(self._h, buf, need.value, L.ptr(offs, C.c_uint64), C.byref(need)))
         return np.frombuffer(buf.raw[:need.value], np.uint8).copy(), offs
 
+    def malformed_docs(self):
+        """Committed doc ids whose bytes are not valid UTF-8 (indexed empty)."""
+        n = self.stats()["malformed_docs"]
+        out = np.zeros(max(n, 1), np.uint64)
+        m = C.c_uint64()
+        L.check(L.load().tfidf_malformed_docs(self._h, L.ptr(out, C.c_uint64), len(out), C.byref(m)))
+        return out[:m.value].tolist()
+
     def doc_len(self, doc):
         ln, nm = C.c_uint32(), C.c_uint8()
         L.check(L.load().tfidf_doc_len(self._h, doc, C.byref(ln), C.byref(nm)))

@@ -17,6 +17,22 @@ from . import _lib as L
 from .engine import ShardIndex, leader_merge
 
 
+def extract_text(data: bytes) -> bytes:
+    """Stand-in for the reference's Tika fallback (AutoDetectParser +
+    BodyContentHandler, Worker.java:201-211) on a file that is not valid
+    UTF-8: plain text in a single-byte Western encoding is decoded as
+    windows-1252 (bytes it leaves undefined as Latin-1) and re-encoded as
+    UTF-8.  Tika's own charset detection and its parsers for binary formats
+    (PDF, Office) are not rebuilt: parity unpinned."""
+    out = []
+    for b in data:
+        try:
+            out.append(bytes([b]).decode("cp1252"))
+        except UnicodeDecodeError:
+            out.append(chr(b))
+    return "".join(out).encode("utf-8")
+
+
 def document_score_info(name: str, score: float):
     """Jackson form of DocumentScoreInfo: {"document": {"name": ...}, "score": double}."""
     return {"document": {"name": name}, "score": float(score)}
@@ -66,7 +82,7 @@ class Worker:
         for p in paths:
             try:
                 k, t = self._read(p)
-            except Exception:
+            except OSError:
                 continue                      # Worker.java:83-85: log and skip
             keys.append(k)
             texts.append(t)
@@ -80,7 +96,10 @@ class Worker:
         rel = os.path.relpath(absp, base) if absp.startswith(base + os.sep) else os.path.basename(absp)
         with open(absp, "rb") as f:
             data = f.read()
-        data.decode("utf-8")                  # Files.readString: strict UTF-8 (Tika fallback not rebuilt)
+        try:
+            data.decode("utf-8")              # Files.readString: strict UTF-8
+        except UnicodeDecodeError:
+            data = extract_text(data)         # MalformedInputException -> Tika (Worker.java:199-211)
         return rel.encode(), data
 
     # Worker.java:190-220 addDocToIndex (updateDocument by Term("path", rel))
