@@ -64,10 +64,7 @@ __device__ __forceinline__ uint32_t block_excl_scan_256(uint32_t v, uint32_t *sh
   return base + x - v;
 }
 
-__device__ __forceinline__ void set_err(uint32_t *err, uint32_t flag, uint32_t doc) {
-  uint32_t old = atomicOr(err, flag);
-  if (old == 0) atomicExch(err + 1, doc);
-}
+__device__ __forceinline__ void set_err(uint32_t *err, uint32_t flag, uint32_t doc) { set_build_err(err, flag, doc); }
 
 // Per-document table in global memory (long path).  Only the owning
 // workgroup touches it, so workgroup-scope atomics are sufficient.
@@ -1220,9 +1217,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     if (PACK) {
       for (uint32_t i = lane; i < nu; i += 64) {
         const uint32_t t = st_tf[i], j = t >> 24;
-        const uint64_t row = pk_row[j] + i - pk_start[j];
-        p.csr_col[row] = st_col[i];
-        p.csr_tf[row] = t & 0xFFFFFFu;
+        csr_put(p, pk_row[j] + i - pk_start[j], st_col[i], t & 0xFFFFFFu, (uint32_t)(d + j));
       }
       if (lane < np) {
         const uint32_t lj = pk_len[lane], nj = pk_nu[lane];
@@ -1238,10 +1233,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     }
     {
       const uint64_t row = csr_row_base(p.offsets, src);
-      for (uint32_t i = lane; i < nu; i += 64) {
-        p.csr_col[row + i] = st_col[i];
-        p.csr_tf[row + i] = st_tf[i];
-      }
+      for (uint32_t i = lane; i < nu; i += 64) csr_put(p, row + i, st_col[i], st_tf[i], (uint32_t)d);
     }
     clear_table(sm, lane);
     if (lane == 0) {
@@ -1493,7 +1485,7 @@ __global__ void __launch_bounds__(1024) k_long_rows(BuildParams p) {
     const uint32_t vals[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
     for (int q = 0; q < 4; q++)
-      if (vals[q]) { p.csr_col[row + at] = i0 + q; p.csr_tf[row + at] = vals[q]; at++; }
+      if (vals[q]) { csr_put(p, row + at, i0 + q, vals[q], (uint32_t)d); at++; }
     __syncthreads();
     if (tid == 0) {
       carry += all;
@@ -1669,8 +1661,7 @@ __global__ void __launch_bounds__(256) k_tokenize_long(BuildParams p) {
       if (__hip_atomic_load(keys + 2 * (size_t)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) continue;
       const uint32_t g = gsl[s];
       const uint32_t pos = atomicAdd(&sm.rcur[g >> p.range_shift], 1u);
-      p.csr_col[base + pos] = g;
-      p.csr_tf[base + pos] = __hip_atomic_load(cnt + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      csr_put(p, base + pos, g, __hip_atomic_load(cnt + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), d);
     }
     __syncthreads();
     if (tid == 0) { sm.len = 0; sm.flags = 0; sm.nu = 0; }
@@ -1738,22 +1729,35 @@ __device__ __forceinline__ InvGroup inv_group(const PostingParams &p, uint64_t d
   return g;
 }
 
-// segment entries off of the group's documents (kInvalidSlot past a segment)
-__device__ __forceinline__ void inv_load(const PostingParams &p, const InvGroup &g, uint32_t off, uint32_t *c,
-                                         uint32_t *t, bool with_tf) {
+// packed CSR words off of the group's documents' segments (0 past a segment)
+__device__ __forceinline__ void inv_load(const PostingParams &p, const InvGroup &g, uint32_t off, uint32_t *c) {
 #pragma unroll
   for (int j = 0; j < kInvDocs; j++) {
     const bool in = g.lo[j] + off < g.hi[j];
-    c[j] = in ? p.csr_col[g.base[j] + g.lo[j] + off] : kInvalidSlot;
-    if (with_tf) t[j] = in ? p.csr_tf[g.base[j] + g.lo[j] + off] : 0u;
+    c[j] = in ? p.csr[g.base[j] + g.lo[j] + off] : 0u;
   }
 }
 
-// grid (n_blocks, n_ranges), 1024 threads, LDS histogram of one slot range.
-// Wave w handles documents d0 + w + 16 (kInvDocs i + j), j < kInvDocs.
+// (block, range) tile of a 1-D grid of tiles_grid() workgroups: the R tiles
+// of a block get workgroup ids congruent mod 8, dispatched together, so they
+// run on one XCD and the CSR lines their row segments share come from that
+// XCD's L2 instead of being fetched once per range (dispatch order is only a
+// placement hint: correctness never depends on it).
+__device__ __forceinline__ bool tile_of(uint32_t w, uint32_t n_blocks, uint32_t R, uint32_t *b, uint32_t *r) {
+  const uint32_t g = w / (8 * R), rem = w - g * 8 * R;
+  *r = rem >> 3;
+  *b = g * 8 + (rem & 7);
+  return *b < n_blocks;
+}
+static uint32_t tiles_grid(uint32_t n_blocks, uint32_t R) { return (n_blocks + 7) / 8 * 8 * R; }
+
+// one workgroup (1024 threads) per (block, range) tile (tile_of), LDS
+// histogram of the range's slots.  Wave w handles documents d0 + w + 16
+// (kInvDocs i + j), j < kInvDocs.
 __global__ void __launch_bounds__(1024) k_df_partial(PostingParams p) {
   extern __shared__ uint32_t hist[];
-  const uint32_t b = blockIdx.x, r = blockIdx.y;
+  uint32_t b, r;
+  if (!tile_of(blockIdx.x, p.n_blocks, p.n_ranges, &b, &r)) return;
   const uint32_t RS = 1u << p.range_shift;
   for (uint32_t i = threadIdx.x; i < RS; i += blockDim.x) hist[i] = 0;
   __syncthreads();
@@ -1765,21 +1769,21 @@ __global__ void __launch_bounds__(1024) k_df_partial(PostingParams p) {
   const uint64_t step = (uint64_t)nw * kInvDocs;
   uint64_t dd = d0 + wid;
   InvGroup cur = inv_group(p, dd, d1, nw, r, false);
-  uint32_t c[kInvDocs], t[kInvDocs];
-  if (dd < d1) inv_load(p, cur, lane, c, t, false);
+  uint32_t c[kInvDocs];
+  if (dd < d1) inv_load(p, cur, lane, c);
   while (dd < d1) {
     const uint64_t dn = dd + step;
     const InvGroup nxt = inv_group(p, dn, d1, nw, r, false);
-    uint32_t cn[kInvDocs], tn[kInvDocs];
-    if (dn < d1) inv_load(p, nxt, lane, cn, tn, false);            // next group in flight
+    uint32_t cn[kInvDocs];
+    if (dn < d1) inv_load(p, nxt, lane, cn);                       // next group in flight
 #pragma unroll
     for (int j = 0; j < kInvDocs; j++)
-      if (c[j] != kInvalidSlot) atomicAdd(&hist[c[j] & rmask], 1u);
+      if (c[j]) atomicAdd(&hist[c[j] & rmask], 1u);
     for (uint32_t off = lane + 64; off < cur.maxn; off += 64) {     // segments longer than 64
-      inv_load(p, cur, off, c, t, false);
+      inv_load(p, cur, off, c);
 #pragma unroll
       for (int j = 0; j < kInvDocs; j++)
-        if (c[j] != kInvalidSlot) atomicAdd(&hist[c[j] & rmask], 1u);
+        if (c[j]) atomicAdd(&hist[c[j] & rmask], 1u);
     }
     cur = nxt;
 #pragma unroll
@@ -1899,17 +1903,17 @@ static_assert(kTmpTfShift <= 22, "temp word layout");
 
 __device__ __forceinline__ void part_entries(const PostingParams &p, uint32_t *bcur, uint32_t rmask, uint64_t bb,
                                              const InvGroup &g, uint64_t dd, uint32_t d0l, uint32_t stride,
-                                             const uint32_t *c, const uint32_t *t, bool *tf_big) {
+                                             const uint32_t *c) {
   const uint32_t lane = threadIdx.x & 63;
   constexpr uint32_t kNoop = kRangeSlots / kSubSlots;       // idle lanes bump a spare cursor
 #pragma unroll
   for (int j = 0; j < kInvDocs; j++) {
-    const bool in = c[j] != kInvalidSlot;
+    const bool in = c[j] != 0;
     if (!__any(in)) continue;                                 // wave-uniform
-    *tf_big |= in && t[j] > kMaxTf;
     const uint32_t sl = c[j] & rmask;
     const uint32_t dl = (uint32_t)(dd + (uint64_t)stride * j) - d0l;
-    const uint32_t val = dl | ((sl & (kSubSlots - 1)) << 13) | (min(t[j], kTmpTfEsc) << kTmpTfShift);
+    const uint32_t tf = csr_tf_field(c[j], p.range_shift);
+    const uint32_t val = dl | ((sl & (kSubSlots - 1)) << 13) | (min(tf, kTmpTfEsc) << kTmpTfShift);
     const uint32_t pos = cursor_bump<kRangeBits - kSubBits + 1>(bcur, in ? sl >> kSubBits : kNoop, lane);
     if (in) p.post_tmp[bb + pos] = val;
   }
@@ -1930,22 +1934,21 @@ struct PartWave {
 
 __device__ __forceinline__ void part_group_staged(const PostingParams &p, uint32_t *bcur, PartWave &w, uint32_t rmask,
                                                   uint64_t bb, const InvGroup &g, uint64_t dd, uint32_t d0l,
-                                                  uint32_t stride, const uint32_t *c, const uint32_t *t,
-                                                  bool *tf_big) {
+                                                  uint32_t stride, const uint32_t *c) {
   const uint32_t lane = threadIdx.x & 63;
   uint64_t val[kInvDocs];
   uint32_t rank[kInvDocs], sj[kInvDocs];
 #pragma unroll
   for (int j = 0; j < kInvDocs; j++) {
-    const bool in = c[j] != kInvalidSlot;
+    const bool in = c[j] != 0;
     const uint32_t sl = c[j] & rmask;
     sj[j] = sl >> kSubBits;
     rank[j] = 0;
     val[j] = 0;
     if (in) {
-      *tf_big |= t[j] > kMaxTf;
       const uint32_t dl = (uint32_t)(dd + (uint64_t)stride * j) - d0l;
-      val[j] = (uint64_t)(dl | ((sl & (kSubSlots - 1)) << 13) | (min(t[j], kTmpTfEsc) << kTmpTfShift)) |
+      const uint32_t tf = csr_tf_field(c[j], p.range_shift);
+      val[j] = (uint64_t)(dl | ((sl & (kSubSlots - 1)) << 13) | (min(tf, kTmpTfEsc) << kTmpTfShift)) |
                ((uint64_t)sj[j] << 56);
       rank[j] = atomicAdd(&w.cnt[sj[j]], 1u);
     }
@@ -1958,7 +1961,7 @@ __device__ __forceinline__ void part_group_staged(const PostingParams &p, uint32
   w.cnt[lane] = 0;
 #pragma unroll
   for (int j = 0; j < kInvDocs; j++)
-    if (c[j] != kInvalidSlot) w.stage[w.soff[sj[j]] + rank[j]] = val[j];
+    if (c[j] != 0) w.stage[w.soff[sj[j]] + rank[j]] = val[j];
   for (uint32_t t0 = 0; t0 < T; t0 += 64) {
     const uint32_t ti = t0 + lane;
     if (ti < T) {
@@ -1974,7 +1977,8 @@ __global__ void __launch_bounds__(1024) k_scatter_part(PostingParams p) {
   __shared__ PartWave pwave[16];
   const uint32_t lane = threadIdx.x & 63, nw = blockDim.x >> 6;
   const uint32_t wid = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const uint32_t b = blockIdx.x, r = blockIdx.y;
+  uint32_t b, r;
+  if (!tile_of(blockIdx.x, p.n_blocks, p.n_ranges, &b, &r)) return;
   const uint32_t RS = 1u << p.range_shift, rmask = RS - 1;
   const uint32_t nsub = RS > kSubSlots ? RS / kSubSlots : 1u;
   const uint32_t *row = p.blk + (size_t)b * p.C + ((size_t)r << p.range_shift);
@@ -1985,27 +1989,25 @@ __global__ void __launch_bounds__(1024) k_scatter_part(PostingParams p) {
   const uint64_t d0 = (uint64_t)b * kBlockDocs;
   const uint64_t d1 = d0 + kBlockDocs < p.n_docs ? d0 + kBlockDocs : p.n_docs;
   const uint64_t step = (uint64_t)nw * kInvDocs;
-  bool tf_big = false;
   uint64_t dd = d0 + wid;
   InvGroup g = inv_group(p, dd, d1, nw, r, false);
-  uint32_t c[kInvDocs], t[kInvDocs];
-  if (dd < d1) inv_load(p, g, lane, c, t, true);
+  uint32_t c[kInvDocs];
+  if (dd < d1) inv_load(p, g, lane, c);
   while (dd < d1) {
     const uint64_t dn = dd + step;
     const InvGroup gn = inv_group(p, dn, d1, nw, r, false);
-    uint32_t cn[kInvDocs], tn[kInvDocs];
-    if (dn < d1) inv_load(p, gn, lane, cn, tn, true);           // next group in flight
-    part_group_staged(p, bcur, pwave[wid], rmask, bb, g, dd, (uint32_t)d0, nw, c, t, &tf_big);
+    uint32_t cn[kInvDocs];
+    if (dn < d1) inv_load(p, gn, lane, cn);                       // next group in flight
+    part_group_staged(p, bcur, pwave[wid], rmask, bb, g, dd, (uint32_t)d0, nw, c);
     for (uint32_t off = lane + 64; off < g.maxn; off += 64) {    // segments longer than 64
-      inv_load(p, g, off, c, t, true);
-      part_entries(p, bcur, rmask, bb, g, dd, (uint32_t)d0, nw, c, t, &tf_big);
+      inv_load(p, g, off, c);
+      part_entries(p, bcur, rmask, bb, g, dd, (uint32_t)d0, nw, c);
     }
     g = gn;
 #pragma unroll
-    for (int j = 0; j < kInvDocs; j++) { c[j] = cn[j]; t[j] = tn[j]; }
+    for (int j = 0; j < kInvDocs; j++) c[j] = cn[j];
     dd = dn;
   }
-  if (tf_big) atomicOr(p.err, kErrTfTooLarge);
 }
 
 // tf of (doc, slot) from the document's CSR row segment of range r (the
@@ -2014,8 +2016,14 @@ __device__ uint32_t csr_tf_of(const PostingParams &p, uint64_t d, uint32_t r, ui
   uint64_t base;
   uint32_t lo, hi;
   doc_segment(p, d, r, &base, &lo, &hi);
-  for (uint32_t i = lo; i < hi; i++)
-    if (p.csr_col[base + i] == slot) return p.csr_tf[base + i];
+  const uint32_t local = csr_local(slot, p.range_shift), esc = csr_esc_value(p.range_shift);
+  for (uint32_t i = lo; i < hi; i++) {
+    const uint32_t e = p.csr[base + i];
+    if (csr_local(e, p.range_shift) == local) {
+      const uint32_t f = csr_tf_field(e, p.range_shift);
+      return f == esc ? csr_esc_tf(p.csr_esc, p.n_esc, base + i) : f;
+    }
+  }
   return 0;
 }
 
@@ -2058,7 +2066,13 @@ __global__ void __launch_bounds__(1024) k_scatter_sort(PostingParams p) {
       const uint32_t doc = d0 + (x[u] & (kBlockDocs - 1));
       uint32_t tf = x[u] >> kTmpTfShift;
       if (in && tf == kTmpTfEsc) tf = csr_tf_of(p, doc, r, (uint32_t)s0 + sl);      // rare: tf >= 1023
-      if (in) p.post[bb + pos] = (uint64_t)doc | ((uint64_t)((tf << 8) | nrm[u]) << 32);
+      if (in) {
+        p.post[bb + pos] = post_word(x[u] & (kBlockDocs - 1), tf, nrm[u]);
+        if (tf >= kPostTfEsc) {                                                 // rare: tf >= 2047
+          const uint32_t at = atomicAdd(p.post_esc_count, 1u);
+          if (at < p.post_esc_cap) p.post_esc[at] = ((bb + pos) << 24) | tf;
+        }
+      }
     }
   }
 }
@@ -2093,7 +2107,7 @@ static void allow_big_lds() {
 hipError_t launch_df_partial(const PostingParams &p, hipStream_t s) {
   allow_big_lds();
   const size_t lds = sizeof(uint32_t) << p.range_shift;
-  hipLaunchKernelGGL(k_df_partial, dim3(p.n_blocks, p.n_ranges), dim3(1024), lds, s, p);
+  hipLaunchKernelGGL(k_df_partial, dim3(tiles_grid(p.n_blocks, p.n_ranges)), dim3(1024), lds, s, p);
   return hipGetLastError();
 }
 hipError_t launch_df_sum(const PostingParams &p, hipStream_t s) {
@@ -2124,7 +2138,7 @@ hipError_t launch_block_base(const PostingParams &p, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t launch_scatter(const PostingParams &p, hipStream_t s) {
-  hipLaunchKernelGGL(k_scatter_part, dim3(p.n_blocks, p.n_ranges), dim3(1024), 0, s, p);
+  hipLaunchKernelGGL(k_scatter_part, dim3(tiles_grid(p.n_blocks, p.n_ranges)), dim3(1024), 0, s, p);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const uint32_t RS = 1u << p.range_shift;

@@ -119,6 +119,17 @@ __device__ __forceinline__ void term_block_range(const QueryParams &p, uint32_t 
   *z = wave_lower_bound(p.post, lo, t1, d0 + kBlockDocs);
 }
 
+// Posting i of the block starting at doc d0 as the u64 word doc | (tf << 8 |
+// norm) << 32 (term-major postings are stored that way; block-major ones are
+// u32 post_word, tf escapes looked up in the sorted escape list)
+__device__ __forceinline__ uint64_t post_at(const QueryParams &p, uint64_t i, uint32_t d0) {
+  if (p.toff) return p.post[i];
+  const uint32_t v = p.post32[i];
+  uint32_t tf = (v >> 13) & kPostTfEsc;
+  if (tf == kPostTfEsc) tf = csr_esc_tf(p.post_esc, p.n_post_esc, i);
+  return (uint64_t)(d0 + (v & (kBlockDocs - 1))) | ((uint64_t)((tf << 8) | (v >> 24)) << 32);
+}
+
 constexpr uint32_t kQTermsFast = 4;   // query terms whose ranges / first chunk are prefetched
 
 // kOps: queries with MUST / MUST_NOT clauses (QueryParser operator words,
@@ -223,7 +234,7 @@ __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
 #pragma unroll
     for (uint32_t j = 0; j < kQTermsFast; j++) {
       pre[j] = 0;
-      if (j < t1 - t0 && sm.tlo[j] + tid < sm.thi[j]) pre[j] = p.post[sm.tlo[j] + tid];
+      if (j < t1 - t0 && sm.tlo[j] + tid < sm.thi[j]) pre[j] = post_at(p, sm.tlo[j] + tid, (uint32_t)d0);
     }
     uint32_t my_new = 0;
     for (uint32_t j = t0; j < t1; j++) {
@@ -262,7 +273,7 @@ __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
           for (uint32_t u = 0; u < kQTermsFast; u++)
             if (u == jj) e = pre[u];
         } else {
-          e = p.post[i];
+          e = post_at(p, i, (uint32_t)d0);
         }
         const uint32_t ld = (uint32_t)(e & 0xFFFFFFFFu) - (uint32_t)d0;
         const uint32_t bit = 1u << (ld & 31);
@@ -681,7 +692,7 @@ __global__ void __launch_bounds__(kPairWaves * 64) k_score_pairs(QueryParams p) 
 #pragma unroll
       for (uint32_t c = 0; c < 2; c++) {
         const uint64_t i = ja + lane + 64 * c;
-        pre[j][c] = (j < nt && i < jz) ? p.post[i] : 0ull;
+        pre[j][c] = (j < nt && i < jz) ? post_at(p, i, d0) : 0ull;
       }
     }
     {
@@ -736,7 +747,7 @@ __global__ void __launch_bounds__(kPairWaves * 64) k_score_pairs(QueryParams p) 
 #pragma unroll
         for (int u = 0; u < 4; u++) {
           const uint64_t i = i0 + 64 * u + lane;
-          e[u] = i < jz ? p.post[i] : 0ull;
+          e[u] = i < jz ? post_at(p, i, d0) : 0ull;
         }
 #pragma unroll
         for (int u = 0; u < 4; u++)

@@ -41,7 +41,9 @@ __global__ void __launch_bounds__(256) k_term_pairs(TermParams p) {
     const uint64_t base = csr_row_base(p.offsets, src);
     const uint32_t n = p.doc_nuniq[d], o = p.row_off[d], nrm = p.doc_norm[d];
     for (uint32_t j = lane; j < n; j += 64) {
-      const uint32_t c = p.csr_col[base + j], t = p.csr_tf[base + j];
+      const uint32_t e = p.csr[base + j], c = csr_local(e, p.slot_bits);
+      uint32_t t = csr_tf_field(e, p.slot_bits);
+      if (t == csr_esc_value(p.slot_bits)) t = csr_esc_tf(p.csr_esc, p.n_esc, base + j);
       if (t >= (1u << 24)) atomicOr(p.err, kErrTfTooLarge);
       p.keys[o + j] = c;
       p.vals[o + j] = d | ((uint64_t)((t << 8) | nrm) << 32);

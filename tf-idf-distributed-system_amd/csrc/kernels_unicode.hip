@@ -282,8 +282,7 @@ __global__ void __launch_bounds__(64) k_tokenize_uwave(BuildParams p) {
       if (sm.khi[s] == 0) continue;
       const uint32_t gs = (uint32_t)sm.klo[s];
       const uint32_t at = atomicAdd(&sm.rcnt[gs >> p.range_shift], 1u);
-      p.csr_col[base + at] = gs;
-      p.csr_tf[base + at] = sm.cnt[s];
+      csr_put(p, base + at, gs, sm.cnt[s], d);
     }
     if (lane == 0) {
       p.doc_len[d] = len;

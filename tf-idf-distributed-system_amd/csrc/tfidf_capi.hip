@@ -163,10 +163,12 @@ struct tfidf_index {
   std::vector<uint32_t> live_map;  // committed -> staged (empty = identity)
   DevBuf d_live_map;
   uint32_t cap_log2 = 18, C = 0, range_shift = 15, R = 1, n_blocks = 0;
-  DevBuf dict, csr_col, csr_tf, doc_len, doc_nuniq, doc_norm, rsplit, long_list, uni_list, counters, blk, bbase, post, post_tmp;
+  DevBuf dict, csr, csr_esc, post_esc, doc_len, doc_nuniq, doc_norm, rsplit, long_list, uni_list, counters, blk, bbase, post, post_tmp;
   DevBuf retry_list;                   // packed wave path: documents deferred to the single-document pass
   DevBuf bad_list;                     // documents that are not valid UTF-8 (indexed empty)
   std::vector<uint32_t> malformed;     // ... of the last commit, ascending committed ids
+  std::vector<uint64_t> h_esc;         // CSR tf escapes of the last build, sorted (csr_put)
+  std::vector<uint64_t> h_post_esc;    // block-major posting tf escapes, sorted (post_word)
   uint32_t pack_docs = 1;              // documents per wave window in the last commit
   uint64_t pack_retried = 0;           // documents the packs deferred in the last commit
   uint64_t unicode_docs = 0;           // documents with non-ASCII text in the last commit
@@ -264,9 +266,9 @@ extern "C" int tfidf_destroy(tfidf_index *ix) {
   DeviceGuard g(ix->cfg.device);
   hipStreamSynchronize(ix->stream);
   hipStreamSynchronize(ix->copy_stream);
-  DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->d_live_map, &ix->dict, &ix->csr_col, &ix->csr_tf, &ix->doc_len,
+  DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->d_live_map, &ix->dict, &ix->csr, &ix->csr_esc, &ix->doc_len,
                     &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->long_list, &ix->uni_list, &ix->counters, &ix->blk,
-                    &ix->retry_list, &ix->bad_list, &ix->bbase, &ix->post, &ix->post_tmp, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->dense, &ix->chunk_list, &ix->chunk_docs, &ix->chunk_fail, &ix->canon_of_slot,
+                    &ix->retry_list, &ix->bad_list, &ix->bbase, &ix->post, &ix->post_tmp, &ix->post_esc, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->dense, &ix->chunk_list, &ix->chunk_docs, &ix->chunk_fail, &ix->canon_of_slot,
                     &ix->q_off, &ix->q_slot, &ix->q_w, &ix->q_role, &ix->q_meta, &ix->cache, &ix->cand, &ix->cand_n, &ix->out_doc,
                     &ix->out_score, &ix->out_n, &ix->hits, &ix->hits_n, &ix->hits_c, &ix->hits_s, &ix->hits_P, &ix->sort_tmp,
                     &ix->row_off, &ix->tvals, &ix->toff, &ix->tdf, &ix->term_tmp, &ix->sent_slot, &ix->vcounts, &ix->vnu,
@@ -708,8 +710,11 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   ix->R = C >> ix->range_shift;
 
   HIP_TRY(ix->dict.reserve((size_t)2 * C * 8));
-  HIP_TRY(ix->csr_col.reserve(row_cap * 4));
-  HIP_TRY(ix->csr_tf.reserve(row_cap * 4));
+  HIP_TRY(ix->csr.reserve(row_cap * 4));
+  // escapes: each needs tf >= the field's escape value, and a row holds at
+  // most row_cap tokens in all, so this bounds their number
+  const uint64_t esc_cap = row_cap / csr_esc_value(ix->range_shift) + 64;
+  HIP_TRY(ix->csr_esc.reserve(esc_cap * 8));
   HIP_TRY(ix->doc_len.reserve(N * 4 + 4));
   HIP_TRY(ix->doc_nuniq.reserve(N * 4 + 4));
   HIP_TRY(ix->doc_norm.reserve(N + 16));
@@ -738,7 +743,7 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   }
 
   // counters: [0..2] stats u64, [3] err flags u32 + [3].hi first doc, [4] long_count, [5] retry_count,
-  // [6] uni_count, [7] occupied dictionary slots, [8] bad_count
+  // [6] uni_count, [7] occupied dictionary slots, [8] bad_count, [9] CSR escape count
   uint64_t *ctr = ix->counters.as<uint64_t>();
   HIP_TRY(hipMemsetAsync(ix->counters.p, 0, 128, s));
   HIP_TRY(hipMemsetAsync(ix->dict.p, 0, (size_t)2 * C * 8, s));
@@ -752,8 +757,10 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   bp.cap_mask = C - 1;
   bp.range_shift = ix->range_shift;
   bp.n_ranges = ix->R;
-  bp.csr_col = ix->csr_col.as<uint32_t>();
-  bp.csr_tf = ix->csr_tf.as<uint32_t>();
+  bp.csr = ix->csr.as<uint32_t>();
+  bp.csr_esc = ix->csr_esc.as<uint64_t>();
+  bp.esc_count = reinterpret_cast<uint32_t *>(ctr + 9);
+  bp.esc_cap = esc_cap;
   bp.doc_len = ix->doc_len.as<uint32_t>();
   bp.doc_nuniq = ix->doc_nuniq.as<uint32_t>();
   bp.doc_norm = ix->doc_norm.as<uint8_t>();
@@ -808,9 +815,9 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
     return TFIDF_OK;
   }
   // one read of the counters: stats (0-2), error flags (3), long (4) and
-  // non-ASCII (6) document counts (32-bit counters in the low halves); read
-  // again only when the long path ran
-  uint64_t hctr[7];
+  // non-ASCII (6) document counts, CSR escapes (9) (32-bit counters in the low
+  // halves); read again only when the long path ran
+  uint64_t hctr[10];
   HIP_TRY(hipMemcpyAsync(hctr, ctr, sizeof hctr, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   const uint32_t n_long = (uint32_t)hctr[4], n_uni = (uint32_t)hctr[6];
@@ -894,7 +901,7 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
       HIP_TRY(launch_tokenize_long(bp, (int)wgs, s));
     }
     HIP_TRY(hipEventRecord(ix->ev[EV_LONG], s));
-    HIP_TRY(hipMemcpyAsync(hctr, ctr, 5 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(hctr, ctr, sizeof hctr, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
   }
   const uint32_t err = (uint32_t)(hctr[3] & 0xFFFFFFFFu), err_doc = (uint32_t)(hctr[3] >> 32);
@@ -908,9 +915,27 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   ix->doc_count = hctr[0];
   ix->sum_ttf = hctr[1];
   ix->nnz = hctr[2];
+  // CSR tf escapes (rare: block-major only for tf >= 2^17): sorted by entry
+  // index for the binary searches of the inversion and tfidf_doc_terms
+  {
+    const uint64_t n_esc = (uint32_t)hctr[9];
+    if (n_esc > esc_cap) return fail(TFIDF_E_CAPACITY, "CSR escape list overflow");
+    ix->h_esc.resize(n_esc);
+    if (n_esc) {
+      HIP_TRY(hipMemcpyAsync(ix->h_esc.data(), ix->csr_esc.p, n_esc * 8, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      std::sort(ix->h_esc.begin(), ix->h_esc.end());
+      HIP_TRY(hipMemcpyAsync(ix->csr_esc.p, ix->h_esc.data(), n_esc * 8, hipMemcpyHostToDevice, s));
+      HIP_TRY(hipStreamSynchronize(s));
+    }
+  }
   if (ix->nnz >= 0xFFFFFFFFull) return fail(TFIDF_E_CAPACITY, "more than 2^32 postings per shard");
-  HIP_TRY(ix->post.reserve(ix->nnz * 8 + 8));
-  HIP_TRY(ix->post_tmp.reserve(ix->nnz * 8 + 8));
+  // postings: block-major u32 (post_word), term-major u64; pass-1 temp words u32
+  // (term-major: the sort's u64 value buffer)
+  HIP_TRY(ix->post.reserve(ix->nnz * (ix->term_major ? 8 : 4) + 8));
+  HIP_TRY(ix->post_tmp.reserve(ix->nnz * (ix->term_major ? 8 : 4) + 8));
+  const uint64_t post_esc_cap = row_cap / kPostTfEsc + 64;       // each needs tf >= 2047 tokens of one doc
+  if (!ix->term_major) HIP_TRY(ix->post_esc.reserve(post_esc_cap * 8));
 
   // the dictionary is final here (wave, Unicode and long paths done): a large
   // host mirror (>= 32 MB, 2^21 slots and up) is copied on the side stream
@@ -935,14 +960,18 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   pp.range_shift = ix->range_shift;
   pp.n_ranges = ix->R;
   pp.n_blocks = ix->n_blocks;
-  pp.csr_col = bp.csr_col;
-  pp.csr_tf = bp.csr_tf;
+  pp.csr = bp.csr;
+  pp.csr_esc = bp.csr_esc;
+  pp.n_esc = ix->h_esc.size();
   pp.rsplit = bp.rsplit;
   pp.doc_norm = bp.doc_norm;
   pp.blk = ix->blk.as<uint32_t>();
   pp.bbase = ix->bbase.as<uint64_t>();
-  pp.post = ix->post.as<uint64_t>();
+  pp.post = ix->post.as<uint32_t>();
   pp.post_tmp = ix->post_tmp.as<uint32_t>();
+  pp.post_esc = ix->post_esc.as<uint64_t>();
+  pp.post_esc_count = reinterpret_cast<uint32_t *>(ctr + 10);
+  pp.post_esc_cap = post_esc_cap;
   pp.err = bp.err;
   HIP_TRY(hipEventRecord(ix->ev[EV_D0], s));
   if (ix->term_major) {
@@ -953,8 +982,9 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
     tp.nnz = ix->nnz;
     tp.C = C;
     tp.slot_bits = ix->cap_log2;
-    tp.csr_col = bp.csr_col;
-    tp.csr_tf = bp.csr_tf;
+    tp.csr = bp.csr;
+    tp.csr_esc = bp.csr_esc;
+    tp.n_esc = ix->h_esc.size();
     tp.doc_nuniq = bp.doc_nuniq;
     tp.doc_norm = bp.doc_norm;
     tp.row_off = ix->row_off.as<uint32_t>();
@@ -1001,9 +1031,19 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   // occupied dictionary slots counted on the device (ctr[7]) instead of a host
   // pass over the mirror (8 M slots at 2^23 took milliseconds)
   HIP_TRY(launch_count_nonzero(ix->dict.as<uint64_t>(), C, reinterpret_cast<unsigned long long *>(ctr + 7), s));
-  uint64_t tail[6];                         // ctr[3] error flags .. ctr[7] occupied slots, ctr[8] malformed
+  uint64_t tail[8];              // ctr[3] error flags .. ctr[7] occupied slots, [8] malformed, [10] posting escapes
   HIP_TRY(hipMemcpyAsync(tail, ctr + 3, sizeof tail, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  {
+    const uint64_t n_pe = ix->term_major ? 0 : (uint32_t)tail[7];
+    if (n_pe > post_esc_cap) return fail(TFIDF_E_CAPACITY, "posting escape list overflow");
+    ix->h_post_esc.resize(n_pe);
+    if (n_pe) {                                // rare (tf >= 2047): sorted for the scorer's binary search
+      HIP_TRY(hipMemcpy(ix->h_post_esc.data(), ix->post_esc.p, n_pe * 8, hipMemcpyDeviceToHost));
+      std::sort(ix->h_post_esc.begin(), ix->h_post_esc.end());
+      HIP_TRY(hipMemcpy(ix->post_esc.p, ix->h_post_esc.data(), n_pe * 8, hipMemcpyHostToDevice));
+    }
+  }
   ix->malformed.resize((uint32_t)tail[5]);
   if (!ix->malformed.empty()) {
     HIP_TRY(hipMemcpy(ix->malformed.data(), ix->bad_list.p, ix->malformed.size() * 4, hipMemcpyDeviceToHost));
@@ -1053,7 +1093,7 @@ extern "C" int tfidf_stats(const tfidf_index *ix, tfidf_index_stats *out) {
   out->unicode_docs = ix->unicode_docs;
   out->long_chunked = ix->long_chunked;
   out->malformed_docs = ix->committed ? ix->malformed.size() : 0;
-  const DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->dict, &ix->csr_col, &ix->csr_tf, &ix->doc_len,
+  const DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->dict, &ix->csr, &ix->csr_esc, &ix->doc_len,
                           &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->blk, &ix->bbase, &ix->post,
                           &ix->toff, &ix->tdf};
   uint64_t tot = 0;
@@ -1170,6 +1210,9 @@ static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint
   }
   QueryParams qp{};
   qp.post = ix->post.as<uint64_t>();
+  qp.post32 = ix->post.as<uint32_t>();
+  qp.post_esc = ix->post_esc.as<uint64_t>();
+  qp.n_post_esc = ix->h_post_esc.size();
   qp.bbase = ix->bbase.as<uint64_t>();
   qp.blk = ix->blk.as<uint32_t>();
   qp.toff = ix->term_major ? ix->toff.as<uint64_t>() : nullptr;
@@ -1495,10 +1538,18 @@ extern "C" int tfidf_doc_terms(tfidf_index *ix, uint64_t doc, char *terms, uint6
   HIP_TRY(hipMemcpy(&nu, ix->doc_nuniq.as<uint32_t>() + doc, 4, hipMemcpyDeviceToHost));
   const uint64_t st = staged_of(ix, doc);
   const uint64_t base = csr_row_base(ix->h_offsets.data(), st);
-  std::vector<uint32_t> col(nu), tf(nu);
+  // packed entries: the row's range segments (rsplit) give each slot's range
+  std::vector<uint32_t> ent(nu), col(nu), tf(nu), split(ix->R);
   if (nu) {
-    HIP_TRY(hipMemcpy(col.data(), ix->csr_col.as<uint32_t>() + base, nu * 4, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(tf.data(), ix->csr_tf.as<uint32_t>() + base, nu * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(ent.data(), ix->csr.as<uint32_t>() + base, nu * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(split.data(), ix->rsplit.as<uint32_t>() + doc * ix->R, ix->R * 4, hipMemcpyDeviceToHost));
+  }
+  const uint32_t rs = ix->range_shift, esc = csr_esc_value(rs);
+  for (uint32_t i = 0, r = 0; i < nu; i++) {
+    while (r + 1 < ix->R && i >= split[r]) r++;
+    col[i] = (r << rs) | csr_local(ent[i], rs);
+    const uint32_t f = csr_tf_field(ent[i], rs);
+    tf[i] = f == esc ? csr_esc_tf(ix->h_esc.data(), ix->h_esc.size(), base + i) : f;
   }
   std::vector<std::pair<std::string, uint32_t>> rows;
   for (uint32_t i = 0; i < nu; i++) {

@@ -28,8 +28,10 @@ struct BuildParams {
   uint32_t cap_mask;          // C - 1
   uint32_t range_shift;       // log2(range size)
   uint32_t n_ranges;          // R = C >> range_shift
-  uint32_t *csr_col;          // padded CSR rows: dictionary slot per entry
-  uint32_t *csr_tf;           // tf per entry
+  uint32_t *csr;              // padded CSR rows, one packed word per entry (csr_pack)
+  uint64_t *csr_esc;          // escape list: (entry index << 24) | tf for tfs the packed field cannot hold
+  uint32_t *esc_count;
+  uint64_t esc_cap;
   uint32_t *doc_len;          // tokens per doc (field length)
   uint32_t *doc_nuniq;        // distinct terms per doc
   uint8_t *doc_norm;          // SmallFloat.intToByte4(len)
@@ -75,6 +77,59 @@ __host__ __device__ inline uint64_t csr_row_base(const uint64_t *offsets, uint64
   return (offsets[src] + src) >> 1;
 }
 
+// Packed CSR entry, one u32 per (document, distinct term): bits [0,
+// range_shift) = the term's dictionary slot minus its range base (the row
+// segment it sits in names the range, rsplit), bits [range_shift, 32) = tf.
+// A tf the field cannot hold stores the all-ones escape there and the exact
+// value goes to the escape list ((entry index << 24) | tf, sorted by the host
+// after the build, binary-searched).  Block-major ranges are 2^15 slots, so
+// the field is 17 bits and only book-sized documents can escape; term-major
+// rows keep the whole slot (range_shift = log2 C).  A word is never 0 (tf >= 1).
+__host__ __device__ inline uint32_t csr_esc_value(uint32_t range_shift) { return 0xFFFFFFFFu >> range_shift; }
+__host__ __device__ inline uint32_t csr_local(uint32_t e, uint32_t range_shift) {
+  return e & ((1u << range_shift) - 1u);
+}
+__host__ __device__ inline uint32_t csr_tf_field(uint32_t e, uint32_t range_shift) { return e >> range_shift; }
+
+// tf of escaped entry idx (0 if absent)
+__host__ __device__ inline uint32_t csr_esc_tf(const uint64_t *esc, uint64_t n, uint64_t idx) {
+  uint64_t a = 0, z = n;
+  while (a < z) {
+    const uint64_t m = (a + z) >> 1;
+    if ((esc[m] >> 24) < idx) a = m + 1; else z = m;
+  }
+  return a < n && (esc[a] >> 24) == idx ? (uint32_t)(esc[a] & 0xFFFFFFu) : 0u;
+}
+
+#if defined(__HIPCC__)
+__device__ inline void set_build_err(uint32_t *err, uint32_t flag, uint32_t doc) {
+  const uint32_t old = atomicOr(err, flag);
+  if (old == 0) atomicExch(err + 1, doc);
+}
+// write CSR entry idx of document doc (dictionary slot, tf)
+__device__ inline void csr_put(const BuildParams &p, uint64_t idx, uint32_t slot, uint32_t tf, uint32_t doc) {
+  const uint32_t esc = csr_esc_value(p.range_shift);
+  uint32_t f = tf;
+  if (tf >= esc) {
+    f = esc;
+    if (tf > kMaxTf) set_build_err(p.err, kErrTfTooLarge, doc);
+    const uint32_t at = atomicAdd(p.esc_count, 1u);
+    if (at < p.esc_cap) p.csr_esc[at] = (idx << 24) | (tf > kMaxTf ? kMaxTf : tf);
+  }
+  p.csr[idx] = csr_local(slot, p.range_shift) | (f << p.range_shift);
+}
+#endif
+
+// Block-major posting (one u32): document within its 8192-doc block (13
+// bits) | min(tf, kPostTfEsc) << 13 | norm byte << 24.  tf >= kPostTfEsc
+// (2047 occurrences of a term in one document) is an escape: the exact value
+// is in the sorted posting escape list (csr_esc_tf format, keyed by posting
+// index).  Term-major postings stay u64: doc | (tf << 8 | norm) << 32.
+constexpr uint32_t kPostTfEsc = 2047;
+__host__ __device__ inline uint32_t post_word(uint32_t doc_local, uint32_t tf, uint32_t norm) {
+  return doc_local | ((tf < kPostTfEsc ? tf : kPostTfEsc) << 13) | (norm << 24);
+}
+
 struct PostingParams {
   const uint64_t *offsets;
   const uint32_t *live_map;
@@ -82,13 +137,18 @@ struct PostingParams {
   uint32_t C;                 // dictionary slots
   uint32_t range_shift, n_ranges;
   uint32_t n_blocks;          // ceil(n_docs / kBlockDocs)
-  const uint32_t *csr_col, *csr_tf, *rsplit;
+  const uint32_t *csr, *rsplit;
+  const uint64_t *csr_esc;    // sorted escape list (csr_put)
+  uint64_t n_esc;
   const uint8_t *doc_norm;
   uint32_t *blk;              // [(n_blocks + 1) * C]: per-block term counts -> per-block exclusive
                               // offsets over slots; row n_blocks = df
   uint64_t *bbase;            // [n_blocks + 1]: first posting of each block (block-major postings)
-  uint64_t *post;             // [nnz]: doc | (tf << 8 | norm) << 32; block b, slot s at
+  uint32_t *post;             // [nnz] block-major postings (post_word); block b, slot s at
                               // bbase[b] + blk[b][s]
+  uint64_t *post_esc;         // (posting index << 24) | tf for tf >= kPostTfEsc
+  uint32_t *post_esc_count;
+  uint64_t post_esc_cap;
   uint32_t *err;
   uint32_t *post_tmp;         // [nnz] scatter pass 1 output (sub-range streams, same regions)
 };
@@ -118,7 +178,9 @@ struct TermParams {
   const uint32_t *live_map;
   uint64_t n_docs, nnz;
   uint32_t C, slot_bits;      // C = 2^slot_bits
-  const uint32_t *csr_col, *csr_tf, *doc_nuniq;
+  const uint32_t *csr, *doc_nuniq;
+  const uint64_t *csr_esc;
+  uint64_t n_esc;
   const uint8_t *doc_norm;
   uint32_t *row_off;          // [n_docs] compact row offsets (exclusive sum of doc_nuniq)
   uint32_t *keys, *keys_alt;  // [nnz] each: sort keys = slot (double buffer)
@@ -133,7 +195,10 @@ hipError_t launch_term_invert(TermParams p, void *tmp, size_t tmp_bytes, hipStre
 
 // --- query scoring (kernels_query.hip) ---
 struct QueryParams {
-  const uint64_t *post;
+  const uint64_t *post;       // term-major postings (toff != nullptr)
+  const uint32_t *post32;     // block-major postings (post_word)
+  const uint64_t *post_esc;   // block-major tf escapes, sorted
+  uint64_t n_post_esc;
   const uint64_t *bbase;      // [n_blocks + 1] first posting of each block
   const uint32_t *blk;        // per-block exclusive offsets over slots [n_blocks * C]
   const uint64_t *toff;       // term-major layout: [C + 1] first posting per slot (nullptr = block-major)
