@@ -2027,53 +2027,59 @@ __device__ uint32_t csr_tf_of(const PostingParams &p, uint64_t d, uint32_t r, ui
   return 0;
 }
 
-// grid (n_blocks, n_ranges, streams per range), 1024 threads: few streams per
-// CU at a time, so the regions being written stay L2-resident
+// grid (n_blocks, n_ranges, streams per range / sort_spw), 1024 threads; a
+// workgroup takes sort_spw streams in turn (8: 3.11 -> 2.87 ms per cfg-2
+// inversion against one stream per workgroup), so few streams per CU are
+// open at a time and the regions being written stay L2-resident
 __global__ void __launch_bounds__(1024) k_scatter_sort(PostingParams p) {
   __shared__ uint32_t cur[kSubSlots + 1];                   // + no-op cursor for idle lanes
-  const uint32_t b = blockIdx.x, r = blockIdx.y, k = blockIdx.z;
+  const uint32_t b = blockIdx.x, r = blockIdx.y;
   const uint32_t RS = 1u << p.range_shift;
   const uint32_t BS = RS < kSubSlots ? RS : kSubSlots;
-  const size_t s0 = ((size_t)r << p.range_shift) + (size_t)k * BS;
+  const uint32_t nsub = RS / BS;
   const uint32_t *row = p.blk + (size_t)b * p.C;
   const uint64_t bb = p.bbase[b];
-  for (uint32_t i = threadIdx.x; i < BS; i += blockDim.x) cur[i] = row[s0 + i];
-  const uint32_t lo = row[s0];
-  const uint32_t hi = s0 + BS < p.C ? row[s0 + BS] : (uint32_t)(p.bbase[b + 1] - bb);
-  __syncthreads();
   const uint32_t d0 = b * kBlockDocs;
   const uint32_t lane = threadIdx.x & 63;
-  constexpr int U = 8;              // entries per thread in flight (8: a ~5 k-entry stream in one round; 4 was 3.4% slower)
-  for (uint32_t e0 = lo; e0 < hi; e0 += U * blockDim.x) {   // uniform trip count: all lanes ballot
-    uint32_t x[U], nrm[U];
+  for (uint32_t k = blockIdx.z * p.sort_spw; k < min(nsub, (blockIdx.z + 1) * p.sort_spw); k++) {
+    const size_t s0 = ((size_t)r << p.range_shift) + (size_t)k * BS;
+    for (uint32_t i = threadIdx.x; i < BS; i += blockDim.x) cur[i] = row[s0 + i];
+    const uint32_t lo = row[s0];
+    const uint32_t hi = s0 + BS < p.C ? row[s0 + BS] : (uint32_t)(p.bbase[b + 1] - bb);
+    __syncthreads();
+    constexpr int U = 8;              // entries per thread in flight (8: a ~5 k-entry stream in one round; 4 was 3.4% slower)
+    for (uint32_t e0 = lo; e0 < hi; e0 += U * blockDim.x) {   // uniform trip count: all lanes ballot
+      uint32_t x[U], nrm[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-      const uint32_t e = e0 + u * blockDim.x + threadIdx.x;
-      x[u] = e < hi ? p.post_tmp[bb + e] : 0u;
-    }
+      for (int u = 0; u < U; u++) {
+        const uint32_t e = e0 + u * blockDim.x + threadIdx.x;
+        x[u] = e < hi ? p.post_tmp[bb + e] : 0u;
+      }
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-      const uint32_t e = e0 + u * blockDim.x + threadIdx.x;
-      nrm[u] = e < hi ? p.doc_norm[d0 + (x[u] & (kBlockDocs - 1))] : 0u;
-    }
+      for (int u = 0; u < U; u++) {
+        const uint32_t e = e0 + u * blockDim.x + threadIdx.x;
+        nrm[u] = e < hi ? p.doc_norm[d0 + (x[u] & (kBlockDocs - 1))] : 0u;
+      }
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-      const uint32_t e = e0 + u * blockDim.x + threadIdx.x;
-      if (__all(e >= hi)) break;
-      const bool in = e < hi;
-      const uint32_t sl = in ? (x[u] >> 13) & (kSubSlots - 1) : kSubSlots;   // kSubSlots: no-op key
-      const uint32_t pos = cursor_bump<kSubBits + 1>(cur, sl, lane);   // (plain LDS atomics: 4% slower)
-      const uint32_t doc = d0 + (x[u] & (kBlockDocs - 1));
-      uint32_t tf = x[u] >> kTmpTfShift;
-      if (in && tf == kTmpTfEsc) tf = csr_tf_of(p, doc, r, (uint32_t)s0 + sl);      // rare: tf >= 1023
-      if (in) {
-        p.post[bb + pos] = post_word(x[u] & (kBlockDocs - 1), tf, nrm[u]);
-        if (tf >= kPostTfEsc) {                                                 // rare: tf >= 2047
-          const uint32_t at = atomicAdd(p.post_esc_count, 1u);
-          if (at < p.post_esc_cap) p.post_esc[at] = ((bb + pos) << 24) | tf;
+      for (int u = 0; u < U; u++) {
+        const uint32_t e = e0 + u * blockDim.x + threadIdx.x;
+        if (__all(e >= hi)) break;
+        const bool in = e < hi;
+        const uint32_t sl = in ? (x[u] >> 13) & (kSubSlots - 1) : kSubSlots;   // kSubSlots: no-op key
+        const uint32_t pos = cursor_bump<kSubBits + 1>(cur, sl, lane);   // (plain LDS atomics: 4% slower)
+        const uint32_t doc = d0 + (x[u] & (kBlockDocs - 1));
+        uint32_t tf = x[u] >> kTmpTfShift;
+        if (in && tf == kTmpTfEsc) tf = csr_tf_of(p, doc, r, (uint32_t)s0 + sl);      // rare: tf >= 1023
+        if (in) {
+          p.post[bb + pos] = post_word(x[u] & (kBlockDocs - 1), tf, nrm[u]);
+          if (tf >= kPostTfEsc) {                                                 // rare: tf >= 2047
+            const uint32_t at = atomicAdd(p.post_esc_count, 1u);
+            if (at < p.post_esc_cap) p.post_esc[at] = ((bb + pos) << 24) | tf;
+          }
         }
       }
     }
+    __syncthreads();                                      // cursors reused by the next stream
   }
 }
 
@@ -2143,7 +2149,8 @@ hipError_t launch_scatter(const PostingParams &p, hipStream_t s) {
   if (e != hipSuccess) return e;
   const uint32_t RS = 1u << p.range_shift;
   const uint32_t nsub = RS > kSubSlots ? RS / kSubSlots : 1u;
-  hipLaunchKernelGGL(k_scatter_sort, dim3(p.n_blocks, p.n_ranges, nsub), dim3(1024), 0, s, p);
+  hipLaunchKernelGGL(k_scatter_sort, dim3(p.n_blocks, p.n_ranges, (nsub + p.sort_spw - 1) / p.sort_spw), dim3(1024),
+                     0, s, p);
   return hipGetLastError();
 }
 

@@ -18,6 +18,8 @@
 //                  in LDS -> (score desc, doc asc).
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "tfidf_common.h"
 #include "tfidf_internal.h"
 
@@ -119,15 +121,30 @@ __device__ __forceinline__ void term_block_range(const QueryParams &p, uint32_t 
   *z = wave_lower_bound(p.post, lo, t1, d0 + kBlockDocs);
 }
 
-// Posting i of the block starting at doc d0 as the u64 word doc | (tf << 8 |
-// norm) << 32 (term-major postings are stored that way; block-major ones are
-// u32 post_word, tf escapes looked up in the sorted escape list)
-__device__ __forceinline__ uint64_t post_at(const QueryParams &p, uint64_t i, uint32_t d0) {
-  if (p.toff) return p.post[i];
-  const uint32_t v = p.post32[i];
-  uint32_t tf = (v >> 13) & kPostTfEsc;
-  if (tf == kPostTfEsc) tf = csr_esc_tf(p.post_esc, p.n_post_esc, i);
-  return (uint64_t)(d0 + (v & (kBlockDocs - 1))) | ((uint64_t)((tf << 8) | (v >> 24)) << 32);
+// Posting words: term-major u64 (doc | (tf << 8 | norm) << 32), block-major
+// u32 post_word (doc within the block | tf | norm; tf escapes looked up in
+// the sorted escape list).  The scorers are instantiated per layout.
+template <bool kTerm> using PostW = typename std::conditional<kTerm, uint64_t, uint32_t>::type;
+template <bool kTerm> __device__ __forceinline__ PostW<kTerm> post_raw(const QueryParams &p, uint64_t i) {
+  if constexpr (kTerm) return p.post[i];
+  else return p.post32[i];
+}
+// posting e (index i) of the block starting at doc d0
+template <bool kTerm>
+__device__ __forceinline__ void post_decode(const QueryParams &p, PostW<kTerm> e, uint64_t i, uint32_t d0,
+                                            uint32_t *ld, uint32_t *tf, uint32_t *nrm) {
+  if constexpr (kTerm) {
+    const uint32_t tfn = (uint32_t)(e >> 32);
+    *ld = (uint32_t)e - d0;
+    *tf = tfn >> 8;
+    *nrm = tfn & 255u;
+  } else {
+    uint32_t t = (e >> 13) & kPostTfEsc;
+    if (t == kPostTfEsc) t = csr_esc_tf(p.post_esc, p.n_post_esc, i);      // rare: tf >= 2047
+    *ld = e & (kBlockDocs - 1);
+    *tf = t;
+    *nrm = e >> 24;
+  }
 }
 
 constexpr uint32_t kQTermsFast = 4;   // query terms whose ranges / first chunk are prefetched
@@ -168,7 +185,7 @@ template <bool kOps> struct ScoreSmem {
 // kAll: all-hits mode (k == 0) as its own instantiation — its LDS sort code
 // made the compiler schedule the top-k instantiation's loops worse (10 k-query
 // batch: 12.4 -> 16.0 ms when they shared one kernel).
-template <bool kOps, bool kAll>
+template <bool kOps, bool kAll, bool kTerm>
 __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
   __shared__ ScoreSmem<kOps> sm;
   const uint32_t tid = threadIdx.x;
@@ -230,11 +247,11 @@ __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
     }
     __syncthreads();
     // first chunk of every term's postings in flight before any is consumed
-    uint64_t pre[kQTermsFast];
+    PostW<kTerm> pre[kQTermsFast];
 #pragma unroll
     for (uint32_t j = 0; j < kQTermsFast; j++) {
       pre[j] = 0;
-      if (j < t1 - t0 && sm.tlo[j] + tid < sm.thi[j]) pre[j] = post_at(p, sm.tlo[j] + tid, (uint32_t)d0);
+      if (j < t1 - t0 && sm.tlo[j] + tid < sm.thi[j]) pre[j] = post_raw<kTerm>(p, sm.tlo[j] + tid);
     }
     uint32_t my_new = 0;
     for (uint32_t j = t0; j < t1; j++) {
@@ -267,22 +284,22 @@ __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
         }
       }
       for (uint64_t i = lo + tid; i < hi; i += blockDim.x) {
-        uint64_t e;
+        PostW<kTerm> e;
         if (jj < kQTermsFast && i == lo + tid) {
 #pragma unroll
           for (uint32_t u = 0; u < kQTermsFast; u++)
             if (u == jj) e = pre[u];
         } else {
-          e = post_at(p, i, (uint32_t)d0);
+          e = post_raw<kTerm>(p, i);
         }
-        const uint32_t ld = (uint32_t)(e & 0xFFFFFFFFu) - (uint32_t)d0;
+        uint32_t ld, tf, nrm;
+        post_decode<kTerm>(p, e, i, (uint32_t)d0, &ld, &tf, &nrm);
         const uint32_t bit = 1u << (ld & 31);
         if (kOps && role == kRoleNot) {
           atomicOr(&sm.notbits[ld >> 5], bit);
           continue;
         }
-        const uint32_t tfn = (uint32_t)(e >> 32);
-        const float sc = bm25_term(w, tfn >> 8, sm.cache[tfn & 255u]);
+        const float sc = bm25_term(w, tf, sm.cache[nrm]);
         uint32_t *bm = (kOps && role == kRoleMust) ? sm.grpbits : sm.hitbits;
         const uint32_t old = atomicOr(&bm[ld >> 5], bit);
         if (old & bit) {
@@ -632,6 +649,7 @@ struct PairSmem {
   float cache[256];
 };
 
+template <bool kTerm>
 __global__ void __launch_bounds__(kPairWaves * 64) k_score_pairs(QueryParams p) {
   __shared__ PairSmem sm;
   const uint32_t lane = threadIdx.x & 63;
@@ -682,7 +700,7 @@ __global__ void __launch_bounds__(kPairWaves * 64) k_score_pairs(QueryParams p) 
     if (P == 0) { if (lane == 0) p.cand_n[pr] = 0; continue; }
     // the first two 64-posting chunks of the first kQTermsFast terms: all in
     // flight before the table is cleared (one HBM latency for a typical pair)
-    uint64_t pre[kQTermsFast][2];
+    PostW<kTerm> pre[kQTermsFast][2];
 #pragma unroll
     for (uint32_t j = 0; j < kQTermsFast; j++) {
       const uint64_t ja = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(a >> 32), j) << 32) |
@@ -692,7 +710,7 @@ __global__ void __launch_bounds__(kPairWaves * 64) k_score_pairs(QueryParams p) 
 #pragma unroll
       for (uint32_t c = 0; c < 2; c++) {
         const uint64_t i = ja + lane + 64 * c;
-        pre[j][c] = (j < nt && i < jz) ? post_at(p, i, d0) : 0ull;
+        pre[j][c] = (j < nt && i < jz) ? post_raw<kTerm>(p, i) : 0;
       }
     }
     {
@@ -706,12 +724,12 @@ __global__ void __launch_bounds__(kPairWaves * 64) k_score_pairs(QueryParams p) 
     uint16_t *list = reinterpret_cast<uint16_t *>(sm.list[w]);
     // insert one posting per lane (inactive lanes: e = 0 and act = false);
     // claimed slots are appended to the wave's hit list
-    auto insert = [&](uint64_t e, bool act, float wj) {
+    auto insert = [&](PostW<kTerm> e, bool act, float wj, uint64_t i) {
       uint32_t claimed = kPairEmpty;
       if (act) {
-        const uint32_t ld = (uint32_t)e - d0;
-        const uint32_t tfn = (uint32_t)(e >> 32);
-        const float sc = bm25_term(wj, tfn >> 8, sm.cache[tfn & 255u]);
+        uint32_t ld, tf, nrm;
+        post_decode<kTerm>(p, e, i, d0, &ld, &tf, &nrm);
+        const float sc = bm25_term(wj, tf, sm.cache[nrm]);
         uint32_t slot = (ld * 0x9E3779B1u) >> 22;
         for (;;) {
           const uint32_t old = atomicCAS(&key[slot], kPairEmpty, ld);
@@ -733,25 +751,25 @@ __global__ void __launch_bounds__(kPairWaves * 64) k_score_pairs(QueryParams p) 
       const float wj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tw), j));
       uint64_t i0 = ja;
       if (j < kQTermsFast) {
-        uint64_t e0 = 0, e1 = 0;
+        PostW<kTerm> e0 = 0, e1 = 0;
 #pragma unroll
         for (uint32_t u = 0; u < kQTermsFast; u++)
           if (u == j) { e0 = pre[u][0]; e1 = pre[u][1]; }
-        insert(e0, ja + lane < jz, wj);
-        if (ja + 64 < jz) insert(e1, ja + 64 + lane < jz, wj);     // uniform
+        insert(e0, ja + lane < jz, wj, ja + lane);
+        if (ja + 64 < jz) insert(e1, ja + 64 + lane < jz, wj, ja + 64 + lane);     // uniform
         i0 = ja + 128;
       }
       // remaining chunks, four loads in flight per step
       for (; i0 < jz; i0 += 256) {
-        uint64_t e[4];
+        PostW<kTerm> e[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
           const uint64_t i = i0 + 64 * u + lane;
-          e[u] = i < jz ? post_at(p, i, d0) : 0ull;
+          e[u] = i < jz ? post_raw<kTerm>(p, i) : 0;
         }
 #pragma unroll
         for (int u = 0; u < 4; u++)
-          if (i0 + 64 * u < jz) insert(e[u], i0 + 64 * u + lane < jz, wj);
+          if (i0 + 64 * u < jz) insert(e[u], i0 + 64 * u + lane < jz, wj, i0 + 64 * u + lane);
       }
     }
     nhit = nlist;
@@ -958,19 +976,26 @@ hipError_t launch_pack_keys(const uint32_t *out_doc, const float *out_score, con
 }
 
 hipError_t launch_score_pairs(const QueryParams &p, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(k_score_pairs, dim3(grid), dim3(kPairWaves * 64), 0, s, p);
+  if (p.toff) hipLaunchKernelGGL(k_score_pairs<true>, dim3(grid), dim3(kPairWaves * 64), 0, s, p);
+  else hipLaunchKernelGGL(k_score_pairs<false>, dim3(grid), dim3(kPairWaves * 64), 0, s, p);
   return hipGetLastError();
+}
+
+template <bool kTerm>
+static void score_blocks_layout(const QueryParams &p, dim3 grid, hipStream_t s) {
+  if (p.k == 0) {
+    if (p.ops) hipLaunchKernelGGL((k_score_blocks<true, true, kTerm>), grid, dim3(kScoreThreads), 0, s, p);
+    else hipLaunchKernelGGL((k_score_blocks<false, true, kTerm>), grid, dim3(kScoreThreads), 0, s, p);
+  } else {
+    if (p.ops) hipLaunchKernelGGL((k_score_blocks<true, false, kTerm>), grid, dim3(kScoreThreads), 0, s, p);
+    else hipLaunchKernelGGL((k_score_blocks<false, false, kTerm>), grid, dim3(kScoreThreads), 0, s, p);
+  }
 }
 
 hipError_t launch_score_blocks(const QueryParams &p, hipStream_t s) {
   const dim3 grid = p.ovf_list ? dim3(p.list_grid) : dim3(p.n_blocks, (p.n_q + p.q_chunk - 1) / p.q_chunk);
-  if (p.k == 0) {
-    if (p.ops) hipLaunchKernelGGL((k_score_blocks<true, true>), grid, dim3(kScoreThreads), 0, s, p);
-    else hipLaunchKernelGGL((k_score_blocks<false, true>), grid, dim3(kScoreThreads), 0, s, p);
-  } else {
-    if (p.ops) hipLaunchKernelGGL((k_score_blocks<true, false>), grid, dim3(kScoreThreads), 0, s, p);
-    else hipLaunchKernelGGL((k_score_blocks<false, false>), grid, dim3(kScoreThreads), 0, s, p);
-  }
+  if (p.toff) score_blocks_layout<true>(p, grid, s);
+  else score_blocks_layout<false>(p, grid, s);
   return hipGetLastError();
 }
 hipError_t launch_merge_topk(const QueryParams &p, hipStream_t s) {

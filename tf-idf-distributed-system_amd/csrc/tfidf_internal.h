@@ -151,6 +151,7 @@ struct PostingParams {
   uint64_t post_esc_cap;
   uint32_t *err;
   uint32_t *post_tmp;         // [nnz] scatter pass 1 output (sub-range streams, same regions)
+  uint32_t sort_spw;          // scatter pass 2: sub-range streams per workgroup
 };
 
 // --- launch wrappers (kernels_index.hip) ---
