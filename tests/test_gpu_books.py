@@ -14,7 +14,7 @@ import pytest
 from oracle import oracle as O
 from tfidf_amd import synth
 from tfidf_amd.engine import ShardIndex
-from test_gpu_parity import assert_hits_equal, build_pair, keyed, random_text
+from test_gpu_parity import assert_hits_equal, build_pair, random_text
 
 pytestmark = pytest.mark.gpu
 
@@ -50,7 +50,7 @@ def test_books_index_equals_oracle(books):
     assert (s["doc_count"], s["sum_ttf"], s["num_terms"], s["nnz"]) == \
         (o.doc_count, o.sum_ttf, o.num_terms, sum(o.vocab().values()))
     for d in (0, 1, 77, 150, 299):
-        assert g.doc_terms(d) == keyed(o.doc_terms(d)), d
+        assert g.doc_terms(d) == o.doc_terms(d), d
         assert g.doc_len(d) == (o.doc_len(d), o.doc_norm(d))
     for q in synth.queries(20, lo=100, hi=10_000) + [b"aaaa", b"aaaa AND aaab NOT aaac"]:
         assert_hits_equal(g.search(q, 10), o.search(q, 10))
@@ -102,7 +102,7 @@ def test_chunk_boundaries_punctuation_books():
     assert (s["doc_count"], s["sum_ttf"], s["num_terms"], s["nnz"]) == \
         (o.doc_count, o.sum_ttf, o.num_terms, sum(o.vocab().values()))
     for d in range(len(texts)):
-        assert g.doc_terms(d) == keyed(o.doc_terms(d)), d
+        assert g.doc_terms(d) == o.doc_terms(d), d
         assert g.doc_len(d) == (o.doc_len(d), o.doc_norm(d))
     for q in [b"ab", b"c9 x_", b"a.b 3,1", b"w" * 12, b"d'e"]:
         assert_hits_equal(g.search(q, 0), o.search(q, 0))

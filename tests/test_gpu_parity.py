@@ -20,19 +20,6 @@ from tfidf_amd._lib import QuerySyntaxError, UnsupportedInput
 pytestmark = pytest.mark.gpu
 
 
-def keyed(terms):
-    """Oracle doc_terms with long (> 16 byte) and non-ASCII terms replaced by
-    the engine's printable 128-bit key: the device keys those terms by hash."""
-    from tfidf_amd.engine import term_key
-    out = {}
-    for t, tf in terms.items():
-        if len(t) > 16 or max(t, default=0) >= 0x80:
-            lo, hi = term_key(t)
-            t = b"#%016x%016x" % (hi, lo)
-        out[t] = tf
-    return out
-
-
 def f32bits(x):
     return np.float32(x).view(np.int32).item()
 
@@ -179,7 +166,7 @@ def test_zipf_stats(zipf):
 def test_zipf_tf_rows(zipf):
     g, o, texts = zipf
     for d in list(range(0, 3000, 97)) + [2999]:
-        assert g.doc_terms(d) == keyed(o.doc_terms(d))
+        assert g.doc_terms(d) == o.doc_terms(d)
         assert g.doc_len(d) == (o.doc_len(d), o.doc_norm(d))
 
 
@@ -237,7 +224,7 @@ def test_punctuation_corpus_parity():
     s = g.stats()
     assert (s["doc_count"], s["sum_ttf"], s["num_terms"]) == (o.doc_count, o.sum_ttf, o.num_terms)
     for d in range(len(texts)):
-        assert g.doc_terms(d) == keyed(o.doc_terms(d)), d
+        assert g.doc_terms(d) == o.doc_terms(d), d
         assert g.doc_len(d) == (o.doc_len(d), o.doc_norm(d))
     for q in [b"a", b"b.c x", b"3,14", b"abc xyz", b"_", b"y" * 19]:
         assert_hits_equal(g.search(q, 0), o.search(q, 0))
@@ -262,7 +249,7 @@ def test_long_documents_path():
         (o.doc_count, o.sum_ttf, o.num_terms, sum(o.vocab().values()))
     for d in range(len(texts)):
         if len(texts[d]) > 4096 or d % 17 == 0:
-            assert g.doc_terms(d) == keyed(o.doc_terms(d)), d
+            assert g.doc_terms(d) == o.doc_terms(d), d
             assert g.doc_len(d) == (o.doc_len(d), o.doc_norm(d))
     for q in synth.queries(15, lo=1, hi=2000) + [b"ab", b"a b c"]:
         assert_hits_equal(g.search(q, 0), o.search(q, 0))
@@ -331,7 +318,7 @@ def test_host_loader_pinned_staging_and_clear():
         o.add_doc(str(d).encode(), text[int(offs[d]):int(offs[d + 1])].tobytes())
     o.commit()
     for i, d in enumerate((0, 17, 39999)):
-        assert a.doc_terms(d) == keyed(o.doc_terms(i))
+        assert a.doc_terms(d) == o.doc_terms(i)
     for x in (a, b, o):
         x.close()
     dc.free()
@@ -348,7 +335,7 @@ def test_malformed_utf8_document_indexed_empty():
     assert s["malformed_docs"] == 2 and s["num_docs"] == 5
     assert (s["doc_count"], s["sum_ttf"], s["num_terms"]) == (o.doc_count, o.sum_ttf, o.num_terms) == (3, 7, 6)
     for d in range(5):
-        assert g.doc_terms(d) == keyed(o.doc_terms(d))
+        assert g.doc_terms(d) == o.doc_terms(d)
         assert g.doc_len(d) == (o.doc_len(d), o.doc_norm(d))
     for q in (b"fine", b"text", b"caf\xc3\xa9"):
         assert_hits_equal(g.search(q, 0), o.search(q, 0))

@@ -260,10 +260,10 @@ inline int parse_query(const uint8_t *q, uint64_t n, QueryPlan *plan) {
   return kQOk;
 }
 
-inline void term_key(const std::string &t, uint64_t *lo, uint64_t *hi) {
+inline void term_key(const std::string &t, uint64_t *lo, uint64_t *hi, uint64_t seed = 0) {
   KeyBuilder kb;
   for (unsigned char c : t) kb.push(c);
-  kb.finish(lo, hi);
+  kb.finish(lo, hi, seed);
 }
 
 }  // namespace tfidf

@@ -10,7 +10,9 @@
 
 namespace tfidf {
 
-// Global dictionary: lo[C] followed by hi[C] (u64 each).  Probing is linear
+// Global dictionary: lo[C], hi[C], ref[C] (u64 each).  ref holds one
+// occurrence of a hashed key's term (dict_ref_word: text offset and byte
+// length), written by the claimer, read by the exact-identity checks.  Probing is linear
 // over the slots starting at the aligned 2-slot bucket of key_hash & (C - 1);
 // one 16 B load of lo covers a bucket.  Claim = CAS lo 0 -> key lo, then
 // publish hi (agent scope).  A resident lo equal to the lo of a key of <= 8
@@ -20,11 +22,22 @@ namespace tfidf {
 // stale "empty" falls through to the CAS, which returns the true value.
 __device__ __forceinline__ bool key_lo_is_short(uint64_t lo) { return (lo >> 63) == 0; }
 
+// reference occurrence word: bit 63 | byte length << 40 | text offset
+TFIDF_HD uint64_t dict_ref_word(uint64_t off, uint32_t len) { return (1ull << 63) | ((uint64_t)len << 40) | off; }
+TFIDF_HD uint64_t dict_ref_off(uint64_t r) { return r & ((1ull << 40) - 1); }
+TFIDF_HD uint32_t dict_ref_len(uint64_t r) { return (uint32_t)(r >> 40) & 0x3FFu; }
+
+// ref (optional): per key, the reference word a successful claim of a hashed
+// key stores; claimed (optional): whether this lane claimed the slot.
 template <int K>
 __device__ __forceinline__ void dict_lookup_multi(uint64_t *dict, uint32_t mask, const uint64_t *lo, const uint64_t *hi,
-                                                  const bool *act, uint32_t *out) {
+                                                  const bool *act, uint32_t *out, const uint64_t *ref = nullptr,
+                                                  bool *claimed = nullptr) {
   uint64_t *dlo = dict;
   uint64_t *dhi = dict + (size_t)mask + 1;
+  if (claimed)
+#pragma unroll
+    for (int j = 0; j < K; j++) claimed[j] = false;
   uint32_t s[K];
   bool done[K];
 #pragma unroll
@@ -69,9 +82,12 @@ __device__ __forceinline__ void dict_lookup_multi(uint64_t *dict, uint32_t mask,
         const unsigned long long old =
             atomicCAS(reinterpret_cast<unsigned long long *>(dlo + js[j]), 0ull, (unsigned long long)lo[j]);
         if (old == 0) {
+          if (ref && (lo[j] & kLoHashed))
+            __hip_atomic_store(dict + 2 * ((size_t)mask + 1) + js[j], ref[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           __hip_atomic_store(dhi + js[j], hi[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           out[j] = js[j];
           done[j] = true;
+          if (claimed) claimed[j] = true;
         } else if (old == lo[j]) {
           if (key_lo_is_short(lo[j])) { out[j] = js[j]; done[j] = true; }
           else { s[j] = js[j]; a[j] = 3; }
@@ -93,9 +109,10 @@ __device__ __forceinline__ void dict_lookup_multi(uint64_t *dict, uint32_t mask,
 }
 
 __device__ __forceinline__ uint32_t dict_find_or_insert(uint64_t *dict, uint32_t mask, uint64_t lo, uint64_t hi,
-                                                        bool active) {
+                                                        bool active, const uint64_t *ref = nullptr,
+                                                        bool *claimed = nullptr) {
   uint32_t out;
-  dict_lookup_multi<1>(dict, mask, &lo, &hi, &active, &out);
+  dict_lookup_multi<1>(dict, mask, &lo, &hi, &active, &out, ref, claimed);
   return out;
 }
 

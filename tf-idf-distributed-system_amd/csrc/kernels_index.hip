@@ -68,7 +68,13 @@ __device__ __forceinline__ void set_err(uint32_t *err, uint32_t flag, uint32_t d
 
 // Per-document table in global memory (long path).  Only the owning
 // workgroup touches it, so workgroup-scope atomics are sufficient.
-__device__ uint32_t gtable_insert(uint64_t *keys, uint32_t *cnt, uint32_t mask, uint64_t lo, uint64_t hi) {
+// Insert / count one token.  pos: per slot the first occurrence
+// (dict_ref_word, document-relative: doc = the document's bytes); occ = this
+// token's.  Under a hashed key every match is checked to spell the same
+// term (a mismatch raises kErrCollision: the build is redone with another
+// hash seed).
+__device__ uint32_t gtable_insert(uint64_t *keys, uint32_t *cnt, uint64_t *pos, uint32_t mask, uint64_t lo, uint64_t hi,
+                                  uint64_t occ, const uint8_t *doc, uint32_t *err, uint32_t d) {
   const uint32_t h0 = dict_hash(lo, hi);
   uint32_t s = (h0 ^ (h0 >> 16)) & mask;
   uint32_t result = kInvalidSlot;
@@ -83,6 +89,7 @@ __device__ uint32_t gtable_insert(uint64_t *keys, uint32_t *cnt, uint32_t mask, 
         bool won = __hip_atomic_compare_exchange_strong(keys + 2 * (size_t)s, &expected, lo, __ATOMIC_RELAXED,
                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (won) {
+          __hip_atomic_store(pos + s, occ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           __hip_atomic_store(keys + 2 * (size_t)s + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           __hip_atomic_fetch_add(cnt + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           result = s;
@@ -97,6 +104,14 @@ __device__ uint32_t gtable_insert(uint64_t *keys, uint32_t *cnt, uint32_t mask, 
       if (clo == lo) {
         chi = __hip_atomic_load(keys + 2 * (size_t)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (chi == hi) {
+          if (lo & kLoHashed) {
+            uint64_t r = 0;
+            for (uint32_t w = 0; w < (1u << 20) && r == 0; w++)     // the claimer stores it right after its CAS
+              r = __hip_atomic_load(pos + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (r != occ && (r == 0 || !uc_same_term(doc + dict_ref_off(r), dict_ref_len(r), doc + dict_ref_off(occ),
+                                                     dict_ref_len(occ))))
+              set_build_err(err, kErrCollision, d);
+          }
           __hip_atomic_fetch_add(cnt + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           result = s;
           done = true;
@@ -291,7 +306,7 @@ __device__ __forceinline__ uint32_t lower4(uint32_t t) {
 }
 
 __device__ __forceinline__ void token_key(const uint8_t *text, uint32_t s, uint32_t e, uint64_t *lo, uint64_t *hi,
-                                          bool *valid) {
+                                          bool *valid, uint64_t seed) {
   const uint32_t n = e - s;
   if (n > kExactKeyChars) {
     KeyBuilder kb;
@@ -301,7 +316,7 @@ __device__ __forceinline__ void token_key(const uint8_t *text, uint32_t s, uint3
       any |= c != '_';
       kb.push(ascii_lower(c));
     }
-    kb.finish(lo, hi);
+    kb.finish(lo, hi, seed);
     *valid = any;
     return;
   }
@@ -828,7 +843,7 @@ __device__ __forceinline__ void hist_batch(WaveSmem &sm, const BuildParams &p, u
 template <bool PACK>
 __device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p, uint32_t lane, uint32_t nu,
                                               uint32_t doc, uint32_t *g, uint32_t *tf, uint32_t *tdoc,
-                                              uint32_t &actm, uint32_t *pk_len, uint32_t *pk_nu) {
+                                              uint32_t &actm, uint32_t *pk_len, uint32_t *pk_nu, uint64_t wbase) {
   const uint32_t dmask = p.cap_mask;
   const uint16_t *slots = reinterpret_cast<const uint16_t *>(sm.list);
   if (PACK && lane < kPackMax) { pk_len[lane] = 0; pk_nu[lane] = 0; }
@@ -861,7 +876,7 @@ __device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p
     }
     // folded (> 8 byte) terms: exact 128-bit keys, one lookup per lane at a time
     while (__any(foldm != 0)) {
-      uint64_t flo = 1, fhi = kKeyValid;
+      uint64_t flo = 1, fhi = kKeyValid, mine = 0;
       uint32_t k = 0;
       const bool fa = foldm != 0;
       if (fa) {
@@ -870,9 +885,12 @@ __device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p
         const uint64_t key = sm.key[slots[lane + 64 * k]];
         const uint32_t n = (uint32_t)key & 0xFFu, tp = (uint32_t)(key >> 13) & 0x1FFFu;
         bool valid;
-        token_key(sm.text, tp, tp + n, &flo, &fhi, &valid);
+        token_key(sm.text, tp, tp + n, &flo, &fhi, &valid, p.hash_seed);
+        mine = dict_ref_word(wbase + tp, n);
       }
-      const uint32_t gg = dict_find_or_insert(p.dict, dmask, flo, fhi, fa);
+      bool cl;
+      const uint32_t gg = dict_find_or_insert(p.dict, dmask, flo, fhi, fa, &mine, &cl);
+      if (fa && (flo & kLoHashed) && !cl && gg != kInvalidSlot) dict_verify(p, gg, mine, doc);   // > 16 bytes
 #pragma unroll
       for (int kk = 0; kk < (int)kWaveK; kk++)
         if (fa && (uint32_t)kk == k) g[kk] = gg;
@@ -1138,7 +1156,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     // ---- dictionary slots of terms lane + 64k
     uint32_t g[kWaveK], tf[kWaveK], tdoc[kWaveK];
     uint32_t actm = 0;
-    resolve_terms<PACK>(sm, p, lane, nu, (uint32_t)d, g, tf, tdoc, actm, pk_len, pk_nu);
+    resolve_terms<PACK>(sm, p, lane, nu, (uint32_t)d, g, tf, tdoc, actm, pk_len, pk_nu, s0 - shift);
     if (p.debug_stop == 4) { clear_table(sm, lane); continue; }
 
     // ---- CSR row grouped by dictionary range (8 ranges per pass), staged in LDS.
@@ -1425,7 +1443,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     }
     uint32_t g[kWaveK], tf[kWaveK], tdoc[kWaveK];
     uint32_t actm = 0;
-    resolve_terms<false>(sm, p, lane, nu, (uint32_t)m.d, g, tf, tdoc, actm, nullptr, nullptr);
+    resolve_terms<false>(sm, p, lane, nu, (uint32_t)m.d, g, tf, tdoc, actm, nullptr, nullptr, m.s0 - m.shift);
     uint32_t *dense = p.dense + (uint64_t)m.gi * C;
 #pragma unroll
     for (int k = 0; k < (int)kWaveK; k++)
@@ -1537,6 +1555,7 @@ __global__ void __launch_bounds__(256) k_tokenize_long(BuildParams p) {
   uint64_t *keys = p.lt_keys + (size_t)blockIdx.x * 2 * (1ull << p.lt_slots_log2);
   uint32_t *cnt = p.lt_cnt + (size_t)blockIdx.x * (1ull << p.lt_slots_log2);
   uint32_t *gsl = p.lt_g + (size_t)blockIdx.x * (1ull << p.lt_slots_log2);
+  uint64_t *tpos = p.lt_pos + (size_t)blockIdx.x * (1ull << p.lt_slots_log2);
   unsigned long long my_doc_count = 0, my_ttf = 0, my_nnz = 0;
 
   for (uint32_t li = blockIdx.x; li < n_long; li += gridDim.x) {
@@ -1548,7 +1567,7 @@ __global__ void __launch_bounds__(256) k_tokenize_long(BuildParams p) {
     uint32_t lg = 10;
     while (lg < p.lt_slots_log2 && (1ull << lg) < L + 2) lg++;
     const uint32_t T = 1u << lg, mask = T - 1;
-    for (uint32_t i = tid; i < T; i += 256) { keys[2 * i] = 0; keys[2 * i + 1] = 0; cnt[i] = 0; }
+    for (uint32_t i = tid; i < T; i += 256) { keys[2 * i] = 0; keys[2 * i + 1] = 0; cnt[i] = 0; tpos[i] = 0; }
     __syncthreads();
     uint32_t my_len = 0;
     bool bad = false;
@@ -1569,10 +1588,12 @@ __global__ void __launch_bounds__(256) k_tokenize_long(BuildParams p) {
         if (e - s > kMaxTokenLen) { atomicOr(&sm.flags, 8u); continue; }   // cut by the Unicode scanner
         uint64_t lo, hi;
         bool valid;
-        token_key(sm.text, s, e, &lo, &hi, &valid);
+        token_key(sm.text, s, e, &lo, &hi, &valid, p.hash_seed);
         if (!valid) continue;
         my_len++;
-        if (gtable_insert(keys, cnt, mask, lo, hi) == kInvalidSlot) atomicOr(&sm.flags, 4u);
+        const uint64_t occ = dict_ref_word(wlo + (s - shift), e - s);
+        if (gtable_insert(keys, cnt, tpos, mask, lo, hi, occ, p.text + s0, p.err, d) == kInvalidSlot)
+          atomicOr(&sm.flags, 4u);
       }
       __syncthreads();
     }
@@ -1582,7 +1603,7 @@ __global__ void __launch_bounds__(256) k_tokenize_long(BuildParams p) {
       // the full-Unicode scanner: thread t takes the tokens starting in its
       // slice of the document, slices cut just after ASCII class-OTHER bytes
       // (the scan restarts there in the start state).
-      for (uint32_t i = tid; i < T; i += 256) { keys[2 * i] = 0; keys[2 * i + 1] = 0; cnt[i] = 0; }
+      for (uint32_t i = tid; i < T; i += 256) { keys[2 * i] = 0; keys[2 * i + 1] = 0; cnt[i] = 0; tpos[i] = 0; }
       __syncthreads();
       my_len = 0;
       const uint8_t *doc = p.text + s0;
@@ -1598,9 +1619,11 @@ __global__ void __launch_bounds__(256) k_tokenize_long(BuildParams p) {
       const uint64_t stop = slice(tid + 1);
       uint64_t ts, te, lo, hi;
       bool ubad = false;
-      while (uc_next_token(doc, L, &pos, stop, &ts, &te, &lo, &hi, &ubad)) {
+      while (uc_next_token(doc, L, &pos, stop, &ts, &te, &lo, &hi, &ubad, p.hash_seed)) {
         my_len++;
-        if (gtable_insert(keys, cnt, mask, lo, hi) == kInvalidSlot) atomicOr(&sm.flags, 4u);
+        if (gtable_insert(keys, cnt, tpos, mask, lo, hi, dict_ref_word(ts, (uint32_t)(te - ts)), doc, p.err, d) ==
+            kInvalidSlot)
+          atomicOr(&sm.flags, 4u);
       }
       if (ubad) atomicOr(&sm.flags, 16u);
       __syncthreads();
@@ -1620,15 +1643,22 @@ __global__ void __launch_bounds__(256) k_tokenize_long(BuildParams p) {
     atomicAdd(&sm.len, my_len);
     // emission: dictionary lookup + range counts
     uint32_t my_nu = 0;
-    for (uint32_t s0 = 0; s0 < T; s0 += 256) {
-      const uint32_t s = s0 + tid;
+    for (uint32_t sb = 0; sb < T; sb += 256) {
+      const uint32_t s = sb + tid;
       uint64_t lo = 0, hi = 0;
       if (s < T) {
         lo = __hip_atomic_load(keys + 2 * (size_t)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         hi = __hip_atomic_load(keys + 2 * (size_t)s + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       const bool act = lo != 0;
-      uint32_t g = dict_find_or_insert(p.dict, p.cap_mask, act ? lo : 1, act ? hi : kKeyValid, act);
+      uint64_t mine = 0;
+      if (act && (lo & kLoHashed)) {
+        const uint64_t r = __hip_atomic_load(tpos + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        mine = dict_ref_word(s0 + dict_ref_off(r), dict_ref_len(r));       // document-relative -> corpus offset
+      }
+      bool cl;
+      uint32_t g = dict_find_or_insert(p.dict, p.cap_mask, act ? lo : 1, act ? hi : kKeyValid, act, &mine, &cl);
+      if (act && (lo & kLoHashed) && !cl && g != kInvalidSlot) dict_verify(p, g, mine, d);
       if (act) {
         if (g == kInvalidSlot) { set_err(p.err, kErrCapacity, d); g = 0; }
         gsl[s] = g;
@@ -2083,8 +2113,28 @@ __global__ void __launch_bounds__(1024) k_scatter_sort(PostingParams p) {
   }
 }
 
+// Hashed-key checks deferred by dict_verify (the slot's reference occurrence
+// was not visible yet): every reference is final after the tokenizers.
+__global__ void __launch_bounds__(256) k_verify_deferred(BuildParams p) {
+  const uint32_t n = min(*p.verify_count, p.verify_cap);
+  const uint64_t *ref = p.dict + 2 * ((size_t)p.cap_mask + 1);
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t slot = (uint32_t)p.verify_defer[2 * (size_t)i];
+    const uint64_t mine = p.verify_defer[2 * (size_t)i + 1], r = ref[slot];
+    if (r == mine) continue;
+    if (r == 0 || !uc_same_term(p.text + dict_ref_off(r), dict_ref_len(r), p.text + dict_ref_off(mine),
+                                dict_ref_len(mine)))
+      set_build_err(p.err, kErrCollision, 0);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // launchers
+
+hipError_t launch_verify_deferred(const BuildParams &p, hipStream_t s) {
+  hipLaunchKernelGGL(k_verify_deferred, dim3(64), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
 
 hipError_t launch_tokenize_wave(const BuildParams &p, int grid, hipStream_t s) {
   if (p.pack > 1) hipLaunchKernelGGL(k_tokenize_wave<true>, dim3(grid), dim3(64), 0, s, p);

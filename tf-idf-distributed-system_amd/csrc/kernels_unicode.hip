@@ -107,6 +107,7 @@ struct UwSmem {
   unsigned long long klo[kUwSlots];   // key lo; after the lookup: dictionary slot
   unsigned long long khi[kUwSlots];   // key hi (VALID bit set: occupied)
   uint32_t cnt[kUwSlots];             // tf
+  uint32_t kpos[kUwSlots];            // first occurrence: start | end << 16 (document bytes)
   uint32_t rcnt[kUwMaxRanges];        // per-range counts, then cursors
   uint8_t tr[kUwStates * kUwClasses]; // WORD DFA transitions
 };
@@ -198,15 +199,17 @@ __global__ void __launch_bounds__(64) k_tokenize_uwave(BuildParams p) {
     const uint64_t stop = cut(lane + 1);
     bool active = pos < stop, ubad = false, overflow = false;
     uint32_t ntok = 0;
+    bool collide = false;
     while (__any(active)) {
       uint64_t lo = 0, hi = 0;
       bool have = false;
+      uint32_t ts32 = 0, te32 = 0;
       if (active) {
-        uint32_t p32 = (uint32_t)pos, ts32, te32;
+        uint32_t p32 = (uint32_t)pos;
         have = uw_next_span(sm.cls, sm.tr, (uint32_t)L, &p32, (uint32_t)stop, &ts32, &te32, &ubad);
         if (have) {
-          const uint64_t cutp = uc_token_key(doc, L, ts32, te32, &lo, &hi);
-          if (cutp < te32) p32 = (uint32_t)cutp;                   // 255-unit cut: rescan from the cut
+          const uint64_t cutp = uc_token_key(doc, L, ts32, te32, &lo, &hi, p.hash_seed);
+          if (cutp < te32) { p32 = (uint32_t)cutp; te32 = (uint32_t)cutp; }   // 255-unit cut: rescan from the cut
         }
         pos = p32;
         active = have;
@@ -219,10 +222,14 @@ __global__ void __launch_bounds__(64) k_tokenize_uwave(BuildParams p) {
         unsigned long long old = 1;
         if (!done) old = atomicCAS(&sm.klo[slot], 0ull, (unsigned long long)lo);
         const bool won = !done && old == 0;
-        if (won) sm.khi[slot] = hi;
+        if (won) { sm.khi[slot] = hi; sm.kpos[slot] = ts32 | (te32 << 16); }
         asm volatile("" ::: "memory");
         bool match = false;
         if (!done && !won && old == lo) match = sm.khi[slot] == hi;
+        if (match && (lo & kLoHashed)) {                    // hashed key: the same term? (kErrCollision if not)
+          const uint32_t kp = sm.kpos[slot], a = kp & 0xFFFFu, z = kp >> 16;
+          collide |= !uc_same_term(doc + a, z - a, doc + ts32, te32 - ts32);
+        }
         if (won || match) {
           atomicAdd(&sm.cnt[slot], 1u);
           done = true;
@@ -232,6 +239,7 @@ __global__ void __launch_bounds__(64) k_tokenize_uwave(BuildParams p) {
       }
       overflow |= !done;
     }
+    if (collide) set_build_err(p.err, kErrCollision, d);
     // ---- distinct terms; documents the wave cannot take go to the long path
     uint32_t occ = 0;
     for (uint32_t s = lane; s < kUwSlots; s += 64) occ += sm.khi[s] != 0;
@@ -243,10 +251,9 @@ __global__ void __launch_bounds__(64) k_tokenize_uwave(BuildParams p) {
     }
     const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)uw_incl_add(ntok, lane), 63);
     // ---- dictionary slots (8 lookups per lane in flight), range counts
-#pragma unroll
     for (int h = 0; h < 2; h++) {
-      uint64_t klo[8], khi[8];
-      bool act[8];
+      uint64_t klo[8], khi[8], mine[8];
+      bool act[8], cl[8];
       uint32_t g[8];
 #pragma unroll
       for (int k = 0; k < 8; k++) {
@@ -254,12 +261,15 @@ __global__ void __launch_bounds__(64) k_tokenize_uwave(BuildParams p) {
         klo[k] = sm.klo[s];
         khi[k] = sm.khi[s];
         act[k] = khi[k] != 0;
+        const uint32_t kp = sm.kpos[s];
+        mine[k] = dict_ref_word(s0 + (kp & 0xFFFFu), (kp >> 16) - (kp & 0xFFFFu));
         if (!act[k]) { klo[k] = 1; khi[k] = kKeyValid; }
       }
-      dict_lookup_multi<8>(p.dict, p.cap_mask, klo, khi, act, g);
+      dict_lookup_multi<8>(p.dict, p.cap_mask, klo, khi, act, g, mine, cl);
 #pragma unroll
       for (int k = 0; k < 8; k++) {
         if (!act[k]) continue;
+        if ((klo[k] & kLoHashed) && !cl[k] && g[k] != kInvalidSlot) dict_verify(p, g[k], mine[k], d);
         uint32_t gs = g[k];
         if (gs == kInvalidSlot) { atomicOr(p.err, kErrCapacity); gs = 0; }
         sm.klo[lane + 64 * (8 * h + k)] = gs;

@@ -169,6 +169,11 @@ struct tfidf_index {
   std::vector<uint32_t> malformed;     // ... of the last commit, ascending committed ids
   std::vector<uint64_t> h_esc;         // CSR tf escapes of the last build, sorted (csr_put)
   std::vector<uint64_t> h_post_esc;    // block-major posting tf escapes, sorted (post_word)
+  uint64_t hash_seed = 0;              // KeyBuilder seed of the committed index (0 unless a collision was met)
+  uint32_t hash_rebuilds = 0;          // builds redone for a hash collision in the last commit
+  uint32_t collision_doc = 0;          // a document of the last detected collision (diagnostics)
+  DevBuf verify_defer, lt_pos;
+  std::unordered_map<uint32_t, std::string> term_cache;   // hashed slots' term strings (slot_term)
   uint32_t pack_docs = 1;              // documents per wave window in the last commit
   uint64_t pack_retried = 0;           // documents the packs deferred in the last commit
   uint64_t unicode_docs = 0;           // documents with non-ASCII text in the last commit
@@ -268,7 +273,7 @@ extern "C" int tfidf_destroy(tfidf_index *ix) {
   hipStreamSynchronize(ix->copy_stream);
   DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->d_live_map, &ix->dict, &ix->csr, &ix->csr_esc, &ix->doc_len,
                     &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->long_list, &ix->uni_list, &ix->counters, &ix->blk,
-                    &ix->retry_list, &ix->bad_list, &ix->bbase, &ix->post, &ix->post_tmp, &ix->post_esc, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->dense, &ix->chunk_list, &ix->chunk_docs, &ix->chunk_fail, &ix->canon_of_slot,
+                    &ix->retry_list, &ix->bad_list, &ix->bbase, &ix->post, &ix->post_tmp, &ix->post_esc, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->lt_pos, &ix->verify_defer, &ix->dense, &ix->chunk_list, &ix->chunk_docs, &ix->chunk_fail, &ix->canon_of_slot,
                     &ix->q_off, &ix->q_slot, &ix->q_w, &ix->q_role, &ix->q_meta, &ix->cache, &ix->cand, &ix->cand_n, &ix->out_doc,
                     &ix->out_score, &ix->out_n, &ix->hits, &ix->hits_n, &ix->hits_c, &ix->hits_s, &ix->hits_P, &ix->sort_tmp,
                     &ix->row_off, &ix->tvals, &ix->toff, &ix->tdf, &ix->term_tmp, &ix->sent_slot, &ix->vcounts, &ix->vnu,
@@ -666,10 +671,11 @@ static float ev_ms(tfidf_index *ix, int a, int b) {
   return ms;
 }
 
-extern "C" int tfidf_commit(tfidf_index *ix) {
-  if (!ix) return fail(TFIDF_E_INVALID_ARG, "NULL index");
-  std::lock_guard<std::mutex> lk(ix->mu);
-  DeviceGuard g(ix->cfg.device);
+// One index build with ix->hash_seed; kRcCollision when two different terms
+// met under one hashed key (tfidf_commit then rebuilds with another seed).
+constexpr int kRcCollision = -1000;
+constexpr uint32_t kVerifyCap = 1u << 20;      // deferred hashed-key checks per build
+static int commit_once(tfidf_index *ix) {
   hipStream_t s = ix->stream;
   // live documents
   ix->n_docs = ix->n_staged - ix->n_dead;
@@ -709,7 +715,8 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   while ((1u << ix->range_shift) < RS) ix->range_shift++;
   ix->R = C >> ix->range_shift;
 
-  HIP_TRY(ix->dict.reserve((size_t)2 * C * 8));
+  HIP_TRY(ix->dict.reserve((size_t)3 * C * 8));          // lo, hi, reference occurrence (dict_device.h)
+  HIP_TRY(ix->verify_defer.reserve((size_t)kVerifyCap * 16));
   HIP_TRY(ix->csr.reserve(row_cap * 4));
   // escapes: each needs tf >= the field's escape value, and a row holds at
   // most row_cap tokens in all, so this bounds their number
@@ -743,10 +750,11 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   }
 
   // counters: [0..2] stats u64, [3] err flags u32 + [3].hi first doc, [4] long_count, [5] retry_count,
-  // [6] uni_count, [7] occupied dictionary slots, [8] bad_count, [9] CSR escape count
+  // [6] uni_count, [7] occupied dictionary slots, [8] bad_count, [9] CSR escape count, [10] posting
+  // escapes, [11] deferred hashed-key checks
   uint64_t *ctr = ix->counters.as<uint64_t>();
   HIP_TRY(hipMemsetAsync(ix->counters.p, 0, 128, s));
-  HIP_TRY(hipMemsetAsync(ix->dict.p, 0, (size_t)2 * C * 8, s));
+  HIP_TRY(hipMemsetAsync(ix->dict.p, 0, (size_t)3 * C * 8, s));
 
   BuildParams bp{};
   bp.text = ix->text.as<uint8_t>();
@@ -757,6 +765,10 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   bp.cap_mask = C - 1;
   bp.range_shift = ix->range_shift;
   bp.n_ranges = ix->R;
+  bp.hash_seed = ix->hash_seed;
+  bp.verify_defer = ix->verify_defer.as<uint64_t>();
+  bp.verify_count = reinterpret_cast<uint32_t *>(ctr + 11);
+  bp.verify_cap = kVerifyCap;
   bp.csr = ix->csr.as<uint32_t>();
   bp.csr_esc = ix->csr_esc.as<uint64_t>();
   bp.esc_count = reinterpret_cast<uint32_t *>(ctr + 9);
@@ -893,9 +905,11 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
       const uint32_t wgs = (uint32_t)std::min<uint64_t>({(uint64_t)n_fb, (uint64_t)ix->num_cus * 2, by_budget});
       HIP_TRY(ix->lt_keys.reserve((size_t)wgs * 2 * (1ull << lg) * 8));
       HIP_TRY(ix->lt_cnt.reserve((size_t)wgs * (1ull << lg) * 4));
+      HIP_TRY(ix->lt_pos.reserve((size_t)wgs * (1ull << lg) * 8));
       HIP_TRY(ix->lt_g.reserve((size_t)wgs * (1ull << lg) * 4));
       bp.lt_keys = ix->lt_keys.as<uint64_t>();
       bp.lt_cnt = ix->lt_cnt.as<uint32_t>();
+      bp.lt_pos = ix->lt_pos.as<uint64_t>();
       bp.lt_g = ix->lt_g.as<uint32_t>();
       bp.lt_slots_log2 = lg;
       HIP_TRY(launch_tokenize_long(bp, (int)wgs, s));
@@ -905,6 +919,7 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
     HIP_TRY(hipStreamSynchronize(s));
   }
   const uint32_t err = (uint32_t)(hctr[3] & 0xFFFFFFFFu), err_doc = (uint32_t)(hctr[3] >> 32);
+  if (err & kErrCollision) { ix->collision_doc = err_doc; return kRcCollision; }
   if (err) {
     ix->committed = false;
     if (err & kErrCapacity)
@@ -1030,6 +1045,8 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
     HIP_TRY(hipMemcpyAsync(ix->h_dict.data(), ix->dict.p, (size_t)2 * C * 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(ix->h_df.data(), ix->df_dev(), (size_t)C * 4,
                          hipMemcpyDeviceToHost, s));
+  // hashed-key identity checks the tokenizers had to defer
+  HIP_TRY(launch_verify_deferred(bp, s));
   // occupied dictionary slots counted on the device (ctr[7]) instead of a host
   // pass over the mirror (8 M slots at 2^23 took milliseconds)
   HIP_TRY(launch_count_nonzero(ix->dict.as<uint64_t>(), C, reinterpret_cast<unsigned long long *>(ctr + 7), s));
@@ -1052,6 +1069,7 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
     std::sort(ix->malformed.begin(), ix->malformed.end());
   }
   const uint32_t err2 = (uint32_t)tail[0];
+  if (err2 & kErrCollision) { ix->collision_doc = (uint32_t)(tail[0] >> 32); return kRcCollision; }
   if (err2 & kErrTfTooLarge) return fail(TFIDF_E_UNSUPPORTED_INPUT, "a term frequency exceeds 2^24 - 1");
   ix->num_terms = tail[4];
 
@@ -1072,6 +1090,31 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   ix->gdf.clear();
   ix->committed = true;
   return upload_cache(ix);
+}
+
+extern "C" int tfidf_commit(tfidf_index *ix) {
+  if (!ix) return fail(TFIDF_E_INVALID_ARG, "NULL index");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  DeviceGuard g(ix->cfg.device);
+  ix->committed = false;                 // a failed rebuild leaves no half-built index behind
+  ix->term_cache.clear();
+  // Hash seeds: 0, then 1, 2, 3 after a detected collision (TFIDF_TEST_WEAK_HASH:
+  // start from a seed under which equal-length hashed keys collide)
+  const char *weak = getenv("TFIDF_TEST_WEAK_HASH");
+  ix->hash_seed = (weak && atoi(weak)) ? kWeakHashSeed : 0;
+  ix->hash_rebuilds = 0;
+  for (uint32_t attempt = 0;; attempt++) {
+    const int rc = commit_once(ix);
+    if (rc != TFIDF_OK) {
+      hipStreamSynchronize(ix->stream);        // nothing of this build may still run on either stream
+      hipStreamSynchronize(ix->copy_stream);
+    }
+    if (rc != kRcCollision) return rc;
+    if (attempt == 3)
+      return fail(TFIDF_E_UNSUPPORTED_INPUT, "hash collisions under 4 seeds (last in document %u)", ix->collision_doc);
+    ix->hash_seed = attempt + 1;
+    ix->hash_rebuilds++;
+  }
 }
 
 extern "C" int tfidf_get_commit_timing(const tfidf_index *ix, tfidf_commit_timing *out) {
@@ -1095,6 +1138,8 @@ extern "C" int tfidf_stats(const tfidf_index *ix, tfidf_index_stats *out) {
   out->unicode_docs = ix->unicode_docs;
   out->long_chunked = ix->long_chunked;
   out->malformed_docs = ix->committed ? ix->malformed.size() : 0;
+  out->hash_seed = ix->hash_seed;
+  out->hash_rebuilds = ix->hash_rebuilds;
   const DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->dict, &ix->csr, &ix->csr_esc, &ix->doc_len,
                           &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->blk, &ix->bbase, &ix->post,
                           &ix->toff, &ix->tdf};
@@ -1122,6 +1167,43 @@ static uint32_t host_lookup(const tfidf_index *ix, uint64_t lo, uint64_t hi) {
   return kInvalidSlot;
 }
 
+// Lower-cased term string of dictionary slot `slot`: decoded from an exact
+// key, or (hashed key) read from its reference occurrence in the corpus.
+struct StrSink {
+  std::string s;
+  void push(uint8_t c) { s.push_back((char)c); }
+};
+static int slot_term(tfidf_index *ix, uint32_t slot, std::string *out) {
+  char b[32];
+  const uint64_t lo = ix->h_dict[slot], hi = ix->h_dict[(size_t)ix->C + slot];
+  if (const uint32_t n = key_decode(lo, hi, b)) { out->assign(b, n); return TFIDF_OK; }
+  auto it = ix->term_cache.find(slot);
+  if (it != ix->term_cache.end()) { *out = it->second; return TFIDF_OK; }
+  uint64_t r = 0;
+  HIP_TRY(hipMemcpy(&r, ix->dict.as<uint64_t>() + 2 * (size_t)ix->C + slot, 8, hipMemcpyDeviceToHost));
+  if (r == 0) return fail(TFIDF_E_STATE, "dictionary slot %u has no reference occurrence", slot);
+  std::vector<uint8_t> raw(dict_ref_len(r));
+  if (!raw.empty())
+    HIP_TRY(hipMemcpy(raw.data(), ix->text.as<uint8_t>() + dict_ref_off(r), raw.size(), hipMemcpyDeviceToHost));
+  StrSink sink;
+  uc_token_bytes(raw.data(), raw.size(), 0, raw.size(), sink);
+  ix->term_cache.emplace(slot, sink.s);
+  *out = sink.s;
+  return TFIDF_OK;
+}
+
+// Dictionary slot of the (lower-cased) term t, kInvalidSlot if absent; a
+// hashed key must also match the slot's term string.
+static uint32_t lookup_term(tfidf_index *ix, const std::string &t) {
+  uint64_t lo, hi;
+  term_key(t, &lo, &hi, ix->hash_seed);
+  const uint32_t s = host_lookup(ix, lo, hi);
+  if (s == kInvalidSlot || !key_is_hashed(lo)) return s;
+  std::string ts;
+  if (slot_term(ix, s, &ts) != TFIDF_OK || ts != t) return kInvalidSlot;
+  return s;
+}
+
 struct PreparedQuery {
   std::vector<uint32_t> slot;
   std::vector<float> w;
@@ -1147,9 +1229,7 @@ static int prepare_query(tfidf_index *ix, const uint8_t *q, uint64_t n, Prepared
   uint32_t n_should = 0;
   bool has_not = false;
   for (const PlanTerm &t : plan.terms) {
-    uint64_t lo, hi;
-    term_key(t.term, &lo, &hi);
-    const uint32_t s = host_lookup(ix, lo, hi);
+    const uint32_t s = lookup_term(ix, t.term);
     if (s == kInvalidSlot) continue;                   // absent term contributes nothing
     float wv = 0.0f;
     if (t.role != kRoleNot) {
@@ -1555,17 +1635,9 @@ extern "C" int tfidf_doc_terms(tfidf_index *ix, uint64_t doc, char *terms, uint6
   }
   std::vector<std::pair<std::string, uint32_t>> rows;
   for (uint32_t i = 0; i < nu; i++) {
-    char b[32];
-    const uint64_t lo = ix->h_dict[col[i]], hi = ix->h_dict[(size_t)ix->C + col[i]];
-    uint32_t n = key_decode(lo, hi, b);
-    std::string s;
-    if (n) s.assign(b, n);
-    else {
-      char hx[48];
-      snprintf(hx, sizeof hx, "#%016llx%016llx", (unsigned long long)hi, (unsigned long long)lo);
-      s = hx;
-    }
-    rows.emplace_back(std::move(s), tf[i]);
+    std::string t;
+    if (int rc = slot_term(ix, col[i], &t)) return rc;
+    rows.emplace_back(std::move(t), tf[i]);
   }
   std::sort(rows.begin(), rows.end());
   uint64_t need = 0;
@@ -1587,9 +1659,7 @@ extern "C" int tfidf_term_df(tfidf_index *ix, const uint8_t *term, uint64_t len,
   if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
   if (int e = wait_gdf(ix)) return e;
   std::string t((const char *)term, len);
-  uint64_t lo, hi;
-  term_key(t, &lo, &hi);
-  const uint32_t s = host_lookup(ix, lo, hi);
+  const uint32_t s = lookup_term(ix, t);
   const uint64_t l = s == kInvalidSlot ? 0 : ix->h_df[s];
   if (df_local) *df_local = l;
   if (df_effective) *df_effective = (s != kInvalidSlot && ix->has_global) ? ix->gdf[s] : l;

@@ -15,6 +15,12 @@
 //     LO_HASHED, hi = VALID | 63 bits of a second chain — no exact form.
 // Bit 63 of hi (VALID) is set for every key so that hi == 0 marks "not
 // written" in the device dictionary.
+// Hashed keys are not trusted to identify a term: every merge of two
+// occurrences under one hashed key (per-document tables, the global
+// dictionary, query lookups) compares the lower-cased strings, the global
+// dictionary keeping one reference occurrence per slot; a mismatch (a real
+// collision) makes the build start over with another hash seed, so no two
+// terms ever share a key in a committed index (tfidf_capi.hip, commit).
 #pragma once
 
 #include <stdint.h>
@@ -40,6 +46,9 @@ constexpr uint32_t kInvalidSlot = 0xFFFFFFFFu;
 // the scorer reads role << 24 | MUST clause index per term
 constexpr uint32_t kRoleShould = 0, kRoleMust = 1, kRoleNot = 2;
 constexpr uint32_t kMaxTf = (1u << 24) - 1;     // tf packs into 24 bits of a posting
+// Hash seed that makes every two hashed keys of equal length collide (test
+// hook TFIDF_TEST_WEAK_HASH: exercises collision detection and the rebuild).
+constexpr uint64_t kWeakHashSeed = 0x5EED0000DEADBEEFull;
 
 // Word_Break classes (ASCII) used by the tokenizer, one bit each.
 constexpr uint8_t kClsL = 1;    // ALetter
@@ -122,11 +131,19 @@ struct KeyBuilder {
       cur = 0;
     }
   }
-  TFIDF_HD void finish(uint64_t *klo, uint64_t *khi) const {
+  // seed: the index's hash seed (0 unless a build met a hash collision and
+  // was redone, tfidf_capi.hip); it changes the hashed forms only.
+  TFIDF_HD void finish(uint64_t *klo, uint64_t *khi, uint64_t seed = 0) const {
+    if (seed == kWeakHashSeed && (na || n > kExactKeyChars)) {      // tests: every same-length pair collides
+      *klo = (na ? 0ull : (w0 & 0x7F7F7F7F7F7F7F7Full)) | kLoLong | kLoHashed;
+      *khi = (uint64_t)n | kKeyValid;
+      return;
+    }
+    const uint64_t sd = seed * 0xD6E8FEB86659FD93ull;
     if (na) {
       const uint64_t t = (uint64_t)n << 56;
-      *klo = (mix64(hb ^ cur ^ t) & 0x7F7F7F7F7F7F7F7Full) | kLoLong | kLoHashed;
-      *khi = mix64(hc + (cur ^ t) * 0x9E3779B97F4A7C15ull) | kKeyValid;
+      *klo = (mix64(hb ^ cur ^ t ^ sd) & 0x7F7F7F7F7F7F7F7Full) | kLoLong | kLoHashed;
+      *khi = mix64(hc + (cur ^ t ^ sd) * 0x9E3779B97F4A7C15ull) | kKeyValid;
     } else if (n <= 8) {
       *klo = w0;
       *khi = kKeyValid;
@@ -135,7 +152,7 @@ struct KeyBuilder {
       *khi = w1 | kKeyValid;
     } else {
       *klo = w0 | kLoLong | kLoHashed;
-      *khi = mix64(hb ^ mix64(hc ^ cur ^ ((uint64_t)n << 56))) | kKeyValid;
+      *khi = mix64(hb ^ mix64(hc ^ cur ^ ((uint64_t)n << 56) ^ sd)) | kKeyValid;
     }
   }
 };

@@ -12,6 +12,7 @@ namespace tfidf {
 constexpr uint32_t kErrCapacity = 4u;
 constexpr uint32_t kErrTfTooLarge = 8u;
 constexpr uint32_t kErrLongScratch = 16u;
+constexpr uint32_t kErrCollision = 32u;   // two different terms under one hashed key: rebuild with another seed
 
 // Long-document path: chunks of kChunk bytes, global per-document table.
 constexpr uint32_t kChunk = 2048;
@@ -24,7 +25,11 @@ struct BuildParams {
   const uint64_t *offsets;    // staged doc offsets [n_staged + 1]
   const uint32_t *live_map;   // committed doc -> staged doc (nullptr = identity)
   uint64_t n_docs;            // committed docs
-  uint64_t *dict;             // 2*C u64: lo[C] (key lo per slot) then hi[C]
+  uint64_t *dict;             // 3*C u64: lo[C] (key lo per slot), hi[C], ref[C] (dict_device.h)
+  uint64_t hash_seed;         // KeyBuilder seed of this build (tfidf_common.h)
+  uint64_t *verify_defer;     // hashed-key checks whose reference was not visible yet: (slot, ref word)
+  uint32_t *verify_count;
+  uint32_t verify_cap;
   uint32_t cap_mask;          // C - 1
   uint32_t range_shift;       // log2(range size)
   uint32_t n_ranges;          // R = C >> range_shift
@@ -46,6 +51,7 @@ struct BuildParams {
   uint32_t *err;              // [0] flags, [1] first offending doc
   // long path scratch (one table region per workgroup)
   uint64_t *lt_keys;          // 2 * lt_slots per workgroup
+  uint64_t *lt_pos;           // lt_slots per workgroup: first occurrence (dict_ref_word, document-relative)
   uint32_t *lt_cnt;           // lt_slots per workgroup
   uint32_t *lt_g;             // lt_slots per workgroup
   uint32_t lt_slots_log2;     // table slots per workgroup (max)
@@ -101,11 +107,40 @@ __host__ __device__ inline uint32_t csr_esc_tf(const uint64_t *esc, uint64_t n, 
   return a < n && (esc[a] >> 24) == idx ? (uint32_t)(esc[a] & 0xFFFFFFu) : 0u;
 }
 
+}  // namespace tfidf
+#if defined(__HIPCC__)
+#include "dict_device.h"
+#include "unicode_scan.h"
+#endif
+namespace tfidf {
 #if defined(__HIPCC__)
 __device__ inline void set_build_err(uint32_t *err, uint32_t flag, uint32_t doc) {
   const uint32_t old = atomicOr(err, flag);
   if (old == 0) atomicExch(err + 1, doc);
 }
+// Exact identity of a hashed term that resolved to global dictionary slot
+// `slot` without claiming it: its occurrence `mine` (dict_ref_word) must
+// spell the same term as the slot's reference occurrence.  A reference not
+// visible yet (claimed by another wave just now) defers the check to
+// k_verify_deferred after the tokenizers.
+__device__ inline void dict_verify(const BuildParams &p, uint32_t slot, uint64_t mine, uint32_t doc) {
+  const uint64_t r = __hip_atomic_load(p.dict + 2 * ((size_t)p.cap_mask + 1) + slot, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+  if (r == mine) return;
+  if (r == 0) {
+    const uint32_t at = atomicAdd(p.verify_count, 1u);
+    if (at < p.verify_cap) {
+      p.verify_defer[2 * (size_t)at] = slot;
+      p.verify_defer[2 * (size_t)at + 1] = mine;
+    } else {
+      set_build_err(p.err, kErrCollision, doc);        // cannot defer: treated as a collision (rebuild)
+    }
+    return;
+  }
+  if (!uc_same_term(p.text + dict_ref_off(r), dict_ref_len(r), p.text + dict_ref_off(mine), dict_ref_len(mine)))
+    set_build_err(p.err, kErrCollision, doc);
+}
+
 // write CSR entry idx of document doc (dictionary slot, tf)
 __device__ inline void csr_put(const BuildParams &p, uint64_t idx, uint32_t slot, uint32_t tf, uint32_t doc) {
   const uint32_t esc = csr_esc_value(p.range_shift);
@@ -165,7 +200,8 @@ constexpr uint64_t kDenseBudget = 2ull << 30;          // per-group dense count 
 hipError_t launch_tokenize_chunks(const BuildParams &p, int grid, hipStream_t s);
 hipError_t launch_long_rows(const BuildParams &p, uint32_t n_docs, hipStream_t s);
 hipError_t launch_tokenize_uwave(const BuildParams &p, int grid, hipStream_t s);   // kernels_unicode.hip
-constexpr uint32_t kUwaveWGsPerCU = 5;    // 64-thread workgroups, ~29 KB LDS each
+constexpr uint32_t kUwaveWGsPerCU = 4;    // 64-thread workgroups, ~33 KB LDS each
+hipError_t launch_verify_deferred(const BuildParams &p, hipStream_t s);           // kernels_index.hip
 hipError_t launch_df_partial(const PostingParams &p, hipStream_t s);
 hipError_t launch_df_sum(const PostingParams &p, hipStream_t s);
 hipError_t launch_row_scan(const PostingParams &p, hipStream_t s);

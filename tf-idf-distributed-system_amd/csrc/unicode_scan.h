@@ -318,27 +318,51 @@ TFIDF_HD uint64_t uc_token_bytes(const uint8_t *s, uint64_t n, uint64_t ts, uint
   return p;
 }
 
-TFIDF_HD uint64_t uc_token_key(const uint8_t *s, uint64_t n, uint64_t ts, uint64_t te, uint64_t *lo, uint64_t *hi) {
+TFIDF_HD uint64_t uc_token_key(const uint8_t *s, uint64_t n, uint64_t ts, uint64_t te, uint64_t *lo, uint64_t *hi,
+                               uint64_t seed = 0) {
   KeyBuilder kb;
   const uint64_t p = uc_token_bytes(s, n, ts, te, kb);
-  kb.finish(lo, hi);
+  kb.finish(lo, hi, seed);
   return p;
+}
+
+// Are the tokens s1[0, n1) and s2[0, n2) (raw bytes, already cut at 255
+// units) the same term, i.e. equal lower-cased code points?  Raw equality
+// first (the common case: the same spelling).
+TFIDF_HD bool uc_same_term(const uint8_t *s1, uint32_t n1, const uint8_t *s2, uint32_t n2) {
+  if (n1 == n2) {
+    uint32_t i = 0;
+    while (i < n1 && s1[i] == s2[i]) i++;
+    if (i == n1) return true;
+  }
+  uint64_t p1 = 0, p2 = 0;
+  while (p1 < n1 && p2 < n2) {
+    uint32_t l1, l2;
+    const uint32_t c1 = utf8_decode(s1, n1, p1, &l1), c2 = utf8_decode(s2, n2, p2, &l2);
+    if (c1 == kUcBad || c2 == kUcBad) return false;
+    const uint32_t x1 = c1 < 0x80u ? (uint32_t)ascii_lower((uint8_t)c1) : uc_lower(c1);
+    const uint32_t x2 = c2 < 0x80u ? (uint32_t)ascii_lower((uint8_t)c2) : uc_lower(c2);
+    if (x1 != x2) return false;
+    p1 += l1;
+    p2 += l2;
+  }
+  return p1 == n1 && p2 == n2;
 }
 
 // Host/device loop body: next token in [*pos, stop) with its key; handles the
 // 255-unit cut (scanning restarts at the cut).
 template <class Src>
 TFIDF_HD bool uc_next_token(const Src &src, const uint8_t *s, uint64_t n, uint64_t *pos, uint64_t stop, uint64_t *ts,
-                            uint64_t *te, uint64_t *lo, uint64_t *hi, bool *bad) {
+                            uint64_t *te, uint64_t *lo, uint64_t *hi, bool *bad, uint64_t seed = 0) {
   if (!uc_next_span(src, n, pos, stop, ts, te, bad)) return false;
-  const uint64_t cut = uc_token_key(s, n, *ts, *te, lo, hi);
+  const uint64_t cut = uc_token_key(s, n, *ts, *te, lo, hi, seed);
   if (cut < *te) { *te = cut; *pos = cut; }
   return true;
 }
 
 TFIDF_HD bool uc_next_token(const uint8_t *s, uint64_t n, uint64_t *pos, uint64_t stop, uint64_t *ts, uint64_t *te,
-                            uint64_t *lo, uint64_t *hi, bool *bad) {
-  return uc_next_token(UcDecodeSrc{s, n}, s, n, pos, stop, ts, te, lo, hi, bad);
+                            uint64_t *lo, uint64_t *hi, bool *bad, uint64_t seed = 0) {
+  return uc_next_token(UcDecodeSrc{s, n}, s, n, pos, stop, ts, te, lo, hi, bad, seed);
 }
 
 }  // namespace tfidf

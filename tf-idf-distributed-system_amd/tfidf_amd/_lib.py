@@ -42,7 +42,7 @@ class IndexStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("num_docs", "doc_count", "sum_ttf", "num_terms", "nnz",
                                           "device_bytes", "long_docs", "text_bytes", "term_major",
                                           "pack_docs", "pack_retried", "unicode_docs", "long_chunked",
-                                          "malformed_docs")]
+                                          "malformed_docs", "hash_seed", "hash_rebuilds")]
 
 
 class CommitTiming(C.Structure):

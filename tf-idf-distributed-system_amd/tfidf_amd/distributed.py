@@ -43,6 +43,12 @@ class HipShardAdapter:
         s = self.shard.stats()
         return int(s["doc_count"]), int(s["sum_ttf"]), int(s["num_docs"])
 
+    def hash_seed(self):
+        """Seed of the shard's hashed term keys (0 unless its commit met a
+        collision and rebuilt): GLOBAL statistics match terms across shards by
+        key, so every shard must use the same one."""
+        return int(self.shard.stats()["hash_seed"])
+
     # -- GLOBAL statistics (term ownership) --------------------------------
     def vocab_partition(self, n_ranks):
         """-> (records int64 [n, 3] (lo, hi, df) grouped by owner, counts int64 [n_ranks]), on device."""
@@ -164,9 +170,13 @@ def global_commit(adapter, group=None, vocab_size=False):
     ws = dist.get_world_size(group)
     me = dist.get_rank(group)
     dc, ttf, _ = adapter.local_stats()                      # host values of the shard's commit
+    seed = adapter.hash_seed() if hasattr(adapter, "hash_seed") else 0
     rec, cnt = adapter.vocab_partition(ws)                  # device, asynchronous
-    meta = torch.cat([cnt.to(torch.int64), torch.tensor([dc, ttf], dtype=torch.int64, device=dev)])
+    meta = torch.cat([cnt.to(torch.int64), torch.tensor([dc, ttf, seed], dtype=torch.int64, device=dev)])
     M = _all_gather(meta, group).cpu().tolist()             # the host sync
+    if len({int(M[r][ws + 2]) for r in range(ws)}) != 1:
+        raise RuntimeError("shards hash terms with different seeds (a commit met a hash collision and rebuilt): "
+                           "GLOBAL statistics need one seed on every shard")
     send = [int(x) for x in M[me][:ws]]
     recv = [int(M[r][me]) for r in range(ws)]
     gdc = sum(int(M[r][ws]) for r in range(ws))

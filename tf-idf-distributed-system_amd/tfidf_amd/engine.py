@@ -222,10 +222,14 @@ class ShardIndex:
     def doc_terms(self, doc):
         ln, _ = self.doc_len(doc)
         cap = ln + 1
-        buf = C.create_string_buffer(cap * 48 + 64)
         tfs = np.zeros(cap, np.uint32)
         n = C.c_uint64()
-        L.check(L.load().tfidf_doc_terms(self._h, doc, buf, len(buf), L.ptr(tfs, C.c_uint32), cap, C.byref(n)))
+        for per in (48, 1024):                   # term strings: up to 255 UTF-16 units (<= 1020 bytes)
+            buf = C.create_string_buffer(cap * per + 64)
+            rc = L.load().tfidf_doc_terms(self._h, doc, buf, len(buf), L.ptr(tfs, C.c_uint32), cap, C.byref(n))
+            if rc != L.E_BUFFER:
+                break
+        L.check(rc)
         terms = buf.raw.split(b"\0")[:n.value]
         return dict(zip(terms, tfs[:n.value].tolist()))
 
