@@ -206,6 +206,14 @@ struct tfidf_index {
   uint64_t n_sent = 0;
 
   // query scratch
+  // query upload / top-k results: one pinned staging buffer and one copy each
+  // way per search (q_in: off | slot | w | role | meta; q_out: doc | score | n)
+  DevBuf q_in, q_out;
+  PinnedVec<uint32_t> q_host, q_res;
+  hipEvent_t q_in_ev = nullptr;        // the last upload out of q_host
+  bool q_in_pending = false;
+  uint32_t *res_doc = nullptr, *res_n = nullptr;
+  float *res_score = nullptr;
   DevBuf q_off, q_slot, q_w, q_role, q_meta, cache, cand, cand_n, out_doc, out_score, out_n, hits, hits_n, hits_c, hits_s, hits_P, sort_tmp;
   float last_ms_scoring = 0, last_ms_total = 0;
 };
@@ -258,6 +266,7 @@ extern "C" int tfidf_create(const tfidf_config *cfg, tfidf_index **out) {
   for (int i = 0; i < 2; i++) hipEventCreateWithFlags(&ix->stage_ev[i], hipEventDisableTiming);
   for (int i = 0; i < 2; i++) hipEventCreateWithFlags(&ix->mir_ev[i], hipEventDisableTiming);
   hipEventCreateWithFlags(&ix->gdf_ev, hipEventDisableTiming);
+  hipEventCreateWithFlags(&ix->q_in_ev, hipEventDisableTiming);
   hipError_t e = ix->offsets.reserve(64);
   if (e != hipSuccess) { delete ix; return fail(TFIDF_E_OOM, "hipMalloc offsets"); }
   uint64_t zero = 0;
@@ -275,11 +284,12 @@ extern "C" int tfidf_destroy(tfidf_index *ix) {
                     &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->long_list, &ix->uni_list, &ix->counters, &ix->blk,
                     &ix->retry_list, &ix->bad_list, &ix->bbase, &ix->post, &ix->post_tmp, &ix->post_esc, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->lt_pos, &ix->verify_defer, &ix->dense, &ix->chunk_list, &ix->chunk_docs, &ix->chunk_fail, &ix->canon_of_slot,
                     &ix->q_off, &ix->q_slot, &ix->q_w, &ix->q_role, &ix->q_meta, &ix->cache, &ix->cand, &ix->cand_n, &ix->out_doc,
-                    &ix->out_score, &ix->out_n, &ix->hits, &ix->hits_n, &ix->hits_c, &ix->hits_s, &ix->hits_P, &ix->sort_tmp,
+                    &ix->out_score, &ix->out_n, &ix->q_in, &ix->q_out, &ix->hits, &ix->hits_n, &ix->hits_c, &ix->hits_s, &ix->hits_P, &ix->sort_tmp,
                     &ix->row_off, &ix->tvals, &ix->toff, &ix->tdf, &ix->term_tmp, &ix->sent_slot, &ix->vcounts, &ix->vnu,
                     &ix->vt_table, &ix->vt_sum, &ix->vt_rslot, &ix->gdf_dev, &ix->ovf};
   for (DevBuf *b : bufs) b->release();
   for (int i = 0; i < EV_N; i++) hipEventDestroy(ix->ev[i]);
+  if (ix->q_in_ev) hipEventDestroy(ix->q_in_ev);
   for (int i = 0; i < 2; i++) {
     if (ix->stage[i]) hipHostFree(ix->stage[i]);
     hipEventDestroy(ix->stage_ev[i]);
@@ -1275,21 +1285,25 @@ struct QueryBatch {
 static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint32_t k) {
   hipStream_t s = ix->stream;
   const std::vector<uint32_t> &qoff = qb.off, &slots = qb.slot;
-  const std::vector<float> &ws = qb.w;
-  HIP_TRY(ix->q_off.reserve(qoff.size() * 4));
-  HIP_TRY(ix->q_slot.reserve(slots.size() * 4 + 4));
-  HIP_TRY(ix->q_w.reserve(ws.size() * 4 + 4));
-  HIP_TRY(hipMemcpyAsync(ix->q_off.p, qoff.data(), qoff.size() * 4, hipMemcpyHostToDevice, s));
-  if (!slots.empty()) {
-    HIP_TRY(hipMemcpyAsync(ix->q_slot.p, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(ix->q_w.p, ws.data(), ws.size() * 4, hipMemcpyHostToDevice, s));
-  }
+  const size_t ns = slots.size(), nr = qb.ops ? ns + qb.meta.size() : 0;
+  const size_t words = qoff.size() + 2 * ns + nr;
+  // one pinned staging buffer, one upload (the previous upload out of it must
+  // have left: batch searches return before their copies run)
+  if (ix->q_in_pending) HIP_TRY(hipEventSynchronize(ix->q_in_ev));
+  HIP_TRY(ix->q_host.resize(words));
+  uint32_t *h = ix->q_host.data();
+  memcpy(h, qoff.data(), qoff.size() * 4);
+  memcpy(h + qoff.size(), slots.data(), ns * 4);
+  memcpy(h + qoff.size() + ns, qb.w.data(), ns * 4);
   if (qb.ops) {
-    HIP_TRY(ix->q_role.reserve(qb.role.size() * 4 + 4));
-    HIP_TRY(ix->q_meta.reserve(qb.meta.size() * 4 + 4));
-    HIP_TRY(hipMemcpyAsync(ix->q_role.p, qb.role.data(), qb.role.size() * 4, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(ix->q_meta.p, qb.meta.data(), qb.meta.size() * 4, hipMemcpyHostToDevice, s));
+    memcpy(h + qoff.size() + 2 * ns, qb.role.data(), ns * 4);
+    memcpy(h + qoff.size() + 3 * ns, qb.meta.data(), qb.meta.size() * 4);
   }
+  HIP_TRY(ix->q_in.reserve(words * 4 + 16));
+  HIP_TRY(hipMemcpyAsync(ix->q_in.p, h, words * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipEventRecord(ix->q_in_ev, s));
+  ix->q_in_pending = true;
+  uint32_t *din = ix->q_in.as<uint32_t>();
   QueryParams qp{};
   qp.post = ix->post.as<uint64_t>();
   qp.post32 = ix->post.as<uint32_t>();
@@ -1302,11 +1316,11 @@ static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint
   qp.n_blocks = ix->n_blocks;
   qp.n_docs = ix->n_docs;
   qp.cache = ix->cache.as<float>();
-  qp.q_off = ix->q_off.as<uint32_t>();
-  qp.q_slot = ix->q_slot.as<uint32_t>();
-  qp.q_w = ix->q_w.as<float>();
-  qp.q_role = qb.ops ? ix->q_role.as<uint32_t>() : nullptr;
-  qp.q_meta = qb.ops ? ix->q_meta.as<uint32_t>() : nullptr;
+  qp.q_off = din;
+  qp.q_slot = din + qoff.size();
+  qp.q_w = reinterpret_cast<const float *>(din + qoff.size() + ns);
+  qp.q_role = qb.ops ? din + qoff.size() + 2 * ns : nullptr;
+  qp.q_meta = qb.ops ? din + qoff.size() + 3 * ns : nullptr;
   qp.ops = qb.ops ? 1u : 0u;
   qp.n_q = n_q;
   qp.k = k;
@@ -1319,14 +1333,16 @@ static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint
   if (k) {
     HIP_TRY(ix->cand.reserve((size_t)n_q * ix->n_blocks * k * 8 + 8));
     HIP_TRY(ix->cand_n.reserve((size_t)n_q * ix->n_blocks * 4 + 4));
-    HIP_TRY(ix->out_doc.reserve((size_t)n_q * k * 4));
-    HIP_TRY(ix->out_score.reserve((size_t)n_q * k * 4));
-    HIP_TRY(ix->out_n.reserve((size_t)n_q * 4));
+    // results contiguous (doc | score | n): a single query reads them back in one copy
+    HIP_TRY(ix->q_out.reserve(((size_t)2 * n_q * k + n_q) * 4 + 16));
+    ix->res_doc = ix->q_out.as<uint32_t>();
+    ix->res_score = reinterpret_cast<float *>(ix->res_doc + (size_t)n_q * k);
+    ix->res_n = ix->res_doc + (size_t)2 * n_q * k;
     qp.cand = ix->cand.as<uint64_t>();
     qp.cand_n = ix->cand_n.as<uint32_t>();
-    qp.out_doc = ix->out_doc.as<uint32_t>();
-    qp.out_score = ix->out_score.as<float>();
-    qp.out_n = ix->out_n.as<uint32_t>();
+    qp.out_doc = ix->res_doc;
+    qp.out_score = ix->res_score;
+    qp.out_n = ix->res_n;
   } else {
     HIP_TRY(ix->hits.reserve((size_t)ix->n_blocks * kBlockDocs * 8 + 8));
     HIP_TRY(ix->hits_n.reserve((size_t)ix->n_blocks * 4 + 4));
@@ -1387,16 +1403,16 @@ extern "C" int tfidf_search(tfidf_index *ix, const uint8_t *q, uint64_t q_len, u
   if (rc) return rc;
   hipStream_t s = ix->stream;
   if (k) {
-    uint32_t n = 0;
-    HIP_TRY(hipMemcpyAsync(&n, ix->out_n.p, 4, hipMemcpyDeviceToHost, s));
+    // one copy of (doc[k] | score[k] | n) into pinned memory, one wait
+    HIP_TRY(ix->q_res.resize((size_t)2 * k + 1));
+    HIP_TRY(hipMemcpyAsync(ix->q_res.data(), ix->res_doc, ((size_t)2 * k + 1) * 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
+    ix->q_in_pending = false;
+    const uint32_t n = ix->q_res[2 * k];
     *n_out = n;
     if (n > cap) return fail(TFIDF_E_BUFFER, "need %u result slots", n);
-    if (n) {
-      HIP_TRY(hipMemcpyAsync(doc_ids, ix->out_doc.p, n * 4, hipMemcpyDeviceToHost, s));
-      HIP_TRY(hipMemcpyAsync(scores, ix->out_score.p, n * 4, hipMemcpyDeviceToHost, s));
-    }
-    HIP_TRY(hipStreamSynchronize(s));
+    memcpy(doc_ids, ix->q_res.data(), n * 4);
+    memcpy(scores, ix->q_res.data() + k, n * 4);
     ix->last_ms_scoring = ev_ms(ix, EV_Q0, EV_Q1);
     ix->last_ms_total = ev_ms(ix, EV_Q0, EV_Q2);
     return TFIDF_OK;
@@ -1450,9 +1466,9 @@ extern "C" int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const 
   int rc = run_scoring(ix, qb, n_q, k);
   if (rc) return rc;
   hipStream_t s = ix->stream;
-  HIP_TRY(hipMemcpyAsync(counts, ix->out_n.p, (size_t)n_q * 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(doc_ids, ix->out_doc.p, (size_t)n_q * k * 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(scores, ix->out_score.p, (size_t)n_q * k * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(counts, ix->res_n, (size_t)n_q * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(doc_ids, ix->res_doc, (size_t)n_q * k * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(scores, ix->res_score, (size_t)n_q * k * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   ix->last_ms_scoring = ev_ms(ix, EV_Q0, EV_Q1);
   ix->last_ms_total = ev_ms(ix, EV_Q0, EV_Q2);
@@ -1498,7 +1514,7 @@ extern "C" int tfidf_search_batch_keys_device(tfidf_index *ix, const uint8_t *q_
   }
   int rc = run_scoring(ix, qb, n_q, k);
   if (rc) return rc;
-  HIP_TRY(launch_pack_keys(ix->out_doc.as<uint32_t>(), ix->out_score.as<float>(), ix->out_n.as<uint32_t>(), n_q, k,
+  HIP_TRY(launch_pack_keys(ix->res_doc, ix->res_score, ix->res_n, n_q, k,
                            doc_base, static_cast<uint64_t *>(d_keys), s));
   HIP_TRY(hipStreamSynchronize(s));
   ix->last_ms_scoring = ev_ms(ix, EV_Q0, EV_Q1);
