@@ -151,7 +151,7 @@ __device__ inline void csr_put(const BuildParams &p, uint64_t idx, uint32_t slot
     const uint32_t at = atomicAdd(p.esc_count, 1u);
     if (at < p.esc_cap) p.csr_esc[at] = (idx << 24) | (tf > kMaxTf ? kMaxTf : tf);
   }
-  p.csr[idx] = csr_local(slot, p.range_shift) | (f << p.range_shift);
+  __builtin_nontemporal_store(csr_local(slot, p.range_shift) | (f << p.range_shift), p.csr + idx);   // read by the next kernel
 }
 #endif
 
