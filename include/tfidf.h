@@ -103,6 +103,8 @@ typedef struct tfidf_index_stats {
                              hash collision was detected and the build redone (term identity stays
                              exact: every merge under a hashed key compares the strings) */
   uint64_t hash_rebuilds; /* builds redone in the last commit because of a hash collision */
+  uint64_t coalesced_batches;  /* tfidf_search_coalesced: batches run / queries served (index lifetime) */
+  uint64_t coalesced_queries;
 } tfidf_index_stats;
 
 /* Per-phase device times of the last commit, measured with HIP events on the
@@ -161,6 +163,13 @@ int tfidf_search(tfidf_index *ix, const uint8_t *q, uint64_t q_len, uint32_t k, 
                  float *scores, uint64_t cap, uint64_t *n_out);
 /* n_q queries; query i = q_utf8[q_offsets[i] .. q_offsets[i+1]).  1 <= k <= 1024.
  * Outputs are n_q x k (row i holds counts[i] valid hits). */
+/* Concurrent single top-k searches (Worker.processDocuments on concurrent
+ * request threads, Worker.java:175-186): same arguments and results as
+ * tfidf_search with 1 <= k <= 1024, but callers arriving together are served
+ * by ONE batched scoring launch (the first waits wait_us for companions).
+ * Thread-safe; a caller blocks until its own results are written. */
+int tfidf_search_coalesced(tfidf_index *ix, const uint8_t *q, uint64_t q_len, uint32_t k, uint32_t *doc_ids,
+                           float *scores, uint64_t cap, uint64_t *n_out, uint32_t wait_us);
 int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const uint64_t *q_offsets, uint32_t n_q,
                        uint32_t k, uint32_t *doc_ids, float *scores, uint32_t *counts);
 /* Per-query device time of the last search call (HIP events, index stream). */

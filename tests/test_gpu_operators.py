@@ -117,3 +117,47 @@ def test_zipf_operator_batch_mixed(zipf):
     qs = [x for pair in zip(plain, ops) for x in pair]
     for k in (10, 100):
         batch_equal(g, o, qs, k)
+
+
+def test_concurrent_searches_coalesce_into_batches():
+    """Concurrent single searches from many threads (the reference's request
+    threads, Worker.java:175-186) share batched scoring launches and each get
+    exactly tfidf_search's answer, including syntax errors."""
+    import threading
+    texts = synth.corpus(6000, V=3000, len_min=10, len_max=120)
+    g = ShardIndex()
+    g.add_documents(texts)
+    g.commit()
+    qs = synth.queries(400, lo=1, hi=2500) + [b"alpha AND beta", b"fast AND", b"aaaa NOT aaab"]
+    want = {}
+    for q in qs:
+        try:
+            want[q] = g.search(q, 10)
+        except QuerySyntaxError:
+            want[q] = "syntax"
+    got, errs = {}, []
+
+    def worker(part):
+        for q in part:
+            try:
+                got[q] = g.search_coalesced(q, 10, wait_us=200)
+            except QuerySyntaxError:
+                got[q] = "syntax"
+            except Exception as e:                      # noqa: BLE001
+                errs.append(e)
+
+    ths = [threading.Thread(target=worker, args=(qs[i::16],)) for i in range(16)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    assert not errs
+    for q in qs:
+        if want[q] == "syntax":
+            assert got[q] == "syntax", q
+        else:
+            assert_hits_equal(got[q], want[q])
+    st = g.stats()
+    assert st["coalesced_queries"] == len(qs)
+    assert st["coalesced_batches"] < len(qs)             # some searches shared a launch
+    g.close()

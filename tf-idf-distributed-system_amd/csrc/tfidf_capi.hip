@@ -11,6 +11,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -172,6 +174,12 @@ struct tfidf_index {
   uint64_t hash_seed = 0;              // KeyBuilder seed of the committed index (0 unless a collision was met)
   uint32_t hash_rebuilds = 0;          // builds redone for a hash collision in the last commit
   uint32_t collision_doc = 0;          // a document of the last detected collision (diagnostics)
+  // tfidf_search_coalesced: concurrent single top-k searches gathered into batches
+  mutable std::mutex cq_mu;
+  std::condition_variable cq_cv;
+  std::vector<struct CoalesceReq *> cq;
+  bool cq_leader = false;
+  uint64_t cq_batches = 0, cq_queries = 0;
   DevBuf verify_defer, lt_pos;
   std::unordered_map<uint32_t, std::string> term_cache;   // hashed slots' term strings (slot_term)
   uint32_t pack_docs = 1;              // documents per wave window in the last commit
@@ -1150,6 +1158,11 @@ extern "C" int tfidf_stats(const tfidf_index *ix, tfidf_index_stats *out) {
   out->malformed_docs = ix->committed ? ix->malformed.size() : 0;
   out->hash_seed = ix->hash_seed;
   out->hash_rebuilds = ix->hash_rebuilds;
+  {
+    std::lock_guard<std::mutex> cl(ix->cq_mu);
+    out->coalesced_batches = ix->cq_batches;
+    out->coalesced_queries = ix->cq_queries;
+  }
   const DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->dict, &ix->csr, &ix->csr_esc, &ix->doc_len,
                           &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->blk, &ix->bbase, &ix->post,
                           &ix->toff, &ix->tdf};
@@ -1472,6 +1485,98 @@ extern "C" int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const 
   HIP_TRY(hipStreamSynchronize(s));
   ix->last_ms_scoring = ev_ms(ix, EV_Q0, EV_Q1);
   ix->last_ms_total = ev_ms(ix, EV_Q0, EV_Q2);
+  return TFIDF_OK;
+}
+
+// Concurrent single searches (the reference's Worker.processDocuments runs on
+// concurrent request threads, Worker.java:175-186).  Requests queue up; the
+// first caller to find no batch forming leads one: it waits wait_us for
+// companions, takes every queued request (up to kCoalesceMax), runs them
+// through the batched scorer (tfidf_search_batch: one launch for all) and
+// hands each caller its own top-k; callers arriving meanwhile form the next
+// batch.  Results are those of tfidf_search(k) for each query, including its
+// errors (a query that does not parse gets TFIDF_E_QUERY_SYNTAX, not []).
+struct CoalesceReq {
+  const uint8_t *q;
+  uint64_t len;
+  uint32_t k;
+  uint32_t *docs;
+  float *scores;
+  uint64_t cap;
+  uint64_t *n_out;
+  int rc;
+  std::string err;
+  bool done;
+};
+constexpr size_t kCoalesceMax = 8192;
+
+extern "C" int tfidf_search_coalesced(tfidf_index *ix, const uint8_t *q, uint64_t q_len, uint32_t k, uint32_t *doc_ids,
+                                      float *scores, uint64_t cap, uint64_t *n_out, uint32_t wait_us) {
+  if (!ix || (!q && q_len) || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  if (k == 0 || k > 1024) return fail(TFIDF_E_INVALID_ARG, "coalesced search needs 1 <= k <= 1024 (all hits: tfidf_search)");
+  CoalesceReq r{q, q_len, k, doc_ids, scores, cap, n_out, TFIDF_OK, std::string(), false};
+  std::unique_lock<std::mutex> lk(ix->cq_mu);
+  ix->cq.push_back(&r);
+  if (ix->cq_leader) {                                    // a batch is forming: ours will be served
+    ix->cq_cv.wait(lk, [&] { return r.done; });
+    if (r.rc != TFIDF_OK) return fail(r.rc, "%s", r.err.c_str());
+    return TFIDF_OK;
+  }
+  ix->cq_leader = true;
+  lk.unlock();
+  if (wait_us) std::this_thread::sleep_for(std::chrono::microseconds(wait_us));
+  lk.lock();
+  const size_t take = std::min(ix->cq.size(), kCoalesceMax);
+  std::vector<CoalesceReq *> batch(ix->cq.begin(), ix->cq.begin() + take);
+  ix->cq.erase(ix->cq.begin(), ix->cq.begin() + take);
+  ix->cq_leader = false;                                  // later arrivals lead the next batch
+  if (!ix->cq.empty()) ix->cq_cv.notify_all();
+  lk.unlock();
+  // queries that do not parse answer as tfidf_search would; the rest go in one batch
+  std::vector<CoalesceReq *> run;
+  std::vector<uint8_t> text;
+  std::vector<uint64_t> offs{0};
+  uint32_t kmax = 0;
+  for (CoalesceReq *c : batch) {
+    QueryPlan plan;
+    const int prc = parse_query(c->q, c->len, &plan);
+    if (prc == kQBadUtf8 || prc == kQSyntax) {
+      c->rc = prc == kQBadUtf8 ? TFIDF_E_UNSUPPORTED_QUERY : TFIDF_E_QUERY_SYNTAX;
+      c->err = prc == kQBadUtf8 ? "query is not valid UTF-8"
+                                : "query does not parse (QueryParser ParseException / TooManyClauses)";
+      *c->n_out = 0;
+      continue;
+    }
+    run.push_back(c);
+    text.insert(text.end(), c->q, c->q + c->len);
+    offs.push_back(text.size());
+    kmax = std::max(kmax, c->k);
+  }
+  int rc = TFIDF_OK;
+  std::string err;
+  if (!run.empty()) {
+    std::vector<uint32_t> docs((size_t)run.size() * kmax), counts(run.size());
+    std::vector<float> sc((size_t)run.size() * kmax);
+    rc = tfidf_search_batch(ix, text.data(), offs.data(), (uint32_t)run.size(), kmax, docs.data(), sc.data(),
+                            counts.data());
+    if (rc != TFIDF_OK) err = tfidf_last_error();
+    for (size_t i = 0; i < run.size(); i++) {
+      CoalesceReq *c = run[i];
+      if (rc != TFIDF_OK) { c->rc = rc; c->err = err; *c->n_out = 0; continue; }
+      const uint64_t n = std::min<uint64_t>(counts[i], c->k);     // a prefix of the kmax list = the top-k
+      *c->n_out = n;
+      if (n > c->cap) { c->rc = TFIDF_E_BUFFER; c->err = "result buffer too small"; continue; }
+      memcpy(c->docs, docs.data() + i * kmax, n * 4);
+      memcpy(c->scores, sc.data() + i * kmax, n * 4);
+    }
+  }
+  lk.lock();
+  ix->cq_batches++;
+  ix->cq_queries += batch.size();
+  for (CoalesceReq *c : batch) c->done = true;
+  ix->cq_cv.notify_all();
+  lk.unlock();
+  if (r.rc != TFIDF_OK) return fail(r.rc, "%s", r.err.c_str());
   return TFIDF_OK;
 }
 

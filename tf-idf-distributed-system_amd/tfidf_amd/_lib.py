@@ -42,7 +42,8 @@ class IndexStats(C.Structure):
     _fields_ = [(n, C.c_uint64) for n in ("num_docs", "doc_count", "sum_ttf", "num_terms", "nnz",
                                           "device_bytes", "long_docs", "text_bytes", "term_major",
                                           "pack_docs", "pack_retried", "unicode_docs", "long_chunked",
-                                          "malformed_docs", "hash_seed", "hash_rebuilds")]
+                                          "malformed_docs", "hash_seed", "hash_rebuilds",
+                                          "coalesced_batches", "coalesced_queries")]
 
 
 class CommitTiming(C.Structure):
@@ -91,6 +92,8 @@ SIGNATURES = {
     "tfidf_get_commit_timing": (C.c_int, [VP, C.POINTER(CommitTiming)]),
     "tfidf_stats": (C.c_int, [VP, C.POINTER(IndexStats)]),
     "tfidf_search": (C.c_int, [VP, C.c_char_p, C.c_uint64, C.c_uint32, U32P, F32P, C.c_uint64, U64P]),
+    "tfidf_search_coalesced": (C.c_int, [VP, C.c_char_p, C.c_uint64, C.c_uint32, U32P, F32P, C.c_uint64, U64P,
+                                         C.c_uint32]),
     "tfidf_search_batch": (C.c_int, [VP, C.c_char_p, U64P, C.c_uint32, C.c_uint32, U32P, F32P, U32P]),
     "tfidf_last_search_ms": (C.c_int, [VP, F32P, F32P]),
     "tfidf_search_batch_keys_device": (C.c_int, [VP, C.c_char_p, U64P, C.c_uint32, C.c_uint32, C.c_uint64, VP]),

@@ -128,6 +128,17 @@ class ShardIndex:
         m = n.value
         return list(zip(docs[:m].tolist(), scores[:m].tolist()))
 
+    def search_coalesced(self, query: bytes, k, wait_us=50):
+        """Thread-safe top-k search that shares one batched scoring launch with
+        the searches other threads issue at the same time (tfidf_search_coalesced)."""
+        docs = np.zeros(k, np.uint32)
+        scores = np.zeros(k, np.float32)
+        n = C.c_uint64()
+        L.check(L.load().tfidf_search_coalesced(self._h, query, len(query), k, L.ptr(docs, C.c_uint32),
+                                                L.ptr(scores, C.c_float), k, C.byref(n), wait_us))
+        m = n.value
+        return list(zip(docs[:m].tolist(), scores[:m].tolist()))
+
     def search_all_arrays(self, query: bytes):
         """All hits as (doc uint32[], score float32[]) in (score desc, doc asc)
         — searcher.search(q, Integer.MAX_VALUE) without per-hit Python objects."""

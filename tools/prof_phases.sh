@@ -19,11 +19,15 @@ python3 - $O $DOCS $STOPS <<'PY'
 import csv, collections, glob, sys
 O, N = sys.argv[1], int(sys.argv[2]); stops = sys.argv[3:]
 def agg(s):
+    # per launch: bench.py runs the build more than once (timed step + the
+    # end-to-end leg), so each counter is averaged over the dispatches
     d = collections.defaultdict(float)
+    n = collections.defaultdict(set)
     for f in glob.glob("%s/s%sg*/*counter_collection.csv" % (O, s)):
         for r in csv.DictReader(open(f)):
             d[r["Counter_Name"]] += float(r["Counter_Value"])
-    return d
+            n[r["Counter_Name"]].add(r["Dispatch_Id"])
+    return {k: v / max(len(n[k]), 1) for k, v in d.items()}
 A = [agg(s) for s in stops]
 keys = sorted(set().union(*[set(a) for a in A]))
 print("%-24s" % "per doc" + "".join("%14s" % ("stop%s" % s) for s in stops) + "   deltas")
