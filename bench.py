@@ -179,13 +179,21 @@ def main():
     idx.add_documents_device(corpus.d_text, corpus.d_offsets, n_docs, corpus.total_bytes)
     adapter = D.HipShardAdapter(idx, dev, doc_base=doc_base) if world > 1 else None
 
+    exch = [0.0]
+
     def step():
-        idx.commit()
+        idx.commit()                     # returns with the build complete (its stream synced)
         if world > 1:
+            # GLOBAL statistics: term-ownership all-to-alls + stats all-gather
+            # (timed on the host: the commit is already complete here)
+            t1 = time.perf_counter()
             D.global_commit(adapter)
+            torch.cuda.synchronize()
+            exch[0] += time.perf_counter() - t1
 
     for _ in range(args.warmup):
         step()
+    exch[0] = 0.0
     phases = {k: 0.0 for k in ("ms_tokenize", "ms_long", "ms_df", "ms_blockscan", "ms_colscan", "ms_scatter",
                                 "ms_total")}
     barrier()
@@ -278,6 +286,8 @@ def main():
         "phases_alg_GBs": phase_gbs,
         "index_build_alg_bytes": b_index,
         "index_build_GBs_end_to_end": b_index / (elapsed / args.steps) / 1e9,
+        "global_exchange_ms_per_step": exch[0] * 1e3 / args.steps if world > 1 else None,
+        "global_exchange_frac_of_step": (exch[0] / elapsed) if world > 1 else None,
         "long_docs": st["long_docs"],
         "unicode_docs": n_unicode,
         "tokenizer_docs_per_window": st["pack_docs"],

@@ -1785,7 +1785,8 @@ __device__ __forceinline__ bool tile_of(uint32_t w, uint32_t n_blocks, uint32_t 
 static uint32_t tiles_grid(uint32_t n_blocks, uint32_t R) { return (n_blocks + 7) / 8 * 8 * R; }
 
 // one workgroup (1024 threads) per (block, range) tile (tile_of), LDS
-// histogram of the range's slots.  Wave w handles documents d0 + w + 16
+// histogram of the range's slots (128 KiB; 16-bit counters, two tiles per CU,
+// measured 0.50 -> 0.52 ms).  Wave w handles documents d0 + w + 16
 // (kInvDocs i + j), j < kInvDocs.
 __global__ void __launch_bounds__(1024) k_df_partial(PostingParams p) {
   extern __shared__ uint32_t hist[];
@@ -2060,10 +2061,10 @@ __device__ uint32_t csr_tf_of(const PostingParams &p, uint64_t d, uint32_t r, ui
   return 0;
 }
 
-// grid (n_blocks, n_ranges, streams per range / sort_spw), 1024 threads; a
-// workgroup takes sort_spw streams in turn (8: 3.11 -> 2.87 ms per cfg-2
-// inversion against one stream per workgroup), so few streams per CU are
-// open at a time and the regions being written stay L2-resident
+// grid (n_blocks, n_ranges, streams per range / sort_spw), 512 threads; a
+// workgroup takes sort_spw = 4 streams in turn, so few streams per CU are open
+// at a time and the regions being written stay L2-resident (cfg-2 inversion:
+// one stream per 1024-thread workgroup 3.11 ms, 8 per 1024 2.87, 4 per 512 2.52)
 __global__ void __launch_bounds__(1024) k_scatter_sort(PostingParams p) {
   __shared__ uint32_t cur[kSubSlots + 1];                   // + no-op cursor for idle lanes
   const uint32_t b = blockIdx.x, r = blockIdx.y;
@@ -2202,7 +2203,12 @@ hipError_t launch_scatter(const PostingParams &p, hipStream_t s) {
   if (e != hipSuccess) return e;
   const uint32_t RS = 1u << p.range_shift;
   const uint32_t nsub = RS > kSubSlots ? RS / kSubSlots : 1u;
-  hipLaunchKernelGGL(k_scatter_sort, dim3(p.n_blocks, p.n_ranges, (nsub + p.sort_spw - 1) / p.sort_spw), dim3(1024),
+  static const uint32_t threads = [] {
+    const char *e = getenv("TFIDF_SORT_THREADS");                 // A/B only
+    const int t = e ? atoi(e) : 512;                             // 512: 2.89 -> 2.52 ms (cfg 2)
+    return (uint32_t)(t == 256 || t == 512 ? t : 1024);
+  }();
+  hipLaunchKernelGGL(k_scatter_sort, dim3(p.n_blocks, p.n_ranges, (nsub + p.sort_spw - 1) / p.sort_spw), dim3(threads),
                      0, s, p);
   return hipGetLastError();
 }

@@ -1005,7 +1005,7 @@ static int commit_once(tfidf_index *ix) {
   pp.post_esc = ix->post_esc.as<uint64_t>();
   pp.post_esc_count = reinterpret_cast<uint32_t *>(ctr + 10);
   pp.post_esc_cap = post_esc_cap;
-  pp.sort_spw = 8;
+  pp.sort_spw = 4;
   if (const char *e = getenv("TFIDF_SORT_SPW")) pp.sort_spw = (uint32_t)std::max(1, atoi(e));   // A/B only
   pp.err = bp.err;
   HIP_TRY(hipEventRecord(ix->ev[EV_D0], s));
