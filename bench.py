@@ -93,6 +93,27 @@ def cpu_baseline(corpus, args, n_docs):
         hits = o.search(q, 0)
         json.dumps([{"document": {"name": o.doc_key(d).decode()}, "score": float(sc)} for d, sc in hits])
     t_all = time.perf_counter() - t0
+    # the GPU engine on the SAME sample and queries (comparable query rates)
+    from tfidf_amd.engine import ShardIndex
+    g = ShardIndex()
+    g.add_documents([raw[int(offs[i]):int(offs[i + 1])] for i in range(n)], [str(i).encode() for i in range(n)])
+    g.commit()
+    g.search(qs[0], 10)
+    t0 = time.perf_counter()
+    for q in qs:
+        g.search(q, 10)
+    g_q = time.perf_counter() - t0
+    blob, koffs = g.doc_keys()                   # every name once (the index's stored field)
+    blob = bytes(blob)
+    t0 = time.perf_counter()
+    for q in qs[:10]:
+        docs, scs = g.search_all_arrays(q)
+        ko = koffs[docs.astype(np.int64)]
+        ke = koffs[docs.astype(np.int64) + 1]
+        json.dumps([{"document": {"name": blob[a:b].decode()}, "score": float(sc)}
+                    for a, b, sc in zip(ko.tolist(), ke.tolist(), scs.tolist())])
+    g_all = time.perf_counter() - t0
+    g.close()
     multi = []
     if T > 1:
         th = [threading.Thread(target=build, args=(j * n, (j + 1) * n, multi)) for j in range(T)]
@@ -111,7 +132,12 @@ def cpu_baseline(corpus, args, n_docs):
            "seconds": t_idx, "queries_per_sec_top10": len(qs) / t_q,
            "queries_per_sec_all_hits_materialised": 10 / t_all,
            "queries_sample": "cfg-2 queries over the %d-doc sample (all hits: + doc key lookup + JSON, "
-                             "as Worker.searchIndex)" % n}
+                             "as Worker.searchIndex)" % n,
+           "gpu_same_sample": {"queries_per_sec_top10": len(qs) / g_q,
+                               "queries_per_sec_all_hits_materialised": 10 / g_all,
+                               "note": "libtfidf on the same sample and queries, through the C ABI from Python"},
+           "host_cpus": os.cpu_count(),
+           "host_cpus_usable": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
     if T > 1:
         out["all_cores"] = {"value": T * n / t_multi, "unit": "docs/s", "threads": T, "seconds": t_multi,
                             "sample": "%d threads, each indexing its own %d-doc shard" % (T, n)}

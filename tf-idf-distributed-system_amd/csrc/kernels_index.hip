@@ -2198,7 +2198,12 @@ hipError_t launch_block_base(const PostingParams &p, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t launch_scatter(const PostingParams &p, hipStream_t s) {
-  hipLaunchKernelGGL(k_scatter_part, dim3(tiles_grid(p.n_blocks, p.n_ranges)), dim3(1024), 0, s, p);
+  static const uint32_t pthreads = [] {
+    const char *e = getenv("TFIDF_PART_THREADS");                 // A/B only
+    const int t = e ? atoi(e) : 1024;
+    return (uint32_t)(t == 256 || t == 512 ? t : 1024);
+  }();
+  hipLaunchKernelGGL(k_scatter_part, dim3(tiles_grid(p.n_blocks, p.n_ranges)), dim3(pthreads), 0, s, p);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   const uint32_t RS = 1u << p.range_shift;
