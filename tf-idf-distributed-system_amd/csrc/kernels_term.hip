@@ -3,39 +3,168 @@
 // The block-major inversion (kernels_index.hip) keeps a dense per-block count
 // table of (N / 8192 + 1) x C words.  With SURVEY §8 cfg 5 (5 M-term vocabulary,
 // millions of short documents per GPU) that table alone would be tens of GB, so
-// above a size threshold the index is inverted term-major instead:
+// above a size threshold the index is inverted term-major instead: postings
+// sorted by (term, doc).  The input rows are already in document order, so the
+// inversion is a STABLE sort of the (doc, term) entries by term.  Hand-written
+// here as an LSD radix sort over one packed 64-bit word per entry:
 //
-//   1. (slot, posting) pairs: every CSR entry becomes key = slot (u32),
-//      value = doc | (tf << 8 | norm) << 32 (the block-major posting word),
-//      written at the document's compact row offset (exclusive sum of
-//      distinct-term counts), i.e. in document order;
-//   2. stable radix sort on the log2(C) slot bits only (rocPRIM onesweep):
-//      documents stay ascending within each term, so the sorted values ARE
-//      the postings;
-//   3. term bounds: toff[s] = first posting of slot s (C + 1 entries, one
-//      binary search per slot), df[s] = toff[s + 1] - toff[s].
-// The scoring kernels only differ from the block-major case in how they find
-// a (doc block, term) segment (a wave-parallel search of the term's
-// doc-sorted list, kernels_query.hip).
+//   key = slot | doc | min(tf, esc) | norm, fields from the top: log2 C slot
+//         bits, ceil(log2 N) doc bits, the rest less 8 for tf, the norm byte
+//         (cfg-5 shape: 23 | 23 | 10 | 8; at most 26 | 26 | 4 | 8)
+//
+//   1. row offsets: exclusive scan of the documents' distinct-term counts;
+//   2. k_term_pairs: one wave per document writes its row's packed words at
+//      its row offset (document order); a tf the field cannot hold goes to an
+//      escape list of (slot << 26 | doc, tf) pairs;
+//   3. per 8-bit digit of the slot bits, low digit first:
+//        k_rs_hist    per tile of 4096 words, the digit histogram (LDS),
+//                     stored digit-major: hist[digit][tile];
+//        scan         exclusive scan of hist -> each (digit, tile) run's
+//                     output start (digit-major order = stable order);
+//        k_rs_scatter per tile: stable rank of every word among the tile's
+//                     words of its digit (16 rounds of 256 words in input
+//                     order; inside a round, wave match masks + per-wave
+//                     digit counts), words placed in LDS in digit order, then
+//                     written out digit run by digit run (coalesced); the
+//                     LAST pass writes the postings doc | (tf << 8 | norm)
+//                     << 32 instead, and adds each (tile, term) run's length
+//                     to df[term] (two atomics per run);
+//   4. toff = exclusive scan of df.
+//
+// Bytes per posting: 12 (pairs) + 3 passes x (8 hist + 16 scatter) for
+// 2^17..2^24-slot dictionaries (rocPRIM's pair sort: 12 B key + value words
+// per pass, plus pairs, copy and bounds: ~100 B).
 //
 // The result is what Lucene's postings hold for the field (per term, docs in
 // ascending order with freq and the doc's norm byte) — reference: inversion
 // inside IndexWriter.updateDocument, J/worker/Worker.java:218; read back by
 // searcher.search at :230.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include "tfidf_common.h"
 #include "tfidf_internal.h"
+#include "wave_ops.h"
 
 namespace tfidf {
 
+constexpr uint32_t kTermDocBits = 26;                   // escape-list key: slot << 26 | doc
+constexpr uint32_t kRsThreads = 256;
+constexpr uint32_t kRsItems = 16;                       // words per thread per tile
+constexpr uint32_t kRsTile = kRsThreads * kRsItems;     // 4096
+constexpr uint32_t kRsWaves = kRsThreads / 64;
+
+// ---------------------------------------------------------------------------
+// exclusive scan of u32 (n <= 2^32 - 1 total): per-block sums, one-block scan
+// of the block sums, then the block-local scans plus bases.
+constexpr uint32_t kScanThreads = 1024, kScanItems = 16, kScanBlock = kScanThreads * kScanItems;
+
+__device__ __forceinline__ uint32_t block_incl_scan(uint32_t x, uint32_t *wsum, uint32_t *total) {
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  if (lane == 63) wsum[wid] = x;
+  __syncthreads();
+  uint32_t base = 0, all = 0;
+  for (uint32_t w = 0; w < nw; w++) {
+    const uint32_t v = wsum[w];
+    if (w < wid) base += v;
+    all += v;
+  }
+  __syncthreads();
+  *total = all;
+  return base + x;
+}
+
+__global__ void __launch_bounds__(kScanThreads) k_scan_sums(const uint32_t *in, uint64_t n, uint32_t *sums) {
+  __shared__ uint32_t wsum[16];
+  const uint64_t b0 = (uint64_t)blockIdx.x * kScanBlock;
+  uint32_t s = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kScanItems; j++) {
+    const uint64_t i = b0 + (uint64_t)j * kScanThreads + threadIdx.x;
+    s += i < n ? in[i] : 0u;
+  }
+  uint32_t tot;
+  block_incl_scan(s, wsum, &tot);
+  if (threadIdx.x == 0) sums[blockIdx.x] = tot;
+}
+
+// one workgroup: exclusive scan of nb block sums in place (nb <= 2^20)
+__global__ void __launch_bounds__(kScanThreads) k_scan_top(uint32_t *sums, uint32_t nb) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  for (uint32_t c0 = 0; c0 < nb; c0 += kScanThreads) {
+    const uint32_t i = c0 + threadIdx.x;
+    const uint32_t v = i < nb ? sums[i] : 0u;
+    uint32_t tot;
+    const uint32_t incl = block_incl_scan(v, wsum, &tot);
+    const uint32_t base = carry;
+    if (i < nb) sums[i] = base + incl - v;
+    __syncthreads();
+    if (threadIdx.x == 0) carry = base + tot;
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(kScanThreads) k_scan_final(const uint32_t *in, uint64_t n, const uint32_t *sums,
+                                                             uint32_t *out) {
+  __shared__ uint32_t wsum[16];
+  const uint64_t b0 = (uint64_t)blockIdx.x * kScanBlock;
+  // thread t scans its kScanItems consecutive words (one strided pass of the
+  // block's words per item index keeps the loads coalesced)
+  uint32_t v[kScanItems], s = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kScanItems; j++) {
+    const uint64_t i = b0 + (uint64_t)threadIdx.x * kScanItems + j;
+    v[j] = i < n ? in[i] : 0u;
+    s += v[j];
+  }
+  uint32_t tot;
+  uint32_t run = sums[blockIdx.x] + block_incl_scan(s, wsum, &tot) - s;
+#pragma unroll
+  for (uint32_t j = 0; j < kScanItems; j++) {
+    const uint64_t i = b0 + (uint64_t)threadIdx.x * kScanItems + j;
+    if (i < n) out[i] = run;
+    run += v[j];
+  }
+}
+
+// scratch: ceil(n / kScanBlock) words
+static hipError_t scan_u32_excl(const uint32_t *in, uint32_t *out, uint64_t n, uint32_t *scratch, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const uint32_t nb = (uint32_t)((n + kScanBlock - 1) / kScanBlock);
+  hipLaunchKernelGGL(k_scan_sums, dim3(nb), dim3(kScanThreads), 0, s, in, n, scratch);
+  hipLaunchKernelGGL(k_scan_top, dim3(1), dim3(kScanThreads), 0, s, scratch, nb);
+  hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(kScanThreads), 0, s, in, n, scratch, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Packed word fields (TermParams.doc_bits / tf_bits, slot_bits = log2 C)
+struct TermLayout {
+  uint32_t sb, db, tb;                 // slot, doc, tf bits; norm = 8
+  __host__ __device__ uint32_t slot_shift() const { return 64 - sb; }
+  __host__ __device__ uint32_t doc_shift() const { return 8 + tb; }
+  __host__ __device__ uint32_t tf_esc() const { return (1u << tb) - 1; }
+  __host__ __device__ uint64_t pack(uint32_t slot, uint64_t doc, uint32_t tf, uint32_t norm) const {
+    return ((uint64_t)slot << slot_shift()) | (doc << doc_shift()) | ((uint64_t)(tf < tf_esc() ? tf : tf_esc()) << 8) |
+           norm;
+  }
+};
+
 // One wave per document (grid-stride): the row is contiguous, so lanes write
-// consecutive pair slots.
+// consecutive words.
 __global__ void __launch_bounds__(256) k_term_pairs(TermParams p) {
   const uint32_t lane = threadIdx.x & 63;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  const uint32_t esc = csr_esc_value(p.slot_bits);
+  const TermLayout ly{p.slot_bits, p.doc_bits, p.tf_bits};
   for (uint64_t d = wave; d < p.n_docs; d += nw) {
     const uint64_t src = p.live_map ? p.live_map[d] : d;
     const uint64_t base = csr_row_base(p.offsets, src);
@@ -43,68 +172,198 @@ __global__ void __launch_bounds__(256) k_term_pairs(TermParams p) {
     for (uint32_t j = lane; j < n; j += 64) {
       const uint32_t e = p.csr[base + j], c = csr_local(e, p.slot_bits);
       uint32_t t = csr_tf_field(e, p.slot_bits);
-      if (t == csr_esc_value(p.slot_bits)) t = csr_esc_tf(p.csr_esc, p.n_esc, base + j);
-      if (t >= (1u << 24)) atomicOr(p.err, kErrTfTooLarge);
-      p.keys[o + j] = c;
-      p.vals[o + j] = d | ((uint64_t)((t << 8) | nrm) << 32);
+      if (t == esc) t = csr_esc_tf(p.csr_esc, p.n_esc, base + j);
+      if (t > kMaxTf) atomicOr(p.err, kErrTfTooLarge);
+      if (t >= ly.tf_esc()) {                                  // rare: exact tf kept aside, keyed (slot, doc)
+        const uint32_t at = atomicAdd(p.tesc_count, 1u);
+        if (at < p.tesc_cap) {                                 // (slot << 26 | doc, tf) pairs
+          p.tesc[2 * (uint64_t)at] = ((uint64_t)c << kTermDocBits) | d;
+          p.tesc[2 * (uint64_t)at + 1] = min(t, kMaxTf);
+        }
+      }
+      p.keys[o + j] = ly.pack(c, d, t, nrm);
     }
   }
 }
 
-// toff[s] = first index i with key[i] >= s, for s in [0, C]: one thread per
-// slot, binary search of the sorted keys (empty slots cost the same as full
-// ones, so sparse tables over a huge C stay parallel).
-__global__ void k_term_bounds(const uint32_t *keys, uint64_t nnz, uint32_t C, uint64_t *toff) {
-  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s > C) return;
-  uint64_t a = 0, z = nnz;
-  while (a < z) {
-    const uint64_t m = (a + z) >> 1;
-    if (keys[m] < s) a = m + 1; else z = m;
+// ---------------------------------------------------------------------------
+// LSD radix passes (8-bit digits of the key bits from `shift`)
+
+__device__ __forceinline__ uint32_t rs_digit(uint64_t k, uint32_t shift, uint32_t mask) {
+  return (uint32_t)(k >> shift) & mask;
+}
+
+// per tile: digit histogram -> hist[digit * n_tiles + tile]
+__global__ void __launch_bounds__(kRsThreads) k_rs_hist(const uint64_t *keys, uint64_t n, uint32_t shift, uint32_t mask,
+                                                        uint32_t n_tiles, uint32_t *hist) {
+  __shared__ uint32_t h[256];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t t0 = (uint64_t)blockIdx.x * kRsTile;
+#pragma unroll
+  for (uint32_t j = 0; j < kRsItems; j++) {
+    const uint64_t i = t0 + (uint64_t)j * kRsThreads + threadIdx.x;
+    if (i < n) atomicAdd(&h[rs_digit(keys[i], shift, mask)], 1u);
   }
-  toff[s] = a;
+  __syncthreads();
+  hist[(uint64_t)threadIdx.x * n_tiles + blockIdx.x] = h[threadIdx.x];
 }
 
-__global__ void k_term_df(const uint64_t *toff, uint32_t C, uint32_t *df) {
-  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s < C) df[s] = (uint32_t)(toff[s + 1] - toff[s]);
-}
+// Per tile: stable rank of each word among the tile's words of its digit.
+// Input order inside the tile is i = 256 j + t (round j, thread t); a round's
+// words are ranked by wave match masks (lanes below with the same digit) plus
+// the per-digit counts of the round's lower waves plus the counts of earlier
+// rounds.  Words go to LDS at (digit start in the tile + rank), then out run
+// by run to hist-scanned global starts.
+struct RsSmem {
+  uint64_t k[kRsTile];
+  uint32_t start[256];                 // digit's first position in the sorted tile
+  uint32_t gpos[256];                  // digit run's global start (scanned hist)
+  uint32_t run[256];                   // words of the digit in earlier rounds
+  uint32_t wcnt[kRsWaves][256];        // words of the digit in this round, per wave
+  uint32_t wsum[kRsWaves];
+};
 
-hipError_t term_invert_tmp_bytes(uint64_t n_docs, uint64_t nnz, uint32_t key_bits, size_t *bytes) {
-  size_t a = 0, b = 0;
-  hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, a, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                                  n_docs ? n_docs : 1);
-  if (e != hipSuccess) return e;
-  hipcub::DoubleBuffer<uint32_t> k(nullptr, nullptr);
-  hipcub::DoubleBuffer<uint64_t> v(nullptr, nullptr);
-  e = hipcub::DeviceRadixSort::SortPairs(nullptr, b, k, v, nnz ? nnz : 1, 0, (int)key_bits);
-  *bytes = (a > b ? a : b) + 256;
-  return e;
-}
-
-hipError_t launch_term_invert(TermParams p, void *tmp, size_t tmp_bytes, hipStream_t s) {
-  hipError_t e;
-  if (p.n_docs == 0 || p.nnz == 0) {
-    hipLaunchKernelGGL(k_term_bounds, dim3(p.C / 256 + 1), dim3(256), 0, s, p.keys, (uint64_t)0, p.C, p.toff);
-    hipLaunchKernelGGL(k_term_df, dim3((p.C + 255) / 256), dim3(256), 0, s, p.toff, p.C, p.df);
-    return hipGetLastError();
-  }
-  e = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, p.doc_nuniq, p.row_off, p.n_docs, s);
-  if (e != hipSuccess) return e;
+// LAST: write postings (and df run lengths) instead of words.
+template <bool LAST>
+__global__ void __launch_bounds__(kRsThreads) k_rs_scatter(const uint64_t *keys, uint64_t *out, uint64_t n,
+                                                           uint32_t shift, uint32_t mask, uint32_t n_tiles,
+                                                           const uint32_t *hist, const uint32_t *gstart, TermParams p) {
+  __shared__ RsSmem sm;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const uint64_t t0 = (uint64_t)blockIdx.x * kRsTile;
+  // the tile's digit starts: exclusive scan of its histogram over digits
   {
-    const uint64_t waves = p.n_docs < (1ull << 20) ? p.n_docs : (1ull << 20);
-    hipLaunchKernelGGL(k_term_pairs, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, p);
+    const uint32_t c = hist[(uint64_t)tid * n_tiles + blockIdx.x];
+    uint32_t tot;
+    sm.start[tid] = block_incl_scan(c, sm.wsum, &tot) - c;
+    sm.gpos[tid] = gstart[(uint64_t)tid * n_tiles + blockIdx.x];
+    sm.run[tid] = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kRsWaves; w++) sm.wcnt[w][tid] = 0;
   }
-  hipcub::DoubleBuffer<uint32_t> k(p.keys, p.keys_alt);
-  hipcub::DoubleBuffer<uint64_t> v(p.vals, p.vals_alt);
-  e = hipcub::DeviceRadixSort::SortPairs(tmp, tmp_bytes, k, v, p.nnz, 0, (int)p.slot_bits, s);
+  uint64_t kv[kRsItems];
+#pragma unroll
+  for (uint32_t j = 0; j < kRsItems; j++) {
+    const uint64_t i = t0 + (uint64_t)j * kRsThreads + tid;
+    kv[j] = i < n ? keys[i] : ~0ull;
+  }
+  __syncthreads();
+  for (uint32_t j = 0; j < kRsItems; j++) {
+    const uint64_t i = t0 + (uint64_t)j * kRsThreads + tid;
+    const bool in = i < n;
+    const uint32_t d = rs_digit(kv[j], shift, mask);
+    const uint64_t peers = peer_mask<9>(in ? d : 256u) & (in ? ~0ull : 0ull);
+    const uint32_t below = (uint32_t)__popcll(peers & ((1ull << lane) - 1));
+    if (in && below == 0) sm.wcnt[wid][d] = (uint32_t)__popcll(peers);
+    __syncthreads();
+    if (in) {
+      uint32_t r = sm.run[d] + below;
+      for (uint32_t w = 0; w < wid; w++) r += sm.wcnt[w][d];
+      sm.k[sm.start[d] + r] = kv[j];
+    }
+    __syncthreads();
+    {
+      uint32_t add = 0;
+#pragma unroll
+      for (uint32_t w = 0; w < kRsWaves; w++) { add += sm.wcnt[w][tid]; sm.wcnt[w][tid] = 0; }
+      sm.run[tid] += add;
+    }
+    __syncthreads();
+  }
+  // out: sorted tile position q holds a word of digit d at global gpos[d] + (q - start[d])
+  const uint64_t cnt = n - t0 < kRsTile ? n - t0 : kRsTile;
+  const TermLayout ly{p.slot_bits, p.doc_bits, p.tf_bits};
+#pragma unroll
+  for (uint32_t j = 0; j < kRsItems; j++) {
+    const uint32_t q = j * kRsThreads + tid;
+    if (q < cnt) {
+      const uint64_t k = sm.k[q];
+      const uint32_t d = rs_digit(k, shift, mask);
+      const uint64_t g = (uint64_t)sm.gpos[d] + (q - sm.start[d]);
+      if (!LAST) {
+        out[g] = k;
+      } else {
+        // the last digit is the top of the key, so the tile is in (term, doc)
+        // order and each term's words are one run here: the run's first and
+        // last words add -first and last + 1 to df[term]
+        const uint32_t slot = (uint32_t)(k >> ly.slot_shift());
+        const uint64_t doc = (k >> ly.doc_shift()) & ((1ull << ly.db) - 1);
+        uint32_t tf = (uint32_t)(k >> 8) & ly.tf_esc();
+        if (tf == ly.tf_esc()) {                               // rare: exact tf from the escape list
+          const uint64_t key = ((uint64_t)slot << kTermDocBits) | doc;
+          uint64_t a = 0, z = p.n_tesc;
+          while (a < z) {
+            const uint64_t m = (a + z) >> 1;
+            if (p.tesc[2 * m] < key) a = m + 1; else z = m;
+          }
+          tf = (uint32_t)p.tesc[2 * a + 1];
+        }
+        out[g] = doc | ((uint64_t)((tf << 8) | (uint32_t)(k & 255u)) << 32);
+        if (q == 0 || (uint32_t)(sm.k[q - 1] >> ly.slot_shift()) != slot) atomicSub(&p.df[slot], (uint32_t)g);
+        if (q + 1 == cnt || (uint32_t)(sm.k[q + 1] >> ly.slot_shift()) != slot) atomicAdd(&p.df[slot], (uint32_t)g + 1);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+
+// toff (u64, C + 1 entries) from the exclusive scan of df (u32)
+__global__ void k_term_toff(const uint32_t *scan, uint32_t C, uint64_t nnz, uint64_t *toff) {
+  const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s < C) toff[s] = scan[s];
+  else if (s == C) toff[C] = nnz;
+}
+
+// scratch layout (u32 words): hist [256 tiles] | scanned hist [256 tiles] |
+// scan block sums | df scan [C]
+static uint64_t scan_sums_words(uint64_t n_docs, uint64_t nnz, uint32_t C) {
+  const uint64_t hist = 256 * ((nnz + kRsTile - 1) / kRsTile);
+  return (std::max<uint64_t>(std::max<uint64_t>(hist, n_docs), C) + kScanBlock - 1) / kScanBlock + 16;
+}
+uint64_t term_invert_scratch_words(uint64_t n_docs, uint64_t nnz, uint32_t C) {
+  const uint64_t hist = 256 * ((nnz + kRsTile - 1) / kRsTile);
+  return 2 * hist + scan_sums_words(n_docs, nnz, C) + C + 16;
+}
+
+hipError_t launch_term_pairs(const TermParams &p, hipStream_t s) {
+  hipError_t e = scan_u32_excl(p.doc_nuniq, p.row_off, p.n_docs, p.scratch, s);
   if (e != hipSuccess) return e;
-  if (v.Current() != p.post) {
-    e = hipMemcpyAsync(p.post, v.Current(), p.nnz * 8, hipMemcpyDeviceToDevice, s);
-    if (e != hipSuccess) return e;
+  const uint64_t waves = p.n_docs < (1ull << 20) ? p.n_docs : (1ull << 20);
+  if (waves) hipLaunchKernelGGL(k_term_pairs, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+
+// After launch_term_pairs and the host sort of the (rare) tf escape list.
+hipError_t launch_term_sort(const TermParams &p, hipStream_t s) {
+  hipError_t e = hipMemsetAsync(p.df, 0, (size_t)p.C * 4, s);
+  if (e != hipSuccess) return e;
+  const uint32_t tiles = (uint32_t)((p.nnz + kRsTile - 1) / kRsTile);
+  uint32_t *hist = p.scratch, *gstart = p.scratch + (size_t)256 * tiles, *sums = gstart + (size_t)256 * tiles;
+  uint32_t *df_scan = sums + scan_sums_words(p.n_docs, p.nnz, p.C);
+  if (p.n_docs && p.nnz) {
+    uint64_t *a = p.keys, *b = p.keys_alt;
+    for (uint32_t lo = 0; lo < p.slot_bits; lo += 8) {
+      const uint32_t bits = p.slot_bits - lo < 8 ? p.slot_bits - lo : 8;
+      const uint32_t shift = 64 - p.slot_bits + lo, mask = (1u << bits) - 1;
+      const bool last = lo + 8 >= p.slot_bits;
+      hipLaunchKernelGGL(k_rs_hist, dim3(tiles), dim3(kRsThreads), 0, s, a, p.nnz, shift, mask, tiles, hist);
+      e = scan_u32_excl(hist, gstart, (uint64_t)256 * tiles, sums, s);
+      if (e != hipSuccess) return e;
+      if (last)
+        hipLaunchKernelGGL(k_rs_scatter<true>, dim3(tiles), dim3(kRsThreads), 0, s, a, p.post, p.nnz, shift, mask,
+                           tiles, hist, gstart, p);
+      else
+        hipLaunchKernelGGL(k_rs_scatter<false>, dim3(tiles), dim3(kRsThreads), 0, s, a, b, p.nnz, shift, mask,
+                           tiles, hist, gstart, p);
+      uint64_t *t = a; a = b; b = t;
+    }
   }
-  hipLaunchKernelGGL(k_term_bounds, dim3(p.C / 256 + 1), dim3(256), 0, s, k.Current(), p.nnz, p.C, p.toff);
-  hipLaunchKernelGGL(k_term_df, dim3((p.C + 255) / 256), dim3(256), 0, s, p.toff, p.C, p.df);
+  // toff = exclusive scan of df
+  e = scan_u32_excl(p.df, df_scan, p.C, sums, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_term_toff, dim3(p.C / 256 + 1), dim3(256), 0, s, df_scan, p.C, p.nnz, p.toff);
   return hipGetLastError();
 }
 

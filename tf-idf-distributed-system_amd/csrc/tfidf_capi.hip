@@ -187,7 +187,7 @@ struct tfidf_index {
   uint64_t unicode_docs = 0;           // documents with non-ASCII text in the last commit
   // term-major inversion (large vocabularies): compact row offsets, sort values (x2), term offsets, df
   bool term_major = false;
-  DevBuf row_off, tvals, toff, tdf, term_tmp;
+  DevBuf row_off, tvals, toff, tdf, term_tmp, term_esc;
   const uint32_t *df_dev() const {
     return term_major ? tdf.as<uint32_t>() : blk.as<uint32_t>() + (size_t)n_blocks * C;
   }
@@ -293,7 +293,7 @@ extern "C" int tfidf_destroy(tfidf_index *ix) {
                     &ix->retry_list, &ix->bad_list, &ix->bbase, &ix->post, &ix->post_tmp, &ix->post_esc, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->lt_pos, &ix->verify_defer, &ix->dense, &ix->chunk_list, &ix->chunk_docs, &ix->chunk_fail, &ix->canon_of_slot,
                     &ix->q_off, &ix->q_slot, &ix->q_w, &ix->q_role, &ix->q_meta, &ix->cache, &ix->cand, &ix->cand_n, &ix->out_doc,
                     &ix->out_score, &ix->out_n, &ix->q_in, &ix->q_out, &ix->hits, &ix->hits_n, &ix->hits_c, &ix->hits_s, &ix->hits_P, &ix->sort_tmp,
-                    &ix->row_off, &ix->tvals, &ix->toff, &ix->tdf, &ix->term_tmp, &ix->sent_slot, &ix->vcounts, &ix->vnu,
+                    &ix->row_off, &ix->tvals, &ix->toff, &ix->tdf, &ix->term_tmp, &ix->term_esc, &ix->sent_slot, &ix->vcounts, &ix->vnu,
                     &ix->vt_table, &ix->vt_sum, &ix->vt_rslot, &ix->gdf_dev, &ix->ovf};
   for (DevBuf *b : bufs) b->release();
   for (int i = 0; i < EV_N; i++) hipEventDestroy(ix->ev[i]);
@@ -769,7 +769,7 @@ static int commit_once(tfidf_index *ix) {
 
   // counters: [0..2] stats u64, [3] err flags u32 + [3].hi first doc, [4] long_count, [5] retry_count,
   // [6] uni_count, [7] occupied dictionary slots, [8] bad_count, [9] CSR escape count, [10] posting
-  // escapes, [11] deferred hashed-key checks
+  // escapes, [11] deferred hashed-key checks, [12] term-major tf escapes
   uint64_t *ctr = ix->counters.as<uint64_t>();
   HIP_TRY(hipMemsetAsync(ix->counters.p, 0, 128, s));
   HIP_TRY(hipMemsetAsync(ix->dict.p, 0, (size_t)3 * C * 8, s));
@@ -1011,12 +1011,17 @@ static int commit_once(tfidf_index *ix) {
   HIP_TRY(hipEventRecord(ix->ev[EV_D0], s));
   if (ix->term_major) {
     TermParams tp{};
+    if (N > kTermMaxDocs)
+      return fail(TFIDF_E_CAPACITY, "the term-major layout holds at most 2^26 documents per shard");
     tp.offsets = bp.offsets;
     tp.live_map = bp.live_map;
     tp.n_docs = N;
     tp.nnz = ix->nnz;
     tp.C = C;
     tp.slot_bits = ix->cap_log2;
+    tp.doc_bits = 1;
+    while ((1ull << tp.doc_bits) < N) tp.doc_bits++;
+    tp.tf_bits = 56 - tp.slot_bits - tp.doc_bits;            // >= 4 (slot, doc <= 26 bits)
     tp.csr = bp.csr;
     tp.csr_esc = bp.csr_esc;
     tp.n_esc = ix->h_esc.size();
@@ -1024,22 +1029,37 @@ static int commit_once(tfidf_index *ix) {
     tp.doc_norm = bp.doc_norm;
     tp.row_off = ix->row_off.as<uint32_t>();
     HIP_TRY(ix->tvals.reserve(ix->nnz * 8 + 16));
-    tp.keys = ix->tvals.as<uint32_t>();
-    tp.keys_alt = tp.keys + ix->nnz + 1;
-    tp.vals = ix->post_tmp.as<uint64_t>();
-    tp.vals_alt = ix->post.as<uint64_t>();
+    tp.keys = ix->post_tmp.as<uint64_t>();
+    tp.keys_alt = ix->tvals.as<uint64_t>();
     tp.post = ix->post.as<uint64_t>();
     tp.toff = ix->toff.as<uint64_t>();
     tp.df = ix->tdf.as<uint32_t>();
     tp.err = bp.err;
-    size_t tb = 0;
-    HIP_TRY(term_invert_tmp_bytes(N, ix->nnz, tp.slot_bits, &tb));
-    HIP_TRY(ix->term_tmp.reserve(tb));
+    tp.tesc_cap = row_cap / ((1u << tp.tf_bits) - 1) + 64;   // each needs tf >= the escape value
+    HIP_TRY(ix->term_esc.reserve(tp.tesc_cap * 16));
+    tp.tesc = ix->term_esc.as<uint64_t>();
+    tp.tesc_count = reinterpret_cast<uint32_t *>(ctr + 12);
+    HIP_TRY(ix->term_tmp.reserve(term_invert_scratch_words(N, ix->nnz, C) * 4));
+    tp.scratch = ix->term_tmp.as<uint32_t>();
     // the whole inversion is reported under ms_scatter
     HIP_TRY(hipEventRecord(ix->ev[EV_DF], s));
     HIP_TRY(hipEventRecord(ix->ev[EV_BSCAN], s));
     HIP_TRY(hipEventRecord(ix->ev[EV_CSCAN], s));
-    HIP_TRY(launch_term_invert(tp, ix->term_tmp.p, tb, s));
+    HIP_TRY(launch_term_pairs(tp, s));
+    {   // tf >= 4095 (rare): the escape list sorted for the postings pass's binary search
+      uint32_t ne = 0;
+      HIP_TRY(hipMemcpyAsync(&ne, tp.tesc_count, 4, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipStreamSynchronize(s));
+      if (ne > tp.tesc_cap) return fail(TFIDF_E_CAPACITY, "term-major escape list overflow");
+      if (ne) {
+        std::vector<std::pair<uint64_t, uint64_t>> h(ne);
+        HIP_TRY(hipMemcpy(h.data(), tp.tesc, ne * 16, hipMemcpyDeviceToHost));
+        std::sort(h.begin(), h.end());
+        HIP_TRY(hipMemcpy(tp.tesc, h.data(), ne * 16, hipMemcpyHostToDevice));
+      }
+      tp.n_tesc = ne;
+    }
+    HIP_TRY(launch_term_sort(tp, s));
     HIP_TRY(hipEventRecord(ix->ev[EV_SCAT], s));
   } else {
     if (ix->n_blocks) {

@@ -210,25 +210,32 @@ hipError_t launch_count_nonzero(const uint64_t *a, uint32_t n, unsigned long lon
 hipError_t launch_scatter(const PostingParams &p, hipStream_t s);
 
 // --- term-major inversion for large vocabularies (kernels_term.hip) ---
+// (hand-written LSD radix sort of packed words slot | doc | tf | norm)
+constexpr uint64_t kTermMaxDocs = 1ull << 26;   // documents per shard in the term-major layout
 struct TermParams {
   const uint64_t *offsets;
   const uint32_t *live_map;
   uint64_t n_docs, nnz;
   uint32_t C, slot_bits;      // C = 2^slot_bits
+  uint32_t doc_bits, tf_bits; // packed word layout (kernels_term.hip TermLayout)
   const uint32_t *csr, *doc_nuniq;
   const uint64_t *csr_esc;
   uint64_t n_esc;
   const uint8_t *doc_norm;
   uint32_t *row_off;          // [n_docs] compact row offsets (exclusive sum of doc_nuniq)
-  uint32_t *keys, *keys_alt;  // [nnz] each: sort keys = slot (double buffer)
-  uint64_t *vals, *vals_alt;  // [nnz] each: posting words (double buffer; one of them is post)
+  uint64_t *keys, *keys_alt;  // [nnz] each: packed words (ping-pong)
+  uint64_t *tesc;             // tf >= 4095: (slot << 26 | doc, tf) u64 pairs, sorted by the host
+  uint32_t *tesc_count;
+  uint64_t tesc_cap, n_tesc;
+  uint32_t *scratch;          // term_invert_scratch_words(n_docs, nnz) u32
   uint64_t *post;             // [nnz] out: doc | (tf << 8 | norm) << 32, term-major, docs ascending
   uint64_t *toff;             // [C + 1] out: first posting of each slot
   uint32_t *df;               // [C] out
   uint32_t *err;
 };
-hipError_t term_invert_tmp_bytes(uint64_t n_docs, uint64_t nnz, uint32_t key_bits, size_t *bytes);
-hipError_t launch_term_invert(TermParams p, void *tmp, size_t tmp_bytes, hipStream_t s);
+uint64_t term_invert_scratch_words(uint64_t n_docs, uint64_t nnz, uint32_t C);
+hipError_t launch_term_pairs(const TermParams &p, hipStream_t s);
+hipError_t launch_term_sort(const TermParams &p, hipStream_t s);
 
 // --- query scoring (kernels_query.hip) ---
 struct QueryParams {
