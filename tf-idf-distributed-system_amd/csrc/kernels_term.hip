@@ -157,19 +157,22 @@ struct TermLayout {
   }
 };
 
-// One wave per document (grid-stride): the row is contiguous, so lanes write
-// consecutive words.
+// Four documents per wave (16 lanes each, grid-stride): the rows are
+// contiguous, so each lane group writes consecutive words; the four rows'
+// metadata loads are in flight together (short rows: ~57 words at cfg 5).
 __global__ void __launch_bounds__(256) k_term_pairs(TermParams p) {
-  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t lane = threadIdx.x & 63, grp = lane >> 4, sl = lane & 15;
   const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
   const uint32_t esc = csr_esc_value(p.slot_bits);
   const TermLayout ly{p.slot_bits, p.doc_bits, p.tf_bits};
-  for (uint64_t d = wave; d < p.n_docs; d += nw) {
+  for (uint64_t d0 = 4 * wave; d0 < p.n_docs; d0 += 4 * nw) {
+    const uint64_t d = d0 + grp;
+    if (d >= p.n_docs) continue;
     const uint64_t src = p.live_map ? p.live_map[d] : d;
     const uint64_t base = csr_row_base(p.offsets, src);
     const uint32_t n = p.doc_nuniq[d], o = p.row_off[d], nrm = p.doc_norm[d];
-    for (uint32_t j = lane; j < n; j += 64) {
+    for (uint32_t j = sl; j < n; j += 16) {
       const uint32_t e = p.csr[base + j], c = csr_local(e, p.slot_bits);
       uint32_t t = csr_tf_field(e, p.slot_bits);
       if (t == esc) t = csr_esc_tf(p.csr_esc, p.n_esc, base + j);
@@ -330,7 +333,7 @@ uint64_t term_invert_scratch_words(uint64_t n_docs, uint64_t nnz, uint32_t C) {
 hipError_t launch_term_pairs(const TermParams &p, hipStream_t s) {
   hipError_t e = scan_u32_excl(p.doc_nuniq, p.row_off, p.n_docs, p.scratch, s);
   if (e != hipSuccess) return e;
-  const uint64_t waves = p.n_docs < (1ull << 20) ? p.n_docs : (1ull << 20);
+  const uint64_t waves = std::min<uint64_t>((p.n_docs + 3) / 4, 1ull << 18);
   if (waves) hipLaunchKernelGGL(k_term_pairs, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, p);
   return hipGetLastError();
 }
