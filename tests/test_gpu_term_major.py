@@ -133,3 +133,33 @@ def test_term_major_empty():
     assert g.stats()["doc_count"] == 0
     assert g.search(b"anything", 0) == []
     g.close()
+
+
+@pytest.mark.parametrize("inversion", [L.INVERSION_BLOCK, L.INVERSION_TERM])
+def test_large_tf_escapes(monkeypatch, inversion):
+    """Term frequencies the packed fields cannot hold take the escape lists:
+    block-major postings hold tf < 2047 (a term 3 000 times in one document
+    escapes); the term-major sort words are squeezed to 4 tf bits here
+    (TFIDF_TEST_TERM_TF_BITS), so every tf >= 15 escapes.  Counts, DF and
+    scores must still equal the oracle's."""
+    monkeypatch.setenv("TFIDF_TEST_TERM_TF_BITS", "4")
+    rng = random.Random(5)
+    texts = []
+    for i in range(300):
+        words = [rng.choice([b"alpha", b"beta", b"gamma", b"delta", b"eps%d" % (i % 7)]) for _ in range(rng.randint(5, 60))]
+        if i % 50 == 3:
+            words += [b"alpha"] * 3000 + [b"gamma"] * 40
+        rng.shuffle(words)
+        texts.append(b" ".join(words))
+    g = build(texts, inversion)
+    o = oracle_of(texts)
+    s = g.stats()
+    assert (s["doc_count"], s["sum_ttf"], s["num_terms"], s["nnz"]) == \
+        (o.doc_count, o.sum_ttf, o.num_terms, sum(o.vocab().values()))
+    for d in range(len(texts)):
+        assert g.doc_terms(d) == o.doc_terms(d), d
+    for q in [b"alpha", b"gamma", b"alpha beta", b"eps3 gamma", b"alpha AND gamma"]:
+        assert_hits_equal(g.search(q, 0), o.search(q, 0))
+        assert_hits_equal(g.search(q, 10), o.search(q, 10))
+    g.close()
+    o.close()

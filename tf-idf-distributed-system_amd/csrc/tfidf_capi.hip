@@ -1022,6 +1022,8 @@ static int commit_once(tfidf_index *ix) {
     tp.doc_bits = 1;
     while ((1ull << tp.doc_bits) < N) tp.doc_bits++;
     tp.tf_bits = 56 - tp.slot_bits - tp.doc_bits;            // >= 4 (slot, doc <= 26 bits)
+    if (const char *e = getenv("TFIDF_TEST_TERM_TF_BITS"))      // tests: exercise the tf escape list
+      tp.tf_bits = std::max(1u, std::min(tp.tf_bits, (uint32_t)atoi(e)));
     tp.csr = bp.csr;
     tp.csr_esc = bp.csr_esc;
     tp.n_esc = ix->h_esc.size();
