@@ -166,6 +166,9 @@ def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    # multi-GPU code path (process group, GLOBAL statistics exchange) even at
+    # one rank: TFIDF_BENCH_DIST=1 rehearses the RCCL collectives on a 1-GPU box
+    dist_on = world > 1 or os.environ.get("TFIDF_BENCH_DIST") == "1"
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
@@ -174,7 +177,7 @@ def main():
     local = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if dist_on:
         backend = os.environ.get("TFIDF_BENCH_BACKEND", "nccl")   # nccl = RCCL over xGMI
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -182,7 +185,7 @@ def main():
             dist.init_process_group(backend)
 
     def barrier():
-        if world > 1:
+        if dist_on:
             dist.barrier()
 
     from tfidf_amd import STATS_GLOBAL, synth
@@ -201,15 +204,15 @@ def main():
             cap += 1
     inv = {"auto": 0, "block": 1, "term": 2}[args.inversion]
     idx = ShardIndex(device=local, vocab_capacity_log2=cap, inversion=inv,
-                     stats_mode=STATS_GLOBAL if world > 1 else 0)
+                     stats_mode=STATS_GLOBAL if dist_on else 0)
     idx.add_documents_device(corpus.d_text, corpus.d_offsets, n_docs, corpus.total_bytes)
-    adapter = D.HipShardAdapter(idx, dev, doc_base=doc_base) if world > 1 else None
+    adapter = D.HipShardAdapter(idx, dev, doc_base=doc_base) if dist_on else None
 
     exch = [0.0]
 
     def step():
         idx.commit()                     # returns with the build complete (its stream synced)
-        if world > 1:
+        if dist_on:
             # GLOBAL statistics: term-ownership all-to-alls + stats all-gather
             # (timed on the host: the commit is already complete here)
             t1 = time.perf_counter()
@@ -233,7 +236,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist_on:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
@@ -300,7 +303,7 @@ def main():
             "cfg2" if (args.vocab, args.len_min, args.len_max) == (100_000, 400, 600) else
             "cfg5-shape" if args.vocab >= 1_000_000 else "custom",
             N, args.len_min, args.len_max, args.vocab,
-            "; GLOBAL stats exchange (term-ownership all-to-all of (term, df) records + stats all-reduce, RCCL)" if world > 1 else ""),
+            "; GLOBAL stats exchange (term-ownership all-to-all of (term, df) records + stats all-reduce, RCCL)" if dist_on else ""),
             "docs_per_gpu": N, "text_bytes_per_gpu": text_bytes, "nnz_per_gpu": nnz,
             "vocab_terms": st["num_terms"], "dict_slots_log2": cap, "inversion": "term-major" if st["term_major"] else "block-major",
             "parallelism": "dp%d (document shards)" % world},
@@ -312,8 +315,8 @@ def main():
         "phases_alg_GBs": phase_gbs,
         "index_build_alg_bytes": b_index,
         "index_build_GBs_end_to_end": b_index / (elapsed / args.steps) / 1e9,
-        "global_exchange_ms_per_step": exch[0] * 1e3 / args.steps if world > 1 else None,
-        "global_exchange_frac_of_step": (exch[0] / elapsed) if world > 1 else None,
+        "global_exchange_ms_per_step": exch[0] * 1e3 / args.steps if dist_on else None,
+        "global_exchange_frac_of_step": (exch[0] / elapsed) if dist_on else None,
         "long_docs": st["long_docs"],
         "unicode_docs": n_unicode,
         "tokenizer_docs_per_window": st["pack_docs"],
@@ -321,7 +324,7 @@ def main():
     }
 
     # ---- queries (outside the timed region) ----
-    if not args.no_queries and world == 1:
+    if not args.no_queries and not dist_on:
         from tfidf_amd.engine import analyze
         qs = synth.queries(max(args.queries, 1))
         # algorithmic bytes: 9 B per posting read (doc u32 + tf u32 + norm u8)
@@ -417,7 +420,7 @@ def main():
         result["queries"] = out
 
     # ---- corpus loader: PCIe-inclusive end-to-end build (not `value`) ----
-    if args.e2e and world == 1:
+    if args.e2e and not dist_on:
         text, offs = corpus.to_host()
         best_add, best_tot = None, None
         for _ in range(2):
@@ -438,13 +441,13 @@ def main():
                     "best of 2"}
         del text, offs
 
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
+    if rank == 0 and not dist_on and args.cpu_sample > 0:
         result["cpu_baseline"] = cpu_baseline(corpus, args, args.cpu_sample)
     corpus.free()
     idx.close()
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

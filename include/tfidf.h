@@ -105,6 +105,8 @@ typedef struct tfidf_index_stats {
   uint64_t hash_rebuilds; /* builds redone in the last commit because of a hash collision */
   uint64_t coalesced_batches;  /* tfidf_search_coalesced: batches run / queries served (index lifetime) */
   uint64_t coalesced_queries;
+  uint64_t unit_batches;   /* batched top-k searches scored by query units (k_score_units) / units run */
+  uint64_t unit_count;
 } tfidf_index_stats;
 
 /* Per-phase device times of the last commit, measured with HIP events on the

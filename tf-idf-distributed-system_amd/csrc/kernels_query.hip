@@ -832,6 +832,430 @@ __global__ void __launch_bounds__(kPairWaves * 64) k_score_pairs(QueryParams p) 
 }
 
 // ---------------------------------------------------------------------------
+// Workgroup per (query, doc-block range) unit — the batched top-k path for
+// plain disjunctions with k <= 64 (cfg 4, block-major postings).  The host
+// cuts each query into units of about kUnitPostings postings (heavy queries
+// into several block ranges).  Per block of the unit, for each query term in
+// query order, the 256 threads add the term's block segment into a dense LDS
+// accumulator of doubles (-0.0 = untouched: every term score is >= +0.0, so
+// -0.0 + s == s and the per-document value is the disjunction's double sum in
+// query order — terms are separated by a barrier); first touches set a bit.
+// Each wave then scans its quarter of the block's hit bits in doc order,
+// rounds the sums to float, keys them (score bits << 32 | ~doc) and keeps the
+// ones above its running k-th best key in a lane-held sorted top-k list
+// (lane j = j-th best).  Once a list is full almost every hit fails that one
+// compare, so there is no per-block selection pass, no candidate array per
+// (query, block) pair and no hash probing: the work is the postings.  At the
+// unit end wave 0 merges the four lists and writes them as the candidates of
+// pair (q, b0) (cand_n = 0 for the unit's other blocks); k_merge_topk orders
+// each query's candidates (several units for a split query).
+constexpr uint32_t kUnitThreads = 256;
+constexpr uint32_t kUnitWaves = kUnitThreads / 64;
+constexpr uint32_t kUnitU = 4;                 // postings per thread in flight
+constexpr uint32_t kUnitPre = 4;               // query terms whose first chunk is prefetched per block
+constexpr uint64_t kNegZeroBits = 0x8000000000000000ull;
+
+struct UnitSmem {
+  double acc[kBlockDocs];                      // -0.0 = untouched
+  uint32_t bits[kBlockDocs / 32];              // touched documents of the block
+  float cache[256];
+  uint64_t seg_a[2][64], seg_z[2][64];         // block segment of each query term (double-buffered)
+  float tw[64];
+  uint64_t lists[kUnitWaves][64];
+  unsigned long long thr;                      // max of the waves' k-th keys: a bound for the unit's k-th key
+  uint32_t unit;
+};
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)l) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)l);
+}
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, 1, 64), hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), 1, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+// bitonic stages over the 64 lanes for sequences of `size` (descending overall)
+__device__ __forceinline__ uint64_t bitonic_stages(uint64_t v, uint32_t lane, uint32_t size) {
+  for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+    const uint64_t o = shfl_xor64(v, (int)stride);
+    const bool desc = (lane & size) == 0, lower = (lane & stride) == 0;
+    v = (lower == desc) ? max(v, o) : min(v, o);
+  }
+  return v;
+}
+
+// Insert the candidate keys of the lanes in cm (all above theta when cm was
+// taken) into the wave's sorted list tk (lane j = j-th largest key, 0 = empty);
+// theta = the k-th key (0 until k are held).  A few candidates: one at a time
+// (shift-insert); many (a list filling up): bitonic sort of the candidates and
+// a bitonic merge with the list (top 64 of the union).
+__device__ __forceinline__ void topk_insert(uint64_t cm, uint64_t key, uint64_t &tk, uint64_t &theta, uint32_t k,
+                                            uint32_t lane) {
+  if (__popcll(cm) > 4) {
+    uint64_t v = ((cm >> lane) & 1ull) ? key : 0ull;
+#pragma unroll
+    for (uint32_t size = 2; size <= 64; size <<= 1) v = bitonic_stages(v, lane, size);
+    tk = max(tk, shfl64(v, 63 - (int)lane));                    // bitonic: the top 64 of both lists
+    tk = bitonic_stages(tk, lane, 64);
+    theta = readlane64(tk, k - 1);
+    return;
+  }
+  while (cm) {
+    const uint32_t l = (uint32_t)__builtin_ctzll(cm);
+    cm &= cm - 1;
+    const uint64_t ck = readlane64(key, l);
+    if (ck <= theta) continue;                                  // wave-uniform
+    const uint32_t pos = (uint32_t)__popcll(__ballot(tk > ck));
+    const uint64_t up = shfl_up64(tk);
+    tk = lane > pos ? up : (lane == pos ? ck : tk);
+    theta = readlane64(tk, k - 1);
+  }
+}
+
+__global__ void __launch_bounds__(kUnitThreads) k_score_units(QueryParams p, const uint4 *units, uint32_t n_units,
+                                                                 uint32_t *unit_ctr) {
+  __shared__ UnitSmem sm;
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t wid = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
+  for (uint32_t i = tid; i < 256; i += kUnitThreads) sm.cache[i] = p.cache[i];
+  {
+    uint4 *a = reinterpret_cast<uint4 *>(sm.acc);
+    for (uint32_t i = tid; i < kBlockDocs / 2; i += kUnitThreads) a[i] = make_uint4(0, 0x80000000u, 0, 0x80000000u);
+    for (uint32_t i = tid; i < kBlockDocs / 32; i += kUnitThreads) sm.bits[i] = 0;
+  }
+  const uint32_t nb = p.n_blocks, k = p.k, C = p.C;
+  for (;;) {
+    if (tid == 0) {
+      sm.unit = atomicAdd(unit_ctr, 1u);
+      sm.thr = 0;
+    }
+    __syncthreads();                                            // also: the previous unit is finished
+    const uint32_t u = sm.unit;
+    if (u >= n_units) break;
+    const uint4 un = units[u];
+    const uint32_t q = un.x, b0 = un.y, b1 = un.z;
+    const uint32_t t0 = p.q_off[q], nt = p.q_off[q + 1] - t0;  // <= 64 (host)
+    uint32_t slot = kInvalidSlot;
+    if (tid < nt) {
+      slot = p.q_slot[t0 + tid];
+      sm.tw[tid] = p.q_w[t0 + tid];
+    }
+    // block segment of term tid (block-major: bbase[b] + blk[b][slot] ..)
+    auto segment = [&](uint32_t b, uint64_t *a, uint64_t *z) {
+      *a = *z = 0;
+      if (slot != kInvalidSlot) {
+        const uint32_t *row = p.blk + (size_t)b * C;
+        const uint64_t bb = p.bbase[b];
+        *a = bb + row[slot];
+        *z = slot + 1 < C ? bb + row[slot + 1] : p.bbase[b + 1];
+      }
+    };
+    // pipeline: at the top of block b, seg[b & 1] = segments of b and seg[(b + 1) & 1]
+    // = segments of b + 1; pre = block b's first chunks (loaded during block b - 1).
+    // Block b issues the segment loads of b + 2 and the first chunks of b + 1.
+    const uint32_t bend = nt ? b1 : b0;                         // a query without terms has no hits
+    if (tid < nt) {
+      uint64_t a, z;
+      segment(b0, &a, &z);
+      sm.seg_a[b0 & 1][tid] = a;
+      sm.seg_z[b0 & 1][tid] = z;
+      if (b0 + 1 < bend) {
+        segment(b0 + 1, &a, &z);
+        sm.seg_a[(b0 + 1) & 1][tid] = a;
+        sm.seg_z[(b0 + 1) & 1][tid] = z;
+      }
+    }
+    __syncthreads();
+    // first chunk of the first kUnitPre terms of block b from seg[par]
+    auto prefetch = [&](uint32_t par, uint32_t (&pre)[kUnitPre][kUnitU]) {
+#pragma unroll
+      for (uint32_t j = 0; j < kUnitPre; j++) {
+        const uint64_t a = j < nt ? sm.seg_a[par][j] : 0ull, z = j < nt ? sm.seg_z[par][j] : 0ull;
+#pragma unroll
+        for (int v = 0; v < (int)kUnitU; v++) {
+          const uint64_t i = a + v * kUnitThreads + tid;
+          pre[j][v] = i < z ? p.post32[i] : 0u;
+        }
+      }
+    };
+    uint32_t pre[kUnitPre][kUnitU];
+    if (b0 < bend) prefetch(b0 & 1, pre);
+    uint64_t tk = 0, theta = 0;
+    for (uint32_t b = b0; b < bend; b++) {
+      const uint32_t d0 = b * kBlockDocs, par = b & 1;
+      __syncthreads();                                          // previous scan done; segments of b + 1 visible
+      uint64_t na = 0, nz = 0;                                  // segments of b + 2, loads in flight
+      if (tid < nt && b + 2 < bend) segment(b + 2, &na, &nz);
+      uint32_t npre[kUnitPre][kUnitU];                          // first chunks of b + 1, loads in flight
+      if (b + 1 < bend) prefetch(par ^ 1, npre);
+      for (uint32_t j = 0; j < nt; j++) {
+        const uint64_t a = sm.seg_a[par][j], z = sm.seg_z[par][j];
+        const float wj = sm.tw[j];
+        for (uint64_t c0 = a; c0 < z; c0 += kUnitThreads * kUnitU) {
+          uint32_t e[kUnitU];
+          if (c0 == a && j < kUnitPre) {
+#pragma unroll
+            for (int v = 0; v < (int)kUnitU; v++) {
+              e[v] = pre[0][v];
+#pragma unroll
+              for (uint32_t jj = 1; jj < kUnitPre; jj++) e[v] = j == jj ? pre[jj][v] : e[v];
+            }
+          } else {
+#pragma unroll
+            for (int v = 0; v < (int)kUnitU; v++) {
+              const uint64_t i = c0 + v * kUnitThreads + tid;
+              e[v] = i < z ? p.post32[i] : 0u;
+            }
+          }
+#pragma unroll
+          for (int v = 0; v < (int)kUnitU; v++) {
+            const uint64_t i = c0 + v * kUnitThreads + tid;
+            if (i < z) {
+              uint32_t ld, tf, nrm;
+              post_decode<false>(p, e[v], i, d0, &ld, &tf, &nrm);
+              const float sc = bm25_term(wj, tf, sm.cache[nrm]);
+              const double old = sm.acc[ld];
+              sm.acc[ld] = old + (double)sc;
+              if ((uint64_t)__double_as_longlong(old) == kNegZeroBits) atomicOr(&sm.bits[ld >> 5], 1u << (ld & 31));
+            }
+          }
+        }
+        __syncthreads();                                        // term j's sums land before term j + 1's
+      }
+      if (tid < nt && b + 2 < bend) {                           // block b's segment slots are free now
+        sm.seg_a[par][tid] = na;
+        sm.seg_z[par][tid] = nz;
+      }
+#pragma unroll
+      for (uint32_t j = 0; j < kUnitPre; j++)
+#pragma unroll
+        for (int v = 0; v < (int)kUnitU; v++) pre[j][v] = npre[j][v];
+      // wave wid scans documents [2048 wid, 2048 wid + 2048): lane l owns bit word 64 wid + l
+      const uint32_t wi = wid * 64 + lane;
+      uint32_t wb = sm.bits[wi];
+      sm.bits[wi] = 0;
+      while (__any(wb != 0)) {
+        uint64_t key = 0;
+        if (wb) {
+          const uint32_t x = wi * 32 + (uint32_t)__builtin_ctz(wb);
+          wb &= wb - 1;
+          const double v = sm.acc[x];
+          sm.acc[x] = __longlong_as_double((long long)kNegZeroBits);
+          key = ((uint64_t)__float_as_uint((float)v) << 32) | (uint64_t)(~(d0 + x));
+        }
+        const uint64_t th = max(theta, (uint64_t)sm.thr);       // no key at or below another wave's k-th key can win
+        topk_insert(__ballot(key > th), key, tk, theta, k, lane);
+        if (lane == 0 && theta > th) atomicMax(&sm.thr, (unsigned long long)theta);
+      }
+    }
+    // merge the waves' lists (wave 0) and write the unit's candidates
+    sm.lists[wid][lane] = lane < k ? tk : 0ull;
+    __syncthreads();
+    if (wid == 0) {
+#pragma unroll
+      for (uint32_t w = 1; w < kUnitWaves; w++) {
+        const uint64_t key = sm.lists[w][lane];
+        topk_insert(__ballot(key > theta), key, tk, theta, k, lane);
+      }
+      const bool has = lane < k && tk != 0;
+      const uint32_t n = (uint32_t)__popcll(__ballot(has));
+      const size_t pr = (size_t)q * nb + b0;
+      if (has) p.cand[pr * k + lane] = tk;
+      if (lane == 0) p.cand_n[pr] = n;
+    }
+    for (uint32_t b = b0 + 1 + tid; b < b1; b += kUnitThreads) p.cand_n[(size_t)q * nb + b] = 0;
+  }
+}
+
+hipError_t launch_score_units(const QueryParams &p, const uint4 *units, uint32_t n_units, uint32_t *unit_ctr, int grid,
+                              hipStream_t s) {
+  hipLaunchKernelGGL(k_score_units, dim3(grid), dim3(kUnitThreads), 0, s, p, units, n_units, unit_ctr);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Wave per (query, doc-block range) unit — the light queries of a batch
+// (few postings per block; the host sends queries averaging more than
+// kWunitLightPost postings per block to k_score_units).  Per block the wave
+// inserts each term's segment (query order) into its private 1024-slot LDS
+// hash table (doc -> double sum, as k_score_pairs), then walks the list of
+// claimed slots: keys above the running k-th best go into the lane-held top-k
+// list (topk_insert), and every claimed slot is reset — no table clear, no
+// per-block selection, no candidate array per (query, block).  A block with
+// more than kWunitPassPost postings is done in 16 passes over doc sub-ranges
+// of 512 documents (at most 512 distinct documents per pass, so the table
+// never fills).  The next block's segments and first posting chunks are
+// loaded while the current block's hits are walked.
+constexpr uint32_t kWunitWaves = kPairWavesPerWG;
+constexpr uint32_t kWunitPassPost = 700;
+
+struct WunitSmem {
+  uint32_t key[kWunitWaves][kPairSlots];          // doc - d0 per slot (kPairEmpty = free)
+  double val[kWunitWaves][kPairSlots];
+  uint16_t list[kWunitWaves][kPairSlots];         // claimed slots of the current pass
+  float cache[256];
+};
+
+__global__ void __launch_bounds__(kWunitWaves * 64) k_score_wunits(QueryParams p, const uint4 *units, uint32_t n_units,
+                                                                      uint32_t *unit_ctr) {
+  __shared__ WunitSmem sm;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) sm.cache[i] = p.cache[i];
+  uint32_t *key = sm.key[w];
+  double *val = sm.val[w];
+  uint16_t *list = sm.list[w];
+  {
+    uint4 *kw = reinterpret_cast<uint4 *>(key);
+#pragma unroll
+    for (int i = 0; i < (int)(kPairSlots / 4 / 64); i++)
+      kw[lane + 64 * i] = make_uint4(kPairEmpty, kPairEmpty, kPairEmpty, kPairEmpty);
+  }
+  __syncthreads();
+  const uint32_t nb = p.n_blocks, k = p.k, C = p.C;
+  for (;;) {
+    uint32_t u = 0;
+    if (lane == 0) u = atomicAdd(unit_ctr, 1u);
+    u = (uint32_t)__builtin_amdgcn_readfirstlane((int)u);
+    if (u >= n_units) break;
+    const uint4 un = units[u];
+    const uint32_t q = un.x, b0 = un.y, b1 = un.z;
+    const uint32_t t0 = p.q_off[q], nt = p.q_off[q + 1] - t0;  // <= 64 (host)
+    uint32_t slot = kInvalidSlot;
+    float tw = 0.f;
+    if (lane < nt) {
+      slot = p.q_slot[t0 + lane];
+      tw = p.q_w[t0 + lane];
+    }
+    auto segment = [&](uint32_t b, uint64_t *a, uint64_t *z) {
+      *a = *z = 0;
+      if (lane < nt && slot != kInvalidSlot) {
+        const uint32_t *row = p.blk + (size_t)b * C;
+        const uint64_t bb = p.bbase[b];
+        *a = bb + row[slot];
+        *z = slot + 1 < C ? bb + row[slot + 1] : p.bbase[b + 1];
+      }
+    };
+    // first two 64-posting chunks of the first kQTermsFast terms of a block
+    auto prefetch = [&](uint64_t a, uint64_t z, uint32_t (&pre)[kQTermsFast][2]) {
+#pragma unroll
+      for (uint32_t j = 0; j < kQTermsFast; j++) {
+        const uint64_t ja = readlane64(a, j), jz = readlane64(z, j);
+#pragma unroll
+        for (uint32_t c = 0; c < 2; c++) {
+          const uint64_t i = ja + lane + 64 * c;
+          pre[j][c] = i < jz ? p.post32[i] : 0u;
+        }
+      }
+    };
+    const uint32_t bend = nt ? b1 : b0;
+    uint64_t a = 0, z = 0, na = 0, nz = 0;
+    uint32_t pre[kQTermsFast][2];
+    if (b0 < bend) {
+      segment(b0, &a, &z);
+      if (b0 + 1 < bend) segment(b0 + 1, &na, &nz);
+      prefetch(a, z, pre);
+    }
+    uint64_t tk = 0, theta = 0;
+    for (uint32_t b = b0; b < bend; b++) {
+      const uint32_t d0 = b * kBlockDocs;
+      uint32_t P = (uint32_t)(z - a);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) P += (uint32_t)__shfl_xor((int)P, o, 64);
+      const uint32_t np = P > kWunitPassPost ? 16u : 1u;          // 16 passes: 512 documents each
+      const uint32_t rsh = np == 1 ? 13u : 9u;
+      for (uint32_t ps = 0; ps < np; ps++) {
+        uint32_t nlist = 0;
+        auto insert = [&](uint32_t e, bool in, float wj, uint64_t i) {
+          uint32_t claimed = kPairEmpty;
+          if (in) {
+            uint32_t ld, tf, nrm;
+            post_decode<false>(p, e, i, d0, &ld, &tf, &nrm);
+            if ((ld >> rsh) == ps) {
+              const float sc = bm25_term(wj, tf, sm.cache[nrm]);
+              uint32_t s = (ld * 0x9E3779B1u) >> 22;
+              for (;;) {
+                const uint32_t old = atomicCAS(&key[s], kPairEmpty, ld);
+                if (old == kPairEmpty) { val[s] = (double)sc; claimed = s; break; }
+                if (old == ld) { val[s] += (double)sc; break; }
+                s = (s + 1) & (kPairSlots - 1);
+              }
+            }
+          }
+          const bool c = claimed != kPairEmpty;
+          const uint64_t m = __ballot(c);
+          if (c) list[nlist + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint16_t)claimed;
+          nlist += (uint32_t)__popcll(m);
+        };
+        for (uint32_t j = 0; j < nt; j++) {
+          const uint64_t ja = readlane64(a, j), jz = readlane64(z, j);
+          const float wj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tw), (int)j));
+          uint64_t i0 = ja;
+          if (ps == 0 && j < kQTermsFast) {
+            uint32_t e0 = pre[0][0], e1 = pre[0][1];
+#pragma unroll
+            for (uint32_t jj = 1; jj < kQTermsFast; jj++)
+              if (jj == j) { e0 = pre[jj][0]; e1 = pre[jj][1]; }
+            insert(e0, ja + lane < jz, wj, ja + lane);
+            if (ja + 64 < jz) insert(e1, ja + 64 + lane < jz, wj, ja + 64 + lane);     // uniform
+            i0 = ja + 128;
+          }
+          for (; i0 < jz; i0 += 256) {
+            uint32_t e[4];
+#pragma unroll
+            for (int v = 0; v < 4; v++) {
+              const uint64_t i = i0 + 64 * v + lane;
+              e[v] = i < jz ? p.post32[i] : 0u;
+            }
+#pragma unroll
+            for (int v = 0; v < 4; v++)
+              if (i0 + 64 * v < jz) insert(e[v], i0 + 64 * v + lane < jz, wj, i0 + 64 * v + lane);
+          }
+        }
+        if (ps + 1 == np) {                                       // next block's loads in flight during the walk
+          a = na;
+          z = nz;
+          if (b + 2 < bend) segment(b + 2, &na, &nz);
+          if (b + 1 < bend) prefetch(a, z, pre);
+        }
+        for (uint32_t h = 0; h < nlist; h += 64) {
+          const uint32_t idx = h + lane;
+          uint64_t kv = 0;
+          if (idx < nlist) {
+            const uint32_t s = list[idx];
+            const uint32_t ld = key[s];
+            kv = ((uint64_t)__float_as_uint((float)val[s]) << 32) | (uint64_t)(~(d0 + ld));
+            key[s] = kPairEmpty;
+          }
+          topk_insert(__ballot(kv > theta), kv, tk, theta, k, lane);
+        }
+      }
+    }
+    const bool has = lane < k && tk != 0;
+    const uint32_t n = (uint32_t)__popcll(__ballot(has));
+    const size_t pr = (size_t)q * nb + b0;
+    if (has) p.cand[pr * k + lane] = tk;
+    if (lane == 0) p.cand_n[pr] = n;
+    for (uint32_t b = b0 + 1 + lane; b < b1; b += 64) p.cand_n[(size_t)q * nb + b] = 0;
+  }
+}
+
+hipError_t launch_score_wunits(const QueryParams &p, const uint4 *units, uint32_t n_units, uint32_t *unit_ctr, int grid,
+                               hipStream_t s) {
+  hipLaunchKernelGGL(k_score_wunits, dim3(grid), dim3(kWunitWaves * 64), 0, s, p, units, n_units, unit_ctr);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // All hits in (score desc, doc asc) order = searcher.search(q, Integer.MAX_VALUE)
 // (Worker.java:230).  k_score_blocks leaves one sorted run per doc block
 // (hits[b * kBlockDocs ...], hits_n[b] keys); k_hits_prefix turns the run

@@ -218,6 +218,8 @@ struct tfidf_index {
   // way per search (q_in: off | slot | w | role | meta; q_out: doc | score | n)
   DevBuf q_in, q_out;
   PinnedVec<uint32_t> q_host, q_res;
+  std::vector<uint32_t> q_units;       // batch scoring units {q, b0, b1, 0} (run_scoring)
+  uint64_t unit_batches = 0, unit_count = 0;
   hipEvent_t q_in_ev = nullptr;        // the last upload out of q_host
   bool q_in_pending = false;
   uint32_t *res_doc = nullptr, *res_n = nullptr;
@@ -1184,6 +1186,8 @@ extern "C" int tfidf_stats(const tfidf_index *ix, tfidf_index_stats *out) {
     std::lock_guard<std::mutex> cl(ix->cq_mu);
     out->coalesced_batches = ix->cq_batches;
     out->coalesced_queries = ix->cq_queries;
+    out->unit_batches = ix->unit_batches;
+    out->unit_count = ix->unit_count;
   }
   const DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->dict, &ix->csr, &ix->csr_esc, &ix->doc_len,
                           &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->blk, &ix->bbase, &ix->post,
@@ -1321,7 +1325,53 @@ static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint
   hipStream_t s = ix->stream;
   const std::vector<uint32_t> &qoff = qb.off, &slots = qb.slot;
   const size_t ns = slots.size(), nr = qb.ops ? ns + qb.meta.size() : 0;
-  const size_t words = qoff.size() + 2 * ns + nr;
+  const size_t npairs = (size_t)n_q * ix->n_blocks;
+  const bool batch = k && npairs >= (size_t)ix->num_cus * 16 && npairs < (1ull << 32);
+  // batches of plain disjunctions, k <= 64, block-major: workgroup per
+  // (query, block range) unit (k_score_units); units of about unit_post
+  // postings, queries above that split into equal block ranges, listed first
+  // (heavy units start early, the light tail balances)
+  std::vector<uint32_t> &units = ix->q_units;
+  units.clear();
+  bool unit_path = batch && k <= kUnitMaxK && !qb.ops && !ix->term_major && !getenv("TFIDF_NO_UNITS");
+  uint32_t n_wunits = 0;                 // the first n_wunits units are wave units
+  if (unit_path) {
+    std::vector<uint64_t> P(n_q, 0);
+    uint64_t T = 0;
+    for (uint32_t q = 0; q < n_q && unit_path; q++) {
+      if (qoff[q + 1] - qoff[q] > kUnitMaxTerms) unit_path = false;
+      for (uint32_t t = qoff[q]; t < qoff[q + 1]; t++)
+        if (slots[t] != kInvalidSlot) P[q] += ix->h_df[slots[t]];
+      T += P[q];
+    }
+    // light queries (at most light_post postings per block on average): wave
+    // units (k_score_wunits, units of ~16 k postings); heavy ones: workgroup
+    // units (k_score_units, dense block accumulator; ~T/4096 postings each)
+    const uint32_t nb = ix->n_blocks;
+    uint64_t light_post = kWunitLightPost;
+    if (const char *e = getenv("TFIDF_WUNIT_LIGHT")) light_post = (uint64_t)atoll(e);   // A/B and test hook
+    uint64_t unit_post = std::min<uint64_t>(std::max<uint64_t>(T / 4096, 8192), 1ull << 17);
+    uint64_t wunit_post = 16384;
+    if (const char *e = getenv("TFIDF_UNIT_POST")) unit_post = wunit_post = std::max(1, atoi(e));   // test hook: force splits
+    for (int pass = 0; pass < 3 && unit_path; pass++)        // light; heavy split; heavy whole
+      for (uint32_t q = 0; q < n_q; q++) {
+        const bool light = P[q] <= light_post * nb;
+        if (light != (pass == 0)) continue;
+        const uint64_t up = light ? wunit_post : unit_post;
+        const uint64_t nch = std::min<uint64_t>(std::max<uint64_t>((P[q] + up - 1) / up, 1), nb);
+        if (!light && (nch > 1) != (pass == 1)) continue;
+        for (uint64_t c = 0; c < nch; c++) {
+          units.push_back(q);
+          units.push_back((uint32_t)(c * nb / nch));
+          units.push_back((uint32_t)((c + 1) * nb / nch));
+          units.push_back(0);
+        }
+        if (light) n_wunits += (uint32_t)nch;
+      }
+    if (!unit_path) units.clear();
+  }
+  const size_t words0 = (qoff.size() + 2 * ns + nr + 3) & ~(size_t)3;    // units 16-B aligned
+  const size_t words = words0 + units.size();
   // one pinned staging buffer, one upload (the previous upload out of it must
   // have left: batch searches return before their copies run)
   if (ix->q_in_pending) HIP_TRY(hipEventSynchronize(ix->q_in_ev));
@@ -1334,6 +1384,7 @@ static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint
     memcpy(h + qoff.size() + 2 * ns, qb.role.data(), ns * 4);
     memcpy(h + qoff.size() + 3 * ns, qb.meta.data(), qb.meta.size() * 4);
   }
+  if (!units.empty()) memcpy(h + words0, units.data(), units.size() * 4);
   HIP_TRY(ix->q_in.reserve(words * 4 + 16));
   HIP_TRY(hipMemcpyAsync(ix->q_in.p, h, words * 4, hipMemcpyHostToDevice, s));
   HIP_TRY(hipEventRecord(ix->q_in_ev, s));
@@ -1385,8 +1436,29 @@ static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint
     qp.hits_n = ix->hits_n.as<uint32_t>();
   }
   HIP_TRY(hipEventRecord(ix->ev[EV_Q0], s));
-  const size_t npairs = (size_t)n_q * ix->n_blocks;
-  if (k && npairs >= (size_t)ix->num_cus * 16 && npairs < (1ull << 32)) {
+  if (unit_path) {
+    HIP_TRY(ix->ovf.reserve(64));
+    uint32_t *ctr = ix->ovf.as<uint32_t>();
+    HIP_TRY(hipMemsetAsync(ctr, 0, 8, s));
+    const uint32_t n_units = (uint32_t)(units.size() / 4), n_gunits = n_units - n_wunits;
+    ix->unit_batches++;
+    ix->unit_count += n_units;
+    const uint4 *ud = reinterpret_cast<const uint4 *>(din + words0);
+    if (n_wunits) {
+      const int grid = (int)std::min<uint64_t>((n_wunits + kWunitWavesPerWG - 1) / kWunitWavesPerWG,
+                                               (uint64_t)ix->num_cus * kWunitWGsPerCU);
+      HIP_TRY(launch_score_wunits(qp, ud, n_wunits, ctr, grid, s));
+    }
+    if (n_gunits) {
+      const int grid = (int)std::min<uint64_t>(n_gunits, (uint64_t)ix->num_cus * kUnitWGsPerCU);
+      HIP_TRY(launch_score_units(qp, ud + n_wunits, n_gunits, ctr + 1, grid, s));
+    }
+    HIP_TRY(hipEventRecord(ix->ev[EV_Q1], s));
+    HIP_TRY(launch_merge_topk(qp, s));
+    HIP_TRY(hipEventRecord(ix->ev[EV_Q2], s));
+    return TFIDF_OK;
+  }
+  if (batch) {
     // batches: wave per (block, query) pair; pairs with many postings are
     // listed for the dense per-block kernel (list mode, persistent grid).
     // Single queries keep the dense kernel: a few hundred pairs cannot fill

@@ -278,6 +278,20 @@ struct QueryParams {
 hipError_t launch_score_pairs(const QueryParams &p, int grid, hipStream_t s);
 constexpr uint32_t kPairWavesPerWG = 2;   // k_score_pairs workgroup = 2 waves (30 KB LDS: 5 per CU)
 hipError_t launch_score_blocks(const QueryParams &p, hipStream_t s);
+// batched top-k (k <= kUnitMaxK, plain disjunctions, block-major): workgroup
+// per (query, block range) unit {q, b0, b1, 0}; units of one query cover
+// [0, n_blocks); unit_ctr zeroed before the launch
+constexpr uint32_t kUnitMaxK = 64;
+constexpr uint32_t kUnitMaxTerms = 64;
+constexpr uint32_t kUnitWGsPerCU = 2;     // 71 KiB LDS each
+hipError_t launch_score_units(const QueryParams &p, const uint4 *units, uint32_t n_units, uint32_t *unit_ctr, int grid,
+                              hipStream_t s);
+// light queries of such batches: wave per unit (hash table per block)
+constexpr uint32_t kWunitWavesPerWG = kPairWavesPerWG;
+constexpr uint32_t kWunitWGsPerCU = 5;    // ~28 KiB LDS each
+constexpr uint32_t kWunitLightPost = 400; // postings per block (query average) up to which a query is light
+hipError_t launch_score_wunits(const QueryParams &p, const uint4 *units, uint32_t n_units, uint32_t *unit_ctr, int grid,
+                               hipStream_t s);
 hipError_t launch_merge_topk(const QueryParams &p, hipStream_t s);
 // all hits: per-block sorted runs (k_score_blocks, k == 0) -> one ordered list:
 // (doc, score) split into out_doc / out_score, or packed keys with doc_base
