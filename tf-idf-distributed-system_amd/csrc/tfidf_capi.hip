@@ -220,6 +220,7 @@ struct tfidf_index {
   PinnedVec<uint32_t> q_host, q_res;
   std::vector<uint32_t> q_units;       // batch scoring units {q, b0, b1, 0} (run_scoring)
   uint64_t unit_batches = 0, unit_count = 0;
+  hipEvent_t q_ev[2] = {nullptr, nullptr};  // fork / join of the wave-unit kernel on copy_stream
   hipEvent_t q_in_ev = nullptr;        // the last upload out of q_host
   bool q_in_pending = false;
   uint32_t *res_doc = nullptr, *res_n = nullptr;
@@ -277,6 +278,7 @@ extern "C" int tfidf_create(const tfidf_config *cfg, tfidf_index **out) {
   for (int i = 0; i < 2; i++) hipEventCreateWithFlags(&ix->mir_ev[i], hipEventDisableTiming);
   hipEventCreateWithFlags(&ix->gdf_ev, hipEventDisableTiming);
   hipEventCreateWithFlags(&ix->q_in_ev, hipEventDisableTiming);
+  for (int i = 0; i < 2; i++) hipEventCreateWithFlags(&ix->q_ev[i], hipEventDisableTiming);
   hipError_t e = ix->offsets.reserve(64);
   if (e != hipSuccess) { delete ix; return fail(TFIDF_E_OOM, "hipMalloc offsets"); }
   uint64_t zero = 0;
@@ -300,6 +302,7 @@ extern "C" int tfidf_destroy(tfidf_index *ix) {
   for (DevBuf *b : bufs) b->release();
   for (int i = 0; i < EV_N; i++) hipEventDestroy(ix->ev[i]);
   if (ix->q_in_ev) hipEventDestroy(ix->q_in_ev);
+  for (int i = 0; i < 2; i++) hipEventDestroy(ix->q_ev[i]);
   for (int i = 0; i < 2; i++) {
     if (ix->stage[i]) hipHostFree(ix->stage[i]);
     hipEventDestroy(ix->stage_ev[i]);
@@ -1444,14 +1447,29 @@ static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint
     ix->unit_batches++;
     ix->unit_count += n_units;
     const uint4 *ud = reinterpret_cast<const uint4 *>(din + words0);
+    // both kinds at once: the wave units on the side stream (fork / join events),
+    // so the two latency-bound kernels share the CUs instead of running in turn
+    const bool both = n_wunits && n_gunits;
+    hipStream_t ws = both ? ix->copy_stream : s;
+    if (both) {
+      HIP_TRY(hipEventRecord(ix->q_ev[0], s));
+      HIP_TRY(hipStreamWaitEvent(ws, ix->q_ev[0], 0));
+    }
     if (n_wunits) {
       const int grid = (int)std::min<uint64_t>((n_wunits + kWunitWavesPerWG - 1) / kWunitWavesPerWG,
                                                (uint64_t)ix->num_cus * kWunitWGsPerCU);
-      HIP_TRY(launch_score_wunits(qp, ud, n_wunits, ctr, grid, s));
+      HIP_TRY(launch_score_wunits(qp, ud, n_wunits, ctr, grid, ws));
     }
     if (n_gunits) {
-      const int grid = (int)std::min<uint64_t>(n_gunits, (uint64_t)ix->num_cus * kUnitWGsPerCU);
+      // (one per CU next to the wave units measured slower: 6.3 -> 7.8 ms at cfg 4)
+      uint32_t per_cu = kUnitWGsPerCU;
+      if (const char *e = getenv("TFIDF_UNIT_WG_PER_CU")) per_cu = (uint32_t)std::max(1, atoi(e));   // A/B
+      const int grid = (int)std::min<uint64_t>(n_gunits, (uint64_t)ix->num_cus * per_cu);
       HIP_TRY(launch_score_units(qp, ud + n_wunits, n_gunits, ctr + 1, grid, s));
+    }
+    if (both) {
+      HIP_TRY(hipEventRecord(ix->q_ev[1], ws));
+      HIP_TRY(hipStreamWaitEvent(s, ix->q_ev[1], 0));
     }
     HIP_TRY(hipEventRecord(ix->ev[EV_Q1], s));
     HIP_TRY(launch_merge_topk(qp, s));

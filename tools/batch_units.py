@@ -31,6 +31,18 @@ def main():
     g.commit()
     bq = synth.queries(int(os.environ.get("NQ", "10000")))
     g.search_batch(bq[:100], 10)
+    if os.environ.get("LIGHTS"):                          # sweep of the light-query threshold (postings/block)
+        for lt in os.environ["LIGHTS"].split(","):
+            os.environ["TFIDF_WUNIT_LIGHT"] = lt
+            (sc, tot), _ = timed(g, bq, 10)
+            print("light<=%s: scoring %.3f total %.3f ms" % (lt, sc, tot), flush=True)
+        os.environ.pop("TFIDF_WUNIT_LIGHT")
+    if os.environ.get("WGS"):                             # sweep: workgroup units per CU next to the wave units
+        for v in os.environ["WGS"].split(","):
+            os.environ["TFIDF_UNIT_WG_PER_CU"] = v
+            (sc, tot), _ = timed(g, bq, 10)
+            print("wg/cu=%s: scoring %.3f total %.3f ms" % (v, sc, tot), flush=True)
+        os.environ.pop("TFIDF_UNIT_WG_PER_CU")
     if os.environ.get("ONLY_UNITS"):                     # profiling: the unit path alone, k = 10
         for _ in range(2):
             g.search_batch(bq, 10)
