@@ -182,6 +182,7 @@ struct tfidf_index {
   uint64_t cq_batches = 0, cq_queries = 0;
   DevBuf verify_defer, lt_pos;
   std::unordered_map<uint32_t, std::string> term_cache;   // hashed slots' term strings (slot_term)
+  std::mutex term_mu;
   uint32_t pack_docs = 1;              // documents per wave window in the last commit
   uint64_t pack_retried = 0;           // documents the packs deferred in the last commit
   uint64_t unicode_docs = 0;           // documents with non-ASCII text in the last commit
@@ -1229,6 +1230,7 @@ static int slot_term(tfidf_index *ix, uint32_t slot, std::string *out) {
   char b[32];
   const uint64_t lo = ix->h_dict[slot], hi = ix->h_dict[(size_t)ix->C + slot];
   if (const uint32_t n = key_decode(lo, hi, b)) { out->assign(b, n); return TFIDF_OK; }
+  std::lock_guard<std::mutex> tl(ix->term_mu);             // batch preparation threads share the cache
   auto it = ix->term_cache.find(slot);
   if (it != ix->term_cache.end()) { *out = it->second; return TFIDF_OK; }
   uint64_t r = 0;
@@ -1323,6 +1325,42 @@ struct QueryBatch {
     ops |= !pq.slot.empty() && pq.meta != 0;
   }
 };
+
+// Prepare a batch's queries (parse, analysis, dictionary lookups, BM25
+// weights) on host threads: large batches spend more time here than on the
+// device (10 k queries: ~10 ms on one thread).  A query that does not parse
+// (or is not UTF-8) has no hits, as the reference answers [] for it
+// (Worker.java:182-185); the batch goes on.
+static int prepare_batch(tfidf_index *ix, const uint8_t *q_utf8, const uint64_t *q_offsets, uint32_t n_q,
+                         QueryBatch *qb) {
+  if (int e = wait_gdf(ix)) return e;                   // once, before the workers read the mirrors
+  std::vector<PreparedQuery> pqs(n_q);
+  auto work = [&](uint32_t a, uint32_t b) {
+    DeviceGuard g(ix->cfg.device);                      // slot_term may read a reference occurrence
+    for (uint32_t i = a; i < b; i++)
+      if (prepare_query(ix, q_utf8 + q_offsets[i], q_offsets[i + 1] - q_offsets[i], &pqs[i]) != TFIDF_OK)
+        pqs[i] = PreparedQuery();
+  };
+  uint32_t nt = std::min<uint32_t>(std::max(1u, std::thread::hardware_concurrency()), 16u);
+  nt = std::max(1u, std::min(nt, n_q / 1024));
+  if (nt <= 1) {
+    work(0, n_q);
+  } else {
+    std::vector<std::thread> th;
+    for (uint32_t t = 1; t < nt; t++) th.emplace_back(work, (uint32_t)((uint64_t)n_q * t / nt), (uint32_t)((uint64_t)n_q * (t + 1) / nt));
+    work(0, (uint32_t)(n_q / nt));
+    for (auto &x : th) x.join();
+  }
+  size_t ns = 0;
+  for (const PreparedQuery &pq : pqs) ns += pq.slot.size();
+  qb->slot.reserve(ns);
+  qb->w.reserve(ns);
+  qb->role.reserve(ns);
+  qb->off.reserve(n_q + 1);
+  qb->meta.reserve(n_q);
+  for (const PreparedQuery &pq : pqs) qb->add(pq);
+  return TFIDF_OK;
+}
 
 static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint32_t k) {
   hipStream_t s = ix->stream;
@@ -1574,15 +1612,8 @@ extern "C" int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const 
   std::lock_guard<std::mutex> lk(ix->mu);
   if (!ix->committed) return fail(TFIDF_E_STATE, "search before commit");
   DeviceGuard g(ix->cfg.device);
-  // a query that does not parse (or is not UTF-8) has no hits, as the
-  // reference answers [] for it (Worker.java:182-185); the batch goes on
   QueryBatch qb;
-  for (uint32_t i = 0; i < n_q; i++) {
-    PreparedQuery pq;
-    if (prepare_query(ix, q_utf8 + q_offsets[i], q_offsets[i + 1] - q_offsets[i], &pq) != TFIDF_OK)
-      pq = PreparedQuery();
-    qb.add(pq);
-  }
+  if (int e = prepare_batch(ix, q_utf8, q_offsets, n_q, &qb)) return e;
   if (n_q == 0) return TFIDF_OK;
   if (ix->n_docs == 0 || qb.slot.empty()) {
     memset(counts, 0, n_q * 4);
@@ -1718,12 +1749,7 @@ extern "C" int tfidf_search_batch_keys_device(tfidf_index *ix, const uint8_t *q_
   if (n_q == 0) return TFIDF_OK;
   hipStream_t s = ix->stream;
   QueryBatch qb;
-  for (uint32_t i = 0; i < n_q; i++) {
-    PreparedQuery pq;
-    if (prepare_query(ix, q_utf8 + q_offsets[i], q_offsets[i + 1] - q_offsets[i], &pq) != TFIDF_OK)
-      pq = PreparedQuery();                            // does not parse -> no hits (Worker.java:182-185)
-    qb.add(pq);
-  }
+  if (int e = prepare_batch(ix, q_utf8, q_offsets, n_q, &qb)) return e;
   if (ix->n_docs == 0 || qb.slot.empty()) {
     HIP_TRY(hipMemsetAsync(d_keys, 0, (size_t)n_q * k * 8, s));
     HIP_TRY(hipStreamSynchronize(s));
