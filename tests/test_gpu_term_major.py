@@ -163,3 +163,23 @@ def test_large_tf_escapes(monkeypatch, inversion):
         assert_hits_equal(g.search(q, 10), o.search(q, 10))
     g.close()
     o.close()
+
+
+@pytest.mark.parametrize("n_docs", [8, 40, 100])
+def test_small_shards_tf_field(n_docs):
+    # few documents leave 56 - slot - doc bits >= 32 for tf: the field is
+    # capped at 24 bits (a 32-bit shift made every tf an escape and the host
+    # divided by zero at 33..64 documents: the bench's 40-book CPU sample)
+    rng = random.Random(n_docs)
+    texts = [b" ".join([b"alpha"] * rng.randint(1, 300) + [synth.word(rng.randint(1, 500)) for _ in range(200)])
+             for _ in range(n_docs)]
+    g = build(texts, L.INVERSION_TERM)
+    o = oracle_of(texts)
+    assert g.stats()["term_major"] == 1
+    for d in range(n_docs):
+        assert g.doc_terms(d) == o.doc_terms(d)
+    for q in [b"alpha", b"alpha aaab", b"aaac aaad aaae"]:
+        assert_hits_equal(g.search(q, 0), o.search(q, 0))
+        assert_hits_equal(g.search(q, 5), o.search(q, 5))
+    g.close()
+    o.close()

@@ -1040,22 +1040,39 @@ __global__ void __launch_bounds__(kUnitThreads) k_score_units(QueryParams p, con
 #pragma unroll
         for (int v = 0; v < (int)kUnitU; v++) pre[j][v] = npre[j][v];
       // wave wid scans documents [2048 wid, 2048 wid + 2048): lane l owns bit word 64 wid + l
+      // two hits per lane per step (both LDS round trips in flight); no key at
+      // or below another wave's k-th key (sm.thr, read once per block) can win
       const uint32_t wi = wid * 64 + lane;
       uint32_t wb = sm.bits[wi];
       sm.bits[wi] = 0;
+      uint64_t th = max(theta, (uint64_t)sm.thr);
+      const uint64_t th_in = th;
       while (__any(wb != 0)) {
-        uint64_t key = 0;
-        if (wb) {
-          const uint32_t x = wi * 32 + (uint32_t)__builtin_ctz(wb);
+        uint32_t x[2];
+        bool has[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          has[h] = wb != 0;
+          x[h] = wi * 32 + (has[h] ? (uint32_t)__builtin_ctz(wb) : 0u);
           wb &= wb - 1;
-          const double v = sm.acc[x];
-          sm.acc[x] = __longlong_as_double((long long)kNegZeroBits);
-          key = ((uint64_t)__float_as_uint((float)v) << 32) | (uint64_t)(~(d0 + x));
         }
-        const uint64_t th = max(theta, (uint64_t)sm.thr);       // no key at or below another wave's k-th key can win
-        topk_insert(__ballot(key > th), key, tk, theta, k, lane);
-        if (lane == 0 && theta > th) atomicMax(&sm.thr, (unsigned long long)theta);
+        double v[2];
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          v[h] = has[h] ? sm.acc[x[h]] : 0.0;
+          if (has[h]) sm.acc[x[h]] = __longlong_as_double((long long)kNegZeroBits);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          const uint64_t key = has[h] ? ((uint64_t)__float_as_uint((float)v[h]) << 32) | (uint64_t)(~(d0 + x[h])) : 0ull;
+          const uint64_t cm = __ballot(key > th);
+          if (cm) {
+            topk_insert(cm, key, tk, theta, k, lane);
+            th = max(th, theta);
+          }
+        }
       }
+      if (lane == 0 && th > th_in) atomicMax(&sm.thr, (unsigned long long)th);
     }
     // merge the waves' lists (wave 0) and write the unit's candidates
     sm.lists[wid][lane] = lane < k ? tk : 0ull;

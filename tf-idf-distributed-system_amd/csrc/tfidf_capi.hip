@@ -1027,7 +1027,9 @@ static int commit_once(tfidf_index *ix) {
     tp.slot_bits = ix->cap_log2;
     tp.doc_bits = 1;
     while ((1ull << tp.doc_bits) < N) tp.doc_bits++;
-    tp.tf_bits = 56 - tp.slot_bits - tp.doc_bits;            // >= 4 (slot, doc <= 26 bits)
+    // >= 4 (slot, doc <= 26 bits); at most 24 (tf <= kMaxTf): a small shard
+    // (40 books: 56 - 18 - 6 = 32) must not reach a 32-bit shift in tf_esc
+    tp.tf_bits = std::min(56u - tp.slot_bits - tp.doc_bits, 24u);
     if (const char *e = getenv("TFIDF_TEST_TERM_TF_BITS"))      // tests: exercise the tf escape list
       tp.tf_bits = std::max(1u, std::min(tp.tf_bits, (uint32_t)atoi(e)));
     tp.csr = bp.csr;
