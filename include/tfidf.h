@@ -288,6 +288,11 @@ int tfidf_synth_corpus(int device, uint64_t seed, uint64_t n_docs, uint64_t doc_
                        uint32_t V, uint32_t len_min, uint32_t len_max, void **d_text, void **d_offsets,
                        uint64_t *total_bytes);
 int tfidf_device_free(int device, void *d_ptr);
+/* Synchronous copy through the library's own HIP runtime (test/bench helper:
+ * a process may hold a second HIP runtime, e.g. PyTorch's bundled one, whose
+ * handles do not see the library's allocations).  kind 1 = host -> device,
+ * 2 = device -> host. */
+int tfidf_device_copy(int device, void *dst, const void *src, uint64_t bytes, int kind);
 
 #ifdef __cplusplus
 }

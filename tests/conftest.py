@@ -19,6 +19,15 @@ for p in (REPO, PKG_DIR):
 
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
+# One HIP runtime per process: PyTorch bundles its own libamdhip64 /
+# libhsa-runtime64 (same soname as /opt/rocm's).  Loaded first, it is the one
+# libtfidf binds to; loaded after libtfidf it is a second runtime that finds no
+# GPU ("No HIP GPUs are available").  Tests mix both, so torch goes first.
+try:
+    import torch  # noqa: F401
+except Exception:
+    pass
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: requires an MI355X GPU and the HIP extension")

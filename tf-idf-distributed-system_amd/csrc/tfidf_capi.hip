@@ -2279,3 +2279,11 @@ extern "C" int tfidf_device_free(int device, void *d_ptr) {
   if (d_ptr) HIP_TRY(hipFree(d_ptr));
   return TFIDF_OK;
 }
+
+extern "C" int tfidf_device_copy(int device, void *dst, const void *src, uint64_t bytes, int kind) {
+  if ((!dst || !src) && bytes) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  if (kind != 1 && kind != 2) return fail(TFIDF_E_INVALID_ARG, "kind must be 1 (H2D) or 2 (D2H)");
+  DeviceGuard g(device);
+  if (bytes) HIP_TRY(hipMemcpy(dst, src, bytes, kind == 1 ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost));
+  return TFIDF_OK;
+}

@@ -191,9 +191,10 @@ struct PostingParams {
 
 // --- launch wrappers (kernels_index.hip) ---
 hipError_t launch_tokenize_wave(const BuildParams &p, int grid, hipStream_t s);
-constexpr uint32_t kWaveWGsPerCU = 8;
+constexpr uint32_t kWaveWGsPerCU = 8;       // 64-thread workgroups per CU (2 waves/SIMD: VGPR- and LDS-bound)
 constexpr uint32_t kPackMaxDocs = 16;     // documents per packed window (<= kPackMax, kernels_index.hip)
-constexpr uint64_t kPackBytes = 2048;     // text per packed window (auto pack size)    // 64-thread workgroups per CU (2 waves/SIMD: VGPR-bound)
+constexpr uint64_t kPackBytes = 2560;     // text per packed window (auto pack size): ~450 tokens, under the
+                                          // wave table's 512 distinct terms (cfg 5: 7 docs, tokenize 16.3 -> 14.9 ms)
 hipError_t launch_tokenize_long(const BuildParams &p, int grid, hipStream_t s);
 constexpr uint32_t kLongCoreBytes = 2048;              // = kCoreBytes (kernels_index.hip)
 constexpr uint64_t kDenseBudget = 2ull << 30;          // per-group dense count arrays (book-sized documents)

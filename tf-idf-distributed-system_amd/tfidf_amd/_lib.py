@@ -121,6 +121,7 @@ SIGNATURES = {
     "tfidf_synth_corpus": (C.c_int, [C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, F64P, C.c_uint32, C.c_uint32,
                                      C.c_uint32, C.POINTER(VP), C.POINTER(VP), U64P]),
     "tfidf_device_free": (C.c_int, [C.c_int, VP]),
+    "tfidf_device_copy": (C.c_int, [C.c_int, VP, VP, C.c_uint64, C.c_int]),
 }
 
 _lib = None

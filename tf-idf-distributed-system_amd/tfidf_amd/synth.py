@@ -97,20 +97,16 @@ def queries(n_q, n_terms=3, lo=100, hi=10_000, seed=SEED + 1):
     return out
 
 
-def _d2h(dst_np, src_ptr, nbytes):
-    hip = C.CDLL("libamdhip64.so")
-    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-    rc = hip.hipMemcpy(dst_np.ctypes.data, C.c_void_p(src_ptr), nbytes, 2)     # hipMemcpyDeviceToHost
-    if rc != 0:
-        raise RuntimeError("hipMemcpy D2H failed: %d" % rc)
+def _d2h(dst_np, src_ptr, nbytes, device=0):
+    """Device -> host through libtfidf's own HIP runtime (a separately loaded
+    libamdhip64 may be another runtime instance, e.g. PyTorch's)."""
+    from . import _lib as L
+    L.check(L.load().tfidf_device_copy(device, C.c_void_p(dst_np.ctypes.data), C.c_void_p(src_ptr), nbytes, 2))
 
 
-def _h2d(dst_ptr, src_np, nbytes):
-    hip = C.CDLL("libamdhip64.so")
-    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-    rc = hip.hipMemcpy(C.c_void_p(dst_ptr), src_np.ctypes.data, nbytes, 1)     # hipMemcpyHostToDevice
-    if rc != 0:
-        raise RuntimeError("hipMemcpy H2D failed: %d" % rc)
+def _h2d(dst_ptr, src_np, nbytes, device=0):
+    from . import _lib as L
+    L.check(L.load().tfidf_device_copy(device, C.c_void_p(dst_ptr), C.c_void_p(src_np.ctypes.data), nbytes, 1))
 
 
 class DeviceCorpus:
@@ -130,9 +126,9 @@ class DeviceCorpus:
         """(text uint8[], offsets uint64[n + 1]) of the first n_docs documents."""
         n = self.n_docs if n_docs is None else min(n_docs, self.n_docs)
         offs = np.zeros(n + 1, np.uint64)
-        _d2h(offs, self.d_offsets, (n + 1) * 8)
+        _d2h(offs, self.d_offsets, (n + 1) * 8, self.device)
         text = np.zeros(int(offs[n]), np.uint8)
-        _d2h(text, self.d_text, int(offs[n]))
+        _d2h(text, self.d_text, int(offs[n]), self.device)
         return text, offs
 
     def inject_unicode(self, frac, seed=SEED + 7):
@@ -148,7 +144,7 @@ class DeviceCorpus:
         starts = offs[pick][(offs[pick + 1] - offs[pick]) >= 4].astype(np.int64)
         text[starts] = 0xC3
         text[starts + 1] = 0xA9
-        _h2d(self.d_text, text, text.nbytes)
+        _h2d(self.d_text, text, text.nbytes, self.device)
         return int(starts.size)
 
     def free(self):
