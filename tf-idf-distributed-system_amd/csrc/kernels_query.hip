@@ -833,37 +833,38 @@ __global__ void __launch_bounds__(kPairWaves * 64) k_score_pairs(QueryParams p) 
 
 // ---------------------------------------------------------------------------
 // Workgroup per (query, doc-block range) unit — the batched top-k path for
-// plain disjunctions with k <= 64 (cfg 4, block-major postings).  The host
-// cuts each query into units of about kUnitPostings postings (heavy queries
-// into several block ranges).  Per block of the unit, for each query term in
-// query order, the 256 threads add the term's block segment into a dense LDS
-// accumulator of doubles (-0.0 = untouched: every term score is >= +0.0, so
-// -0.0 + s == s and the per-document value is the disjunction's double sum in
-// query order — terms are separated by a barrier); first touches set a bit.
-// Each wave then scans its quarter of the block's hit bits in doc order,
-// rounds the sums to float, keys them (score bits << 32 | ~doc) and keeps the
-// ones above its running k-th best key in a lane-held sorted top-k list
-// (lane j = j-th best).  Once a list is full almost every hit fails that one
-// compare, so there is no per-block selection pass, no candidate array per
-// (query, block) pair and no hash probing: the work is the postings.  At the
-// unit end wave 0 merges the four lists and writes them as the candidates of
-// pair (q, b0) (cand_n = 0 for the unit's other blocks); k_merge_topk orders
-// each query's candidates (several units for a split query).
+// heavy plain disjunctions with k <= 64 (cfg 4, block-major postings; the
+// light queries take k_score_wunits).  The host cuts each query into units of
+// about T/4096 postings (heavy queries into several block ranges).  Per block
+// of the unit, for each query term in query order, the 256 threads add the
+// term's block segment into a dense LDS accumulator of doubles: a document's
+// first touch (its bit in `bits`, set by the atomic that tests it) stores the
+// term score, later terms add to it — the disjunction's double sum in query
+// order, terms separated by a barrier.  Each wave then walks its quarter of
+// the block's touched documents in doc order, rounds the sums to float, keys
+// them (score bits << 32 | ~doc) and keeps the ones above its running k-th
+// best key in a lane-held sorted top-k list (lane j = j-th best); once that
+// key's score exceeds the lightest term's weight, documents only that term
+// touched are not walked at all (`obits`).  No per-block selection pass, no
+// candidate array per (query, block) pair, no hash probing.  At the unit end
+// wave 0 merges the four lists and writes them as the candidates of pair
+// (q, b0) (cand_n = 0 for the unit's other blocks); k_merge_topk orders each
+// query's candidates (several units for a split query).
 constexpr uint32_t kUnitThreads = 256;
 constexpr uint32_t kUnitWaves = kUnitThreads / 64;
 constexpr uint32_t kUnitU = 4;                 // postings per thread in flight
 constexpr uint32_t kUnitPre = 4;               // query terms whose first chunk is prefetched per block
-constexpr uint64_t kNegZeroBits = 0x8000000000000000ull;
 
 struct UnitSmem {
-  double acc[kBlockDocs];                      // -0.0 = untouched
+  double acc[kBlockDocs];                      // valid where bits is set
   uint32_t bits[kBlockDocs / 32];              // touched documents of the block
+  uint32_t obits[kBlockDocs / 32];             // touched by a term other than the lightest one
   float cache[256];
   uint64_t seg_a[2][64], seg_z[2][64];         // block segment of each query term (double-buffered)
   float tw[64];
   uint64_t lists[kUnitWaves][64];
   unsigned long long thr;                      // max of the waves' k-th keys: a bound for the unit's k-th key
-  uint32_t unit;
+  uint32_t unit, light;                        // the query term of least weight (BM25 bound of its score)
 };
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
@@ -927,11 +928,7 @@ __global__ void __launch_bounds__(kUnitThreads) k_score_units(QueryParams p, con
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t wid = (uint32_t)__builtin_amdgcn_readfirstlane((int)(tid >> 6));
   for (uint32_t i = tid; i < 256; i += kUnitThreads) sm.cache[i] = p.cache[i];
-  {
-    uint4 *a = reinterpret_cast<uint4 *>(sm.acc);
-    for (uint32_t i = tid; i < kBlockDocs / 2; i += kUnitThreads) a[i] = make_uint4(0, 0x80000000u, 0, 0x80000000u);
-    for (uint32_t i = tid; i < kBlockDocs / 32; i += kUnitThreads) sm.bits[i] = 0;
-  }
+  for (uint32_t i = tid; i < kBlockDocs / 32; i += kUnitThreads) sm.bits[i] = sm.obits[i] = 0;
   const uint32_t nb = p.n_blocks, k = p.k, C = p.C;
   for (;;) {
     if (tid == 0) {
@@ -945,9 +942,19 @@ __global__ void __launch_bounds__(kUnitThreads) k_score_units(QueryParams p, con
     const uint32_t q = un.x, b0 = un.y, b1 = un.z;
     const uint32_t t0 = p.q_off[q], nt = p.q_off[q + 1] - t0;  // <= 64 (host)
     uint32_t slot = kInvalidSlot;
+    float tw = 0.f;
     if (tid < nt) {
       slot = p.q_slot[t0 + tid];
-      sm.tw[tid] = p.q_w[t0 + tid];
+      tw = p.q_w[t0 + tid];
+      sm.tw[tid] = tw;
+    }
+    if (wid == 0) {                                             // the lightest term (least BM25 weight)
+      const uint32_t wb = lane < nt ? __float_as_uint(tw) : 0xFFFFFFFFu;   // weights > 0: bit order
+      uint32_t m = wb;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) m = min(m, (uint32_t)__shfl_xor((int)m, o, 64));
+      const uint64_t eq = __ballot(wb == m);
+      if (lane == 0) sm.light = (uint32_t)__builtin_ctzll(eq);
     }
     // block segment of term tid (block-major: bbase[b] + blk[b][slot] ..)
     auto segment = [&](uint32_t b, uint64_t *a, uint64_t *z) {
@@ -1000,6 +1007,7 @@ __global__ void __launch_bounds__(kUnitThreads) k_score_units(QueryParams p, con
       for (uint32_t j = 0; j < nt; j++) {
         const uint64_t a = sm.seg_a[par][j], z = sm.seg_z[par][j];
         const float wj = sm.tw[j];
+        const bool other = j != sm.light;
         for (uint64_t c0 = a; c0 < z; c0 += kUnitThreads * kUnitU) {
           uint32_t e[kUnitU];
           if (c0 == a && j < kUnitPre) {
@@ -1023,9 +1031,17 @@ __global__ void __launch_bounds__(kUnitThreads) k_score_units(QueryParams p, con
               uint32_t ld, tf, nrm;
               post_decode<false>(p, e[v], i, d0, &ld, &tf, &nrm);
               const float sc = bm25_term(wj, tf, sm.cache[nrm]);
-              const double old = sm.acc[ld];
-              sm.acc[ld] = old + (double)sc;
-              if ((uint64_t)__double_as_longlong(old) == kNegZeroBits) atomicOr(&sm.bits[ld >> 5], 1u << (ld & 31));
+              // acc[ld] is valid where bits has ld (set by an earlier term of this
+              // block): first touch stores the term score, later ones add to it
+              const uint32_t bm = 1u << (ld & 31);
+              if (j == 0) {
+                sm.acc[ld] = (double)sc;
+                atomicOr(&sm.bits[ld >> 5], bm);
+              } else {
+                const uint32_t ob = atomicOr(&sm.bits[ld >> 5], bm);
+                sm.acc[ld] = (ob & bm) ? sm.acc[ld] + (double)sc : (double)sc;
+              }
+              if (other) atomicOr(&sm.obits[ld >> 5], bm);
             }
           }
         }
@@ -1042,11 +1058,20 @@ __global__ void __launch_bounds__(kUnitThreads) k_score_units(QueryParams p, con
       // wave wid scans documents [2048 wid, 2048 wid + 2048): lane l owns bit word 64 wid + l
       // two hits per lane per step (both LDS round trips in flight); no key at
       // or below another wave's k-th key (sm.thr, read once per block) can win
+      // Once the k-th key's score exceeds the lightest term's weight w_l, a
+      // document touched by that term alone (score <= w_l: a BM25 term score
+      // never exceeds its weight) cannot enter the top-k: walk the documents
+      // some other term touched (obits) only.  Heavy queries are a frequent,
+      // low-idf term plus rarer ones: most hits are skipped unread.  (Skipping
+      // that term's postings themselves was measured slower: 5.7 -> 6.3 ms at
+      // cfg 4 — a wave of its postings almost always holds a few to score.)
       const uint32_t wi = wid * 64 + lane;
-      uint32_t wb = sm.bits[wi];
-      sm.bits[wi] = 0;
       uint64_t th = max(theta, (uint64_t)sm.thr);
       const uint64_t th_in = th;
+      const bool prune = nt > 1 && sm.tw[sm.light] < __uint_as_float((uint32_t)(th >> 32));
+      uint32_t wb = prune ? sm.obits[wi] : sm.bits[wi];
+      sm.bits[wi] = 0;
+      sm.obits[wi] = 0;
       while (__any(wb != 0)) {
         uint32_t x[2];
         bool has[2];
@@ -1060,7 +1085,6 @@ __global__ void __launch_bounds__(kUnitThreads) k_score_units(QueryParams p, con
 #pragma unroll
         for (int h = 0; h < 2; h++) {
           v[h] = has[h] ? sm.acc[x[h]] : 0.0;
-          if (has[h]) sm.acc[x[h]] = __longlong_as_double((long long)kNegZeroBits);
         }
 #pragma unroll
         for (int h = 0; h < 2; h++) {
