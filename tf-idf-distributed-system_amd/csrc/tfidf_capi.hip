@@ -1614,6 +1614,8 @@ extern "C" int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const 
   std::lock_guard<std::mutex> lk(ix->mu);
   if (!ix->committed) return fail(TFIDF_E_STATE, "search before commit");
   DeviceGuard g(ix->cfg.device);
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
   QueryBatch qb;
   if (int e = prepare_batch(ix, q_utf8, q_offsets, n_q, &qb)) return e;
   if (n_q == 0) return TFIDF_OK;
@@ -1621,15 +1623,29 @@ extern "C" int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const 
     memset(counts, 0, n_q * 4);
     return TFIDF_OK;
   }
+  const auto t1 = clk::now();
   int rc = run_scoring(ix, qb, n_q, k);
   if (rc) return rc;
+  const auto t2 = clk::now();
+  // results are contiguous on the device (doc | score | n): one copy into
+  // pinned memory, then into the caller's (usually pageable) arrays
   hipStream_t s = ix->stream;
-  HIP_TRY(hipMemcpyAsync(counts, ix->res_n, (size_t)n_q * 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(doc_ids, ix->res_doc, (size_t)n_q * k * 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(scores, ix->res_score, (size_t)n_q * k * 4, hipMemcpyDeviceToHost, s));
+  const size_t words = (size_t)2 * n_q * k + n_q;
+  HIP_TRY(ix->q_res.resize(words));
+  HIP_TRY(hipMemcpyAsync(ix->q_res.data(), ix->res_doc, words * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
+  ix->q_in_pending = false;
+  const auto t3 = clk::now();
+  memcpy(doc_ids, ix->q_res.data(), (size_t)n_q * k * 4);
+  memcpy(scores, ix->q_res.data() + (size_t)n_q * k, (size_t)n_q * k * 4);
+  memcpy(counts, ix->q_res.data() + (size_t)2 * n_q * k, (size_t)n_q * 4);
   ix->last_ms_scoring = ev_ms(ix, EV_Q0, EV_Q1);
   ix->last_ms_total = ev_ms(ix, EV_Q0, EV_Q2);
+  if (getenv("TFIDF_HOST_TIMING")) {          // profiling only
+    auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    fprintf(stderr, "batch %u: prepare %.3f  submit %.3f  wait %.3f  copy-out %.3f ms (device %.3f)\n", n_q,
+            ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, clk::now()), ix->last_ms_total);
+  }
   return TFIDF_OK;
 }
 
