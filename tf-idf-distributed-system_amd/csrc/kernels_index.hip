@@ -2067,6 +2067,8 @@ __device__ uint32_t csr_tf_of(const PostingParams &p, uint64_t d, uint32_t r, ui
 // one stream per 1024-thread workgroup 3.11 ms, 8 per 1024 2.87, 4 per 512 2.52)
 __global__ void __launch_bounds__(1024) k_scatter_sort(PostingParams p) {
   __shared__ uint32_t cur[kSubSlots + 1];                   // + no-op cursor for idle lanes
+  __shared__ uint8_t bnorm[kBlockDocs];                     // the block's norm bytes: an LDS read per entry
+                                                            // instead of a global load that waits on the temp word
   const uint32_t b = blockIdx.x, r = blockIdx.y;
   const uint32_t RS = 1u << p.range_shift;
   const uint32_t BS = RS < kSubSlots ? RS : kSubSlots;
@@ -2075,6 +2077,16 @@ __global__ void __launch_bounds__(1024) k_scatter_sort(PostingParams p) {
   const uint64_t bb = p.bbase[b];
   const uint32_t d0 = b * kBlockDocs;
   const uint32_t lane = threadIdx.x & 63;
+  {
+    const uint32_t nd = (uint32_t)min((uint64_t)kBlockDocs, p.n_docs - d0);
+    for (uint32_t i = threadIdx.x * 16; i < nd; i += blockDim.x * 16) {
+      if (i + 16 <= nd) {
+        *reinterpret_cast<uint4 *>(&bnorm[i]) = *reinterpret_cast<const uint4 *>(p.doc_norm + d0 + i);
+      } else {
+        for (uint32_t j = i; j < nd; j++) bnorm[j] = p.doc_norm[d0 + j];
+      }
+    }
+  }
   for (uint32_t k = blockIdx.z * p.sort_spw; k < min(nsub, (blockIdx.z + 1) * p.sort_spw); k++) {
     const size_t s0 = ((size_t)r << p.range_shift) + (size_t)k * BS;
     for (uint32_t i = threadIdx.x; i < BS; i += blockDim.x) cur[i] = row[s0 + i];
@@ -2092,7 +2104,7 @@ __global__ void __launch_bounds__(1024) k_scatter_sort(PostingParams p) {
 #pragma unroll
       for (int u = 0; u < U; u++) {
         const uint32_t e = e0 + u * blockDim.x + threadIdx.x;
-        nrm[u] = e < hi ? p.doc_norm[d0 + (x[u] & (kBlockDocs - 1))] : 0u;
+        nrm[u] = e < hi ? bnorm[x[u] & (kBlockDocs - 1)] : 0u;
       }
 #pragma unroll
       for (int u = 0; u < U; u++) {
