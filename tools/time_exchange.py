@@ -31,6 +31,8 @@ def main():
     D.global_commit(ad)
     ws, me = dist.get_world_size(), dist.get_rank()
     for rep in range(4):
+        if os.environ.get("COMMIT"):                  # as bench.py's step: a fresh commit first
+            idx.commit()
         T = []
         torch.cuda.synchronize()
         T.append(time.perf_counter())
@@ -59,6 +61,8 @@ def main():
         ad.import_global_df(back, dc, ttf)
         torch.cuda.synchronize()
         T.append(time.perf_counter())
+        if os.environ.get("COMMIT"):
+            idx.commit()
         t0 = time.perf_counter()
         D.global_commit(ad)
         torch.cuda.synchronize()
