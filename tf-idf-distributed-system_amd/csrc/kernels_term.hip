@@ -189,6 +189,34 @@ __global__ void __launch_bounds__(256) k_term_pairs(TermParams p) {
   }
 }
 
+// Long rows (book-sized documents, SURVEY cfg 1: ~24 k distinct terms per
+// row, a few hundred rows): four documents per wave would leave most of the
+// chip idle (300 books -> 75 waves), so workgroup (x, y) takes entries
+// y * 256 + t, stepping by gridDim.y * 256, of documents x, x + gridDim.x, ...
+__global__ void __launch_bounds__(256) k_term_pairs_wide(TermParams p) {
+  const uint32_t esc = csr_esc_value(p.slot_bits);
+  const TermLayout ly{p.slot_bits, p.doc_bits, p.tf_bits};
+  for (uint64_t d = blockIdx.x; d < p.n_docs; d += gridDim.x) {
+    const uint64_t src = p.live_map ? p.live_map[d] : d;
+    const uint64_t base = csr_row_base(p.offsets, src);
+    const uint32_t n = p.doc_nuniq[d], o = p.row_off[d], nrm = p.doc_norm[d];
+    for (uint32_t j = blockIdx.y * blockDim.x + threadIdx.x; j < n; j += gridDim.y * blockDim.x) {
+      const uint32_t e = p.csr[base + j], c = csr_local(e, p.slot_bits);
+      uint32_t t = csr_tf_field(e, p.slot_bits);
+      if (t == esc) t = csr_esc_tf(p.csr_esc, p.n_esc, base + j);
+      if (t > kMaxTf) atomicOr(p.err, kErrTfTooLarge);
+      if (t >= ly.tf_esc()) {
+        const uint32_t at = atomicAdd(p.tesc_count, 1u);
+        if (at < p.tesc_cap) {
+          p.tesc[2 * (uint64_t)at] = ((uint64_t)c << kTermDocBits) | d;
+          p.tesc[2 * (uint64_t)at + 1] = min(t, kMaxTf);
+        }
+      }
+      p.keys[o + j] = ly.pack(c, d, t, nrm);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // LSD radix passes (8-bit digits of the key bits from `shift`)
 
@@ -333,6 +361,13 @@ uint64_t term_invert_scratch_words(uint64_t n_docs, uint64_t nnz, uint32_t C) {
 hipError_t launch_term_pairs(const TermParams &p, hipStream_t s) {
   hipError_t e = scan_u32_excl(p.doc_nuniq, p.row_off, p.n_docs, p.scratch, s);
   if (e != hipSuccess) return e;
+  if (p.n_docs && p.nnz / p.n_docs > 2048) {                  // long rows: many workgroups per row
+    const uint64_t avg = p.nnz / p.n_docs;
+    const unsigned gy = (unsigned)std::min<uint64_t>((avg + 1023) / 1024, 64);
+    const unsigned gx = (unsigned)std::min<uint64_t>(p.n_docs, 1u << 16);
+    hipLaunchKernelGGL(k_term_pairs_wide, dim3(gx, gy), dim3(256), 0, s, p);
+    return hipGetLastError();
+  }
   const uint64_t waves = std::min<uint64_t>((p.n_docs + 3) / 4, 1ull << 18);
   if (waves) hipLaunchKernelGGL(k_term_pairs, dim3((unsigned)((waves + 3) / 4)), dim3(256), 0, s, p);
   return hipGetLastError();
