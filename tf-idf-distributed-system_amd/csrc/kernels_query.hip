@@ -18,6 +18,8 @@
 //                  in LDS -> (score desc, doc asc).
 #include <hip/hip_runtime.h>
 
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "tfidf_common.h"
@@ -1463,8 +1465,100 @@ hipError_t launch_score_blocks(const QueryParams &p, hipStream_t s) {
   else score_blocks_layout<false>(p, grid, s);
   return hipGetLastError();
 }
+// Wave per query: the same merge for up to kMergeWaveRegs x 64 candidate slots
+// (n_blocks x k; cfg 2: 123 x 10) and k <= 64, all in registers — no
+// workgroup barriers (k_merge_topk's 1024-thread radix passes: 17 us for one
+// query).  Keys are unique: radix select of the k-th largest from the first
+// differing bit (8-bit digits, wave histogram in LDS, wave_select_bin), then
+// the winners are gathered one per lane and bitonic-sorted (descending).
+constexpr int kMergeWaveRegs = 32;
+constexpr uint32_t kMergeWavesPerWG = 4;
+
+__global__ void __launch_bounds__(64 * kMergeWavesPerWG) k_merge_topk_wave(QueryParams p) {
+  __shared__ uint32_t hist_all[kMergeWavesPerWG][256];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t q = blockIdx.x * kMergeWavesPerWG + w;
+  uint32_t *hist = hist_all[w];
+  for (uint32_t i = lane; i < 256; i += 64) hist[i] = 0;
+  if (q >= p.n_q) return;                                   // wave-uniform; the wave owns its histogram
+  const uint32_t k = p.k, nb = p.n_blocks, nflat = nb * k;
+  const uint64_t *cand = p.cand + (size_t)q * nflat;
+  const uint32_t *cn = p.cand_n + (size_t)q * nb;
+  const uint32_t inv = (uint32_t)((0xFFFFFFFFull + k) / k);   // f / k = umulhi(f, inv) (f < 2^11, 2 <= k <= 64)
+  uint64_t kv[kMergeWaveRegs];
+  uint64_t lmin = ~0ull, lmax = 0;
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int r = 0; r < kMergeWaveRegs; r++) {
+    const uint32_t f = lane + 64u * r;
+    kv[r] = 0;
+    if (f < nflat) {
+      const uint32_t b = k == 1 ? f : __umulhi(f, inv);
+      if (f - b * k < cn[b]) kv[r] = cand[f];
+    }
+    if (kv[r]) { lmin = min(lmin, kv[r]); lmax = max(lmax, kv[r]); cnt++; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    cnt += (uint32_t)__shfl_xor((int)cnt, o, 64);
+    lmin = min(lmin, (uint64_t)__shfl_xor((long long)lmin, o, 64));
+    lmax = max(lmax, (uint64_t)__shfl_xor((long long)lmax, o, 64));
+  }
+  const uint32_t M = cnt, kk = M < k ? M : k;
+  uint64_t T = 1, tmask = ~0ull;                            // take (key & tmask) >= T (keys > 0)
+  if (M > k) {
+    int rb = 64 - __builtin_clzll(lmin ^ lmax);
+    uint64_t prefix = rb < 64 ? lmax & (~0ull << rb) : 0ull;
+    uint32_t rem = k;
+    while (rb > 0) {
+      const int wd = rb < 8 ? rb : 8, sh = rb - wd;
+      const uint64_t hmask = rb < 64 ? (~0ull << rb) : 0ull;
+      const uint32_t dmask = (1u << wd) - 1;
+#pragma unroll
+      for (int r = 0; r < kMergeWaveRegs; r++)
+        if (kv[r] && (kv[r] & hmask) == prefix) atomicAdd(&hist[(uint32_t)(kv[r] >> sh) & dmask], 1u);
+      uint32_t above;
+      const uint32_t bin = wave_select_bin(hist, rem, &above);
+      const uint32_t inbin = hist[bin];
+#pragma unroll
+      for (int i = 0; i < 4; i++) hist[lane + 64 * i] = 0;
+      prefix |= (uint64_t)bin << sh;
+      rem -= above;
+      rb = sh;
+      if (inbin == rem) break;
+    }
+    tmask = ~0ull << rb;
+    T = prefix;
+  }
+  // gather the kk winners one per lane (lane order = flat order), sort descending
+  uint64_t mine = 0;
+  uint32_t base = 0;
+#pragma unroll
+  for (int r = 0; r < kMergeWaveRegs; r++) {
+    const bool take = kv[r] && (kv[r] & tmask) >= T;
+    const uint64_t m = __ballot(take);
+    const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+    // lane `pos` receives this key: scatter through the LDS histogram space
+    if (take) reinterpret_cast<uint64_t *>(hist)[pos & 127] = kv[r];
+    base += (uint32_t)__popcll(m);
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (lane < kk) mine = reinterpret_cast<uint64_t *>(hist)[lane];
+#pragma unroll
+  for (uint32_t size = 2; size <= 64; size <<= 1) mine = bitonic_stages(mine, lane, size);
+  if (lane < kk) {
+    p.out_doc[(size_t)q * k + lane] = ~(uint32_t)(mine & 0xFFFFFFFFu);
+    p.out_score[(size_t)q * k + lane] = __uint_as_float((uint32_t)(mine >> 32));
+  }
+  if (lane == 0) p.out_n[q] = kk;
+}
+
 hipError_t launch_merge_topk(const QueryParams &p, hipStream_t s) {
-  hipLaunchKernelGGL(k_merge_topk, dim3(p.n_q), dim3(1024), 0, s, p);
+  if (p.k <= 64 && (uint64_t)p.n_blocks * p.k <= 64u * kMergeWaveRegs && !getenv("TFIDF_MERGE_WG"))
+    hipLaunchKernelGGL(k_merge_topk_wave, dim3((p.n_q + kMergeWavesPerWG - 1) / kMergeWavesPerWG),
+                       dim3(64 * kMergeWavesPerWG), 0, s, p);
+  else
+    hipLaunchKernelGGL(k_merge_topk, dim3(p.n_q), dim3(1024), 0, s, p);
   return hipGetLastError();
 }
 
