@@ -176,6 +176,10 @@ int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const uint64_t *q
                        uint32_t k, uint32_t *doc_ids, float *scores, uint32_t *counts);
 /* Per-query device time of the last search call (HIP events, index stream). */
 int tfidf_last_search_ms(const tfidf_index *ix, float *ms_scoring, float *ms_total);
+/* Device-time measurement of searches (HIP events around scoring; on by
+ * default).  Off for serving: the three event records cost ~17 us per single
+ * query (cfg 2: 72 -> 55 us p50); tfidf_last_search_ms then reports -1. */
+int tfidf_set_query_timing(tfidf_index *ix, int on);
 
 /* ---- device-resident results (multi-GPU orchestration; no reference
  * counterpart: they feed the RCCL all-gather that replaces Leader.java:51-70) ----

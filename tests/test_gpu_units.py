@@ -120,3 +120,21 @@ def test_units_not_for_large_k_or_long_queries(corpus):
     docs, scores, counts = g.search_batch(long_q, 10)
     assert g.stats()["unit_batches"] == before
     assert rows(docs, scores, counts, len(long_q) - 1) == want(o, long_q[-1], 10)
+
+
+def test_query_timing_toggle(corpus):
+    # serving configuration: no HIP events around searches (tfidf_set_query_timing)
+    g, o = corpus
+    qs = queries()[:50]
+    g.set_query_timing(False)
+    try:
+        off = [g.search(q, 10) for q in qs[:20]]
+        assert g.last_search_ms() == (-1.0, -1.0)
+        d_off, s_off, c_off = g.search_batch(qs, 10)
+    finally:
+        g.set_query_timing(True)
+    on = [g.search(q, 10) for q in qs[:20]]
+    assert g.last_search_ms()[1] > 0
+    d_on, s_on, c_on = g.search_batch(qs, 10)
+    assert off == on
+    assert (c_off == c_on).all() and (d_off == d_on).all() and (s_off.view("i4") == s_on.view("i4")).all()

@@ -221,6 +221,7 @@ struct tfidf_index {
   PinnedVec<uint32_t> q_host, q_res;
   std::vector<uint32_t> q_units;       // batch scoring units {q, b0, b1, 0} (run_scoring)
   uint64_t unit_batches = 0, unit_count = 0;
+  bool q_timing = true;                // record HIP events around each search (tfidf_set_query_timing)
   hipEvent_t q_ev[2] = {nullptr, nullptr};  // fork / join of the wave-unit kernel on copy_stream
   hipEvent_t q_in_ev = nullptr;        // the last upload out of q_host
   bool q_in_pending = false;
@@ -691,6 +692,7 @@ static int upload_cache(tfidf_index *ix, bool sync = true) {
 
 static float ev_ms(tfidf_index *ix, int a, int b) {
   float ms = 0;
+  if (a >= EV_Q0 && !ix->q_timing) return -1.0f;   // query timing off: not measured
   hipEventElapsedTime(&ms, ix->ev[a], ix->ev[b]);
   return ms;
 }
@@ -1478,7 +1480,7 @@ static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint
     qp.hits = ix->hits.as<uint64_t>();
     qp.hits_n = ix->hits_n.as<uint32_t>();
   }
-  HIP_TRY(hipEventRecord(ix->ev[EV_Q0], s));
+  if (ix->q_timing) HIP_TRY(hipEventRecord(ix->ev[EV_Q0], s));
   if (unit_path) {
     HIP_TRY(ix->ovf.reserve(64));
     uint32_t *ctr = ix->ovf.as<uint32_t>();
@@ -1511,9 +1513,9 @@ static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint
       HIP_TRY(hipEventRecord(ix->q_ev[1], ws));
       HIP_TRY(hipStreamWaitEvent(s, ix->q_ev[1], 0));
     }
-    HIP_TRY(hipEventRecord(ix->ev[EV_Q1], s));
+    if (ix->q_timing) HIP_TRY(hipEventRecord(ix->ev[EV_Q1], s));
     HIP_TRY(launch_merge_topk(qp, s));
-    HIP_TRY(hipEventRecord(ix->ev[EV_Q2], s));
+    if (ix->q_timing) HIP_TRY(hipEventRecord(ix->ev[EV_Q2], s));
     return TFIDF_OK;
   }
   if (batch) {
@@ -1544,9 +1546,9 @@ static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint
     }
   }
   HIP_TRY(launch_score_blocks(qp, s));
-  HIP_TRY(hipEventRecord(ix->ev[EV_Q1], s));
+  if (ix->q_timing) HIP_TRY(hipEventRecord(ix->ev[EV_Q1], s));
   if (k) HIP_TRY(launch_merge_topk(qp, s));
-  HIP_TRY(hipEventRecord(ix->ev[EV_Q2], s));
+  if (ix->q_timing) HIP_TRY(hipEventRecord(ix->ev[EV_Q2], s));
   return TFIDF_OK;
 }
 
@@ -1591,7 +1593,7 @@ extern "C" int tfidf_search(tfidf_index *ix, const uint8_t *q, uint64_t q_len, u
   HIP_TRY(launch_hits_order(ix->hits.as<uint64_t>(), ix->hits_n.as<uint32_t>(), R, ix->hits_P.as<uint64_t>(),
                             ix->hits_c.as<uint64_t>(), ix->hits.as<uint64_t>(), ix->out_doc.as<uint32_t>(),
                             ix->out_score.as<float>(), nullptr, 0, ix->num_cus * 4, s));
-  HIP_TRY(hipEventRecord(ix->ev[EV_Q2], s));
+  if (ix->q_timing) HIP_TRY(hipEventRecord(ix->ev[EV_Q2], s));
   uint64_t H = 0;
   HIP_TRY(hipMemcpyAsync(&H, ix->hits_P.as<uint64_t>() + R, 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
@@ -1741,6 +1743,13 @@ extern "C" int tfidf_search_coalesced(tfidf_index *ix, const uint8_t *q, uint64_
   return TFIDF_OK;
 }
 
+extern "C" int tfidf_set_query_timing(tfidf_index *ix, int on) {
+  if (!ix) return fail(TFIDF_E_INVALID_ARG, "NULL index");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  ix->q_timing = on != 0;
+  return TFIDF_OK;
+}
+
 extern "C" int tfidf_last_search_ms(const tfidf_index *ix, float *ms_scoring, float *ms_total) {
   if (!ix) return fail(TFIDF_E_INVALID_ARG, "NULL index");
   if (ms_scoring) *ms_scoring = ix->last_ms_scoring;
@@ -1807,7 +1816,7 @@ extern "C" int tfidf_search_all_keys_device(tfidf_index *ix, const uint8_t *q, u
   HIP_TRY(launch_hits_order(ix->hits.as<uint64_t>(), ix->hits_n.as<uint32_t>(), R, ix->hits_P.as<uint64_t>(),
                             ix->hits_c.as<uint64_t>(), ix->hits.as<uint64_t>(), nullptr, nullptr,
                             static_cast<uint64_t *>(d_keys), doc_base, ix->num_cus * 4, s));
-  HIP_TRY(hipEventRecord(ix->ev[EV_Q2], s));
+  if (ix->q_timing) HIP_TRY(hipEventRecord(ix->ev[EV_Q2], s));
   HIP_TRY(hipMemcpyAsync(n_out, ix->hits_P.as<uint64_t>() + R, 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   ix->last_ms_scoring = ev_ms(ix, EV_Q0, EV_Q1);

@@ -96,6 +96,7 @@ SIGNATURES = {
                                          C.c_uint32]),
     "tfidf_search_batch": (C.c_int, [VP, C.c_char_p, U64P, C.c_uint32, C.c_uint32, U32P, F32P, U32P]),
     "tfidf_last_search_ms": (C.c_int, [VP, F32P, F32P]),
+    "tfidf_set_query_timing": (C.c_int, [VP, C.c_int]),
     "tfidf_search_batch_keys_device": (C.c_int, [VP, C.c_char_p, U64P, C.c_uint32, C.c_uint32, C.c_uint64, VP]),
     "tfidf_search_all_keys_device": (C.c_int, [VP, C.c_char_p, C.c_uint64, C.c_uint64, VP, C.c_uint64, U64P]),
     "tfidf_set_stream": (C.c_int, [VP, VP]),

@@ -192,6 +192,10 @@ class ShardIndex:
         """Issue device work on the caller's HIP stream (int handle); None = the index's own stream."""
         L.check(L.load().tfidf_set_stream(self._h, L.OWN_STREAM if stream is None else C.c_void_p(stream)))
 
+    def set_query_timing(self, on: bool):
+        """HIP-event device timing of searches (on by default; off for serving)."""
+        L.check(L.load().tfidf_set_query_timing(self._h, 1 if on else 0))
+
     def last_search_ms(self):
         a, b = C.c_float(), C.c_float()
         L.check(L.load().tfidf_last_search_ms(self._h, C.byref(a), C.byref(b)))
