@@ -554,6 +554,26 @@ __device__ __forceinline__ uint32_t bucket_probe(ulonglong2 e, uint32_t s, uint6
   return hit ? (f0 ? s : s + 1) : kLookupPending;
 }
 
+// The same over the aligned 4-slot group of s (two 16 B loads, e0 = slots
+// 0-1, e1 = slots 2-3; slots >= s considered in probe order): a key displaced
+// by up to three slots from its home is found in the first round.
+__device__ __forceinline__ uint32_t group_probe(ulonglong2 e0, ulonglong2 e1, uint32_t s, uint64_t lo,
+                                                uint32_t *claim) {
+  const uint32_t g0 = s & ~3u, off = s & 3u;
+  const uint64_t v[4] = {e0.x, e0.y, e1.x, e1.y};
+  uint32_t hit = kLookupPending, cl = kInvalidSlot;
+#pragma unroll
+  for (int i = 3; i >= 0; i--) {                           // the lowest slot >= s decides
+    if ((uint32_t)i >= off) {
+      const bool f = v[i] == lo, z = v[i] == 0;
+      hit = f ? g0 + i : (z ? kLookupPending : hit);
+      cl = f ? kInvalidSlot : (z ? g0 + i : cl);
+    }
+  }
+  *claim = cl;
+  return hit;
+}
+
 // Claim slot cs for short key lo (CAS on lo, then publish hi).  Returns the
 // slot if it now holds lo, else kLookupPending with *s advanced past cs.
 __device__ __forceinline__ uint32_t dict_claim_short(uint64_t *dict, uint32_t mask, uint32_t cs, uint64_t lo,
@@ -843,7 +863,7 @@ __device__ __forceinline__ void hist_batch(WaveSmem &sm, const BuildParams &p, u
 // lengths / term counts accumulated into pk_len / pk_nu).  Short keys by
 // bucket probes with all of a lane's loads in flight, unresolved ones through
 // a one-per-lane retry queue; folded (> 8 byte) keys one per lane at a time.
-template <bool PACK>
+template <bool PACK, bool G4>
 __device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p, uint32_t lane, uint32_t nu,
                                               uint32_t doc, uint32_t *g, uint32_t *tf, uint32_t *tdoc,
                                               uint32_t &actm, uint32_t *pk_len, uint32_t *pk_nu, uint64_t wbase) {
@@ -923,12 +943,18 @@ __device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p
         uint32_t qs = qm.x, qg = qa ? kLookupPending : kInvalidSlot;
         for (uint32_t it = 0; it < dmask + 4096 && __any(qg == kLookupPending); it++) {
           if (qg == kLookupPending) {
-            const ulonglong2 e = *reinterpret_cast<const ulonglong2 *>(p.dict + (qs & ~1u));
             uint32_t cs;
-            qg = bucket_probe(e, qs, ql, &cs);
+            if constexpr (G4) {
+              const ulonglong2 e0 = *reinterpret_cast<const ulonglong2 *>(p.dict + (qs & ~3u));
+              const ulonglong2 e1 = *reinterpret_cast<const ulonglong2 *>(p.dict + (qs & ~3u) + 2);
+              qg = group_probe(e0, e1, qs, ql, &cs);
+            } else {
+              const ulonglong2 e = *reinterpret_cast<const ulonglong2 *>(p.dict + (qs & ~1u));
+              qg = bucket_probe(e, qs, ql, &cs);
+            }
             if (qg == kLookupPending) {
               if (cs != kInvalidSlot) qg = dict_claim_short(p.dict, dmask, cs, ql, &qs);
-              else qs = ((qs | 1u) + 1u) & dmask;
+              else qs = ((qs | (G4 ? 3u : 1u)) + 1u) & dmask;
             }
           }
         }
@@ -940,21 +966,30 @@ __device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p
         break;
       }
       if (round > dmask) break;                          // table exhausted: capacity error below
-      ulonglong2 e[kWaveK];
+      // G4 (dictionaries of >= 2^21 slots, outside L2): the aligned 4-slot group
+      // of each probe (two 16 B loads) — fewer dependent rounds at high load
+      // (cfg 5: tokenize 14.9 -> 12.9 ms); 2-slot buckets otherwise (the extra
+      // registers spill: cfg 2 8.27 -> 8.77 ms)
+      ulonglong2 e0[kWaveK], e1[G4 ? kWaveK : 1];
 #pragma unroll
-      for (int k = 0; k < (int)kWaveK; k++)
-        e[k] = *reinterpret_cast<const ulonglong2 *>(p.dict + (g[k] == kLookupPending ? (ps[k] & ~1u) : 0u));
+      for (int k = 0; k < (int)kWaveK; k++) {
+        const uint32_t gs = g[k] == kLookupPending ? (ps[k] & (G4 ? ~3u : ~1u)) : 0u;
+        e0[k] = *reinterpret_cast<const ulonglong2 *>(p.dict + gs);
+        if constexpr (G4) e1[k] = *reinterpret_cast<const ulonglong2 *>(p.dict + gs + 2);
+      }
       uint32_t cs[kWaveK];
       bool anyclaim = false;
 #pragma unroll
       for (int k = 0; k < (int)kWaveK; k++) {
         const bool pend = g[k] == kLookupPending;
         uint32_t c;
-        const uint32_t r = bucket_probe(e[k], ps[k], lo[k], &c);
+        uint32_t r;
+        if constexpr (G4) r = group_probe(e0[k], e1[k], ps[k], lo[k], &c);
+        else r = bucket_probe(e0[k], ps[k], lo[k], &c);
         cs[k] = pend ? c : kInvalidSlot;
         anyclaim |= pend & (c != kInvalidSlot);
         const bool adv = pend & (r == kLookupPending) & (c == kInvalidSlot);
-        ps[k] = adv ? (((ps[k] | 1u) + 1u) & dmask) : ps[k];
+        ps[k] = adv ? (((ps[k] | (G4 ? 3u : 1u)) + 1u) & dmask) : ps[k];
         g[k] = pend ? r : g[k];
       }
       if (__any(anyclaim)) {
@@ -979,7 +1014,7 @@ __device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p
 // sharing one window.  A pack that cannot take the packed path (window or
 // token/term capacity, non-contiguous sources, an empty or non-ASCII document)
 // sends its documents to retry_list for a PACK = false pass.
-template <bool PACK>
+template <bool PACK, bool G4>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_tokenize_wave(BuildParams p) {
   __shared__ WaveSmem sm;
   const uint32_t lane = threadIdx.x;
@@ -1159,7 +1194,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     // ---- dictionary slots of terms lane + 64k
     uint32_t g[kWaveK], tf[kWaveK], tdoc[kWaveK];
     uint32_t actm = 0;
-    resolve_terms<PACK>(sm, p, lane, nu, (uint32_t)d, g, tf, tdoc, actm, pk_len, pk_nu, s0 - shift);
+    resolve_terms<PACK, G4>(sm, p, lane, nu, (uint32_t)d, g, tf, tdoc, actm, pk_len, pk_nu, s0 - shift);
     if (p.debug_stop == 4) { clear_table(sm, lane); continue; }
 
     // ---- CSR row grouped by dictionary range (8 ranges per pass), staged in LDS.
@@ -1446,7 +1481,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     }
     uint32_t g[kWaveK], tf[kWaveK], tdoc[kWaveK];
     uint32_t actm = 0;
-    resolve_terms<false>(sm, p, lane, nu, (uint32_t)m.d, g, tf, tdoc, actm, nullptr, nullptr, m.s0 - m.shift);
+    resolve_terms<false, false>(sm, p, lane, nu, (uint32_t)m.d, g, tf, tdoc, actm, nullptr, nullptr, m.s0 - m.shift);
     uint32_t *dense = p.dense + (uint64_t)m.gi * C;
 #pragma unroll
     for (int k = 0; k < (int)kWaveK; k++)
@@ -2153,8 +2188,14 @@ hipError_t launch_verify_deferred(const BuildParams &p, hipStream_t s) {
 }
 
 hipError_t launch_tokenize_wave(const BuildParams &p, int grid, hipStream_t s) {
-  if (p.pack > 1) hipLaunchKernelGGL(k_tokenize_wave<true>, dim3(grid), dim3(64), 0, s, p);
-  else hipLaunchKernelGGL(k_tokenize_wave<false>, dim3(grid), dim3(64), 0, s, p);
+  const bool g4 = (uint64_t)p.cap_mask + 1 >= (1ull << 21);   // dictionary beyond L2: 4-slot probe groups
+  if (p.pack > 1) {
+    if (g4) hipLaunchKernelGGL((k_tokenize_wave<true, true>), dim3(grid), dim3(64), 0, s, p);
+    else hipLaunchKernelGGL((k_tokenize_wave<true, false>), dim3(grid), dim3(64), 0, s, p);
+  } else {
+    if (g4) hipLaunchKernelGGL((k_tokenize_wave<false, true>), dim3(grid), dim3(64), 0, s, p);
+    else hipLaunchKernelGGL((k_tokenize_wave<false, false>), dim3(grid), dim3(64), 0, s, p);
+  }
   return hipGetLastError();
 }
 hipError_t launch_tokenize_chunks(const BuildParams &p, int grid, hipStream_t s) {
