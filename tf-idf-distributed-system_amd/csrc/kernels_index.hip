@@ -1197,9 +1197,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     resolve_terms<PACK, G4>(sm, p, lane, nu, (uint32_t)d, g, tf, tdoc, actm, pk_len, pk_nu, s0 - shift);
     if (p.debug_stop == 4) { clear_table(sm, lane); continue; }
 
-    // ---- CSR row grouped by dictionary range (8 ranges per pass), staged in LDS.
-    // Eight 16-bit range counters per lane live in two u64 words (ranges 0-3,
-    // 4-7): field access is one 64-bit select + shift, no branches.
+    // ---- CSR row grouped by dictionary range (PACK: by (document, range)),
+    // staged in LDS.  G <= kWaveGroups groups (host: pack <= kWaveGroups / R).
     uint32_t *st_col = reinterpret_cast<uint32_t *>(sm.key);
     uint32_t *st_tf = st_col + kWaveSlots;
     const uint32_t st_noop = kWaveSlots - 64 + lane;          // unused staging words (nu <= kWaveTerms)
@@ -1207,6 +1206,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     // is one contiguous run of the staging area starting at pk_start[j]
     const uint32_t rbits = (uint32_t)__builtin_ctz(R);
     const uint32_t G = PACK ? np << rbits : R;
+    if (PACK && G > kWaveGroups) {                          // cannot happen (host pack limit)
+      clear_table(sm, lane);
+      defer_pack(p, d, np, lane);
+      continue;
+    }
     if (PACK) {
       const uint32_t nuj = lane < np ? pk_nu[lane] : 0u;
       const uint32_t incl = wave_incl_add(nuj);
@@ -1215,59 +1219,41 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         pk_row[lane] = (pofs + src + lane) >> 1;             // csr_row_base of document src + lane
       }
     }
-    uint32_t run = 0;
-    for (uint32_t rb = 0; rb < G; rb += 8) {
-      uint64_t c0 = 0, c1 = 0;
-      uint32_t fk[kWaveK];
+    // Group ranks by LDS atomics on per-group counters in the count array
+    // (consumed by resolve_terms): [0, 128) counters, then exclusive group
+    // bases; idle terms bump no-op counters [128, 192).  Order inside a
+    // (document, range) segment is free (one entry per slot).  Replaces the
+    // packed 16-bit range-field wave scans of round 2 (~20 -> ~8 VALU per term).
+    static_assert(kWaveGroups == 128 && kWaveSlots / 2 >= 192, "group counters");
+    uint32_t *gcnt = sm.cnt;
+    gcnt[lane] = 0;
+    gcnt[lane + 64] = 0;
+    uint32_t grp[kWaveK], rank[kWaveK];
 #pragma unroll
-      for (int k = 0; k < (int)kWaveK; k++) {
-        const uint32_t f = (PACK ? (tdoc[k] << rbits) + (g[k] >> p.range_shift) : (g[k] >> p.range_shift)) - rb;
-        const bool inr = ((actm >> k) & 1u) && f < 8;
-        fk[k] = inr ? f : 8u;                                  // 8 = not in this pass
-        const uint64_t inc = inr ? (1ull << (16 * (f & 3))) : 0ull;
-        c0 += (f & 4) ? 0ull : inc;
-        c1 += (f & 4) ? inc : 0ull;
-      }
-      // wave exclusive scan of the 8 fields (4 u32 words) + totals
-      uint32_t w[4] = {(uint32_t)c0, (uint32_t)(c0 >> 32), (uint32_t)c1, (uint32_t)(c1 >> 32)};
-      uint32_t tot[4];
+    for (int k = 0; k < (int)kWaveK; k++) {
+      const bool act = (actm >> k) & 1u;
+      grp[k] = act ? (PACK ? (tdoc[k] << rbits) + (g[k] >> p.range_shift) : (g[k] >> p.range_shift)) : 128u + lane;
+      rank[k] = atomicAdd(&gcnt[grp[k]], 1u);
+    }
+    const uint32_t c0 = gcnt[lane], c1 = gcnt[lane + 64];
+    const uint32_t i0 = wave_incl_add(c0);
+    const uint32_t i1 = wave_incl_add(c1) + (uint32_t)__builtin_amdgcn_readlane((int)i0, 63);
+    gcnt[lane] = i0 - c0;
+    gcnt[lane + 64] = i1 - c1;
 #pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const uint32_t incl = wave_incl_add(w[i]);
-        tot[i] = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-        w[i] = incl - w[i];
+    for (int h = 0; h < 2; h++) {
+      const uint32_t gg = lane + 64 * h, e = h ? i1 : i0;
+      if (gg < G) {
+        if (PACK) p.rsplit[(d + (gg >> rbits)) * R + (gg & (R - 1))] = e - pk_start[gg >> rbits];
+        else p.rsplit[d * R + gg] = e;
       }
-      // exclusive scan of the 8 totals (wave-uniform), packed the same way
-      uint64_t fb0 = 0, fb1 = 0;
-      uint32_t acc = 0, lane_base = 0, lane_tot = 0;
+    }
 #pragma unroll
-      for (int f = 0; f < 8; f++) {
-        const uint32_t t = (tot[f >> 1] >> (16 * (f & 1))) & 0xFFFFu;
-        if (f < 4) fb0 |= (uint64_t)acc << (16 * f); else fb1 |= (uint64_t)acc << (16 * (f - 4));
-        if ((uint32_t)f == lane) { lane_base = acc; lane_tot = t; }
-        acc += t;
-      }
-      if (!PACK && lane < 8 && rb + lane < R) p.rsplit[d * R + rb + lane] = run + lane_base + lane_tot;
-      if (PACK && lane < 8 && rb + lane < G) {
-        const uint32_t gg = rb + lane, j = gg >> rbits;
-        p.rsplit[(d + j) * R + (gg & (R - 1))] = run + lane_base + lane_tot - pk_start[j];
-      }
-      uint64_t pk0 = ((uint64_t)w[0] | ((uint64_t)w[1] << 32)) + fb0;
-      uint64_t pk1 = ((uint64_t)w[2] | ((uint64_t)w[3] << 32)) + fb1;
-#pragma unroll
-      for (int k = 0; k < (int)kWaveK; k++) {
-        const uint32_t f = fk[k];
-        const bool inr = f < 8;
-        const uint64_t wsel = (f & 4) ? pk1 : pk0;
-        const uint32_t sh = 16 * (f & 3);
-        const uint32_t pos = inr ? run + ((uint32_t)(wsel >> sh) & 0xFFFFu) : st_noop;
-        const uint64_t inc = inr ? (1ull << sh) : 0ull;
-        pk0 += (f & 4) ? 0ull : inc;
-        pk1 += (f & 4) ? inc : 0ull;
-        st_col[pos] = g[k];
-        st_tf[pos] = PACK ? tf[k] | (tdoc[k] << 24) : tf[k];
-      }
-      run += acc;
+    for (int k = 0; k < (int)kWaveK; k++) {
+      const bool act = (actm >> k) & 1u;
+      const uint32_t pos = act ? gcnt[grp[k]] + rank[k] : st_noop;
+      st_col[pos] = g[k];
+      st_tf[pos] = PACK ? tf[k] | (tdoc[k] << 24) : tf[k];
     }
     asm volatile("" ::: "memory");
     if (PACK) {
@@ -1758,7 +1744,10 @@ __device__ __forceinline__ void doc_segment(const PostingParams &p, uint64_t d, 
 // the next group's segment loads before the current group's LDS atomics and
 // stores (gfx9 counts stores in vmcnt: waiting for loads issued after a
 // store would also wait for the store).
-constexpr int kInvDocs = 8;
+#ifndef TFIDF_INV_DOCS
+#define TFIDF_INV_DOCS 8
+#endif
+constexpr int kInvDocs = TFIDF_INV_DOCS;   // A/B: -DTFIDF_INV_DOCS=16
 
 struct InvGroup {               // wave-uniform
   uint64_t base[kInvDocs];

@@ -764,6 +764,7 @@ static int commit_once(tfidf_index *ix) {
     const uint64_t avg = ix->n_staged ? ix->text_bytes / ix->n_staged : 0;
     if (avg) pack = (uint32_t)std::min<uint64_t>(kPackMaxDocs, std::max<uint64_t>(1, kPackBytes / avg));
     if (const char *e = getenv("TFIDF_PACK_DOCS")) pack = (uint32_t)std::max(1, std::min(atoi(e), (int)kPackMaxDocs));
+    pack = std::min(pack, std::max(1u, kWaveGroups / ix->R));   // (document, range) groups per unit
   }
   if (pack > 1) HIP_TRY(ix->retry_list.reserve(N * 4 + 4));
   if (ix->term_major) {

@@ -192,6 +192,7 @@ struct PostingParams {
 // --- launch wrappers (kernels_index.hip) ---
 hipError_t launch_tokenize_wave(const BuildParams &p, int grid, hipStream_t s);
 constexpr uint32_t kWaveWGsPerCU = 8;       // 64-thread workgroups per CU (2 waves/SIMD: VGPR- and LDS-bound)
+constexpr uint32_t kWaveGroups = 128;     // CSR row groups per wave unit (documents x ranges, k_tokenize_wave)
 constexpr uint32_t kPackMaxDocs = 16;     // documents per packed window (<= kPackMax, kernels_index.hip)
 constexpr uint64_t kPackBytes = 2560;     // text per packed window (auto pack size): ~450 tokens, under the
                                           // wave table's 512 distinct terms (cfg 5: 7 docs, tokenize 16.3 -> 14.9 ms)
