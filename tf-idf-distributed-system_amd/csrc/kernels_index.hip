@@ -970,27 +970,35 @@ __device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p
       // of each probe (two 16 B loads) — fewer dependent rounds at high load
       // (cfg 5: tokenize 14.9 -> 12.9 ms); 2-slot buckets otherwise (the extra
       // registers spill: cfg 2 8.27 -> 8.77 ms)
-      ulonglong2 e0[kWaveK], e1[G4 ? kWaveK : 1];
-#pragma unroll
-      for (int k = 0; k < (int)kWaveK; k++) {
-        const uint32_t gs = g[k] == kLookupPending ? (ps[k] & (G4 ? ~3u : ~1u)) : 0u;
-        e0[k] = *reinterpret_cast<const ulonglong2 *>(p.dict + gs);
-        if constexpr (G4) e1[k] = *reinterpret_cast<const ulonglong2 *>(p.dict + gs + 2);
-      }
+      // G4: probes in two halves of kWaveK / 2 terms (two 16 B loads each) so
+      // the group registers of all eight are not live at once
+      constexpr int KH = G4 ? (int)kWaveK / 2 : (int)kWaveK;
       uint32_t cs[kWaveK];
       bool anyclaim = false;
 #pragma unroll
-      for (int k = 0; k < (int)kWaveK; k++) {
-        const bool pend = g[k] == kLookupPending;
-        uint32_t c;
-        uint32_t r;
-        if constexpr (G4) r = group_probe(e0[k], e1[k], ps[k], lo[k], &c);
-        else r = bucket_probe(e0[k], ps[k], lo[k], &c);
-        cs[k] = pend ? c : kInvalidSlot;
-        anyclaim |= pend & (c != kInvalidSlot);
-        const bool adv = pend & (r == kLookupPending) & (c == kInvalidSlot);
-        ps[k] = adv ? (((ps[k] | (G4 ? 3u : 1u)) + 1u) & dmask) : ps[k];
-        g[k] = pend ? r : g[k];
+      for (int h = 0; h < (int)kWaveK / KH; h++) {
+        ulonglong2 e0[KH], e1[G4 ? KH : 1];
+#pragma unroll
+        for (int i = 0; i < KH; i++) {
+          const int k = h * KH + i;
+          const uint32_t gs = g[k] == kLookupPending ? (ps[k] & (G4 ? ~3u : ~1u)) : 0u;
+          e0[i] = *reinterpret_cast<const ulonglong2 *>(p.dict + gs);
+          if constexpr (G4) e1[i] = *reinterpret_cast<const ulonglong2 *>(p.dict + gs + 2);
+        }
+#pragma unroll
+        for (int i = 0; i < KH; i++) {
+          const int k = h * KH + i;
+          const bool pend = g[k] == kLookupPending;
+          uint32_t c;
+          uint32_t r;
+          if constexpr (G4) r = group_probe(e0[i], e1[i], ps[k], lo[k], &c);
+          else r = bucket_probe(e0[i], ps[k], lo[k], &c);
+          cs[k] = pend ? c : kInvalidSlot;
+          anyclaim |= pend & (c != kInvalidSlot);
+          const bool adv = pend & (r == kLookupPending) & (c == kInvalidSlot);
+          ps[k] = adv ? (((ps[k] | (G4 ? 3u : 1u)) + 1u) & dmask) : ps[k];
+          g[k] = pend ? r : g[k];
+        }
       }
       if (__any(anyclaim)) {
 #pragma unroll
