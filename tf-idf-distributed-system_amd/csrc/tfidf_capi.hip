@@ -979,18 +979,23 @@ static int commit_once(tfidf_index *ix) {
   const uint64_t post_esc_cap = row_cap / kPostTfEsc + 64;       // each needs tf >= 2047 tokens of one doc
   if (!ix->term_major) HIP_TRY(ix->post_esc.reserve(post_esc_cap * 8));
 
-  // the dictionary is final here (wave, Unicode and long paths done): a large
-  // host mirror (>= 32 MB, 2^21 slots and up) is copied on the side stream
-  // while the inversion runs (cfg-5 shape, 2^23 slots: 30.2 -> 28.4 ms per
-  // build); a small one stays on the main stream after it (measured: the
-  // cross-stream hand-off cost the 300-book shape 2 ms for a 4 MB copy)
+  // the dictionary is final here (wave, Unicode and long paths done): its host
+  // mirror, the deferred identity checks and the occupied-slot count run on the
+  // side stream while the inversion runs (cfg-5 shape, 2^23 slots: 30.2 -> 28.4
+  // ms per build; cfg 2: the 4 MB mirror, the checks and the count left ~0.2 ms
+  // of copies, kernels and launch gaps after the inversion).  TFIDF_MIRROR_MAIN=1
+  // keeps a mirror below 32 MB on the main stream after the inversion (A/B).
   HIP_TRY(ix->h_dict.resize((size_t)2 * C));
   HIP_TRY(ix->h_df.resize(C));
-  const bool mirror_side = (size_t)2 * C * 8 >= (32u << 20);
+  static const bool mirror_main = getenv("TFIDF_MIRROR_MAIN") != nullptr;
+  const bool mirror_side = !mirror_main || (size_t)2 * C * 8 >= (32u << 20);
   if (mirror_side) {
     HIP_TRY(hipEventRecord(ix->mir_ev[0], s));
     HIP_TRY(hipStreamWaitEvent(ix->copy_stream, ix->mir_ev[0], 0));
     HIP_TRY(hipMemcpyAsync(ix->h_dict.data(), ix->dict.p, (size_t)2 * C * 8, hipMemcpyDeviceToHost, ix->copy_stream));
+    HIP_TRY(launch_verify_deferred(bp, ix->copy_stream));
+    HIP_TRY(launch_count_nonzero(ix->dict.as<uint64_t>(), C, reinterpret_cast<unsigned long long *>(ctr + 7),
+                                 ix->copy_stream));
     HIP_TRY(hipEventRecord(ix->mir_ev[1], ix->copy_stream));
   }
 
@@ -1090,17 +1095,19 @@ static int commit_once(tfidf_index *ix) {
     HIP_TRY(hipEventRecord(ix->ev[EV_SCAT], s));
   }
   // host mirrors for query analysis: dictionary keys + df
-  if (mirror_side)
-    HIP_TRY(hipStreamWaitEvent(s, ix->mir_ev[1], 0));   // dictionary mirror (side stream)
-  else
+  if (!mirror_side)
     HIP_TRY(hipMemcpyAsync(ix->h_dict.data(), ix->dict.p, (size_t)2 * C * 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(ix->h_df.data(), ix->df_dev(), (size_t)C * 4,
                          hipMemcpyDeviceToHost, s));
-  // hashed-key identity checks the tokenizers had to defer
-  HIP_TRY(launch_verify_deferred(bp, s));
-  // occupied dictionary slots counted on the device (ctr[7]) instead of a host
-  // pass over the mirror (8 M slots at 2^23 took milliseconds)
-  HIP_TRY(launch_count_nonzero(ix->dict.as<uint64_t>(), C, reinterpret_cast<unsigned long long *>(ctr + 7), s));
+  if (mirror_side) {
+    HIP_TRY(hipStreamWaitEvent(s, ix->mir_ev[1], 0));   // mirror, checks and count (side stream)
+  } else {
+    // hashed-key identity checks the tokenizers had to defer
+    HIP_TRY(launch_verify_deferred(bp, s));
+    // occupied dictionary slots counted on the device (ctr[7]) instead of a host
+    // pass over the mirror (8 M slots at 2^23 took milliseconds)
+    HIP_TRY(launch_count_nonzero(ix->dict.as<uint64_t>(), C, reinterpret_cast<unsigned long long *>(ctr + 7), s));
+  }
   uint64_t tail[8];              // ctr[3] error flags .. ctr[7] occupied slots, [8] malformed, [10] posting escapes
   HIP_TRY(hipMemcpyAsync(tail, ctr + 3, sizeof tail, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
