@@ -989,15 +989,9 @@ static int commit_once(tfidf_index *ix) {
   HIP_TRY(ix->h_df.resize(C));
   static const bool mirror_main = getenv("TFIDF_MIRROR_MAIN") != nullptr;
   const bool mirror_side = !mirror_main || (size_t)2 * C * 8 >= (32u << 20);
-  if (mirror_side) {
-    HIP_TRY(hipEventRecord(ix->mir_ev[0], s));
-    HIP_TRY(hipStreamWaitEvent(ix->copy_stream, ix->mir_ev[0], 0));
-    HIP_TRY(hipMemcpyAsync(ix->h_dict.data(), ix->dict.p, (size_t)2 * C * 8, hipMemcpyDeviceToHost, ix->copy_stream));
-    HIP_TRY(launch_verify_deferred(bp, ix->copy_stream));
-    HIP_TRY(launch_count_nonzero(ix->dict.as<uint64_t>(), C, reinterpret_cast<unsigned long long *>(ctr + 7),
-                                 ix->copy_stream));
-    HIP_TRY(hipEventRecord(ix->mir_ev[1], ix->copy_stream));
-  }
+  // (the side-stream work is enqueued after the inversion's launches, so the
+  // host's enqueue time does not delay the first inversion kernel)
+  if (mirror_side) HIP_TRY(hipEventRecord(ix->mir_ev[0], s));
 
   PostingParams pp{};
   pp.offsets = bp.offsets;
@@ -1093,6 +1087,14 @@ static int commit_once(tfidf_index *ix) {
     HIP_TRY(hipEventRecord(ix->ev[EV_CSCAN], s));
     if (ix->n_blocks) HIP_TRY(launch_scatter(pp, s));
     HIP_TRY(hipEventRecord(ix->ev[EV_SCAT], s));
+  }
+  if (mirror_side) {
+    HIP_TRY(hipStreamWaitEvent(ix->copy_stream, ix->mir_ev[0], 0));
+    HIP_TRY(hipMemcpyAsync(ix->h_dict.data(), ix->dict.p, (size_t)2 * C * 8, hipMemcpyDeviceToHost, ix->copy_stream));
+    HIP_TRY(launch_verify_deferred(bp, ix->copy_stream));
+    HIP_TRY(launch_count_nonzero(ix->dict.as<uint64_t>(), C, reinterpret_cast<unsigned long long *>(ctr + 7),
+                                 ix->copy_stream));
+    HIP_TRY(hipEventRecord(ix->mir_ev[1], ix->copy_stream));
   }
   // host mirrors for query analysis: dictionary keys + df
   if (!mirror_side)
