@@ -1134,16 +1134,28 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     }
     bool longtok = false;
     {
+      // the k-th start pairs with the k-th end; starts of the low half first
+      // (their ends in the low half, else the high half, else nz), then the
+      // high half's (every low-half end is taken by then)
       uint32_t at = tincl - nts;
       uint32_t s0 = (uint32_t)S, s1 = (uint32_t)(S >> 32), e0 = (uint32_t)E, e1 = (uint32_t)(E >> 32);
-      while (s0 | s1) {
-        const uint32_t tp = lane * 64 + (s0 ? (uint32_t)__builtin_ctz(s0) : 32 + (uint32_t)__builtin_ctz(s1));
-        const uint32_t te = (e0 | e1) ? lane * 64 + (e0 ? (uint32_t)__builtin_ctz(e0) : 32 + (uint32_t)__builtin_ctz(e1))
-                                      : nz;
-        if (s0) s0 &= s0 - 1; else s1 &= s1 - 1;
+      const uint32_t l64 = lane * 64;
+      while (s0) {
+        const uint32_t tp = l64 + (uint32_t)__builtin_ctz(s0);
+        const uint32_t te = e0 ? l64 + (uint32_t)__builtin_ctz(e0) : (e1 ? l64 + 32 + (uint32_t)__builtin_ctz(e1) : nz);
+        s0 &= s0 - 1;
         if (e0) e0 &= e0 - 1; else e1 &= e1 - 1;
         longtok |= te - tp > 8;
-        const uint32_t j = PACK ? dbase + (uint32_t)__popcll(bm & ((2ull << (tp - 64 * lane)) - 1)) : 0u;
+        const uint32_t j = PACK ? dbase + (uint32_t)__popcll(bm & ((2ull << (tp - l64)) - 1)) : 0u;
+        sm.list[at++] = span_entry(tp, te, j);
+      }
+      while (s1) {
+        const uint32_t tp = l64 + 32 + (uint32_t)__builtin_ctz(s1);
+        const uint32_t te = e1 ? l64 + 32 + (uint32_t)__builtin_ctz(e1) : nz;
+        s1 &= s1 - 1;
+        e1 &= e1 - 1;
+        longtok |= te - tp > 8;
+        const uint32_t j = PACK ? dbase + (uint32_t)__popcll(bm & ((2ull << (tp - l64)) - 1)) : 0u;
         sm.list[at++] = span_entry(tp, te, j);
       }
     }
