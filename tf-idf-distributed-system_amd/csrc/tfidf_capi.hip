@@ -987,8 +987,11 @@ static int commit_once(tfidf_index *ix) {
   // keeps a mirror below 32 MB on the main stream after the inversion (A/B).
   HIP_TRY(ix->h_dict.resize((size_t)2 * C));
   HIP_TRY(ix->h_df.resize(C));
+  // On a caller's stream (tfidf_set_stream: torch's stream under torch.distributed)
+  // the small mirror stays on the main stream: the cross-stream hand-off cost the
+  // one-rank RCCL rehearsal ~1 ms per step (tools/ab_dist3.sh: 12.4-12.8 vs 11.4-11.6)
   static const bool mirror_main = getenv("TFIDF_MIRROR_MAIN") != nullptr;
-  const bool mirror_side = !mirror_main || (size_t)2 * C * 8 >= (32u << 20);
+  const bool mirror_side = (!mirror_main && s == ix->own_stream) || (size_t)2 * C * 8 >= (32u << 20);
   // (the side-stream work is enqueued after the inversion's launches, so the
   // host's enqueue time does not delay the first inversion kernel)
   if (mirror_side) HIP_TRY(hipEventRecord(ix->mir_ev[0], s));
