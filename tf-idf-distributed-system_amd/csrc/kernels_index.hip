@@ -1174,7 +1174,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         else if (rem > 128) { hist_batch<4, true, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 256; }
         else { hist_batch<2, true, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 128; }
       } else {
-        if (rem > 256) { hist_batch<8, false, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 512; }
+        // 513..640 tokens (U[400, 600]-token documents: ~40 % of cfg 2) in one batch
+        if (!PACK && rem > 512 && rem <= 640) { hist_batch<10, false, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 640; }
+        else if (rem > 256) { hist_batch<8, false, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 512; }
         else if (rem > 128) { hist_batch<4, false, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 256; }
         else { hist_batch<2, false, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 128; }
       }
