@@ -1170,7 +1170,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     for (uint32_t tb = 0; tb < ntok && !overflow;) {       // batch width by what is left
       const uint32_t rem = ntok - tb;
       if (anylong) {
-        if (rem > 256) { hist_batch<8, true, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 512; }
+        if (!PACK && rem > 512 && rem <= 640) { hist_batch<10, true, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 640; }
+        else if (rem > 256) { hist_batch<8, true, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 512; }
         else if (rem > 128) { hist_batch<4, true, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 256; }
         else { hist_batch<2, true, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 128; }
       } else {
