@@ -11,13 +11,17 @@ GLOBAL-statistics exchange (vocabulary all-gather + DF all-reduce over RCCL).
 Query throughput is measured after the timed region: cfg-2 single 3-term
 queries (top-10 and all-hits) and cfg-4 batched 10k queries (top-10).
 
-Launch: python bench.py [--gpus N --steps K --warmup W]; for N > 1 under
-torch.distributed.run (one process per GPU, RCCL).
+Launch: python bench.py [--gpus N --steps K --warmup W].  N > 1 runs one
+process per GPU (RCCL): under torch.distributed.run (WORLD_SIZE must equal N),
+or, started without a launcher, bench.py starts torch.distributed.run with N
+ranks itself as a child process before touching the GPU and exits with its
+return code (rank 0's JSON line reaches the same stdout).
 """
 import argparse
-import ctypes as C
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -55,34 +59,75 @@ def parse():
     return ap.parse_args()
 
 
+def launcher_cmd(n_gpus, argv, port=None):
+    """torch.distributed.run command that runs this script with n_gpus ranks."""
+    if port is None:
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % n_gpus,
+            "--master-addr=127.0.0.1", "--master-port=%d" % port, os.path.abspath(__file__)] + list(argv)
+
+
+def launch_or_check(args, argv):
+    """None to run here; else the exit code.  --gpus N > 1 without a launcher
+    (WORLD_SIZE unset): run N ranks under torch.distributed.run as a child
+    (nothing here has touched the GPU yet); under a launcher WORLD_SIZE must be N."""
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None:
+        if args.gpus > 1:
+            return subprocess.call(launcher_cmd(args.gpus, argv))
+        return None
+    if int(ws) != args.gpus:
+        print("bench.py: --gpus %d but the launcher started WORLD_SIZE=%s ranks" % (args.gpus, ws), file=sys.stderr)
+        return 2
+    return None
+
+
+def cpu_threads():
+    """Threads for the all-cores CPU baseline: the CPUs this process may run
+    on, capped by the GPU box's per-GPU CPU share (the pool allots 16 CPUs per
+    GPU and exports OMP_NUM_THREADS=16; os.cpu_count() / the affinity mask
+    show the whole 8-GPU machine).  -> (threads, reason)."""
+    usable = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    if share and share < usable:
+        return share, ("OMP_NUM_THREADS=%d: the box's CPU share for this one GPU (%d CPUs usable are the whole "
+                       "machine's, shared with the other GPUs' jobs)" % (share, usable))
+    return usable, "all usable CPUs (sched_getaffinity)"
+
+
 def cpu_baseline(corpus, args, n_docs):
-    """Reference-semantics CPU restatement (oracle/) on the same corpus:
-    docs indexed/sec single-threaded on the first n_docs, and with T host
-    threads each indexing its own n_docs-doc shard (the reference's
-    N-worker layout, one IndexWriter per worker); top-10 and all-hits +
-    materialised (name, score) JSON query rates on the single-thread index."""
-    import threading
+    """Reference-semantics CPU restatement (oracle/, C) on the same corpus:
+    docs indexed/sec by C threads with no Python in the timed region
+    (orc_bulk_build): 1 thread over the first n_docs, then T threads each
+    indexing its own n_docs-doc share (the reference's N-worker layout, one
+    IndexWriter per worker) and the scaling curve 1, 2, 4, ... T; top-10 and
+    all-hits + materialised (name, score) JSON query rates on an n_docs index."""
     from oracle import oracle as O
     from tfidf_amd import synth
-    T = max(1, int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1))
-    T = min(T, 16, max(1, corpus.n_docs // n_docs))
+    T, why = cpu_threads()
+    T = max(1, min(T, corpus.n_docs // n_docs))
     n = min(n_docs, corpus.n_docs)
     text, offs = corpus.to_host(n * T)
-    raw = text.tobytes()
+    # single thread: the first n documents
+    t_idx, ttf1 = O.bulk_build(text[:int(offs[n])], offs[:n + 1], 1)
+    # scaling curve: t threads over t * n documents (each thread's index as large as the single one's)
+    curve = {}
+    t = 2
+    while t <= T:
+        sec, _ = O.bulk_build(text[:int(offs[t * n])], offs[:t * n + 1], t)
+        curve[t] = t * n / sec
+        t *= 2
+    if T > 1 and T not in curve:
+        sec, _ = O.bulk_build(text, offs, T)
+        curve[T] = T * n / sec
+    raw = text[:int(offs[n])].tobytes()
     del text
-
-    def build(lo, hi, out):
-        o = O.OracleIndex()
-        for i in range(lo, hi):
-            o.add_doc(str(i).encode(), raw[int(offs[i]):int(offs[i + 1])])
-        o.commit()
-        out.append(o)
-
-    single = []
-    t0 = time.perf_counter()
-    build(0, n, single)
-    t_idx = time.perf_counter() - t0
-    o = single[0]
+    o = O.OracleIndex()
+    for i in range(n):
+        o.add_doc(str(i).encode(), raw[int(offs[i]):int(offs[i + 1])])
+    o.commit()
     qs = synth.queries(50)
     t0 = time.perf_counter()
     for q in qs:
@@ -93,6 +138,7 @@ def cpu_baseline(corpus, args, n_docs):
         hits = o.search(q, 0)
         json.dumps([{"document": {"name": o.doc_key(d).decode()}, "score": float(sc)} for d, sc in hits])
     t_all = time.perf_counter() - t0
+    o.close()
     # the GPU engine on the SAME sample and queries (comparable query rates)
     from tfidf_amd.engine import ShardIndex
     g = ShardIndex()
@@ -114,22 +160,12 @@ def cpu_baseline(corpus, args, n_docs):
                     for a, b, sc in zip(ko.tolist(), ke.tolist(), scs.tolist())])
     g_all = time.perf_counter() - t0
     g.close()
-    multi = []
-    if T > 1:
-        th = [threading.Thread(target=build, args=(j * n, (j + 1) * n, multi)) for j in range(T)]
-        t0 = time.perf_counter()
-        for x in th:
-            x.start()
-        for x in th:
-            x.join()
-        t_multi = time.perf_counter() - t0
-    for x in single + multi:
-        x.close()
-    out = {"value": n / t_idx, "unit": "docs/s", "cores": 1, "kind": "port",
+    single = n / t_idx
+    out = {"value": single, "unit": "docs/s", "cores": 1, "kind": "port",
            "sample": "first %d docs (%.1f MB) of the same synthetic corpus, oracle/ C restatement of "
-                     "Lucene 9.8 analysis+inversion+stats, 1 thread; no JDK/Lucene in the image" % (
-                         n, float(offs[n]) / 1e6),
-           "seconds": t_idx, "queries_per_sec_top10": len(qs) / t_q,
+                     "Lucene 9.8 analysis+inversion+stats, 1 C thread (no Python in the timed region); "
+                     "no JDK/Lucene in the image" % (n, float(offs[n]) / 1e6),
+           "seconds": t_idx, "sum_ttf": ttf1, "queries_per_sec_top10": len(qs) / t_q,
            "queries_per_sec_all_hits_materialised": 10 / t_all,
            "queries_sample": "cfg-2 queries over the %d-doc sample (all hits: + doc key lookup + JSON, "
                              "as Worker.searchIndex)" % n,
@@ -139,8 +175,11 @@ def cpu_baseline(corpus, args, n_docs):
            "host_cpus": os.cpu_count(),
            "host_cpus_usable": len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None}
     if T > 1:
-        out["all_cores"] = {"value": T * n / t_multi, "unit": "docs/s", "threads": T, "seconds": t_multi,
-                            "sample": "%d threads, each indexing its own %d-doc shard" % (T, n)}
+        out["all_cores"] = {"value": curve[T], "unit": "docs/s", "threads": T, "threads_reason": why,
+                            "seconds": T * n / curve[T], "scaling_efficiency": curve[T] / (T * single),
+                            "curve_docs_per_s": {str(k): v for k, v in sorted(curve.items())},
+                            "sample": "%d C threads (orc_bulk_build), each indexing its own %d-doc share of the "
+                                      "same corpus into its own index" % (T, n)}
     return out
 
 
@@ -164,6 +203,9 @@ def measured_copy_GBs(dev, nbytes=1 << 30, reps=5):
 
 def main():
     args = parse()
+    rc = launch_or_check(args, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     # multi-GPU code path (process group, GLOBAL statistics exchange) even at

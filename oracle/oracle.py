@@ -62,6 +62,7 @@ def _load():
         "orc_norm_cache": (None, [C.c_float, C.c_float, C.c_float, f32p]),
         "orc_bm25": (C.c_float, [C.c_float, C.c_uint32, C.c_float]),
         "orc_leader_merge": (C.c_int64, [C.c_char_p, u64p, C.c_uint64, f64p, u64p, f64p]),
+        "orc_bulk_build": (C.c_int, [C.c_void_p, u64p, C.c_uint64, C.c_uint32, f64p, u64p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(lib, name)
@@ -268,3 +269,18 @@ def leader_merge(responses):
     m = lib().orc_leader_merge(names, _p(offs, C.c_uint64), n, _p(sc, C.c_double),
                                _p(first, C.c_uint64), _p(sums, C.c_double))
     return [(flat[int(first[i])][0], float(sums[i])) for i in range(m)]
+
+
+def bulk_build(text, offsets, n_threads):
+    """CPU baseline (bench.py only): n_threads C threads, each indexing its own
+    contiguous share of the corpus (uint8 text, uint64 offsets[n + 1]) into
+    its own index; no Python in the timed region.  -> (seconds, sum_ttf)."""
+    import numpy as np
+    text = np.ascontiguousarray(text, np.uint8)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    sec, ttf = C.c_double(), C.c_uint64()
+    rc = lib().orc_bulk_build(C.c_void_p(text.ctypes.data), _p(offsets, C.c_uint64), len(offsets) - 1,
+                              n_threads, C.byref(sec), C.byref(ttf))
+    if rc != 0:
+        raise RuntimeError("orc_bulk_build failed: %d" % rc)
+    return sec.value, ttf.value

@@ -23,9 +23,13 @@
  *    order.
  * Compile with -ffp-contract=off and no fast-math (SSE float = Java float).
  */
+#define _POSIX_C_SOURCE 200809L
 #include "tfidf_oracle.h"
 
 #include <math.h>
+#include <pthread.h>
+#include <stdio.h>
+#include <time.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -1181,4 +1185,58 @@ int64_t orc_leader_merge(const uint8_t *names, const uint64_t *offsets, uint64_t
   for (uint64_t i = 0; i < n; i++) free(u[i].u);
   free(u); free(idx);
   return m + 1;
+}
+
+/* ---- CPU baseline: one index per thread (bench.py cpu_baseline) ---------- */
+typedef struct {
+  const uint8_t *text;
+  const uint64_t *offsets;
+  uint64_t lo, hi, ttf;
+  int rc;
+} bulk_part;
+
+static void *bulk_worker(void *arg) {
+  bulk_part *w = (bulk_part *)arg;
+  orc_index *ix = orc_create(1.2f, 0.75f);
+  if (!ix) { w->rc = ORC_E_NOMEM; return NULL; }
+  char key[24];
+  for (uint64_t d = w->lo; d < w->hi && w->rc == ORC_OK; d++) {
+    const int kl = snprintf(key, sizeof key, "%llu", (unsigned long long)d);
+    const int rc = orc_add_doc(ix, (const uint8_t *)key, (uint64_t)kl, w->text + w->offsets[d],
+                               w->offsets[d + 1] - w->offsets[d]);
+    if (rc != ORC_OK && rc != ORC_E_UNSUPPORTED) w->rc = rc;
+  }
+  if (w->rc == ORC_OK) w->rc = orc_commit(ix);
+  w->ttf = orc_sum_ttf(ix);
+  orc_destroy(ix);
+  return NULL;
+}
+
+int orc_bulk_build(const uint8_t *text, const uint64_t *offsets, uint64_t n_docs, uint32_t n_threads,
+                   double *seconds, uint64_t *sum_ttf) {
+  if (!text || !offsets || !seconds || !sum_ttf || n_threads == 0) return ORC_E_ARG;
+  bulk_part *parts = (bulk_part *)calloc(n_threads, sizeof(bulk_part));
+  pthread_t *th = (pthread_t *)calloc(n_threads, sizeof(pthread_t));
+  if (!parts || !th) { free(parts); free(th); return ORC_E_NOMEM; }
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  uint32_t started = 0;
+  int rc = ORC_OK;
+  for (uint32_t t = 0; t < n_threads; t++) {
+    parts[t] = (bulk_part){text, offsets, n_docs * t / n_threads, n_docs * (t + 1) / n_threads, 0, ORC_OK};
+    if (pthread_create(&th[t], NULL, bulk_worker, &parts[t]) != 0) { rc = ORC_E_NOMEM; break; }
+    started++;
+  }
+  uint64_t ttf = 0;
+  for (uint32_t t = 0; t < started; t++) {
+    pthread_join(th[t], NULL);
+    if (parts[t].rc != ORC_OK) rc = parts[t].rc;
+    ttf += parts[t].ttf;
+  }
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  *seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+  *sum_ttf = ttf;
+  free(parts);
+  free(th);
+  return rc;
 }

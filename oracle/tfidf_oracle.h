@@ -113,6 +113,16 @@ float orc_bm25(float weight, uint32_t tf, float norm_inverse);
 int64_t orc_leader_merge(const uint8_t *names, const uint64_t *offsets, uint64_t n,
                          const double *scores, uint64_t *out_first, double *out_sum);
 
+/* CPU baseline only (bench.py cpu_baseline; never the checker): n_threads
+ * POSIX threads, thread t indexes documents [t*n/T, (t+1)*n/T) of the corpus
+ * (text + offsets[n_docs + 1]) into ITS OWN index — the reference's N-worker
+ * layout, one IndexWriter per worker (Worker.java:67-88) — keyed by the
+ * decimal document number, and commits it.  *seconds = wall time of the
+ * parallel region (thread start to the last commit); *sum_ttf = tokens
+ * indexed over all threads (a check that the work was done).  Returns ORC_OK. */
+int orc_bulk_build(const uint8_t *text, const uint64_t *offsets, uint64_t n_docs, uint32_t n_threads,
+                   double *seconds, uint64_t *sum_ttf);
+
 #ifdef __cplusplus
 }
 #endif

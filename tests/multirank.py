@@ -30,7 +30,10 @@ def corpus():
     return texts, names
 
 
-QUERIES = synth.queries(12, lo=1, hi=1500) + [b"aaaa", b"aaab aaac", b"aaab AND aaac", b"aaaa NOT aaab"]
+# the last two do not parse (dangling operator, nothing but an operator):
+# Worker.processDocuments answers [] and the Leader merges nothing
+QUERIES = synth.queries(12, lo=1, hi=1500) + [b"aaaa", b"aaab aaac", b"aaab AND aaac", b"aaaa NOT aaab",
+                                              b"aaab AND", b"OR"]
 
 
 def free_port():
@@ -51,6 +54,7 @@ def _keys(docs, scores, base):
 class OracleShardAdapter:
     """The CPU oracle behind HipShardAdapter's interface (host tensors)."""
     device = torch.device("cpu")
+    query_errors = (O.QuerySyntaxError,)
 
     def __init__(self, texts, names, doc_base):
         self.o = O.OracleIndex()
@@ -171,7 +175,7 @@ def run_rank(rank, world, port, kind, out_path):
     nv, dc, ttf = D.global_commit(ad, vocab_size=True)
     res.update(n_vocab=nv, dc=dc, ttf=ttf)
     res["topk"] = [[[d, float(s)] for d, s in D.global_search(ad, q, K)] for q in QUERIES]
-    res["all"] = [[[d, float(s)] for d, s in D.global_search(ad, q, 0)] for q in QUERIES[:6]]
+    res["all"] = [[[d, float(s)] for d, s in D.global_search(ad, q, 0)] for q in QUERIES[:6] + QUERIES[-2:]]
     bd, bs, bc = D.global_search_batch(ad, QUERIES, K)
     res["batch"] = [[[int(bd[i, j]), float(bs[i, j])] for j in range(int(bc[i]))] for i in range(len(QUERIES))]
     # the canonical (all-gather + sorted union) form must agree
@@ -203,7 +207,7 @@ def expected():
             return []
 
     out["topk"] = [search(one, q, K) for q in QUERIES]
-    out["all"] = [search(one, q, 0) for q in QUERIES[:6]]
+    out["all"] = [search(one, q, 0) for q in QUERIES[:6] + QUERIES[-2:]]
     one.close()
     return out
 
@@ -250,3 +254,111 @@ def check(res, world):
     for got, w in zip(res["shard"], expected_shard(world)):
         assert [bytes.fromhex(n) for n, _ in got] == [n for n, _ in w]
         assert [s for _, s in got] == [s for _, s in w]          # double sums, exactly
+
+
+# ---------------------------------------------------------------------------
+# Hash-seed agreement (GLOBAL statistics match hashed term keys across shards:
+# a shard that met a collision rebuilt under a later seed, and the others must
+# follow it).  Corpus with hashed keys: terms over 16 bytes and non-ASCII terms.
+
+def seed_corpus():
+    rng = np.random.default_rng(11)
+    base = synth.corpus(400, V=3000, len_min=10, len_max=60)
+    longw = [bytes(rng.integers(97, 123, int(rng.integers(17, 21))).astype(np.uint8)) for _ in range(40)]
+    uni = [w.encode() for w in ("café", "naïve", "über", "façade", "señor", "ångström", "smörgåsbord",
+                                 "crème", "brûlée", "jalapeño", "Ελλάδα", "москва", "日本語")]
+    texts = []
+    for i, t in enumerate(base):
+        extra = [longw[int(j)] for j in rng.integers(0, len(longw), 3)] + [uni[int(j)] for j in
+                                                                           rng.integers(0, len(uni), 2)]
+        texts.append(t + b" " + b" ".join(extra))
+    names = [b"s%04d.txt" % i for i in range(len(texts))]
+    return texts, names
+
+
+SEED_QUERIES = [b"caf\xc3\xa9 aaab", b"na\xc3\xafve \xc3\xbcber", b"aaaa"]
+
+
+def _seed_queries():
+    texts, _ = seed_corpus()
+    toks = texts[5].split(b" ")
+    return SEED_QUERIES + [b" ".join(toks[-5:-2]), toks[-4]]
+
+
+class AttemptOracleAdapter(OracleShardAdapter):
+    """Oracle adapter with a simulated hash-seed attempt: ``start`` is the
+    attempt this shard's commit ended at; ``collide_at`` = attempts at which a
+    recommit meets a collision (and moves on to the next)."""
+
+    def __init__(self, texts, names, doc_base, start, collide_at=()):
+        super().__init__(texts, names, doc_base)
+        self.attempt = start
+        self.collide_at = set(collide_at)
+        self.recommits = []
+
+    def hash_attempt(self):
+        return self.attempt
+
+    def recommit(self, attempt):
+        self.recommits.append(attempt)
+        while attempt in self.collide_at:
+            attempt += 1
+        self.attempt = attempt
+        return attempt
+
+
+def run_rank_seed(rank, world, port, kind, out_path):
+    """kind "oracle": world 3, shard attempts (0, 1, 0); shard 2 collides again
+    at attempt 1, so the ranks agree on 2 after two rounds.  kind "hip": the
+    real engine, shard 1 (only) under TFIDF_TEST_WEAK_HASH (every pair of
+    equal-length hashed keys collides: its commit moves to attempt 1)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    texts, names = seed_corpus()
+    lo, hi = D.shard_range(len(texts), rank, world)
+    idx = None
+    if kind == "hip":
+        from tfidf_amd.engine import ShardIndex
+        torch.cuda.set_device(0)
+        if rank == 1:
+            os.environ["TFIDF_TEST_WEAK_HASH"] = "1"
+        idx = ShardIndex(device=0)
+        idx.add_documents(texts[lo:hi], names[lo:hi])
+        idx.commit()
+        os.environ.pop("TFIDF_TEST_WEAK_HASH", None)
+        ad = D.HipShardAdapter(idx, torch.device("cuda", 0), doc_base=lo)
+        before = ad.hash_attempt()
+    else:
+        ad = AttemptOracleAdapter(texts[lo:hi], names[lo:hi], lo, start=(0, 1, 0)[rank],
+                                  collide_at=(1,) if rank == 2 else ())
+        before = ad.hash_attempt()
+    nv, dc, ttf = D.global_commit(ad, vocab_size=True)
+    res = {"before": before, "after": ad.hash_attempt(), "n_vocab": nv, "dc": dc, "ttf": ttf,
+           "recommits": getattr(ad, "recommits", None),
+           "topk": [[[d, float(s)] for d, s in D.global_search(ad, q, K)] for q in _seed_queries()]}
+    with open("%s.%d" % (out_path, rank), "w") as f:
+        json.dump(res, f)
+    dist.barrier()
+    dist.destroy_process_group()
+    if idx is not None:
+        idx.close()
+
+
+def check_seed(out_path, world):
+    res = [json.load(open("%s.%d" % (out_path, r))) for r in range(world)]
+    texts, _ = seed_corpus()
+    one = O.OracleIndex()
+    for i, t in enumerate(texts):
+        one.add_doc(str(i).encode(), t)
+    one.commit()
+    want = [one.search(q, K) for q in _seed_queries()]
+    assert all(w for w in want)
+    for r in res:
+        assert (r["n_vocab"], r["dc"], r["ttf"]) == (one.num_terms, one.doc_count, one.sum_ttf)
+        assert len({x["after"] for x in res}) == 1
+        for got, w in zip(r["topk"], want):
+            assert [d for d, _ in got] == [d for d, _ in w]
+            assert [np.float32(s) for _, s in got] == [np.float32(s) for _, s in w]
+    one.close()
+    return res

@@ -101,3 +101,36 @@ def test_leader_merge_matches_oracle():
 
 def test_leader_merge_empty():
     assert leader_merge([]) == []
+
+
+def _java_order(names):
+    """String.compareTo order (UTF-16 code units) = byte order of UTF-16-BE."""
+    return sorted(names, key=lambda s: s.decode("utf-8").encode("utf-16-be"))
+
+
+def test_sort_names_is_utf16_code_unit_order():
+    from tfidf_amd.engine import sort_names
+    # BMP above the surrogates (U+E000..U+FFFF) sorts ABOVE supplementary code
+    # points (lead surrogates 0xD800..0xDBFF), and the top of plane 16 below
+    # U+E000; U+FFFF and U+10FFFF differ
+    cps = [0x41, 0x7A, 0xE9, 0x4E2D, 0xD7FF, 0xE000, 0xF8FF, 0xFFFD, 0xFFFF, 0x10000, 0x1F600, 0x10E000,
+           0x10FFFF]
+    rng = np.random.default_rng(3)
+    names = [chr(c).encode() for c in cps]
+    for _ in range(300):
+        n = int(rng.integers(1, 5))
+        names.append("".join(chr(cps[int(i)]) for i in rng.integers(0, len(cps), n)).encode())
+    names += [b"a", b"ab", b"a\xf0\x9f\x98\x80", "a￿".encode()]
+    offs = np.zeros(len(names) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(x) for x in names], dtype=np.uint64)
+    perm = sort_names(np.frombuffer(b"".join(names), np.uint8), offs)
+    got = [names[int(i)] for i in perm]
+    assert got == _java_order(names)
+    assert chr(0xFFFF).encode() != chr(0x10FFFF).encode()
+    assert _java_order([chr(0xFFFF).encode(), chr(0x10FFFF).encode()])[0] == chr(0x10FFFF).encode()
+
+
+def test_leader_merge_orders_supplementary_names_like_java():
+    names = ["\U0001F600.txt", ".txt", "\U0010FFFF.txt", "￿.txt", "z.txt"]
+    resp = [[(n.encode(), 1.0) for n in names]]
+    assert [n for n, _ in leader_merge(resp)] == _java_order([n.encode() for n in names])

@@ -23,3 +23,14 @@ def test_distributed_modes_equal_oracle(tmp_path, world):
     out = str(tmp_path / "r.json")
     mp.spawn(M.run_rank, args=(world, M.free_port(), "oracle", out), nprocs=world, join=True)
     M.check(json.load(open(out)), world)
+
+
+def test_hash_seed_agreement(tmp_path):
+    """Shards that hashed with different seeds agree on the highest: the others
+    re-commit under it (and agree again when that seed collides there)."""
+    out = str(tmp_path / "s.json")
+    mp.spawn(M.run_rank_seed, args=(3, M.free_port(), "oracle", out), nprocs=3, join=True)
+    res = M.check_seed(out, 3)
+    assert [r["before"] for r in res] == [0, 1, 0]
+    assert [r["after"] for r in res] == [2, 2, 2]
+    assert [r["recommits"] for r in res] == [[1, 2], [2], [1]]

@@ -21,3 +21,14 @@ def test_hip_adapter_multirank(tmp_path, world):
     out = str(tmp_path / "r.json")
     mp.spawn(M.run_rank, args=(world, M.free_port(), "hip", out), nprocs=world, join=True)
     M.check(json.load(open(out)), world)
+
+
+def test_hip_hash_seed_agreement(tmp_path):
+    """Shard 1 meets hash collisions (TFIDF_TEST_WEAK_HASH) and commits under
+    seed attempt 1; shard 0 re-commits under it and GLOBAL statistics and
+    rankings equal the single-index oracle."""
+    out = str(tmp_path / "s.json")
+    mp.spawn(M.run_rank_seed, args=(2, M.free_port(), "hip", out), nprocs=2, join=True)
+    res = M.check_seed(out, 2)
+    assert [r["before"] for r in res] == [0, 1]
+    assert [r["after"] for r in res] == [1, 1]

@@ -119,11 +119,16 @@ def test_zipf_operator_batch_mixed(zipf):
         batch_equal(g, o, qs, k)
 
 
-def test_concurrent_searches_coalesce_into_batches():
+@pytest.mark.parametrize("cap", [None, 3])
+def test_concurrent_searches_coalesce_into_batches(monkeypatch, cap):
     """Concurrent single searches from many threads (the reference's request
     threads, Worker.java:175-186) share batched scoring launches and each get
-    exactly tfidf_search's answer, including syntax errors."""
+    exactly tfidf_search's answer, including syntax errors.  cap = 3: batches
+    of at most 3 requests (TFIDF_COALESCE_MAX), so a leader's own request is
+    often left over (it leads again) and left-over requests need a new leader."""
     import threading
+    if cap:
+        monkeypatch.setenv("TFIDF_COALESCE_MAX", str(cap))
     texts = synth.corpus(6000, V=3000, len_min=10, len_max=120)
     g = ShardIndex()
     g.add_documents(texts)
@@ -160,4 +165,6 @@ def test_concurrent_searches_coalesce_into_batches():
     st = g.stats()
     assert st["coalesced_queries"] == len(qs)
     assert st["coalesced_batches"] < len(qs)             # some searches shared a launch
+    if cap:
+        assert st["coalesced_batches"] >= len(qs) / cap
     g.close()

@@ -134,6 +134,8 @@ constexpr uint32_t kMaxBlockCapLog2 = 21;
 
 enum { EV_START, EV_TOK, EV_L0, EV_LONG, EV_D0, EV_DF, EV_BSCAN, EV_CSCAN, EV_SCAT, EV_Q0, EV_Q1, EV_Q2, EV_N };
 
+constexpr size_t kCoalesceMaxDefault = 8192;   // tfidf_search_coalesced: requests per batch
+
 struct tfidf_index {
   tfidf_config cfg;
   std::mutex mu;
@@ -173,12 +175,14 @@ struct tfidf_index {
   std::vector<uint64_t> h_post_esc;    // block-major posting tf escapes, sorted (post_word)
   uint64_t hash_seed = 0;              // KeyBuilder seed of the committed index (0 unless a collision was met)
   uint32_t hash_rebuilds = 0;          // builds redone for a hash collision in the last commit
+  uint32_t hash_floor = 0;             // first seed attempt of the next commit (tfidf_set_hash_attempt)
   uint32_t collision_doc = 0;          // a document of the last detected collision (diagnostics)
   // tfidf_search_coalesced: concurrent single top-k searches gathered into batches
   mutable std::mutex cq_mu;
   std::condition_variable cq_cv;
   std::vector<struct CoalesceReq *> cq;
   bool cq_leader = false;
+  size_t cq_max = kCoalesceMaxDefault;  // requests per batch
   uint64_t cq_batches = 0, cq_queries = 0;
   DevBuf verify_defer, lt_pos;
   std::unordered_map<uint32_t, std::string> term_cache;   // hashed slots' term strings (slot_term)
@@ -270,6 +274,7 @@ extern "C" int tfidf_create(const tfidf_config *cfg, tfidf_index **out) {
     return fail(TFIDF_E_HIP, "hipStreamCreate failed");
   }
   ix->stream = ix->own_stream;
+  if (const char *cm = getenv("TFIDF_COALESCE_MAX")) ix->cq_max = std::max(1, atoi(cm));   // tests: small batches
   if (hipStreamCreateWithFlags(&ix->copy_stream, hipStreamNonBlocking) != hipSuccess) {
     hipStreamDestroy(ix->own_stream);
     delete ix;
@@ -1162,11 +1167,13 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   ix->committed = false;                 // a failed rebuild leaves no half-built index behind
   ix->term_cache.clear();
   // Hash seeds: 0, then 1, 2, 3 after a detected collision (TFIDF_TEST_WEAK_HASH:
-  // start from a seed under which equal-length hashed keys collide)
+  // start from a seed under which equal-length hashed keys collide).  A floor
+  // set by tfidf_set_hash_attempt (GLOBAL statistics: every shard must hash
+  // with one seed) skips the earlier attempts.
   const char *weak = getenv("TFIDF_TEST_WEAK_HASH");
-  ix->hash_seed = (weak && atoi(weak)) ? kWeakHashSeed : 0;
-  ix->hash_rebuilds = 0;
-  for (uint32_t attempt = 0;; attempt++) {
+  ix->hash_seed = ix->hash_floor ? ix->hash_floor : ((weak && atoi(weak)) ? kWeakHashSeed : 0);
+  ix->hash_rebuilds = ix->hash_floor;
+  for (uint32_t attempt = ix->hash_floor;; attempt++) {
     const int rc = commit_once(ix);
     if (rc != TFIDF_OK) {
       hipStreamSynchronize(ix->stream);        // nothing of this build may still run on either stream
@@ -1178,6 +1185,14 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
     ix->hash_seed = attempt + 1;
     ix->hash_rebuilds++;
   }
+}
+
+extern "C" int tfidf_set_hash_attempt(tfidf_index *ix, uint32_t attempt) {
+  if (!ix) return fail(TFIDF_E_INVALID_ARG, "NULL index");
+  if (attempt > 3) return fail(TFIDF_E_INVALID_ARG, "hash seed attempt %u > 3", attempt);
+  std::lock_guard<std::mutex> lk(ix->mu);
+  ix->hash_floor = attempt;
+  return TFIDF_OK;
 }
 
 extern "C" int tfidf_get_commit_timing(const tfidf_index *ix, tfidf_commit_timing *out) {
@@ -1667,7 +1682,7 @@ extern "C" int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const 
 // Concurrent single searches (the reference's Worker.processDocuments runs on
 // concurrent request threads, Worker.java:175-186).  Requests queue up; the
 // first caller to find no batch forming leads one: it waits wait_us for
-// companions, takes every queued request (up to kCoalesceMax), runs them
+// companions, takes every queued request (up to cq_max), runs them
 // through the batched scorer (tfidf_search_batch: one launch for all) and
 // hands each caller its own top-k; callers arriving meanwhile form the next
 // batch.  Results are those of tfidf_search(k) for each query, including its
@@ -1684,31 +1699,10 @@ struct CoalesceReq {
   std::string err;
   bool done;
 };
-constexpr size_t kCoalesceMax = 8192;
 
-extern "C" int tfidf_search_coalesced(tfidf_index *ix, const uint8_t *q, uint64_t q_len, uint32_t k, uint32_t *doc_ids,
-                                      float *scores, uint64_t cap, uint64_t *n_out, uint32_t wait_us) {
-  if (!ix || (!q && q_len) || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
-  if (k == 0 || k > 1024) return fail(TFIDF_E_INVALID_ARG, "coalesced search needs 1 <= k <= 1024 (all hits: tfidf_search)");
-  CoalesceReq r{q, q_len, k, doc_ids, scores, cap, n_out, TFIDF_OK, std::string(), false};
-  std::unique_lock<std::mutex> lk(ix->cq_mu);
-  ix->cq.push_back(&r);
-  if (ix->cq_leader) {                                    // a batch is forming: ours will be served
-    ix->cq_cv.wait(lk, [&] { return r.done; });
-    if (r.rc != TFIDF_OK) return fail(r.rc, "%s", r.err.c_str());
-    return TFIDF_OK;
-  }
-  ix->cq_leader = true;
-  lk.unlock();
-  if (wait_us) std::this_thread::sleep_for(std::chrono::microseconds(wait_us));
-  lk.lock();
-  const size_t take = std::min(ix->cq.size(), kCoalesceMax);
-  std::vector<CoalesceReq *> batch(ix->cq.begin(), ix->cq.begin() + take);
-  ix->cq.erase(ix->cq.begin(), ix->cq.begin() + take);
-  ix->cq_leader = false;                                  // later arrivals lead the next batch
-  if (!ix->cq.empty()) ix->cq_cv.notify_all();
-  lk.unlock();
-  // queries that do not parse answer as tfidf_search would; the rest go in one batch
+// One coalesced batch: queries that do not parse answer as tfidf_search
+// would; the rest go through one tfidf_search_batch launch.
+static void coalesced_run(tfidf_index *ix, const std::vector<CoalesceReq *> &batch) {
   std::vector<CoalesceReq *> run;
   std::vector<uint8_t> text;
   std::vector<uint64_t> offs{0};
@@ -1728,29 +1722,58 @@ extern "C" int tfidf_search_coalesced(tfidf_index *ix, const uint8_t *q, uint64_
     offs.push_back(text.size());
     kmax = std::max(kmax, c->k);
   }
-  int rc = TFIDF_OK;
-  std::string err;
-  if (!run.empty()) {
-    std::vector<uint32_t> docs((size_t)run.size() * kmax), counts(run.size());
-    std::vector<float> sc((size_t)run.size() * kmax);
-    rc = tfidf_search_batch(ix, text.data(), offs.data(), (uint32_t)run.size(), kmax, docs.data(), sc.data(),
-                            counts.data());
-    if (rc != TFIDF_OK) err = tfidf_last_error();
-    for (size_t i = 0; i < run.size(); i++) {
-      CoalesceReq *c = run[i];
-      if (rc != TFIDF_OK) { c->rc = rc; c->err = err; *c->n_out = 0; continue; }
-      const uint64_t n = std::min<uint64_t>(counts[i], c->k);     // a prefix of the kmax list = the top-k
-      *c->n_out = n;
-      if (n > c->cap) { c->rc = TFIDF_E_BUFFER; c->err = "result buffer too small"; continue; }
-      memcpy(c->docs, docs.data() + i * kmax, n * 4);
-      memcpy(c->scores, sc.data() + i * kmax, n * 4);
-    }
+  if (run.empty()) return;
+  std::vector<uint32_t> docs((size_t)run.size() * kmax), counts(run.size());
+  std::vector<float> sc((size_t)run.size() * kmax);
+  const int rc = tfidf_search_batch(ix, text.data(), offs.data(), (uint32_t)run.size(), kmax, docs.data(), sc.data(),
+                                    counts.data());
+  const std::string err = rc != TFIDF_OK ? std::string(tfidf_last_error()) : std::string();
+  for (size_t i = 0; i < run.size(); i++) {
+    CoalesceReq *c = run[i];
+    if (rc != TFIDF_OK) { c->rc = rc; c->err = err; *c->n_out = 0; continue; }
+    const uint64_t n = std::min<uint64_t>(counts[i], c->k);     // a prefix of the kmax list = the top-k
+    *c->n_out = n;
+    if (n > c->cap) { c->rc = TFIDF_E_BUFFER; c->err = "result buffer too small"; continue; }
+    memcpy(c->docs, docs.data() + i * kmax, n * 4);
+    memcpy(c->scores, sc.data() + i * kmax, n * 4);
   }
-  lk.lock();
-  ix->cq_batches++;
-  ix->cq_queries += batch.size();
-  for (CoalesceReq *c : batch) c->done = true;
-  ix->cq_cv.notify_all();
+}
+
+
+extern "C" int tfidf_search_coalesced(tfidf_index *ix, const uint8_t *q, uint64_t q_len, uint32_t k, uint32_t *doc_ids,
+                                      float *scores, uint64_t cap, uint64_t *n_out, uint32_t wait_us) {
+  if (!ix || (!q && q_len) || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  if (k == 0 || k > 1024) return fail(TFIDF_E_INVALID_ARG, "coalesced search needs 1 <= k <= 1024 (all hits: tfidf_search)");
+  CoalesceReq r{q, q_len, k, doc_ids, scores, cap, n_out, TFIDF_OK, std::string(), false};
+  std::unique_lock<std::mutex> lk(ix->cq_mu);
+  ix->cq.push_back(&r);
+  bool slept = false;
+  for (;;) {
+    // served by a leader, or no batch is forming: lead one.  A leader whose own
+    // request did not fit its (capped) batch comes back here; requests left
+    // over after a capped batch are woken and one of their callers leads next.
+    ix->cq_cv.wait(lk, [&] { return r.done || !ix->cq_leader; });
+    if (r.done) break;
+    ix->cq_leader = true;
+    if (wait_us && !slept) {
+      slept = true;
+      lk.unlock();
+      std::this_thread::sleep_for(std::chrono::microseconds(wait_us));
+      lk.lock();
+    }
+    const size_t take = std::min(ix->cq.size(), ix->cq_max);
+    std::vector<CoalesceReq *> batch(ix->cq.begin(), ix->cq.begin() + take);
+    ix->cq.erase(ix->cq.begin(), ix->cq.begin() + take);
+    ix->cq_leader = false;                                // later arrivals lead the next batch
+    if (!ix->cq.empty()) ix->cq_cv.notify_all();
+    lk.unlock();
+    coalesced_run(ix, batch);
+    lk.lock();
+    ix->cq_batches++;
+    ix->cq_queries += batch.size();
+    for (CoalesceReq *c : batch) c->done = true;
+    ix->cq_cv.notify_all();
+  }
   lk.unlock();
   if (r.rc != TFIDF_OK) return fail(r.rc, "%s", r.err.c_str());
   return TFIDF_OK;
@@ -2028,6 +2051,28 @@ extern "C" int tfidf_vocab_export_device(tfidf_index *ix, void *d_keys, void *d_
   return TFIDF_OK;
 }
 
+extern "C" int tfidf_vocab_export(tfidf_index *ix, uint64_t *keys, uint32_t *df_local, uint32_t *df_effective,
+                                  uint64_t cap, uint64_t *n_out) {
+  if (!ix || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  std::lock_guard<std::mutex> lk(ix->mu);
+  if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
+  if (int e = wait_gdf(ix)) return e;
+  *n_out = ix->num_terms;
+  if (ix->num_terms > cap) return fail(TFIDF_E_BUFFER, "need %llu terms", (unsigned long long)ix->num_terms);
+  std::vector<std::pair<std::pair<uint64_t, uint64_t>, uint32_t>> v;   // ((hi, lo), slot)
+  v.reserve(ix->num_terms);
+  for (uint32_t s = 0; s < ix->C; s++)
+    if (ix->h_dict[s]) v.push_back({{ix->h_dict[(size_t)ix->C + s], ix->h_dict[s]}, s});
+  std::sort(v.begin(), v.end());
+  for (size_t i = 0; i < v.size(); i++) {
+    const uint32_t s = v[i].second;
+    if (keys) { keys[2 * i] = v[i].first.second; keys[2 * i + 1] = v[i].first.first; }
+    if (df_local) df_local[i] = ix->h_df[s];
+    if (df_effective) df_effective[i] = ix->has_global ? ix->gdf[s] : ix->h_df[s];
+  }
+  return TFIDF_OK;
+}
+
 extern "C" int tfidf_vocab_canonicalize_device(tfidf_index *ix, const void *d_all_keys, uint64_t n_all,
                                                void *d_df_canonical, uint64_t cap, uint64_t *n_canonical) {
   if (!ix || !n_canonical) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
@@ -2054,6 +2099,17 @@ extern "C" int tfidf_vocab_canonicalize_device(tfidf_index *ix, const void *d_al
   return TFIDF_OK;
 }
 
+// The device-buffer exchange calls run on ix->stream.  On a caller's stream
+// (tfidf_set_stream) they stay asynchronous: the caller's allocator orders
+// its buffers on that stream.  On the index's own stream nothing orders the
+// caller's buffers against the work, so the call returns only once the work
+// that reads or writes them is done.
+static int exchange_done(tfidf_index *ix) {
+  if (ix->stream == ix->own_stream && hipStreamSynchronize(ix->stream) != hipSuccess)
+    return fail(TFIDF_E_HIP, "hipStreamSynchronize failed");
+  return TFIDF_OK;
+}
+
 extern "C" int tfidf_vocab_partition_device(tfidf_index *ix, uint32_t n_ranks, void *d_records, uint64_t cap,
                                             void *d_counts, uint64_t *n_out) {
   if (!ix || !n_out || !d_counts || n_ranks == 0 || n_ranks > 1024)
@@ -2074,7 +2130,7 @@ extern "C" int tfidf_vocab_partition_device(tfidf_index *ix, uint32_t n_ranks, v
   HIP_TRY(vocab_scatter(ix->dict.as<uint64_t>(), ix->df_dev(), ix->C, n_ranks, cur, (uint64_t *)d_records,
                         ix->sent_slot.as<uint32_t>(), s));
   ix->n_sent = ix->num_terms;
-  return TFIDF_OK;                                     // asynchronous on the index's stream
+  return exchange_done(ix);                            // asynchronous on a caller's stream
 }
 
 extern "C" int tfidf_vocab_reduce_device(tfidf_index *ix, const void *d_records, uint64_t n, void *d_df_out,
@@ -2101,7 +2157,7 @@ extern "C" int tfidf_vocab_reduce_device(tfidf_index *ix, const void *d_records,
   HIP_TRY(vocab_reduce((const uint64_t *)d_records, n, ix->vt_table.as<uint64_t>(), (uint32_t)(T - 1),
                        ix->vt_sum.as<uint32_t>(), ix->vt_rslot.as<uint32_t>(), (uint32_t *)d_df_out, nu, s));
   if (d_n_unique) HIP_TRY(hipMemcpyAsync(d_n_unique, nu, 8, hipMemcpyDeviceToDevice, s));
-  return TFIDF_OK;                                     // asynchronous on the index's stream
+  return exchange_done(ix);                            // asynchronous on a caller's stream
 }
 
 extern "C" int tfidf_set_global_df_device(tfidf_index *ix, const void *d_df, uint64_t n, uint64_t doc_count,
@@ -2126,6 +2182,7 @@ extern "C" int tfidf_set_global_df_device(tfidf_index *ix, const void *d_df, uin
   ix->has_global = true;
   ix->g_doc_count = doc_count;
   ix->g_sum_ttf = sum_ttf;
+  if (int e = exchange_done(ix)) return e;
   return upload_cache(ix, false);
 }
 
@@ -2186,9 +2243,9 @@ extern "C" int tfidf_clear_global_stats(tfidf_index *ix) {
 
 // String.compareTo order of two UTF-8 names: Java compares UTF-16 code units,
 // so a supplementary code point (a surrogate pair, lead 0xD800..0xDBFF)
-// sorts below U+E000..U+FFFF although its code point is larger.  Code points
-// are compared with U+E000..U+FFFF lifted above the supplementary planes; a
-// malformed sequence compares by its bytes.
+// sorts below U+E000..U+FFFF although its code point is larger.  Both names
+// are walked as UTF-16 code units (a supplementary code point yields its lead,
+// then its trail surrogate); a malformed UTF-8 sequence compares by its bytes.
 static bool utf8_next(const uint8_t *s, uint64_t n, uint64_t *i, uint32_t *cp) {
   const uint8_t c = s[*i];
   uint32_t len = c < 0x80 ? 1 : (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : (c >> 3) == 30 ? 4 : 0;
@@ -2203,21 +2260,39 @@ static bool utf8_next(const uint8_t *s, uint64_t n, uint64_t *i, uint32_t *cp) {
   return true;
 }
 
+struct Utf16Units {                // UTF-8 bytes -> UTF-16 code units
+  const uint8_t *s;
+  uint64_t n, i = 0;
+  uint32_t trail = 0;              // pending trail surrogate of a supplementary code point
+  bool more() const { return trail || i < n; }
+  // next code unit; false (at byte i) if the UTF-8 there is malformed
+  bool next(uint32_t *u) {
+    if (trail) { *u = trail; trail = 0; return true; }
+    uint32_t cp;
+    if (!utf8_next(s, n, &i, &cp)) return false;
+    if (cp >= 0x10000) {
+      *u = 0xD800 + ((cp - 0x10000) >> 10);
+      trail = 0xDC00 + ((cp - 0x10000) & 0x3FF);
+    } else {
+      *u = cp;
+    }
+    return true;
+  }
+};
+
 static int utf16_compare(const uint8_t *a, uint64_t na, const uint8_t *b, uint64_t nb) {
-  uint64_t i = 0, j = 0;
-  while (i < na && j < nb) {
-    const uint64_t i0 = i, j0 = j;
-    uint32_t x, y;
-    if (!utf8_next(a, na, &i, &x) || !utf8_next(b, nb, &j, &y)) {   // malformed: bytes from here on
+  Utf16Units x{a, na}, y{b, nb};
+  while (x.more() && y.more()) {
+    const uint64_t i0 = x.i, j0 = y.i;
+    uint32_t u, v;
+    if (!x.next(&u) || !y.next(&v)) {                     // malformed: bytes from here on
       const uint64_t ra = na - i0, rb = nb - j0;
       const int c = memcmp(a + i0, b + j0, std::min(ra, rb));
       return c ? c : (ra < rb ? -1 : ra > rb);
     }
-    if (x >= 0xE000 && x <= 0xFFFF) x += 0x100000;
-    if (y >= 0xE000 && y <= 0xFFFF) y += 0x100000;
-    if (x != y) return x < y ? -1 : 1;
+    if (u != v) return u < v ? -1 : 1;
   }
-  return (na - i) == 0 && (nb - j) == 0 ? 0 : ((na - i) == 0 ? -1 : 1);
+  return x.more() ? 1 : (y.more() ? -1 : 0);
 }
 
 extern "C" int tfidf_sort_names(const uint8_t *names, const uint64_t *offsets, uint64_t n, uint64_t *perm) {

@@ -89,6 +89,7 @@ SIGNATURES = {
     "tfidf_load": (C.c_int, [VP, C.c_char_p]),
     "tfidf_add_docs_device": (C.c_int, [VP, VP, VP, C.c_uint64, C.c_uint64]),
     "tfidf_commit": (C.c_int, [VP]),
+    "tfidf_set_hash_attempt": (C.c_int, [VP, C.c_uint32]),
     "tfidf_get_commit_timing": (C.c_int, [VP, C.POINTER(CommitTiming)]),
     "tfidf_stats": (C.c_int, [VP, C.POINTER(IndexStats)]),
     "tfidf_search": (C.c_int, [VP, C.c_char_p, C.c_uint64, C.c_uint32, U32P, F32P, C.c_uint64, U64P]),
@@ -108,6 +109,7 @@ SIGNATURES = {
     "tfidf_doc_terms": (C.c_int, [VP, C.c_uint64, C.c_char_p, C.c_uint64, U32P, C.c_uint64, U64P]),
     "tfidf_term_df": (C.c_int, [VP, C.c_char_p, C.c_uint64, U64P, U64P]),
     "tfidf_vocab_size": (C.c_int, [VP, U64P]),
+    "tfidf_vocab_export": (C.c_int, [VP, U64P, U32P, U32P, C.c_uint64, U64P]),
     "tfidf_vocab_export_device": (C.c_int, [VP, VP, VP, C.c_uint64, U64P]),
     "tfidf_vocab_canonicalize_device": (C.c_int, [VP, VP, C.c_uint64, VP, C.c_uint64, U64P]),
     "tfidf_set_global_stats_device": (C.c_int, [VP, VP, C.c_uint64, C.c_uint64, C.c_uint64]),

@@ -27,6 +27,18 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
+from . import _lib as L
+
+# A query that does not parse (QueryParser ParseException / TooManyClauses) or
+# is not valid UTF-8: the reference's Worker answers [] (Worker.java:182-185),
+# so its Leader merges nothing.  The parse is deterministic, so every rank
+# raises for the same query and all of them skip the collectives together.
+QUERY_ERRORS = (L.QuerySyntaxError, L.UnsupportedQuery)
+
+
+def _query_errors(adapter):
+    return QUERY_ERRORS + tuple(getattr(adapter, "query_errors", ()))
+
 
 class HipShardAdapter:
     """Adapter over a ShardIndex whose buffers live on ``device`` (cuda:N).
@@ -43,11 +55,21 @@ class HipShardAdapter:
         s = self.shard.stats()
         return int(s["doc_count"]), int(s["sum_ttf"]), int(s["num_docs"])
 
-    def hash_seed(self):
-        """Seed of the shard's hashed term keys (0 unless its commit met a
-        collision and rebuilt): GLOBAL statistics match terms across shards by
-        key, so every shard must use the same one."""
-        return int(self.shard.stats()["hash_seed"])
+    def hash_attempt(self):
+        """Seed attempt of the shard's hashed term keys (0 unless its commit met
+        a collision and rebuilt): GLOBAL statistics match terms across shards by
+        key, so every shard must hash with the same seed."""
+        return int(self.shard.stats()["hash_rebuilds"])
+
+    def recommit(self, attempt):
+        """Rebuild the shard starting from seed attempt ``attempt`` (agreement
+        on one seed across ranks); -> the attempt now in force."""
+        self.shard.set_hash_attempt(attempt)
+        try:
+            self.shard.commit()
+        finally:
+            self.shard.set_hash_attempt(0)
+        return self.hash_attempt()
 
     # -- GLOBAL statistics (term ownership) --------------------------------
     def vocab_partition(self, n_ranks):
@@ -164,19 +186,28 @@ def _all_gather_var(t, n, group):
 def global_commit(adapter, group=None, vocab_size=False):
     """GLOBAL statistics by term ownership; call after the shard's own commit.
     Returns (global vocabulary size or None, docCount, sumTTF).  Host syncs:
-    one read of the gathered [per-owner counts | docCount | sumTTF] rows (the
-    all-to-all split sizes), plus one more only when vocab_size is asked for."""
+    one read of the gathered [per-owner counts | docCount | sumTTF | seed
+    attempt] rows (the all-to-all split sizes), plus one more only when
+    vocab_size is asked for.  Shards whose commits hashed with different seeds
+    (a collision on one shard) first agree on the highest: the others re-commit
+    under it, and the rows are gathered again."""
     dev = _dev(adapter)
     ws = dist.get_world_size(group)
     me = dist.get_rank(group)
-    dc, ttf, _ = adapter.local_stats()                      # host values of the shard's commit
-    seed = adapter.hash_seed() if hasattr(adapter, "hash_seed") else 0
-    rec, cnt = adapter.vocab_partition(ws)                  # device, asynchronous
-    meta = torch.cat([cnt.to(torch.int64), torch.tensor([dc, ttf, seed], dtype=torch.int64, device=dev)])
-    M = _all_gather(meta, group).cpu().tolist()             # the host sync
-    if len({int(M[r][ws + 2]) for r in range(ws)}) != 1:
-        raise RuntimeError("shards hash terms with different seeds (a commit met a hash collision and rebuilt): "
-                           "GLOBAL statistics need one seed on every shard")
+    while True:
+        dc, ttf, _ = adapter.local_stats()                  # host values of the shard's commit
+        att = adapter.hash_attempt() if hasattr(adapter, "hash_attempt") else 0
+        rec, cnt = adapter.vocab_partition(ws)              # device, asynchronous
+        meta = torch.cat([cnt.to(torch.int64), torch.tensor([dc, ttf, att], dtype=torch.int64, device=dev)])
+        M = _all_gather(meta, group).cpu().tolist()         # the host sync
+        top = max(int(M[r][ws + 2]) for r in range(ws))
+        if all(int(M[r][ws + 2]) == top for r in range(ws)):
+            break
+        # a shard met a hash collision and rebuilt under a later seed: keys are
+        # matched across shards, so the shards below it re-commit under that
+        # seed (which may collide there in turn: agree again)
+        if att < top:
+            adapter.recommit(top)
     send = [int(x) for x in M[me][:ws]]
     recv = [int(M[r][me]) for r in range(ws)]
     gdc = sum(int(M[r][ws]) for r in range(ws))
@@ -232,9 +263,13 @@ def _keys_to_hits(keys):
 def global_search(adapter, query: bytes, k: int, group=None):
     """Per-rank top-k (k >= 1) or every hit (k == 0, searcher.search(q,
     Integer.MAX_VALUE)) with global doc ids; all-gather of the packed keys;
-    device merge.  Returns [(global doc, score)] in (score desc, doc asc)."""
+    device merge.  Returns [(global doc, score)] in (score desc, doc asc);
+    [] for a query that does not parse (as the batch path, and the reference)."""
     if k == 0:
-        mine = adapter.all_keys(query)
+        try:
+            mine = adapter.all_keys(query)
+        except _query_errors(adapter):
+            return []
         allk, _ = _all_gather_var(mine, mine.shape[0], group)
         allk = torch.sort(allk, descending=True).values
         return _keys_to_hits(allk)
@@ -320,7 +355,10 @@ def shard_search(adapter, names: ShardNames, query: bytes, group=None):
     summed in rank order (HashMap.merge Double::sum, Leader.java:73-77) and the
     result is ordered by name (TreeMap, :80-88).  Returns [(name, score)]."""
     ws = dist.get_world_size(group)
-    keys = adapter.all_keys(query, doc_base=0)                      # local doc ids
+    try:
+        keys = adapter.all_keys(query, doc_base=0)                  # local doc ids
+    except _query_errors(adapter):
+        return []
     doc = (~keys) & 0xFFFFFFFF
     rec = torch.stack([names.local_ids[doc], keys >> 32], 1)        # (name id, score bits)
     allr, ns = _all_gather_var(rec, rec.shape[0], group)            # rank order

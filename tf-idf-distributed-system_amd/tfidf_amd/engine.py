@@ -104,6 +104,10 @@ class ShardIndex:
     def commit(self):
         L.check(L.load().tfidf_commit(self._h))
 
+    def set_hash_attempt(self, attempt):
+        """Seed attempt (0..3) the following commits start from (tfidf_set_hash_attempt)."""
+        L.check(L.load().tfidf_set_hash_attempt(self._h, attempt))
+
     def commit_timing(self):
         t = L.CommitTiming()
         L.check(L.load().tfidf_get_commit_timing(self._h, C.byref(t)))
@@ -259,6 +263,18 @@ class ShardIndex:
         L.check(L.load().tfidf_vocab_size(self._h, C.byref(n)))
         return n.value
 
+    def vocab_export(self):
+        """(keys uint64 [n, 2] (lo, hi) sorted by (hi, lo), df_local uint32 [n],
+        df_effective uint32 [n]): the vocabulary with the statistics in force."""
+        n = self.vocab_size()
+        keys = np.zeros((max(n, 1), 2), np.uint64)
+        dl = np.zeros(max(n, 1), np.uint32)
+        de = np.zeros(max(n, 1), np.uint32)
+        m = C.c_uint64()
+        L.check(L.load().tfidf_vocab_export(self._h, L.ptr(keys, C.c_uint64), L.ptr(dl, C.c_uint32),
+                                            L.ptr(de, C.c_uint32), len(dl), C.byref(m)))
+        return keys[:m.value], dl[:m.value], de[:m.value]
+
     def vocab_export_device(self, d_keys, d_df, cap):
         n = C.c_uint64()
         L.check(L.load().tfidf_vocab_export_device(self._h, C.c_void_p(d_keys), C.c_void_p(d_df), cap, C.byref(n)))
@@ -276,14 +292,18 @@ class ShardIndex:
 
     def vocab_partition_device(self, n_ranks, d_records, cap, d_counts):
         """Records (lo, hi, df) grouped by owner rank into d_records, per-owner
-        counts (u64) into d_counts; asynchronous on the index's stream -> n records."""
+        counts (u64) into d_counts -> n records.  Asynchronous on a stream set
+        by set_stream (the buffers must then stay live until that stream
+        reaches the work: torch tensors of that stream do); on the index's own
+        stream it returns with the work done."""
         n = C.c_uint64()
         L.check(L.load().tfidf_vocab_partition_device(self._h, n_ranks, C.c_void_p(d_records), cap,
                                                       C.c_void_p(d_counts), C.byref(n)))
         return n.value
 
     def vocab_reduce_device(self, d_records, n, d_df_out, d_n_unique=None):
-        """Owner side: summed df per received record (asynchronous)."""
+        """Owner side: summed df per received record (asynchronous on a
+        set_stream stream, like vocab_partition_device)."""
         L.check(L.load().tfidf_vocab_reduce_device(self._h, C.c_void_p(d_records), n, C.c_void_p(d_df_out),
                                                    C.c_void_p(d_n_unique) if d_n_unique else None))
 
