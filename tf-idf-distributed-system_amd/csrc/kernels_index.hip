@@ -420,7 +420,7 @@ struct WaveSmem {
   alignas(16) uint32_t list[kWaveTokens];        // token spans (start | end << 16); then term slots (u16)
   alignas(16) uint64_t qkey[kWaveQueue];         // histogram retry queue
   alignas(16) uint16_t qslot[kWaveQueue];
-  alignas(16) uint64_t noop[64];                 // per-lane no-op atomic target (stays 0)
+  alignas(16) uint2 sel[64];                     // key byte-selector table (init_sel_table)
 };
 
 // DPP wave-wide inclusive prefix sum (row shifts, then row broadcasts 15/31).
@@ -443,7 +443,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 // PACK: *wbase = the same mask before the joiner rules (letters, digits, '_').
 template <bool PACK>
 __device__ __forceinline__ uint64_t lane_word_mask(const uint8_t *text, uint32_t lane, bool *bad, bool *under,
-                                                   uint64_t *wbase) {
+                                                   uint64_t *wbase, bool *upper) {
   uint32_t x[16];
   {
     const uint4 *t = reinterpret_cast<const uint4 *>(text + lane * 64);
@@ -455,14 +455,17 @@ __device__ __forceinline__ uint64_t lane_word_mask(const uint8_t *text, uint32_t
   }
   // pass 1: letter/digit flags (neighbour context), non-ASCII, joiner presence
   uint32_t LD[16];
-  uint32_t badacc = 0, P = 0;
+  uint32_t badacc = 0, P = 0, U = 0;
 #pragma unroll
   for (int i = 0; i < 16; i++) {
     const uint32_t D = swar_digit(x[i]);
-    LD[i] = swar_letter(x[i]) | (D >> 1);
+    const uint32_t Lt = swar_letter(x[i]);
+    LD[i] = Lt | (D >> 1);
+    U |= Lt & ~(x[i] << 2);                                     // letters without the 0x20 bit: 'A'..'Z'
     badacc |= x[i];
     P |= (x[i] + 0x59595959u) & ~(x[i] + 0x44444444u) & ~D;   // ' ( ) * + , - . / : ; (candidate joiners)
   }
+  *upper = __any(U != 0);
   uint32_t ldp = __shfl_up(LD[15], 1, 64);
   uint32_t ldn = __shfl_down(LD[0], 1, 64);
   if (lane == 0) ldp = 0;
@@ -696,164 +699,218 @@ __device__ __forceinline__ void clear_table(WaveSmem &sm, uint32_t lane) {
   for (int q = 0; q < (int)(kWaveSlots * 2 / 16 / 64); q++) cw[lane + 64 * q] = make_uint4(0, 0, 0, 0);
 }
 
-// One batch of the per-document histogram: lane l keys tokens tb + l + 64k
-// (k < K) of the token list, all LDS reads in flight, then probe rounds over
-// the table (branch-free: idle lanes CAS a no-op slot), then a retry queue of
-// two entries per lane once few tokens are left.
+// ---- histogram, lane-mask form (round 3).  Per-token state that is a
+// yes/no per lane (in range, pending, hit) stays in wave lane masks (SGPRs):
+// the probe bookkeeping and the token / distinct-term counts are scalar
+// instructions, and the conditional LDS atomics run under EXEC instead of
+// being aimed at no-op slots.  Keys are cut out of the staged text with one
+// v_perm_b32 per key dword, whose selector (from a small LDS table indexed by
+// token length and start & 3) both aligns the bytes and zeroes those past the
+// token's end.  Slot hash: one full-rate 24-bit multiply.
+//
+// Selector table (in the wave's former no-op area): entry 4 n + o, n = 0..8
+// bytes, o = start & 3: {sel0, sel1}; key dword 0 = perm(dw1, dw0, sel0),
+// dword 1 = perm(dw2, dw1, sel1) where dw0..2 are the text dwords from
+// start & ~3; selector byte 12 yields 0x00.
+constexpr uint32_t kSelEntries = 36;
+__device__ __forceinline__ void init_sel_table(uint2 *tab, uint32_t lane) {
+  if (lane < kSelEntries) {
+    const uint32_t n = lane >> 2, o = lane & 3;
+    uint32_t s0 = 0, s1 = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; i++) {
+      s0 |= (i < n ? o + i : 12u) << (8 * i);
+      s1 |= (i + 4 < n ? o + i : 12u) << (8 * i);
+    }
+    tab[lane] = make_uint2(s0, s1);
+  }
+}
+__device__ __forceinline__ uint32_t table_slot(uint32_t l0, uint32_t l1) {
+  const uint32_t x = l0 ^ __builtin_amdgcn_alignbit(l1, l1, 16);
+  return (uint32_t)__umul24(x ^ (x >> 11), 0x2C1B3Du) >> (32 - kWaveSlotBits);
+}
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+__device__ __forceinline__ void count_add(WaveSmem &sm, uint32_t slot) {
+  atomicAdd(&sm.cnt[slot >> 1], 1u << (16 * (slot & 1)));
+}
+// Does a table entry `old` resolve the token keyed `tk` (claimed: old == 0)?
+template <bool FOLD>
+__device__ __forceinline__ bool entry_hit(const WaveSmem &sm, uint64_t old, uint64_t tk) {
+  bool hit = (old == 0) | (old == tk);
+  if (FOLD && !hit && ((old & tk) >> 63) && ((old ^ tk) & ~kFoldPosMask) == 0)
+    hit = span_same(sm.text, (uint32_t)(old >> 13) & 0x1FFFu, (uint32_t)(tk >> 13) & 0x1FFFu, (uint32_t)tk & 0xFFu);
+  return hit;
+}
+
+// One batch of 64 K tokens [tb, tb + 64 K) of the list (entries past ntok
+// are ignored).  claims / toks: wave-uniform running counts of distinct
+// terms / counted tokens.
 template <int K, bool FOLD, bool PACK>
-__device__ __forceinline__ void hist_batch(WaveSmem &sm, const BuildParams &p, uint64_t d, uint32_t lane, uint32_t tb,
-                                           uint32_t ntok, bool under, unsigned long long *noop, uint32_t &claims,
-                                           uint32_t &toks, bool &overflow) {
+__device__ __forceinline__ void hist2(WaveSmem &sm, uint32_t lane, uint32_t tb, uint32_t ntok, bool under, bool upper,
+                                      uint32_t &claims, uint32_t &toks, bool &overflow) {
   const uint32_t *tw = reinterpret_cast<const uint32_t *>(sm.text);
+  const uint2 *sel = sm.sel;
+  const uint32_t left = ntok - tb;                       // wave-uniform
+  uint32_t ent[K], dw[K][3];
+  uint2 sl[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) ent[k] = sm.list[tb + lane + 64 * k];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const uint32_t tp = ent[k] & kSpanMask, n = ((ent[k] >> 16) & kSpanMask) - tp;
+    const uint32_t a0 = tp >> 2;
+    dw[k][0] = tw[a0]; dw[k][1] = tw[a0 + 1]; dw[k][2] = tw[a0 + 2];
+    sl[k] = sel[(min(n, 8u) << 2) | (tp & 3u)];
+  }
   uint64_t tkey[K];
   uint32_t slot[K];
-  uint32_t pendm = 0, longm = 0;
-  // keys of <= 8 bytes: all list reads, then all text reads, then the math
-  uint32_t ent[K];
+  bool pend[K], lng[K];
+  uint32_t t0[K], t1[K];
 #pragma unroll
   for (int k = 0; k < K; k++) {
-    const uint32_t idx = tb + lane + 64 * k;
-    ent[k] = sm.list[idx < ntok ? idx : 0u];
+    t0[k] = __builtin_amdgcn_perm(dw[k][1], dw[k][0], sl[k].x);
+    t1[k] = __builtin_amdgcn_perm(dw[k][2], dw[k][1], sl[k].y);
   }
-  uint32_t dw[K][3];
+  if (upper) {
 #pragma unroll
-  for (int k = 0; k < K; k++) {
-    const uint32_t a0 = (ent[k] & kSpanMask) >> 2;
-    dw[k][0] = tw[a0]; dw[k][1] = tw[a0 + 1]; dw[k][2] = tw[a0 + 2];
+    for (int k = 0; k < K; k++) { t0[k] = lower4(t0[k]); t1[k] = lower4(t1[k]); }
   }
 #pragma unroll
   for (int k = 0; k < K; k++) {
-    const bool in = tb + lane + 64 * k < ntok;
-    const uint32_t tp = ent[k] & kSpanMask, n = ((ent[k] >> 16) & kSpanMask) - tp, o = tp & 3;
-    const uint64_t m64 = n >= 8 ? ~0ull : ((1ull << (8 * n)) - 1);
-    const uint32_t t0 = __builtin_amdgcn_alignbyte(dw[k][1], dw[k][0], o) & (uint32_t)m64;
-    const uint32_t t1 = __builtin_amdgcn_alignbyte(dw[k][2], dw[k][1], o) & (uint32_t)(m64 >> 32);
-    const bool valid = !(FOLD && under) |
-                       ((((t0 ^ 0x5F5F5F5Fu) & (uint32_t)m64) | ((t1 ^ 0x5F5F5F5Fu) & (uint32_t)(m64 >> 32))) != 0);
-    const uint32_t l0 = lower4(t0) | (PACK ? pack_tag(span_doc(ent[k])) : 0u), l1 = lower4(t1);
-    tkey[k] = (uint64_t)l0 | ((uint64_t)l1 << 32);
-    slot[k] = ((l0 ^ rotl32(l1, 16)) * 0x85EBCA77u) >> (32 - kWaveSlotBits);
-    pendm |= (uint32_t)(in & (n <= 8) & valid) << k;
-    longm |= (uint32_t)(in & (n > 8)) << k;
+    const uint32_t tp = ent[k] & kSpanMask, n = ((ent[k] >> 16) & kSpanMask) - tp;
+    const bool in = lane + 64u * k < left;
+    bool valid = true;
+    if (FOLD && under)   // a span of '_' only is not a token
+      valid = (t0[k] != __builtin_amdgcn_perm(0x5F5F5F5Fu, 0x5F5F5F5Fu, sl[k].x)) |
+              (t1[k] != __builtin_amdgcn_perm(0x5F5F5F5Fu, 0x5F5F5F5Fu, sl[k].y));
+    const uint32_t l0 = t0[k] | (PACK ? pack_tag(span_doc(ent[k])) : 0u);
+    tkey[k] = (uint64_t)l0 | ((uint64_t)t1[k] << 32);
+    slot[k] = table_slot(l0, t1[k]);
+    pend[k] = in & (n <= 8) & valid;
+    lng[k] = FOLD && (in & (n > 8));
   }
-  if (FOLD && __any(longm != 0)) {                      // tokens of 9..255 bytes: folded keys
-    bool toolong = false;
+  if (FOLD) {                                            // tokens of 9..255 bytes: folded keys
+    bool anyl = false;
 #pragma unroll
-    for (int k = 0; k < K; k++) {
-      if ((longm >> k) & 1u) {
-        const uint32_t e = sm.list[tb + lane + 64 * k];
-        const uint32_t tp = e & kSpanMask, n = ((e >> 16) & kSpanMask) - tp;
-        if (n > kMaxTokenLen) {
-          toolong = true;
-        } else {
-          uint32_t h;
-          bool valid;
-          tkey[k] = fold_key(sm.text, tp, n, &h, &valid);
-          if (PACK) {
-            tkey[k] |= (uint64_t)span_doc(e) << 8;
-            h ^= span_doc(e) * 0x9E3779B1u;
-          }
-          slot[k] = h >> (32 - kWaveSlotBits);
-          pendm |= (uint32_t)valid << k;
-        }
-      }
-    }
-    if (__any(toolong)) { overflow = true; return; }    // > 255 chars: the long path cuts it
-  }
-  toks += (uint32_t)__popc(pendm);
-  for (uint32_t round = 0;; round++) {
-    const uint32_t np = (uint32_t)__popc(pendm);
-    const uint32_t pincl = wave_incl_add(np);
-    const uint32_t P = (uint32_t)__builtin_amdgcn_readlane((int)pincl, 63);
-    if (P == 0) return;
-    if (round >= kWaveSlots) { overflow = true; return; }
-    if (P <= kWaveQueue) {                                // few left: two-per-lane queue
-      // retry queue: two unresolved tokens per lane, probed until resolved
-      uint32_t at = pincl - np;
-#pragma unroll
-      for (int k = 0; k < K; k++)
-        if ((pendm >> k) & 1u) { sm.qkey[at] = tkey[k]; sm.qslot[at] = (uint16_t)slot[k]; at++; }
-      asm volatile("" ::: "memory");
-      if (P > kWaveQueue) { overflow = true; return; }     // cannot happen for K <= 2
-      uint64_t qk[2];
-      uint32_t qs[2];
-      bool qp[2];
-#pragma unroll
-      for (int i = 0; i < 2; i++) {
-        const uint32_t idx = lane + 64 * i;
-        qp[i] = idx < P;
-        qk[i] = qp[i] ? sm.qkey[idx] : 0ull;
-        qs[i] = qp[i] ? sm.qslot[idx] : 0u;
-      }
-      for (uint32_t it = 0; __any(qp[0] | qp[1]); it++) {
-        if (it >= kWaveSlots) { overflow = true; return; }
-        uint64_t old[2];
-#pragma unroll
-        for (int i = 0; i < 2; i++)
-          old[i] = atomicCAS(qp[i] ? reinterpret_cast<unsigned long long *>(&sm.key[qs[i]]) : noop,
-                             qp[i] ? 0ull : ~0ull, (unsigned long long)qk[i]);
-        __builtin_amdgcn_sched_barrier(0);     // every CAS issued before the first result is waited on
-#pragma unroll
-        for (int i = 0; i < 2; i++) {
-          bool hit = qp[i] & ((old[i] == 0) | (old[i] == qk[i]));
-          const bool fc = FOLD && qp[i] & !hit & (((old[i] & qk[i]) >> 63) != 0) &
-                          (((old[i] ^ qk[i]) & ~kFoldPosMask) == 0);
-          if (fc)
-            hit = span_same(sm.text, (uint32_t)(old[i] >> 13) & 0x1FFFu, (uint32_t)(qk[i] >> 13) & 0x1FFFu,
-                            (uint32_t)qk[i] & 0xFFu);
-          atomicAdd(hit ? &sm.cnt[qs[i] >> 1] : reinterpret_cast<uint32_t *>(noop),
-                    hit ? 1u << (16 * (qs[i] & 1)) : 0u);
-          claims += (uint32_t)(hit & (old[i] == 0));
-          const bool adv = qp[i] & !hit;
-          qs[i] = adv ? ((qs[i] + 1) & (kWaveSlots - 1)) : qs[i];
-          qp[i] = adv;
-        }
-      }
-      return;
-    }
-    // one probe round for every pending token (no-op CAS for the others)
-    uint64_t old[K];
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-      const bool pend = (pendm >> k) & 1u;
-      old[k] = atomicCAS(pend ? reinterpret_cast<unsigned long long *>(&sm.key[slot[k]]) : noop,
-                         pend ? 0ull : ~0ull, (unsigned long long)tkey[k]);
-    }
-    // keep all K returning CASes in flight together: without this barrier the
-    // scheduler interleaves each result's compare and so waits out every round
-    // trip in turn (measured: K serialized LDS latencies per probe round)
-    __builtin_amdgcn_sched_barrier(0);
-    uint32_t foldm = 0;
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-      const bool pend = (pendm >> k) & 1u;
-      const bool z = old[k] == 0;
-      const bool hit = pend & (z | (old[k] == tkey[k]));
-      atomicAdd(hit ? &sm.cnt[slot[k] >> 1] : reinterpret_cast<uint32_t *>(noop),
-                hit ? 1u << (16 * (slot[k] & 1)) : 0u);
-      claims += (uint32_t)(hit & z);
-      pendm &= ~((uint32_t)hit << k);
-      // same folded hash, other position: exact compare below (always false without long tokens)
-      const bool fc = FOLD && pend & !hit & (((old[k] & tkey[k]) >> 63) != 0) &
-                      (((old[k] ^ tkey[k]) & ~kFoldPosMask) == 0);
-      foldm |= (uint32_t)fc << k;
-      const bool adv = pend & !hit & !fc;
-      slot[k] = adv ? ((slot[k] + 1) & (kWaveSlots - 1)) : slot[k];
-    }
-    if (FOLD && __any(foldm != 0)) {                      // same length and hash: compare bytes
+    for (int k = 0; k < K; k++) anyl |= lng[k];
+    if (__any(anyl)) {
+      bool toolong = false;
 #pragma unroll
       for (int k = 0; k < K; k++) {
-        if ((foldm >> k) & 1u) {
-          if (span_same(sm.text, (uint32_t)(old[k] >> 13) & 0x1FFFu, (uint32_t)(tkey[k] >> 13) & 0x1FFFu,
-                        (uint32_t)tkey[k] & 0xFFu)) {
-            atomicAdd(&sm.cnt[slot[k] >> 1], 1u << (16 * (slot[k] & 1)));
-            pendm &= ~(1u << k);
+        if (lng[k]) {
+          const uint32_t e = ent[k];
+          const uint32_t tp = e & kSpanMask, n = ((e >> 16) & kSpanMask) - tp;
+          if (n > kMaxTokenLen) {
+            toolong = true;
           } else {
-            slot[k] = (slot[k] + 1) & (kWaveSlots - 1);
+            uint32_t h;
+            bool valid;
+            tkey[k] = fold_key(sm.text, tp, n, &h, &valid);
+            if (PACK) {
+              tkey[k] |= (uint64_t)span_doc(e) << 8;
+              h ^= span_doc(e) * 0x9E3779B1u;
+            }
+            slot[k] = h >> (32 - kWaveSlotBits);
+            pend[k] = valid;
           }
         }
       }
+      if (__any(toolong)) { overflow = true; return; }     // > 255 chars: the long path cuts it
     }
+  }
+  uint32_t P = 0;
+#pragma unroll
+  for (int k = 0; k < K; k++) P += (uint32_t)__popcll(__ballot(pend[k]));
+  toks += P;
+  // round 1: every token's home slot, all CASes in flight
+  uint64_t old[K];
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    old[k] = 0;
+    if (pend[k]) old[k] = atomicCAS(reinterpret_cast<unsigned long long *>(&sm.key[slot[k]]), 0ull,
+                                    (unsigned long long)tkey[k]);
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  P = 0;
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    const bool hit = pend[k] && entry_hit<FOLD>(sm, old[k], tkey[k]);
+    if (hit) count_add(sm, slot[k]);
+    claims += (uint32_t)__popcll(__ballot(hit & (old[k] == 0)));
+    pend[k] = pend[k] & !hit;
+    if (pend[k]) slot[k] = (slot[k] + 1) & (kWaveSlots - 1);
+    P += (uint32_t)__popcll(__ballot(pend[k]));
+  }
+  // further rounds over every pending token while many remain
+  for (uint32_t round = 1; P > kWaveQueue; round++) {
+    if (round >= kWaveSlots) { overflow = true; return; }
+#pragma unroll
+    for (int k = 0; k < K; k++)
+      if (pend[k]) old[k] = atomicCAS(reinterpret_cast<unsigned long long *>(&sm.key[slot[k]]), 0ull,
+                                      (unsigned long long)tkey[k]);
+    __builtin_amdgcn_sched_barrier(0);
+    P = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const bool hit = pend[k] && entry_hit<FOLD>(sm, old[k], tkey[k]);
+      if (hit) count_add(sm, slot[k]);
+      claims += (uint32_t)__popcll(__ballot(hit & (old[k] == 0)));
+      pend[k] = pend[k] & !hit;
+      if (pend[k]) slot[k] = (slot[k] + 1) & (kWaveSlots - 1);
+      P += (uint32_t)__popcll(__ballot(pend[k]));
+    }
+  }
+  if (P == 0) return;
+  // the rest (<= 128): compacted into a queue, one or two per lane, probed to the end
+  {
+    uint32_t at = 0;
+#pragma unroll
+    for (int k = 0; k < K; k++) {
+      const uint64_t m = __ballot(pend[k]);
+      if (m) {
+        if (pend[k]) {
+          const uint32_t q = at + lanes_below(m);
+          sm.qkey[q] = tkey[k];
+          sm.qslot[q] = (uint16_t)slot[k];
+        }
+        at += (uint32_t)__popcll(m);
+      }
+    }
+  }
+  asm volatile("" ::: "memory");
+  uint64_t qk[2];
+  uint32_t qs[2];
+  bool qp[2];
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    qp[i] = lane + 64u * i < P;
+    qk[i] = qp[i] ? sm.qkey[lane + 64 * i] : 0ull;
+    qs[i] = qp[i] ? sm.qslot[lane + 64 * i] : 0u;
+  }
+  const int nq = P > 64 ? 2 : 1;
+  for (uint32_t it = 0;; it++) {
+    if (it >= kWaveSlots) { overflow = true; return; }
+    uint64_t qo[2] = {0, 0};
+#pragma unroll
+    for (int i = 0; i < 2; i++)
+      if (i < nq && qp[i]) qo[i] = atomicCAS(reinterpret_cast<unsigned long long *>(&sm.key[qs[i]]), 0ull,
+                                             (unsigned long long)qk[i]);
+    __builtin_amdgcn_sched_barrier(0);
+    bool more = false;
+#pragma unroll
+    for (int i = 0; i < 2; i++) {
+      if (i < nq) {
+        const bool hit = qp[i] && entry_hit<FOLD>(sm, qo[i], qk[i]);
+        if (hit) count_add(sm, qs[i]);
+        claims += (uint32_t)__popcll(__ballot(hit & (qo[i] == 0)));
+        qp[i] = qp[i] & !hit;
+        if (qp[i]) qs[i] = (qs[i] + 1) & (kWaveSlots - 1);
+        more |= qp[i];
+      }
+    }
+    if (!__any(more)) break;
   }
 }
 
@@ -1027,7 +1084,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   __shared__ WaveSmem sm;
   const uint32_t lane = threadIdx.x;
   clear_table(sm, lane);           // table starts empty; every document leaves it empty
-  sm.noop[lane] = 0;
+  init_sel_table(sm.sel, lane);
   unsigned long long my_doc_count = 0, my_ttf = 0, my_nnz = 0;
   uint4 v[4] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
   const uint64_t n_units = PACK ? (p.n_docs + p.pack - 1) / p.pack : (p.doc_list ? *p.doc_list_count : p.n_docs);
@@ -1038,7 +1095,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   }
   const uint32_t R = p.n_ranges;
   uint16_t *slots = reinterpret_cast<uint16_t *>(sm.list);
-  unsigned long long *noop = reinterpret_cast<unsigned long long *>(&sm.noop[lane]);
   // PACK per-document scratch in the histogram queue area (free after the histogram)
   uint32_t *pk_len = reinterpret_cast<uint32_t *>(sm.qkey), *pk_nu = pk_len + kPackMax,
            *pk_start = pk_len + 2 * kPackMax;
@@ -1082,7 +1138,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     // ---- classify + spans -> dense token list
     bool bad, under;
     uint64_t wbase = 0;
-    uint64_t W = lane_word_mask<PACK>(sm.text, lane, &bad, &under, &wbase);
+    bool upper;
+    uint64_t W = lane_word_mask<PACK>(sm.text, lane, &bad, &under, &wbase, &upper);
     // PACK: document boundaries q_j (window position of document j's first
     // byte, j >= 1).  No token spans one: a joiner next to q_j that is a word
     // byte only through its neighbour across q_j is dropped, and a token is
@@ -1165,24 +1222,23 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     // ---- per-document histogram in LDS (folded-key and '_'-only checks only
     // when the document holds a token of more than 8 bytes or a '_')
     const bool anylong = __any(longtok) || under;
-    uint32_t claims = 0, toks = 0;
+    uint32_t nu = 0, len = 0;
     bool overflow = false;
     for (uint32_t tb = 0; tb < ntok && !overflow;) {       // batch width by what is left
       const uint32_t rem = ntok - tb;
       if (anylong) {
-        if (!PACK && rem > 512 && rem <= 640) { hist_batch<10, true, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 640; }
-        else if (rem > 256) { hist_batch<8, true, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 512; }
-        else if (rem > 128) { hist_batch<4, true, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 256; }
-        else { hist_batch<2, true, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 128; }
+        if (!PACK && rem > 512 && rem <= 640) { hist2<10, true, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 640; }
+        else if (rem > 256) { hist2<8, true, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 512; }
+        else if (rem > 128) { hist2<4, true, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 256; }
+        else { hist2<2, true, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 128; }
       } else {
         // 513..640 tokens (U[400, 600]-token documents: ~40 % of cfg 2) in one batch
-        if (!PACK && rem > 512 && rem <= 640) { hist_batch<10, false, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 640; }
-        else if (rem > 256) { hist_batch<8, false, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 512; }
-        else if (rem > 128) { hist_batch<4, false, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 256; }
-        else { hist_batch<2, false, PACK>(sm, p, d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 128; }
+        if (!PACK && rem > 512 && rem <= 640) { hist2<10, false, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 640; }
+        else if (rem > 256) { hist2<8, false, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 512; }
+        else if (rem > 128) { hist2<4, false, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 256; }
+        else { hist2<2, false, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 128; }
       }
     }
-    const uint32_t len = wave_sum(toks), nu = wave_sum(claims);
     if (overflow || nu > kWaveTerms) {                      // wave-uniform: long path
       clear_table(sm, lane);
       if (PACK) defer_pack(p, d, np, lane);
@@ -1368,11 +1424,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   __shared__ WaveSmem sm;
   const uint32_t lane = threadIdx.x;
   clear_table(sm, lane);
-  sm.noop[lane] = 0;
+  init_sel_table(sm.sel, lane);
   uint4 v[4] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
   const uint64_t n_units = p.n_chunks;
   const uint64_t C = (uint64_t)p.cap_mask + 1;
-  unsigned long long *noop = reinterpret_cast<unsigned long long *>(&sm.noop[lane]);
   uint16_t *slots = reinterpret_cast<uint16_t *>(sm.list);
   ChunkMeta meta;
   auto prefetch = [&](const ChunkMeta &m) {
@@ -1408,7 +1463,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     const uint32_t fail_at = m.gi;
     bool bad, under;
     uint64_t wbase = 0;
-    const uint64_t W = lane_word_mask<false>(sm.text, lane, &bad, &under, &wbase);
+    bool upper;
+    const uint64_t W = lane_word_mask<false>(sm.text, lane, &bad, &under, &wbase, &upper);
     if (bad) {                                               // non-ASCII: the whole document -> long path
       if (lane == 0) p.chunk_fail[fail_at] = 1u;
       continue;
@@ -1450,21 +1506,20 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     }
     asm volatile("" ::: "memory");
     const bool anylong = __any(longtok) || under;
-    uint32_t claims = 0, toks = 0;
+    uint32_t nu = 0, toks = 0;
     bool overflow = false;
     for (uint32_t tb = 0; tb < ntok && !overflow;) {
       const uint32_t rem = ntok - tb;
       if (anylong) {
-        if (rem > 256) { hist_batch<8, true, false>(sm, p, m.d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 512; }
-        else if (rem > 128) { hist_batch<4, true, false>(sm, p, m.d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 256; }
-        else { hist_batch<2, true, false>(sm, p, m.d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 128; }
+        if (rem > 256) { hist2<8, true, false>(sm, lane, tb, ntok, under, upper, nu, toks, overflow); tb += 512; }
+        else if (rem > 128) { hist2<4, true, false>(sm, lane, tb, ntok, under, upper, nu, toks, overflow); tb += 256; }
+        else { hist2<2, true, false>(sm, lane, tb, ntok, under, upper, nu, toks, overflow); tb += 128; }
       } else {
-        if (rem > 256) { hist_batch<8, false, false>(sm, p, m.d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 512; }
-        else if (rem > 128) { hist_batch<4, false, false>(sm, p, m.d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 256; }
-        else { hist_batch<2, false, false>(sm, p, m.d, lane, tb, ntok, under, noop, claims, toks, overflow); tb += 128; }
+        if (rem > 256) { hist2<8, false, false>(sm, lane, tb, ntok, under, upper, nu, toks, overflow); tb += 512; }
+        else if (rem > 128) { hist2<4, false, false>(sm, lane, tb, ntok, under, upper, nu, toks, overflow); tb += 256; }
+        else { hist2<2, false, false>(sm, lane, tb, ntok, under, upper, nu, toks, overflow); tb += 128; }
       }
     }
-    const uint32_t nu = wave_sum(claims);
     if (overflow || nu > kWaveTerms) {
       clear_table(sm, lane);
       if (lane == 0) p.chunk_fail[fail_at] = 1u;
