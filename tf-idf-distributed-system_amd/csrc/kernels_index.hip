@@ -382,6 +382,9 @@ constexpr uint32_t kWaveSlots = 1024;             // per-document LDS table
 constexpr uint32_t kWaveSlotBits = 10;
 constexpr uint32_t kWaveTokens = 1024;            // token list capacity
 constexpr uint32_t kWaveK = 8;                    // tokens / terms per lane in flight
+#ifndef TFIDF_HIST10
+#define TFIDF_HIST10 0                            // 10-token-per-lane batches for 513..640-token documents
+#endif
 constexpr uint32_t kWaveTerms = 64 * kWaveK;      // distinct terms per document (wave path)
 constexpr uint32_t kWaveQueue = 128;              // histogram retry queue: two entries per lane
 constexpr uint32_t kDictQueue = 64;               // dictionary retry queue: one entry per lane
@@ -632,8 +635,8 @@ template <bool PACK>
 __device__ __forceinline__ DocMeta unit_meta(const BuildParams &p, uint64_t u, uint32_t lane) {
   DocMeta m;
   if (!PACK) {
-    m.d = p.doc_list ? p.doc_list[u] : u;
-    m.src = p.live_map ? p.live_map[m.d] : m.d;
+    m.d = TFIDF_COLD(doc_list) ? TFIDF_COLD(doc_list)[u] : u;
+    m.src = TFIDF_COLD(live_map) ? TFIDF_COLD(live_map)[m.d] : m.d;
     m.s0 = p.offsets[m.src];
     m.L = p.offsets[m.src + 1] - m.s0;
     m.pofs = 0;
@@ -644,7 +647,7 @@ __device__ __forceinline__ DocMeta unit_meta(const BuildParams &p, uint64_t u, u
     const uint32_t np = (uint32_t)min((uint64_t)p.pack, p.n_docs - m.d);
     const uint32_t j = lane < np ? lane : np - 1;
     // lane j < np: source of document d + j; lanes >= np: one past the last source
-    const uint64_t sj = (p.live_map ? (uint64_t)p.live_map[m.d + j] : m.d + j) + (lane < np ? 0u : 1u);
+    const uint64_t sj = (TFIDF_COLD(live_map) ? (uint64_t)TFIDF_COLD(live_map)[m.d + j] : m.d + j) + (lane < np ? 0u : 1u);
     m.src = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(sj >> 32), 0) << 32) |
             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sj, 0);
     const bool contig = __all(lane > np || sj == m.src + lane);
@@ -669,9 +672,9 @@ __device__ __forceinline__ bool fits_wave(const DocMeta &m) { return m.ok && m.s
 // PACK: documents d .. d + np - 1 go to the single-document pass.
 __device__ __forceinline__ void defer_pack(const BuildParams &p, uint64_t d, uint32_t np, uint32_t lane) {
   uint32_t base = 0;
-  if (lane == 0) base = atomicAdd(p.retry_count, np);
+  if (lane == 0) base = atomicAdd(TFIDF_COLD(retry_count), np);
   base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
-  if (lane < np) p.retry_list[base + lane] = (uint32_t)(d + lane);
+  if (lane < np) TFIDF_COLD(retry_list)[base + lane] = (uint32_t)(d + lane);
 }
 
 __device__ __forceinline__ void prefetch_wave(const BuildParams &p, const DocMeta &m, uint32_t lane, uint4 *v) {
@@ -732,16 +735,50 @@ __device__ __forceinline__ uint32_t table_slot(uint32_t l0, uint32_t l1) {
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
-__device__ __forceinline__ void count_add(WaveSmem &sm, uint32_t slot) {
-  atomicAdd(&sm.cnt[slot >> 1], 1u << (16 * (slot & 1)));
-}
-// Does a table entry `old` resolve the token keyed `tk` (claimed: old == 0)?
-template <bool FOLD>
-__device__ __forceinline__ bool entry_hit(const WaveSmem &sm, uint64_t old, uint64_t tk) {
-  bool hit = (old == 0) | (old == tk);
-  if (FOLD && !hit && ((old & tk) >> 63) && ((old ^ tk) & ~kFoldPosMask) == 0)
-    hit = span_same(sm.text, (uint32_t)(old >> 13) & 0x1FFFu, (uint32_t)(tk >> 13) & 0x1FFFu, (uint32_t)tk & 0xFFu);
-  return hit;
+// Wave lane masks as per-lane predicates: the SGPR mask is the VCC operand
+// of the consuming instruction (no VALU).
+__device__ __forceinline__ bool lane_in(uint64_t m) { return __builtin_amdgcn_inverse_ballot_w64(m); }
+
+// One probe of up to J tokens per lane, the pending ones masked by pm[j]
+// (wave lane masks): CAS on the slot (a lane with nothing to probe aims at a
+// selector-table entry, never 0, so its compare-with-0 never writes), count
+// the hits, retire them from pm, advance the others one slot.  Returns the
+// tokens still pending.
+template <int J, bool FOLD>
+__device__ __forceinline__ uint32_t probe_round(WaveSmem &sm, uint32_t lane, const uint64_t *tk, uint32_t *slot,
+                                                uint64_t *pm, uint32_t &claims) {
+  unsigned long long *idle = reinterpret_cast<unsigned long long *>(&sm.sel[lane & 31]);
+  uint32_t *idle32 = reinterpret_cast<uint32_t *>(idle);
+  uint64_t old[J];
+#pragma unroll
+  for (int j = 0; j < J; j++)
+    old[j] = atomicCAS(lane_in(pm[j]) ? reinterpret_cast<unsigned long long *>(&sm.key[slot[j]]) : idle, 0ull,
+                       (unsigned long long)tk[j]);
+  __builtin_amdgcn_sched_barrier(0);     // every CAS issued before the first result is waited on
+  uint32_t P = 0;
+#pragma unroll
+  for (int j = 0; j < J; j++) {
+    const uint64_t zm = __ballot(old[j] == 0) & pm[j];
+    uint64_t hm = (__ballot(old[j] == tk[j]) & pm[j]) | zm;
+    if (FOLD) {   // same length and folded hash, other position: compare the bytes
+      const uint64_t fm = __ballot((((old[j] & tk[j]) >> 63) != 0) & (((old[j] ^ tk[j]) & ~kFoldPosMask) == 0)) &
+                          pm[j] & ~hm;
+      if (fm) {
+        bool same = false;
+        if (lane_in(fm))
+          same = span_same(sm.text, (uint32_t)(old[j] >> 13) & 0x1FFFu, (uint32_t)(tk[j] >> 13) & 0x1FFFu,
+                           (uint32_t)tk[j] & 0xFFu);
+        hm |= __ballot(same) & fm;
+      }
+    }
+    const bool hit = lane_in(hm);
+    atomicAdd(hit ? &sm.cnt[slot[j] >> 1] : idle32, hit ? 1u << (16 * (slot[j] & 1)) : 0u);
+    claims += (uint32_t)__popcll(zm);
+    pm[j] &= ~hm;
+    slot[j] = (slot[j] + (lane_in(pm[j]) ? 1u : 0u)) & (kWaveSlots - 1);
+    P += (uint32_t)__popcll(pm[j]);
+  }
+  return P;
 }
 
 // One batch of 64 K tokens [tb, tb + 64 K) of the list (entries past ntok
@@ -751,7 +788,6 @@ template <int K, bool FOLD, bool PACK>
 __device__ __forceinline__ void hist2(WaveSmem &sm, uint32_t lane, uint32_t tb, uint32_t ntok, bool under, bool upper,
                                       uint32_t &claims, uint32_t &toks, bool &overflow) {
   const uint32_t *tw = reinterpret_cast<const uint32_t *>(sm.text);
-  const uint2 *sel = sm.sel;
   const uint32_t left = ntok - tb;                       // wave-uniform
   uint32_t ent[K], dw[K][3];
   uint2 sl[K];
@@ -762,11 +798,10 @@ __device__ __forceinline__ void hist2(WaveSmem &sm, uint32_t lane, uint32_t tb, 
     const uint32_t tp = ent[k] & kSpanMask, n = ((ent[k] >> 16) & kSpanMask) - tp;
     const uint32_t a0 = tp >> 2;
     dw[k][0] = tw[a0]; dw[k][1] = tw[a0 + 1]; dw[k][2] = tw[a0 + 2];
-    sl[k] = sel[(min(n, 8u) << 2) | (tp & 3u)];
+    sl[k] = sm.sel[(min(n, 8u) << 2) | (tp & 3u)];
   }
-  uint64_t tkey[K];
+  uint64_t tkey[K], pm[K];
   uint32_t slot[K];
-  bool pend[K], lng[K];
   uint32_t t0[K], t1[K];
 #pragma unroll
   for (int k = 0; k < K; k++) {
@@ -777,6 +812,7 @@ __device__ __forceinline__ void hist2(WaveSmem &sm, uint32_t lane, uint32_t tb, 
 #pragma unroll
     for (int k = 0; k < K; k++) { t0[k] = lower4(t0[k]); t1[k] = lower4(t1[k]); }
   }
+  uint64_t lm = 0;                                       // FOLD: lanes with a token of 9+ bytes, per k (bit k)
 #pragma unroll
   for (int k = 0; k < K; k++) {
     const uint32_t tp = ent[k] & kSpanMask, n = ((ent[k] >> 16) & kSpanMask) - tp;
@@ -788,79 +824,43 @@ __device__ __forceinline__ void hist2(WaveSmem &sm, uint32_t lane, uint32_t tb, 
     const uint32_t l0 = t0[k] | (PACK ? pack_tag(span_doc(ent[k])) : 0u);
     tkey[k] = (uint64_t)l0 | ((uint64_t)t1[k] << 32);
     slot[k] = table_slot(l0, t1[k]);
-    pend[k] = in & (n <= 8) & valid;
-    lng[k] = FOLD && (in & (n > 8));
+    pm[k] = __ballot(in & (n <= 8) & valid);
+    if (FOLD) lm |= (uint64_t)(__ballot(in & (n > 8)) != 0) << k;
   }
-  if (FOLD) {                                            // tokens of 9..255 bytes: folded keys
-    bool anyl = false;
+  if (FOLD && lm) {                                      // tokens of 9..255 bytes: folded keys
+    bool toolong = false;
 #pragma unroll
-    for (int k = 0; k < K; k++) anyl |= lng[k];
-    if (__any(anyl)) {
-      bool toolong = false;
-#pragma unroll
-      for (int k = 0; k < K; k++) {
-        if (lng[k]) {
-          const uint32_t e = ent[k];
-          const uint32_t tp = e & kSpanMask, n = ((e >> 16) & kSpanMask) - tp;
+    for (int k = 0; k < K; k++) {
+      if ((lm >> k) & 1u) {
+        const uint32_t e = ent[k];
+        const uint32_t tp = e & kSpanMask, n = ((e >> 16) & kSpanMask) - tp;
+        bool ok = false;
+        if (lane + 64u * k < left && n > 8) {
           if (n > kMaxTokenLen) {
             toolong = true;
           } else {
             uint32_t h;
-            bool valid;
-            tkey[k] = fold_key(sm.text, tp, n, &h, &valid);
+            tkey[k] = fold_key(sm.text, tp, n, &h, &ok);
             if (PACK) {
               tkey[k] |= (uint64_t)span_doc(e) << 8;
               h ^= span_doc(e) * 0x9E3779B1u;
             }
             slot[k] = h >> (32 - kWaveSlotBits);
-            pend[k] = valid;
           }
         }
+        pm[k] |= __ballot(ok);
       }
-      if (__any(toolong)) { overflow = true; return; }     // > 255 chars: the long path cuts it
     }
+    if (__any(toolong)) { overflow = true; return; }     // > 255 chars: the long path cuts it
   }
   uint32_t P = 0;
 #pragma unroll
-  for (int k = 0; k < K; k++) P += (uint32_t)__popcll(__ballot(pend[k]));
+  for (int k = 0; k < K; k++) P += (uint32_t)__popcll(pm[k]);
   toks += P;
-  // round 1: every token's home slot, all CASes in flight
-  uint64_t old[K];
-#pragma unroll
-  for (int k = 0; k < K; k++) {
-    old[k] = 0;
-    if (pend[k]) old[k] = atomicCAS(reinterpret_cast<unsigned long long *>(&sm.key[slot[k]]), 0ull,
-                                    (unsigned long long)tkey[k]);
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  P = 0;
-#pragma unroll
-  for (int k = 0; k < K; k++) {
-    const bool hit = pend[k] && entry_hit<FOLD>(sm, old[k], tkey[k]);
-    if (hit) count_add(sm, slot[k]);
-    claims += (uint32_t)__popcll(__ballot(hit & (old[k] == 0)));
-    pend[k] = pend[k] & !hit;
-    if (pend[k]) slot[k] = (slot[k] + 1) & (kWaveSlots - 1);
-    P += (uint32_t)__popcll(__ballot(pend[k]));
-  }
-  // further rounds over every pending token while many remain
-  for (uint32_t round = 1; P > kWaveQueue; round++) {
+  // probe rounds over every token while many remain (the first resolves ~90 %)
+  for (uint32_t round = 0; P > kWaveQueue; round++) {
     if (round >= kWaveSlots) { overflow = true; return; }
-#pragma unroll
-    for (int k = 0; k < K; k++)
-      if (pend[k]) old[k] = atomicCAS(reinterpret_cast<unsigned long long *>(&sm.key[slot[k]]), 0ull,
-                                      (unsigned long long)tkey[k]);
-    __builtin_amdgcn_sched_barrier(0);
-    P = 0;
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-      const bool hit = pend[k] && entry_hit<FOLD>(sm, old[k], tkey[k]);
-      if (hit) count_add(sm, slot[k]);
-      claims += (uint32_t)__popcll(__ballot(hit & (old[k] == 0)));
-      pend[k] = pend[k] & !hit;
-      if (pend[k]) slot[k] = (slot[k] + 1) & (kWaveSlots - 1);
-      P += (uint32_t)__popcll(__ballot(pend[k]));
-    }
+    P = probe_round<K, FOLD>(sm, lane, tkey, slot, pm, claims);
   }
   if (P == 0) return;
   // the rest (<= 128): compacted into a queue, one or two per lane, probed to the end
@@ -868,49 +868,32 @@ __device__ __forceinline__ void hist2(WaveSmem &sm, uint32_t lane, uint32_t tb, 
     uint32_t at = 0;
 #pragma unroll
     for (int k = 0; k < K; k++) {
-      const uint64_t m = __ballot(pend[k]);
-      if (m) {
-        if (pend[k]) {
-          const uint32_t q = at + lanes_below(m);
+      if (pm[k]) {
+        if (lane_in(pm[k])) {
+          const uint32_t q = at + lanes_below(pm[k]);
           sm.qkey[q] = tkey[k];
           sm.qslot[q] = (uint16_t)slot[k];
         }
-        at += (uint32_t)__popcll(m);
+        at += (uint32_t)__popcll(pm[k]);
       }
     }
   }
   asm volatile("" ::: "memory");
   uint64_t qk[2];
   uint32_t qs[2];
-  bool qp[2];
+  uint64_t qm[2];
 #pragma unroll
   for (int i = 0; i < 2; i++) {
-    qp[i] = lane + 64u * i < P;
-    qk[i] = qp[i] ? sm.qkey[lane + 64 * i] : 0ull;
-    qs[i] = qp[i] ? sm.qslot[lane + 64 * i] : 0u;
+    const bool qp = lane + 64u * i < P;
+    qk[i] = qp ? sm.qkey[lane + 64 * i] : 0ull;
+    qs[i] = qp ? sm.qslot[lane + 64 * i] : 0u;
+    qm[i] = __ballot(qp);
   }
-  const int nq = P > 64 ? 2 : 1;
   for (uint32_t it = 0;; it++) {
     if (it >= kWaveSlots) { overflow = true; return; }
-    uint64_t qo[2] = {0, 0};
-#pragma unroll
-    for (int i = 0; i < 2; i++)
-      if (i < nq && qp[i]) qo[i] = atomicCAS(reinterpret_cast<unsigned long long *>(&sm.key[qs[i]]), 0ull,
-                                             (unsigned long long)qk[i]);
-    __builtin_amdgcn_sched_barrier(0);
-    bool more = false;
-#pragma unroll
-    for (int i = 0; i < 2; i++) {
-      if (i < nq) {
-        const bool hit = qp[i] && entry_hit<FOLD>(sm, qo[i], qk[i]);
-        if (hit) count_add(sm, qs[i]);
-        claims += (uint32_t)__popcll(__ballot(hit & (qo[i] == 0)));
-        qp[i] = qp[i] & !hit;
-        if (qp[i]) qs[i] = (qs[i] + 1) & (kWaveSlots - 1);
-        more |= qp[i];
-      }
-    }
-    if (!__any(more)) break;
+    const uint32_t left_q = P > 64 ? probe_round<2, FOLD>(sm, lane, qk, qs, qm, claims)
+                                   : probe_round<1, FOLD>(sm, lane, qk, qs, qm, claims);
+    if (left_q == 0) return;
   }
 }
 
@@ -965,7 +948,7 @@ __device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p
         const uint64_t key = sm.key[slots[lane + 64 * k]];
         const uint32_t n = (uint32_t)key & 0xFFu, tp = (uint32_t)(key >> 13) & 0x1FFFu;
         bool valid;
-        token_key(sm.text, tp, tp + n, &flo, &fhi, &valid, p.hash_seed);
+        token_key(sm.text, tp, tp + n, &flo, &fhi, &valid, TFIDF_COLD(hash_seed));
         mine = dict_ref_word(wbase + tp, n);
       }
       bool cl;
@@ -1070,7 +1053,7 @@ __device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p
       caperr |= e;
       if (e) g[k] = 0;
     }
-    if (caperr) set_err(p.err, kErrCapacity, doc);
+    if (caperr) set_err(TFIDF_COLD(err), kErrCapacity, doc);
   }
 }
 
@@ -1087,7 +1070,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   init_sel_table(sm.sel, lane);
   unsigned long long my_doc_count = 0, my_ttf = 0, my_nnz = 0;
   uint4 v[4] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
-  const uint64_t n_units = PACK ? (p.n_docs + p.pack - 1) / p.pack : (p.doc_list ? *p.doc_list_count : p.n_docs);
+  const uint64_t n_units = PACK ? (p.n_docs + p.pack - 1) / p.pack : (TFIDF_COLD(doc_list) ? *TFIDF_COLD(doc_list_count) : p.n_docs);
   DocMeta meta;
   if (blockIdx.x < n_units) {
     meta = unit_meta<PACK>(p, blockIdx.x, lane);
@@ -1108,7 +1091,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     const uint64_t un = u + gridDim.x;
     if (!fits) {
       if (PACK) defer_pack(p, d, np, lane);
-      else if (lane == 0) p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
+      else if (lane == 0) TFIDF_COLD(long_list)[atomicAdd(TFIDF_COLD(long_count), 1u)] = (uint32_t)d;
       if (un < n_units) { meta = unit_meta<PACK>(p, un, lane); prefetch_wave(p, meta, lane, v); }
       continue;                                             // wave-uniform
     }
@@ -1163,7 +1146,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     }
     if (bad) {                                              // non-ASCII: the Unicode wave path
       if (PACK) defer_pack(p, d, np, lane);
-      else if (lane == 0) p.uni_list[atomicAdd(p.uni_count, 1u)] = (uint32_t)d;
+      else if (lane == 0) TFIDF_COLD(uni_list)[atomicAdd(TFIDF_COLD(uni_count), 1u)] = (uint32_t)d;
       continue;
     }
     const uint64_t wlast = __ballot((W >> 63) & 1ull);
@@ -1186,7 +1169,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     const uint32_t ntok = (uint32_t)__builtin_amdgcn_readlane((int)tincl, 63);
     if (ntok > kWaveTokens) {                               // wave-uniform
       if (PACK) defer_pack(p, d, np, lane);
-      else if (lane == 0) p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
+      else if (lane == 0) TFIDF_COLD(long_list)[atomicAdd(TFIDF_COLD(long_count), 1u)] = (uint32_t)d;
       continue;
     }
     bool longtok = false;
@@ -1227,13 +1210,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     for (uint32_t tb = 0; tb < ntok && !overflow;) {       // batch width by what is left
       const uint32_t rem = ntok - tb;
       if (anylong) {
-        if (!PACK && rem > 512 && rem <= 640) { hist2<10, true, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 640; }
+        if (TFIDF_HIST10 && !PACK && rem > 512 && rem <= 640) { hist2<10, true, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 640; }
         else if (rem > 256) { hist2<8, true, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 512; }
         else if (rem > 128) { hist2<4, true, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 256; }
         else { hist2<2, true, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 128; }
       } else {
         // 513..640 tokens (U[400, 600]-token documents: ~40 % of cfg 2) in one batch
-        if (!PACK && rem > 512 && rem <= 640) { hist2<10, false, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 640; }
+        if (TFIDF_HIST10 && !PACK && rem > 512 && rem <= 640) { hist2<10, false, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 640; }
         else if (rem > 256) { hist2<8, false, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 512; }
         else if (rem > 128) { hist2<4, false, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 256; }
         else { hist2<2, false, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 128; }
@@ -1242,7 +1225,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     if (overflow || nu > kWaveTerms) {                      // wave-uniform: long path
       clear_table(sm, lane);
       if (PACK) defer_pack(p, d, np, lane);
-      else if (lane == 0) p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
+      else if (lane == 0) TFIDF_COLD(long_list)[atomicAdd(TFIDF_COLD(long_count), 1u)] = (uint32_t)d;
       continue;
     }
     if (p.debug_stop == 3) { clear_table(sm, lane); continue; }
@@ -1367,9 +1350,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     }
   }
   if (my_ttf | my_nnz | my_doc_count) {                    // lane 0 (PACK: lanes < pack)
-    atomicAdd(&p.stats[0], my_doc_count);
-    atomicAdd(&p.stats[1], my_ttf);
-    atomicAdd(&p.stats[2], my_nnz);
+    atomicAdd(&TFIDF_COLD(stats)[0], my_doc_count);
+    atomicAdd(&TFIDF_COLD(stats)[1], my_ttf);
+    atomicAdd(&TFIDF_COLD(stats)[2], my_nnz);
   }
 }
 

@@ -114,6 +114,20 @@ __host__ __device__ inline uint32_t csr_esc_tf(const uint64_t *esc, uint64_t n, 
 #endif
 namespace tfidf {
 #if defined(__HIPCC__)
+// Cold parameters of the BuildParams kernels (every one takes the block as its
+// only argument, so it sits at offset 0 of the kernarg segment): read at the
+// point of use.  The asm makes the pointer opaque, so the scalar load is not
+// hoisted out of the document loop and its value not kept live in SGPRs (the
+// wave tokenizer used to spill ~100 of them to VGPR lanes and restore them
+// with v_readlane in its hot loops).
+typedef const BuildParams __attribute__((address_space(4))) KBuildParams;
+__device__ __forceinline__ KBuildParams *cold_args() {
+  KBuildParams *q = (KBuildParams *)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(q));
+  return q;
+}
+#define TFIDF_COLD(f) (cold_args()->f)
+
 __device__ inline void set_build_err(uint32_t *err, uint32_t flag, uint32_t doc) {
   const uint32_t old = atomicOr(err, flag);
   if (old == 0) atomicExch(err + 1, doc);
@@ -128,17 +142,18 @@ __device__ inline void dict_verify(const BuildParams &p, uint32_t slot, uint64_t
                                        __HIP_MEMORY_SCOPE_AGENT);
   if (r == mine) return;
   if (r == 0) {
-    const uint32_t at = atomicAdd(p.verify_count, 1u);
-    if (at < p.verify_cap) {
-      p.verify_defer[2 * (size_t)at] = slot;
-      p.verify_defer[2 * (size_t)at + 1] = mine;
+    const uint32_t at = atomicAdd(TFIDF_COLD(verify_count), 1u);
+    if (at < TFIDF_COLD(verify_cap)) {
+      uint64_t *vd = TFIDF_COLD(verify_defer);
+      vd[2 * (size_t)at] = slot;
+      vd[2 * (size_t)at + 1] = mine;
     } else {
-      set_build_err(p.err, kErrCollision, doc);        // cannot defer: treated as a collision (rebuild)
+      set_build_err(TFIDF_COLD(err), kErrCollision, doc);   // cannot defer: treated as a collision (rebuild)
     }
     return;
   }
   if (!uc_same_term(p.text + dict_ref_off(r), dict_ref_len(r), p.text + dict_ref_off(mine), dict_ref_len(mine)))
-    set_build_err(p.err, kErrCollision, doc);
+    set_build_err(TFIDF_COLD(err), kErrCollision, doc);
 }
 
 // write CSR entry idx of document doc (dictionary slot, tf)
@@ -147,9 +162,9 @@ __device__ inline void csr_put(const BuildParams &p, uint64_t idx, uint32_t slot
   uint32_t f = tf;
   if (tf >= esc) {
     f = esc;
-    if (tf > kMaxTf) set_build_err(p.err, kErrTfTooLarge, doc);
-    const uint32_t at = atomicAdd(p.esc_count, 1u);
-    if (at < p.esc_cap) p.csr_esc[at] = (idx << 24) | (tf > kMaxTf ? kMaxTf : tf);
+    if (tf > kMaxTf) set_build_err(TFIDF_COLD(err), kErrTfTooLarge, doc);
+    const uint32_t at = atomicAdd(TFIDF_COLD(esc_count), 1u);
+    if (at < TFIDF_COLD(esc_cap)) TFIDF_COLD(csr_esc)[at] = (idx << 24) | (tf > kMaxTf ? kMaxTf : tf);
   }
   __builtin_nontemporal_store(csr_local(slot, p.range_shift) | (f << p.range_shift), p.csr + idx);   // read by the next kernel
 }

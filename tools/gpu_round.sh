@@ -1,15 +1,11 @@
 #!/bin/bash
-# Round-end rehearsal on the GPU box: whole GPU suite, smoke, default bench,
-# then the round profile (kernel trace of the bench command + HBM traffic
-# passes).  Every GPU step bounded; stop at the first failure.
+# One GPU call: parity tests (TESTS, default all), variant A/B bench, per-phase counters (PHASES=1)
 set -o pipefail
-mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
-rc=$?; tail -4 gpurun_out/gpu_tests.log; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
-rc=$?; tail -2 gpurun_out/smoke.log; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 400 python -u bench.py > gpurun_out/bench.log 2> gpurun_out/bench.err
-rc=$?; [ $rc -ne 0 ] && { tail -20 gpurun_out/bench.err; exit $rc; }
-tail -1 gpurun_out/bench.log
-[ -n "${NO_PROF:-}" ] && exit 0
-TAG=${TAG:-r01} SQ=${SQ:-} bash tools/prof_round.sh
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; mkdir -p gpurun_out
+if [ "${TESTS:-tests}" != none ]; then
+  timeout -k 10 600 python -u -m pytest -x -q -m gpu --timeout 300 --timeout-method thread ${TESTS:-tests} > gpurun_out/rt_tests.log 2>&1
+  rc=$?; tail -3 gpurun_out/rt_tests.log; [ $rc -ne 0 ] && { grep -E "Error|error|assert" gpurun_out/rt_tests.log | head -30; exit $rc; }
+fi
+bash tools/variant_bench.sh || exit $?
+[ -n "$PHASES" ] && { bash tools/gpu_phases_ab.sh || exit $?; }
+exit 0
