@@ -108,6 +108,7 @@ typedef struct tfidf_index_stats {
   uint64_t coalesced_queries;
   uint64_t unit_batches;   /* batched top-k searches scored by query units (k_score_units) / units run */
   uint64_t unit_count;
+  uint64_t fused_queries;  /* tfidf_search top-k calls served by the one-launch fused path (index lifetime) */
 } tfidf_index_stats;
 
 /* Per-phase device times of the last commit, measured with HIP events on the

@@ -1,0 +1,73 @@
+"""The one-launch single-query path of tfidf_search (top-k): the query's terms
+ride in the kernel arguments, every block workgroup scores its block
+(k_score_blocks) and writes its top-k candidates to pinned host memory, and
+the host merges them — no upload, no download, no merge kernel
+(Worker.searchIndex, Worker.java:222-241).  Against the C oracle and against
+the unfused path (TFIDF_NO_FUSED) on the same index; bar: doc ids and float32
+score bits identical.
+"""
+import pytest
+
+from tfidf_amd import synth
+from test_gpu_parity import assert_hits_equal, build_pair
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def corpus():
+    # 5 doc blocks (8192 docs each) with a cross-block tie storm: many documents
+    # share one score, so the merge's (score desc, doc asc) order is exercised
+    texts = synth.corpus(36000, V=6000, len_min=8, len_max=60)
+    for i in range(0, 36000, 97):
+        texts[i] = b"tiedterm filler"
+    g, o = build_pair(texts)
+    yield g, o
+    g.close()
+    o.close()
+
+
+QUERIES = synth.queries(30, lo=1, hi=3000) + [b"tiedterm", b"tiedterm filler aaaa", b"zzzzzz", b"aaaa"]
+OPS = [b"aaaa AND aaab", b"tiedterm NOT aaab", b"aaab OR aaac NOT aaaa", b"aaaa AND NOT"]
+
+
+@pytest.mark.parametrize("k", [1, 10, 64, 300])
+def test_fused_equals_oracle(corpus, k):
+    g, o = corpus
+    f0 = g.stats()["fused_queries"]
+    n = 0
+    for q in QUERIES:
+        assert_hits_equal(g.search(q, k), o.search(q, k))
+        n += 1
+    assert g.stats()["fused_queries"] - f0 >= n - 2          # queries without a present term do not launch
+
+
+def test_fused_operator_queries(corpus):
+    g, o = corpus
+    from oracle import oracle as O
+    for q in OPS:
+        for k in (3, 10):
+            try:
+                want = o.search(q, k)
+            except O.QuerySyntaxError:
+                continue
+            assert_hits_equal(g.search(q, k), want)
+
+
+def test_fused_equals_unfused(corpus, monkeypatch):
+    g, _ = corpus
+    got = [g.search(q, 10) for q in QUERIES + OPS[:3]]
+    monkeypatch.setenv("TFIDF_NO_FUSED", "1")
+    f0 = g.stats()["fused_queries"]
+    ref = [g.search(q, 10) for q in QUERIES + OPS[:3]]
+    assert g.stats()["fused_queries"] == f0
+    assert got == ref
+
+
+def test_fused_back_to_back_counter_reset(corpus):
+    """The merge counter is reset by the merger: many consecutive launches on
+    one stream stay correct (a stale counter would merge too early)."""
+    g, o = corpus
+    want = o.search(QUERIES[0], 10)
+    for _ in range(50):
+        assert_hits_equal(g.search(QUERIES[0], 10), want)

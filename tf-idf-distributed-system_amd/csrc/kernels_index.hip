@@ -1924,7 +1924,7 @@ __global__ void __launch_bounds__(256) k_df_sum(PostingParams p) {
 }
 
 // per block row: exclusive scan over slots in place (one workgroup per row);
-// the row total goes to bbase[b + 1] (turned into bases by k_block_base).
+// the row total goes to bbase[b + 1] (turned into bases by k_block_scan).
 // Tiles of 16384 slots: each thread loads 16 consecutive counts with four
 // 16 B loads (coalesced across the workgroup), scans them in registers, and a
 // workgroup scan of the 1024 thread totals gives the offsets.
@@ -1985,17 +1985,6 @@ __global__ void __launch_bounds__(1024) k_row_scan(PostingParams p) {
     __syncthreads();
   }
   if (tid == 0) p.bbase[blockIdx.x + 1] = carry_sh;
-}
-
-// bbase[b + 1] holds block b's total: exclusive scan over blocks (tiny).
-__global__ void k_block_base(PostingParams p) {
-  if (threadIdx.x != 0) return;
-  uint64_t run = 0;
-  p.bbase[0] = 0;
-  for (uint32_t b = 0; b < p.n_blocks; b++) {
-    run += p.bbase[b + 1];
-    p.bbase[b + 1] = run;
-  }
 }
 
 // Inversion in two passes so that every store stream stays L2-resident.
@@ -2214,6 +2203,37 @@ __global__ void __launch_bounds__(1024) k_scatter_sort(PostingParams p) {
   }
 }
 
+// block totals in bbase[b + 1] -> block bases, in place (one workgroup; every
+// total of a round is read before the barrier, written after it)
+__global__ void __launch_bounds__(1024) k_block_scan(PostingParams p) {
+  __shared__ uint64_t wsum[16];
+  const uint32_t B = p.n_blocks;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  uint64_t carry = 0;
+  for (uint32_t i0 = 0; i0 < B; i0 += 1024) {
+    const uint32_t i = i0 + tid;
+    const uint64_t v = i < B ? p.bbase[i + 1] : 0ull;
+    uint64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(x, o, 64);
+      if (lane >= (uint32_t)o) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    uint64_t base = carry, all = 0;
+    for (uint32_t w = 0; w < 16; w++) {
+      const uint64_t s = wsum[w];
+      if (w < wid) base += s;
+      all += s;
+    }
+    __syncthreads();
+    if (i < B) p.bbase[i + 1] = base + x;            // inclusive = the next block's base
+    carry += all;
+  }
+  if (tid == 0) p.bbase[0] = 0;
+}
+
 // Hashed-key checks deferred by dict_verify (the slot's reference occurrence
 // was not visible yet): every reference is final after the tokenizers.
 __global__ void __launch_bounds__(256) k_verify_deferred(BuildParams p) {
@@ -2297,7 +2317,7 @@ hipError_t launch_count_nonzero(const uint64_t *a, uint32_t n, unsigned long lon
   return hipGetLastError();
 }
 hipError_t launch_block_base(const PostingParams &p, hipStream_t s) {
-  hipLaunchKernelGGL(k_block_base, dim3(1), dim3(64), 0, s, p);
+  hipLaunchKernelGGL(k_block_scan, dim3(1), dim3(1024), 0, s, p);   // (serial k_block_base: 15 us at 123 blocks)
   return hipGetLastError();
 }
 hipError_t launch_scatter(const PostingParams &p, hipStream_t s) {

@@ -93,6 +93,24 @@ __device__ __forceinline__ uint32_t wave_select_bin(const uint32_t *hist, uint32
   return 255u - (4u * src + fi);
 }
 
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
+  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+// bitonic stages over the 64 lanes for sequences of `size` (descending overall)
+__device__ __forceinline__ uint64_t bitonic_stages(uint64_t v, uint32_t lane, uint32_t size) {
+  for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+    const uint64_t o = shfl_xor64(v, (int)stride);
+    const bool desc = (lane & size) == 0, lower = (lane & stride) == 0;
+    v = (lower == desc) ? max(v, o) : min(v, o);
+  }
+  return v;
+}
+
 // Wave-cooperative lower bound over one term's doc-ascending postings
 // (term-major layout): first i in [lo, hi) with doc(post[i]) >= x.  Each step
 // samples 64 evenly spaced postings, so a list of df entries takes
@@ -151,6 +169,85 @@ __device__ __forceinline__ void post_decode(const QueryParams &p, PostW<kTerm> e
 
 constexpr uint32_t kQTermsFast = 4;   // query terms whose ranges / first chunk are prefetched
 
+constexpr int kMergeWaveRegs = 32;
+constexpr uint32_t kMergeWavesPerWG = 4;
+
+// One query's merge of its per-block candidate lists by one wave (see
+// k_merge_topk_wave); hist: the wave's 256-word LDS histogram, zero on entry.
+__device__ __forceinline__ void merge_query_wave(const QueryParams &p, uint32_t q, uint32_t *hist) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t k = p.k, nb = p.n_blocks, nflat = nb * k;
+  const uint64_t *cand = p.cand + (size_t)q * nflat;
+  const uint32_t *cn = p.cand_n + (size_t)q * nb;
+  const uint32_t inv = (uint32_t)((0xFFFFFFFFull + k) / k);   // f / k = umulhi(f, inv) (f < 2^11, 2 <= k <= 64)
+  uint64_t kv[kMergeWaveRegs];
+  uint64_t lmin = ~0ull, lmax = 0;
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int r = 0; r < kMergeWaveRegs; r++) {
+    const uint32_t f = lane + 64u * r;
+    kv[r] = 0;
+    if (f < nflat) {
+      const uint32_t b = k == 1 ? f : __umulhi(f, inv);
+      if (f - b * k < cn[b]) kv[r] = cand[f];
+    }
+    if (kv[r]) { lmin = min(lmin, kv[r]); lmax = max(lmax, kv[r]); cnt++; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    cnt += (uint32_t)__shfl_xor((int)cnt, o, 64);
+    lmin = min(lmin, (uint64_t)__shfl_xor((long long)lmin, o, 64));
+    lmax = max(lmax, (uint64_t)__shfl_xor((long long)lmax, o, 64));
+  }
+  const uint32_t M = cnt, kk = M < k ? M : k;
+  uint64_t T = 1, tmask = ~0ull;                            // take (key & tmask) >= T (keys > 0)
+  if (M > k) {
+    int rb = 64 - __builtin_clzll(lmin ^ lmax);
+    uint64_t prefix = rb < 64 ? lmax & (~0ull << rb) : 0ull;
+    uint32_t rem = k;
+    while (rb > 0) {
+      const int wd = rb < 8 ? rb : 8, sh = rb - wd;
+      const uint64_t hmask = rb < 64 ? (~0ull << rb) : 0ull;
+      const uint32_t dmask = (1u << wd) - 1;
+#pragma unroll
+      for (int r = 0; r < kMergeWaveRegs; r++)
+        if (kv[r] && (kv[r] & hmask) == prefix) atomicAdd(&hist[(uint32_t)(kv[r] >> sh) & dmask], 1u);
+      uint32_t above;
+      const uint32_t bin = wave_select_bin(hist, rem, &above);
+      const uint32_t inbin = hist[bin];
+#pragma unroll
+      for (int i = 0; i < 4; i++) hist[lane + 64 * i] = 0;
+      prefix |= (uint64_t)bin << sh;
+      rem -= above;
+      rb = sh;
+      if (inbin == rem) break;
+    }
+    tmask = ~0ull << rb;
+    T = prefix;
+  }
+  // gather the kk winners one per lane (lane order = flat order), sort descending
+  uint64_t mine = 0;
+  uint32_t base = 0;
+#pragma unroll
+  for (int r = 0; r < kMergeWaveRegs; r++) {
+    const bool take = kv[r] && (kv[r] & tmask) >= T;
+    const uint64_t m = __ballot(take);
+    const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
+    // lane `pos` receives this key: scatter through the LDS histogram space
+    if (take) reinterpret_cast<uint64_t *>(hist)[pos & 127] = kv[r];
+    base += (uint32_t)__popcll(m);
+  }
+  __builtin_amdgcn_wave_barrier();
+  if (lane < kk) mine = reinterpret_cast<uint64_t *>(hist)[lane];
+#pragma unroll
+  for (uint32_t size = 2; size <= 64; size <<= 1) mine = bitonic_stages(mine, lane, size);
+  if (lane < kk) {
+    p.out_doc[(size_t)q * k + lane] = ~(uint32_t)(mine & 0xFFFFFFFFu);
+    p.out_score[(size_t)q * k + lane] = __uint_as_float((uint32_t)(mine >> 32));
+  }
+  if (lane == 0) p.out_n[q] = kk;
+}
+
 // kOps: queries with MUST / MUST_NOT clauses (QueryParser operator words,
 // analysis.h).  Per document: acc = the current MUST clause's double sum, then
 // the SHOULD double sum; req = double sum of the MUST clauses' float scores;
@@ -187,6 +284,16 @@ template <bool kOps> struct ScoreSmem {
 // kAll: all-hits mode (k == 0) as its own instantiation — its LDS sort code
 // made the compiler schedule the top-k instantiation's loops worse (10 k-query
 // batch: 12.4 -> 16.0 ms when they shared one kernel).
+// Query arrays: device memory, or (single fused queries, inl_n > 0) the
+// kernel arguments themselves (no upload before the launch).
+__device__ __forceinline__ uint32_t q_off_of(const QueryParams &p, uint32_t q) {
+  return p.inl_n ? (q ? p.inl_n : 0u) : p.q_off[q];
+}
+__device__ __forceinline__ uint32_t q_slot_of(const QueryParams &p, uint32_t j) { return p.inl_n ? p.inl_slot[j] : p.q_slot[j]; }
+__device__ __forceinline__ float q_w_of(const QueryParams &p, uint32_t j) { return p.inl_n ? p.inl_w[j] : p.q_w[j]; }
+__device__ __forceinline__ uint32_t q_role_of(const QueryParams &p, uint32_t j) { return p.inl_n ? p.inl_role[j] : p.q_role[j]; }
+__device__ __forceinline__ uint32_t q_meta_of(const QueryParams &p, uint32_t q) { return p.inl_n ? p.inl_meta : p.q_meta[q]; }
+
 template <bool kOps, bool kAll, bool kTerm>
 __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
   __shared__ ScoreSmem<kOps> sm;
@@ -222,22 +329,22 @@ __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
     for (uint32_t i = tid; i < 256; i += blockDim.x) sm.hist[i] = 0;
     if (tid == 0) { sm.nhit = 0; sm.outn = 0; sm.smin = 0xFFFFFFFFu; sm.smax = 0; }
     __syncthreads();
-    const uint32_t t0 = p.q_off[q], t1 = p.q_off[q + 1];
-    const uint32_t ngroups = kOps ? (p.q_meta[q] & 0xFFFFu) : 0u;
+    const uint32_t t0 = q_off_of(p, q), t1 = q_off_of(p, q + 1);
+    const uint32_t ngroups = kOps ? (q_meta_of(p, q) & 0xFFFFu) : 0u;
     bool alive = true;                                     // kOps: a document still meets every MUST clause
     if (p.toff) {
       // term-major layout: wave j finds term j's segment for this block in the
       // term's doc-sorted list (two 64-ary searches)
       const uint32_t wv = tid >> 6;
       if (wv < t1 - t0 && wv < kQTermsFast) {
-        const uint32_t slot = p.q_slot[t0 + wv];
+        const uint32_t slot = q_slot_of(p, t0 + wv);
         uint64_t a = 0, z = 0;
         if (slot != kInvalidSlot) term_block_range(p, slot, (uint32_t)d0, &a, &z);
-        if ((tid & 63) == 0) { sm.tlo[wv] = a; sm.thi[wv] = z; sm.tw[wv] = p.q_w[t0 + wv]; }
+        if ((tid & 63) == 0) { sm.tlo[wv] = a; sm.thi[wv] = z; sm.tw[wv] = q_w_of(p, t0 + wv); }
       }
     } else if (tid < t1 - t0 && tid < kQTermsFast) {
       // block-major layout: all terms' ranges in one round trip (thread j fetches term j)
-      const uint32_t slot = p.q_slot[t0 + tid];
+      const uint32_t slot = q_slot_of(p, t0 + tid);
       uint64_t a = 0, z = 0;
       if (slot != kInvalidSlot) {
         a = bb + row[slot];
@@ -245,7 +352,7 @@ __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
       }
       sm.tlo[tid] = a;
       sm.thi[tid] = z;
-      sm.tw[tid] = p.q_w[t0 + tid];
+      sm.tw[tid] = q_w_of(p, t0 + tid);
     }
     __syncthreads();
     // first chunk of every term's postings in flight before any is consumed
@@ -259,7 +366,7 @@ __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
     for (uint32_t j = t0; j < t1; j++) {
       if (kOps && !alive) break;                           // uniform: no document can match any more
       const uint32_t jj = j - t0;
-      const uint32_t role = kOps ? p.q_role[j] >> 24 : kRoleShould;
+      const uint32_t role = kOps ? q_role_of(p, j) >> 24 : kRoleShould;
       uint64_t lo, hi;
       float w;
       if (jj < kQTermsFast) {
@@ -267,8 +374,8 @@ __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
         hi = sm.thi[jj];
         w = sm.tw[jj];
       } else {
-        const uint32_t slot = p.q_slot[j];
-        w = p.q_w[j];
+        const uint32_t slot = q_slot_of(p, j);
+        w = q_w_of(p, j);
         if (slot == kInvalidSlot) {                        // uniform
           lo = hi = 0;
         } else if (p.toff) {
@@ -312,10 +419,10 @@ __global__ void __launch_bounds__(kScoreThreads) k_score_blocks(QueryParams p) {
         }
       }
       __syncthreads();                                     // term order = the disjunction's sum order
-      if (kOps && role == kRoleMust && (j + 1 == t1 || p.q_role[j + 1] != p.q_role[j])) {
+      if (kOps && role == kRoleMust && (j + 1 == t1 || q_role_of(p, j + 1) != q_role_of(p, j))) {
         // end of MUST clause g: fold its float score into req for the documents
         // that met every MUST clause so far (one 32-doc word per thread)
-        const uint32_t g = p.q_role[j] & 0xFFFFFFu;
+        const uint32_t g = q_role_of(p, j) & 0xFFFFFFu;
         uint32_t rb = 0;
         if (tid < kBlockDocs / 32) {
           const uint32_t gb = sm.grpbits[tid];
@@ -876,24 +983,6 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t l) {
 __device__ __forceinline__ uint64_t shfl_up64(uint64_t v) {
   const uint32_t lo = (uint32_t)__shfl_up((int)(uint32_t)v, 1, 64), hi = (uint32_t)__shfl_up((int)(uint32_t)(v >> 32), 1, 64);
   return ((uint64_t)hi << 32) | lo;
-}
-
-__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
-  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m, 64), hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m, 64);
-  return ((uint64_t)hi << 32) | lo;
-}
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src) {
-  const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src, 64), hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src, 64);
-  return ((uint64_t)hi << 32) | lo;
-}
-// bitonic stages over the 64 lanes for sequences of `size` (descending overall)
-__device__ __forceinline__ uint64_t bitonic_stages(uint64_t v, uint32_t lane, uint32_t size) {
-  for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-    const uint64_t o = shfl_xor64(v, (int)stride);
-    const bool desc = (lane & size) == 0, lower = (lane & stride) == 0;
-    v = (lower == desc) ? max(v, o) : min(v, o);
-  }
-  return v;
 }
 
 // Insert the candidate keys of the lanes in cm (all above theta when cm was
@@ -1471,8 +1560,6 @@ hipError_t launch_score_blocks(const QueryParams &p, hipStream_t s) {
 // query).  Keys are unique: radix select of the k-th largest from the first
 // differing bit (8-bit digits, wave histogram in LDS, wave_select_bin), then
 // the winners are gathered one per lane and bitonic-sorted (descending).
-constexpr int kMergeWaveRegs = 32;
-constexpr uint32_t kMergeWavesPerWG = 4;
 
 __global__ void __launch_bounds__(64 * kMergeWavesPerWG) k_merge_topk_wave(QueryParams p) {
   __shared__ uint32_t hist_all[kMergeWavesPerWG][256];
@@ -1481,76 +1568,7 @@ __global__ void __launch_bounds__(64 * kMergeWavesPerWG) k_merge_topk_wave(Query
   uint32_t *hist = hist_all[w];
   for (uint32_t i = lane; i < 256; i += 64) hist[i] = 0;
   if (q >= p.n_q) return;                                   // wave-uniform; the wave owns its histogram
-  const uint32_t k = p.k, nb = p.n_blocks, nflat = nb * k;
-  const uint64_t *cand = p.cand + (size_t)q * nflat;
-  const uint32_t *cn = p.cand_n + (size_t)q * nb;
-  const uint32_t inv = (uint32_t)((0xFFFFFFFFull + k) / k);   // f / k = umulhi(f, inv) (f < 2^11, 2 <= k <= 64)
-  uint64_t kv[kMergeWaveRegs];
-  uint64_t lmin = ~0ull, lmax = 0;
-  uint32_t cnt = 0;
-#pragma unroll
-  for (int r = 0; r < kMergeWaveRegs; r++) {
-    const uint32_t f = lane + 64u * r;
-    kv[r] = 0;
-    if (f < nflat) {
-      const uint32_t b = k == 1 ? f : __umulhi(f, inv);
-      if (f - b * k < cn[b]) kv[r] = cand[f];
-    }
-    if (kv[r]) { lmin = min(lmin, kv[r]); lmax = max(lmax, kv[r]); cnt++; }
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    cnt += (uint32_t)__shfl_xor((int)cnt, o, 64);
-    lmin = min(lmin, (uint64_t)__shfl_xor((long long)lmin, o, 64));
-    lmax = max(lmax, (uint64_t)__shfl_xor((long long)lmax, o, 64));
-  }
-  const uint32_t M = cnt, kk = M < k ? M : k;
-  uint64_t T = 1, tmask = ~0ull;                            // take (key & tmask) >= T (keys > 0)
-  if (M > k) {
-    int rb = 64 - __builtin_clzll(lmin ^ lmax);
-    uint64_t prefix = rb < 64 ? lmax & (~0ull << rb) : 0ull;
-    uint32_t rem = k;
-    while (rb > 0) {
-      const int wd = rb < 8 ? rb : 8, sh = rb - wd;
-      const uint64_t hmask = rb < 64 ? (~0ull << rb) : 0ull;
-      const uint32_t dmask = (1u << wd) - 1;
-#pragma unroll
-      for (int r = 0; r < kMergeWaveRegs; r++)
-        if (kv[r] && (kv[r] & hmask) == prefix) atomicAdd(&hist[(uint32_t)(kv[r] >> sh) & dmask], 1u);
-      uint32_t above;
-      const uint32_t bin = wave_select_bin(hist, rem, &above);
-      const uint32_t inbin = hist[bin];
-#pragma unroll
-      for (int i = 0; i < 4; i++) hist[lane + 64 * i] = 0;
-      prefix |= (uint64_t)bin << sh;
-      rem -= above;
-      rb = sh;
-      if (inbin == rem) break;
-    }
-    tmask = ~0ull << rb;
-    T = prefix;
-  }
-  // gather the kk winners one per lane (lane order = flat order), sort descending
-  uint64_t mine = 0;
-  uint32_t base = 0;
-#pragma unroll
-  for (int r = 0; r < kMergeWaveRegs; r++) {
-    const bool take = kv[r] && (kv[r] & tmask) >= T;
-    const uint64_t m = __ballot(take);
-    const uint32_t pos = base + (uint32_t)__popcll(m & ((1ull << lane) - 1));
-    // lane `pos` receives this key: scatter through the LDS histogram space
-    if (take) reinterpret_cast<uint64_t *>(hist)[pos & 127] = kv[r];
-    base += (uint32_t)__popcll(m);
-  }
-  __builtin_amdgcn_wave_barrier();
-  if (lane < kk) mine = reinterpret_cast<uint64_t *>(hist)[lane];
-#pragma unroll
-  for (uint32_t size = 2; size <= 64; size <<= 1) mine = bitonic_stages(mine, lane, size);
-  if (lane < kk) {
-    p.out_doc[(size_t)q * k + lane] = ~(uint32_t)(mine & 0xFFFFFFFFu);
-    p.out_score[(size_t)q * k + lane] = __uint_as_float((uint32_t)(mine >> 32));
-  }
-  if (lane == 0) p.out_n[q] = kk;
+  merge_query_wave(p, q, hist);
 }
 
 hipError_t launch_merge_topk(const QueryParams &p, hipStream_t s) {

@@ -255,6 +255,7 @@ hipError_t launch_term_pairs(const TermParams &p, hipStream_t s);
 hipError_t launch_term_sort(const TermParams &p, hipStream_t s);
 
 // --- query scoring (kernels_query.hip) ---
+constexpr uint32_t kInlTerms = 32;          // query terms carried in QueryParams (fused single query)
 struct QueryParams {
   const uint64_t *post;       // term-major postings (toff != nullptr)
   const uint32_t *post32;     // block-major postings (post_word)
@@ -291,6 +292,14 @@ struct QueryParams {
   uint32_t *ovf2_list;        // pairs of operator queries (q_meta != 0), for k_score_blocks<true>
   uint32_t *ovf2_count;
   uint32_t list_grid;         // k_score_blocks workgroups in list mode
+  // single query, one launch (tfidf_search, k <= 64): the query terms ride in
+  // the kernel arguments (inl_n > 0: no upload) and the blocks' candidates go
+  // to pinned host memory (cand / cand_n), merged by the host
+  uint32_t inl_n;
+  uint32_t inl_meta;
+  uint32_t inl_slot[kInlTerms];
+  float inl_w[kInlTerms];
+  uint32_t inl_role[kInlTerms];
 };
 hipError_t launch_score_pairs(const QueryParams &p, int grid, hipStream_t s);
 constexpr uint32_t kPairWavesPerWG = 2;   // k_score_pairs workgroup = 2 waves (30 KB LDS: 5 per CU)
