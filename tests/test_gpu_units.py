@@ -138,3 +138,17 @@ def test_query_timing_toggle(corpus):
     d_on, s_on, c_on = g.search_batch(qs, 10)
     assert off == on
     assert (c_off == c_on).all() and (d_off == d_on).all() and (s_off.view("i4") == s_on.view("i4")).all()
+
+
+@pytest.mark.parametrize("chunks", ["1", "3", "7"])
+def test_pipelined_batch_chunks_equal_oracle(corpus, chunks, monkeypatch):
+    """tfidf_search_batch prepares chunk c + 1 on the host while chunk c scores:
+    any chunking (uneven chunks, a chunk whose queries have no present term)
+    gives the oracle's rows in the caller's order."""
+    g, o = corpus
+    qs = queries()[:1200] + [b"zzzzzz qqqqqq"] * 300 + queries()[1200:]
+    monkeypatch.setenv("TFIDF_BATCH_CHUNKS", chunks)
+    docs, scores, counts = g.search_batch(qs, 10)
+    for i in range(0, len(qs), 7):
+        assert rows(docs, scores, counts, i) == want(o, qs[i], 10), (chunks, i, qs[i])
+    assert all(counts[i] == 0 for i in range(1200, 1500))

@@ -228,6 +228,7 @@ struct tfidf_index {
   std::vector<uint32_t> q_units;       // batch scoring units {q, b0, b1, 0} (run_scoring)
   uint64_t unit_batches = 0, unit_count = 0, fused_queries = 0;
   bool q_timing = true;                // record HIP events around each search (tfidf_set_query_timing)
+  bool q_rec_start = true;             // run_scoring records EV_Q0 (false: a later chunk of a pipelined batch)
   hipEvent_t q_ev[2] = {nullptr, nullptr};  // fork / join of the wave-unit kernel on copy_stream
   hipEvent_t q_in_ev = nullptr;        // the last upload out of q_host
   bool q_in_pending = false;
@@ -1366,6 +1367,57 @@ struct QueryBatch {
 // device (10 k queries: ~10 ms on one thread).  A query that does not parse
 // (or is not UTF-8) has no hits, as the reference answers [] for it
 // (Worker.java:182-185); the batch goes on.
+// Persistent host workers for batch query preparation (spawning 16 threads per
+// batch cost ~0.5 ms of a 10 k-query batch).  run(n, fn): fn(a, b) over `parts`
+// slices of [0, n), the caller taking slice 0; one batch at a time.
+struct PrepPool {
+  std::vector<std::thread> th;
+  std::mutex run_mu, mu;
+  std::condition_variable cv, done_cv;
+  std::function<void(uint32_t, uint32_t)> fn;
+  uint32_t n = 0, parts = 0, next = 0, finished = 0;
+  uint64_t gen = 0;
+  explicit PrepPool(uint32_t workers) {
+    for (uint32_t i = 0; i < workers; i++) th.emplace_back([this] { loop(); });
+  }
+  void slice(uint32_t i) { fn((uint32_t)((uint64_t)n * i / parts), (uint32_t)((uint64_t)n * (i + 1) / parts)); }
+  void loop() {
+    uint64_t seen = 0;
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv.wait(lk, [&] { return gen != seen; });
+      seen = gen;
+      while (next < parts) {
+        const uint32_t i = next++;
+        lk.unlock();
+        slice(i);
+        lk.lock();
+        if (++finished == parts) done_cv.notify_all();
+      }
+    }
+  }
+  void run(uint32_t n_items, uint32_t n_parts, std::function<void(uint32_t, uint32_t)> f) {
+    std::lock_guard<std::mutex> rl(run_mu);
+    std::unique_lock<std::mutex> lk(mu);
+    fn = std::move(f);
+    n = n_items;
+    parts = n_parts;
+    next = 1;                                           // slice 0: the caller
+    finished = 0;
+    gen++;
+    cv.notify_all();
+    lk.unlock();
+    slice(0);
+    lk.lock();
+    if (++finished < parts) done_cv.wait(lk, [&] { return finished == parts; });
+  }
+};
+static PrepPool *prep_pool() {
+  // never destroyed: its threads block forever on an idle pool
+  static PrepPool *pool = new PrepPool(std::min<uint32_t>(std::max(1u, std::thread::hardware_concurrency()), 16u) - 1);
+  return pool;
+}
+
 static int prepare_batch(tfidf_index *ix, const uint8_t *q_utf8, const uint64_t *q_offsets, uint32_t n_q,
                          QueryBatch *qb) {
   if (int e = wait_gdf(ix)) return e;                   // once, before the workers read the mirrors
@@ -1377,15 +1429,9 @@ static int prepare_batch(tfidf_index *ix, const uint8_t *q_utf8, const uint64_t 
         pqs[i] = PreparedQuery();
   };
   uint32_t nt = std::min<uint32_t>(std::max(1u, std::thread::hardware_concurrency()), 16u);
-  nt = std::max(1u, std::min(nt, n_q / 1024));
-  if (nt <= 1) {
-    work(0, n_q);
-  } else {
-    std::vector<std::thread> th;
-    for (uint32_t t = 1; t < nt; t++) th.emplace_back(work, (uint32_t)((uint64_t)n_q * t / nt), (uint32_t)((uint64_t)n_q * (t + 1) / nt));
-    work(0, (uint32_t)(n_q / nt));
-    for (auto &x : th) x.join();
-  }
+  nt = std::max(1u, std::min(nt, n_q / 128));
+  if (nt <= 1) work(0, n_q);
+  else prep_pool()->run(n_q, nt, work);
   size_t ns = 0;
   for (const PreparedQuery &pq : pqs) ns += pq.slot.size();
   qb->slot.reserve(ns);
@@ -1511,7 +1557,7 @@ static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint
     qp.hits = ix->hits.as<uint64_t>();
     qp.hits_n = ix->hits_n.as<uint32_t>();
   }
-  if (ix->q_timing) HIP_TRY(hipEventRecord(ix->ev[EV_Q0], s));
+  if (ix->q_timing && ix->q_rec_start) HIP_TRY(hipEventRecord(ix->ev[EV_Q0], s));
   if (unit_path) {
     HIP_TRY(ix->ovf.reserve(64));
     uint32_t *ctr = ix->ovf.as<uint32_t>();
@@ -1719,35 +1765,69 @@ extern "C" int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const 
   DeviceGuard g(ix->cfg.device);
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
-  QueryBatch qb;
-  if (int e = prepare_batch(ix, q_utf8, q_offsets, n_q, &qb)) return e;
   if (n_q == 0) return TFIDF_OK;
-  if (ix->n_docs == 0 || qb.slot.empty()) {
-    memset(counts, 0, n_q * 4);
+  if (ix->n_docs == 0) {
+    memset(counts, 0, (size_t)n_q * 4);
     return TFIDF_OK;
   }
-  const auto t1 = clk::now();
-  int rc = run_scoring(ix, qb, n_q, k);
-  if (rc) return rc;
-  const auto t2 = clk::now();
-  // results are contiguous on the device (doc | score | n): one copy into
-  // pinned memory, then into the caller's (usually pageable) arrays
+  // Pipelined in chunks: chunk c + 1 is prepared on the host (parse, analysis,
+  // dictionary lookups, weights) while chunk c scores on the device; each
+  // chunk's results are copied (stream-ordered) into its region of one pinned
+  // buffer.  The first chunk is the largest, so the device buffers sized by it
+  // are never re-allocated under a pending chunk.  TFIDF_BATCH_CHUNKS overrides.
+  // 10 k queries at cfg 2 (tools/gpu_batch_ab.sh): 1 chunk 7.6 ms end to end
+  // (prepare 1.5 on the pool, device 5.65), 2 chunks 7.0 (device 6.05), 4
+  // chunks 7.45 (device 6.9: every chunk pays the unit kernels' tail)
+  uint32_t n_chunks = n_q >= 4096 ? 2 : 1;
+  if (const char *e = getenv("TFIDF_BATCH_CHUNKS")) n_chunks = (uint32_t)std::max(1, std::min(atoi(e), 64));
+  n_chunks = std::max(1u, std::min(n_chunks, n_q));
   hipStream_t s = ix->stream;
   const size_t words = (size_t)2 * n_q * k + n_q;
   HIP_TRY(ix->q_res.resize(words));
-  HIP_TRY(hipMemcpyAsync(ix->q_res.data(), ix->res_doc, words * 4, hipMemcpyDeviceToHost, s));
+  double t_prep = 0, t_sub = 0;
+  bool any = false;
+  uint32_t c0 = 0;
+  for (uint32_t c = 0; c < n_chunks; c++) {
+    const uint32_t c1 = (uint32_t)((uint64_t)n_q * (c + 1) / n_chunks);
+    const uint32_t nc = c1 - c0;                         // non-increasing over c
+    const auto ta = clk::now();
+    QueryBatch qb;
+    if (int e = prepare_batch(ix, q_utf8, q_offsets + c0, nc, &qb)) { ix->q_rec_start = true; return e; }
+    const auto tb = clk::now();
+    uint32_t *hres = ix->q_res.data() + (size_t)2 * c0 * k + c0;
+    if (qb.slot.empty()) {
+      memset(hres + (size_t)2 * nc * k, 0, (size_t)nc * 4);   // no term of the chunk is present
+    } else {
+      ix->q_rec_start = !any;
+      const int rc = run_scoring(ix, qb, nc, k);
+      ix->q_rec_start = true;
+      if (rc) return rc;
+      HIP_TRY(hipMemcpyAsync(hres, ix->res_doc, ((size_t)2 * nc * k + nc) * 4, hipMemcpyDeviceToHost, s));
+      any = true;
+    }
+    t_prep += std::chrono::duration<double, std::milli>(tb - ta).count();
+    t_sub += std::chrono::duration<double, std::milli>(clk::now() - tb).count();
+    c0 = c1;
+  }
+  const auto t2 = clk::now();
   HIP_TRY(hipStreamSynchronize(s));
   ix->q_in_pending = false;
   const auto t3 = clk::now();
-  memcpy(doc_ids, ix->q_res.data(), (size_t)n_q * k * 4);
-  memcpy(scores, ix->q_res.data() + (size_t)n_q * k, (size_t)n_q * k * 4);
-  memcpy(counts, ix->q_res.data() + (size_t)2 * n_q * k, (size_t)n_q * 4);
-  ix->last_ms_scoring = ev_ms(ix, EV_Q0, EV_Q1);
-  ix->last_ms_total = ev_ms(ix, EV_Q0, EV_Q2);
+  c0 = 0;
+  for (uint32_t c = 0; c < n_chunks; c++) {
+    const uint32_t c1 = (uint32_t)((uint64_t)n_q * (c + 1) / n_chunks), nc = c1 - c0;
+    const uint32_t *hres = ix->q_res.data() + (size_t)2 * c0 * k + c0;
+    memcpy(doc_ids + (size_t)c0 * k, hres, (size_t)nc * k * 4);
+    memcpy(scores + (size_t)c0 * k, hres + (size_t)nc * k, (size_t)nc * k * 4);
+    memcpy(counts + c0, hres + (size_t)2 * nc * k, (size_t)nc * 4);
+    c0 = c1;
+  }
+  ix->last_ms_scoring = any ? ev_ms(ix, EV_Q0, EV_Q1) : 0.0f;
+  ix->last_ms_total = any ? ev_ms(ix, EV_Q0, EV_Q2) : 0.0f;
   if (getenv("TFIDF_HOST_TIMING")) {          // profiling only
     auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
-    fprintf(stderr, "batch %u: prepare %.3f  submit %.3f  wait %.3f  copy-out %.3f ms (device %.3f)\n", n_q,
-            ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, clk::now()), ix->last_ms_total);
+    fprintf(stderr, "batch %u (%u chunks): prepare %.3f  submit %.3f  wait %.3f  copy-out %.3f  total %.3f ms (device %.3f)\n",
+            n_q, n_chunks, t_prep, t_sub, ms(t2, t3), ms(t3, clk::now()), ms(t0, clk::now()), ix->last_ms_total);
   }
   return TFIDF_OK;
 }
