@@ -386,6 +386,7 @@ constexpr uint32_t kWaveK = 8;                    // tokens / terms per lane in 
 #define TFIDF_HIST10 0                            // 10-token-per-lane batches for 513..640-token documents
 #endif
 constexpr uint32_t kWaveTerms = 64 * kWaveK;      // distinct terms per document (wave path)
+static_assert(kWaveTerms == kPairWords, "a chunk unit stores at most kWaveTerms pairs");
 constexpr uint32_t kWaveQueue = 128;              // histogram retry queue: two entries per lane
 constexpr uint32_t kDictQueue = 64;               // dictionary retry queue: one entry per lane
 constexpr uint64_t kFoldBit = 1ull << 63;
@@ -1363,10 +1364,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
 // (UAX#29 decisions look at most two characters around a position; a token
 // that runs past the post margin is longer than 255 characters), keeps the
 // tokens STARTING in its core, counts them in its LDS table, resolves the
-// distinct terms in the global dictionary (resolve_terms) and adds the counts
-// into the document's dense per-slot array (global atomics).  k_long_rows then
-// turns each document's dense array into its CSR row (slot order, so grouped
-// by range) and zeroes it.  A chunk that cannot take this path (non-ASCII
+// distinct terms in the global dictionary (resolve_terms) and stores them as
+// the unit's pair list ((slot within bucket) << kPairTfBits | tf), grouped by
+// slot bucket (slot >> pair_bshift; bucket starts in pair_ub).  k_long_rows
+// then sums each document's pair lists window by window in LDS into its CSR
+// row.  (Round 2 added the counts into a dense per-document array in HBM with
+// global atomics: ~20 M scattered memory-side atomics per 300-book build cost
+// 0.43 of the 1.29 ms, and scanning the 1 MB arrays another 0.26.)  A chunk
+// that cannot take this path (non-ASCII
 // text, a token of more than 255 characters, more than 512 distinct terms)
 // marks its document, which then goes to k_tokenize_long as a whole.
 constexpr uint32_t kCoreBytes = kLongCoreBytes;
@@ -1410,7 +1415,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   init_sel_table(sm.sel, lane);
   uint4 v[4] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
   const uint64_t n_units = p.n_chunks;
-  const uint64_t C = (uint64_t)p.cap_mask + 1;
   uint16_t *slots = reinterpret_cast<uint16_t *>(sm.list);
   ChunkMeta meta;
   auto prefetch = [&](const ChunkMeta &m) {
@@ -1529,74 +1533,175 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     uint32_t g[kWaveK], tf[kWaveK], tdoc[kWaveK];
     uint32_t actm = 0;
     resolve_terms<false, false>(sm, p, lane, nu, (uint32_t)m.d, g, tf, tdoc, actm, nullptr, nullptr, m.s0 - m.shift);
-    uint32_t *dense = p.dense + (uint64_t)m.gi * C;
+    {   // the unit's (slot, tf) pairs, counting-sorted by slot bucket in LDS (text and retry
+        // queue are dead here), stored as one contiguous run; bucket starts to pair_ub
+      uint32_t *bcnt = reinterpret_cast<uint32_t *>(sm.qkey);          // [0, 64) counts, [64, 128) starts
+      uint32_t *stage = reinterpret_cast<uint32_t *>(sm.text);
+      const uint32_t bsh = p.pair_bshift, nb = p.pair_nb, bmask = (1u << bsh) - 1u;
+      bcnt[lane] = 0;
+      asm volatile("" ::: "memory");
+      uint32_t rank[kWaveK];
 #pragma unroll
-    for (int k = 0; k < (int)kWaveK; k++)
-      if ((actm >> k) & 1u) atomicAdd(&dense[g[k]], tf[k]);
+      for (int k = 0; k < (int)kWaveK; k++) rank[k] = ((actm >> k) & 1u) ? atomicAdd(&bcnt[g[k] >> bsh], 1u) : 0u;
+      asm volatile("" ::: "memory");
+      const uint32_t n = bcnt[lane];
+      const uint32_t incl = wave_incl_add(n);
+      const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      bcnt[64 + lane] = incl - n;
+      uint32_t *ub = p.pair_ub + u * (nb + 1);
+      if (lane < nb) ub[lane] = incl - n;
+      if (lane == 0) ub[nb] = total;
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int k = 0; k < (int)kWaveK; k++)
+        if ((actm >> k) & 1u) stage[bcnt[64 + (g[k] >> bsh)] + rank[k]] = ((g[k] & bmask) << kPairTfBits) | tf[k];
+      asm volatile("" ::: "memory");
+      uint32_t *pr = p.pairs + u * kPairWords;
+      for (uint32_t i = lane; i < total; i += 64) pr[i] = stage[i];
+    }
     clear_table(sm, lane);
   }
 }
 
-// One workgroup per long document of the group: dense per-slot counts ->
-// CSR row in slot order (col = slot, tf = count), range splits, length,
-// norm, statistics; the dense array is zeroed for the next group.  A
-// document some chunk could not take goes to long_list (k_tokenize_long).
-__global__ void __launch_bounds__(1024) k_long_rows(BuildParams p) {
-  __shared__ uint32_t wsum[16];
-  __shared__ uint32_t carry;
+// One workgroup per long document of the group: its units' pair lists ->
+// CSR row, window by window (kRangeSlots slots; a window never straddles a
+// range, so the row stays grouped by range; order inside a window is free),
+// range splits, length, norm, statistics.  Per window: LDS counters zeroed,
+// the units' pairs of the window's bucket are added (below), then
+// each thread takes 32 counters (8 conflict-free 16 B reads) and a
+// workgroup scan places the non-zero ones.  A document some chunk could not
+// take goes to long_list (k_tokenize_long).
+constexpr uint32_t kLrUpt = TFIDF_LR_UPT;                   // units per thread in a segment round
+constexpr uint32_t kLrUnits = kLrUpt * kLrThreads;
+constexpr uint32_t kLrPer = kLrWin / kLrThreads;            // window counters per thread (emission)
+__global__ void __launch_bounds__(kLrThreads) TFIDF_LR_ATTR k_long_rows(BuildParams p) {
+  extern __shared__ uint32_t acc[];                       // [W] counters of the current window
+  __shared__ uint32_t wsum[kLrThreads / 64];
+  __shared__ uint32_t ulo[kLrUnits], upre[kLrUnits];
   __shared__ unsigned long long lsum;
   const uint32_t gi = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const uint64_t d = p.chunk_docs[gi];
-  const uint32_t C = p.cap_mask + 1;
-  uint32_t *dense = p.dense + (uint64_t)gi * C;
-  const bool failed = p.chunk_fail[gi] != 0;
-  if (failed) {
-    for (uint32_t i = tid; i < C / 4; i += blockDim.x) reinterpret_cast<uint4 *>(dense)[i] = make_uint4(0, 0, 0, 0);
+  if (p.chunk_fail[gi] != 0) {
     if (tid == 0) p.long_list[atomicAdd(p.long_count, 1u)] = (uint32_t)d;
     return;
   }
+  const uint32_t C = p.cap_mask + 1;
+  const uint32_t W = C < kLrWin ? C : kLrWin;             // power of two
+  const uint32_t wlog = 31 - __builtin_clz(W);
+  const uint32_t bsh = p.pair_bshift, nb = p.pair_nb;
   const uint64_t src = p.live_map ? p.live_map[d] : d;
   const uint64_t row = csr_row_base(p.offsets, src);
   const uint32_t RS = 1u << p.range_shift;
-  if (tid == 0) { carry = 0; lsum = 0; }
+  const uint32_t u0 = p.chunk_pre[gi], u1 = p.chunk_pre[gi + 1];
+  if (tid == 0) lsum = 0;
+  for (uint32_t i = tid; i < W / 4; i += kLrThreads) reinterpret_cast<uint4 *>(acc)[i] = make_uint4(0, 0, 0, 0);
   __syncthreads();
+  uint32_t carry = 0;
   unsigned long long my_len = 0;
-  for (uint32_t t0 = 0; t0 < C; t0 += 4 * 1024) {
-    const uint32_t i0 = t0 + 4 * tid;
-    uint4 x = make_uint4(0, 0, 0, 0);
-    if (i0 < C) {
-      x = reinterpret_cast<const uint4 *>(dense)[i0 >> 2];
-      reinterpret_cast<uint4 *>(dense)[i0 >> 2] = make_uint4(0, 0, 0, 0);
-    }
-    const uint32_t nz = (x.x != 0) + (x.y != 0) + (x.z != 0) + (x.w != 0);
-    my_len += (unsigned long long)x.x + x.y + x.z + x.w;
-    uint32_t incl = nz;
+  for (uint32_t t0 = 0; t0 < C; t0 += W) {
+    const uint32_t j = t0 >> bsh;                                 // the window's bucket
+    const uint32_t wsel = (t0 & ((1u << bsh) - 1u)) >> wlog;      // the window inside its bucket
+    // the window's bucket segments of up to kLrUnits units at a time: segment
+    // starts and an exclusive scan of their lengths in LDS, then the flattened
+    // entries, consecutive threads on consecutive words of a segment (coalesced;
+    // a thread per unit reading its own segment touched 64 lines per load), the
+    // unit of each entry by binary search of the scan
+    for (uint32_t ur = u0; ur < u1; ur += kLrUnits) {
+      const uint32_t nr = u1 - ur < kLrUnits ? u1 - ur : kLrUnits;
+      uint32_t cu[kLrUpt];
+      uint32_t tsum = 0;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t y = __shfl_up(incl, o, 64);
-      if (lane >= (uint32_t)o) incl += y;
+      for (int h = 0; h < (int)kLrUpt; h++) {
+        const uint32_t i = kLrUpt * tid + h;
+        cu[h] = 0;
+        if (i < nr) {
+          const uint32_t *ubr = p.pair_ub + (uint64_t)(ur + i) * (nb + 1);
+          const uint32_t lo = ubr[j];
+          cu[h] = ubr[j + 1] - lo;
+          ulo[i] = lo;
+        }
+        tsum += cu[h];
+      }
+      const uint32_t tin = wave_incl_add(tsum);
+      if (lane == 63) wsum[wid] = tin;
+      __syncthreads();
+      uint32_t tb = 0, T = 0;
+      for (uint32_t w = 0; w < kLrThreads / 64; w++) {
+        const uint32_t sw = wsum[w];
+        if (w < wid) tb += sw;
+        T += sw;
+      }
+      tb += tin - tsum;
+#pragma unroll
+      for (int h = 0; h < (int)kLrUpt; h++) {
+        if (kLrUpt * tid + h < nr) upre[kLrUpt * tid + h] = tb;
+        tb += cu[h];
+      }
+      __syncthreads();
+      constexpr int kIn = TFIDF_LR_IN;
+      for (uint32_t f0 = 0; f0 < T; f0 += kIn * kLrThreads) {
+        uint32_t ws[kIn], at[kIn];
+#pragma unroll
+        for (int q = 0; q < kIn; q++) at[q] = 0;
+        // last i with upre[i] <= f: the kIn searches step together (fixed trip count, their
+        // LDS reads overlap; a data-dependent loop per entry ran them one after another)
+        for (int step = 31 - __builtin_clz(nr); step >= 0; step--) {
+#pragma unroll
+          for (int q = 0; q < kIn; q++) {
+            const uint32_t f = f0 + (uint32_t)q * kLrThreads + tid, m = at[q] + (1u << step);
+            if (m < nr && upre[m] <= f) at[q] = m;
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < kIn; q++) {
+          const uint32_t f = f0 + (uint32_t)q * kLrThreads + tid;
+          ws[q] = f < T ? p.pairs[(uint64_t)(ur + at[q]) * kPairWords + ulo[at[q]] + (f - upre[at[q]])] : 0u;
+        }
+#pragma unroll
+        for (int q = 0; q < kIn; q++) {
+          const uint32_t loc = ws[q] >> kPairTfBits;
+          if (ws[q] && (loc >> wlog) == wsel) atomicAdd(&acc[loc & (W - 1)], ws[q] & ((1u << kPairTfBits) - 1u));
+        }
+      }
+      __syncthreads();                                            // wsum, ulo, upre reused
     }
+    __syncthreads();
+    // kLrPer (<= 32) counters per thread: i = (q * kLrThreads + tid) * 4 + c
+    uint32_t v[kLrPer];
+    uint32_t nz = 0;
+    const uint32_t nq = W / (4 * kLrThreads);                    // 16 B reads per thread (else one, partial)
+#pragma unroll
+    for (int q = 0; q < (int)kLrPer / 4; q++) {
+      uint4 x = make_uint4(0, 0, 0, 0);
+      const uint32_t i4 = (uint32_t)q * kLrThreads + tid;
+      if ((uint32_t)q < nq || (q == 0 && i4 < W / 4)) {
+        x = reinterpret_cast<uint4 *>(acc)[i4];
+        reinterpret_cast<uint4 *>(acc)[i4] = make_uint4(0, 0, 0, 0);   // zero for the next window
+      }
+      v[4 * q] = x.x; v[4 * q + 1] = x.y; v[4 * q + 2] = x.z; v[4 * q + 3] = x.w;
+      nz += (x.x != 0) + (x.y != 0) + (x.z != 0) + (x.w != 0);
+      my_len += (unsigned long long)x.x + x.y + x.z + x.w;
+    }
+    const uint32_t incl = wave_incl_add(nz);
     if (lane == 63) wsum[wid] = incl;
     __syncthreads();
     uint32_t base = carry, all = 0;
-    for (uint32_t w = 0; w < 16; w++) {
+    for (uint32_t w = 0; w < kLrThreads / 64; w++) {
       const uint32_t sw = wsum[w];
       if (w < wid) base += sw;
       all += sw;
     }
     uint32_t at = base + incl - nz;
-    const uint32_t vals[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
-    for (int q = 0; q < 4; q++)
-      if (vals[q]) { csr_put(p, row + at, i0 + q, vals[q], (uint32_t)d); at++; }
-    __syncthreads();
-    if (tid == 0) {
-      carry += all;
-      const uint32_t t1 = min(t0 + 4 * 1024, C);
-      // a range ends inside [t0, t1): its split = entries below its end
-      if ((t1 & (RS - 1)) == 0 || t1 == C) p.rsplit[d * p.n_ranges + ((t1 - 1) >> p.range_shift)] = carry;
-    }
-    __syncthreads();
+    for (int q = 0; q < (int)kLrPer / 4; q++)
+#pragma unroll
+      for (int c = 0; c < 4; c++)
+        if (v[4 * q + c]) { csr_put(p, row + at, t0 + ((uint32_t)q * kLrThreads + tid) * 4 + c, v[4 * q + c], (uint32_t)d); at++; }
+    carry += all;
+    const uint32_t t1 = t0 + W;
+    // a range ends at the window's end: its split = entries below it
+    if (tid == 0 && ((t1 & (RS - 1)) == 0 || t1 == C)) p.rsplit[d * p.n_ranges + ((t1 - 1) >> p.range_shift)] = carry;
+    __syncthreads();                                              // wsum and acc reused by the next window
   }
   if (my_len) atomicAdd(&lsum, my_len);
   __syncthreads();
@@ -2273,7 +2378,13 @@ hipError_t launch_tokenize_chunks(const BuildParams &p, int grid, hipStream_t s)
   return hipGetLastError();
 }
 hipError_t launch_long_rows(const BuildParams &p, uint32_t n_docs, hipStream_t s) {
-  hipLaunchKernelGGL(k_long_rows, dim3(n_docs), dim3(1024), 0, s, p);
+  static bool big = false;
+  if (!big) {
+    hipFuncSetAttribute((const void *)k_long_rows, hipFuncAttributeMaxDynamicSharedMemorySize, 4 * kLrWin);
+    big = true;
+  }
+  const uint32_t C = p.cap_mask + 1;
+  hipLaunchKernelGGL(k_long_rows, dim3(n_docs), dim3(kLrThreads), (C < kLrWin ? C : kLrWin) * 4, s, p);
   return hipGetLastError();
 }
 hipError_t launch_tokenize_long(const BuildParams &p, int grid, hipStream_t s) {

@@ -198,7 +198,7 @@ struct tfidf_index {
     return term_major ? tdf.as<uint32_t>() : blk.as<uint32_t>() + (size_t)n_blocks * C;
   }
   DevBuf lt_keys, lt_cnt, lt_g;
-  DevBuf dense, chunk_list, chunk_docs, chunk_fail;   // book-sized documents (chunk-parallel)
+  DevBuf pairs, pair_ub, chunk_list, chunk_docs, chunk_fail;   // book-sized documents (chunk-parallel)
   uint64_t long_chunked = 0;           // long documents the chunk path took in the last commit
   uint32_t lt_log2 = 0, lt_wgs = 64;   // lt_wgs: long-path workgroups always allowed
   PinnedVec<uint64_t> h_dict;        // host mirrors for query analysis (pinned)
@@ -304,7 +304,7 @@ extern "C" int tfidf_destroy(tfidf_index *ix) {
   hipStreamSynchronize(ix->copy_stream);
   DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->d_live_map, &ix->dict, &ix->csr, &ix->csr_esc, &ix->doc_len,
                     &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->long_list, &ix->uni_list, &ix->counters, &ix->blk,
-                    &ix->retry_list, &ix->bad_list, &ix->bbase, &ix->post, &ix->post_tmp, &ix->post_esc, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->lt_pos, &ix->verify_defer, &ix->dense, &ix->chunk_list, &ix->chunk_docs, &ix->chunk_fail, &ix->canon_of_slot,
+                    &ix->retry_list, &ix->bad_list, &ix->bbase, &ix->post, &ix->post_tmp, &ix->post_esc, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->lt_pos, &ix->verify_defer, &ix->pairs, &ix->pair_ub, &ix->chunk_list, &ix->chunk_docs, &ix->chunk_fail, &ix->canon_of_slot,
                     &ix->q_off, &ix->q_slot, &ix->q_w, &ix->q_role, &ix->q_meta, &ix->cache, &ix->cand, &ix->cand_n, &ix->out_doc,
                     &ix->out_score, &ix->out_n, &ix->q_in, &ix->q_out, &ix->hits, &ix->hits_n, &ix->hits_c, &ix->hits_s, &ix->hits_P, &ix->sort_tmp,
                     &ix->row_off, &ix->tvals, &ix->toff, &ix->tdf, &ix->term_tmp, &ix->term_esc, &ix->sent_slot, &ix->vcounts, &ix->vnu,
@@ -874,32 +874,39 @@ static int commit_once(tfidf_index *ix) {
   if (n_long) {
     HIP_TRY(hipEventRecord(ix->ev[EV_L0], s));
     // book-sized documents: chunk-parallel (k_tokenize_chunk + k_long_rows),
-    // in groups whose dense per-slot count arrays fit kDenseBudget; documents
-    // a chunk could not take come back in long_list for k_tokenize_long
+    // in groups whose unit pair lists fit kPairBudget; documents a chunk
+    // could not take come back in long_list for k_tokenize_long
     std::vector<uint32_t> ldocs(n_long);
     HIP_TRY(hipMemcpyAsync(ldocs.data(), ix->long_list.p, (size_t)n_long * 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    const uint64_t group_max = std::max<uint64_t>(1, kDenseBudget / ((uint64_t)C * 4));
-    const uint64_t gsz = std::min<uint64_t>(n_long, group_max);
-    if (ix->dense.bytes < gsz * C * 4) {
-      HIP_TRY(ix->dense.reserve(gsz * C * 4));
-      HIP_TRY(hipMemsetAsync(ix->dense.p, 0, ix->dense.bytes, s));     // k_long_rows leaves it zeroed
-    }
+    // pair buckets: at most 64, each a whole number of k_long_rows' LDS windows
+    const uint32_t wlog = std::min<uint32_t>(ix->cap_log2, kLrWinBits);
+    const uint32_t bsh = std::max<uint32_t>(wlog, ix->cap_log2 > 6 ? ix->cap_log2 - 6 : 0);
+    const uint32_t nb = 1u << (ix->cap_log2 - bsh);
+    const uint64_t unit_max = std::max<uint64_t>(1, kPairBudget / ((uint64_t)kPairWords * 4));
     // per group: the first unit (document, core) of each document, prefix form
     std::vector<uint32_t> pre;
-    std::vector<uint64_t> gpre;                      // offset of each group's prefix array
-    for (uint64_t g0 = 0; g0 < n_long; g0 += gsz) {
-      gpre.push_back(pre.size());
-      uint64_t acc = 0;
-      for (uint64_t i = g0; i < std::min<uint64_t>(n_long, g0 + gsz); i++) {
-        const uint64_t st = ix->live_map.empty() ? ldocs[i] : ix->live_map[ldocs[i]];
-        const uint64_t L = ix->h_offsets[st + 1] - ix->h_offsets[st];
-        pre.push_back((uint32_t)acc);
-        acc += (L + kLongCoreBytes - 1) / kLongCoreBytes;
+    std::vector<uint64_t> gpre, gdoc;               // each group's prefix array offset and first document
+    uint64_t acc = 0, max_units = 0;
+    for (uint64_t i = 0; i < n_long; i++) {
+      const uint64_t st = ix->live_map.empty() ? ldocs[i] : ix->live_map[ldocs[i]];
+      const uint64_t L = ix->h_offsets[st + 1] - ix->h_offsets[st];
+      const uint64_t units = (L + kLongCoreBytes - 1) / kLongCoreBytes;
+      if (i == 0 || acc + units > unit_max) {
+        if (i) { pre.push_back((uint32_t)acc); max_units = std::max(max_units, acc); }
+        gpre.push_back(pre.size());
+        gdoc.push_back(i);
+        acc = 0;
       }
-      if (acc >= 0xFFFFFFFFull) return fail(TFIDF_E_CAPACITY, "too many document chunks");
       pre.push_back((uint32_t)acc);
+      acc += units;
+      if (acc >= 0xFFFFFFFFull) return fail(TFIDF_E_CAPACITY, "too many document chunks");
     }
+    pre.push_back((uint32_t)acc);
+    max_units = std::max(max_units, acc);
+    gdoc.push_back(n_long);
+    HIP_TRY(ix->pairs.reserve(max_units * kPairWords * 4));
+    HIP_TRY(ix->pair_ub.reserve(max_units * (nb + 1) * 4));
     HIP_TRY(ix->chunk_list.reserve(pre.size() * 4 + 8));
     HIP_TRY(ix->chunk_docs.reserve((size_t)n_long * 4));
     HIP_TRY(ix->chunk_fail.reserve((size_t)n_long * 4));
@@ -908,14 +915,17 @@ static int commit_once(tfidf_index *ix) {
     HIP_TRY(hipMemsetAsync(ix->chunk_fail.p, 0, (size_t)n_long * 4, s));
     HIP_TRY(hipMemsetAsync(bp.long_count, 0, 4, s));                   // the fallback list restarts
     for (size_t gi = 0; gi < gpre.size(); gi++) {
-      const uint64_t g0 = gi * gsz, n = std::min<uint64_t>(gsz, n_long - g0);
+      const uint64_t g0 = gdoc[gi], n = gdoc[gi + 1] - g0;
       BuildParams cp = bp;
       cp.chunk_pre = ix->chunk_list.as<uint32_t>() + gpre[gi];
       cp.n_group_docs = (uint32_t)n;
       cp.n_chunks = pre[gpre[gi] + n];
       cp.chunk_docs = ix->chunk_docs.as<uint32_t>() + g0;
       cp.chunk_fail = ix->chunk_fail.as<uint32_t>() + g0;
-      cp.dense = ix->dense.as<uint32_t>();
+      cp.pairs = ix->pairs.as<uint32_t>();
+      cp.pair_ub = ix->pair_ub.as<uint32_t>();
+      cp.pair_bshift = bsh;
+      cp.pair_nb = nb;
       const uint64_t grid = std::min<uint64_t>(cp.n_chunks, (uint64_t)ix->num_cus * kWaveWGsPerCU);
       HIP_TRY(launch_tokenize_chunks(cp, (int)grid, s));
       HIP_TRY(launch_long_rows(cp, (uint32_t)n, s));

@@ -67,13 +67,16 @@ struct BuildParams {
   const uint32_t *doc_list_count;
   // book-sized documents, chunk-parallel (k_tokenize_chunk / k_long_rows):
   // the group's documents, their first unit (chunk_pre[n_group_docs + 1],
-  // unit = (document, core)), dense per-slot counts (group x C u32, zero
-  // between uses), failure flags
+  // unit = (document, core)), each unit's pair list (kWaveTerms u32 words:
+  // (slot & (2^pair_bshift - 1)) << kPairTfBits | tf, grouped by bucket
+  // slot >> pair_bshift) with its pair_nb + 1 bucket starts, failure flags
   const uint32_t *chunk_pre;
   uint32_t n_group_docs;
   uint64_t n_chunks;
   const uint32_t *chunk_docs;
-  uint32_t *dense;
+  uint32_t *pairs;
+  uint32_t *pair_ub;
+  uint32_t pair_bshift, pair_nb;
   uint32_t *chunk_fail;
 };
 
@@ -213,7 +216,26 @@ constexpr uint64_t kPackBytes = 2560;     // text per packed window (auto pack s
                                           // wave table's 512 distinct terms (cfg 5: 7 docs, tokenize 16.3 -> 14.9 ms)
 hipError_t launch_tokenize_long(const BuildParams &p, int grid, hipStream_t s);
 constexpr uint32_t kLongCoreBytes = 2048;              // = kCoreBytes (kernels_index.hip)
-constexpr uint64_t kDenseBudget = 2ull << 30;          // per-group dense count arrays (book-sized documents)
+constexpr uint64_t kPairBudget = 2ull << 30;           // per-group unit pair lists (book-sized documents)
+constexpr uint32_t kPairWords = 512;                    // pair list capacity per unit (= kWaveTerms)
+#ifndef TFIDF_LR_WIN_BITS
+#define TFIDF_LR_WIN_BITS 15
+#define TFIDF_LR_THREADS 1024
+#endif
+#ifndef TFIDF_LR_IN
+#define TFIDF_LR_IN 16
+#define TFIDF_LR_UPT 2
+#endif
+#ifdef TFIDF_LR_WPE
+#define TFIDF_LR_ATTR __attribute__((amdgpu_waves_per_eu(TFIDF_LR_WPE)))
+#else
+#define TFIDF_LR_ATTR
+#endif
+constexpr uint32_t kLrWinBits = TFIDF_LR_WIN_BITS;      // k_long_rows: LDS window of 2^kLrWinBits u32 counters (<= a range)
+constexpr uint32_t kLrWin = 1u << kLrWinBits;
+constexpr uint32_t kLrThreads = TFIDF_LR_THREADS;       // k_long_rows workgroup (kLrWin / kLrThreads <= 32)
+static_assert(kLrWinBits <= kRangeBits && kLrWin / kLrThreads <= 32 && kLrWin / kLrThreads >= 4, "k_long_rows window");
+constexpr uint32_t kPairTfBits = 12;                    // tf field of a pair word (a 2 KB core holds < 2^11 tokens)
 hipError_t launch_tokenize_chunks(const BuildParams &p, int grid, hipStream_t s);
 hipError_t launch_long_rows(const BuildParams &p, uint32_t n_docs, hipStream_t s);
 hipError_t launch_tokenize_uwave(const BuildParams &p, int grid, hipStream_t s);   // kernels_unicode.hip
