@@ -1485,9 +1485,90 @@ __global__ void __launch_bounds__(256) k_merge_runs(MergeRunsParams p) {
   }
 }
 
+// Levels 0-2 in one launch: workgroup g merges runs [8g, 8g + 8) (an 8-way
+// merge as three pairwise levels).  A group of <= kGroupCap keys is staged in
+// LDS once (ping-pong halves), merged there level by level, and written out
+// compact at its output offset; a larger group runs the same three levels
+// through global memory (spare, dst) inside the workgroup.  The remaining
+// levels (3, 4, ...) are k_merge_runs over the compact group runs.
+constexpr uint32_t kGroupRuns = 8;
+constexpr uint32_t kGroupCap = 8192;
+constexpr uint32_t kGroupThreads = 1024;
+
+// merge outputs [o, oend) of one level of a group: runs start at rb[] (compact
+// offsets, rb[kGroupRuns] = n), pairs of span runs
+__device__ __forceinline__ void group_level_chunk(const uint64_t *S, uint64_t *D, const uint32_t *rb, uint32_t span,
+                                                  uint32_t o, uint32_t oend) {
+  const uint32_t half = span >> 1;
+  while (o < oend) {
+    uint32_t m = 0;                                             // pair holding output o
+    for (uint32_t c = span; c < kGroupRuns; c += span)
+      if (rb[c] <= o) m = c;
+    const uint32_t ps = rb[m], pm = rb[min(m + half, kGroupRuns)], pe = rb[min(m + span, kGroupRuns)];
+    const uint32_t la = pm - ps, lb = pe - pm;
+    const uint64_t *A = S + ps, *Bv = S + pm;
+    const uint32_t j = o - ps;
+    uint32_t lo = j > lb ? j - lb : 0, hi = min(j, la);
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (A[mid] > Bv[j - mid - 1]) lo = mid + 1; else hi = mid;
+    }
+    uint32_t ia = lo, ib = j - lo;
+    const uint32_t stop = min(oend, pe);
+    for (; o < stop; o++) {
+      if (ib >= lb || (ia < la && A[ia] > Bv[ib])) D[o] = A[ia++];
+      else D[o] = Bv[ib++];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kGroupThreads) k_merge_group(MergeRunsParams p, uint64_t *spare) {
+  extern __shared__ uint64_t lds[];                             // [2][kGroupCap]
+  __shared__ uint32_t rb[kGroupRuns + 1];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t r0 = blockIdx.x * kGroupRuns;
+  const uint64_t ps = p.P[r0];
+  if (tid <= kGroupRuns) rb[tid] = (uint32_t)(p.P[min(r0 + tid, p.R)] - ps);
+  __syncthreads();
+  const uint32_t n = rb[kGroupRuns];
+  if (n == 0) return;                                           // workgroup-uniform
+  const bool in_lds = n <= kGroupCap;
+  uint64_t *X = in_lds ? lds : spare + ps, *Y = in_lds ? lds + kGroupCap : p.dst + ps;
+  // gapped runs (run r at src + r * kBlockDocs) -> compact X
+  for (uint32_t i = tid; i < n; i += kGroupThreads) {
+    uint32_t r = 0;
+#pragma unroll
+    for (uint32_t c = 1; c < kGroupRuns; c++) r = rb[c] <= i ? c : r;
+    X[i] = p.src[(uint64_t)(r0 + r) * kBlockDocs + (i - rb[r])];
+  }
+  __syncthreads();
+  const uint32_t per = (n + kGroupThreads - 1) / kGroupThreads;
+  for (uint32_t span = 2; span <= kGroupRuns; span <<= 1) {      // X -> Y, swap
+    const uint32_t o = min(tid * per, n), oend = min(o + per, n);
+    group_level_chunk(X, Y, rb, span, o, oend);
+    __syncthreads();
+    uint64_t *t = X; X = Y; Y = t;
+  }
+  // X holds the merged group (global path: spare, dst, spare, dst -> dst after 3 levels)
+  for (uint32_t i = tid; i < n; i += kGroupThreads) {
+    const uint64_t key = X[i], o = ps + i;
+    if (!p.final) {
+      if (in_lds) p.dst[o] = key;                               // (global path: already in dst)
+    } else {
+      const uint32_t doc = ~(uint32_t)(key & 0xFFFFFFFFull);
+      if (p.out_doc) {
+        p.out_doc[o] = doc;
+        p.out_score[o] = __uint_as_float((uint32_t)(key >> 32));
+      } else {
+        p.dst[o] = (key & 0xFFFFFFFF00000000ull) | (uint64_t)(~(uint32_t)(doc + p.doc_base));
+      }
+    }
+  }
+}
+
 hipError_t launch_hits_order(const uint64_t *hits, const uint32_t *hits_n, uint32_t R, uint64_t *P, uint64_t *tmp0,
-                             uint64_t *tmp1, uint32_t *out_doc, float *out_score, uint64_t *keys_out,
-                             uint64_t doc_base, int grid, hipStream_t s) {
+                             uint64_t *tmp1, uint64_t *tmp2, uint32_t *out_doc, float *out_score, uint64_t *keys_out,
+                             uint64_t doc_base, uint64_t hits_bound, int grid, hipStream_t s) {
   hipLaunchKernelGGL(k_hits_prefix, dim3(1), dim3(1024), 0, s, hits_n, R, P);
   uint32_t levels = 1;
   while ((1u << levels) < R) levels++;
@@ -1497,7 +1578,35 @@ hipError_t launch_hits_order(const uint64_t *hits, const uint32_t *hits_n, uint3
   mp.doc_base = doc_base;
   const uint64_t *src = hits;
   uint64_t *bufs[2] = {tmp0, tmp1};
-  for (uint32_t L = 0; L < levels; L++) {
+  uint32_t L0 = 0;
+  // Group merging pays when the groups fit in LDS: used when the query's hit
+  // bound (sum of its scoring terms' df) averages <= kHitsGroupAvg per group; a
+  // group that overflows anyway is merged correctly, one workgroup through
+  // global memory (slow: k_merge_group 22 us on average with the bench's heavy
+  // queries included).  TFIDF_HITS_PAIRWISE / TFIDF_HITS_GROUPS force a path (tests).
+  bool groups = hits_bound * kGroupRuns <= (uint64_t)R * kHitsGroupAvg;
+  if (getenv("TFIDF_HITS_PAIRWISE")) groups = false;
+  if (getenv("TFIDF_HITS_GROUPS")) groups = true;
+  if (groups) {                                                 // levels 0-2: one workgroup per 8 runs
+    static bool big = false;
+    if (!big) {
+      hipFuncSetAttribute((const void *)k_merge_group, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          2 * kGroupCap * 8);
+      big = true;
+    }
+    mp.src = hits;
+    mp.gapped = 1;
+    mp.final = levels <= 3;
+    mp.dst = mp.final && keys_out ? keys_out : tmp0;
+    mp.out_doc = mp.final && !keys_out ? out_doc : nullptr;
+    mp.out_score = mp.final && !keys_out ? out_score : nullptr;
+    hipLaunchKernelGGL(k_merge_group, dim3((R + kGroupRuns - 1) / kGroupRuns), dim3(kGroupThreads),
+                       2 * kGroupCap * 8, s, mp, tmp2);
+    if (mp.final) return hipGetLastError();
+    src = tmp0;                                                 // level 2's buffer (bufs[0])
+    L0 = 3;
+  }
+  for (uint32_t L = L0; L < levels; L++) {
     mp.src = src;
     mp.level = L;
     mp.gapped = L == 0;

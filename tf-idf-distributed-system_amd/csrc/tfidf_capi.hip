@@ -234,7 +234,7 @@ struct tfidf_index {
   bool q_in_pending = false;
   uint32_t *res_doc = nullptr, *res_n = nullptr;
   float *res_score = nullptr;
-  DevBuf q_off, q_slot, q_w, q_role, q_meta, cache, cand, cand_n, out_doc, out_score, out_n, hits, hits_n, hits_c, hits_s, hits_P, sort_tmp;
+  DevBuf q_off, q_slot, q_w, q_role, q_meta, cache, cand, cand_n, out_doc, out_score, out_n, hits, hits_n, hits_c, hits_s, hits_P, sort_tmp;   // hits_s: spare for oversized merge groups
   float last_ms_scoring = 0, last_ms_total = 0;
 };
 
@@ -1311,6 +1311,14 @@ struct PreparedQuery {
   uint32_t meta = 0;             // MUST clause count | has MUST_NOT << 31
 };
 
+// upper bound of a query's hits on this shard: the sum of its scoring terms' local df
+static uint64_t hits_bound(const tfidf_index *ix, const PreparedQuery &pq) {
+  uint64_t b = 0;
+  for (size_t i = 0; i < pq.slot.size(); i++)
+    if ((pq.role[i] >> 24) != kRoleNot) b += ix->h_df[pq.slot[i]];
+  return b;
+}
+
 // Query plan (analysis.h) -> dictionary slots + BM25 weights.  A term absent
 // from this shard's dictionary has no scorer (TermWeight.scorer == null): a
 // SHOULD or MUST_NOT term is dropped, a MUST clause without any present term
@@ -1744,12 +1752,14 @@ extern "C" int tfidf_search(tfidf_index *ix, const uint8_t *q, uint64_t q_len, u
   // all hits: per-block sorted runs -> merge passes on the device -> (doc, score)
   const uint32_t R = ix->n_blocks;
   HIP_TRY(ix->hits_c.reserve((size_t)R * kBlockDocs * 8 + 8));
+  HIP_TRY(ix->hits_s.reserve((size_t)R * kBlockDocs * 8 + 8));
   HIP_TRY(ix->hits_P.reserve(((size_t)R + 1) * 8));
   HIP_TRY(ix->out_doc.reserve((size_t)R * kBlockDocs * 4 + 4));
   HIP_TRY(ix->out_score.reserve((size_t)R * kBlockDocs * 4 + 4));
   HIP_TRY(launch_hits_order(ix->hits.as<uint64_t>(), ix->hits_n.as<uint32_t>(), R, ix->hits_P.as<uint64_t>(),
-                            ix->hits_c.as<uint64_t>(), ix->hits.as<uint64_t>(), ix->out_doc.as<uint32_t>(),
-                            ix->out_score.as<float>(), nullptr, 0, ix->num_cus * 4, s));
+                            ix->hits_c.as<uint64_t>(), ix->hits.as<uint64_t>(), ix->hits_s.as<uint64_t>(),
+                            ix->out_doc.as<uint32_t>(),
+                            ix->out_score.as<float>(), nullptr, 0, hits_bound(ix, pq), ix->num_cus * 4, s));
   if (ix->q_timing) HIP_TRY(hipEventRecord(ix->ev[EV_Q2], s));
   uint64_t H = 0;
   HIP_TRY(hipMemcpyAsync(&H, ix->hits_P.as<uint64_t>() + R, 8, hipMemcpyDeviceToHost, s));
@@ -2011,10 +2021,11 @@ extern "C" int tfidf_search_all_keys_device(tfidf_index *ix, const uint8_t *q, u
   hipStream_t s = ix->stream;
   const uint32_t R = ix->n_blocks;
   HIP_TRY(ix->hits_c.reserve((size_t)R * kBlockDocs * 8 + 8));
+  HIP_TRY(ix->hits_s.reserve((size_t)R * kBlockDocs * 8 + 8));
   HIP_TRY(ix->hits_P.reserve(((size_t)R + 1) * 8));
   HIP_TRY(launch_hits_order(ix->hits.as<uint64_t>(), ix->hits_n.as<uint32_t>(), R, ix->hits_P.as<uint64_t>(),
-                            ix->hits_c.as<uint64_t>(), ix->hits.as<uint64_t>(), nullptr, nullptr,
-                            static_cast<uint64_t *>(d_keys), doc_base, ix->num_cus * 4, s));
+                            ix->hits_c.as<uint64_t>(), ix->hits.as<uint64_t>(), ix->hits_s.as<uint64_t>(), nullptr, nullptr,
+                            static_cast<uint64_t *>(d_keys), doc_base, hits_bound(ix, pq), ix->num_cus * 4, s));
   if (ix->q_timing) HIP_TRY(hipEventRecord(ix->ev[EV_Q2], s));
   HIP_TRY(hipMemcpyAsync(n_out, ix->hits_P.as<uint64_t>() + R, 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));

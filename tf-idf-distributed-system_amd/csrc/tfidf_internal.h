@@ -348,8 +348,9 @@ hipError_t launch_merge_topk(const QueryParams &p, hipStream_t s);
 hipError_t launch_pack_keys(const uint32_t *out_doc, const float *out_score, const uint32_t *out_n, uint32_t n_q,
                             uint32_t k, uint64_t doc_base, uint64_t *keys, hipStream_t s);
 hipError_t launch_hits_order(const uint64_t *hits, const uint32_t *hits_n, uint32_t R, uint64_t *P, uint64_t *tmp0,
-                             uint64_t *tmp1, uint32_t *out_doc, float *out_score, uint64_t *keys_out,
-                             uint64_t doc_base, int grid, hipStream_t s);
+                             uint64_t *tmp1, uint64_t *tmp2, uint32_t *out_doc, float *out_score, uint64_t *keys_out,
+                             uint64_t doc_base, uint64_t hits_bound, int grid, hipStream_t s);
+constexpr uint64_t kHitsGroupAvg = 6144;   // all hits: 8-run LDS group merge when hits per group average <= this
 
 // --- GLOBAL statistics by term ownership (kernels_vocab.hip) ---
 hipError_t vocab_count(const uint64_t *dict, uint32_t C, uint32_t G, uint32_t *counts, hipStream_t s);
