@@ -199,6 +199,8 @@ struct tfidf_index {
   }
   DevBuf lt_keys, lt_cnt, lt_g;
   DevBuf pairs, pair_ub, chunk_list, chunk_docs, chunk_fail;   // book-sized documents (chunk-parallel)
+  PinnedVec<uint32_t> ldocs_h, pre_h;                            // their host staging
+  PinnedVec<uint64_t> hctr_h;                                    // build counters read back after the tokenizers
   uint64_t long_chunked = 0;           // long documents the chunk path took in the last commit
   uint32_t lt_log2 = 0, lt_wgs = 64;   // lt_wgs: long-path workgroups always allowed
   PinnedVec<uint64_t> h_dict;        // host mirrors for query analysis (pinned)
@@ -864,8 +866,9 @@ static int commit_once(tfidf_index *ix) {
   // one read of the counters: stats (0-2), error flags (3), long (4) and
   // non-ASCII (6) document counts, CSR escapes (9) (32-bit counters in the low
   // halves); read again only when the long path ran
-  uint64_t hctr[10];
-  HIP_TRY(hipMemcpyAsync(hctr, ctr, sizeof hctr, hipMemcpyDeviceToHost, s));
+  HIP_TRY(ix->hctr_h.resize(10));                      // pinned: a pageable read is staged by the runtime
+  uint64_t *hctr = ix->hctr_h.data();
+  HIP_TRY(hipMemcpyAsync(hctr, ctr, 10 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   const uint32_t n_long = (uint32_t)hctr[4], n_uni = (uint32_t)hctr[6];
   ix->long_chunked = 0;
@@ -876,7 +879,9 @@ static int commit_once(tfidf_index *ix) {
     // book-sized documents: chunk-parallel (k_tokenize_chunk + k_long_rows),
     // in groups whose unit pair lists fit kPairBudget; documents a chunk
     // could not take come back in long_list for k_tokenize_long
-    std::vector<uint32_t> ldocs(n_long);
+    // pinned host buffers: pageable copies are staged synchronously by the runtime
+    PinnedVec<uint32_t> &ldocs = ix->ldocs_h;
+    HIP_TRY(ldocs.resize(n_long));
     HIP_TRY(hipMemcpyAsync(ldocs.data(), ix->long_list.p, (size_t)n_long * 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
     // pair buckets: at most 64, each a whole number of k_long_rows' LDS windows
@@ -910,8 +915,10 @@ static int commit_once(tfidf_index *ix) {
     HIP_TRY(ix->chunk_list.reserve(pre.size() * 4 + 8));
     HIP_TRY(ix->chunk_docs.reserve((size_t)n_long * 4));
     HIP_TRY(ix->chunk_fail.reserve((size_t)n_long * 4));
-    HIP_TRY(hipMemcpyAsync(ix->chunk_list.p, pre.data(), pre.size() * 4, hipMemcpyHostToDevice, s));
-    HIP_TRY(hipMemcpyAsync(ix->chunk_docs.p, ldocs.data(), (size_t)n_long * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(ix->pre_h.resize(pre.size()));
+    memcpy(ix->pre_h.data(), pre.data(), pre.size() * 4);
+    HIP_TRY(hipMemcpyAsync(ix->chunk_list.p, ix->pre_h.data(), pre.size() * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(ix->chunk_docs.p, ix->long_list.p, (size_t)n_long * 4, hipMemcpyDeviceToDevice, s));
     HIP_TRY(hipMemsetAsync(ix->chunk_fail.p, 0, (size_t)n_long * 4, s));
     HIP_TRY(hipMemsetAsync(bp.long_count, 0, 4, s));                   // the fallback list restarts
     for (size_t gi = 0; gi < gpre.size(); gi++) {
@@ -960,7 +967,7 @@ static int commit_once(tfidf_index *ix) {
       HIP_TRY(launch_tokenize_long(bp, (int)wgs, s));
     }
     HIP_TRY(hipEventRecord(ix->ev[EV_LONG], s));
-    HIP_TRY(hipMemcpyAsync(hctr, ctr, sizeof hctr, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(hctr, ctr, 10 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
   }
   const uint32_t err = (uint32_t)(hctr[3] & 0xFFFFFFFFu), err_doc = (uint32_t)(hctr[3] >> 32);
