@@ -217,6 +217,67 @@ __global__ void __launch_bounds__(256) k_term_pairs_wide(TermParams p) {
   }
 }
 
+// Tile-aligned form (round 3): workgroup t writes exactly the words of radix
+// tile t (indices [t, t + 1) * kRsTile, starting inside document tile_doc[t])
+// and stores the tile's histogram of the first radix digit (the slot's low
+// bits), so the sort's first k_rs_hist pass — a full read of the words — is
+// not needed.  Each wave walks four documents per step (16 lanes each) on its
+// own, until its documents start past the tile; a document that straddles a
+// tile boundary is split between the two workgroups.
+__global__ void __launch_bounds__(256) k_term_pairs_tiled(TermParams p, const uint32_t *tile_doc, uint32_t *hist) {
+  __shared__ uint32_t h[256];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, grp = lane >> 4, sl = lane & 15, wid = tid >> 6;
+  h[tid] = 0;
+  __syncthreads();
+  const uint32_t esc = csr_esc_value(p.slot_bits);
+  const TermLayout ly{p.slot_bits, p.doc_bits, p.tf_bits};
+  const uint32_t mask0 = (1u << (p.slot_bits < 8 ? p.slot_bits : 8)) - 1;
+  const uint64_t i0 = (uint64_t)blockIdx.x * kRsTile, i1 = min(i0 + kRsTile, p.nnz);
+  for (uint64_t db = tile_doc[blockIdx.x];; db += 16) {
+    const uint64_t d = db + 4 * wid + grp;
+    bool before_end = false;
+    if (d < p.n_docs) {
+      const uint64_t o = p.row_off[d];
+      before_end = o < i1;
+      if (before_end) {
+        const uint32_t n = p.doc_nuniq[d];
+        const uint64_t jlo = o < i0 ? i0 - o : 0, jhi = min((uint64_t)n, i1 - o);
+        if (jlo < jhi) {
+          const uint64_t src = p.live_map ? p.live_map[d] : d;
+          const uint64_t base = csr_row_base(p.offsets, src);
+          const uint32_t nrm = p.doc_norm[d];
+          for (uint64_t j = jlo + sl; j < jhi; j += 16) {
+            const uint32_t e = p.csr[base + j], c = csr_local(e, p.slot_bits);
+            uint32_t t = csr_tf_field(e, p.slot_bits);
+            if (t == esc) t = csr_esc_tf(p.csr_esc, p.n_esc, base + j);
+            if (t > kMaxTf) atomicOr(p.err, kErrTfTooLarge);
+            if (t >= ly.tf_esc()) {                                // rare: exact tf kept aside, keyed (slot, doc)
+              const uint32_t at = atomicAdd(p.tesc_count, 1u);
+              if (at < p.tesc_cap) {
+                p.tesc[2 * (uint64_t)at] = ((uint64_t)c << kTermDocBits) | d;
+                p.tesc[2 * (uint64_t)at + 1] = min(t, kMaxTf);
+              }
+            }
+            p.keys[o + j] = ly.pack(c, d, t, nrm);
+            atomicAdd(&h[c & mask0], 1u);
+          }
+        }
+      }
+    }
+    if (!__any(before_end)) break;                             // documents are in row order (wave-uniform)
+  }
+  __syncthreads();
+  hist[(uint64_t)blockIdx.x * 256 + tid] = h[tid];
+}
+
+// tile t's first word lies in the row of document tile_doc[t]
+__global__ void k_tile_docs(const uint32_t *row_off, const uint32_t *nuniq, uint64_t n_docs, uint32_t *tile_doc) {
+  const uint64_t d = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= n_docs) return;
+  const uint64_t o = row_off[d], n = nuniq[d];
+  for (uint64_t t = (o + kRsTile - 1) / kRsTile; t * kRsTile < o + n; t++) tile_doc[t] = (uint32_t)d;
+}
+
 // ---------------------------------------------------------------------------
 // LSD radix passes (8-bit digits of the key bits from `shift`)
 
@@ -414,14 +475,32 @@ static uint64_t scan_sums_words(uint64_t n_docs, uint64_t nnz, uint32_t C) {
   return std::max<uint64_t>((std::max<uint64_t>(std::max<uint64_t>(hist, n_docs), C) + kScanBlock - 1) / kScanBlock,
                             col) + 16;
 }
-uint64_t term_invert_scratch_words(uint64_t n_docs, uint64_t nnz, uint32_t C) {
+// ... | tile_doc [tiles] (k_term_pairs_tiled)
+static uint64_t tile_doc_offset(uint64_t n_docs, uint64_t nnz, uint32_t C) {
   const uint64_t hist = 256 * ((nnz + kRsTile - 1) / kRsTile);
   return 2 * hist + scan_sums_words(n_docs, nnz, C) + C + 16;
+}
+uint64_t term_invert_scratch_words(uint64_t n_docs, uint64_t nnz, uint32_t C) {
+  return tile_doc_offset(n_docs, nnz, C) + (nnz + kRsTile - 1) / kRsTile + 16;
+}
+// Book-sized rows (SURVEY cfg 1) keep the row kernels (k_term_pairs_wide: many
+// workgroups per row) and the first k_rs_hist pass; TFIDF_TERM_PAIRS_ROWS forces them (A/B)
+static bool term_rows_path(const TermParams &p) {
+  return getenv("TFIDF_TERM_PAIRS_ROWS") != nullptr || (p.n_docs && p.nnz / p.n_docs > 2048);
 }
 
 hipError_t launch_term_pairs(const TermParams &p, hipStream_t s) {
   hipError_t e = scan_u32_excl(p.doc_nuniq, p.row_off, p.n_docs, p.scratch, s);
   if (e != hipSuccess) return e;
+  if (!term_rows_path(p)) {
+    const uint32_t tiles = (uint32_t)((p.nnz + kRsTile - 1) / kRsTile);
+    if (!tiles) return hipGetLastError();
+    uint32_t *tile_doc = p.scratch + tile_doc_offset(p.n_docs, p.nnz, p.C);
+    hipLaunchKernelGGL(k_tile_docs, dim3((unsigned)((p.n_docs + 255) / 256)), dim3(256), 0, s, p.row_off, p.doc_nuniq,
+                       p.n_docs, tile_doc);
+    hipLaunchKernelGGL(k_term_pairs_tiled, dim3(tiles), dim3(256), 0, s, p, tile_doc, p.scratch);
+    return hipGetLastError();
+  }
   if (p.n_docs && p.nnz / p.n_docs > 2048) {                  // long rows: many workgroups per row
     const uint64_t avg = p.nnz / p.n_docs;
     const unsigned gy = (unsigned)std::min<uint64_t>((avg + 1023) / 1024, 64);
@@ -447,7 +526,8 @@ hipError_t launch_term_sort(const TermParams &p, hipStream_t s) {
       const uint32_t bits = p.slot_bits - lo < 8 ? p.slot_bits - lo : 8;
       const uint32_t shift = 64 - p.slot_bits + lo, mask = (1u << bits) - 1;
       const bool last = lo + 8 >= p.slot_bits;
-      hipLaunchKernelGGL(k_rs_hist, dim3(tiles), dim3(kRsThreads), 0, s, a, p.nnz, shift, mask, tiles, hist);
+      if (lo > 0 || term_rows_path(p))                          // (first digit: from k_term_pairs_tiled)
+        hipLaunchKernelGGL(k_rs_hist, dim3(tiles), dim3(kRsThreads), 0, s, a, p.nnz, shift, mask, tiles, hist);
       const uint32_t groups = (tiles + kColGroup - 1) / kColGroup;
       hipLaunchKernelGGL(k_col_sums, dim3(groups), dim3(256), 0, s, hist, tiles, sums);
       hipLaunchKernelGGL(k_col_bases, dim3(1), dim3(256), 0, s, sums, groups);
