@@ -58,6 +58,31 @@ def test_books_index_equals_oracle(books):
     g.close()
 
 
+@pytest.mark.parametrize("cap_log2,inversion", [(22, "auto"), (18, "block")])
+def test_books_many_groups_wide_dictionary(books, monkeypatch, cap_log2, inversion):
+    """The chunk path in many groups (TFIDF_TEST_PAIR_UNITS: ~15 books per
+    group instead of one group for all) and with bucketed pair lists of two
+    windows per bucket (2^22 dictionary slots: 64 buckets of 2^16 slots), or
+    with block-major CSR rows (8 dictionary ranges: range splits at window ends)."""
+    from tfidf_amd import _lib as L
+    texts, names, o, _ = books
+    monkeypatch.setenv("TFIDF_TEST_PAIR_UNITS", "5000")
+    inv = L.INVERSION_BLOCK if inversion == "block" else L.INVERSION_AUTO
+    g = ShardIndex(vocab_capacity_log2=cap_log2, inversion=inv)
+    g.add_documents(texts, names)
+    g.commit()
+    s = g.stats()
+    assert s["long_chunked"] == 300
+    assert (s["doc_count"], s["sum_ttf"], s["num_terms"], s["nnz"]) == \
+        (o.doc_count, o.sum_ttf, o.num_terms, sum(o.vocab().values()))
+    for d in (0, 14, 15, 16, 150, 299):                         # group edges (~15 books per group)
+        assert g.doc_terms(d) == o.doc_terms(d), d
+        assert g.doc_len(d) == (o.doc_len(d), o.doc_norm(d))
+    for q in synth.queries(8, lo=100, hi=10_000, seed=7) + [b"aaaa"]:
+        assert_hits_equal(g.search(q, 10), o.search(q, 10))
+    g.close()
+
+
 def test_books_leader_one_worker(books):
     """Leader + 1 worker (Leader.java:39-92 over Worker.java:57-94,222-241):
     the worker's JSON hits and the leader's name-ordered map equal the oracle."""

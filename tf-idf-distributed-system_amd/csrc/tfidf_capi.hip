@@ -888,7 +888,8 @@ static int commit_once(tfidf_index *ix) {
     const uint32_t wlog = std::min<uint32_t>(ix->cap_log2, kLrWinBits);
     const uint32_t bsh = std::max<uint32_t>(wlog, ix->cap_log2 > 6 ? ix->cap_log2 - 6 : 0);
     const uint32_t nb = 1u << (ix->cap_log2 - bsh);
-    const uint64_t unit_max = std::max<uint64_t>(1, kPairBudget / ((uint64_t)kPairWords * 4));
+    uint64_t unit_max = std::max<uint64_t>(1, kPairBudget / ((uint64_t)kPairWords * 4));
+    if (const char *e = getenv("TFIDF_TEST_PAIR_UNITS")) unit_max = std::max(1, atoi(e));   // tests: many groups
     // per group: the first unit (document, core) of each document, prefix form
     std::vector<uint32_t> pre;
     std::vector<uint64_t> gpre, gdoc;               // each group's prefix array offset and first document
