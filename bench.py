@@ -220,11 +220,11 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if dist_on:
-        backend = os.environ.get("TFIDF_BENCH_BACKEND", "nccl")   # nccl = RCCL over xGMI
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
+        # the process group only bootstraps (RCCL unique id, barriers, the
+        # max-over-ranks time); the data-path collectives are the library's
+        # own RCCL communicator (over xGMI), or with TFIDF_BENCH_BACKEND=gloo
+        # (ranks sharing a GPU in a rehearsal) the group's collectives as callbacks
+        dist.init_process_group("gloo")
 
     def barrier():
         if dist_on:
@@ -248,7 +248,11 @@ def main():
     idx = ShardIndex(device=local, vocab_capacity_log2=cap, inversion=inv,
                      stats_mode=STATS_GLOBAL if dist_on else 0)
     idx.add_documents_device(corpus.d_text, corpus.d_offsets, n_docs, corpus.total_bytes)
-    adapter = D.HipShardAdapter(idx, dev, doc_base=doc_base) if dist_on else None
+    adapter = None
+    if dist_on:
+        transport = "callback" if os.environ.get("TFIDF_BENCH_BACKEND", "rccl") == "gloo" else "rccl"
+        comm = D.Comm.from_group(device=local, transport=transport)
+        adapter = D.DistShard(idx, comm, doc_base=doc_base)
 
     exch = [0.0]
 
@@ -256,9 +260,10 @@ def main():
         idx.commit()                     # returns with the build complete (its stream synced)
         if dist_on:
             # GLOBAL statistics: term-ownership all-to-alls + stats all-gather
-            # (timed on the host: the commit is already complete here)
+            # (libtfidf tfidf_dist_global_commit; timed on the host: the commit
+            # is already complete here)
             t1 = time.perf_counter()
-            D.global_commit(adapter)
+            adapter.global_commit()
             torch.cuda.synchronize()
             exch[0] += time.perf_counter() - t1
 
@@ -279,7 +284,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if dist_on:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        e = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     for k in phases:
@@ -449,14 +454,14 @@ def main():
     elif not args.no_queries:
         # node-level queries over the sharded corpus with GLOBAL statistics:
         # each rank scores every query on its shard, per-rank top-k keys are
-        # all-gathered over RCCL and merged on device (distributed.py)
+        # all-gathered over RCCL and merged on device (tfidf_dist_search_batch)
         bq = synth.queries(args.batch_queries)
-        D.global_search_batch(adapter, bq[:100], 10)
+        adapter.search_batch(bq[:100], 10)
         out = {}
         for k in (10, 100):
             barrier()
             t0 = time.perf_counter()
-            D.global_search_batch(adapter, bq, k)
+            adapter.search_batch(bq, k)
             barrier()
             out["batch%dk_top%d_qps" % (len(bq) // 1000, k)] = len(bq) / (time.perf_counter() - t0)
         qs = synth.queries(max(args.queries, 1) // 4 or 1)
@@ -464,7 +469,7 @@ def main():
         for q in qs:
             barrier()
             t1 = time.perf_counter()
-            D.global_search(adapter, q, 100)
+            adapter.search_arrays(q, 100)
             lat.append(time.perf_counter() - t1)
         out["single_top100_p50_ms"] = float(np.percentile(lat, 50)) * 1e3
         out["single_top100_qps"] = 1.0 / float(np.mean(lat))
@@ -496,11 +501,13 @@ def main():
     if rank == 0 and not dist_on and args.cpu_sample > 0:
         result["cpu_baseline"] = cpu_baseline(corpus, args, args.cpu_sample)
     corpus.free()
-    idx.close()
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist_on:
+        dist.barrier()
+        comm.close()
         dist.destroy_process_group()
+    idx.close()
 
 
 if __name__ == "__main__":

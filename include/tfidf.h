@@ -27,6 +27,9 @@
  *       reference's 1-worker semantics, Leader.java:39-92 with one worker)
  *   tfidf_leader_merge
  *       me/zookeeper/leader_election/leader/Leader.java:73-88 (sum per name, TreeMap order)
+ *   tfidf_node_* / tfidf_dist_* / tfidf_comm_*
+ *       Leader.java:39-92 start (fan-out :51-70 over Worker.java:222-241, merge :73-88)
+ *       with the workers as GPU shards and RCCL collectives in place of HTTP
  *
  * Conventions: every call returns an int status (TFIDF_OK == 0); the message
  * of the last failure on the calling thread is tfidf_last_error().  Buffers
@@ -304,6 +307,157 @@ int tfidf_leader_merge(const uint8_t *names, const uint64_t *offsets, uint64_t n
 /* Stable permutation of n UTF-8 names in String.compareTo (UTF-16) order (the
  * TreeMap order of Leader.java:80-88; the multi-GPU name table). */
 int tfidf_sort_names(const uint8_t *names, const uint64_t *offsets, uint64_t n, uint64_t *perm);
+
+/* ==========================================================================
+ * Node level: documents sharded over GPUs, one shard (tfidf_index) per GPU.
+ *
+ * Replaces the reference's fan-out + merge, Leader.java:39-92 (POST
+ * {worker}/worker/process to every registered worker, :51-70; merge by name,
+ * :73-88) over each worker's Worker.java:222-241 searchIndex, with
+ * collectives between the shards (RCCL over xGMI on one MI355X node):
+ *   GLOBAL statistics (cfg.stats_mode TFIDF_STATS_GLOBAL: the reference's
+ *     1-worker results on a sharded corpus): per commit, each term's (key, df)
+ *     records go to an owner rank (all-to-all), the owner sums df and answers
+ *     (all-to-all back); docCount / sumTotalTermFreq summed; per query, every
+ *     shard's top-k as merge keys, all-gathered and merged on the device.
+ *     Global doc id = shard base + local id (contiguous shards): (score desc,
+ *     doc asc) is the single-index order.  At most 2^32 documents per node.
+ *   SHARD statistics (TFIDF_STATS_SHARD: the reference's N-worker results):
+ *     every shard scores with its own statistics and returns ALL its hits;
+ *     the hits are summed per document name in double in rank (= worker
+ *     response) order (HashMap.merge Double::sum, Leader.java:73-77) and
+ *     ordered by String.compareTo (TreeMap, :80-88).
+ *
+ * Two process models, one orchestration (the code below the ABI is the same):
+ *   (1) tfidf_node: ONE process owns every GPU of a device list (SURVEY §8b:
+ *       "one JVM owns all 8 GPUs"); one host thread per shard; collectives
+ *       over an RCCL communicator of the devices (ncclCommInitAll), or an
+ *       in-process host transport when a device repeats (tests) or
+ *       TFIDF_NODE_INPROC is asked for.
+ *   (2) SPMD, one process per GPU: each rank creates its own tfidf_index and a
+ *       tfidf_comm (built-in RCCL from a unique id the caller broadcasts, or
+ *       the caller's own collectives through tfidf_collectives), and calls the
+ *       tfidf_dist_* functions collectively (every rank, same order).
+ * ========================================================================== */
+typedef struct tfidf_comm tfidf_comm;
+typedef struct tfidf_node tfidf_node;
+
+#define TFIDF_COLL_HOST 0    /* collective buffers are host memory (gloo / MPI / sockets ...) */
+#define TFIDF_COLL_DEVICE 1  /* device memory of the rank's GPU, ordered on `stream` (a hipStream_t) */
+
+/* Caller-supplied collectives (the transport of process model (2) when the
+ * built-in RCCL communicator is not used).  Each returns 0 on success.
+ *   all_gather   : recv[r * bytes .. (r + 1) * bytes) = rank r's send, bytes each
+ *   all_to_all_v : send_bytes[r] bytes at send + send_offs[r] go to rank r;
+ *                  recv_bytes[r] bytes from rank r land at recv + recv_offs[r]
+ * Buffers may be NULL when their byte counts are 0.  With TFIDF_COLL_DEVICE the
+ * call may be asynchronous on `stream`; with TFIDF_COLL_HOST it must be complete
+ * on return. */
+typedef struct tfidf_collectives {
+  void *ctx;
+  int32_t memory;              /* TFIDF_COLL_HOST or TFIDF_COLL_DEVICE */
+  int (*all_gather)(void *ctx, const void *send, void *recv, uint64_t bytes, void *stream);
+  int (*all_to_all_v)(void *ctx, const void *send, const uint64_t *send_bytes, const uint64_t *send_offs,
+                      void *recv, const uint64_t *recv_bytes, const uint64_t *recv_offs, void *stream);
+} tfidf_collectives;
+
+/* A communicator over the caller's collectives (the table is copied). */
+int tfidf_comm_create(int32_t rank, int32_t world, const tfidf_collectives *coll, tfidf_comm **out);
+/* Built-in RCCL communicator (librccl of the HIP runtime the library runs on,
+ * loaded at first use): rank 0 calls tfidf_rccl_unique_id, the caller sends the
+ * 128 bytes to every rank (its own channel), then every rank calls
+ * tfidf_comm_init_rccl with its rank and GPU (collective). */
+int tfidf_rccl_unique_id(uint8_t id[128]);
+int tfidf_comm_init_rccl(const uint8_t id[128], int32_t rank, int32_t world, int32_t device, tfidf_comm **out);
+/* `world` communicators of one process sharing an in-process host transport
+ * (comms[0 .. world-1], rank i = comms[i]); each rank's calls run on its own
+ * thread.  The transport tfidf_node uses when shards share a device. */
+int tfidf_comm_create_inproc(int32_t world, tfidf_comm **comms);
+int tfidf_comm_destroy(tfidf_comm *c);
+int tfidf_comm_info(const tfidf_comm *c, int32_t *rank, int32_t *world, int32_t *transport);
+#define TFIDF_TRANSPORT_CALLBACK 0
+#define TFIDF_TRANSPORT_RCCL 1
+#define TFIDF_TRANSPORT_INPROC 2
+/* Transport check (no index needed): an all-gather of each rank's id and an
+ * all-to-all-v of rank-tagged bytes through the communicator, verified on
+ * every rank.  Collective. */
+int tfidf_comm_selftest(tfidf_comm *c);
+
+/* ---- process model (2): per-rank calls, collective over the communicator ----
+ * Every rank calls each of them, in the same order, after its own
+ * tfidf_commit; a rank whose index is not committed still takes part, and then
+ * every rank returns TFIDF_E_STATE together.  A query that does not parse
+ * (TFIDF_E_QUERY_SYNTAX / _UNSUPPORTED_QUERY) fails on every rank alike before
+ * any collective (the reference's Worker answers [] and its Leader merges
+ * nothing, Worker.java:182-185).
+ *
+ * tfidf_dist_global_commit: GLOBAL statistics (term ownership); the shards
+ *   whose commits hashed long / non-ASCII terms with different seeds first agree
+ *   on the highest attempt (the others re-commit under it).  Outputs may be
+ *   NULL (n_vocab = distinct terms over all shards: one more collective).
+ * tfidf_dist_search: k >= 1 top-k, or k == 0 every hit, with global doc ids
+ *   (doc_base = this shard's first global id); *n_out = hits; TFIDF_E_BUFFER if
+ *   they exceed cap (the first cap are written; the whole list stays readable
+ *   through tfidf_dist_last_hits, no collective).
+ * tfidf_dist_search_batch: n_q queries, 1 <= k <= 1024, outputs n_q x k.
+ * tfidf_dist_shard_commit: SHARD mode name table (every rank's document keys,
+ *   sorted by String.compareTo, de-duplicated); *n_names may be NULL.
+ * tfidf_dist_shard_search: Leader.start over the ranks: *n_out distinct names,
+ *   *n_bytes of name text; read them with tfidf_dist_last_names. */
+int tfidf_dist_global_commit(tfidf_index *ix, tfidf_comm *c, uint64_t *n_vocab, uint64_t *doc_count,
+                             uint64_t *sum_ttf);
+int tfidf_dist_search(tfidf_index *ix, tfidf_comm *c, uint64_t doc_base, const uint8_t *q, uint64_t q_len,
+                      uint32_t k, uint64_t *doc_ids, float *scores, uint64_t cap, uint64_t *n_out);
+int tfidf_dist_search_batch(tfidf_index *ix, tfidf_comm *c, uint64_t doc_base, const uint8_t *q_utf8,
+                            const uint64_t *q_offsets, uint32_t n_q, uint32_t k, uint64_t *doc_ids, float *scores,
+                            uint32_t *counts);
+int tfidf_dist_shard_commit(tfidf_index *ix, tfidf_comm *c, uint64_t *n_names);
+int tfidf_dist_shard_search(tfidf_index *ix, tfidf_comm *c, const uint8_t *q, uint64_t q_len, uint64_t *n_out,
+                            uint64_t *n_bytes);
+/* Results of the communicator's last search (local copies, no collective). */
+int tfidf_dist_last_hits(const tfidf_comm *c, uint64_t *doc_ids, float *scores, uint64_t cap, uint64_t *n_out);
+/* names concatenated into buf (cap bytes), offsets[n + 1], scores[n] (double sums) */
+int tfidf_dist_last_names(const tfidf_comm *c, uint8_t *buf, uint64_t cap, uint64_t *offsets, double *scores,
+                          uint64_t n_cap, uint64_t *n_out, uint64_t *n_bytes);
+
+/* ---- process model (1): one process, one shard per GPU of a device list ----
+ * cfg applies to every shard (cfg->device is ignored; cfg->stats_mode selects
+ * GLOBAL or SHARD results).  tfidf_node_create: the devices of device_mask (bit
+ * i = HIP device i).  tfidf_node_create_devices: an explicit list (a repeated
+ * device forces the in-process transport). */
+#define TFIDF_NODE_INPROC 1u   /* flags: in-process host transport instead of RCCL */
+int tfidf_node_create(const tfidf_config *cfg, uint64_t device_mask, tfidf_node **out);
+int tfidf_node_create_devices(const tfidf_config *cfg, const int32_t *devices, uint32_t n_devices, uint32_t flags,
+                              tfidf_node **out);
+int tfidf_node_destroy(tfidf_node *n);
+/* shard i's index (owned by the node): per-shard calls such as tfidf_add_docs_device */
+int tfidf_node_shard(tfidf_node *n, uint32_t i, tfidf_index **ix, uint32_t *n_shards);
+/* Documents go to one shard (shard >= 0: the caller routes, as Leader.upload
+ * picks a worker, Leader.java:153-207) or are split contiguously over the shards
+ * (shard == -1).  Replace-by-key applies within a shard. */
+int tfidf_node_add_docs(tfidf_node *n, int32_t shard, const uint8_t *utf8, const uint64_t *offsets, uint64_t n_docs,
+                        const uint8_t *keys, const uint64_t *key_offsets);
+/* Commits every shard (in parallel), then GLOBAL statistics or the SHARD name table. */
+int tfidf_node_commit(tfidf_node *n);
+/* GLOBAL mode; same results as tfidf_dist_search / _batch (global doc ids). */
+int tfidf_node_search(tfidf_node *n, const uint8_t *q, uint64_t q_len, uint32_t k, uint64_t *doc_ids, float *scores,
+                      uint64_t cap, uint64_t *n_out);
+int tfidf_node_search_batch(tfidf_node *n, const uint8_t *q_utf8, const uint64_t *q_offsets, uint32_t n_q, uint32_t k,
+                            uint64_t *doc_ids, float *scores, uint32_t *counts);
+/* SHARD mode (Leader.start): name-ordered {name: double} of the merged hits. */
+int tfidf_node_search_names(tfidf_node *n, const uint8_t *q, uint64_t q_len, uint8_t *buf, uint64_t cap,
+                            uint64_t *offsets, double *scores, uint64_t n_cap, uint64_t *n_out, uint64_t *n_bytes);
+/* Global doc id -> its document key (Worker.java:235-236, across shards). */
+int tfidf_node_doc_key(tfidf_node *n, uint64_t doc, uint8_t *buf, uint64_t cap, uint64_t *n_out);
+typedef struct tfidf_node_stats {
+  uint64_t n_shards;
+  uint64_t num_docs;      /* all shards */
+  uint64_t doc_count;     /* node statistics in force (GLOBAL: exchanged; SHARD: sum of the shards') */
+  uint64_t sum_ttf;
+  uint64_t num_terms;     /* distinct terms over all shards (GLOBAL mode), else 0 */
+  uint64_t transport;     /* TFIDF_TRANSPORT_RCCL or _INPROC */
+} tfidf_node_stats;
+int tfidf_node_stats_get(const tfidf_node *n, tfidf_node_stats *out);
 
 /* ---- synthetic corpus (bench/test input generator, device side) ----
  * Zipf(s) over V ranks, rank r -> bijective base-26 word of

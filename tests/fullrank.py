@@ -9,8 +9,9 @@ World 8 over gloo, every rank's ShardIndex on cuda:0 (RCCL needs one GPU per
 rank; the 8-GPU RCCL run is the driver's).  Rank r generates documents
 [r N/8, (r+1) N/8) of the global synthetic corpus in HBM (DeviceCorpus,
 doc_base) and indexes them; the ranks exchange statistics with the production
-code (distributed.global_commit) and answer queries with it
-(global_search / global_search_batch).  Checks, none of which use an oracle
+code (the library's tfidf_dist_global_commit, through distributed.DistShard
+over a callback communicator on the gloo group) and answer queries with it
+(tfidf_dist_search / tfidf_dist_search_batch).  Checks, none of which use an oracle
 index of the whole corpus (it would not finish in a test):
 
 * every shard's df of its WHOLE vocabulary = an independent torch count of its
@@ -24,7 +25,11 @@ index of the whole corpus (it would not finish in a test):
   oracle's Lucene arithmetic (oracle.idf / avgdl / norm_cache / bm25) from the
   global statistics and the hit's TF row; the merged list = the top-100 of the
   union of the shards' own top-100 lists; one-term all-hits counts = global df;
-* the 10 k-query batch merged over the shards = per-query global_search.
+* completeness: the merged top-100 of multi-term queries = the top-100 of
+  every document of the node that holds a query term, each scored from the
+  corpus bytes alone (span keys -> tf, generator lengths -> norms) with the
+  independent global statistics (test_gpu_fullsize.independent_topk);
+* the 10 k-query batch merged over the shards = per-query searches.
 
 Every rank records failed checks instead of raising (a raising rank would
 leave the others in a collective); rank files are asserted by the parent.
@@ -42,7 +47,7 @@ from tfidf_amd import distributed as D
 from tfidf_amd import synth
 from tfidf_amd.engine import ShardIndex
 
-from test_gpu_fullsize import f32bits, independent_df
+from test_gpu_fullsize import f32bits, independent_df, independent_topk, span_keys, term_lo
 
 K1, B = 1.2, 0.75
 
@@ -66,6 +71,19 @@ def doc_lengths_range(base, n, len_min, len_max, seed=synth.SEED):
     d = np.arange(base, base + n, dtype=np.uint64)
     h = synth._mix64(s2 ^ ((d << np.uint64(20)) | np.uint64(0xFFFFF)))
     return len_min + (h % np.uint64(len_max - len_min + 1)).astype(np.int64)
+
+
+def _gather_var(a):
+    """1-D int64 numpy arrays of every rank, concatenated in rank order (gloo)."""
+    n = torch.tensor([len(a)], dtype=torch.int64)
+    ns = [torch.zeros(1, dtype=torch.int64) for _ in range(dist.get_world_size())]
+    dist.all_gather(ns, n)
+    m = max(int(x.item()) for x in ns)
+    pad = torch.zeros(max(m, 1), dtype=torch.int64)
+    pad[:len(a)] = torch.from_numpy(np.ascontiguousarray(a, np.int64))
+    parts = [torch.zeros(max(m, 1), dtype=torch.int64) for _ in ns]
+    dist.all_gather(parts, pad)
+    return np.concatenate([p[:int(k.item())].numpy() for p, k in zip(parts, ns)])
 
 
 def _gather_obj(x, world):
@@ -100,8 +118,9 @@ def run(rank, world, port, cfg, out_path, concurrent_counts=2):
     g.commit()
     st = g.stats()
     info.update(nnz=st["nnz"], terms=st["num_terms"], term_major=st["term_major"])
-    ad = D.HipShardAdapter(g, torch.device("cuda", 0), doc_base=base)
-    n_vocab, gdc, gttf = D.global_commit(ad, vocab_size=True)
+    comm = D.Comm.from_group(transport="callback")
+    ad = D.DistShard(g, comm, doc_base=base)
+    n_vocab, gdc, gttf = ad.global_commit(vocab_size=True)
     torch.cuda.synchronize()
     progress("built and exchanged: %d docs, %d terms locally, %d globally" % (n, st["num_terms"], n_vocab))
 
@@ -126,10 +145,10 @@ def run(rank, world, port, cfg, out_path, concurrent_counts=2):
     ind_lo = np.fromiter(ind.keys(), np.int64, len(ind))
     ind_df = np.fromiter(ind.values(), np.int64, len(ind))
     del ind
-    glo, _ = D._all_gather_var(torch.from_numpy(ind_lo), len(ind_lo), None)
-    gdf, _ = D._all_gather_var(torch.from_numpy(ind_df), len(ind_df), None)
-    uk, inv = np.unique(glo.numpy(), return_inverse=True)
-    gsum = np.bincount(inv, weights=gdf.numpy()).astype(np.int64)
+    glo = _gather_var(ind_lo)
+    gdf = _gather_var(ind_df)
+    uk, inv = np.unique(glo, return_inverse=True)
+    gsum = np.bincount(inv, weights=gdf).astype(np.int64)
     del glo, gdf, inv
     check(n_vocab == len(uk), "global vocabulary %d != %d distinct terms over the shards" % (n_vocab, len(uk)))
     pos = np.searchsorted(uk, lo)
@@ -138,6 +157,34 @@ def run(rank, world, port, cfg, out_path, concurrent_counts=2):
     check(bad.size == 0, "%d terms' GLOBAL df != sum of independent shard counts" % bad.size)
     info["global_vocab"] = int(len(uk))
     progress("statistics checked")
+
+    # ---- completeness: the merged top-100 = the top-100 of EVERY document of
+    # the node holding a query term, scored from the corpus bytes alone with
+    # the independent GLOBAL statistics (each rank scores its own documents;
+    # the candidates meet on the host) — no engine kernel involved
+    def gdf_of(term):
+        kk = term_lo(term)
+        i = int(np.searchsorted(uk, kk))
+        return int(gsum[i]) if i < len(uk) and uk[i] == kk else 0
+
+    qs_c = c["queries"]()[:8]
+    cand = None
+    for turn in range(0, world, concurrent_counts):
+        if turn <= rank < turn + concurrent_counts:
+            key, dk = span_keys(dc, n)
+            cand = independent_topk(key, dk, n, base, qs_c, TOPK, gdf_of, n_total, int(tot.item()), lens)
+            del key, dk
+            torch.cuda.empty_cache()
+        dist.barrier()
+    allc = _gather_obj(cand, world)
+    for qi, q in enumerate(qs_c):
+        union = sorted([x for part in allc for x in part[qi]], key=lambda x: (-x[1], x[0]))[:TOPK]
+        hits = ad.search(q, TOPK)
+        check([d for d, _ in hits] == [d for d, _ in union], "query %r: merged top-%d misses documents" % (q, TOPK))
+        check([f32bits(x) for _, x in hits] == [f32bits(x) for _, x in union],
+              "query %r: merged top-%d scores != independent" % (q, TOPK))
+    del allc, cand
+    progress("completeness checked")
 
     # ---- top-100 over the shards -----------------------------------------
     cache = O.norm_cache(K1, B, O.avgdl(gttf, gdc))
@@ -159,7 +206,7 @@ def run(rank, world, port, cfg, out_path, concurrent_counts=2):
     qs = c["queries"]()
     n_checked = 0
     for q in qs:
-        hits = D.global_search(ad, q, TOPK)
+        hits = ad.search(q, TOPK)
         check(len(hits) == TOPK, "query %r: %d hits" % (q, len(hits)))
         ks = [(-s, d) for d, s in hits]
         check(ks == sorted(ks), "query %r: not (score desc, doc asc)" % q)
@@ -177,17 +224,17 @@ def run(rank, world, port, cfg, out_path, concurrent_counts=2):
     progress("top-%d checked" % TOPK)
     for q in qs[:3]:                                     # one term, every hit: exactly the global df
         t = q.split(b" ")[0]
-        allh = D.global_search(ad, t, 0)
+        allh = ad.search(t, 0)
         check(len(allh) == df_global(t) or df_global(t) == 0, "all hits of %r: %d" % (t, len(allh)))
         ks = [(-s, d) for d, s in allh]
         check(ks == sorted(ks), "all hits of %r: order" % t)
 
     # ---- cfg 4 on the shards: the batch merged once = per-query searches ---
     bq = c["batch"]()
-    bd, bs, bc = D.global_search_batch(ad, bq, 10)
+    bd, bs, bc = ad.search_batch(bq, 10)
     step = max(1, len(bq) // 150)
     for i in range(0, len(bq), step):
-        one = D.global_search(ad, bq[i], 10)
+        one = ad.search(bq[i], 10)
         got = list(zip(bd[i, :bc[i]].tolist(), bs[i, :bc[i]].tolist()))
         check(got == one, "batch query %d != global_search" % i)
     info["batch_queries"] = len(bq)
@@ -196,6 +243,7 @@ def run(rank, world, port, cfg, out_path, concurrent_counts=2):
     with open("%s.%d" % (out_path, rank), "w") as f:
         json.dump({"errors": errors, "info": info}, f)
     dist.barrier()
+    comm.close()
     dist.destroy_process_group()
     g.close()
     dc.free()

@@ -1,16 +1,20 @@
-"""World-size-2 (and 3) CPU rehearsal of the multi-GPU orchestration in
-tfidf_amd/distributed.py over the gloo backend.  The per-rank engine is the
-CPU oracle behind the same adapter interface HipShardAdapter implements
-(tests/multirank.py); the orchestration code under test is the production
-code: GLOBAL statistics by term ownership and by the canonical union, top-k,
-all-hits and batched merges, and SHARD mode (every worker's hits summed by
-document name in rank order, ordered by name — Leader.java:39-92).
+"""CPU tests of the node-level transports (csrc/tfidf_dist.hip, include/tfidf.h
+"Node level"), no GPU needed: the orchestration's collectives go through a
+tfidf_comm, and these check each transport end to end through the library.
 
-GLOBAL mode over G shards must equal the single-index (1-worker) result;
-SHARD mode must equal per-worker oracles + the oracle's Leader merge.
-(test_gpu_multirank.py runs the same rank body over the HIP engine.)
+* callback transport over a torch.distributed gloo group (world 2 and 3, one
+  process per rank): the library calls the group's all_gather /
+  all_to_all_single on host buffers through ctypes callbacks — the path the
+  GPU multi-rank tests (ranks sharing one GPU) and a Java host with its own
+  collectives take;
+* in-process transport (world 1..5, one thread per rank): the transport
+  tfidf_node uses for shards that share a device.
+
+The orchestration itself over real shards (GLOBAL / SHARD results against the
+oracle, hash-seed agreement) needs indices, i.e. a GPU: test_gpu_multirank.py,
+test_gpu_node.py, test_gpu_fullsize_multirank.py.
 """
-import json
+import threading
 
 import pytest
 import torch.multiprocessing as mp
@@ -18,19 +22,60 @@ import torch.multiprocessing as mp
 import multirank as M
 
 
+def _rank_selftest(rank, world, port):
+    import os
+    import torch.distributed as dist
+    from tfidf_amd.distributed import Comm
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    c = Comm.from_group(transport="callback")
+    assert c.info() == (rank, world, "callback")
+    for _ in range(3):
+        c.selftest()
+    c.close()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
 @pytest.mark.parametrize("world", [2, 3])
-def test_distributed_modes_equal_oracle(tmp_path, world):
-    out = str(tmp_path / "r.json")
-    mp.spawn(M.run_rank, args=(world, M.free_port(), "oracle", out), nprocs=world, join=True)
-    M.check(json.load(open(out)), world)
+def test_callback_transport_gloo(world):
+    mp.spawn(_rank_selftest, args=(world, M.free_port()), nprocs=world, join=True)
 
 
-def test_hash_seed_agreement(tmp_path):
-    """Shards that hashed with different seeds agree on the highest: the others
-    re-commit under it (and agree again when that seed collides there)."""
-    out = str(tmp_path / "s.json")
-    mp.spawn(M.run_rank_seed, args=(3, M.free_port(), "oracle", out), nprocs=3, join=True)
-    res = M.check_seed(out, 3)
-    assert [r["before"] for r in res] == [0, 1, 0]
-    assert [r["after"] for r in res] == [2, 2, 2]
-    assert [r["recommits"] for r in res] == [[1, 2], [2], [1]]
+@pytest.mark.parametrize("world", [1, 2, 3, 5])
+def test_inproc_transport_threads(world):
+    from tfidf_amd.distributed import Comm
+    comms = Comm.inproc(world)
+    errs = [None] * world
+
+    def run(i):
+        try:
+            assert comms[i].info() == (i, world, "inproc")
+            for _ in range(4):
+                comms[i].selftest()
+        except Exception as e:          # surfaced by the assert below
+            errs[i] = e
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=60)
+    assert not any(t.is_alive() for t in th)
+    assert errs == [None] * world
+    for c in comms:
+        c.close()
+
+
+def test_comm_arguments_rejected():
+    import ctypes as C
+    from tfidf_amd import _lib as L
+    from tfidf_amd.distributed import AG_FN, A2A_FN, Collectives
+    lib = L.load()
+    h = C.c_void_p()
+    coll = Collectives(None, 0, AG_FN(lambda *a: 0), A2A_FN(lambda *a: 0))
+    assert lib.tfidf_comm_create(2, 2, C.byref(coll), C.byref(h)) == L.E_INVALID_ARG     # rank >= world
+    coll.memory = 7
+    assert lib.tfidf_comm_create(0, 2, C.byref(coll), C.byref(h)) == L.E_INVALID_ARG     # unknown memory kind
+    assert lib.tfidf_comm_create_inproc(0, (C.c_void_p * 1)()) == L.E_INVALID_ARG

@@ -59,9 +59,11 @@ def expected_score(g, st, q_terms, d, cache):
     return float(np.float32(acc))
 
 
-def independent_df(dc, n):
-    """{term key lo: df} of the synthetic corpus (lower-case ASCII words of
-    <= 8 bytes separated by ' ' / '\\n'), counted with torch ops on cuda:0."""
+def span_keys(dc, n):
+    """(key int64[spans], doc int64[spans]) on cuda:0: every word of the
+    synthetic corpus (lower-case ASCII words of <= 8 bytes separated by ' ' /
+    '\n') as its little-endian byte key, and its document — plain torch ops
+    over the host copy of the corpus bytes, none of the engine's kernels."""
     import torch
     text, offs = dc.to_host(n)
     t = torch.from_numpy(text).cuda()
@@ -97,7 +99,13 @@ def independent_df(dc, n):
         key |= torch.where(ln > j, b, torch.zeros_like(b)) << (8 * j)
     del ln, t
     doc = torch.searchsorted(o[1:].contiguous(), starts, right=True)
-    del starts
+    return key, doc
+
+
+def independent_df(dc, n):
+    """{term key lo: df} of the synthetic corpus, counted with torch ops on cuda:0."""
+    import torch
+    key, doc = span_keys(dc, n)
     bits = max(1, (n - 1).bit_length())
     assert int(key.max()).bit_length() + bits <= 63
     pairs = torch.unique((key << bits) | doc)
@@ -106,6 +114,55 @@ def independent_df(dc, n):
     out = dict(zip(terms.cpu().numpy().tolist(), df.cpu().numpy().tolist()))
     del pairs, terms, df
     torch.cuda.empty_cache()
+    return out
+
+
+def term_lo(term: bytes):
+    return int.from_bytes(term.ljust(8, b"\0"), "little")
+
+
+def bm25_vec(w, tf, cache_at_norm):
+    """Lucene BM25Scorer.score, vectorised in IEEE float32 (Java op order, no
+    FMA): w - w / (1f + (float) tf * cache[norm])."""
+    w = np.float32(w)
+    tf = tf.astype(np.float32)
+    return w - w / (np.float32(1.0) + tf * cache_at_norm)
+
+
+def independent_topk(key, doc, n, doc_base, queries, k, df_of, doc_count, sum_ttf, lens):
+    """Completeness check: every document of [doc_base, doc_base + n) that
+    holds a query term, scored from the corpus bytes alone (span keys -> tf per
+    document; norm byte from the generator's length; BM25 in float32, the
+    disjunction summed in double) with the given statistics (df_of(term) /
+    docCount / sumTTF), ranked (score desc, doc asc) -> its top k as [(global
+    doc, float score)] per query.  No engine kernel is involved."""
+    import torch
+    from oracle import oracle as O
+    cache = O.norm_cache(K1, B, O.avgdl(sum_ttf, doc_count))
+    norms = np.array([O.int_to_byte4(int(x)) for x in range(int(lens.max()) + 1)], np.int64)[lens]
+    cnorm = cache[norms]
+    out = []
+    for q in queries:
+        terms = list(dict.fromkeys(q.split(b" ")))
+        acc = np.zeros(n, np.float64)
+        hit = np.zeros(n, bool)
+        for t in terms:
+            m = key == term_lo(t)
+            tf = torch.bincount(doc[m], minlength=n).cpu().numpy()
+            if not tf.any():
+                continue
+            w = O.idf(df_of(t), doc_count)
+            nz = np.nonzero(tf)[0]
+            s = bm25_vec(w, tf[nz], cnorm[nz])
+            # vectorised arithmetic = the oracle's scalar Lucene arithmetic
+            for j in nz[:: max(1, len(nz) // 5)][:5]:
+                assert np.float32(O.bm25(w, int(tf[j]), float(cnorm[j]))) == s[np.searchsorted(nz, j)]
+            acc[nz] += s.astype(np.float64)
+            hit[nz] = True
+        d = np.nonzero(hit)[0]
+        sc = acc[d].astype(np.float32)
+        order = np.lexsort((d, -sc))[:k]
+        out.append([(int(d[i]) + doc_base, float(sc[i])) for i in order])
     return out
 
 
@@ -155,6 +212,19 @@ def check_corpus(g, dc, n, len_min, len_max, queries, rng):
             assert f32bits(s) == f32bits(expected_score(g, st, terms, d, cache)), (q, d)
         keys = [(-s, d) for d, s in hits]
         assert keys == sorted(keys)
+    # completeness: the engine's top-k of multi-term queries = the top-k of
+    # EVERY document holding a query term, scored from the corpus bytes alone
+    key, doc = span_keys(dc, n)
+    dfs = independent_df(dc, n)
+    cq = queries[:8]
+    want = independent_topk(key, doc, n, 0, cq, 100, lambda t: dfs[term_lo(t)], n, int(lens.sum()), lens)
+    del key, doc
+    for q, w in zip(cq, want):
+        got = g.search(q, 100)
+        assert [d for d, _ in got] == [d for d, _ in w], q
+        assert [f32bits(x) for _, x in got] == [f32bits(x) for _, x in w], q
+    import torch
+    torch.cuda.empty_cache()
     # one-term all-hits: exactly df hits, (score desc, doc asc), top-k = prefix
     for q in queries[:3]:
         t = q.split(b" ")[0]
@@ -200,5 +270,24 @@ def test_cfg5_shape_full_size_6m_short_docs():
     assert st["term_major"] == 1 and st["pack_docs"] > 1 and st["pack_retried"] < n // 1000
     qs = synth.queries(200, lo=100, hi=20_000) + synth.queries(40, lo=100_000, hi=4_000_000, seed=9)
     check_corpus(g, dc, n, 48, 80, qs, np.random.default_rng(5))
+    g.close()
+    dc.free()
+
+
+@pytest.mark.parametrize("n_gpus", [4, 2])
+def test_cfg5_shape_per_shard_sizes_at_2_and_4_gpus(n_gpus):
+    """BASELINE cfg 5 (50 M docs) split over 4 or 2 GPUs: the per-GPU shard
+    (12.5 M / 25 M docs x U[48, 80] tokens, V = 5 M, 2^23 slots) built on one
+    device and checked like the 8-GPU share — the per-GPU capacities a 2- or
+    4-GPU node needs (term-major layout, packed windows)."""
+    n = 50_000_000 // n_gpus
+    dc = synth.DeviceCorpus(n, V=5_000_000, len_min=48, len_max=80)
+    g = ShardIndex(vocab_capacity_log2=23)
+    g.add_documents_device(dc.d_text, dc.d_offsets, dc.n_docs, dc.total_bytes)
+    g.commit()
+    st = g.stats()
+    assert st["term_major"] == 1 and st["pack_docs"] > 1 and st["pack_retried"] < n // 1000
+    qs = synth.queries(60, lo=100, hi=20_000) + synth.queries(20, lo=100_000, hi=4_000_000, seed=9)
+    check_corpus(g, dc, n, 48, 80, qs, np.random.default_rng(7 + n_gpus))
     g.close()
     dc.free()

@@ -31,15 +31,21 @@ QUERIES = synth.queries(30, lo=1, hi=3000) + [b"tiedterm", b"tiedterm filler aaa
 OPS = [b"aaaa AND aaab", b"tiedterm NOT aaab", b"aaab OR aaac NOT aaaa", b"aaaa AND NOT"]
 
 
-@pytest.mark.parametrize("k", [1, 10, 64, 300])
+@pytest.mark.parametrize("k", [1, 10, 64, 300, 1024])
 def test_fused_equals_oracle(corpus, k):
+    """k <= 64 takes the fused launch; larger k the unfused path (run_scoring +
+    the device merge: the fused path's host merge of n_blocks x k candidates
+    grows with k) — both equal the oracle."""
     g, o = corpus
     f0 = g.stats()["fused_queries"]
     n = 0
     for q in QUERIES:
         assert_hits_equal(g.search(q, k), o.search(q, k))
         n += 1
-    assert g.stats()["fused_queries"] - f0 >= n - 2          # queries without a present term do not launch
+    if k <= 64:
+        assert g.stats()["fused_queries"] - f0 >= n - 2      # queries without a present term do not launch
+    else:
+        assert g.stats()["fused_queries"] == f0
 
 
 def test_fused_operator_queries(corpus):

@@ -1,10 +1,10 @@
-"""The multi-GPU orchestration over the REAL engine: world size 2 and 3,
-every rank a process with its own HipShardAdapter / ShardIndex on cuda:0,
-collectives over gloo (RCCL needs one GPU per rank; the 8-GPU RCCL run is the
-driver's).  Same rank body and checks as test_distributed_gloo.py
-(tests/multirank.py): GLOBAL term-ownership and canonical statistics, top-k /
-all-hits / batched merges with device merge keys, and SHARD mode's
-Leader-style merge by name — all against the CPU oracle.
+"""The node-level orchestration of libtfidf (tfidf_dist_*, process model (2):
+one process per rank) over the REAL engine: world size 2 and 3, every rank a
+process with its own ShardIndex on cuda:0, the library's collectives through a
+callback communicator on a gloo group (RCCL needs one GPU per rank; the 8-GPU
+RCCL run is the driver's).  GLOBAL term-ownership statistics, top-k /
+all-hits / batched merges of device merge keys, and SHARD mode's Leader-style
+merge by name — all against the CPU oracle (tests/multirank.py).
 """
 import json
 

@@ -1594,12 +1594,8 @@ hipError_t launch_hits_order(const uint64_t *hits, const uint32_t *hits_n, uint3
   if (getenv("TFIDF_HITS_PAIRWISE")) groups = false;
   if (getenv("TFIDF_HITS_GROUPS")) groups = true;
   if (groups) {                                                 // levels 0-2: one workgroup per 8 runs
-    static bool big = false;
-    if (!big) {
-      hipFuncSetAttribute((const void *)k_merge_group, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          2 * kGroupCap * 8);
-      big = true;
-    }
+    static std::atomic<uint64_t> big{0};
+    allow_dyn_lds((const void *)k_merge_group, 2 * kGroupCap * 8, big);
     mp.src = hits;
     mp.gapped = 1;
     mp.final = levels <= 3;

@@ -832,8 +832,16 @@ static int commit_once(tfidf_index *ix) {
   HIP_TRY(hipEventRecord(ix->ev[EV_START], s));
   if (N) {
     const uint64_t units = (N + pack - 1) / pack;
-    const uint64_t grid = std::min<uint64_t>(units, (uint64_t)ix->num_cus * kWaveWGsPerCU);
-    HIP_TRY(launch_tokenize_wave(bp, (int)grid, s));
+    // one document per 4-wave workgroup (k_tokenize_wg) for one-document
+    // windows; packed windows (short documents) keep the wave kernel.
+    // TFIDF_TOK_WG=1 selects it (A/B; the phase stops of TFIDF_DEBUG_STOP
+    // exist in the wave kernel only).
+    const bool wg = pack <= 1 && !bp.debug_stop && getenv("TFIDF_TOK_WG");
+    uint64_t wpc = wg ? kWgWGsPerCU : kWaveWGsPerCU;
+    if (const char *e = getenv("TFIDF_WAVE_WGS_PER_CU")) wpc = (uint64_t)std::max(1, atoi(e));   // profiling only
+    const uint64_t grid = std::min<uint64_t>(units, (uint64_t)ix->num_cus * wpc);
+    if (wg) HIP_TRY(launch_tokenize_wg(bp, (int)grid, s));
+    else HIP_TRY(launch_tokenize_wave(bp, (int)grid, s));
     if (pack > 1 && !bp.debug_stop) {       // documents the packs could not take: one per wave
       uint32_t n_retry = 0;
       HIP_TRY(hipMemcpyAsync(&n_retry, ctr + 5, 4, hipMemcpyDeviceToHost, s));
@@ -1533,7 +1541,12 @@ static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint
     memcpy(h + qoff.size() + 3 * ns, qb.meta.data(), qb.meta.size() * 4);
   }
   if (!units.empty()) memcpy(h + words0, units.data(), units.size() * 4);
-  HIP_TRY(ix->q_in.reserve(words * 4 + 16));
+  if (words * 4 + 16 > ix->q_in.bytes) {
+    // a pending chunk of a pipelined batch may still read q_in: finish it
+    // before the buffer is replaced (1.5x headroom, so later chunks rarely grow it)
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(ix->q_in.reserve(words * 6 + 16));
+  }
   HIP_TRY(hipMemcpyAsync(ix->q_in.p, h, words * 4, hipMemcpyHostToDevice, s));
   HIP_TRY(hipEventRecord(ix->q_in_ev, s));
   ix->q_in_pending = true;
@@ -1668,7 +1681,10 @@ extern "C" int tfidf_search(tfidf_index *ix, const uint8_t *q, uint64_t q_len, u
   if (rc) return rc;
   if (pq.slot.empty() || ix->n_docs == 0) { ix->last_ms_scoring = ix->last_ms_total = 0; return TFIDF_OK; }
   hipStream_t s = ix->stream;
-  if (k && pq.slot.size() <= kInlTerms && !getenv("TFIDF_NO_FUSED")) {
+  // fused path for k <= kFusedMaxK: each block workgroup writes its k
+  // candidates to pinned host memory over PCIe and the host merges n_blocks x k
+  // keys, a cost that grows with k (larger k: run_scoring + the device merge)
+  if (k && k <= kFusedMaxK && pq.slot.size() <= kInlTerms && !getenv("TFIDF_NO_FUSED")) {
     // one launch: query terms in the kernel arguments, block scoring with the
     // candidates written to pinned host memory, merged here
     HIP_TRY(ix->q_res.resize((size_t)2 * k + 1));
@@ -1801,8 +1817,10 @@ extern "C" int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const 
   // Pipelined in chunks: chunk c + 1 is prepared on the host (parse, analysis,
   // dictionary lookups, weights) while chunk c scores on the device; each
   // chunk's results are copied (stream-ordered) into its region of one pinned
-  // buffer.  The first chunk is the largest, so the device buffers sized by it
-  // are never re-allocated under a pending chunk.  TFIDF_BATCH_CHUNKS overrides.
+  // buffer.  Chunks are ceil-sized, so the first one is the largest and the
+  // buffers sized by the query count (cand, cand_n, q_out) are reserved by it;
+  // q_in (sized by each chunk's terms) grows with an explicit stream sync in
+  // run_scoring.  TFIDF_BATCH_CHUNKS overrides.
   // 10 k queries at cfg 2 (tools/gpu_batch_ab.sh): 1 chunk 7.6 ms end to end
   // (prepare 1.5 on the pool, device 5.65), 2 chunks 7.0 (device 6.05), 4
   // chunks 7.45 (device 6.9: every chunk pays the unit kernels' tail)
@@ -1816,8 +1834,8 @@ extern "C" int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const 
   bool any = false;
   uint32_t c0 = 0;
   for (uint32_t c = 0; c < n_chunks; c++) {
-    const uint32_t c1 = (uint32_t)((uint64_t)n_q * (c + 1) / n_chunks);
-    const uint32_t nc = c1 - c0;                         // non-increasing over c
+    const uint32_t c1 = (uint32_t)(((uint64_t)n_q * (c + 1) + n_chunks - 1) / n_chunks);
+    const uint32_t nc = c1 - c0;                         // the first chunk is the largest (ceil split)
     const auto ta = clk::now();
     QueryBatch qb;
     if (int e = prepare_batch(ix, q_utf8, q_offsets + c0, nc, &qb)) { ix->q_rec_start = true; return e; }
@@ -1843,7 +1861,7 @@ extern "C" int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const 
   const auto t3 = clk::now();
   c0 = 0;
   for (uint32_t c = 0; c < n_chunks; c++) {
-    const uint32_t c1 = (uint32_t)((uint64_t)n_q * (c + 1) / n_chunks), nc = c1 - c0;
+    const uint32_t c1 = (uint32_t)(((uint64_t)n_q * (c + 1) + n_chunks - 1) / n_chunks), nc = c1 - c0;
     const uint32_t *hres = ix->q_res.data() + (size_t)2 * c0 * k + c0;
     memcpy(doc_ids + (size_t)c0 * k, hres, (size_t)nc * k * 4);
     memcpy(scores + (size_t)c0 * k, hres + (size_t)nc * k, (size_t)nc * k * 4);
@@ -1879,6 +1897,7 @@ struct CoalesceReq {
   int rc;
   std::string err;
   bool done;
+  bool taken;        // in a batch a leader took (waits for that batch, never leads)
 };
 
 // One coalesced batch: queries that do not parse answer as tfidf_search
@@ -1925,15 +1944,17 @@ extern "C" int tfidf_search_coalesced(tfidf_index *ix, const uint8_t *q, uint64_
                                       float *scores, uint64_t cap, uint64_t *n_out, uint32_t wait_us) {
   if (!ix || (!q && q_len) || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
   if (k == 0 || k > 1024) return fail(TFIDF_E_INVALID_ARG, "coalesced search needs 1 <= k <= 1024 (all hits: tfidf_search)");
-  CoalesceReq r{q, q_len, k, doc_ids, scores, cap, n_out, TFIDF_OK, std::string(), false};
+  CoalesceReq r{q, q_len, k, doc_ids, scores, cap, n_out, TFIDF_OK, std::string(), false, false};
   std::unique_lock<std::mutex> lk(ix->cq_mu);
   ix->cq.push_back(&r);
   bool slept = false;
   for (;;) {
-    // served by a leader, or no batch is forming: lead one.  A leader whose own
-    // request did not fit its (capped) batch comes back here; requests left
-    // over after a capped batch are woken and one of their callers leads next.
-    ix->cq_cv.wait(lk, [&] { return r.done || !ix->cq_leader; });
+    // served by a leader, or not yet taken and no batch is forming: lead one.
+    // A request a running leader took waits for that leader (taking part in
+    // the next batch would run an empty one).  A leader whose own request did
+    // not fit its (capped) batch comes back here; requests left over after a
+    // capped batch are woken and one of their callers leads next.
+    ix->cq_cv.wait(lk, [&] { return r.done || (!r.taken && !ix->cq_leader); });
     if (r.done) break;
     ix->cq_leader = true;
     if (wait_us && !slept) {
@@ -1942,9 +1963,10 @@ extern "C" int tfidf_search_coalesced(tfidf_index *ix, const uint8_t *q, uint64_
       std::this_thread::sleep_for(std::chrono::microseconds(wait_us));
       lk.lock();
     }
-    const size_t take = std::min(ix->cq.size(), ix->cq_max);
+    const size_t take = std::min(ix->cq.size(), ix->cq_max);   // >= 1: r itself is queued
     std::vector<CoalesceReq *> batch(ix->cq.begin(), ix->cq.begin() + take);
     ix->cq.erase(ix->cq.begin(), ix->cq.begin() + take);
+    for (CoalesceReq *c : batch) c->taken = true;
     ix->cq_leader = false;                                // later arrivals lead the next batch
     if (!ix->cq.empty()) ix->cq_cv.notify_all();
     lk.unlock();
@@ -2462,7 +2484,7 @@ struct Utf16Units {                // UTF-8 bytes -> UTF-16 code units
   }
 };
 
-static int utf16_compare(const uint8_t *a, uint64_t na, const uint8_t *b, uint64_t nb) {
+int tfidf::utf16_compare(const uint8_t *a, uint64_t na, const uint8_t *b, uint64_t nb) {
   Utf16Units x{a, na}, y{b, nb};
   while (x.more() && y.more()) {
     const uint64_t i0 = x.i, j0 = y.i;
@@ -2582,3 +2604,12 @@ extern "C" int tfidf_device_copy(int device, void *dst, const void *src, uint64_
   if (bytes) HIP_TRY(hipMemcpy(dst, src, bytes, kind == 1 ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost));
   return TFIDF_OK;
 }
+
+// ---------------------------------------------------------------------------
+// internal accessors for the node-level orchestration (tfidf_dist.hip)
+
+hipStream_t tfidf::index_stream(tfidf_index *ix) { return ix->stream; }
+int tfidf::index_device(const tfidf_index *ix) { return ix->cfg.device; }
+bool tfidf::index_committed(const tfidf_index *ix) { return ix->committed; }
+uint64_t tfidf::index_num_docs(const tfidf_index *ix) { return ix->committed ? ix->n_docs : 0; }
+int tfidf::set_error(int code, const char *msg) { return fail(code, "%s", msg); }

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "tfidf_common.h"
 
 namespace tfidf {
@@ -207,8 +209,24 @@ struct PostingParams {
   uint32_t sort_spw;          // scatter pass 2: sub-range streams per workgroup
 };
 
+// Raise a kernel's dynamic-LDS limit on the current device, once per device:
+// the attribute applies to the device current at the call, so a process with
+// indices on several GPUs sets it on each (idempotent, so concurrent first
+// calls are harmless).
+inline void allow_dyn_lds(const void *fn, int bytes, std::atomic<uint64_t> &done_mask) {
+  int dev = 0;
+  hipGetDevice(&dev);
+  const uint64_t bit = 1ull << (dev & 63);
+  if (done_mask.load(std::memory_order_acquire) & bit) return;
+  hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  done_mask.fetch_or(bit, std::memory_order_acq_rel);
+}
+
 // --- launch wrappers (kernels_index.hip) ---
 hipError_t launch_tokenize_wave(const BuildParams &p, int grid, hipStream_t s);
+// one document per 256-thread workgroup (4 waves), ASCII one-document windows (pack 1)
+hipError_t launch_tokenize_wg(const BuildParams &p, int grid, hipStream_t s);
+constexpr uint32_t kWgWGsPerCU = 8;         // 256-thread workgroups per CU (~19.6 KB LDS each)
 constexpr uint32_t kWaveWGsPerCU = 8;       // 64-thread workgroups per CU (2 waves/SIMD: VGPR- and LDS-bound)
 constexpr uint32_t kWaveGroups = 128;     // CSR row groups per wave unit (documents x ranges, k_tokenize_wave)
 constexpr uint32_t kPackMaxDocs = 16;     // documents per packed window (<= kPackMax, kernels_index.hip)
@@ -278,6 +296,7 @@ hipError_t launch_term_sort(const TermParams &p, hipStream_t s);
 
 // --- query scoring (kernels_query.hip) ---
 constexpr uint32_t kInlTerms = 32;          // query terms carried in QueryParams (fused single query)
+constexpr uint32_t kFusedMaxK = 64;         // tfidf_search top-k through the fused single-query launch up to this k
 struct QueryParams {
   const uint64_t *post;       // term-major postings (toff != nullptr)
   const uint32_t *post32;     // block-major postings (post_word)
@@ -360,6 +379,25 @@ hipError_t vocab_scatter(const uint64_t *dict, const uint32_t *df, uint32_t C, u
 hipError_t vocab_reduce(const uint64_t *records, uint64_t n, uint64_t *table, uint32_t tmask, uint32_t *sums,
                         uint32_t *rslot, uint32_t *out, unsigned long long *n_unique, hipStream_t s);
 hipError_t vocab_import(const uint32_t *sent_slot, const uint32_t *gdf_in, uint64_t n, uint32_t *gdf, hipStream_t s);
+
+// --- index internals the node-level orchestration reads (tfidf_capi.hip) ---
+}  // namespace tfidf
+struct tfidf_index;
+namespace tfidf {
+hipStream_t index_stream(tfidf_index *ix);
+int index_device(const tfidf_index *ix);
+bool index_committed(const tfidf_index *ix);
+uint64_t index_num_docs(const tfidf_index *ix);
+int set_error(int code, const char *msg);       // sets tfidf_last_error() of the calling thread
+// String.compareTo order of two UTF-8 names (UTF-16 code units; Leader.java:80-88 TreeMap)
+int utf16_compare(const uint8_t *a, uint64_t na, const uint8_t *b, uint64_t nb);
+
+// --- node-level merges (tfidf_dist.hip) ---
+// lists (q, r) of `len` merge keys at keys + r * rstride + q * qstride, each
+// sorted descending (0 = empty, last): out[q * k_out + i] = the i-th largest
+// key of query q over all n_lists lists (i < k_out), 0 past the last one
+hipError_t launch_merge_lists(const uint64_t *keys, uint32_t n_lists, uint64_t rstride, uint64_t qstride, uint64_t len,
+                              uint32_t n_q, uint64_t *out, uint64_t k_out, hipStream_t s);
 
 // --- synthetic corpus (kernels_synth.hip) ---
 hipError_t synth_doc_lengths(uint64_t seed, uint64_t n_docs, uint64_t doc_base, const double *cdf,

@@ -123,6 +123,35 @@ SIGNATURES = {
     "tfidf_leader_merge": (C.c_int, [C.c_char_p, U64P, C.c_uint64, F64P, U64P, F64P, U64P]),
     "tfidf_synth_corpus": (C.c_int, [C.c_int, C.c_uint64, C.c_uint64, C.c_uint64, F64P, C.c_uint32, C.c_uint32,
                                      C.c_uint32, C.POINTER(VP), C.POINTER(VP), U64P]),
+    # node level (csrc/tfidf_dist.hip)
+    "tfidf_comm_create": (C.c_int, [C.c_int32, C.c_int32, VP, C.POINTER(VP)]),
+    "tfidf_rccl_unique_id": (C.c_int, [VP]),
+    "tfidf_comm_init_rccl": (C.c_int, [VP, C.c_int32, C.c_int32, C.c_int32, C.POINTER(VP)]),
+    "tfidf_comm_create_inproc": (C.c_int, [C.c_int32, C.POINTER(VP)]),
+    "tfidf_comm_destroy": (C.c_int, [VP]),
+    "tfidf_comm_info": (C.c_int, [VP, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
+    "tfidf_comm_selftest": (C.c_int, [VP]),
+    "tfidf_dist_global_commit": (C.c_int, [VP, VP, U64P, U64P, U64P]),
+    "tfidf_dist_search": (C.c_int, [VP, VP, C.c_uint64, C.c_char_p, C.c_uint64, C.c_uint32, U64P, F32P, C.c_uint64,
+                                    U64P]),
+    "tfidf_dist_search_batch": (C.c_int, [VP, VP, C.c_uint64, C.c_char_p, U64P, C.c_uint32, C.c_uint32, U64P, F32P,
+                                          U32P]),
+    "tfidf_dist_shard_commit": (C.c_int, [VP, VP, U64P]),
+    "tfidf_dist_shard_search": (C.c_int, [VP, VP, C.c_char_p, C.c_uint64, U64P, U64P]),
+    "tfidf_dist_last_hits": (C.c_int, [VP, U64P, F32P, C.c_uint64, U64P]),
+    "tfidf_dist_last_names": (C.c_int, [VP, C.c_char_p, C.c_uint64, U64P, F64P, C.c_uint64, U64P, U64P]),
+    "tfidf_node_create": (C.c_int, [VP, C.c_uint64, C.POINTER(VP)]),
+    "tfidf_node_create_devices": (C.c_int, [VP, C.POINTER(C.c_int32), C.c_uint32, C.c_uint32, C.POINTER(VP)]),
+    "tfidf_node_destroy": (C.c_int, [VP]),
+    "tfidf_node_shard": (C.c_int, [VP, C.c_uint32, C.POINTER(VP), U32P]),
+    "tfidf_node_add_docs": (C.c_int, [VP, C.c_int32, C.c_char_p, U64P, C.c_uint64, C.c_char_p, U64P]),
+    "tfidf_node_commit": (C.c_int, [VP]),
+    "tfidf_node_search": (C.c_int, [VP, C.c_char_p, C.c_uint64, C.c_uint32, U64P, F32P, C.c_uint64, U64P]),
+    "tfidf_node_search_batch": (C.c_int, [VP, C.c_char_p, U64P, C.c_uint32, C.c_uint32, U64P, F32P, U32P]),
+    "tfidf_node_search_names": (C.c_int, [VP, C.c_char_p, C.c_uint64, C.c_char_p, C.c_uint64, U64P, F64P,
+                                          C.c_uint64, U64P, U64P]),
+    "tfidf_node_doc_key": (C.c_int, [VP, C.c_uint64, C.c_char_p, C.c_uint64, U64P]),
+    "tfidf_node_stats_get": (C.c_int, [VP, VP]),
     "tfidf_device_free": (C.c_int, [C.c_int, VP]),
     "tfidf_device_copy": (C.c_int, [C.c_int, VP, VP, C.c_uint64, C.c_int]),
 }

@@ -1,387 +1,337 @@
-"""Multi-GPU orchestration: documents sharded across ranks (one process per
-GPU), exchanges over torch.distributed — backend "nccl" is RCCL over xGMI on
-MI355X; "gloo" is used by the CPU tests and one-GPU rehearsals.
+"""Node-level search over GPU shards: a thin ctypes layer over libtfidf's
+node-level C ABI (include/tfidf.h, "Node level").  The orchestration itself —
+GLOBAL statistics by term ownership, hash-seed agreement, top-k / all-hits /
+batch merges of device merge keys, SHARD mode's name table and Leader-style
+merge — is C++ in the library (csrc/tfidf_dist.hip), the same code a Java host
+reaches over JNI.  It replaces the reference's
+Leader.start fan-out + merge (Leader.java:39-92) over Worker.searchIndex
+(Worker.java:222-241) with collectives between GPU shards.
+
+Transports of a Comm (one per rank, one process per GPU):
+  * "rccl": the library's built-in RCCL communicator (over xGMI on MI355X);
+    the 128-byte unique id travels over the torch.distributed group.
+  * "callback": the group's own collectives (gloo, host memory) passed to the
+    library as C callbacks (tfidf_collectives) — the CPU tests and several
+    ranks sharing one GPU.
+Node: one process owning a device list (tfidf_node_*).
 
 Two modes:
-  * SHARD (the reference's N-worker semantics, Leader.java:39-92): every rank
-    scores with its own statistics and returns ALL its hits
-    (Worker.java:230, Integer.MAX_VALUE); the hits are summed by document
-    name in double, in rank (= worker response) order, and ordered by name
-    (TreeMap, String.compareTo).  shard_commit builds the name table once per
-    commit; shard_search does the per-query exchange and a device merge.
-  * GLOBAL (the reference's 1-worker semantics on a sharded corpus):
-      1. term ownership: every shard sends its (term key, df) records to the
-         term's owner rank (all-to-all); the owner sums df over identical keys
-         on device and answers record by record (all-to-all back);
-         {docCount, sumTTF} are summed.  O(vocabulary) per rank, one host
-         sync (the split sizes).  (global_commit_canonical is the older
-         all-gather + sorted-union form.)
-      2. per-rank top-k (or all hits) with global doc ids as packed merge keys
-         (score bits << 32 | ~doc) written by the engine into device memory,
-         all-gathered, merged on device by (score desc, doc asc).
-
-The engine is passed in as an adapter (HipShardAdapter in production; the
-CPU tests inject an oracle-backed adapter with the same methods).
+  * GLOBAL (the reference's 1-worker results on a sharded corpus): exchanged
+    docFreq / docCount / sumTotalTermFreq, global doc ids = shard base + local.
+  * SHARD (the reference's N workers, Leader.java:39-92): each rank scores with
+    its own statistics; every hit summed per document name in rank order
+    (Double::sum), ordered by name (TreeMap, String.compareTo).
 """
+import ctypes as C
+
 import numpy as np
-import torch
-import torch.distributed as dist
 
 from . import _lib as L
 
 # A query that does not parse (QueryParser ParseException / TooManyClauses) or
 # is not valid UTF-8: the reference's Worker answers [] (Worker.java:182-185),
-# so its Leader merges nothing.  The parse is deterministic, so every rank
-# raises for the same query and all of them skip the collectives together.
+# so its Leader merges nothing.  Every rank fails alike, before any collective.
 QUERY_ERRORS = (L.QuerySyntaxError, L.UnsupportedQuery)
 
+AG_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p)
+A2A_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_void_p,
+                     C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.c_void_p)
 
-def _query_errors(adapter):
-    return QUERY_ERRORS + tuple(getattr(adapter, "query_errors", ()))
+
+class Collectives(C.Structure):
+    _fields_ = [("ctx", C.c_void_p), ("memory", C.c_int32), ("all_gather", AG_FN), ("all_to_all_v", A2A_FN)]
 
 
-class HipShardAdapter:
-    """Adapter over a ShardIndex whose buffers live on ``device`` (cuda:N).
-    The index issues its device work on torch's current stream of that device,
-    so library calls and collectives are stream-ordered without host syncs."""
+def _host_view(addr, n):
+    return np.ctypeslib.as_array((C.c_uint8 * n).from_address(addr)) if n else np.zeros(0, np.uint8)
 
-    def __init__(self, shard, device, doc_base=0):
-        self.shard = shard
-        self.device = torch.device(device)
-        self.doc_base = doc_base
-        self.shard.set_stream(torch.cuda.current_stream(self.device).cuda_stream)
 
-    def local_stats(self):
-        s = self.shard.stats()
-        return int(s["doc_count"]), int(s["sum_ttf"]), int(s["num_docs"])
+def torch_host_collectives(group=None):
+    """tfidf_collectives over a torch.distributed group on host tensors (gloo):
+    the library stages device data through host memory around each call."""
+    import torch
+    import torch.distributed as dist
 
-    def hash_attempt(self):
-        """Seed attempt of the shard's hashed term keys (0 unless its commit met
-        a collision and rebuilt): GLOBAL statistics match terms across shards by
-        key, so every shard must hash with the same seed."""
-        return int(self.shard.stats()["hash_rebuilds"])
+    ws = dist.get_world_size(group)
 
-    def recommit(self, attempt):
-        """Rebuild the shard starting from seed attempt ``attempt`` (agreement
-        on one seed across ranks); -> the attempt now in force."""
-        self.shard.set_hash_attempt(attempt)
+    def all_gather(ctx, send, recv, nbytes, stream):
         try:
-            self.shard.commit()
-        finally:
-            self.shard.set_hash_attempt(0)
-        return self.hash_attempt()
+            src = torch.from_numpy(_host_view(send, nbytes).copy())
+            parts = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(ws)]
+            dist.all_gather(parts, src, group=group)
+            _host_view(recv, nbytes * ws)[:] = torch.cat(parts).numpy()
+            return 0
+        except Exception:                               # an exception must not cross the C frames
+            return 1
 
-    # -- GLOBAL statistics (term ownership) --------------------------------
-    def vocab_partition(self, n_ranks):
-        """-> (records int64 [n, 3] (lo, hi, df) grouped by owner, counts int64 [n_ranks]), on device."""
-        n = self.shard.vocab_size()
-        rec = torch.empty((max(n, 1), 3), dtype=torch.int64, device=self.device)
-        cnt = torch.empty(n_ranks, dtype=torch.int64, device=self.device)
-        n2 = self.shard.vocab_partition_device(n_ranks, rec.data_ptr(), max(n, 1), cnt.data_ptr())
-        return rec[:n2], cnt
+    def all_to_all_v(ctx, send, sb, so, recv, rb, ro, stream):
+        try:
+            sbl = [int(sb[r]) for r in range(ws)]
+            rbl = [int(rb[r]) for r in range(ws)]
+            inp = np.concatenate([_host_view(send + int(so[r]), sbl[r]) if sbl[r] else np.zeros(0, np.uint8)
+                                  for r in range(ws)]) if send else np.zeros(sum(sbl), np.uint8)
+            out = torch.empty(sum(rbl), dtype=torch.uint8)
+            dist.all_to_all_single(out, torch.from_numpy(np.ascontiguousarray(inp)), output_split_sizes=rbl,
+                                   input_split_sizes=sbl, group=group)
+            o = out.numpy()
+            at = 0
+            for r in range(ws):
+                if rbl[r]:
+                    _host_view(recv + int(ro[r]), rbl[r])[:] = o[at:at + rbl[r]]
+                at += rbl[r]
+            return 0
+        except Exception:
+            return 1
 
-    def vocab_reduce(self, records):
-        """Owner side: (summed df int32 per received record, distinct terms int64 [1]), on device."""
-        records = records.contiguous()
-        out = torch.empty(max(records.shape[0], 1), dtype=torch.int32, device=self.device)
-        nu = torch.zeros(1, dtype=torch.int64, device=self.device)
-        self.shard.vocab_reduce_device(records.data_ptr(), records.shape[0], out.data_ptr(), nu.data_ptr())
-        return out[:records.shape[0]], nu
+    return all_gather, all_to_all_v
 
-    def import_global_df(self, gdf, doc_count, sum_ttf):
-        gdf = gdf.contiguous()
-        self.shard.set_global_df_device(gdf.data_ptr(), gdf.shape[0], doc_count, sum_ttf)
 
-    # canonical (all-gather + sorted union) form
-    def export_vocab(self):
-        n = self.shard.vocab_size()
-        keys = torch.zeros((max(n, 1), 2), dtype=torch.int64, device=self.device)
-        df = torch.zeros(max(n, 1), dtype=torch.int32, device=self.device)
-        self.shard.vocab_export_device(keys.data_ptr(), df.data_ptr(), n)
-        return keys[:n], df[:n]
+class Comm:
+    """A tfidf_comm (one rank of a communicator)."""
 
-    def canonicalize(self, all_keys):
-        m = all_keys.shape[0]
-        dfc = torch.zeros(max(m, 1), dtype=torch.int32, device=self.device)
-        n = self.shard.vocab_canonicalize_device(all_keys.data_ptr(), m, dfc.data_ptr(), max(m, 1))
-        return dfc[:n]
+    def __init__(self, handle, keep=()):
+        self._h = handle
+        self._keep = keep                                # ctypes callbacks must outlive the communicator
 
-    def import_global(self, dfc, doc_count, sum_ttf):
-        dfc = dfc.contiguous()
-        self.shard.set_global_stats_device(dfc.data_ptr(), dfc.shape[0], doc_count, sum_ttf)
+    @classmethod
+    def from_group(cls, group=None, device=0, transport="auto"):
+        """Communicator over a torch.distributed group: the built-in RCCL one
+        ("rccl"; default when the group's backend is nccl) or the group's
+        collectives as host callbacks ("callback"; default for gloo)."""
+        import torch.distributed as dist
+        lib = L.load()
+        rank, ws = dist.get_rank(group), dist.get_world_size(group)
+        if transport == "auto":
+            transport = "rccl" if dist.get_backend(group) == "nccl" else "callback"
+        h = C.c_void_p()
+        if transport == "rccl":
+            uid = (C.c_uint8 * 128)()
+            if rank == 0:
+                L.check(lib.tfidf_rccl_unique_id(uid))
+            box = [bytes(uid)]
+            dist.broadcast_object_list(box, src=0, group=group)
+            uid = (C.c_uint8 * 128).from_buffer_copy(box[0])
+            L.check(lib.tfidf_comm_init_rccl(uid, rank, ws, device, C.byref(h)))
+            return cls(h)
+        ag, a2a = torch_host_collectives(group)
+        cag, ca2a = AG_FN(ag), A2A_FN(a2a)
+        coll = Collectives(None, 0, cag, ca2a)
+        L.check(lib.tfidf_comm_create(rank, ws, C.byref(coll), C.byref(h)))
+        return cls(h, keep=(cag, ca2a))
 
-    # -- search: packed merge keys in device memory ----------------------------
-    def topk_keys(self, queries, k):
-        """int64 [n_q, k] merge keys (global doc ids), 0 = empty slot."""
-        keys = torch.empty((len(queries), k), dtype=torch.int64, device=self.device)
-        self.shard.search_batch_keys_device(queries, k, self.doc_base, keys.data_ptr())
-        return keys
+    @classmethod
+    def inproc(cls, world):
+        """`world` communicators of this process (one thread per rank)."""
+        arr = (C.c_void_p * world)()
+        L.check(L.load().tfidf_comm_create_inproc(world, arr))
+        return [cls(C.c_void_p(arr[i])) for i in range(world)]
 
-    def all_keys(self, query, doc_base=None):
-        """int64 [H] merge keys of every hit, ordered (score desc, doc asc)."""
-        n = max(self.shard.stats()["num_docs"], 1)
-        keys = torch.empty(n, dtype=torch.int64, device=self.device)
-        h = self.shard.search_all_keys_device(query, self.doc_base if doc_base is None else doc_base,
-                                              keys.data_ptr(), n)
-        return keys[:h]
+    def info(self):
+        r, w, t = C.c_int32(), C.c_int32(), C.c_int32()
+        L.check(L.load().tfidf_comm_info(self._h, C.byref(r), C.byref(w), C.byref(t)))
+        return r.value, w.value, {0: "callback", 1: "rccl", 2: "inproc"}[t.value]
 
-    def doc_names(self):
-        """(uint8 blob, uint64 offsets[num_docs + 1]) of the shard's document keys."""
-        return self.shard.doc_keys()
+    def selftest(self):
+        L.check(L.load().tfidf_comm_selftest(self._h))
 
-    # host-array forms (tools)
-    def search_topk(self, query, k):
-        return self.shard.search_arrays(query, k)
+    def close(self):
+        if self._h:
+            L.load().tfidf_comm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def _offsets(items):
+    offs = np.zeros(len(items) + 1, np.uint64)
+    if items:
+        offs[1:] = np.cumsum([len(x) for x in items], dtype=np.uint64)
+    return offs
+
+
+class DistShard:
+    """One rank's shard in process model (2): every method is collective
+    (every rank calls it, in the same order)."""
+
+    def __init__(self, shard, comm, doc_base=0):
+        self.shard = shard
+        self.comm = comm
+        self.doc_base = doc_base
+
+    # -- statistics -----------------------------------------------------------
+    def global_commit(self, vocab_size=False):
+        """GLOBAL statistics (after this rank's own commit) -> (global
+        vocabulary size or None, docCount, sumTTF)."""
+        nv, dc, ttf = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        L.check(L.load().tfidf_dist_global_commit(self.shard._h, self.comm._h, C.byref(nv) if vocab_size else None,
+                                                  C.byref(dc), C.byref(ttf)))
+        return (nv.value if vocab_size else None), dc.value, ttf.value
+
+    def shard_commit(self):
+        """SHARD mode name table (once per commit) -> distinct names over all ranks."""
+        n = C.c_uint64()
+        L.check(L.load().tfidf_dist_shard_commit(self.shard._h, self.comm._h, C.byref(n)))
+        return n.value
+
+    # -- GLOBAL search ------------------------------------------------------------
+    def search_arrays(self, query: bytes, k):
+        """(global doc int64[], score float32[]) in (score desc, doc asc);
+        k == 0: every hit; [] for a query that does not parse."""
+        lib = L.load()
+        cap = max(k, 1) if k else 1 << 16
+        docs = np.zeros(cap, np.uint64)
+        scores = np.zeros(cap, np.float32)
+        n = C.c_uint64()
+        try:
+            rc = lib.tfidf_dist_search(self.shard._h, self.comm._h, self.doc_base, query, len(query), k,
+                                       L.ptr(docs, C.c_uint64), L.ptr(scores, C.c_float), cap, C.byref(n))
+            if rc == L.E_BUFFER:
+                docs = np.zeros(n.value, np.uint64)
+                scores = np.zeros(n.value, np.float32)
+                rc = lib.tfidf_dist_last_hits(self.comm._h, L.ptr(docs, C.c_uint64), L.ptr(scores, C.c_float),
+                                              n.value, C.byref(n))
+            L.check(rc)
+        except QUERY_ERRORS:
+            return np.zeros(0, np.int64), np.zeros(0, np.float32)
+        return docs[:n.value].astype(np.int64), scores[:n.value]
+
+    def search(self, query: bytes, k):
+        d, s = self.search_arrays(query, k)
+        return list(zip(d.tolist(), s.tolist()))
 
     def search_batch(self, queries, k):
-        return self.shard.search_batch(queries, k)
+        """(docs int64[n_q, k], scores float32[n_q, k], counts int64[n_q]), global doc ids."""
+        nq = len(queries)
+        offs = _offsets(queries)
+        docs = np.zeros((nq, k), np.uint64)
+        scores = np.zeros((nq, k), np.float32)
+        counts = np.zeros(nq, np.uint32)
+        L.check(L.load().tfidf_dist_search_batch(self.shard._h, self.comm._h, self.doc_base, b"".join(queries),
+                                                 L.ptr(offs, C.c_uint64), nq, k, L.ptr(docs, C.c_uint64),
+                                                 L.ptr(scores, C.c_float), L.ptr(counts, C.c_uint32)))
+        return docs.astype(np.int64), scores, counts.astype(np.int64)
+
+    # -- SHARD search (Leader.start) ------------------------------------------------
+    def shard_search(self, query: bytes):
+        """[(name bytes, double)] in String.compareTo order."""
+        n, nb = C.c_uint64(), C.c_uint64()
+        try:
+            L.check(L.load().tfidf_dist_shard_search(self.shard._h, self.comm._h, query, len(query), C.byref(n),
+                                                     C.byref(nb)))
+        except QUERY_ERRORS:
+            return []
+        return _last_names(self.comm._h, n.value, nb.value)
+
+
+def _last_names(h, n, nb):
+    buf = C.create_string_buffer(max(nb, 1))
+    offs = np.zeros(n + 1, np.uint64)
+    sc = np.zeros(max(n, 1), np.float64)
+    m, b = C.c_uint64(), C.c_uint64()
+    L.check(L.load().tfidf_dist_last_names(h, buf, max(nb, 1), L.ptr(offs, C.c_uint64), L.ptr(sc, C.c_double),
+                                           n, C.byref(m), C.byref(b)))
+    raw = buf.raw
+    return [(raw[int(offs[i]):int(offs[i + 1])], float(sc[i])) for i in range(m.value)]
+
+
+class Node:
+    """Process model (1): one process, one shard per device (tfidf_node_*)."""
+
+    def __init__(self, devices=(0,), stats_mode=L.STATS_GLOBAL, inproc=False, vocab_capacity_log2=18,
+                 inversion=L.INVERSION_AUTO):
+        lib = L.load()
+        cfg = L.Config()
+        L.check(lib.tfidf_config_init(C.byref(cfg)))
+        cfg.stats_mode = stats_mode
+        cfg.vocab_capacity_log2 = vocab_capacity_log2
+        cfg.inversion = inversion
+        dev = (C.c_int32 * len(devices))(*devices)
+        h = C.c_void_p()
+        L.check(lib.tfidf_node_create_devices(C.byref(cfg), dev, len(devices), 1 if inproc else 0, C.byref(h)))
+        self._h = h
+
+    def close(self):
+        if self._h:
+            L.load().tfidf_node_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def add_documents(self, texts, keys=None, shard=-1):
+        offs = _offsets(texts)
+        koffs = _offsets(keys) if keys is not None else None
+        L.check(L.load().tfidf_node_add_docs(self._h, shard, b"".join(texts), L.ptr(offs, C.c_uint64), len(texts),
+                                             b"".join(keys) if keys is not None else None,
+                                             L.ptr(koffs, C.c_uint64) if keys is not None else None))
+
+    def commit(self):
+        L.check(L.load().tfidf_node_commit(self._h))
+
+    def stats(self):
+        s = NodeStats()
+        L.check(L.load().tfidf_node_stats_get(self._h, C.byref(s)))
+        return {f: getattr(s, f) for f, _ in NodeStats._fields_}
+
+    def search(self, query: bytes, k):
+        lib = L.load()
+        cap = max(k, 1) if k else max(self.stats()["num_docs"], 1)
+        docs = np.zeros(cap, np.uint64)
+        scores = np.zeros(cap, np.float32)
+        n = C.c_uint64()
+        try:
+            L.check(lib.tfidf_node_search(self._h, query, len(query), k, L.ptr(docs, C.c_uint64),
+                                          L.ptr(scores, C.c_float), cap, C.byref(n)))
+        except QUERY_ERRORS:
+            return []
+        return list(zip(docs[:n.value].astype(np.int64).tolist(), scores[:n.value].tolist()))
+
+    def search_batch(self, queries, k):
+        nq = len(queries)
+        offs = _offsets(queries)
+        docs = np.zeros((nq, k), np.uint64)
+        scores = np.zeros((nq, k), np.float32)
+        counts = np.zeros(nq, np.uint32)
+        L.check(L.load().tfidf_node_search_batch(self._h, b"".join(queries), L.ptr(offs, C.c_uint64), nq, k,
+                                                 L.ptr(docs, C.c_uint64), L.ptr(scores, C.c_float),
+                                                 L.ptr(counts, C.c_uint32)))
+        return docs.astype(np.int64), scores, counts.astype(np.int64)
+
+    def search_names(self, query: bytes):
+        lib = L.load()
+        n, nb = C.c_uint64(), C.c_uint64()
+        try:
+            rc = lib.tfidf_node_search_names(self._h, query, len(query), None, 0, None, None, 0, C.byref(n), C.byref(nb))
+            if rc != L.E_BUFFER:
+                L.check(rc)
+            if n.value == 0:
+                return []
+        except QUERY_ERRORS:
+            return []
+        buf = C.create_string_buffer(max(nb.value, 1))
+        offs = np.zeros(n.value + 1, np.uint64)
+        sc = np.zeros(n.value, np.float64)
+        L.check(lib.tfidf_node_search_names(self._h, query, len(query), buf, nb.value, L.ptr(offs, C.c_uint64),
+                                            L.ptr(sc, C.c_double), n.value, C.byref(n), C.byref(nb)))
+        raw = buf.raw
+        return [(raw[int(offs[i]):int(offs[i + 1])], float(sc[i])) for i in range(n.value)]
 
     def doc_key(self, doc):
-        return self.shard.doc_key(doc)
+        buf = C.create_string_buffer(4096)
+        n = C.c_uint64()
+        L.check(L.load().tfidf_node_doc_key(self._h, doc, buf, 4096, C.byref(n)))
+        return buf.raw[:n.value]
 
 
-def _dev(adapter):
-    return adapter.device if isinstance(adapter.device, torch.device) else torch.device(adapter.device)
-
-
-def _host_coll(group):
-    """gloo collectives run on host tensors here (the CPU tests and the one-GPU rehearsal)."""
-    return dist.get_backend(group) == "gloo"
-
-
-def _a2a(out, inp, out_splits, in_splits, group):
-    if _host_coll(group) and inp.is_cuda:
-        o = out.cpu()
-        dist.all_to_all_single(o, inp.cpu(), output_split_sizes=out_splits, input_split_sizes=in_splits,
-                               group=group)
-        out.copy_(o)
-    else:
-        dist.all_to_all_single(out, inp, output_split_sizes=out_splits, input_split_sizes=in_splits, group=group)
-
-
-def _all_gather(t, group):
-    """-> tensor [world, *t.shape] (same device as t)."""
-    ws = dist.get_world_size(group)
-    if _host_coll(group):
-        src = t.detach().cpu().contiguous()
-        parts = [torch.empty_like(src) for _ in range(ws)]
-        dist.all_gather(parts, src, group=group)
-        return torch.stack(parts).to(t.device)
-    out = torch.empty((ws,) + tuple(t.shape), dtype=t.dtype, device=t.device)
-    dist.all_gather_into_tensor(out, t.contiguous(), group=group)
-    return out
-
-
-def _all_gather_var(t, n, group):
-    """Rows [0, n) of t from every rank -> (tensor [sum n_r, ...] in rank order, [n_r]).
-    One host read (the counts)."""
-    ns = _all_gather(torch.tensor([n], dtype=torch.int64, device=t.device), group).view(-1).tolist()
-    m = max(max(ns), 1)
-    pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
-    pad[:n] = t[:n]
-    g = _all_gather(pad, group)
-    return torch.cat([g[r, :ns[r]] for r in range(len(ns))], 0), ns
-
-
-def global_commit(adapter, group=None, vocab_size=False):
-    """GLOBAL statistics by term ownership; call after the shard's own commit.
-    Returns (global vocabulary size or None, docCount, sumTTF).  Host syncs:
-    one read of the gathered [per-owner counts | docCount | sumTTF | seed
-    attempt] rows (the all-to-all split sizes), plus one more only when
-    vocab_size is asked for.  Shards whose commits hashed with different seeds
-    (a collision on one shard) first agree on the highest: the others re-commit
-    under it, and the rows are gathered again."""
-    dev = _dev(adapter)
-    ws = dist.get_world_size(group)
-    me = dist.get_rank(group)
-    while True:
-        dc, ttf, _ = adapter.local_stats()                  # host values of the shard's commit
-        att = adapter.hash_attempt() if hasattr(adapter, "hash_attempt") else 0
-        rec, cnt = adapter.vocab_partition(ws)              # device, asynchronous
-        meta = torch.cat([cnt.to(torch.int64), torch.tensor([dc, ttf, att], dtype=torch.int64, device=dev)])
-        M = _all_gather(meta, group).cpu().tolist()         # the host sync
-        top = max(int(M[r][ws + 2]) for r in range(ws))
-        if all(int(M[r][ws + 2]) == top for r in range(ws)):
-            break
-        # a shard met a hash collision and rebuilt under a later seed: keys are
-        # matched across shards, so the shards below it re-commit under that
-        # seed (which may collide there in turn: agree again)
-        if att < top:
-            adapter.recommit(top)
-    send = [int(x) for x in M[me][:ws]]
-    recv = [int(M[r][me]) for r in range(ws)]
-    gdc = sum(int(M[r][ws]) for r in range(ws))
-    gttf = sum(int(M[r][ws + 1]) for r in range(ws))
-    got = torch.empty((sum(recv), 3), dtype=torch.int64, device=dev)
-    _a2a(got, rec.contiguous(), recv, send, group)
-    ans, nu = adapter.vocab_reduce(got)
-    back = torch.empty(sum(send), dtype=torch.int32, device=dev)
-    _a2a(back, ans.contiguous(), send, recv, group)
-    adapter.import_global_df(back, gdc, gttf)
-    n_vocab = None
-    if vocab_size:
-        nu = nu.clone()
-        if _host_coll(group) and nu.is_cuda:
-            h = nu.cpu()
-            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
-            n_vocab = int(h.item())
-        else:
-            dist.all_reduce(nu, op=dist.ReduceOp.SUM, group=group)
-            n_vocab = int(nu.item())
-    return n_vocab, gdc, gttf
-
-
-def global_commit_canonical(adapter, group=None):
-    """All-gather + sorted-union form of GLOBAL statistics (canonical term
-    ids; O(G x vocabulary) per rank).  Same results as global_commit."""
-    dev = _dev(adapter)
-    keys, df = adapter.export_vocab()
-    padded, ns = _all_gather_var(keys, keys.shape[0], group)
-    all_keys = padded.contiguous()
-    dfc = adapter.canonicalize(all_keys)
-    if _host_coll(group) and dfc.is_cuda:
-        h = dfc.cpu()
-        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
-        dfc.copy_(h)
-    else:
-        dist.all_reduce(dfc, op=dist.ReduceOp.SUM, group=group)
-    dc, ttf, _ = adapter.local_stats()
-    st = torch.tensor([dc, ttf], dtype=torch.int64, device=dev)
-    st = _all_gather(st, group).sum(0).tolist()
-    adapter.import_global(dfc, int(st[0]), int(st[1]))
-    return int(dfc.shape[0]), int(st[0]), int(st[1])
-
-
-def _keys_to_hits(keys):
-    """Descending merge keys (int64, > 0) -> [(global doc, float score)]."""
-    k = keys.cpu().numpy().view(np.uint64)
-    doc = (~k & np.uint64(0xFFFFFFFF)).astype(np.int64)
-    sc = (k >> np.uint64(32)).astype(np.uint32).view(np.float32)
-    return list(zip(doc.tolist(), sc.tolist()))
-
-
-def global_search(adapter, query: bytes, k: int, group=None):
-    """Per-rank top-k (k >= 1) or every hit (k == 0, searcher.search(q,
-    Integer.MAX_VALUE)) with global doc ids; all-gather of the packed keys;
-    device merge.  Returns [(global doc, score)] in (score desc, doc asc);
-    [] for a query that does not parse (as the batch path, and the reference)."""
-    if k == 0:
-        try:
-            mine = adapter.all_keys(query)
-        except _query_errors(adapter):
-            return []
-        allk, _ = _all_gather_var(mine, mine.shape[0], group)
-        allk = torch.sort(allk, descending=True).values
-        return _keys_to_hits(allk)
-    mine = adapter.topk_keys([query], k)[0]
-    allk = _all_gather(mine, group).view(-1)
-    top = torch.topk(allk, min(k, allk.numel()), largest=True, sorted=True).values
-    return _keys_to_hits(top[top != 0])
-
-
-def merge_keys(docs, scores, counts, doc_base, device):
-    """Per-rank batch top-k host arrays -> int64 merge keys [n_q, k] on
-    ``device``: (float32 score bits << 32) | ~global_doc; empty slots 0
-    (adapters without device key output)."""
-    nq, k = docs.shape
-    valid = np.arange(k)[None, :] < counts.astype(np.int64)[:, None]
-    g = (docs.astype(np.uint64) + np.uint64(doc_base)) & np.uint64(0xFFFFFFFF)
-    key = (scores.view(np.uint32).astype(np.uint64) << np.uint64(32)) | (~g & np.uint64(0xFFFFFFFF))
-    key = np.where(valid, key, np.uint64(0)).view(np.int64)
-    return torch.from_numpy(np.ascontiguousarray(key)).to(device)
-
-
-def global_search_batch(adapter, queries, k: int, group=None):
-    """Batched step 2 (cfg 3/4): every rank scores the whole batch on its
-    shard into device merge keys, the [n_q, k] keys are all-gathered once (one
-    RCCL collective for the batch) and the global top-k of each query is a
-    device top-k over the ws*k candidates.  Returns (docs int64[n_q, k],
-    scores float32[n_q, k], counts int64[n_q]) as numpy arrays (global doc ids)."""
-    mine = adapter.topk_keys(queries, k)                            # [n_q, k] on device
-    allk = _all_gather(mine, group)                                 # [ws, n_q, k]
-    allk = allk.permute(1, 0, 2).reshape(len(queries), -1)          # [n_q, ws * k]
-    top = torch.topk(allk, k, dim=1, largest=True, sorted=True).values
-    top = top.cpu().numpy().view(np.uint64)
-    cnt = (top != 0).sum(axis=1)
-    gdoc = (~top & np.uint64(0xFFFFFFFF)).astype(np.int64)
-    sc = (top >> np.uint64(32)).astype(np.uint32).view(np.float32)
-    return gdoc, sc, cnt
-
-
-# ---------------------------------------------------------------------------
-# SHARD mode: the reference's N workers (Leader.java:39-92)
-
-class ShardNames:
-    """Global document-name table of SHARD mode: every distinct name of every
-    rank, sorted by String.compareTo (TreeMap order); ``local_ids`` maps this
-    rank's local doc ids to name ids (device int64)."""
-
-    def __init__(self, names, local_ids):
-        self.names = names
-        self.local_ids = local_ids
-
-
-def shard_commit(adapter, group=None):
-    """Once per commit (SHARD mode): all-gather the document names, sort their
-    union by String.compareTo (tfidf_sort_names), map local docs to name ids."""
-    from .engine import sort_names
-    dev = _dev(adapter)
-    blob, offs = adapter.doc_names()
-    n = len(offs) - 1
-    lens = torch.from_numpy((offs[1:] - offs[:-1]).astype(np.int64))
-    all_lens, ns = _all_gather_var(lens.to(dev), n, group)
-    all_blob, _ = _all_gather_var(torch.from_numpy(np.ascontiguousarray(blob, np.uint8)).to(dev), len(blob), group)
-    all_lens = all_lens.cpu().numpy()
-    all_blob = all_blob.cpu().numpy()
-    aoffs = np.zeros(len(all_lens) + 1, np.uint64)
-    aoffs[1:] = np.cumsum(all_lens, dtype=np.uint64)
-    perm = sort_names(all_blob, aoffs)
-    names, nid = [], np.zeros(len(all_lens), np.int64)
-    prev = None
-    for p in perm.tolist():
-        nm = all_blob[int(aoffs[p]):int(aoffs[p + 1])].tobytes()
-        if nm != prev:
-            names.append(nm)
-            prev = nm
-        nid[p] = len(names) - 1
-    me = dist.get_rank(group)
-    lo = int(sum(ns[:me]))
-    return ShardNames(names, torch.from_numpy(nid[lo:lo + n]).to(dev))
-
-
-def shard_search(adapter, names: ShardNames, query: bytes, group=None):
-    """Leader.start over the ranks: each rank's every hit under its own
-    statistics, all-gathered; per name the scores ((double) of the float) are
-    summed in rank order (HashMap.merge Double::sum, Leader.java:73-77) and the
-    result is ordered by name (TreeMap, :80-88).  Returns [(name, score)]."""
-    ws = dist.get_world_size(group)
-    try:
-        keys = adapter.all_keys(query, doc_base=0)                  # local doc ids
-    except _query_errors(adapter):
-        return []
-    doc = (~keys) & 0xFFFFFFFF
-    rec = torch.stack([names.local_ids[doc], keys >> 32], 1)        # (name id, score bits)
-    allr, ns = _all_gather_var(rec, rec.shape[0], group)            # rank order
-    if allr.shape[0] == 0:
-        return []
-    nid = allr[:, 0]
-    val = allr[:, 1].to(torch.int32).view(torch.float32).to(torch.float64)
-    nid_s, order = torch.sort(nid, stable=True)                     # rank order kept within a name
-    val_s = val[order]
-    first = torch.ones_like(nid_s, dtype=torch.bool)
-    first[1:] = nid_s[1:] != nid_s[:-1]
-    seg = torch.cumsum(first.to(torch.int64), 0) - 1
-    pos = torch.arange(nid_s.numel(), device=nid_s.device)
-    start = torch.zeros(int(seg[-1]) + 1, dtype=torch.int64, device=nid_s.device)
-    start[seg[first]] = pos[first]
-    occ = pos - start[seg]                                          # 0 .. ws-1 within a name
-    sums = torch.zeros(start.numel(), dtype=torch.float64, device=nid_s.device)
-    for j in range(ws):                                             # Double::sum in response order
-        m = occ == j
-        if bool(m.any()):
-            sums.index_add_(0, seg[m], val_s[m])
-    uid = nid_s[first].cpu().tolist()
-    return [(names.names[u], float(s)) for u, s in zip(uid, sums.cpu().tolist())]
+class NodeStats(C.Structure):
+    _fields_ = [(n, C.c_uint64) for n in ("n_shards", "num_docs", "doc_count", "sum_ttf", "num_terms", "transport")]
 
 
 def shard_range(n_docs, rank, world):
