@@ -1494,6 +1494,54 @@ __device__ __forceinline__ void hist_wg(WgSmem &sm, uint32_t t, uint32_t lane, u
   }
 }
 
+// Dictionary slot of a folded (> 8 byte) table key of the staged window
+// (wbase = corpus offset of window byte 0): the exact 128-bit key, find or
+// insert, the identity check of hashed keys.  Out of line: its key builder and
+// probe state would otherwise raise the workgroup tokenizer's register peak
+// for a path short-word corpora never take.  Every input arrives as an
+// argument: a callee has no kernel-argument segment of its own, so the
+// TFIDF_COLD reads of the kernels are not available here.
+struct FoldArgs {
+  uint64_t *dict;
+  const uint8_t *text;           // corpus (device): reference occurrences
+  uint64_t hash_seed;
+  uint64_t *verify_defer;
+  uint32_t *verify_count;
+  uint32_t *err;
+  uint32_t verify_cap, cap_mask;
+};
+__device__ __noinline__ uint32_t wg_fold_slot(const FoldArgs &a, const uint8_t *win, uint64_t key, bool fa,
+                                              uint64_t wbase, uint32_t doc) {
+  uint64_t flo = 1, fhi = kKeyValid, mine = 0;
+  if (fa) {
+    const uint32_t n = (uint32_t)key & 0xFFu, tp = (uint32_t)(key >> 13) & 0x1FFFu;
+    bool valid;
+    token_key(win, tp, tp + n, &flo, &fhi, &valid, a.hash_seed);
+    mine = dict_ref_word(wbase + tp, n);
+  }
+  bool cl;
+  const uint32_t gg = dict_find_or_insert(a.dict, a.cap_mask, flo, fhi, fa, &mine, &cl);
+  if (fa && (flo & kLoHashed) && !cl && gg != kInvalidSlot) {        // dict_verify
+    const uint64_t r = __hip_atomic_load(a.dict + 2 * ((size_t)a.cap_mask + 1) + gg, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    if (r != mine) {
+      if (r == 0) {
+        const uint32_t at = atomicAdd(a.verify_count, 1u);
+        if (at < a.verify_cap) {
+          a.verify_defer[2 * (size_t)at] = gg;
+          a.verify_defer[2 * (size_t)at + 1] = mine;
+        } else {
+          set_build_err(a.err, kErrCollision, doc);
+        }
+      } else if (!uc_same_term(a.text + dict_ref_off(r), dict_ref_len(r), a.text + dict_ref_off(mine),
+                               dict_ref_len(mine))) {
+        set_build_err(a.err, kErrCollision, doc);
+      }
+    }
+  }
+  return gg;
+}
+
 template <bool G4>
 #ifdef TFIDF_WG_WPE
 #define TFIDF_WG_ATTR __attribute__((amdgpu_waves_per_eu(TFIDF_WG_WPE)))
@@ -1697,29 +1745,7 @@ __global__ void __launch_bounds__(kWgThreads) TFIDF_WG_ATTR k_tokenize_wg(BuildP
         lo[k] = sh ? key : 0ull;
         foldm |= (uint32_t)f << k;
         ps[k] = dict_home(dict_hash_short(lo[k]), dmask) & ~1u;
-        g[k] = (sh | f) ? kLookupPending : kInvalidSlot;
-        if (f) lo[k] = key;                               // the folded table key (position + length)
-      }
-      // folded (> 8 byte) terms: exact 128-bit keys, one lookup per lane at a time
-      while (__any(foldm != 0)) {
-        uint64_t flo = 1, fhi = kKeyValid, mine = 0;
-        uint32_t k = 0;
-        const bool fa = foldm != 0;
-        if (fa) {
-          k = (uint32_t)__builtin_ctz(foldm);
-          foldm &= foldm - 1;
-          const uint64_t key = k == 0 ? lo[0] : lo[K - 1];
-          const uint32_t n = (uint32_t)key & 0xFFu, tp = (uint32_t)(key >> 13) & 0x1FFFu;
-          bool valid;
-          token_key(sm.text, tp, tp + n, &flo, &fhi, &valid, TFIDF_COLD(hash_seed));
-          mine = dict_ref_word((s0 - shift) + tp, n);
-        }
-        bool cl;
-        const uint32_t gg = dict_find_or_insert(p.dict, dmask, flo, fhi, fa, &mine, &cl);
-        if (fa && (flo & kLoHashed) && !cl && gg != kInvalidSlot) dict_verify(p, gg, mine, (uint32_t)d);
-#pragma unroll
-        for (int kk = 0; kk < K; kk++)
-          if (fa && (uint32_t)kk == k) { g[kk] = gg; lo[kk] = 0; }
+        g[k] = sh ? kLookupPending : kInvalidSlot;        // folded ones: resolved after the short ones
       }
       // short terms: bucket (G4: 4-slot group) probes, both of a lane's loads in flight
       for (uint32_t round = 0;; round++) {
@@ -1753,6 +1779,30 @@ __global__ void __launch_bounds__(kWgThreads) TFIDF_WG_ATTR k_tokenize_wg(BuildP
           for (int k = 0; k < K; k++)
             if (cs[k] != kInvalidSlot) g[k] = dict_claim_short(p.dict, dmask, cs[k], lo[k], &ps[k]);
         }
+      }
+      // folded (> 8 byte) terms, after the short ones (their probe state is
+      // dead by then): exact 128-bit keys, one lookup per lane at a time
+      while (__any(foldm != 0)) {
+        uint32_t k = 0;
+        const bool fa = foldm != 0;
+        if (fa) {
+          k = (uint32_t)__builtin_ctz(foldm);
+          foldm &= foldm - 1;
+        }
+        FoldArgs fa_args;
+        fa_args.dict = p.dict;
+        fa_args.text = p.text;
+        fa_args.hash_seed = TFIDF_COLD(hash_seed);
+        fa_args.verify_defer = TFIDF_COLD(verify_defer);
+        fa_args.verify_count = TFIDF_COLD(verify_count);
+        fa_args.err = TFIDF_COLD(err);
+        fa_args.verify_cap = TFIDF_COLD(verify_cap);
+        fa_args.cap_mask = dmask;
+        const uint32_t gg = wg_fold_slot(fa_args, sm.text, sm.key[slots[t + kWgThreads * k] & (kWaveSlots - 1)], fa,
+                                         s0 - shift, (uint32_t)d);
+#pragma unroll
+        for (int kk = 0; kk < K; kk++)
+          if (fa && (uint32_t)kk == k) g[kk] = gg;
       }
       bool caperr = false;
 #pragma unroll
@@ -1802,10 +1852,12 @@ __global__ void __launch_bounds__(kWgThreads) TFIDF_WG_ATTR k_tokenize_wg(BuildP
       p.doc_len[d] = len;
       p.doc_nuniq[d] = nu;
       p.doc_norm[d] = (uint8_t)int_to_byte4(len);
-      my_doc_count += len > 0;
-      my_ttf += len;
-      my_nnz += nu;
     }
+    // workgroup-uniform counts: scalar accumulators (no VGPRs across the loop)
+    const uint32_t ulen = (uint32_t)__builtin_amdgcn_readfirstlane((int)len);
+    my_doc_count += ulen > 0;
+    my_ttf += ulen;
+    my_nnz += (uint32_t)__builtin_amdgcn_readfirstlane((int)nu);
   }
   if (t == 0 && (my_ttf | my_nnz | my_doc_count)) {
     atomicAdd(&TFIDF_COLD(stats)[0], my_doc_count);
