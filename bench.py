@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--cap-log2", type=int, default=0,
                     help="dictionary slots 2^x (0 = smallest power of two >= 1.6 x vocab, at least 2^18)")
     ap.add_argument("--inversion", choices=("auto", "block", "term"), default="auto")
+    ap.add_argument("--unicode-every", type=int, default=0,
+                    help="one non-ASCII word per this many bytes of every document (book-like text)")
     ap.add_argument("--unicode-frac", type=float, default=0.0,
                     help="fraction of documents made non-ASCII (Unicode tokenizer path); 0 = the cfg-2 corpus")
     ap.add_argument("--no-e2e", dest="e2e", action="store_false",
@@ -238,7 +240,7 @@ def main():
     doc_base = rank * n_docs
     corpus = synth.DeviceCorpus(n_docs, V=args.vocab, len_min=args.len_min, len_max=args.len_max,
                                 doc_base=doc_base, device=local)
-    n_unicode = corpus.inject_unicode(args.unicode_frac)
+    n_unicode = corpus.inject_unicode(args.unicode_frac) + corpus.inject_unicode_every(args.unicode_every)
     cap = args.cap_log2
     if not cap:
         cap = 18

@@ -146,3 +146,34 @@ def test_book_corpus_long_unicode_docs():
         assert_hits_equal(g.search(qb, 3), o.search(qb, 3))
     g.close()
     o.close()
+
+
+def test_book_unicode_chunks():
+    """Books (cfg 1 shape) whose text is mostly ASCII with a non-ASCII word
+    every few hundred words (curly apostrophes, accents, a CJK pair, an emoji):
+    the units holding non-ASCII text take the Unicode chunk kernel
+    (k_tokenize_uchunk) and the book stays on the chunk path instead of going
+    to k_tokenize_long whole; one book with an unspaced CJK run longer than a
+    unit's leading margin falls back to the long path for that book.  All =
+    the oracle."""
+    rng = random.Random(21)
+    sprinkle = ["it’s", "don’t", "café", "naïve", "Élan", "straße", "中文", "😀", "ΣΟΦΙΑ", "ﬁne"]
+    texts = []
+    for i in range(9):
+        words = [synth.word(rng.randint(1, 20000)).decode() for _ in range(rng.randint(20000, 40000))]
+        for j in range(rng.randint(0, 50), len(words), rng.randint(150, 450)):
+            words[j] = rng.choice(sprinkle)
+        texts.append(" ".join(words).encode())
+    cjk = " ".join(synth.word(rng.randint(1, 5000)).decode() for _ in range(6000))
+    texts.append((cjk + " " + "中文分词器" * 300 + " " + cjk).encode())      # 4.5 KB without a split byte
+    g, o = build_pair(texts)
+    st = g.stats()
+    assert st["long_docs"] == len(texts)
+    assert st["long_chunked"] == len(texts) - 1                         # only the CJK book goes to the long path
+    check(g, o, texts)
+    for q in ["café it’s", "naïve straße", "中文 " + synth.word(7).decode(), "ﬁne 😀", synth.word(99).decode()]:
+        qb = q.encode()
+        assert_hits_equal(g.search(qb, 0), o.search(qb, 0))
+        assert_hits_equal(g.search(qb, 5), o.search(qb, 5))
+    g.close()
+    o.close()

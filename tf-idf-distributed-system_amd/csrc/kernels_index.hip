@@ -1883,40 +1883,6 @@ __global__ void __launch_bounds__(kWgThreads) TFIDF_WG_ATTR k_tokenize_wg(BuildP
 // that cannot take this path (non-ASCII
 // text, a token of more than 255 characters, more than 512 distinct terms)
 // marks its document, which then goes to k_tokenize_long as a whole.
-constexpr uint32_t kCoreBytes = kLongCoreBytes;
-constexpr uint32_t kPreBytes = 64;
-constexpr uint32_t kPostBytes = 320;
-static_assert(kPreBytes + kCoreBytes + kPostBytes + 16 <= kWaveWindow, "chunk window");
-
-struct ChunkMeta {
-  uint64_t s0, L;                 // window: corpus bytes [s0, s0 + L)
-  uint32_t shift, core_lo, core_hi, gi;
-  uint64_t d;
-};
-
-__device__ __forceinline__ ChunkMeta chunk_meta(const BuildParams &p, uint64_t u) {
-  // group document holding unit u: chunk_pre[gi] <= u < chunk_pre[gi + 1] (binary search, scalar loads)
-  uint32_t lo = 0, hi = p.n_group_docs;
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (p.chunk_pre[mid] <= u) lo = mid; else hi = mid;
-  }
-  const uint2 e = make_uint2(lo, (uint32_t)(u - p.chunk_pre[lo]));
-  ChunkMeta m;
-  m.gi = e.x;
-  m.d = p.chunk_docs[e.x];
-  const uint64_t src = p.live_map ? p.live_map[m.d] : m.d;
-  const uint64_t dlo = p.offsets[src], dl = p.offsets[src + 1] - dlo;
-  const uint64_t clo = (uint64_t)e.y * kCoreBytes, chi = min(dl, clo + kCoreBytes);
-  const uint64_t ws = clo > kPreBytes ? clo - kPreBytes : 0, we = min(dl, chi + kPostBytes);
-  m.s0 = dlo + ws;
-  m.L = we - ws;
-  m.core_lo = (uint32_t)(clo - ws);
-  m.core_hi = (uint32_t)(chi - ws);
-  m.shift = (uint32_t)(reinterpret_cast<uintptr_t>(p.text + m.s0) & 15);
-  return m;
-}
-
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_tokenize_chunk(BuildParams p) {
   __shared__ WaveSmem sm;
   const uint32_t lane = threadIdx.x;
@@ -1961,8 +1927,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     uint64_t wbase = 0;
     bool upper;
     const uint64_t W = lane_word_mask<false>(sm.text, lane, &bad, &under, &wbase, &upper);
-    if (bad) {                                               // non-ASCII: the whole document -> long path
-      if (lane == 0) p.chunk_fail[fail_at] = 1u;
+    if (bad) {                                               // non-ASCII: the Unicode chunk kernel
+      if (lane == 0) {
+        if (p.uchunk_list) p.uchunk_list[atomicAdd(p.uchunk_count, 1u)] = (uint32_t)u;
+        else p.chunk_fail[fail_at] = 1u;
+      }
       continue;
     }
     const uint64_t wlast = __ballot((W >> 63) & 1ull);

@@ -316,4 +316,247 @@ hipError_t launch_tokenize_uwave(const BuildParams &p, int grid, hipStream_t s) 
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Book-sized documents, units with non-ASCII text (round 4).  k_tokenize_chunk
+// lists a (document, 2 KB core) unit whose window holds a byte >= 0x80; this
+// kernel tokenizes that unit with the Unicode scanner instead of sending the
+// whole book to k_tokenize_long.  One wavefront per unit: the window (core +
+// context margins) is staged in LDS with per-byte classes; the scan starts at
+// a split point (the byte before it is ASCII class OTHER: the scanner's start
+// state holds there) at or before the core, lanes take slices between split
+// points, and only tokens STARTING in the core are counted (a token crossing
+// the core's start belongs to the unit before).  The unit's distinct terms are
+// resolved in the dictionary and stored as its bucketed (slot, tf) pair list,
+// exactly as k_tokenize_chunk stores an ASCII unit's, for k_long_rows.  A unit
+// this cannot take decides its document for the long path (chunk_fail): no
+// split point in the leading margin (e.g. unspaced CJK), a token that reaches
+// the window's end before the document's, a token over 255 UTF-16 units,
+// malformed UTF-8, > kPairWords distinct terms.
+
+// uw_next_span with one more outcome: *at_end = the span scan reached byte n
+// while a longer match was still possible (the window ends there, not the
+// document: the token's true extent is unknown)
+__device__ __forceinline__ bool uc_window_span(const uint8_t *cls, const uint8_t *tr, uint32_t n, uint32_t *pos,
+                                               uint32_t stop, uint32_t *ts, uint32_t *te, bool *bad, bool *at_end) {
+  while (*pos < stop) {
+    const uint32_t i = *pos;
+    const uint32_t v = cls[i];
+    if (v == 0xFFu) { *bad = true; return false; }
+    const uint32_t c = v & 31u, l = (v >> 5) + 1;
+    const uint32_t st0 = tr[kWStart * kUwClasses + c];
+    if (st0 != kWDead) {
+      uint32_t st = st0, p = i + l, last = uc_word_accepting(st) ? p : i, erun = p;
+      bool dead = false;
+      while (p < n) {
+        const uint32_t w = cls[p];
+        if (w == 0xFFu) { *bad = true; return false; }
+        const uint32_t cw = w & 31u;
+        if (!uc_is_extender(cw)) {
+          const uint32_t ns = tr[st * kUwClasses + cw];
+          if (ns == kWDead) { dead = true; break; }
+          st = ns;
+        }
+        p += (w >> 5) + 1;
+        if (uc_word_accepting(st)) last = p;
+        else if (st == kWELead) erun = p;
+      }
+      if (!dead) *at_end = true;
+      if (last > i) { *ts = i; *te = last; *pos = last; return true; }
+      uint32_t q = i + l;
+      while (q < erun && (cls[q] & 31u) != kUcExtendSA) q += (cls[q] >> 5) + 1;
+      *pos = q;
+      continue;
+    }
+    if (c == kUcOther || c == kUcExtend || c == kUcZWJ || c == kUcMidLetter || c == kUcMidNumLet ||
+        c == kUcMidNum || c == kUcSQuote || c == kUcDQuote) {
+      *pos = i + l;
+      continue;
+    }
+    const UwClassSrcRef src{cls};
+    uint64_t p64 = i, ts64, te64;
+    if (!uc_next_span(src, n, &p64, (uint64_t)i + 1, &ts64, &te64, bad)) {
+      *pos = (uint32_t)p64;
+      if (*bad) return false;
+      continue;
+    }
+    // SA runs / Han / emoji units: conservatively, a span ending near the window end is unknown
+    if (te64 + 8 >= n) *at_end = true;
+    *ts = (uint32_t)ts64; *te = (uint32_t)te64; *pos = (uint32_t)p64;
+    return true;
+  }
+  return false;
+}
+
+__global__ void __launch_bounds__(64) k_tokenize_uchunk(BuildParams p) {
+  __shared__ UwSmem sm;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t n_units = *p.uchunk_count;
+  if (blockIdx.x >= n_units) return;                        // block-uniform
+  for (uint32_t e = lane; e < kUwStates * kUwClasses; e += 64)
+    sm.tr[e] = (uint8_t)uc_word_next(e / kUwClasses, e % kUwClasses);
+  __syncthreads();
+  for (uint32_t it = blockIdx.x; it < n_units; it += gridDim.x) {
+    const uint32_t u = p.uchunk_list[it];
+    const ChunkMeta m = chunk_meta(p, u);
+    const uint64_t src = p.live_map ? p.live_map[m.d] : m.d;
+    const bool doc_end = m.s0 + m.L == p.offsets[src + 1];  // the window reaches the document's end
+    const uint32_t L = (uint32_t)m.L;
+    // ---- stage the window (aligned 16 B loads) + clear the table
+    const uint32_t nchunks = (m.shift + L + 15) >> 4;
+    const uint4 *gsrc = reinterpret_cast<const uint4 *>(p.text + m.s0 - m.shift);
+    uint4 *dst = reinterpret_cast<uint4 *>(sm.text);
+    for (uint32_t c = lane; c < nchunks; c += 64) dst[c] = gsrc[c];
+    for (uint32_t s = lane; s < kUwSlots; s += 64) { sm.klo[s] = 0; sm.khi[s] = 0; sm.cnt[s] = 0; }
+    __syncthreads();
+    const uint8_t *doc = sm.text + m.shift;
+    // ---- classes (a char cut by the window's edges is 0xFF: a scan never lands there unless it must fail)
+    for (uint32_t j = 0; j < 64; j += 4) {
+      const uint32_t i0 = 64 * lane + j;
+      for (uint32_t q = i0; q < i0 + 4 && q < L; q++) {
+        const uint32_t x = doc[q];
+        uint32_t v;
+        if (x < 0x80u) v = uc_ascii_class(x);
+        else if ((x & 0xC0u) == 0x80u) v = 0xFFu;
+        else {
+          uint32_t l;
+          const uint32_t cp = utf8_decode(doc, L, q, &l);
+          v = cp == kUcBad ? 0xFFu : (uc_class(cp) | ((l - 1) << 5));
+        }
+        sm.cls[q] = (uint8_t)v;
+      }
+    }
+    __syncthreads();
+    // ---- scan origin: a split point at or before the core (the document's start for its first unit)
+    uint32_t start0 = m.core_lo;
+    bool fail = false;
+    if (m.core_lo > 0) {
+      // latest q in [1, core_lo] whose preceding byte is a split byte (lanes test 64 candidates)
+      const uint32_t q = m.core_lo - lane;
+      const bool ok = lane < m.core_lo && uc_split_byte(doc[q - 1]);
+      const uint64_t bm = __ballot(ok);
+      if (bm) start0 = m.core_lo - (uint32_t)__builtin_ctzll(bm);
+      else fail = true;                                       // no split point in the leading margin
+    }
+    // ---- slices: lane l scans tokens starting in [cut(l), cut(l + 1)); counted if they start in the core
+    const uint32_t hi = m.core_hi;
+    const uint32_t seg = (hi - start0 + 63) >> 6;
+    auto cut = [&](uint32_t t) -> uint32_t {
+      if (t == 0) return start0;
+      uint32_t q = start0 + t * seg;
+      if (q >= hi) return hi;
+      while (q < hi && !uc_split_byte(doc[q - 1])) q++;
+      return q;
+    };
+    uint32_t pos = fail ? hi : cut(lane);
+    const uint32_t stop = fail ? hi : cut(lane + 1);
+    bool active = pos < stop, ubad = false, overflow = false, at_end = false, collide = false;
+    while (__any(active)) {
+      uint64_t lo = 0, khv = 0;
+      bool have = false;
+      uint32_t ts32 = 0, te32 = 0;
+      if (active) {
+        uint32_t p32 = pos;
+        have = uc_window_span(sm.cls, sm.tr, L, &p32, stop, &ts32, &te32, &ubad, &at_end);
+        if (have) {
+          const uint64_t cutp = uc_token_key(doc, L, ts32, te32, &lo, &khv, p.hash_seed);
+          if (cutp < te32) overflow = true;                   // > 255 units: the long path cuts it
+        }
+        pos = p32;
+        active = have;
+        have = have && ts32 >= m.core_lo;                     // tokens starting in the core only
+      }
+      uint32_t slot = dict_hash(lo, khv) >> (32 - kUwSlotBits);
+      bool done = !have;
+      for (uint32_t r = 0; r < kUwSlots && __any(!done); r++) {
+        unsigned long long old = 1;
+        if (!done) old = atomicCAS(&sm.klo[slot], 0ull, (unsigned long long)lo);
+        const bool won = !done && old == 0;
+        if (won) { sm.khi[slot] = khv; sm.kpos[slot] = ts32 | (te32 << 16); }
+        asm volatile("" ::: "memory");
+        bool match = false;
+        if (!done && !won && old == lo) match = sm.khi[slot] == khv;
+        if (match && (lo & kLoHashed)) {
+          const uint32_t kp = sm.kpos[slot], a = kp & 0xFFFFu, z = kp >> 16;
+          collide |= !uc_same_term(doc + a, z - a, doc + ts32, te32 - ts32);
+        }
+        if (won || match) {
+          atomicAdd(&sm.cnt[slot], 1u);
+          done = true;
+        } else if (!done) {
+          slot = (slot + 1) & (kUwSlots - 1);
+        }
+      }
+      overflow |= !done;
+    }
+    if (collide) set_build_err(p.err, kErrCollision, (uint32_t)m.d);
+    uint32_t occ = 0;
+    for (uint32_t s = lane; s < kUwSlots; s += 64) occ += sm.khi[s] != 0;
+    const uint32_t nu = (uint32_t)__builtin_amdgcn_readlane((int)uw_incl_add(occ, lane), 63);
+    if (fail || __any(ubad) || __any(overflow) || (__any(at_end) && !doc_end) || nu > kPairWords) {
+      if (lane == 0) p.chunk_fail[m.gi] = 1u;                // wave-uniform: the document goes to the long path
+      __syncthreads();
+      continue;
+    }
+    // ---- dictionary slots (8 lookups per lane in flight); bucket counts
+    const uint32_t bsh = p.pair_bshift, nb = p.pair_nb, bmask = (1u << bsh) - 1u;
+    uint32_t *bcnt = sm.rcnt;                                 // [0, 64) counts, then starts
+    bcnt[lane] = 0;
+    __syncthreads();
+    for (int h = 0; h < 2; h++) {
+      uint64_t klo[8], khi[8], mine[8];
+      bool act[8], cl[8];
+      uint32_t g[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint32_t s = lane + 64 * (8 * h + k);
+        klo[k] = sm.klo[s];
+        khi[k] = sm.khi[s];
+        act[k] = khi[k] != 0;
+        const uint32_t kp = sm.kpos[s];
+        mine[k] = dict_ref_word(m.s0 + (kp & 0xFFFFu), (kp >> 16) - (kp & 0xFFFFu));
+        if (!act[k]) { klo[k] = 1; khi[k] = kKeyValid; }
+      }
+      dict_lookup_multi<8>(p.dict, p.cap_mask, klo, khi, act, g, mine, cl);
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        if (!act[k]) continue;
+        if ((klo[k] & kLoHashed) && !cl[k] && g[k] != kInvalidSlot) dict_verify(p, g[k], mine[k], (uint32_t)m.d);
+        uint32_t gs = g[k];
+        if (gs == kInvalidSlot) { atomicOr(p.err, kErrCapacity); gs = 0; }
+        sm.klo[lane + 64 * (8 * h + k)] = gs;
+        atomicAdd(&bcnt[gs >> bsh], 1u);
+      }
+    }
+    __syncthreads();
+    // ---- the unit's pair list, counting-sorted by bucket (k_tokenize_chunk's format)
+    {
+      const uint32_t c = lane < nb ? bcnt[lane] : 0u;
+      const uint32_t incl = uw_incl_add(c, lane);
+      const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      uint32_t *ub = p.pair_ub + (uint64_t)u * (nb + 1);
+      if (lane < nb) ub[lane] = incl - c;
+      if (lane == 0) ub[nb] = total;
+      __syncthreads();
+      if (lane < nb) bcnt[lane] = incl - c;                   // cursors
+      __syncthreads();
+      uint32_t *stage = reinterpret_cast<uint32_t *>(sm.cls);  // classes are dead here
+      for (uint32_t s = lane; s < kUwSlots; s += 64) {
+        if (sm.khi[s] == 0) continue;
+        const uint32_t gs = (uint32_t)sm.klo[s];
+        const uint32_t at = atomicAdd(&bcnt[gs >> bsh], 1u);
+        stage[at] = ((gs & bmask) << kPairTfBits) | sm.cnt[s];
+      }
+      __syncthreads();
+      uint32_t *pr = p.pairs + (uint64_t)u * kPairWords;
+      for (uint32_t i = lane; i < total; i += 64) pr[i] = stage[i];
+    }
+    __syncthreads();
+  }
+}
+
+hipError_t launch_tokenize_uchunk(const BuildParams &p, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(k_tokenize_uchunk, dim3(grid), dim3(64), 0, s, p);
+  return hipGetLastError();
+}
+
 }  // namespace tfidf

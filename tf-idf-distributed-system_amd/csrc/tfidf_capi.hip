@@ -198,7 +198,7 @@ struct tfidf_index {
     return term_major ? tdf.as<uint32_t>() : blk.as<uint32_t>() + (size_t)n_blocks * C;
   }
   DevBuf lt_keys, lt_cnt, lt_g;
-  DevBuf pairs, pair_ub, chunk_list, chunk_docs, chunk_fail;   // book-sized documents (chunk-parallel)
+  DevBuf pairs, pair_ub, chunk_list, chunk_docs, chunk_fail, uchunk;   // book-sized documents (chunk-parallel)
   PinnedVec<uint32_t> ldocs_h, pre_h;                            // their host staging
   PinnedVec<uint64_t> hctr_h;                                    // build counters read back after the tokenizers
   uint64_t long_chunked = 0;           // long documents the chunk path took in the last commit
@@ -306,7 +306,7 @@ extern "C" int tfidf_destroy(tfidf_index *ix) {
   hipStreamSynchronize(ix->copy_stream);
   DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->d_live_map, &ix->dict, &ix->csr, &ix->csr_esc, &ix->doc_len,
                     &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->long_list, &ix->uni_list, &ix->counters, &ix->blk,
-                    &ix->retry_list, &ix->bad_list, &ix->bbase, &ix->post, &ix->post_tmp, &ix->post_esc, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->lt_pos, &ix->verify_defer, &ix->pairs, &ix->pair_ub, &ix->chunk_list, &ix->chunk_docs, &ix->chunk_fail, &ix->canon_of_slot,
+                    &ix->retry_list, &ix->bad_list, &ix->bbase, &ix->post, &ix->post_tmp, &ix->post_esc, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->lt_pos, &ix->verify_defer, &ix->pairs, &ix->pair_ub, &ix->chunk_list, &ix->chunk_docs, &ix->chunk_fail, &ix->uchunk, &ix->canon_of_slot,
                     &ix->q_off, &ix->q_slot, &ix->q_w, &ix->q_role, &ix->q_meta, &ix->cache, &ix->cand, &ix->cand_n, &ix->out_doc,
                     &ix->out_score, &ix->out_n, &ix->q_in, &ix->q_out, &ix->hits, &ix->hits_n, &ix->hits_c, &ix->hits_s, &ix->hits_P, &ix->sort_tmp,
                     &ix->row_off, &ix->tvals, &ix->toff, &ix->tdf, &ix->term_tmp, &ix->term_esc, &ix->sent_slot, &ix->vcounts, &ix->vnu,
@@ -924,6 +924,7 @@ static int commit_once(tfidf_index *ix) {
     HIP_TRY(ix->chunk_list.reserve(pre.size() * 4 + 8));
     HIP_TRY(ix->chunk_docs.reserve((size_t)n_long * 4));
     HIP_TRY(ix->chunk_fail.reserve((size_t)n_long * 4));
+    HIP_TRY(ix->uchunk.reserve(max_units * 4 + 16));     // [0] count, [4 ..] units with non-ASCII text
     HIP_TRY(ix->pre_h.resize(pre.size()));
     memcpy(ix->pre_h.data(), pre.data(), pre.size() * 4);
     HIP_TRY(hipMemcpyAsync(ix->chunk_list.p, ix->pre_h.data(), pre.size() * 4, hipMemcpyHostToDevice, s));
@@ -942,8 +943,16 @@ static int commit_once(tfidf_index *ix) {
       cp.pair_ub = ix->pair_ub.as<uint32_t>();
       cp.pair_bshift = bsh;
       cp.pair_nb = nb;
+      // units with non-ASCII text: the Unicode chunk kernel (TFIDF_NO_UCHUNK: their
+      // documents go to k_tokenize_long whole, as before round 4; A/B only)
+      const bool uch = !getenv("TFIDF_NO_UCHUNK");
+      cp.uchunk_count = uch ? ix->uchunk.as<uint32_t>() : nullptr;
+      cp.uchunk_list = uch ? ix->uchunk.as<uint32_t>() + 4 : nullptr;
+      if (uch) HIP_TRY(hipMemsetAsync(ix->uchunk.p, 0, 4, s));
       const uint64_t grid = std::min<uint64_t>(cp.n_chunks, (uint64_t)ix->num_cus * kWaveWGsPerCU);
       HIP_TRY(launch_tokenize_chunks(cp, (int)grid, s));
+      if (uch)      // the count is read on the device: exits at once when no unit was listed
+        HIP_TRY(launch_tokenize_uchunk(cp, (int)std::min<uint64_t>(cp.n_chunks, (uint64_t)ix->num_cus * kUwaveWGsPerCU), s));
       HIP_TRY(launch_long_rows(cp, (uint32_t)n, s));
     }
     uint32_t n_fb = 0;

@@ -80,6 +80,10 @@ struct BuildParams {
   uint32_t *pair_ub;
   uint32_t pair_bshift, pair_nb;
   uint32_t *chunk_fail;
+  // units whose window holds non-ASCII text: k_tokenize_chunk lists them for
+  // k_tokenize_uchunk (nullptr: such a unit fails its document)
+  uint32_t *uchunk_list;
+  uint32_t *uchunk_count;
 };
 
 __host__ __device__ inline uint64_t csr_row_base(const uint64_t *offsets, uint64_t src) {
@@ -257,6 +261,7 @@ constexpr uint32_t kPairTfBits = 12;                    // tf field of a pair wo
 hipError_t launch_tokenize_chunks(const BuildParams &p, int grid, hipStream_t s);
 hipError_t launch_long_rows(const BuildParams &p, uint32_t n_docs, hipStream_t s);
 hipError_t launch_tokenize_uwave(const BuildParams &p, int grid, hipStream_t s);   // kernels_unicode.hip
+hipError_t launch_tokenize_uchunk(const BuildParams &p, int grid, hipStream_t s);  // kernels_unicode.hip
 constexpr uint32_t kUwaveWGsPerCU = 4;    // 64-thread workgroups, ~33 KB LDS each
 hipError_t launch_verify_deferred(const BuildParams &p, hipStream_t s);           // kernels_index.hip
 hipError_t launch_df_partial(const PostingParams &p, hipStream_t s);
@@ -407,5 +412,45 @@ hipError_t synth_doc_text(uint64_t seed, uint64_t n_docs, uint64_t doc_base, con
                           const uint32_t *guide, uint32_t V, uint32_t len_min, uint32_t len_max,
                           const uint64_t *offsets, uint8_t *text, hipStream_t s);
 hipError_t exclusive_scan_u64(const uint64_t *in, uint64_t *out, uint64_t n, hipStream_t s);
+
+#if defined(__HIPCC__)
+// Book-sized documents: unit = (document, kCoreBytes core) with context
+// margins (k_tokenize_chunk, k_tokenize_uchunk).
+constexpr uint32_t kCoreBytes = kLongCoreBytes;
+constexpr uint32_t kPreBytes = 64;
+constexpr uint32_t kPostBytes = 320;
+static_assert(kPreBytes + kCoreBytes + kPostBytes + 16 <= 4096, "chunk window: a wave window holds it");
+
+struct ChunkMeta {
+  uint64_t s0, L;                 // window: corpus bytes [s0, s0 + L)
+  uint32_t shift, core_lo, core_hi, gi;
+  uint64_t d;
+};
+
+__device__ __forceinline__ ChunkMeta chunk_meta(const BuildParams &p, uint64_t u) {
+  // group document holding unit u: chunk_pre[gi] <= u < chunk_pre[gi + 1] (binary search, scalar loads)
+  uint32_t lo = 0, hi = p.n_group_docs;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (p.chunk_pre[mid] <= u) lo = mid; else hi = mid;
+  }
+  const uint2 e = make_uint2(lo, (uint32_t)(u - p.chunk_pre[lo]));
+  ChunkMeta m;
+  m.gi = e.x;
+  m.d = p.chunk_docs[e.x];
+  const uint64_t src = p.live_map ? p.live_map[m.d] : m.d;
+  const uint64_t dlo = p.offsets[src], dl = p.offsets[src + 1] - dlo;
+  const uint64_t clo = (uint64_t)e.y * kCoreBytes, chi = min(dl, clo + kCoreBytes);
+  const uint64_t ws = clo > kPreBytes ? clo - kPreBytes : 0, we = min(dl, chi + kPostBytes);
+  m.s0 = dlo + ws;
+  m.L = we - ws;
+  m.core_lo = (uint32_t)(clo - ws);
+  m.core_hi = (uint32_t)(chi - ws);
+  m.shift = (uint32_t)(reinterpret_cast<uintptr_t>(p.text + m.s0) & 15);
+  return m;
+}
+
+
+#endif
 
 }  // namespace tfidf

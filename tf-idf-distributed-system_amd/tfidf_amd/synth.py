@@ -147,6 +147,28 @@ class DeviceCorpus:
         _h2d(self.d_text, text, text.nbytes, self.device)
         return int(starts.size)
 
+    def inject_unicode_every(self, every, seed=SEED + 11):
+        """Book-like text: about one non-ASCII word per `every` bytes of every
+        document (same byte length): at each target position the next word
+        start's first two letters become U+00E9 (C3 A9).  Returns the number of
+        words changed."""
+        if every <= 0:
+            return 0
+        text, offs = self.to_host()
+        t = text
+        # word starts with two letters: after a separator byte (or at 0)
+        is_l = (t >= 97) & (t <= 122)
+        st = np.nonzero(is_l[1:-1] & is_l[2:] & ((t[:-2] == 32) | (t[:-2] == 10)))[0] + 1
+        rng = np.random.default_rng(seed)
+        tgt = np.arange(0, len(t), every, dtype=np.int64) + rng.integers(0, max(every // 2, 1), 1)[0]
+        i = np.searchsorted(st, tgt)
+        i = np.unique(i[i < len(st)])
+        pos = st[i]
+        text[pos] = 0xC3
+        text[pos + 1] = 0xA9
+        _h2d(self.d_text, text, text.nbytes, self.device)
+        return int(pos.size)
+
     def free(self):
         from . import _lib as L
         if self.d_text:
