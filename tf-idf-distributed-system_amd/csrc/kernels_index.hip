@@ -503,6 +503,71 @@ __device__ __forceinline__ uint64_t lane_word_mask(const uint8_t *text, uint32_t
   return W;
 }
 
+// The same masks from the staged window chunks still in registers (round 4):
+// row k of the window = chunks 64 k .. 64 k + 63, lane l holding chunk
+// 64 k + l = window bytes [16 (64 k + l), +16); only the rows the document
+// reaches (nrows) are classified.  A chunk's 16 word bits go to LDS (wm16[c],
+// PACK: the pre-joiner bits to wb16[c]) and lane L reads back its contiguous
+// 64-byte segment (chunks 4 L .. 4 L + 3) as one u64: no strided ds_read_b128
+// of the text (the round-3 classify's bank conflicts) and no work on the rows
+// past the document.  Neighbour bytes across chunks by wave shuffles, across
+// rows from the staged text (lanes 0 / 63).
+template <bool PACK>
+__device__ __forceinline__ uint64_t regs_word_mask(const uint4 *v, uint32_t nrows, const uint8_t *text,
+                                                   uint16_t *wm16, uint16_t *wb16, uint32_t lane, bool *bad,
+                                                   bool *under, uint64_t *wbase, bool *upper) {
+  uint32_t badacc = 0, U = 0, us = 0;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    if ((uint32_t)k >= nrows) break;                          // wave-uniform
+    const uint32_t x[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+    uint32_t LD[4], P = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint32_t D = swar_digit(x[i]);
+      const uint32_t Lt = swar_letter(x[i]);
+      LD[i] = Lt | (D >> 1);
+      U |= Lt & ~(x[i] << 2);
+      badacc |= x[i];
+      P |= (x[i] + 0x59595959u) & ~(x[i] + 0x44444444u) & ~D;
+    }
+    uint32_t ldp = (uint32_t)__shfl_up((int)LD[3], 1, 64);
+    uint32_t ldn = (uint32_t)__shfl_down((int)LD[0], 1, 64);
+    if (lane == 0) ldp = k ? ld_byte(text[1024 * k - 1]) << 24 : 0u;
+    if (lane == 63) ldn = k < 3 ? ld_byte(text[1024 * k + 1024]) : 0u;
+    const bool mids = __any((P & 0x80808080u) != 0);
+    uint32_t W = 0, WB = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint32_t u = swar_eq(x[i], 0x5F5F5F5Fu);
+      us |= u;
+      uint32_t c = LD[i] | (LD[i] << 1) | u;
+      if (PACK) WB |= swar_nib(c & 0x80808080u) << (4 * i);
+      if (mids) {
+        const uint32_t prev4 = i ? LD[i - 1] : ldp;
+        const uint32_t next4 = i < 3 ? LD[i + 1] : ldn;
+        const uint32_t pf = __builtin_amdgcn_alignbyte(LD[i], prev4, 3);
+        const uint32_t nf = __builtin_amdgcn_alignbyte(next4, LD[i], 1);
+        const uint32_t both = pf & nf;
+        const uint32_t dq = swar_eq(x[i], 0x2E2E2E2Eu) | swar_eq(x[i], 0x27272727u);
+        const uint32_t ml = dq | swar_eq(x[i], 0x3A3A3A3Au);
+        const uint32_t mn = dq | swar_eq(x[i], 0x2C2C2C2Cu) | swar_eq(x[i], 0x3B3B3B3Bu);
+        c |= (ml & both) | (mn & (both << 1));
+      }
+      W |= swar_nib(c & 0x80808080u) << (4 * i);
+    }
+    wm16[64 * k + lane] = (uint16_t)W;
+    if (PACK) wb16[64 * k + lane] = (uint16_t)WB;
+  }
+  asm volatile("" ::: "memory");
+  *upper = __any(U != 0);
+  *bad = __any((badacc & 0x80808080u) != 0);
+  *under = __any(us != 0);
+  const bool in = (lane >> 4) < nrows;
+  if (PACK) *wbase = in ? reinterpret_cast<const uint64_t *>(wb16)[lane] : 0ull;
+  return in ? reinterpret_cast<const uint64_t *>(wm16)[lane] : 0ull;
+}
+
 // Folded table key of a token of 9..255 bytes at tp (see above); *h slot hash.
 __device__ __noinline__ uint64_t fold_key(const uint8_t *text, uint32_t tp, uint32_t n, uint32_t *h, bool *valid) {
   const uint32_t *tw = reinterpret_cast<const uint32_t *>(text);
@@ -1113,17 +1178,25 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
           val.w &= keep_range(16 * c + 12, shift, hi_b);
         }
         dst[c] = val;
+        v[k] = val;                                         // classified from registers below
       }
     }
-    if (un < n_units) { meta = unit_meta<PACK>(p, un, lane); prefetch_wave(p, meta, lane, v); }
     asm volatile("" ::: "memory");
-    if (p.debug_stop == 1) continue;
 
-    // ---- classify + spans -> dense token list
+    // ---- classify (window chunks in registers) + spans -> dense token list
     bool bad, under;
     uint64_t wbase = 0;
     bool upper;
-    uint64_t W = lane_word_mask<PACK>(sm.text, lane, &bad, &under, &wbase, &upper);
+    uint64_t W;
+    {
+      const uint32_t nrows = (shift + (uint32_t)L + 1023) >> 10;
+      uint16_t *wm16 = reinterpret_cast<uint16_t *>(sm.list);            // the token list is written after
+      W = regs_word_mask<PACK>(v, nrows, sm.text, wm16, wm16 + 256, lane, &bad, &under, &wbase, &upper);
+    }
+    // the next document's window, now that this one's registers are consumed
+    if (un < n_units) { meta = unit_meta<PACK>(p, un, lane); prefetch_wave(p, meta, lane, v); }
+    asm volatile("" ::: "memory");
+    if (p.debug_stop == 1) continue;
     // PACK: document boundaries q_j (window position of document j's first
     // byte, j >= 1).  No token spans one: a joiner next to q_j that is a word
     // byte only through its neighbour across q_j is dropped, and a token is
@@ -1351,515 +1424,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     }
   }
   if (my_ttf | my_nnz | my_doc_count) {                    // lane 0 (PACK: lanes < pack)
-    atomicAdd(&TFIDF_COLD(stats)[0], my_doc_count);
-    atomicAdd(&TFIDF_COLD(stats)[1], my_ttf);
-    atomicAdd(&TFIDF_COLD(stats)[2], my_nnz);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Workgroup-per-document tokenizer (round 4; the ASCII one-document-per-window
-// path of k_tokenize_wave).  Four waves share one document and one LDS arena,
-// so a CU keeps eight documents in flight as before, but every SIMD now hosts
-// eight waves instead of two: each wave holds two tokens / terms per lane (not
-// eight), so the kernel fits in ~64 VGPRs, and the LDS / L2 round trips of one
-// wave are covered by the others' work (the one-wave kernel left its SIMD idle
-// ~40 % of the time).  Phases meet at workgroup barriers that order
-// LDS only (lds_barrier: the next document's prefetch and the CSR stores stay
-// in flight across them):
-//   stage    : thread t holds window chunk t (16 B) of the next document in
-//              registers (prefetched one document ahead), writes it to LDS
-//   classify : the thread classifies its own 16 bytes in registers (SWAR; the
-//              neighbour bytes' flags by wave shuffles, LDS at wave edges) ->
-//              16 word bits; token starts S and ends E; the i-th start pairs
-//              with the i-th end, so one workgroup scan of (|S|, |E|) places
-//              every start and end of the dense token list directly
-//   histogram: tokens t + 256 k (k < 2, a pass per 512 tokens) counted in
-//              the LDS table by returning 64-bit CASes (probe_round)
-//   compact  : slots t + 256 j (j < 4) -> dense list of occupied slots (scan)
-//   dictionary: terms t + 256 k resolved in the global table (bucket / group
-//              probes, claims), folded keys one at a time
-//   CSR row  : ranks inside dictionary-range groups by LDS atomics, group
-//              bases by one wave scan, staged in LDS, stored coalesced
-constexpr uint32_t kWgThreads = 256;
-constexpr uint32_t kWgK = 2;                          // tokens / terms per thread per pass
-static_assert(kWgThreads * 16 == kWaveWindow, "one 16 B window chunk per thread");
-static_assert(kWgThreads * kWgK * 2 == kWaveTokens && kWgThreads * kWgK == kWaveTerms, "capacities");
-
-struct WgSmem {
-  alignas(16) uint8_t text[kWaveWindow + 32];    // +32 (zero): key reads run past a token's end
-  alignas(16) uint64_t key[kWaveSlots];          // term table
-  alignas(16) uint32_t cnt[kWaveSlots / 2];      // u16 counts, two per word
-  alignas(16) uint32_t list[kWaveTokens];        // token spans (start | end << 16); occupied slots (u16); CSR staging
-  alignas(16) uint2 sel[64];                     // key byte-selector table (init_sel_table)
-  uint32_t gcnt[kWaveGroups];                    // CSR row: per-range counters, then exclusive bases
-  uint32_t red[4][4];                            // cross-wave totals: [site][wave]
-  uint32_t flg[4];                               // per wave: bad | under << 1 | upper << 2 | overflow << 3
-};
-
-// exclusive prefix of x over the workgroup (thread order) and the total; red:
-// this call site's four words
-__device__ __forceinline__ uint32_t wg_scan(uint32_t x, uint32_t *red, uint32_t *total) {
-  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint32_t inc = wave_incl_add(x);
-  if (lane == 63) red[w] = inc;
-  lds_barrier();
-  const uint32_t r0 = red[0], r1 = red[1], r2 = red[2], r3 = red[3];
-  *total = r0 + r1 + r2 + r3;
-  return (w > 0 ? r0 : 0u) + (w > 1 ? r1 : 0u) + (w > 2 ? r2 : 0u) + inc - x;
-}
-
-// word bit (UAX#29 ASCII rules, lane_word_mask) of window byte q from its
-// staged neighbours: the thread that starts at q + 1 needs it at a wave edge
-__device__ __forceinline__ uint32_t word_bit_at(const uint8_t *text, uint32_t q) {
-  const uint32_t c = text[q], cp = q ? text[q - 1] : 0u, cn = text[q + 1];
-  const uint32_t f = ld_byte(c);
-  if (f || c == '_') return 1u;
-  const uint32_t both = ld_byte(cp) & ld_byte(cn);            // bit 7 letters, bit 6 digits
-  const bool ml = c == '.' || c == '\'' || c == ':';
-  const bool mn = c == '.' || c == '\'' || c == ',' || c == ';';
-  return ((ml && (both & 0x80u)) || (mn && (both & 0x40u))) ? 1u : 0u;
-}
-
-// One pass of up to 512 tokens [tb, tb + 512) of the list: tokens tb + t + 256 k.
-template <bool FOLD>
-__device__ __forceinline__ void hist_wg(WgSmem &sm, uint32_t t, uint32_t lane, uint32_t tb, uint32_t ntok, bool under,
-                                        bool upper, uint32_t &claims, uint32_t &toks, bool &overflow) {
-  constexpr int K = (int)kWgK;
-  const uint32_t *tw = reinterpret_cast<const uint32_t *>(sm.text);
-  uint32_t ent[K], dw[K][3];
-  uint2 sl[K];
-  bool in[K];
-#pragma unroll
-  for (int k = 0; k < K; k++) {
-    const uint32_t i = tb + t + kWgThreads * k;
-    in[k] = i < ntok;
-    ent[k] = in[k] ? sm.list[i] : 0u;
-  }
-#pragma unroll
-  for (int k = 0; k < K; k++) {
-    const uint32_t tp = ent[k] & kSpanMask, n = ((ent[k] >> 16) & kSpanMask) - tp;
-    const uint32_t a0 = tp >> 2;
-    dw[k][0] = tw[a0]; dw[k][1] = tw[a0 + 1]; dw[k][2] = tw[a0 + 2];
-    sl[k] = sm.sel[(min(n, 8u) << 2) | (tp & 3u)];
-  }
-  uint64_t tkey[K], pm[K];
-  uint32_t slot[K], t0[K], t1[K];
-#pragma unroll
-  for (int k = 0; k < K; k++) {
-    t0[k] = __builtin_amdgcn_perm(dw[k][1], dw[k][0], sl[k].x);
-    t1[k] = __builtin_amdgcn_perm(dw[k][2], dw[k][1], sl[k].y);
-  }
-  if (upper) {
-#pragma unroll
-    for (int k = 0; k < K; k++) { t0[k] = lower4(t0[k]); t1[k] = lower4(t1[k]); }
-  }
-#pragma unroll
-  for (int k = 0; k < K; k++) {
-    const uint32_t tp = ent[k] & kSpanMask, n = ((ent[k] >> 16) & kSpanMask) - tp;
-    bool valid = true;
-    if (FOLD && under)   // a span of '_' only is not a token
-      valid = (t0[k] != __builtin_amdgcn_perm(0x5F5F5F5Fu, 0x5F5F5F5Fu, sl[k].x)) |
-              (t1[k] != __builtin_amdgcn_perm(0x5F5F5F5Fu, 0x5F5F5F5Fu, sl[k].y));
-    tkey[k] = (uint64_t)t0[k] | ((uint64_t)t1[k] << 32);
-    slot[k] = table_slot(t0[k], t1[k]);
-    pm[k] = __ballot(in[k] & (n <= 8) & valid);
-  }
-  if (FOLD) {                                            // tokens of 9..255 bytes: folded keys
-    bool toolong = false;
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-      const uint32_t tp = ent[k] & kSpanMask, n = ((ent[k] >> 16) & kSpanMask) - tp;
-      bool ok = false;
-      if (in[k] && n > 8) {
-        if (n > kMaxTokenLen) {
-          toolong = true;
-        } else {
-          uint32_t h;
-          tkey[k] = fold_key(sm.text, tp, n, &h, &ok);
-          slot[k] = h >> (32 - kWaveSlotBits);
-        }
-      }
-      pm[k] |= __ballot(ok);
-    }
-    if (__any(toolong)) { overflow = true; return; }     // > 255 chars: the long path cuts it
-  }
-  uint32_t P = 0;
-#pragma unroll
-  for (int k = 0; k < K; k++) P += (uint32_t)__popcll(pm[k]);
-  toks += P;
-  for (uint32_t round = 0; P > 0; round++) {
-    if (round >= kWaveSlots) { overflow = true; return; }
-    P = probe_round<K, FOLD>(sm, lane, tkey, slot, pm, claims);
-  }
-}
-
-// Dictionary slot of a folded (> 8 byte) table key of the staged window
-// (wbase = corpus offset of window byte 0): the exact 128-bit key, find or
-// insert, the identity check of hashed keys.  Out of line: its key builder and
-// probe state would otherwise raise the workgroup tokenizer's register peak
-// for a path short-word corpora never take.  Every input arrives as an
-// argument: a callee has no kernel-argument segment of its own, so the
-// TFIDF_COLD reads of the kernels are not available here.
-struct FoldArgs {
-  uint64_t *dict;
-  const uint8_t *text;           // corpus (device): reference occurrences
-  uint64_t hash_seed;
-  uint64_t *verify_defer;
-  uint32_t *verify_count;
-  uint32_t *err;
-  uint32_t verify_cap, cap_mask;
-};
-__device__ __noinline__ uint32_t wg_fold_slot(const FoldArgs &a, const uint8_t *win, uint64_t key, bool fa,
-                                              uint64_t wbase, uint32_t doc) {
-  uint64_t flo = 1, fhi = kKeyValid, mine = 0;
-  if (fa) {
-    const uint32_t n = (uint32_t)key & 0xFFu, tp = (uint32_t)(key >> 13) & 0x1FFFu;
-    bool valid;
-    token_key(win, tp, tp + n, &flo, &fhi, &valid, a.hash_seed);
-    mine = dict_ref_word(wbase + tp, n);
-  }
-  bool cl;
-  const uint32_t gg = dict_find_or_insert(a.dict, a.cap_mask, flo, fhi, fa, &mine, &cl);
-  if (fa && (flo & kLoHashed) && !cl && gg != kInvalidSlot) {        // dict_verify
-    const uint64_t r = __hip_atomic_load(a.dict + 2 * ((size_t)a.cap_mask + 1) + gg, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
-    if (r != mine) {
-      if (r == 0) {
-        const uint32_t at = atomicAdd(a.verify_count, 1u);
-        if (at < a.verify_cap) {
-          a.verify_defer[2 * (size_t)at] = gg;
-          a.verify_defer[2 * (size_t)at + 1] = mine;
-        } else {
-          set_build_err(a.err, kErrCollision, doc);
-        }
-      } else if (!uc_same_term(a.text + dict_ref_off(r), dict_ref_len(r), a.text + dict_ref_off(mine),
-                               dict_ref_len(mine))) {
-        set_build_err(a.err, kErrCollision, doc);
-      }
-    }
-  }
-  return gg;
-}
-
-template <bool G4>
-#ifdef TFIDF_WG_WPE
-#define TFIDF_WG_ATTR __attribute__((amdgpu_waves_per_eu(TFIDF_WG_WPE)))
-#else
-#define TFIDF_WG_ATTR
-#endif
-__global__ void __launch_bounds__(kWgThreads) TFIDF_WG_ATTR k_tokenize_wg(BuildParams p) {
-  __shared__ WgSmem sm;
-  constexpr int K = (int)kWgK;
-  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
-  {
-    // table starts empty; every document leaves it empty
-    uint4 *kw = reinterpret_cast<uint4 *>(sm.key);
-    uint4 *cw = reinterpret_cast<uint4 *>(sm.cnt);
-    kw[t] = make_uint4(0, 0, 0, 0);
-    kw[t + 256] = make_uint4(0, 0, 0, 0);
-    if (t < 128) cw[t] = make_uint4(0, 0, 0, 0);
-    if (t < 2) reinterpret_cast<uint4 *>(sm.text + kWaveWindow)[t] = make_uint4(0, 0, 0, 0);
-    if (w == 0) init_sel_table(sm.sel, lane);
-  }
-  unsigned long long my_doc_count = 0, my_ttf = 0, my_nnz = 0;
-  uint4 v = make_uint4(0, 0, 0, 0);
-  const uint64_t n_units = TFIDF_COLD(doc_list) ? *TFIDF_COLD(doc_list_count) : p.n_docs;
-  DocMeta meta;
-  auto prefetch = [&](const DocMeta &m) {
-    if (!fits_wave(m)) return;
-    const uint32_t nchunks = (uint32_t)((m.shift + m.L + 15) >> 4);
-    const uint4 *src = reinterpret_cast<const uint4 *>(reinterpret_cast<uintptr_t>(p.text + m.s0) & ~(uintptr_t)15);
-    if (t < nchunks) v = gload16(src + t);
-  };
-  if (blockIdx.x < n_units) {
-    meta = unit_meta<false>(p, blockIdx.x, lane);
-    prefetch(meta);
-  }
-  const uint32_t R = p.n_ranges;
-  uint16_t *slots = reinterpret_cast<uint16_t *>(sm.list);
-  lds_barrier();
-
-  for (uint64_t u = blockIdx.x; u < n_units; u += gridDim.x) {
-    const uint64_t d = meta.d, src = meta.src, L = meta.L, s0 = meta.s0;
-    const uint32_t shift = meta.shift;
-    const bool fits = fits_wave(meta);
-    const uint64_t un = u + gridDim.x;
-    if (!fits) {
-      if (t == 0) TFIDF_COLD(long_list)[atomicAdd(TFIDF_COLD(long_count), 1u)] = (uint32_t)d;
-      if (un < n_units) { meta = unit_meta<false>(p, un, lane); prefetch(meta); }
-      continue;                                             // workgroup-uniform
-    }
-    // ---- stage: window chunk t (bytes outside the document zeroed)
-    uint4 x;
-    {
-      const uint32_t hi_b = shift + (uint32_t)L;
-      const uint32_t nchunks = (hi_b + 15) >> 4;
-      x = t < nchunks ? v : make_uint4(0, 0, 0, 0);
-      if (t == 0 || t == nchunks - 1) {
-        x.x &= keep_range(16 * t, shift, hi_b);
-        x.y &= keep_range(16 * t + 4, shift, hi_b);
-        x.z &= keep_range(16 * t + 8, shift, hi_b);
-        x.w &= keep_range(16 * t + 12, shift, hi_b);
-      }
-      reinterpret_cast<uint4 *>(sm.text)[t] = x;
-    }
-    if (t < kWaveGroups) sm.gcnt[t] = 0;
-    if (un < n_units) { meta = unit_meta<false>(p, un, lane); prefetch(meta); }
-    lds_barrier();                                          // #1 text staged
-
-    // ---- classify the thread's 16 bytes (registers)
-    uint32_t S, E, flags;
-    {
-      const uint32_t xs[4] = {x.x, x.y, x.z, x.w};
-      uint32_t LD[4], badacc = 0, P = 0, U = 0, us = 0;
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const uint32_t D = swar_digit(xs[i]);
-        const uint32_t Lt = swar_letter(xs[i]);
-        LD[i] = Lt | (D >> 1);
-        U |= Lt & ~(xs[i] << 2);
-        badacc |= xs[i];
-        P |= (xs[i] + 0x59595959u) & ~(xs[i] + 0x44444444u) & ~D;
-      }
-      uint32_t ldp = (uint32_t)__shfl_up((int)LD[3], 1, 64);
-      uint32_t ldn = (uint32_t)__shfl_down((int)LD[0], 1, 64);
-      if (lane == 0) ldp = t ? ld_byte(sm.text[16 * t - 1]) << 24 : 0u;
-      if (lane == 63) ldn = ld_byte(sm.text[16 * t + 16]);   // text[4096] is zero
-      const bool mids = __any((P & 0x80808080u) != 0);
-      uint32_t W = 0;
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const uint32_t uu = swar_eq(xs[i], 0x5F5F5F5Fu);
-        us |= uu;
-        uint32_t c = LD[i] | (LD[i] << 1) | uu;
-        if (mids) {
-          const uint32_t prev4 = i ? LD[i - 1] : ldp;
-          const uint32_t next4 = i < 3 ? LD[i + 1] : ldn;
-          const uint32_t pf = __builtin_amdgcn_alignbyte(LD[i], prev4, 3);
-          const uint32_t nf = __builtin_amdgcn_alignbyte(next4, LD[i], 1);
-          const uint32_t both = pf & nf;
-          const uint32_t dq = swar_eq(xs[i], 0x2E2E2E2Eu) | swar_eq(xs[i], 0x27272727u);
-          const uint32_t ml = dq | swar_eq(xs[i], 0x3A3A3A3Au);
-          const uint32_t mn = dq | swar_eq(xs[i], 0x2C2C2C2Cu) | swar_eq(xs[i], 0x3B3B3B3Bu);
-          c |= (ml & both) | (mn & (both << 1));
-        }
-        W |= swar_nib(c & 0x80808080u) << (4 * i);
-      }
-      // word bit of the byte before this thread's bytes
-      uint32_t prevb = ((uint32_t)__shfl_up((int)W, 1, 64) >> 15) & 1u;
-      if (lane == 0) prevb = t ? word_bit_at(sm.text, 16 * t - 1) : 0u;
-      S = W & ~((W << 1) | prevb) & 0xFFFFu;
-      E = ~W & ((W << 1) | prevb) & 0xFFFFu;
-      if (t == kWgThreads - 1 && (W >> 15)) E |= 1u << 16;  // a word running to the window end
-      flags = (__any((badacc & 0x80808080u) != 0) ? 1u : 0u) | (__any(us != 0) ? 2u : 0u) |
-              (__any(U != 0) ? 4u : 0u);
-    }
-    if (lane == 0) sm.flg[w] = flags;
-    uint32_t tot;
-    const uint32_t se = wg_scan((uint32_t)__popc(S) | ((uint32_t)__popc(E) << 16), sm.red[0], &tot);   // #2
-    const uint32_t fl = sm.flg[0] | sm.flg[1] | sm.flg[2] | sm.flg[3];
-    const uint32_t ntok = tot & 0xFFFFu;
-    if (fl & 1u) {                                          // non-ASCII: the Unicode wave path
-      if (t == 0) TFIDF_COLD(uni_list)[atomicAdd(TFIDF_COLD(uni_count), 1u)] = (uint32_t)d;
-      continue;
-    }
-    if (ntok > kWaveTokens) {                               // too many tokens: long path
-      if (t == 0) TFIDF_COLD(long_list)[atomicAdd(TFIDF_COLD(long_count), 1u)] = (uint32_t)d;
-      continue;
-    }
-    {
-      // the i-th start pairs with the i-th end: place both halves directly
-      uint16_t *tok16 = reinterpret_cast<uint16_t *>(sm.list);
-      uint32_t rs = se & 0xFFFFu, re = se >> 16;
-      while (S) {
-        tok16[2 * rs++] = (uint16_t)(16 * t + (uint32_t)__builtin_ctz(S));
-        S &= S - 1;
-      }
-      while (E) {
-        tok16[2 * re++ + 1] = (uint16_t)(16 * t + (uint32_t)__builtin_ctz(E));
-        E &= E - 1;
-      }
-    }
-    lds_barrier();                                          // #3 token list complete
-
-    // ---- histogram
-    const bool under = (fl & 2u) != 0, upper = (fl & 4u) != 0;
-    uint32_t claims = 0, toks = 0;
-    bool overflow = false;
-    for (uint32_t tb = 0; tb < ntok && !overflow; tb += kWgThreads * K) {
-      bool fold = under;
-#pragma unroll
-      for (int k = 0; k < K; k++) {
-        const uint32_t i = tb + t + kWgThreads * k;
-        if (i < ntok) {
-          const uint32_t e = sm.list[i];
-          fold |= ((e >> 16) & kSpanMask) - (e & kSpanMask) > 8;
-        }
-      }
-      if (__any(fold)) hist_wg<true>(sm, t, lane, tb, ntok, under, upper, claims, toks, overflow);
-      else hist_wg<false>(sm, t, lane, tb, ntok, under, upper, claims, toks, overflow);
-    }
-    if (lane == 0) { sm.red[1][w] = claims; sm.red[2][w] = toks; sm.flg[w] = overflow ? 8u : 0u; }
-    lds_barrier();                                          // #4 table complete
-    const uint32_t nu = sm.red[1][0] + sm.red[1][1] + sm.red[1][2] + sm.red[1][3];
-    const uint32_t len = sm.red[2][0] + sm.red[2][1] + sm.red[2][2] + sm.red[2][3];
-    const bool ovf = ((sm.flg[0] | sm.flg[1] | sm.flg[2] | sm.flg[3]) & 8u) != 0;
-
-    // ---- occupied slots t + 256 j -> dense list
-    uint32_t occ = 0;
-#pragma unroll
-    for (int j = 0; j < 4; j++) occ |= (sm.key[t + kWgThreads * j] != 0 ? 1u : 0u) << j;
-    if (ovf || nu > kWaveTerms) {                           // workgroup-uniform: long path
-#pragma unroll
-      for (int j = 0; j < 4; j++) sm.key[t + kWgThreads * j] = 0;
-      if (t < 128) reinterpret_cast<uint4 *>(sm.cnt)[t] = make_uint4(0, 0, 0, 0);
-      if (t == 0) TFIDF_COLD(long_list)[atomicAdd(TFIDF_COLD(long_count), 1u)] = (uint32_t)d;
-      continue;                                             // (the next document's stage barrier orders the clear)
-    }
-    {
-      uint32_t ntot;
-      uint32_t at = wg_scan((uint32_t)__popc(occ), sm.red[3], &ntot);   // #5a
-#pragma unroll
-      for (int j = 0; j < 4; j++)
-        if ((occ >> j) & 1u) slots[at++] = (uint16_t)(t + kWgThreads * j);
-    }
-    lds_barrier();                                          // #5 slot list complete
-
-    // ---- dictionary slots of terms t + 256 k
-    const uint32_t dmask = p.cap_mask;
-    uint32_t g[K], tf[K];
-    bool act[K];
-    {
-      uint64_t lo[K];
-      uint32_t ps[K], foldm = 0;
-#pragma unroll
-      for (int k = 0; k < K; k++) {
-        const uint32_t idx = t + kWgThreads * k;
-        act[k] = idx < nu;
-        const uint32_t sidx = slots[act[k] ? idx : 0u] & (kWaveSlots - 1);
-        const uint64_t key = sm.key[sidx];
-        tf[k] = (sm.cnt[sidx >> 1] >> (16 * (sidx & 1))) & 0xFFFFu;
-        const bool f = act[k] & ((key & kFoldBit) != 0);
-        const bool sh = act[k] & !f;
-        lo[k] = sh ? key : 0ull;
-        foldm |= (uint32_t)f << k;
-        ps[k] = dict_home(dict_hash_short(lo[k]), dmask) & ~1u;
-        g[k] = sh ? kLookupPending : kInvalidSlot;        // folded ones: resolved after the short ones
-      }
-      // short terms: bucket (G4: 4-slot group) probes, both of a lane's loads in flight
-      for (uint32_t round = 0;; round++) {
-        bool pend = false;
-#pragma unroll
-        for (int k = 0; k < K; k++) pend |= g[k] == kLookupPending;
-        if (!__any(pend) || round > dmask) break;
-        ulonglong2 e0[K], e1[G4 ? K : 1];
-#pragma unroll
-        for (int k = 0; k < K; k++) {
-          const uint32_t gs = g[k] == kLookupPending ? (ps[k] & (G4 ? ~3u : ~1u)) : 0u;
-          e0[k] = *reinterpret_cast<const ulonglong2 *>(p.dict + gs);
-          if constexpr (G4) e1[k] = *reinterpret_cast<const ulonglong2 *>(p.dict + gs + 2);
-        }
-        uint32_t cs[K];
-        bool anyclaim = false;
-#pragma unroll
-        for (int k = 0; k < K; k++) {
-          const bool pk = g[k] == kLookupPending;
-          uint32_t c, r;
-          if constexpr (G4) r = group_probe(e0[k], e1[k], ps[k], lo[k], &c);
-          else r = bucket_probe(e0[k], ps[k], lo[k], &c);
-          cs[k] = pk ? c : kInvalidSlot;
-          anyclaim |= pk & (c != kInvalidSlot);
-          const bool adv = pk & (r == kLookupPending) & (c == kInvalidSlot);
-          ps[k] = adv ? (((ps[k] | (G4 ? 3u : 1u)) + 1u) & dmask) : ps[k];
-          g[k] = pk ? r : g[k];
-        }
-        if (__any(anyclaim)) {
-#pragma unroll
-          for (int k = 0; k < K; k++)
-            if (cs[k] != kInvalidSlot) g[k] = dict_claim_short(p.dict, dmask, cs[k], lo[k], &ps[k]);
-        }
-      }
-      // folded (> 8 byte) terms, after the short ones (their probe state is
-      // dead by then): exact 128-bit keys, one lookup per lane at a time
-      while (__any(foldm != 0)) {
-        uint32_t k = 0;
-        const bool fa = foldm != 0;
-        if (fa) {
-          k = (uint32_t)__builtin_ctz(foldm);
-          foldm &= foldm - 1;
-        }
-        FoldArgs fa_args;
-        fa_args.dict = p.dict;
-        fa_args.text = p.text;
-        fa_args.hash_seed = TFIDF_COLD(hash_seed);
-        fa_args.verify_defer = TFIDF_COLD(verify_defer);
-        fa_args.verify_count = TFIDF_COLD(verify_count);
-        fa_args.err = TFIDF_COLD(err);
-        fa_args.verify_cap = TFIDF_COLD(verify_cap);
-        fa_args.cap_mask = dmask;
-        const uint32_t gg = wg_fold_slot(fa_args, sm.text, sm.key[slots[t + kWgThreads * k] & (kWaveSlots - 1)], fa,
-                                         s0 - shift, (uint32_t)d);
-#pragma unroll
-        for (int kk = 0; kk < K; kk++)
-          if (fa && (uint32_t)kk == k) g[kk] = gg;
-      }
-      bool caperr = false;
-#pragma unroll
-      for (int k = 0; k < K; k++) {
-        const bool e = act[k] & ((g[k] == kInvalidSlot) | (g[k] == kLookupPending));
-        caperr |= e;
-        if (e) g[k] = 0;
-      }
-      if (caperr) set_err(TFIDF_COLD(err), kErrCapacity, (uint32_t)d);
-    }
-
-    // ---- CSR row grouped by dictionary range: ranks by LDS atomics
-    uint32_t grp[K], rank[K];
-#pragma unroll
-    for (int k = 0; k < K; k++) {
-      grp[k] = g[k] >> p.range_shift;
-      rank[k] = act[k] ? atomicAdd(&sm.gcnt[grp[k]], 1u) : 0u;
-    }
-    lds_barrier();                                          // #6 counters final; table reads done
-    // the table is free: clear it for the next document (slots t + 256 j)
-#pragma unroll
-    for (int j = 0; j < 4; j++) sm.key[t + kWgThreads * j] = 0;
-    if (t < 128) reinterpret_cast<uint4 *>(sm.cnt)[t] = make_uint4(0, 0, 0, 0);
-    if (w == 0) {
-      const uint32_t c = lane < R ? sm.gcnt[lane] : 0u;
-      const uint32_t incl = wave_incl_add(c);
-      if (lane < R) {
-        sm.gcnt[lane] = incl - c;
-        p.rsplit[d * R + lane] = incl;
-      }
-    }
-    lds_barrier();                                          // #7 group bases
-    uint32_t *st_col = sm.list, *st_tf = sm.list + kWaveTerms;
-#pragma unroll
-    for (int k = 0; k < K; k++)
-      if (act[k]) {
-        const uint32_t pos = sm.gcnt[grp[k]] + rank[k];
-        st_col[pos] = g[k];
-        st_tf[pos] = tf[k];
-      }
-    lds_barrier();                                          // #8 row staged
-    {
-      const uint64_t row = csr_row_base(p.offsets, src);
-      for (uint32_t i = t; i < nu; i += kWgThreads) csr_put(p, row + i, st_col[i], st_tf[i], (uint32_t)d);
-    }
-    if (t == 0) {
-      p.doc_len[d] = len;
-      p.doc_nuniq[d] = nu;
-      p.doc_norm[d] = (uint8_t)int_to_byte4(len);
-    }
-    // workgroup-uniform counts: scalar accumulators (no VGPRs across the loop)
-    const uint32_t ulen = (uint32_t)__builtin_amdgcn_readfirstlane((int)len);
-    my_doc_count += ulen > 0;
-    my_ttf += ulen;
-    my_nnz += (uint32_t)__builtin_amdgcn_readfirstlane((int)nu);
-  }
-  if (t == 0 && (my_ttf | my_nnz | my_doc_count)) {
     atomicAdd(&TFIDF_COLD(stats)[0], my_doc_count);
     atomicAdd(&TFIDF_COLD(stats)[1], my_ttf);
     atomicAdd(&TFIDF_COLD(stats)[2], my_nnz);
@@ -2840,11 +2404,6 @@ hipError_t launch_verify_deferred(const BuildParams &p, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_tokenize_wg(const BuildParams &p, int grid, hipStream_t s) {
-  if (p.cap_mask + 1 >= (1u << 21)) hipLaunchKernelGGL(k_tokenize_wg<true>, dim3(grid), dim3(kWgThreads), 0, s, p);
-  else hipLaunchKernelGGL(k_tokenize_wg<false>, dim3(grid), dim3(kWgThreads), 0, s, p);
-  return hipGetLastError();
-}
 hipError_t launch_tokenize_wave(const BuildParams &p, int grid, hipStream_t s) {
   const bool g4 = (uint64_t)p.cap_mask + 1 >= (1ull << 21);   // dictionary beyond L2: 4-slot probe groups
   if (p.pack > 1) {

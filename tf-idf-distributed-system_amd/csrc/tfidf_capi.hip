@@ -832,16 +832,10 @@ static int commit_once(tfidf_index *ix) {
   HIP_TRY(hipEventRecord(ix->ev[EV_START], s));
   if (N) {
     const uint64_t units = (N + pack - 1) / pack;
-    // one document per 4-wave workgroup (k_tokenize_wg) for one-document
-    // windows; packed windows (short documents) keep the wave kernel.
-    // TFIDF_TOK_WG=1 selects it (A/B; the phase stops of TFIDF_DEBUG_STOP
-    // exist in the wave kernel only).
-    const bool wg = pack <= 1 && !bp.debug_stop && getenv("TFIDF_TOK_WG");
-    uint64_t wpc = wg ? kWgWGsPerCU : kWaveWGsPerCU;
+    uint64_t wpc = kWaveWGsPerCU;
     if (const char *e = getenv("TFIDF_WAVE_WGS_PER_CU")) wpc = (uint64_t)std::max(1, atoi(e));   // profiling only
     const uint64_t grid = std::min<uint64_t>(units, (uint64_t)ix->num_cus * wpc);
-    if (wg) HIP_TRY(launch_tokenize_wg(bp, (int)grid, s));
-    else HIP_TRY(launch_tokenize_wave(bp, (int)grid, s));
+    HIP_TRY(launch_tokenize_wave(bp, (int)grid, s));
     if (pack > 1 && !bp.debug_stop) {       // documents the packs could not take: one per wave
       uint32_t n_retry = 0;
       HIP_TRY(hipMemcpyAsync(&n_retry, ctr + 5, 4, hipMemcpyDeviceToHost, s));

@@ -228,9 +228,6 @@ inline void allow_dyn_lds(const void *fn, int bytes, std::atomic<uint64_t> &done
 
 // --- launch wrappers (kernels_index.hip) ---
 hipError_t launch_tokenize_wave(const BuildParams &p, int grid, hipStream_t s);
-// one document per 256-thread workgroup (4 waves), ASCII one-document windows (pack 1)
-hipError_t launch_tokenize_wg(const BuildParams &p, int grid, hipStream_t s);
-constexpr uint32_t kWgWGsPerCU = 8;         // 256-thread workgroups per CU (~19.6 KB LDS each)
 constexpr uint32_t kWaveWGsPerCU = 8;       // 64-thread workgroups per CU (2 waves/SIMD: VGPR- and LDS-bound)
 constexpr uint32_t kWaveGroups = 128;     // CSR row groups per wave unit (documents x ranges, k_tokenize_wave)
 constexpr uint32_t kPackMaxDocs = 16;     // documents per packed window (<= kPackMax, kernels_index.hip)
