@@ -102,17 +102,19 @@ def span_keys(dc, n):
     return key, doc
 
 
-def independent_df(dc, n):
-    """{term key lo: df} of the synthetic corpus, counted with torch ops on cuda:0."""
+def span_df(key, doc, n):
+    """{term key lo: df} from the spans of span_keys (torch ops on cuda:0)."""
     import torch
-    key, doc = span_keys(dc, n)
     bits = max(1, (n - 1).bit_length())
-    assert int(key.max()).bit_length() + bits <= 63
-    pairs = torch.unique((key << bits) | doc)
-    del key, doc
-    terms, df = torch.unique_consecutive(pairs >> bits, return_counts=True)
-    out = dict(zip(terms.cpu().numpy().tolist(), df.cpu().numpy().tolist()))
-    del pairs, terms, df
+    # dense term ids, so (term, doc) fits one int64 at any shard size
+    # (5-byte keys x 25 M documents would need 64 bits)
+    terms, tid = torch.unique(key, return_inverse=True)
+    assert (terms.numel() - 1).bit_length() + bits <= 63
+    pairs = torch.unique((tid << bits) | doc)
+    del tid
+    ids, df = torch.unique_consecutive(pairs >> bits, return_counts=True)
+    out = dict(zip(terms[ids].cpu().numpy().tolist(), df.cpu().numpy().tolist()))
+    del pairs, terms, ids, df
     torch.cuda.empty_cache()
     return out
 
@@ -179,9 +181,16 @@ def engine_df(g):
     return dict(zip(k[:, 0].tolist(), df.cpu().numpy().tolist()))
 
 
+def independent_df(dc, n):
+    """{term key lo: df} of the synthetic corpus, counted with torch ops on cuda:0."""
+    key, doc = span_keys(dc, n)
+    return span_df(key, doc, n)
+
+
 def check_corpus(g, dc, n, len_min, len_max, queries, rng):
     st = g.stats()
-    want_df = independent_df(dc, n)
+    key, doc = span_keys(dc, n)
+    want_df = span_df(key, doc, n)
     got_df = engine_df(g)
     assert len(got_df) == len(want_df) == st["num_terms"]
     assert got_df == want_df
@@ -214,10 +223,8 @@ def check_corpus(g, dc, n, len_min, len_max, queries, rng):
         assert keys == sorted(keys)
     # completeness: the engine's top-k of multi-term queries = the top-k of
     # EVERY document holding a query term, scored from the corpus bytes alone
-    key, doc = span_keys(dc, n)
-    dfs = independent_df(dc, n)
     cq = queries[:8]
-    want = independent_topk(key, doc, n, 0, cq, 100, lambda t: dfs[term_lo(t)], n, int(lens.sum()), lens)
+    want = independent_topk(key, doc, n, 0, cq, 100, lambda t: want_df[term_lo(t)], n, int(lens.sum()), lens)
     del key, doc
     for q, w in zip(cq, want):
         got = g.search(q, 100)

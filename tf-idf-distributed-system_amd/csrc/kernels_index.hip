@@ -646,6 +646,37 @@ __device__ __forceinline__ uint32_t group_probe(ulonglong2 e0, ulonglong2 e1, ui
   return hit;
 }
 
+// The same over the aligned N-slot window of s (N / 2 16 B loads in e[]):
+// the retry queue's probes, so a key displaced further than its first
+// round's bucket costs one more dependent round trip, not one per bucket.
+template <int N>
+__device__ __forceinline__ uint32_t window_probe(const ulonglong2 *e, uint32_t s, uint64_t lo, uint32_t *claim) {
+  const uint32_t g0 = s & ~(uint32_t)(N - 1), off = s & (uint32_t)(N - 1);
+  uint32_t hit = kLookupPending, cl = kInvalidSlot;
+#pragma unroll
+  for (int i = N - 1; i >= 0; i--) {                       // the lowest slot >= s decides
+    if ((uint32_t)i >= off) {
+      const uint64_t v = (i & 1) ? e[i >> 1].y : e[i >> 1].x;
+      const bool f = v == lo, z = v == 0;
+      hit = f ? g0 + i : (z ? kLookupPending : hit);
+      cl = f ? kInvalidSlot : (z ? g0 + i : cl);
+    }
+  }
+  *claim = cl;
+  return hit;
+}
+#ifndef TFIDF_QWIN_G4
+#define TFIDF_QWIN_G4 16
+#endif
+#ifndef TFIDF_QWIN_G2
+#define TFIDF_QWIN_G2 2
+#endif
+// slots per retry-queue probe: one 128 B line (16) for dictionaries outside
+// L2 (G4; cfg 5 tokenize 11.95 -> 11.27 ms, 8 slots 11.55), the 2-slot bucket
+// for L2-resident ones (8 there: cfg 2 6.78 -> 6.87 ms, 4: 6.81)
+template <bool G4>
+constexpr int queue_win() { return G4 ? TFIDF_QWIN_G4 : TFIDF_QWIN_G2; }
+
 // Claim slot cs for short key lo (CAS on lo, then publish hi).  Returns the
 // slot if it now holds lo, else kLookupPending with *s advanced past cs.
 __device__ __forceinline__ uint32_t dict_claim_short(uint64_t *dict, uint32_t mask, uint32_t cs, uint64_t lo,
@@ -1050,17 +1081,15 @@ __device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p
         for (uint32_t it = 0; it < dmask + 4096 && __any(qg == kLookupPending); it++) {
           if (qg == kLookupPending) {
             uint32_t cs;
-            if constexpr (G4) {
-              const ulonglong2 e0 = *reinterpret_cast<const ulonglong2 *>(p.dict + (qs & ~3u));
-              const ulonglong2 e1 = *reinterpret_cast<const ulonglong2 *>(p.dict + (qs & ~3u) + 2);
-              qg = group_probe(e0, e1, qs, ql, &cs);
-            } else {
-              const ulonglong2 e = *reinterpret_cast<const ulonglong2 *>(p.dict + (qs & ~1u));
-              qg = bucket_probe(e, qs, ql, &cs);
-            }
+            constexpr int QW = queue_win<G4>();
+            ulonglong2 e[QW / 2];
+            const ulonglong2 *wp = reinterpret_cast<const ulonglong2 *>(p.dict + (qs & ~(uint32_t)(QW - 1)));
+#pragma unroll
+            for (int i = 0; i < QW / 2; i++) e[i] = wp[i];
+            qg = window_probe<QW>(e, qs, ql, &cs);
             if (qg == kLookupPending) {
               if (cs != kInvalidSlot) qg = dict_claim_short(p.dict, dmask, cs, ql, &qs);
-              else qs = ((qs | (G4 ? 3u : 1u)) + 1u) & dmask;
+              else qs = ((qs | (uint32_t)(QW - 1)) + 1u) & dmask;
             }
           }
         }
@@ -1077,7 +1106,9 @@ __device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p
       // (cfg 5: tokenize 14.9 -> 12.9 ms); 2-slot buckets otherwise (the extra
       // registers spill: cfg 2 8.27 -> 8.77 ms)
       // G4: probes in two halves of kWaveK / 2 terms (two 16 B loads each) so
-      // the group registers of all eight are not live at once
+      // the group registers of all eight are not live at once.  (An 8-slot
+      // window here, two terms at a time: 91 VGPRs spilled, cfg 5 tokenize
+      // 13.1 -> 16.6 ms.)
       constexpr int KH = G4 ? (int)kWaveK / 2 : (int)kWaveK;
       uint32_t cs[kWaveK];
       bool anyclaim = false;
@@ -2405,7 +2436,10 @@ hipError_t launch_verify_deferred(const BuildParams &p, hipStream_t s) {
 }
 
 hipError_t launch_tokenize_wave(const BuildParams &p, int grid, hipStream_t s) {
-  const bool g4 = (uint64_t)p.cap_mask + 1 >= (1ull << 21);   // dictionary beyond L2: 4-slot probe groups
+#ifndef TFIDF_G4_BITS
+#define TFIDF_G4_BITS 21
+#endif
+  const bool g4 = (uint64_t)p.cap_mask + 1 >= (1ull << TFIDF_G4_BITS);   // dictionary beyond L2: 4-slot probe groups
   if (p.pack > 1) {
     if (g4) hipLaunchKernelGGL((k_tokenize_wave<true, true>), dim3(grid), dim3(64), 0, s, p);
     else hipLaunchKernelGGL((k_tokenize_wave<true, false>), dim3(grid), dim3(64), 0, s, p);

@@ -4,7 +4,7 @@
 # batched queries).  Every GPU step bounded; stop at the first failure.
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 500 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --durations=15 --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
 rc=$?; tail -4 gpurun_out/gpu_tests.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 rc=$?; tail -2 gpurun_out/smoke.log; [ $rc -ne 0 ] && exit $rc
