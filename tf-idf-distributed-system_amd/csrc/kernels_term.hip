@@ -17,14 +17,14 @@
 //      its row offset (document order); a tf the field cannot hold goes to an
 //      escape list of (slot << 26 | doc, tf) pairs;
 //   3. per 8-bit digit of the slot bits, low digit first:
-//        k_rs_hist    per tile of 4096 words, the digit histogram (LDS),
+//        k_rs_hist    per tile of 8192 words, the digit histogram (LDS),
 //                     stored digit-major: hist[digit][tile];
 //        scan         exclusive scan of hist -> each (digit, tile) run's
 //                     output start (digit-major order = stable order);
 //        k_rs_scatter per tile: stable rank of every word among the tile's
-//                     words of its digit (16 rounds of 256 words in input
-//                     order; inside a round, wave match masks + per-wave
-//                     digit counts), words placed in LDS in digit order, then
+//                     words of its digit (each wave ranks a quarter of the
+//                     tile in input order against its own digit counters;
+//                     per-wave bases by one scan), words placed in LDS in digit order, then
 //                     written out digit run by digit run (coalesced); the
 //                     LAST pass writes the postings doc | (tf << 8 | norm)
 //                     << 32 instead, and adds each (tile, term) run's length
@@ -48,9 +48,14 @@
 namespace tfidf {
 
 constexpr uint32_t kTermDocBits = 26;                   // escape-list key: slot << 26 | doc
-constexpr uint32_t kRsThreads = 256;
+#ifndef TFIDF_RS_THREADS
+#define TFIDF_RS_THREADS 512
+#endif
+constexpr uint32_t kRsThreads = TFIDF_RS_THREADS;      // radix tile = kRsThreads x kRsItems words (>= 256 threads;
+                                                        // 8192-word tiles: digit runs twice as long, cfg-5 sort
+                                                        // 8.08 -> 7.61 ms; 16384 (one workgroup per CU) 9.34)
 constexpr uint32_t kRsItems = 16;                       // words per thread per tile
-constexpr uint32_t kRsTile = kRsThreads * kRsItems;     // 4096
+constexpr uint32_t kRsTile = kRsThreads * kRsItems;     // 8192
 constexpr uint32_t kRsWaves = kRsThreads / 64;
 
 // ---------------------------------------------------------------------------
@@ -292,7 +297,7 @@ __device__ __forceinline__ uint32_t rs_digit(uint64_t k, uint32_t shift, uint32_
 __global__ void __launch_bounds__(kRsThreads) k_rs_hist(const uint64_t *keys, uint64_t n, uint32_t shift, uint32_t mask,
                                                         uint32_t n_tiles, uint32_t *hist) {
   __shared__ uint32_t h[256];
-  h[threadIdx.x] = 0;
+  if (threadIdx.x < 256) h[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t t0 = (uint64_t)blockIdx.x * kRsTile;
 #pragma unroll
@@ -301,7 +306,7 @@ __global__ void __launch_bounds__(kRsThreads) k_rs_hist(const uint64_t *keys, ui
     if (i < n) atomicAdd(&h[rs_digit(keys[i], shift, mask)], 1u);
   }
   __syncthreads();
-  hist[(uint64_t)blockIdx.x * 256 + threadIdx.x] = h[threadIdx.x];
+  if (threadIdx.x < 256) hist[(uint64_t)blockIdx.x * 256 + threadIdx.x] = h[threadIdx.x];
 }
 
 // Exclusive scan of the tile-major histogram in (digit, tile) order — every
@@ -361,19 +366,24 @@ __global__ void __launch_bounds__(256) k_col_final(const uint32_t *hist, uint32_
 }
 
 // Per tile: stable rank of each word among the tile's words of its digit.
-// Input order inside the tile is i = 256 j + t (round j, thread t); a round's
-// words are ranked by wave match masks (lanes below with the same digit) plus
-// the per-digit counts of the round's lower waves plus the counts of earlier
-// rounds.  Words go to LDS at (digit start in the tile + rank), then out run
-// by run to hist-scanned global starts.
+// Wave w takes the tile's w-th quarter (1024 consecutive words: item j of
+// lane l is word 1024 w + 64 j + l, so a wave walks its words in input
+// order) and ranks them against its own LDS digit counters (cursor_bump: peer
+// masks rank the lanes of one instruction, the lowest peer's returning add
+// gives their base); after one
+// barrier the counters become per-wave digit bases (an exclusive scan over
+// the waves, thread = digit), and each word goes to LDS at (digit start in
+// the tile + earlier waves' words of its digit + its rank in the wave), then
+// out run by run to hist-scanned global starts.  Three barriers per tile
+// (round 3's 16 block-wide rounds of 256 words took three each: 48).
 struct RsSmem {
   uint64_t k[kRsTile];
   uint32_t start[256];                 // digit's first position in the sorted tile
   uint32_t gpos[256];                  // digit run's global start (scanned hist)
-  uint32_t run[256];                   // words of the digit in earlier rounds
-  uint32_t wcnt[kRsWaves][256];        // words of the digit in this round, per wave
+  uint32_t wcnt[kRsWaves][257];        // the wave's words per digit (256: past the end), then bases
   uint32_t wsum[kRsWaves];
 };
+constexpr uint32_t kRsWaveWords = kRsItems * 64;        // consecutive words per wave
 
 // LAST: write postings (and df run lengths) instead of words.
 template <bool LAST>
@@ -385,43 +395,51 @@ __global__ void __launch_bounds__(kRsThreads) k_rs_scatter(const uint64_t *keys,
   const uint64_t t0 = (uint64_t)blockIdx.x * kRsTile;
   // the tile's digit starts: exclusive scan of its histogram over digits
   {
-    const uint32_t c = hist[(uint64_t)blockIdx.x * 256 + tid];
+    const uint32_t c = tid < 256 ? hist[(uint64_t)blockIdx.x * 256 + tid] : 0u;
     uint32_t tot;
-    sm.start[tid] = block_incl_scan(c, sm.wsum, &tot) - c;
-    sm.gpos[tid] = gstart[(uint64_t)blockIdx.x * 256 + tid];
-    sm.run[tid] = 0;
+    const uint32_t st = block_incl_scan(c, sm.wsum, &tot) - c;
+    if (tid < 256) {
+      sm.start[tid] = st;
+      sm.gpos[tid] = gstart[(uint64_t)blockIdx.x * 256 + tid];
 #pragma unroll
-    for (uint32_t w = 0; w < kRsWaves; w++) sm.wcnt[w][tid] = 0;
+      for (uint32_t w = 0; w < kRsWaves; w++) sm.wcnt[w][tid] = 0;
+    }
+    if (tid < kRsWaves) sm.wcnt[tid][256] = 0;
   }
+  const uint64_t wb = t0 + (uint64_t)wid * kRsWaveWords;
   uint64_t kv[kRsItems];
 #pragma unroll
   for (uint32_t j = 0; j < kRsItems; j++) {
-    const uint64_t i = t0 + (uint64_t)j * kRsThreads + tid;
+    const uint64_t i = wb + (uint64_t)j * 64 + lane;
     kv[j] = i < n ? keys[i] : ~0ull;
   }
   __syncthreads();
-  for (uint32_t j = 0; j < kRsItems; j++) {
-    const uint64_t i = t0 + (uint64_t)j * kRsThreads + tid;
-    const bool in = i < n;
-    const uint32_t d = rs_digit(kv[j], shift, mask);
-    const uint64_t peers = peer_mask<9>(in ? d : 256u) & (in ? ~0ull : 0ull);
-    const uint32_t below = (uint32_t)__popcll(peers & ((1ull << lane) - 1));
-    if (in && below == 0) sm.wcnt[wid][d] = (uint32_t)__popcll(peers);
-    __syncthreads();
-    if (in) {
-      uint32_t r = sm.run[d] + below;
-      for (uint32_t w = 0; w < wid; w++) r += sm.wcnt[w][d];
-      sm.k[sm.start[d] + r] = kv[j];
-    }
-    __syncthreads();
-    {
-      uint32_t add = 0;
+  uint32_t dr[kRsItems];                                   // digit (9 bits) | rank in the wave << 9
+  const bool full = t0 + kRsTile <= n;                     // block-uniform
 #pragma unroll
-      for (uint32_t w = 0; w < kRsWaves; w++) { add += sm.wcnt[w][tid]; sm.wcnt[w][tid] = 0; }
-      sm.run[tid] += add;
-    }
-    __syncthreads();
+  for (uint32_t j = 0; j < kRsItems; j++) {
+    const bool in = wb + (uint64_t)j * 64 + lane < n;
+    const uint32_t d = in ? rs_digit(kv[j], shift, mask) : 256u;
+    const uint32_t r = full ? cursor_bump<8>(sm.wcnt[wid], d, lane) : cursor_bump<9>(sm.wcnt[wid], d, lane);
+    dr[j] = d | (r << 9);
   }
+  __syncthreads();
+  if (tid < 256) {
+    uint32_t run = 0;                                      // digit tid: words of the lower waves
+#pragma unroll
+    for (uint32_t w = 0; w < kRsWaves; w++) {
+      const uint32_t c = sm.wcnt[w][tid];
+      sm.wcnt[w][tid] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t j = 0; j < kRsItems; j++) {
+    const uint32_t d = dr[j] & 511u;
+    if (d < 256) sm.k[sm.start[d] + sm.wcnt[wid][d] + (dr[j] >> 9)] = kv[j];
+  }
+  __syncthreads();
   // out: sorted tile position q holds a word of digit d at global gpos[d] + (q - start[d])
   const uint64_t cnt = n - t0 < kRsTile ? n - t0 : kRsTile;
   const TermLayout ly{p.slot_bits, p.doc_bits, p.tf_bits};
