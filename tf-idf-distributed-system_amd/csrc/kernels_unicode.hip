@@ -387,13 +387,39 @@ __device__ __forceinline__ bool uc_window_span(const uint8_t *cls, const uint8_t
   return false;
 }
 
-__global__ void __launch_bounds__(64) k_tokenize_uchunk(BuildParams p) {
-  __shared__ UwSmem sm;
+// The unit's LDS: a window of at most kPreBytes + kCoreBytes + kPostBytes
+// bytes (+ 15 alignment) and a 512-slot term table (a 2 KB core holds at most
+// kPairWords distinct terms) — 19 KB, eight workgroups per CU (round 4's first
+// form used the 4 KB-window, 1024-slot document layout: 33 KB, four per CU).
+constexpr uint32_t kUcWindow = kPreBytes + kCoreBytes + kPostBytes + 16;
+constexpr uint32_t kUcSlots = 512;
+constexpr uint32_t kUcSlotBits = 9;
+struct UcSmem {
+  alignas(16) uint8_t text[kUcWindow + 16];
+  alignas(16) uint8_t cls[kUcWindow];
+  unsigned long long klo[kUcSlots];   // key lo; after the lookup: dictionary slot
+  unsigned long long khi[kUcSlots];   // key hi (VALID bit set: occupied)
+  uint32_t cnt[kUcSlots];             // tf
+  uint32_t kpos[kUcSlots];            // first occurrence: start | end << 16 (window bytes)
+  uint16_t occ[kUcSlots];             // occupied slots, compacted
+  uint32_t rcnt[64];                  // bucket counts, then cursors
+  uint8_t tr[kUwStates * kUwClasses]; // WORD DFA transitions
+  uint8_t asc[128];                   // ASCII byte -> scanner class
+};
+
+__device__ __forceinline__ void uc_clear_all(UcSmem &sm, uint32_t lane) {
+  for (uint32_t s = lane; s < kUcSlots; s += 64) { sm.klo[s] = 0; sm.khi[s] = 0; sm.cnt[s] = 0; }
+}
+
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_tokenize_uchunk(BuildParams p) {
+  __shared__ UcSmem sm;
   const uint32_t lane = threadIdx.x;
   const uint32_t n_units = *p.uchunk_count;
   if (blockIdx.x >= n_units) return;                        // block-uniform
   for (uint32_t e = lane; e < kUwStates * kUwClasses; e += 64)
     sm.tr[e] = (uint8_t)uc_word_next(e / kUwClasses, e % kUwClasses);
+  for (uint32_t e = lane; e < 128; e += 64) sm.asc[e] = (uint8_t)uc_ascii_class(e);
+  uc_clear_all(sm, lane);
   __syncthreads();
   for (uint32_t it = blockIdx.x; it < n_units; it += gridDim.x) {
     const uint32_t u = p.uchunk_list[it];
@@ -401,29 +427,40 @@ __global__ void __launch_bounds__(64) k_tokenize_uchunk(BuildParams p) {
     const uint64_t src = p.live_map ? p.live_map[m.d] : m.d;
     const bool doc_end = m.s0 + m.L == p.offsets[src + 1];  // the window reaches the document's end
     const uint32_t L = (uint32_t)m.L;
-    // ---- stage the window (aligned 16 B loads) + clear the table
+    // ---- stage the window (aligned 16 B loads); the table is empty here
     const uint32_t nchunks = (m.shift + L + 15) >> 4;
     const uint4 *gsrc = reinterpret_cast<const uint4 *>(p.text + m.s0 - m.shift);
     uint4 *dst = reinterpret_cast<uint4 *>(sm.text);
     for (uint32_t c = lane; c < nchunks; c += 64) dst[c] = gsrc[c];
-    for (uint32_t s = lane; s < kUwSlots; s += 64) { sm.klo[s] = 0; sm.khi[s] = 0; sm.cnt[s] = 0; }
     __syncthreads();
     const uint8_t *doc = sm.text + m.shift;
-    // ---- classes (a char cut by the window's edges is 0xFF: a scan never lands there unless it must fail)
-    for (uint32_t j = 0; j < 64; j += 4) {
-      const uint32_t i0 = 64 * lane + j;
-      for (uint32_t q = i0; q < i0 + 4 && q < L; q++) {
-        const uint32_t x = doc[q];
-        uint32_t v;
-        if (x < 0x80u) v = uc_ascii_class(x);
-        else if ((x & 0xC0u) == 0x80u) v = 0xFFu;
-        else {
-          uint32_t l;
-          const uint32_t cp = utf8_decode(doc, L, q, &l);
-          v = cp == kUcBad ? 0xFFu : (uc_class(cp) | ((l - 1) << 5));
+    // ---- classes, four consecutive bytes per lane per step (consecutive lanes
+    // on consecutive dwords: no LDS bank conflicts); a char cut by the window's
+    // edges is 0xFF: a scan never lands there unless it must fail
+    for (uint32_t i0 = 4 * lane; i0 < L; i0 += 256) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int b = 0; b < 4; b++) w |= (i0 + b < L ? (uint32_t)doc[i0 + b] : 0x20u) << (8 * b);
+      uint32_t out = 0;
+      if ((w & 0x80808080u) == 0) {
+#pragma unroll
+        for (int b = 0; b < 4; b++) out |= (uint32_t)sm.asc[(w >> (8 * b)) & 0x7Fu] << (8 * b);
+      } else {
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const uint32_t x = (w >> (8 * b)) & 0xFFu;
+          uint32_t v;
+          if (x < 0x80u) v = sm.asc[x];
+          else if ((x & 0xC0u) == 0x80u || i0 + b >= L) v = 0xFFu;
+          else {
+            uint32_t l;
+            const uint32_t cp = utf8_decode(doc, L, i0 + b, &l);
+            v = cp == kUcBad ? 0xFFu : (uc_class(cp) | ((l - 1) << 5));
+          }
+          out |= v << (8 * b);
         }
-        sm.cls[q] = (uint8_t)v;
       }
+      *reinterpret_cast<uint32_t *>(&sm.cls[i0]) = out;      // bytes past L: never read
     }
     __syncthreads();
     // ---- scan origin: a split point at or before the core (the document's start for its first unit)
@@ -465,9 +502,9 @@ __global__ void __launch_bounds__(64) k_tokenize_uchunk(BuildParams p) {
         active = have;
         have = have && ts32 >= m.core_lo;                     // tokens starting in the core only
       }
-      uint32_t slot = dict_hash(lo, khv) >> (32 - kUwSlotBits);
+      uint32_t slot = dict_hash(lo, khv) >> (32 - kUcSlotBits);
       bool done = !have;
-      for (uint32_t r = 0; r < kUwSlots && __any(!done); r++) {
+      for (uint32_t r = 0; r < kUcSlots && __any(!done); r++) {
         unsigned long long old = 1;
         if (!done) old = atomicCAS(&sm.klo[slot], 0ull, (unsigned long long)lo);
         const bool won = !done && old == 0;
@@ -483,47 +520,64 @@ __global__ void __launch_bounds__(64) k_tokenize_uchunk(BuildParams p) {
           atomicAdd(&sm.cnt[slot], 1u);
           done = true;
         } else if (!done) {
-          slot = (slot + 1) & (kUwSlots - 1);
+          slot = (slot + 1) & (kUcSlots - 1);
         }
       }
       overflow |= !done;
     }
     if (collide) set_build_err(p.err, kErrCollision, (uint32_t)m.d);
-    uint32_t occ = 0;
-    for (uint32_t s = lane; s < kUwSlots; s += 64) occ += sm.khi[s] != 0;
-    const uint32_t nu = (uint32_t)__builtin_amdgcn_readlane((int)uw_incl_add(occ, lane), 63);
+    // ---- occupied slots, compacted (lane l: slots [8 l, 8 l + 8))
+    uint32_t nu;
+    {
+      uint32_t om = 0;
+#pragma unroll
+      for (int k = 0; k < (int)(kUcSlots / 64); k++) om |= (uint32_t)(sm.khi[(kUcSlots / 64) * lane + k] != 0) << k;
+      const uint32_t c = (uint32_t)__popc(om);
+      const uint32_t incl = uw_incl_add(c, lane);
+      nu = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      uint32_t at = incl - c;
+      while (om) {
+        sm.occ[at++] = (uint16_t)((kUcSlots / 64) * lane + (uint32_t)__builtin_ctz(om));
+        om &= om - 1;
+      }
+    }
     if (fail || __any(ubad) || __any(overflow) || (__any(at_end) && !doc_end) || nu > kPairWords) {
       if (lane == 0) p.chunk_fail[m.gi] = 1u;                // wave-uniform: the document goes to the long path
       __syncthreads();
+      uc_clear_all(sm, lane);
+      __syncthreads();
       continue;
     }
-    // ---- dictionary slots (8 lookups per lane in flight); bucket counts
+    __syncthreads();
+    // ---- dictionary slots of the occupied entries (<= 8 per lane, in flight together); bucket counts
     const uint32_t bsh = p.pair_bshift, nb = p.pair_nb, bmask = (1u << bsh) - 1u;
     uint32_t *bcnt = sm.rcnt;                                 // [0, 64) counts, then starts
     bcnt[lane] = 0;
     __syncthreads();
-    for (int h = 0; h < 2; h++) {
-      uint64_t klo[8], khi[8], mine[8];
-      bool act[8], cl[8];
-      uint32_t g[8];
+    for (int h = 0; h < 2; h++) {                            // two halves of four (registers: 2 waves / SIMD)
+      uint64_t klo[4], khi[4], mine[4];
+      bool act[4], cl[4];
+      uint32_t g[4], sl[4];
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const uint32_t s = lane + 64 * (8 * h + k);
-        klo[k] = sm.klo[s];
-        khi[k] = sm.khi[s];
-        act[k] = khi[k] != 0;
-        const uint32_t kp = sm.kpos[s];
+      for (int k = 0; k < 4; k++) {
+        const uint32_t i = lane + 64 * (4 * h + k);
+        act[k] = i < nu;
+        sl[k] = act[k] ? sm.occ[i] : 0u;
+        klo[k] = sm.klo[sl[k]];
+        khi[k] = sm.khi[sl[k]];
+        const uint32_t kp = sm.kpos[sl[k]];
         mine[k] = dict_ref_word(m.s0 + (kp & 0xFFFFu), (kp >> 16) - (kp & 0xFFFFu));
         if (!act[k]) { klo[k] = 1; khi[k] = kKeyValid; }
       }
-      dict_lookup_multi<8>(p.dict, p.cap_mask, klo, khi, act, g, mine, cl);
+      if (!__any(act[0])) break;                              // wave-uniform: no terms left
+      dict_lookup_multi<4>(p.dict, p.cap_mask, klo, khi, act, g, mine, cl);
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
+      for (int k = 0; k < 4; k++) {
         if (!act[k]) continue;
         if ((klo[k] & kLoHashed) && !cl[k] && g[k] != kInvalidSlot) dict_verify(p, g[k], mine[k], (uint32_t)m.d);
         uint32_t gs = g[k];
         if (gs == kInvalidSlot) { atomicOr(p.err, kErrCapacity); gs = 0; }
-        sm.klo[lane + 64 * (8 * h + k)] = gs;
+        sm.klo[sl[k]] = gs;
         atomicAdd(&bcnt[gs >> bsh], 1u);
       }
     }
@@ -539,9 +593,9 @@ __global__ void __launch_bounds__(64) k_tokenize_uchunk(BuildParams p) {
       __syncthreads();
       if (lane < nb) bcnt[lane] = incl - c;                   // cursors
       __syncthreads();
-      uint32_t *stage = reinterpret_cast<uint32_t *>(sm.cls);  // classes are dead here
-      for (uint32_t s = lane; s < kUwSlots; s += 64) {
-        if (sm.khi[s] == 0) continue;
+      uint32_t *stage = reinterpret_cast<uint32_t *>(sm.cls);  // classes are dead here (kPairWords words fit)
+      for (uint32_t i = lane; i < nu; i += 64) {
+        const uint32_t s = sm.occ[i];
         const uint32_t gs = (uint32_t)sm.klo[s];
         const uint32_t at = atomicAdd(&bcnt[gs >> bsh], 1u);
         stage[at] = ((gs & bmask) << kPairTfBits) | sm.cnt[s];
@@ -549,6 +603,11 @@ __global__ void __launch_bounds__(64) k_tokenize_uchunk(BuildParams p) {
       __syncthreads();
       uint32_t *pr = p.pairs + (uint64_t)u * kPairWords;
       for (uint32_t i = lane; i < total; i += 64) pr[i] = stage[i];
+      // reset the occupied slots for the next unit
+      for (uint32_t i = lane; i < nu; i += 64) {
+        const uint32_t s = sm.occ[i];
+        sm.klo[s] = 0; sm.khi[s] = 0; sm.cnt[s] = 0;
+      }
     }
     __syncthreads();
   }

@@ -946,7 +946,7 @@ static int commit_once(tfidf_index *ix) {
       const uint64_t grid = std::min<uint64_t>(cp.n_chunks, (uint64_t)ix->num_cus * kWaveWGsPerCU);
       HIP_TRY(launch_tokenize_chunks(cp, (int)grid, s));
       if (uch)      // the count is read on the device: exits at once when no unit was listed
-        HIP_TRY(launch_tokenize_uchunk(cp, (int)std::min<uint64_t>(cp.n_chunks, (uint64_t)ix->num_cus * kUwaveWGsPerCU), s));
+        HIP_TRY(launch_tokenize_uchunk(cp, (int)std::min<uint64_t>(cp.n_chunks, (uint64_t)ix->num_cus * kUchunkWGsPerCU), s));
       HIP_TRY(launch_long_rows(cp, (uint32_t)n, s));
     }
     uint32_t n_fb = 0;
