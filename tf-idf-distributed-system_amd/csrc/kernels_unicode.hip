@@ -348,6 +348,26 @@ __device__ __forceinline__ bool uc_window_span(const uint8_t *cls, const uint8_t
       uint32_t st = st0, p = i + l, last = uc_word_accepting(st) ? p : i, erun = p;
       bool dead = false;
       while (p < n) {
+        if (st == kWA || st == kWN) {
+          // ASCII letters / digits (class bytes 0x01 / 0x03) keep the state in
+          // {A, N} (WB5, WB8-WB10), both accepting: skip the run four class
+          // bytes per aligned LDS read instead of a DFA step per byte
+          const uint32_t *c32 = reinterpret_cast<const uint32_t *>(cls);
+          uint32_t q = p;
+          while (q < n) {
+            const uint32_t x = __builtin_amdgcn_alignbyte(c32[(q >> 2) + 1], c32[q >> 2], q & 3);
+            const uint32_t m = (x & 0xFDFDFDFDu) ^ 0x01010101u;          // zero byte: ASCII alnum
+            const uint32_t run = m ? (uint32_t)__builtin_ctz(m) >> 3 : 4u;
+            q += min(run, n - q);
+            if (run < 4) break;
+          }
+          if (q > p) {
+            st = cls[q - 1] == 0x01u ? kWA : kWN;
+            p = q;
+            last = p;
+            if (p >= n) break;
+          }
+        }
         const uint32_t w = cls[p];
         if (w == 0xFFu) { *bad = true; return false; }
         const uint32_t cw = w & 31u;
@@ -409,6 +429,24 @@ struct UcSmem {
 
 __device__ __forceinline__ void uc_clear_all(UcSmem &sm, uint32_t lane) {
   for (uint32_t s = lane; s < kUcSlots; s += 64) { sm.klo[s] = 0; sm.khi[s] = 0; sm.cnt[s] = 0; }
+}
+
+// Key of a token of n <= 8 bytes at (aligned) window byte a when they are all
+// ASCII: the lower-cased bytes, as KeyBuilder gives them (uc_token_key's
+// UTF-8 walk is for the rest).  false: a byte >= 0x80.
+__device__ __forceinline__ uint32_t uc_lower4(uint32_t t) {
+  const uint32_t up = (t + 0x3F3F3F3Fu) & ~(t + 0x25252525u) & 0x80808080u;   // 'A'..'Z' (ASCII bytes)
+  return t | (up >> 2);
+}
+__device__ __forceinline__ bool uc_short_ascii_key(const uint8_t *text, uint32_t a, uint32_t n, uint64_t *lo) {
+  const uint32_t *t32 = reinterpret_cast<const uint32_t *>(text);
+  const uint32_t w0 = t32[a >> 2], w1 = t32[(a >> 2) + 1], w2 = t32[(a >> 2) + 2], o = a & 3;
+  uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, o), x1 = __builtin_amdgcn_alignbyte(w2, w1, o);
+  x0 &= n >= 4 ? 0xFFFFFFFFu : (1u << (8 * n)) - 1u;
+  x1 &= n >= 8 ? 0xFFFFFFFFu : (n <= 4 ? 0u : (1u << (8 * (n - 4))) - 1u);
+  if ((x0 | x1) & 0x80808080u) return false;
+  *lo = (uint64_t)uc_lower4(x0) | ((uint64_t)uc_lower4(x1) << 32);
+  return true;
 }
 
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_tokenize_uchunk(BuildParams p) {
@@ -495,8 +533,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         uint32_t p32 = pos;
         have = uc_window_span(sm.cls, sm.tr, L, &p32, stop, &ts32, &te32, &ubad, &at_end);
         if (have) {
-          const uint64_t cutp = uc_token_key(doc, L, ts32, te32, &lo, &khv, p.hash_seed);
-          if (cutp < te32) overflow = true;                   // > 255 units: the long path cuts it
+          if (te32 - ts32 <= 8 && uc_short_ascii_key(sm.text, m.shift + ts32, te32 - ts32, &lo)) {
+            khv = kKeyValid;                                  // most tokens: <= 8 ASCII bytes
+          } else {
+            const uint64_t cutp = uc_token_key(doc, L, ts32, te32, &lo, &khv, p.hash_seed);
+            if (cutp < te32) overflow = true;                 // > 255 units: the long path cuts it
+          }
         }
         pos = p32;
         active = have;
