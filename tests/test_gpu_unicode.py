@@ -177,3 +177,74 @@ def test_book_unicode_chunks():
         assert_hits_equal(g.search(qb, 5), o.search(qb, 5))
     g.close()
     o.close()
+
+
+def prose_book(rng, n_words):
+    """Book-like prose: sentence capitals, ALL-CAPS names, curly and ASCII
+    quotes / apostrophes, em dashes, numbers with separators ("1,000", "3.14"),
+    letter-digit mixes, hyphens, ellipses, snake_case, accented words in mixed
+    case — the characters real books put between and inside ASCII words."""
+    accented = ["Émile", "ÉCOLE", "café", "Café", "naïve", "façade", "Zoë", "señor", "Über", "übermäßig", "ﬁnal"]
+    out, cap = [], True
+    for _ in range(n_words):
+        r = rng.random()
+        if r < 0.04:
+            w = rng.choice(accented)
+        elif r < 0.07:
+            w = rng.choice(["1,000", "3.14", "2024", "12:30", "A4", "x86_64", "v2.0", "1,234,567.89", "4th"])
+        elif r < 0.10:
+            w = rng.choice(["it’s", "don’t", "can't", "O’Neil", "rock’n’roll", "l’été", "we'd"])
+        elif r < 0.12:
+            w = synth.word(rng.randint(1, 3000)).decode() + "-" + synth.word(rng.randint(1, 3000)).decode()
+        elif r < 0.13:
+            w = synth.word(rng.randint(1, 800)).decode().upper()
+        elif r < 0.135:
+            w = "snake_" + synth.word(rng.randint(1, 500)).decode()
+        else:
+            w = synth.word(rng.randint(1, 20000)).decode()
+        if cap:
+            w = w[:1].upper() + w[1:]
+            cap = False
+        q = rng.random()
+        if q < 0.03:
+            w = "“" + w + "”"
+        elif q < 0.05:
+            w = "\"" + w + "\""
+        elif q < 0.06:
+            w = "‘" + w + "’"
+        out.append(w)
+        p = rng.random()
+        if p < 0.06:
+            out.append(rng.choice([". ", "! ", "? ", "… ", "... "]))
+            cap = True
+        elif p < 0.10:
+            out.append(rng.choice([", ", "; ", ": ", " — ", "—", " – ", " (", ") "]))
+        elif p < 0.11:
+            out.append("\n\n")
+            cap = True
+        else:
+            out.append(" ")
+    return "".join(out).encode()
+
+
+def test_book_prose_unicode_chunks():
+    """Books of realistic prose (curly quotes, em dashes, contractions with
+    U+2019, accented capitals, numbers with separators) on the chunk path: the
+    Unicode chunk kernel's ASCII shortcuts (runs of letters / digits skipped in
+    the DFA's A / N states, keys of <= 8 ASCII bytes built directly) meet every
+    join rule (WB6/7 MidLetter, WB11/12 MidNum, MidNumLet, Single_Quote,
+    ExtendNumLet) next to non-ASCII characters.  All = the oracle."""
+    rng = random.Random(33)
+    texts = [prose_book(rng, rng.randint(12000, 22000)) for _ in range(8)]
+    texts += [prose_book(rng, rng.randint(50, 400)) for _ in range(200)]        # short documents: the Unicode wave
+    g, o = build_pair(texts)
+    st = g.stats()
+    assert st["long_docs"] >= 8 and st["long_chunked"] >= 8
+    check(g, o, texts)
+    for q in ["café Émile", "it’s don’t", "1,000 3.14", "ÉCOLE école", "rock’n’roll", "snake_" + synth.word(3).decode(),
+              "x86_64 v2.0", synth.word(12).decode() + " " + synth.word(400).decode(), "o’neil über"]:
+        qb = q.encode()
+        assert_hits_equal(g.search(qb, 0), o.search(qb, 0))
+        assert_hits_equal(g.search(qb, 7), o.search(qb, 7))
+    g.close()
+    o.close()
