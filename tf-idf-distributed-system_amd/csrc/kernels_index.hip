@@ -994,24 +994,16 @@ __device__ __forceinline__ void hist2(WaveSmem &sm, uint32_t lane, uint32_t tb, 
   }
 }
 
-template <bool G4>
-__device__ __forceinline__ void probe_short_terms(const BuildParams &p, uint32_t lane, uint64_t *lo, uint32_t *ps,
-                                                  uint32_t *g, uint64_t *qarea);
-
 // Dictionary slots of the document's distinct terms (table entries listed in
 // slots[0, nu)): lane l resolves terms l + 64k (k < kWaveK) -> g[k], with
 // their counts tf[k] (and, PACK, the pack-local document tdoc[k]; per-document
 // lengths / term counts accumulated into pk_len / pk_nu).  Short keys by
 // bucket probes with all of a lane's loads in flight, unresolved ones through
 // a one-per-lane retry queue; folded (> 8 byte) keys one per lane at a time.
-// SPLIT (k_tokenize_wave's split form): only the folded keys are resolved
-// here; every term is staged for k_resolve_wave at entry ebase + lane + 64k
-// (tl_key = short key, or kFoldBit | slot; csr = tf | tdoc << 24).
-template <bool PACK, bool G4, bool SPLIT = false>
+template <bool PACK, bool G4>
 __device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p, uint32_t lane, uint32_t nu,
                                               uint32_t doc, uint32_t *g, uint32_t *tf, uint32_t *tdoc,
-                                              uint32_t &actm, uint32_t *pk_len, uint32_t *pk_nu, uint64_t wbase,
-                                              uint64_t ebase = 0) {
+                                              uint32_t &actm, uint32_t *pk_len, uint32_t *pk_nu, uint64_t wbase) {
   const uint32_t dmask = p.cap_mask;
   const uint16_t *slots = reinterpret_cast<const uint16_t *>(sm.list);
   if (PACK && lane < kPackMax) { pk_len[lane] = 0; pk_nu[lane] = 0; }
@@ -1063,44 +1055,7 @@ __device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p
       for (int kk = 0; kk < (int)kWaveK; kk++)
         if (fa && (uint32_t)kk == k) g[kk] = gg;
     }
-    if constexpr (SPLIT) {
-      bool caperr = false;
-      uint64_t *tk = TFIDF_COLD(tl_key) + ebase;
-      uint32_t *tw = p.csr + ebase;
-#pragma unroll
-      for (int k = 0; k < (int)kWaveK; k++) {
-        if ((actm >> k) & 1u) {
-          const bool f = g[k] != kLookupPending;
-          caperr |= f & (g[k] == kInvalidSlot);
-          __builtin_nontemporal_store(f ? kFoldBit | (g[k] == kInvalidSlot ? 0u : g[k]) : lo[k], tk + lane + 64 * k);
-          __builtin_nontemporal_store(tf[k] | (tdoc[k] << 24), tw + lane + 64 * k);
-        }
-      }
-      if (caperr) set_err(TFIDF_COLD(err), kErrCapacity, doc);
-      return;
-    }
-    probe_short_terms<G4>(p, lane, lo, ps, g, sm.key);
-    bool caperr = false;
-#pragma unroll
-    for (int k = 0; k < (int)kWaveK; k++) {
-      const bool e = (((actm >> k) & 1u) != 0) & ((g[k] == kInvalidSlot) | (g[k] == kLookupPending));
-      caperr |= e;
-      if (e) g[k] = 0;
-    }
-    if (caperr) set_err(TFIDF_COLD(err), kErrCapacity, doc);
-  }
-}
-
-// Dictionary slots g[k] of short keys lo[k] (g[k] == kLookupPending; probe
-// start ps[k]): bucket probes with all of a lane's loads in flight per round,
-// the last <= kDictQueue through a one-per-lane retry queue in qarea (LDS,
-// 2 * kDictQueue + kWaveTerms / 2 words).  Unresolved (table full): g[k]
-// stays kLookupPending or kInvalidSlot.
-template <bool G4>
-__device__ __forceinline__ void probe_short_terms(const BuildParams &p, uint32_t lane, uint64_t *lo, uint32_t *ps,
-                                                  uint32_t *g, uint64_t *qarea) {
-  const uint32_t dmask = p.cap_mask;
-  {
+    // short terms: bucket probes, all of a lane's loads in flight per round
     for (uint32_t round = 0;; round++) {
       uint32_t np = 0;
 #pragma unroll
@@ -1109,10 +1064,10 @@ __device__ __forceinline__ void probe_short_terms(const BuildParams &p, uint32_t
       const uint32_t P = (uint32_t)__builtin_amdgcn_readlane((int)pincl, 63);
       if (P == 0) break;
       if (round > 0 && P <= kDictQueue) {
-        // retry queue: (lo, probe slot, term index)
-        uint64_t *qlo = qarea;
-        uint2 *qmeta = reinterpret_cast<uint2 *>(qarea + kDictQueue);
-        uint32_t *res = reinterpret_cast<uint32_t *>(qarea + 2 * kDictQueue);
+        // retry queue in the (no longer needed) table: (lo, probe slot, term index)
+        uint64_t *qlo = sm.key;
+        uint2 *qmeta = reinterpret_cast<uint2 *>(sm.key + kDictQueue);
+        uint32_t *res = reinterpret_cast<uint32_t *>(sm.key + 2 * kDictQueue);
         uint32_t at = pincl - np;
 #pragma unroll
         for (int k = 0; k < (int)kWaveK; k++)
@@ -1188,6 +1143,14 @@ __device__ __forceinline__ void probe_short_terms(const BuildParams &p, uint32_t
           if (cs[k] != kInvalidSlot) g[k] = dict_claim_short(p.dict, dmask, cs[k], lo[k], &ps[k]);
       }
     }
+    bool caperr = false;
+#pragma unroll
+    for (int k = 0; k < (int)kWaveK; k++) {
+      const bool e = (((actm >> k) & 1u) != 0) & ((g[k] == kInvalidSlot) | (g[k] == kLookupPending));
+      caperr |= e;
+      if (e) g[k] = 0;
+    }
+    if (caperr) set_err(TFIDF_COLD(err), kErrCapacity, doc);
   }
 }
 
@@ -1196,11 +1159,7 @@ __device__ __forceinline__ void probe_short_terms(const BuildParams &p, uint32_t
 // sharing one window.  A pack that cannot take the packed path (window or
 // token/term capacity, non-contiguous sources, an empty or non-ASCII document)
 // sends its documents to retry_list for a PACK = false pass.
-//
-// SPLIT: the tokenizer half of the split form — the unit's distinct terms are
-// staged (resolve_terms<SPLIT>) and tl_n[u] = their number (kInvalidSlot: the
-// unit went elsewhere); k_resolve_wave resolves them and writes the rows.
-template <bool PACK, bool G4, bool SPLIT = false>
+template <bool PACK, bool G4>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_tokenize_wave(BuildParams p) {
   __shared__ WaveSmem sm;
   const uint32_t lane = threadIdx.x;
@@ -1227,7 +1186,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     const uint64_t pofs = meta.pofs;
     const bool fits = fits_wave(meta);
     const uint64_t un = u + gridDim.x;
-    if (SPLIT && lane == 0) TFIDF_COLD(tl_n)[u] = kInvalidSlot;
     if (!fits) {
       if (PACK) defer_pack(p, d, np, lane);
       else if (lane == 0) TFIDF_COLD(long_list)[atomicAdd(TFIDF_COLD(long_count), 1u)] = (uint32_t)d;
@@ -1403,37 +1361,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     // ---- dictionary slots of terms lane + 64k
     uint32_t g[kWaveK], tf[kWaveK], tdoc[kWaveK];
     uint32_t actm = 0;
-    if constexpr (SPLIT) {
-      if (PACK && (np << __builtin_ctz(R)) > kWaveGroups) {   // cannot happen (host pack limit)
-        clear_table(sm, lane);
-        defer_pack(p, d, np, lane);
-        continue;
-      }
-      // stage the terms at the unit's first row (a pack's rows are contiguous)
-      resolve_terms<PACK, G4, true>(sm, p, lane, nu, (uint32_t)d, g, tf, tdoc, actm, pk_len, pk_nu, s0 - shift,
-                                    (s0 + src) >> 1);
-      clear_table(sm, lane);
-      if (PACK) {
-        if (lane < np) {
-          const uint32_t lj = pk_len[lane], nj = pk_nu[lane];
-          p.doc_len[d + lane] = lj;
-          p.doc_nuniq[d + lane] = nj;
-          p.doc_norm[d + lane] = (uint8_t)int_to_byte4(lj);
-          my_doc_count += lj > 0;
-          my_ttf += lj;
-          my_nnz += nj;
-        }
-      } else if (lane == 0) {
-        p.doc_len[d] = len;
-        p.doc_nuniq[d] = nu;
-        p.doc_norm[d] = (uint8_t)int_to_byte4(len);
-        my_doc_count += len > 0;
-        my_ttf += len;
-        my_nnz += nu;
-      }
-      if (lane == 0) TFIDF_COLD(tl_n)[u] = p.debug_stop == 4 ? kInvalidSlot : nu;
-      continue;
-    }
     resolve_terms<PACK, G4>(sm, p, lane, nu, (uint32_t)d, g, tf, tdoc, actm, pk_len, pk_nu, s0 - shift);
     if (p.debug_stop == 4) { clear_table(sm, lane); continue; }
 
@@ -1531,140 +1458,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     atomicAdd(&TFIDF_COLD(stats)[0], my_doc_count);
     atomicAdd(&TFIDF_COLD(stats)[1], my_ttf);
     atomicAdd(&TFIDF_COLD(stats)[2], my_nnz);
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Split form, second kernel: the dictionary half of k_tokenize_wave.  For each
-// unit the tokenizer staged (tl_n[u] terms at the unit's first row: tl_key =
-// short key or kFoldBit | slot, csr = tf | pack-local document << 24), one
-// wave resolves the short keys (probe_short_terms: all of a lane's probes in
-// flight) and writes the unit's CSR rows grouped by dictionary range, exactly
-// as the fused kernel's row phase.  No text, no term table: ~5 KB of LDS and
-// far fewer registers per wave than the tokenizer, so several times as many
-// waves per CU overlap their dictionary round trips (the fused kernel's
-// dictionary phase is a third of its wave time and mostly waiting, §5).
-constexpr uint32_t kResWaves = 4;
-struct ResSmem {
-  alignas(16) uint32_t stage[2 * kWaveTerms];   // retry queue (probe_short_terms), then CSR staging (col, tf)
-  alignas(16) uint32_t gcnt[192];               // group counters [0, 128), no-op counters [128, 192)
-  alignas(16) uint64_t pk_row[kPackMax];
-  alignas(16) uint32_t pk_start[kPackMax];
-};
-static_assert(2 * kWaveTerms * 4 >= (2 * kDictQueue + kWaveTerms / 2) * 8, "retry queue in the staging area");
-
-template <bool PACK, bool G4>
-__global__ void __launch_bounds__(64 * kResWaves) k_resolve_wave(BuildParams p) {
-  __shared__ ResSmem smw[kResWaves];
-  const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & 63;
-  ResSmem &sm = smw[wv];
-  const uint64_t n_units = PACK ? (p.n_docs + p.pack - 1) / p.pack : (TFIDF_COLD(doc_list) ? *TFIDF_COLD(doc_list_count) : p.n_docs);
-  const uint32_t R = p.n_ranges, rbits = (uint32_t)__builtin_ctz(R);
-  const uint32_t dmask = p.cap_mask;
-  for (uint64_t u = (uint64_t)blockIdx.x * kResWaves + wv; u < n_units; u += (uint64_t)gridDim.x * kResWaves) {
-    const uint32_t nu = TFIDF_COLD(tl_n)[u];
-    if (nu == kInvalidSlot) continue;                       // wave-uniform
-    uint64_t d, src;
-    uint32_t np = 1;
-    if (PACK) {
-      d = u * p.pack;
-      np = (uint32_t)min((uint64_t)p.pack, p.n_docs - d);
-    } else {
-      d = TFIDF_COLD(doc_list) ? TFIDF_COLD(doc_list)[u] : u;
-    }
-    src = TFIDF_COLD(live_map) ? TFIDF_COLD(live_map)[d] : d;
-    const uint64_t ebase = csr_row_base(p.offsets, src);
-    uint64_t lo[kWaveK];
-    uint32_t ps[kWaveK], g[kWaveK], tf[kWaveK], tdoc[kWaveK];
-    uint32_t actm = 0;
-    {
-      const uint64_t *tk = TFIDF_COLD(tl_key) + ebase;
-      const uint32_t *tw = p.csr + ebase;
-      uint64_t key[kWaveK];
-      uint32_t w[kWaveK];
-#pragma unroll
-      for (int k = 0; k < (int)kWaveK; k++) {
-        const uint32_t idx = lane + 64 * k;
-        key[k] = 0;
-        w[k] = 0;
-        if (idx < nu) { key[k] = __builtin_nontemporal_load(tk + idx); w[k] = __builtin_nontemporal_load(tw + idx); }
-      }
-#pragma unroll
-      for (int k = 0; k < (int)kWaveK; k++) {
-        const bool in = lane + 64 * k < nu;
-        const bool f = (key[k] & kFoldBit) != 0;
-        tf[k] = w[k] & 0xFFFFFFu;
-        tdoc[k] = w[k] >> 24;
-        lo[k] = in & !f ? key[k] : 0ull;
-        g[k] = in ? (f ? (uint32_t)key[k] : kLookupPending) : kInvalidSlot;
-        ps[k] = dict_home(dict_hash_short(lo[k]), dmask) & ~1u;
-        actm |= (uint32_t)in << k;
-      }
-    }
-    probe_short_terms<G4>(p, lane, lo, ps, g, reinterpret_cast<uint64_t *>(sm.stage));
-    {
-      bool caperr = false;
-#pragma unroll
-      for (int k = 0; k < (int)kWaveK; k++) {
-        const bool e = (((actm >> k) & 1u) != 0) & ((g[k] == kInvalidSlot) | (g[k] == kLookupPending));
-        caperr |= e;
-        if (e) g[k] = 0;
-      }
-      if (caperr) set_err(TFIDF_COLD(err), kErrCapacity, (uint32_t)d);
-    }
-    asm volatile("" ::: "memory");
-    // ---- CSR rows grouped by (document,) dictionary range: the fused kernel's row phase
-    uint32_t *st_col = sm.stage, *st_tf = sm.stage + kWaveTerms;
-    const uint32_t G = PACK ? np << rbits : R;
-    if (PACK) {
-      const uint32_t nuj = lane < np ? p.doc_nuniq[d + lane] : 0u;
-      const uint32_t incl = wave_incl_add(nuj);
-      if (lane < np) {
-        sm.pk_start[lane] = incl - nuj;
-        sm.pk_row[lane] = csr_row_base(p.offsets, src + lane);
-      }
-    }
-    uint32_t *gcnt = sm.gcnt;
-    gcnt[lane] = 0;
-    gcnt[lane + 64] = 0;
-    uint32_t grp[kWaveK], rank[kWaveK];
-#pragma unroll
-    for (int k = 0; k < (int)kWaveK; k++) {
-      const bool act = (actm >> k) & 1u;
-      grp[k] = act ? (PACK ? (tdoc[k] << rbits) + (g[k] >> p.range_shift) : (g[k] >> p.range_shift)) : 128u + lane;
-      rank[k] = atomicAdd(&gcnt[grp[k]], 1u);
-    }
-    const uint32_t c0 = gcnt[lane], c1 = gcnt[lane + 64];
-    const uint32_t i0 = wave_incl_add(c0);
-    const uint32_t i1 = wave_incl_add(c1) + (uint32_t)__builtin_amdgcn_readlane((int)i0, 63);
-    gcnt[lane] = i0 - c0;
-    gcnt[lane + 64] = i1 - c1;
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const uint32_t gg = lane + 64 * h, e = h ? i1 : i0;
-      if (gg < G) {
-        if (PACK) p.rsplit[(d + (gg >> rbits)) * R + (gg & (R - 1))] = e - sm.pk_start[gg >> rbits];
-        else p.rsplit[d * R + gg] = e;
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < (int)kWaveK; k++) {
-      if ((actm >> k) & 1u) {
-        const uint32_t pos = gcnt[grp[k]] + rank[k];
-        st_col[pos] = g[k];
-        st_tf[pos] = PACK ? tf[k] | (tdoc[k] << 24) : tf[k];
-      }
-    }
-    asm volatile("" ::: "memory");
-    if (PACK) {
-      for (uint32_t i = lane; i < nu; i += 64) {
-        const uint32_t t = st_tf[i], j = t >> 24;
-        csr_put(p, sm.pk_row[j] + i - sm.pk_start[j], st_col[i], t & 0xFFFFFFu, (uint32_t)(d + j));
-      }
-    } else {
-      for (uint32_t i = lane; i < nu; i += 64) csr_put(p, ebase + i, st_col[i], st_tf[i], (uint32_t)d);
-    }
-    asm volatile("" ::: "memory");
   }
 }
 
@@ -2647,18 +2440,6 @@ hipError_t launch_tokenize_wave(const BuildParams &p, int grid, hipStream_t s) {
 #define TFIDF_G4_BITS 21
 #endif
   const bool g4 = (uint64_t)p.cap_mask + 1 >= (1ull << TFIDF_G4_BITS);   // dictionary beyond L2: 4-slot probe groups
-  if (p.tl_n) {                                   // split form: tokenizer, then the dictionary / row kernel
-    if (p.pack > 1) {
-      hipLaunchKernelGGL((k_tokenize_wave<true, false, true>), dim3(grid), dim3(64), 0, s, p);
-      if (g4) hipLaunchKernelGGL((k_resolve_wave<true, true>), dim3(grid), dim3(64 * kResWaves), 0, s, p);
-      else hipLaunchKernelGGL((k_resolve_wave<true, false>), dim3(grid), dim3(64 * kResWaves), 0, s, p);
-    } else {
-      hipLaunchKernelGGL((k_tokenize_wave<false, false, true>), dim3(grid), dim3(64), 0, s, p);
-      if (g4) hipLaunchKernelGGL((k_resolve_wave<false, true>), dim3(grid), dim3(64 * kResWaves), 0, s, p);
-      else hipLaunchKernelGGL((k_resolve_wave<false, false>), dim3(grid), dim3(64 * kResWaves), 0, s, p);
-    }
-    return hipGetLastError();
-  }
   if (p.pack > 1) {
     if (g4) hipLaunchKernelGGL((k_tokenize_wave<true, true>), dim3(grid), dim3(64), 0, s, p);
     else hipLaunchKernelGGL((k_tokenize_wave<true, false>), dim3(grid), dim3(64), 0, s, p);

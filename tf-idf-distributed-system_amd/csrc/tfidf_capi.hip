@@ -170,7 +170,6 @@ struct tfidf_index {
   uint32_t cap_log2 = 18, C = 0, range_shift = 15, R = 1, n_blocks = 0;
   DevBuf dict, csr, csr_esc, post_esc, doc_len, doc_nuniq, doc_norm, rsplit, long_list, uni_list, counters, blk, bbase, post, post_tmp;
   DevBuf retry_list;                   // packed wave path: documents deferred to the single-document pass
-  DevBuf tl_key, tl_n;                 // split wave path: staged terms (row entries) and per-unit counts
   DevBuf bad_list;                     // documents that are not valid UTF-8 (indexed empty)
   std::vector<uint32_t> malformed;     // ... of the last commit, ascending committed ids
   std::vector<uint64_t> h_esc;         // CSR tf escapes of the last build, sorted (csr_put)
@@ -778,14 +777,6 @@ static int commit_once(tfidf_index *ix) {
     pack = std::min(pack, std::max(1u, kWaveGroups / ix->R));   // (document, range) groups per unit
   }
   if (pack > 1) HIP_TRY(ix->retry_list.reserve(N * 4 + 4));
-  // split wave path (k_tokenize_wave<SPLIT> + k_resolve_wave): the tokenizer
-  // stages each unit's distinct terms in row entries for the dictionary kernel
-  bool split = kWaveSplit;
-  if (const char *e = getenv("TFIDF_SPLIT")) split = atoi(e) != 0;   // A/B only
-  if (split) {
-    HIP_TRY(ix->tl_key.reserve(row_cap * 8));
-    HIP_TRY(ix->tl_n.reserve(N * 4 + 4));
-  }
   if (ix->term_major) {
     HIP_TRY(ix->row_off.reserve(N * 4 + 4));
     HIP_TRY(ix->toff.reserve(((size_t)C + 1) * 8));
@@ -834,8 +825,6 @@ static int commit_once(tfidf_index *ix) {
   if (const char *ds = getenv("TFIDF_DEBUG_STOP")) bp.debug_stop = (uint32_t)atoi(ds);   // profiling only
   bp.pack = pack;
   bp.retry_list = pack > 1 ? ix->retry_list.as<uint32_t>() : nullptr;
-  bp.tl_key = split ? ix->tl_key.as<uint64_t>() : nullptr;
-  bp.tl_n = split ? ix->tl_n.as<uint32_t>() : nullptr;
   bp.retry_count = reinterpret_cast<uint32_t *>(ctr + 5);
   ix->pack_docs = pack;
   ix->pack_retried = 0;

@@ -84,12 +84,6 @@ struct BuildParams {
   // k_tokenize_uchunk (nullptr: such a unit fails its document)
   uint32_t *uchunk_list;
   uint32_t *uchunk_count;
-  // split wave path (tl_n != nullptr): k_tokenize_wave stages each unit's
-  // distinct terms (tl_key[row entry] = short key or kFoldBit | slot, csr[row
-  // entry] = tf | pack-local doc << 24; tl_n[unit] = their number or
-  // 0xFFFFFFFF) and k_resolve_wave resolves them and writes the rows
-  uint64_t *tl_key;
-  uint32_t *tl_n;
 };
 
 __host__ __device__ inline uint64_t csr_row_base(const uint64_t *offsets, uint64_t src) {
@@ -235,7 +229,6 @@ inline void allow_dyn_lds(const void *fn, int bytes, std::atomic<uint64_t> &done
 // --- launch wrappers (kernels_index.hip) ---
 hipError_t launch_tokenize_wave(const BuildParams &p, int grid, hipStream_t s);
 constexpr uint32_t kWaveWGsPerCU = 8;       // 64-thread workgroups per CU (2 waves/SIMD: VGPR- and LDS-bound)
-constexpr bool kWaveSplit = false;            // split wave path by default (TFIDF_SPLIT overrides)
 constexpr uint32_t kWaveGroups = 128;     // CSR row groups per wave unit (documents x ranges, k_tokenize_wave)
 constexpr uint32_t kPackMaxDocs = 16;     // documents per packed window (<= kPackMax, kernels_index.hip)
 constexpr uint64_t kPackBytes = 2560;     // text per packed window (auto pack size): ~450 tokens, under the
