@@ -385,6 +385,21 @@ struct RsSmem {
 };
 constexpr uint32_t kRsWaveWords = kRsItems * 64;        // consecutive words per wave
 
+// Tile of workgroup b: workgroups go to the 8 XCDs round-robin (b mod 8), so
+// XCD x gets the contiguous tile range [x n / 8, (x + 1) n / 8) in order.
+// The workgroups running together on one XCD then hold consecutive tiles,
+// whose runs of one digit are adjacent in the output: the lines two runs
+// share are completed in that XCD's L2 instead of being written partially
+// from two XCDs.
+#ifndef TFIDF_RS_XCD
+#define TFIDF_RS_XCD 1
+#endif
+__device__ __forceinline__ uint32_t rs_tile(uint32_t b, uint32_t n) {
+  if (!TFIDF_RS_XCD) return b;
+  const uint32_t x = b & 7u, i = b >> 3, q = n >> 3, r = n & 7u;
+  return x * q + min(x, r) + i;
+}
+
 // LAST: write postings (and df run lengths) instead of words.
 template <bool LAST>
 __global__ void __launch_bounds__(kRsThreads) k_rs_scatter(const uint64_t *keys, uint64_t *out, uint64_t n,
@@ -392,15 +407,16 @@ __global__ void __launch_bounds__(kRsThreads) k_rs_scatter(const uint64_t *keys,
                                                            const uint32_t *hist, const uint32_t *gstart, TermParams p) {
   __shared__ RsSmem sm;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const uint64_t t0 = (uint64_t)blockIdx.x * kRsTile;
+  const uint32_t tile = rs_tile(blockIdx.x, n_tiles);
+  const uint64_t t0 = (uint64_t)tile * kRsTile;
   // the tile's digit starts: exclusive scan of its histogram over digits
   {
-    const uint32_t c = tid < 256 ? hist[(uint64_t)blockIdx.x * 256 + tid] : 0u;
+    const uint32_t c = tid < 256 ? hist[(uint64_t)tile * 256 + tid] : 0u;
     uint32_t tot;
     const uint32_t st = block_incl_scan(c, sm.wsum, &tot) - c;
     if (tid < 256) {
       sm.start[tid] = st;
-      sm.gpos[tid] = gstart[(uint64_t)blockIdx.x * 256 + tid];
+      sm.gpos[tid] = gstart[(uint64_t)tile * 256 + tid];
 #pragma unroll
       for (uint32_t w = 0; w < kRsWaves; w++) sm.wcnt[w][tid] = 0;
     }
