@@ -945,7 +945,7 @@ __global__ void __launch_bounds__(kPairWaves * 64) k_score_pairs(QueryParams p) 
 // heavy plain disjunctions with k <= 64 (cfg 4, block-major postings; the
 // light queries take k_score_wunits).  The host cuts each query into units of
 // about T/4096 postings (heavy queries into several block ranges).  Per block
-// of the unit, for each query term in query order, the 256 threads add the
+// of the unit, for each query term in query order, the 512 threads add the
 // term's block segment into a dense LDS accumulator of doubles: a document's
 // first touch (its bit in `bits`, set by the atomic that tests it) stores the
 // term score, later terms add to it — the disjunction's double sum in query
@@ -959,8 +959,16 @@ __global__ void __launch_bounds__(kPairWaves * 64) k_score_pairs(QueryParams p) 
 // wave 0 merges the four lists and writes them as the candidates of pair
 // (q, b0) (cand_n = 0 for the unit's other blocks); k_merge_topk orders each
 // query's candidates (several units for a split query).
-constexpr uint32_t kUnitThreads = 256;
+#ifndef TFIDF_UNIT_THREADS
+#define TFIDF_UNIT_THREADS 512   // 8 waves: 4 per SIMD at two workgroups per CU (256 threads: batch device 6.06 ms, 512: 5.81)
+#endif
+constexpr uint32_t kUnitThreads = TFIDF_UNIT_THREADS;
 constexpr uint32_t kUnitWaves = kUnitThreads / 64;
+// hit scan: wave w walks bit words [w, w + 1) * kUnitScanWords, kUnitLanesPerWord
+// lanes per word (each its share of the word's bits)
+constexpr uint32_t kUnitScanWords = kBlockDocs / 32 / kUnitWaves;
+constexpr uint32_t kUnitLanesPerWord = 64 / kUnitScanWords;
+static_assert(kUnitScanWords * kUnitWaves == kBlockDocs / 32 && kUnitLanesPerWord * kUnitScanWords == 64, "scan layout");
 constexpr uint32_t kUnitU = 4;                 // postings per thread in flight
 constexpr uint32_t kUnitPre = 4;               // query terms whose first chunk is prefetched per block
 
@@ -1146,7 +1154,7 @@ __global__ void __launch_bounds__(kUnitThreads) k_score_units(QueryParams p, con
       for (uint32_t j = 0; j < kUnitPre; j++)
 #pragma unroll
         for (int v = 0; v < (int)kUnitU; v++) pre[j][v] = npre[j][v];
-      // wave wid scans documents [2048 wid, 2048 wid + 2048): lane l owns bit word 64 wid + l
+      // wave wid scans documents [32 kUnitScanWords wid, + 32 kUnitScanWords): kUnitLanesPerWord lanes per bit word
       // two hits per lane per step (both LDS round trips in flight); no key at
       // or below another wave's k-th key (sm.thr, read once per block) can win
       // Once the k-th key's score exceeds the lightest term's weight w_l, a
@@ -1156,13 +1164,18 @@ __global__ void __launch_bounds__(kUnitThreads) k_score_units(QueryParams p, con
       // low-idf term plus rarer ones: most hits are skipped unread.  (Skipping
       // that term's postings themselves was measured slower: 5.7 -> 6.3 ms at
       // cfg 4 — a wave of its postings almost always holds a few to score.)
-      const uint32_t wi = wid * 64 + lane;
+      const uint32_t wi = wid * kUnitScanWords + lane / kUnitLanesPerWord;
+      constexpr uint32_t kLaneBits = 32 / kUnitLanesPerWord;
+      const uint32_t lmask = kUnitLanesPerWord == 1 ? 0xFFFFFFFFu
+                                                    : ((1u << kLaneBits) - 1u) << (kLaneBits * (lane % kUnitLanesPerWord));
       uint64_t th = max(theta, (uint64_t)sm.thr);
       const uint64_t th_in = th;
       const bool prune = nt > 1 && sm.tw[sm.light] < __uint_as_float((uint32_t)(th >> 32));
-      uint32_t wb = prune ? sm.obits[wi] : sm.bits[wi];
-      sm.bits[wi] = 0;
-      sm.obits[wi] = 0;
+      uint32_t wb = (prune ? sm.obits[wi] : sm.bits[wi]) & lmask;
+      if (lane % kUnitLanesPerWord == 0) {                      // after the word's lanes read it (wave order)
+        sm.bits[wi] = 0;
+        sm.obits[wi] = 0;
+      }
       while (__any(wb != 0)) {
         uint32_t x[2];
         bool has[2];
