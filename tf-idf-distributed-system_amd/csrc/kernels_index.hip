@@ -1159,6 +1159,9 @@ __device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p
 // sharing one window.  A pack that cannot take the packed path (window or
 // token/term capacity, non-contiguous sources, an empty or non-ASCII document)
 // sends its documents to retry_list for a PACK = false pass.
+#ifndef TFIDF_WAVE_XCD
+#define TFIDF_WAVE_XCD 1
+#endif
 template <bool PACK, bool G4>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_tokenize_wave(BuildParams p) {
   __shared__ WaveSmem sm;
@@ -1168,9 +1171,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   unsigned long long my_doc_count = 0, my_ttf = 0, my_nnz = 0;
   uint4 v[4] = {make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0), make_uint4(0, 0, 0, 0)};
   const uint64_t n_units = PACK ? (p.n_docs + p.pack - 1) / p.pack : (TFIDF_COLD(doc_list) ? *TFIDF_COLD(doc_list_count) : p.n_docs);
+  // Units of this workgroup: XCD x (= workgroup mod 8, the dispatch order)
+  // takes the contiguous eighth [x, x + 1) * n_units / 8 of the units, so
+  // the documents running together on one XCD are neighbours and the CSR
+  // lines their rows share are completed in that XCD's L2.
+  const bool xm = TFIDF_WAVE_XCD && (gridDim.x & 7u) == 0 && n_units >= 8ull * gridDim.x;
+  const uint64_t per = (n_units + 7) / 8;
+  const uint64_t ubeg = xm ? (blockIdx.x & 7u) * per + (blockIdx.x >> 3) : blockIdx.x;
+  const uint64_t uend = xm ? min(n_units, ((blockIdx.x & 7u) + 1) * per) : n_units;
+  const uint64_t ustep = xm ? gridDim.x >> 3 : gridDim.x;
   DocMeta meta;
-  if (blockIdx.x < n_units) {
-    meta = unit_meta<PACK>(p, blockIdx.x, lane);
+  if (ubeg < uend) {
+    meta = unit_meta<PACK>(p, ubeg, lane);
     prefetch_wave(p, meta, lane, v);
   }
   const uint32_t R = p.n_ranges;
@@ -1180,16 +1192,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
            *pk_start = pk_len + 2 * kPackMax;
   uint64_t *pk_row = sm.qkey + 2 * kPackMax;
 
-  for (uint64_t u = blockIdx.x; u < n_units; u += gridDim.x) {
+  for (uint64_t u = ubeg; u < uend; u += ustep) {
     const uint64_t d = meta.d, src = meta.src, L = meta.L, s0 = meta.s0;
     const uint32_t shift = meta.shift, np = meta.np;
     const uint64_t pofs = meta.pofs;
     const bool fits = fits_wave(meta);
-    const uint64_t un = u + gridDim.x;
+    const uint64_t un = u + ustep;
     if (!fits) {
       if (PACK) defer_pack(p, d, np, lane);
       else if (lane == 0) TFIDF_COLD(long_list)[atomicAdd(TFIDF_COLD(long_count), 1u)] = (uint32_t)d;
-      if (un < n_units) { meta = unit_meta<PACK>(p, un, lane); prefetch_wave(p, meta, lane, v); }
+      if (un < uend) { meta = unit_meta<PACK>(p, un, lane); prefetch_wave(p, meta, lane, v); }
       continue;                                             // wave-uniform
     }
     // ---- stage: registers -> LDS (whole window; bytes outside the document
@@ -1225,7 +1237,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       W = regs_word_mask<PACK>(v, nrows, sm.text, wm16, wm16 + 256, lane, &bad, &under, &wbase, &upper);
     }
     // the next document's window, now that this one's registers are consumed
-    if (un < n_units) { meta = unit_meta<PACK>(p, un, lane); prefetch_wave(p, meta, lane, v); }
+    if (un < uend) { meta = unit_meta<PACK>(p, un, lane); prefetch_wave(p, meta, lane, v); }
     asm volatile("" ::: "memory");
     if (p.debug_stop == 1) continue;
     // PACK: document boundaries q_j (window position of document j's first
