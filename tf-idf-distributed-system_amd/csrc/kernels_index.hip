@@ -1175,7 +1175,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   // takes the contiguous eighth [x, x + 1) * n_units / 8 of the units, so
   // the documents running together on one XCD are neighbours and the CSR
   // lines their rows share are completed in that XCD's L2.
-  const bool xm = TFIDF_WAVE_XCD && (gridDim.x & 7u) == 0 && n_units >= 8ull * gridDim.x;
+  const bool xm = TFIDF_WAVE_XCD && (gridDim.x & 7u) == 0 && n_units >= gridDim.x;
   const uint64_t per = (n_units + 7) / 8;
   const uint64_t ubeg = xm ? (blockIdx.x & 7u) * per + (blockIdx.x >> 3) : blockIdx.x;
   const uint64_t uend = xm ? min(n_units, ((blockIdx.x & 7u) + 1) * per) : n_units;
