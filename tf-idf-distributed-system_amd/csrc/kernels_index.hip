@@ -1506,10 +1506,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     for (int k = 0; k < 4; k++)
       if (lane + 64 * k < nchunks) v[k] = gload16(src + lane + 64 * k);
   };
+  uint32_t my_uc = 0;                                        // units this wave flagged for k_tokenize_uchunk
   if (blockIdx.x < n_units) { meta = chunk_meta(p, blockIdx.x); prefetch(meta); }
   for (uint64_t u = blockIdx.x; u < n_units; u += gridDim.x) {
     const ChunkMeta m = meta;
     const uint64_t un = u + gridDim.x;
+    uint32_t hib = 0;                                          // OR of the window's bytes: bit 7s = non-ASCII
     {   // stage (bytes outside the window zeroed), then fetch the next unit
       const uint32_t hi_b = m.shift + (uint32_t)m.L;
       const uint32_t nchunks = (hi_b + 15) >> 4;
@@ -1524,23 +1526,28 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
           val.z &= keep_range(16 * c + 8, m.shift, hi_b);
           val.w &= keep_range(16 * c + 12, m.shift, hi_b);
         }
+        hib |= val.x | val.y | val.z | val.w;
         dst[c] = val;
       }
     }
     if (un < n_units) { meta = chunk_meta(p, un); prefetch(meta); }
     asm volatile("" ::: "memory");
     const uint32_t fail_at = m.gi;
-    bool bad, under;
-    uint64_t wbase = 0;
-    bool upper;
-    const uint64_t W = lane_word_mask<false>(sm.text, lane, &bad, &under, &wbase, &upper);
-    if (bad) {                                               // non-ASCII: the Unicode chunk kernel
+    // non-ASCII text (the classifier's own test, from the staged registers, so
+    // such a unit is not classified here): flagged for the Unicode chunk kernel
+    // (a flag per unit, counted once per wave at the end — a list appended
+    // with one atomic per unit serialised 15 k units on one counter)
+    if (__any((hib & 0x80808080u) != 0)) {
       if (lane == 0) {
-        if (p.uchunk_list) p.uchunk_list[atomicAdd(p.uchunk_count, 1u)] = (uint32_t)u;
+        if (p.uchunk_list) { p.uchunk_list[u] = 1u; my_uc++; }
         else p.chunk_fail[fail_at] = 1u;
       }
       continue;
     }
+    bool bad, under;
+    uint64_t wbase = 0;
+    bool upper;
+    const uint64_t W = lane_word_mask<false>(sm.text, lane, &bad, &under, &wbase, &upper);
     const uint64_t wlast = __ballot((W >> 63) & 1ull);
     const uint64_t prevW = lane ? (wlast >> (lane - 1)) & 1ull : 0ull;
     const uint64_t S = W & ~((W << 1) | prevW);
@@ -1646,6 +1653,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     }
     clear_table(sm, lane);
   }
+  if (my_uc) atomicAdd(p.uchunk_count, my_uc);              // lane 0
 }
 
 // One workgroup per long document of the group: its units' pair lists ->

@@ -452,15 +452,15 @@ __device__ __forceinline__ bool uc_short_ascii_key(const uint8_t *text, uint32_t
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_tokenize_uchunk(BuildParams p) {
   __shared__ UcSmem sm;
   const uint32_t lane = threadIdx.x;
-  const uint32_t n_units = *p.uchunk_count;
-  if (blockIdx.x >= n_units) return;                        // block-uniform
+  // units flagged by k_tokenize_chunk (uchunk_list[u] != 0; *uchunk_count of them)
+  if (*p.uchunk_count == 0) return;                         // block-uniform
   for (uint32_t e = lane; e < kUwStates * kUwClasses; e += 64)
     sm.tr[e] = (uint8_t)uc_word_next(e / kUwClasses, e % kUwClasses);
   for (uint32_t e = lane; e < 128; e += 64) sm.asc[e] = (uint8_t)uc_ascii_class(e);
   uc_clear_all(sm, lane);
   __syncthreads();
-  for (uint32_t it = blockIdx.x; it < n_units; it += gridDim.x) {
-    const uint32_t u = p.uchunk_list[it];
+  for (uint32_t u = blockIdx.x; u < p.n_chunks; u += gridDim.x) {
+    if (p.uchunk_list[u] == 0) continue;                    // block-uniform
     const ChunkMeta m = chunk_meta(p, u);
     const uint64_t src = p.live_map ? p.live_map[m.d] : m.d;
     const bool doc_end = m.s0 + m.L == p.offsets[src + 1];  // the window reaches the document's end

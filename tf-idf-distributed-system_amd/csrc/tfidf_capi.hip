@@ -918,7 +918,7 @@ static int commit_once(tfidf_index *ix) {
     HIP_TRY(ix->chunk_list.reserve(pre.size() * 4 + 8));
     HIP_TRY(ix->chunk_docs.reserve((size_t)n_long * 4));
     HIP_TRY(ix->chunk_fail.reserve((size_t)n_long * 4));
-    HIP_TRY(ix->uchunk.reserve(max_units * 4 + 16));     // [0] count, [4 ..] units with non-ASCII text
+    HIP_TRY(ix->uchunk.reserve(max_units * 4 + 16));     // [0] count, [4 ..] per unit: non-ASCII text
     HIP_TRY(ix->pre_h.resize(pre.size()));
     memcpy(ix->pre_h.data(), pre.data(), pre.size() * 4);
     HIP_TRY(hipMemcpyAsync(ix->chunk_list.p, ix->pre_h.data(), pre.size() * 4, hipMemcpyHostToDevice, s));
@@ -942,7 +942,7 @@ static int commit_once(tfidf_index *ix) {
       const bool uch = !getenv("TFIDF_NO_UCHUNK");
       cp.uchunk_count = uch ? ix->uchunk.as<uint32_t>() : nullptr;
       cp.uchunk_list = uch ? ix->uchunk.as<uint32_t>() + 4 : nullptr;
-      if (uch) HIP_TRY(hipMemsetAsync(ix->uchunk.p, 0, 4, s));
+      if (uch) HIP_TRY(hipMemsetAsync(ix->uchunk.p, 0, (size_t)(cp.n_chunks + 4) * 4, s));
       const uint64_t grid = std::min<uint64_t>(cp.n_chunks, (uint64_t)ix->num_cus * kWaveWGsPerCU);
       HIP_TRY(launch_tokenize_chunks(cp, (int)grid, s));
       if (uch)      // the count is read on the device: exits at once when no unit was listed
