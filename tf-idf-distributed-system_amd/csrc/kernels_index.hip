@@ -1154,6 +1154,13 @@ __device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p
   }
 }
 
+// A flag per document for k_tokenize_uwave (no shared counter: a list
+// appended with one atomic per document serialised a corpus of non-ASCII
+// documents on one address).  Not inlined: inline, the store changed the
+// tokenizer's register allocation (247 VGPRs, cfg-2 tokenize +0.1 ms).  The
+// array is an argument: a called function has no kernarg pointer (TFIDF_COLD).
+__device__ __noinline__ void flag_unicode(uint32_t *flags, uint64_t d) { flags[d] = 1u; }
+
 // Units: PACK = false, one document per unit (documents 0..n_docs-1, or the
 // doc_list entries); PACK = true, unit u = documents [u * pack, u * pack + pack)
 // sharing one window.  A pack that cannot take the packed path (window or
@@ -1263,7 +1270,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     }
     if (bad) {                                              // non-ASCII: the Unicode wave path
       if (PACK) defer_pack(p, d, np, lane);
-      else if (lane == 0) TFIDF_COLD(uni_list)[atomicAdd(TFIDF_COLD(uni_count), 1u)] = (uint32_t)d;
+      else if (lane == 0) flag_unicode(TFIDF_COLD(uni_list), d);
       continue;
     }
     const uint64_t wlast = __ballot((W >> 63) & 1ull);

@@ -48,294 +48,14 @@ struct UwClassSrcRef {
 constexpr uint32_t kUwClasses = 19;     // kUc* classes
 constexpr uint32_t kUwStates = 12;      // kW* states (incl. kWDead)
 
-// WORD-rule scan over chars (not units): an extender keeps the DFA state (it
-// belongs to the unit of the preceding head), any other class takes a
-// transition of the LDS table built from uc_word_next.  Same spans as
-// uc_next_span (unicode_scan.h), with one LDS read per char for the class and
-// one for the transition instead of the branchy unit walk.
-__device__ __forceinline__ bool uw_next_span(const uint8_t *cls, const uint8_t *tr, uint32_t n, uint32_t *pos,
-                                             uint32_t stop, uint32_t *ts, uint32_t *te, bool *bad) {
-  while (*pos < stop) {
-    const uint32_t i = *pos;
-    const uint32_t v = cls[i];
-    if (v == 0xFFu) { *bad = true; return false; }
-    const uint32_t c = v & 31u, l = (v >> 5) + 1;
-    const uint32_t st0 = tr[kWStart * kUwClasses + c];
-    if (st0 != kWDead) {                                  // ALetter / Hebrew / Numeric / Katakana / ENL
-      uint32_t st = st0, p = i + l, last = uc_word_accepting(st) ? p : i, erun = p;
-      while (p < n) {
-        const uint32_t w = cls[p];
-        if (w == 0xFFu) { *bad = true; return false; }
-        const uint32_t cw = w & 31u;
-        if (!uc_is_extender(cw)) {
-          const uint32_t ns = tr[st * kUwClasses + cw];
-          if (ns == kWDead) break;
-          st = ns;
-        }
-        p += (w >> 5) + 1;
-        if (uc_word_accepting(st)) last = p;
-        else if (st == kWELead) erun = p;
-      }
-      if (last > i) { *ts = i; *te = last; *pos = last; return true; }
-      uint32_t q = i + l;                                 // ENL run, no core: see uc_next_span
-      while (q < erun && (cls[q] & 31u) != kUcExtendSA) q += (cls[q] >> 5) + 1;
-      *pos = q;
-      continue;
-    }
-    if (c == kUcOther || c == kUcExtend || c == kUcZWJ || c == kUcMidLetter || c == kUcMidNumLet ||
-        c == kUcMidNum || c == kUcSQuote || c == kUcDQuote) {
-      *pos = i + l;                                       // [^]
-      continue;
-    }
-    // SA runs, Han / Hiragana / emoji / Regional_Indicator units: the shared scanner
-    const UwClassSrcRef src{cls};
-    uint64_t p64 = i, ts64, te64;
-    if (!uc_next_span(src, n, &p64, (uint64_t)i + 1, &ts64, &te64, bad)) {
-      *pos = (uint32_t)p64;
-      if (*bad) return false;
-      continue;
-    }
-    *ts = (uint32_t)ts64; *te = (uint32_t)te64; *pos = (uint32_t)p64;
-    return true;
-  }
-  return false;
-}
-
-struct UwSmem {
-  alignas(16) uint8_t text[kUwWindow + 16];
-  alignas(16) uint8_t cls[kUwWindow];
-  unsigned long long klo[kUwSlots];   // key lo; after the lookup: dictionary slot
-  unsigned long long khi[kUwSlots];   // key hi (VALID bit set: occupied)
-  uint32_t cnt[kUwSlots];             // tf
-  uint32_t kpos[kUwSlots];            // first occurrence: start | end << 16 (document bytes)
-  uint32_t rcnt[kUwMaxRanges];        // per-range counts, then cursors
-  uint8_t tr[kUwStates * kUwClasses]; // WORD DFA transitions
-};
-
-__device__ __forceinline__ uint32_t uw_incl_add(uint32_t x, uint32_t lane) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
-    if (lane >= (uint32_t)o) x += y;
-  }
-  return x;
-}
-
-__global__ void __launch_bounds__(64) k_tokenize_uwave(BuildParams p) {
-  __shared__ UwSmem sm;
-  const uint32_t lane = threadIdx.x;
-  const uint32_t n_uni = *p.uni_count;
-  const uint32_t R = p.n_ranges;
-  unsigned long long my_dc = 0, my_ttf = 0, my_nnz = 0;
-  if (blockIdx.x >= n_uni) return;                          // block-uniform
-  for (uint32_t e = lane; e < kUwStates * kUwClasses; e += 64)
-    sm.tr[e] = (uint8_t)uc_word_next(e / kUwClasses, e % kUwClasses);
-  __syncthreads();
-
-  for (uint32_t it = blockIdx.x; it < n_uni; it += gridDim.x) {
-    const uint32_t d = p.uni_list[it];
-    const uint64_t src = p.live_map ? p.live_map[d] : d;
-    const uint64_t s0 = p.offsets[src];
-    const uint64_t L = p.offsets[src + 1] - s0;
-    if (L > kUwWindow || R > kUwMaxRanges) {                // wave-uniform
-      if (lane == 0) p.long_list[atomicAdd(p.long_count, 1u)] = d;
-      continue;
-    }
-    // ---- stage (aligned 16 B loads) + clear the table
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p.text + s0);
-    const uint32_t shift = (uint32_t)(a & 15);
-    const uint32_t nchunks = (uint32_t)((shift + L + 15) >> 4);
-    const uint4 *gsrc = reinterpret_cast<const uint4 *>(a - shift);
-    uint4 *dst = reinterpret_cast<uint4 *>(sm.text);
-    for (uint32_t c = lane; c < nchunks; c += 64) dst[c] = gsrc[c];
-    for (uint32_t s = lane; s < kUwSlots; s += 64) { sm.klo[s] = 0; sm.khi[s] = 0; sm.cnt[s] = 0; }
-    sm.rcnt[lane] = 0;
-    __syncthreads();
-    const uint8_t *doc = sm.text + shift;
-    // ---- classes: lane l decodes bytes [64 l, 64 l + 64); ASCII words take no table read
-    for (uint32_t j = 0; j < 64; j += 4) {
-      const uint32_t i0 = 64 * lane + j;
-      if (i0 >= L) break;
-      uint32_t w = 0;
-#pragma unroll
-      for (int b = 0; b < 4; b++) w |= (i0 + b < L ? (uint32_t)doc[i0 + b] : 0x20u) << (8 * b);
-      uint32_t out = 0;
-      if ((w & 0x80808080u) == 0) {
-#pragma unroll
-        for (int b = 0; b < 4; b++) out |= uc_ascii_class((w >> (8 * b)) & 0xFFu) << (8 * b);
-      } else {
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-          const uint32_t x = (w >> (8 * b)) & 0xFFu;
-          uint32_t v;
-          if (x < 0x80u) v = uc_ascii_class(x);
-          else if ((x & 0xC0u) == 0x80u || i0 + b >= L) v = 0xFFu;
-          else {
-            uint32_t l;
-            const uint32_t cp = utf8_decode(doc, L, i0 + b, &l);
-            v = cp == kUcBad ? 0xFFu : (uc_class(cp) | ((l - 1) << 5));
-          }
-          out |= v << (8 * b);
-        }
-      }
-      const uint32_t keep = L - i0 >= 4 ? 4u : (uint32_t)(L - i0);
-#pragma unroll
-      for (int b = 0; b < 4; b++)
-        if ((uint32_t)b < keep) sm.cls[i0 + b] = (uint8_t)(out >> (8 * b));
-    }
-    __syncthreads();
-
-
-    // ---- slices: lane l scans tokens starting in [cut(l), cut(l + 1))
-    const uint64_t seg = (L + 63) >> 6;
-    auto cut = [&](uint64_t t) -> uint64_t {
-      if (t == 0) return 0;
-      uint64_t q = t * seg;
-      if (q >= L) return L;
-      while (q < L && !uc_split_byte(doc[q - 1])) q++;
-      return q;
-    };
-    uint64_t pos = cut(lane);
-    const uint64_t stop = cut(lane + 1);
-    bool active = pos < stop, ubad = false, overflow = false;
-    uint32_t ntok = 0;
-    bool collide = false;
-    while (__any(active)) {
-      uint64_t lo = 0, hi = 0;
-      bool have = false;
-      uint32_t ts32 = 0, te32 = 0;
-      if (active) {
-        uint32_t p32 = (uint32_t)pos;
-        have = uw_next_span(sm.cls, sm.tr, (uint32_t)L, &p32, (uint32_t)stop, &ts32, &te32, &ubad);
-        if (have) {
-          const uint64_t cutp = uc_token_key(doc, L, ts32, te32, &lo, &hi, p.hash_seed);
-          if (cutp < te32) { p32 = (uint32_t)cutp; te32 = (uint32_t)cutp; }   // 255-unit cut: rescan from the cut
-        }
-        pos = p32;
-        active = have;
-      }
-      ntok += have;
-      // round insert: probe from the key's home slot, linear
-      uint32_t slot = dict_hash(lo, hi) >> (32 - kUwSlotBits);
-      bool done = !have;
-      for (uint32_t r = 0; r < kUwSlots && __any(!done); r++) {
-        unsigned long long old = 1;
-        if (!done) old = atomicCAS(&sm.klo[slot], 0ull, (unsigned long long)lo);
-        const bool won = !done && old == 0;
-        if (won) { sm.khi[slot] = hi; sm.kpos[slot] = ts32 | (te32 << 16); }
-        asm volatile("" ::: "memory");
-        bool match = false;
-        if (!done && !won && old == lo) match = sm.khi[slot] == hi;
-        if (match && (lo & kLoHashed)) {                    // hashed key: the same term? (kErrCollision if not)
-          const uint32_t kp = sm.kpos[slot], a = kp & 0xFFFFu, z = kp >> 16;
-          collide |= !uc_same_term(doc + a, z - a, doc + ts32, te32 - ts32);
-        }
-        if (won || match) {
-          atomicAdd(&sm.cnt[slot], 1u);
-          done = true;
-        } else if (!done) {
-          slot = (slot + 1) & (kUwSlots - 1);
-        }
-      }
-      overflow |= !done;
-    }
-    if (collide) set_build_err(p.err, kErrCollision, d);
-    // ---- distinct terms; documents the wave cannot take go to the long path
-    uint32_t occ = 0;
-    for (uint32_t s = lane; s < kUwSlots; s += 64) occ += sm.khi[s] != 0;
-    const uint32_t nu = (uint32_t)__builtin_amdgcn_readlane((int)uw_incl_add(occ, lane), 63);
-    if (__any(ubad) || __any(overflow) || nu > kUwMaxTerms) {   // wave-uniform
-      if (lane == 0) p.long_list[atomicAdd(p.long_count, 1u)] = d;
-      __syncthreads();
-      continue;
-    }
-    const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)uw_incl_add(ntok, lane), 63);
-    // ---- dictionary slots (8 lookups per lane in flight), range counts
-    for (int h = 0; h < 2; h++) {
-      uint64_t klo[8], khi[8], mine[8];
-      bool act[8], cl[8];
-      uint32_t g[8];
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const uint32_t s = lane + 64 * (8 * h + k);
-        klo[k] = sm.klo[s];
-        khi[k] = sm.khi[s];
-        act[k] = khi[k] != 0;
-        const uint32_t kp = sm.kpos[s];
-        mine[k] = dict_ref_word(s0 + (kp & 0xFFFFu), (kp >> 16) - (kp & 0xFFFFu));
-        if (!act[k]) { klo[k] = 1; khi[k] = kKeyValid; }
-      }
-      dict_lookup_multi<8>(p.dict, p.cap_mask, klo, khi, act, g, mine, cl);
-#pragma unroll
-      for (int k = 0; k < 8; k++) {
-        if (!act[k]) continue;
-        if ((klo[k] & kLoHashed) && !cl[k] && g[k] != kInvalidSlot) dict_verify(p, g[k], mine[k], d);
-        uint32_t gs = g[k];
-        if (gs == kInvalidSlot) { atomicOr(p.err, kErrCapacity); gs = 0; }
-        sm.klo[lane + 64 * (8 * h + k)] = gs;
-        atomicAdd(&sm.rcnt[gs >> p.range_shift], 1u);
-      }
-    }
-    __syncthreads();
-    // ---- row segments: inclusive ends per range, cursors = exclusive starts
-    {
-      const uint32_t c = lane < R ? sm.rcnt[lane] : 0u;
-      const uint32_t incl = uw_incl_add(c, lane);
-      if (lane < R) {
-        p.rsplit[(uint64_t)d * R + lane] = incl;
-        sm.rcnt[lane] = incl - c;
-      }
-    }
-    __syncthreads();
-    const uint64_t base = csr_row_base(p.offsets, src);
-    for (uint32_t s = lane; s < kUwSlots; s += 64) {
-      if (sm.khi[s] == 0) continue;
-      const uint32_t gs = (uint32_t)sm.klo[s];
-      const uint32_t at = atomicAdd(&sm.rcnt[gs >> p.range_shift], 1u);
-      csr_put(p, base + at, gs, sm.cnt[s], d);
-    }
-    if (lane == 0) {
-      p.doc_len[d] = len;
-      p.doc_nuniq[d] = nu;
-      p.doc_norm[d] = (uint8_t)int_to_byte4(len);
-      my_dc += len > 0;
-      my_ttf += len;
-      my_nnz += nu;
-    }
-    __syncthreads();
-  }
-  if (lane == 0 && (my_ttf | my_nnz)) {
-    atomicAdd(&p.stats[0], my_dc);
-    atomicAdd(&p.stats[1], my_ttf);
-    atomicAdd(&p.stats[2], my_nnz);
-  }
-}
-
-hipError_t launch_tokenize_uwave(const BuildParams &p, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(k_tokenize_uwave, dim3(grid), dim3(64), 0, s, p);
-  return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
-// Book-sized documents, units with non-ASCII text (round 4).  k_tokenize_chunk
-// lists a (document, 2 KB core) unit whose window holds a byte >= 0x80; this
-// kernel tokenizes that unit with the Unicode scanner instead of sending the
-// whole book to k_tokenize_long.  One wavefront per unit: the window (core +
-// context margins) is staged in LDS with per-byte classes; the scan starts at
-// a split point (the byte before it is ASCII class OTHER: the scanner's start
-// state holds there) at or before the core, lanes take slices between split
-// points, and only tokens STARTING in the core are counted (a token crossing
-// the core's start belongs to the unit before).  The unit's distinct terms are
-// resolved in the dictionary and stored as its bucketed (slot, tf) pair list,
-// exactly as k_tokenize_chunk stores an ASCII unit's, for k_long_rows.  A unit
-// this cannot take decides its document for the long path (chunk_fail): no
-// split point in the leading margin (e.g. unspaced CJK), a token that reaches
-// the window's end before the document's, a token over 255 UTF-16 units,
-// malformed UTF-8, > kPairWords distinct terms.
-
-// uw_next_span with one more outcome: *at_end = the span scan reached byte n
-// while a longer match was still possible (the window ends there, not the
-// document: the token's true extent is unknown)
+// WORD-rule scan over chars (not units), from *pos up to stop: the next token
+// span [*ts, *te).  An extender keeps the DFA state (it belongs to the unit
+// of the preceding head), any other class takes a transition of the LDS table
+// built from uc_word_next; the same spans as uc_next_span (unicode_scan.h),
+// with one LDS read per char for the class and one for the transition.  Runs
+// of ASCII letters / digits are skipped four class bytes per LDS read.
+// *at_end = the scan reached byte n while a longer match was still possible
+// (a window that ends there, not the document: the token's extent is unknown)
 __device__ __forceinline__ bool uc_window_span(const uint8_t *cls, const uint8_t *tr, uint32_t n, uint32_t *pos,
                                                uint32_t stop, uint32_t *ts, uint32_t *te, bool *bad, bool *at_end) {
   while (*pos < stop) {
@@ -407,6 +127,298 @@ __device__ __forceinline__ bool uc_window_span(const uint8_t *cls, const uint8_t
   return false;
 }
 
+// Key of a token of n <= 8 bytes at (aligned) window byte a when they are all
+// ASCII: the lower-cased bytes, as KeyBuilder gives them (uc_token_key's
+// UTF-8 walk is for the rest).  false: a byte >= 0x80.
+__device__ __forceinline__ uint32_t uc_lower4(uint32_t t) {
+  const uint32_t up = (t + 0x3F3F3F3Fu) & ~(t + 0x25252525u) & 0x80808080u;   // 'A'..'Z' (ASCII bytes)
+  return t | (up >> 2);
+}
+__device__ __forceinline__ bool uc_short_ascii_key(const uint8_t *text, uint32_t a, uint32_t n, uint64_t *lo) {
+  const uint32_t *t32 = reinterpret_cast<const uint32_t *>(text);
+  const uint32_t w0 = t32[a >> 2], w1 = t32[(a >> 2) + 1], w2 = t32[(a >> 2) + 2], o = a & 3;
+  uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, o), x1 = __builtin_amdgcn_alignbyte(w2, w1, o);
+  x0 &= n >= 4 ? 0xFFFFFFFFu : (1u << (8 * n)) - 1u;
+  x1 &= n >= 8 ? 0xFFFFFFFFu : (n <= 4 ? 0u : (1u << (8 * (n - 4))) - 1u);
+  if ((x0 | x1) & 0x80808080u) return false;
+  *lo = (uint64_t)uc_lower4(x0) | ((uint64_t)uc_lower4(x1) << 32);
+  return true;
+}
+
+struct UwSmem {
+  alignas(16) uint8_t text[kUwWindow + 16];
+  alignas(16) uint8_t cls[kUwWindow + 16];
+  unsigned long long klo[kUwSlots];   // key lo; after the lookup: dictionary slot
+  unsigned long long khi[kUwSlots];   // key hi (VALID bit set: occupied)
+  uint32_t cnt[kUwSlots];             // tf
+  uint32_t kpos[kUwSlots];            // first occurrence: start | end << 16 (document bytes)
+  uint16_t occ[kUwSlots];             // occupied slots, compacted
+  uint32_t rcnt[kUwMaxRanges];        // per-range counts, then cursors
+  uint8_t tr[kUwStates * kUwClasses]; // WORD DFA transitions
+  uint8_t asc[128];                   // ASCII byte -> scanner class
+};
+
+__device__ __forceinline__ uint32_t uw_incl_add(uint32_t x, uint32_t lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+    if (lane >= (uint32_t)o) x += y;
+  }
+  return x;
+}
+
+// Documents flagged by k_tokenize_wave (uni_list[d] != 0: a flag per
+// document, no shared counter — a list appended with one atomic per document
+// serialised a corpus of non-ASCII documents on one address, ~4.7 ns each):
+// the wave reads 64 flags at a time, takes the flagged documents of each
+// group in turn and counts them into *uni_count.  Round 4: classes four
+// consecutive bytes per lane (no LDS bank conflicts), the ASCII-run skip and
+// the direct key of short ASCII tokens of the Unicode chunk kernel,
+// dictionary lookups and row writes over the compacted occupied slots only
+// (was: all 1 024 slots, two rounds), occupied slots reset after the document
+// instead of a full table clear.
+__global__ void __launch_bounds__(64) k_tokenize_uwave(BuildParams p) {
+  __shared__ UwSmem sm;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t R = p.n_ranges;
+  unsigned long long my_dc = 0, my_ttf = 0, my_nnz = 0;
+  uint32_t my_uni = 0;
+  bool ready = false;                                       // tables built (at the first flagged document)
+
+  for (uint64_t b0 = (uint64_t)blockIdx.x * 64; b0 < p.n_docs; b0 += (uint64_t)gridDim.x * 64) {
+    uint64_t fm = __ballot(b0 + lane < p.n_docs && p.uni_list[b0 + lane] != 0);
+    my_uni += (uint32_t)__popcll(fm);
+    while (fm) {
+    const uint32_t d = (uint32_t)(b0 + (uint64_t)__builtin_ctzll(fm));
+    fm &= fm - 1;
+    if (!ready) {                                           // wave-uniform
+      for (uint32_t e = lane; e < kUwStates * kUwClasses; e += 64)
+        sm.tr[e] = (uint8_t)uc_word_next(e / kUwClasses, e % kUwClasses);
+      for (uint32_t e = lane; e < 128; e += 64) sm.asc[e] = (uint8_t)uc_ascii_class(e);
+      for (uint32_t s = lane; s < kUwSlots; s += 64) { sm.klo[s] = 0; sm.khi[s] = 0; sm.cnt[s] = 0; }
+      __syncthreads();
+      ready = true;
+    }
+    const uint64_t src = p.live_map ? p.live_map[d] : d;
+    const uint64_t s0 = p.offsets[src];
+    const uint64_t L = p.offsets[src + 1] - s0;
+    if (L > kUwWindow || R > kUwMaxRanges) {                // wave-uniform
+      if (lane == 0) p.long_list[atomicAdd(p.long_count, 1u)] = d;
+      continue;
+    }
+    // ---- stage (aligned 16 B loads); the table is empty here
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p.text + s0);
+    const uint32_t shift = (uint32_t)(a & 15);
+    const uint32_t nchunks = (uint32_t)((shift + L + 15) >> 4);
+    const uint4 *gsrc = reinterpret_cast<const uint4 *>(a - shift);
+    uint4 *dst = reinterpret_cast<uint4 *>(sm.text);
+    for (uint32_t c = lane; c < nchunks; c += 64) dst[c] = gsrc[c];
+    sm.rcnt[lane] = 0;
+    __syncthreads();
+    const uint8_t *doc = sm.text + shift;
+    // ---- classes, four consecutive bytes per lane per step
+    for (uint32_t i0 = 4 * lane; i0 < L; i0 += 256) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int b = 0; b < 4; b++) w |= (i0 + b < L ? (uint32_t)doc[i0 + b] : 0x20u) << (8 * b);
+      uint32_t out = 0;
+      if ((w & 0x80808080u) == 0) {
+#pragma unroll
+        for (int b = 0; b < 4; b++) out |= (uint32_t)sm.asc[(w >> (8 * b)) & 0x7Fu] << (8 * b);
+      } else {
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const uint32_t x = (w >> (8 * b)) & 0xFFu;
+          uint32_t v;
+          if (x < 0x80u) v = sm.asc[x];
+          else if ((x & 0xC0u) == 0x80u || i0 + b >= L) v = 0xFFu;
+          else {
+            uint32_t l;
+            const uint32_t cp = utf8_decode(doc, L, i0 + b, &l);
+            v = cp == kUcBad ? 0xFFu : (uc_class(cp) | ((l - 1) << 5));
+          }
+          out |= v << (8 * b);
+        }
+      }
+      *reinterpret_cast<uint32_t *>(&sm.cls[i0]) = out;      // bytes past L: never taken
+    }
+    __syncthreads();
+
+    // ---- slices: lane l scans tokens starting in [cut(l), cut(l + 1))
+    const uint64_t seg = (L + 63) >> 6;
+    auto cut = [&](uint64_t t) -> uint64_t {
+      if (t == 0) return 0;
+      uint64_t q = t * seg;
+      if (q >= L) return L;
+      while (q < L && !uc_split_byte(doc[q - 1])) q++;
+      return q;
+    };
+    uint32_t pos = (uint32_t)cut(lane);
+    const uint32_t stop = (uint32_t)cut(lane + 1);
+    bool active = pos < stop, ubad = false, overflow = false, at_end = false;
+    uint32_t ntok = 0;
+    bool collide = false;
+    while (__any(active)) {
+      uint64_t lo = 0, hi = 0;
+      bool have = false;
+      uint32_t ts32 = 0, te32 = 0;
+      if (active) {
+        uint32_t p32 = pos;
+        have = uc_window_span(sm.cls, sm.tr, (uint32_t)L, &p32, stop, &ts32, &te32, &ubad, &at_end);
+        if (have) {
+          if (te32 - ts32 <= 8 && uc_short_ascii_key(sm.text, shift + ts32, te32 - ts32, &lo)) {
+            hi = kKeyValid;                                   // most tokens: <= 8 ASCII bytes
+          } else {
+            const uint64_t cutp = uc_token_key(doc, L, ts32, te32, &lo, &hi, p.hash_seed);
+            if (cutp < te32) { p32 = (uint32_t)cutp; te32 = (uint32_t)cutp; }   // 255-unit cut: rescan from the cut
+          }
+        }
+        pos = p32;
+        active = have;
+      }
+      ntok += have;
+      // round insert: probe from the key's home slot, linear
+      uint32_t slot = dict_hash(lo, hi) >> (32 - kUwSlotBits);
+      bool done = !have;
+      for (uint32_t r = 0; r < kUwSlots && __any(!done); r++) {
+        unsigned long long old = 1;
+        if (!done) old = atomicCAS(&sm.klo[slot], 0ull, (unsigned long long)lo);
+        const bool won = !done && old == 0;
+        if (won) { sm.khi[slot] = hi; sm.kpos[slot] = ts32 | (te32 << 16); }
+        asm volatile("" ::: "memory");
+        bool match = false;
+        if (!done && !won && old == lo) match = sm.khi[slot] == hi;
+        if (match && (lo & kLoHashed)) {                    // hashed key: the same term? (kErrCollision if not)
+          const uint32_t kp = sm.kpos[slot], ka = kp & 0xFFFFu, kz = kp >> 16;
+          collide |= !uc_same_term(doc + ka, kz - ka, doc + ts32, te32 - ts32);
+        }
+        if (won || match) {
+          atomicAdd(&sm.cnt[slot], 1u);
+          done = true;
+        } else if (!done) {
+          slot = (slot + 1) & (kUwSlots - 1);
+        }
+      }
+      overflow |= !done;
+    }
+    if (collide) set_build_err(p.err, kErrCollision, d);
+    // ---- occupied slots, compacted (lane l: slots [16 l, 16 l + 16))
+    uint32_t nu;
+    {
+      uint32_t om = 0;
+#pragma unroll
+      for (int k = 0; k < (int)(kUwSlots / 64); k++) om |= (uint32_t)(sm.khi[(kUwSlots / 64) * lane + k] != 0) << k;
+      const uint32_t c = (uint32_t)__popc(om);
+      const uint32_t incl = uw_incl_add(c, lane);
+      nu = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+      uint32_t at = incl - c;
+      while (om) {
+        sm.occ[at++] = (uint16_t)((kUwSlots / 64) * lane + (uint32_t)__builtin_ctz(om));
+        om &= om - 1;
+      }
+    }
+    __syncthreads();
+    if (__any(ubad) || __any(overflow) || nu > kUwMaxTerms) {   // wave-uniform: the long path
+      if (lane == 0) p.long_list[atomicAdd(p.long_count, 1u)] = d;
+      for (uint32_t i = lane; i < nu; i += 64) {
+        const uint32_t s = sm.occ[i];
+        sm.klo[s] = 0; sm.khi[s] = 0; sm.cnt[s] = 0;
+      }
+      __syncthreads();
+      continue;
+    }
+    const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)uw_incl_add(ntok, lane), 63);
+    // ---- dictionary slots of the occupied entries (8 lookups per lane in flight), range counts
+    for (uint32_t h = 0; h * 512 < nu; h++) {
+      uint64_t klo[8], khi[8], mine[8];
+      bool act[8], cl[8];
+      uint32_t g[8], sl[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const uint32_t i = lane + 64 * (8 * h + k);
+        act[k] = i < nu;
+        sl[k] = act[k] ? sm.occ[i] : 0u;
+        klo[k] = sm.klo[sl[k]];
+        khi[k] = sm.khi[sl[k]];
+        const uint32_t kp = sm.kpos[sl[k]];
+        mine[k] = dict_ref_word(s0 + (kp & 0xFFFFu), (kp >> 16) - (kp & 0xFFFFu));
+        if (!act[k]) { klo[k] = 1; khi[k] = kKeyValid; }
+      }
+      dict_lookup_multi<8>(p.dict, p.cap_mask, klo, khi, act, g, mine, cl);
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        if (!act[k]) continue;
+        if ((klo[k] & kLoHashed) && !cl[k] && g[k] != kInvalidSlot) dict_verify(p, g[k], mine[k], d);
+        uint32_t gs = g[k];
+        if (gs == kInvalidSlot) { atomicOr(p.err, kErrCapacity); gs = 0; }
+        sm.klo[sl[k]] = gs;
+        atomicAdd(&sm.rcnt[gs >> p.range_shift], 1u);
+      }
+    }
+    __syncthreads();
+    // ---- row segments: inclusive ends per range, cursors = exclusive starts
+    {
+      const uint32_t c = lane < R ? sm.rcnt[lane] : 0u;
+      const uint32_t incl = uw_incl_add(c, lane);
+      if (lane < R) {
+        p.rsplit[(uint64_t)d * R + lane] = incl;
+        sm.rcnt[lane] = incl - c;
+      }
+    }
+    __syncthreads();
+    const uint64_t base = csr_row_base(p.offsets, src);
+    for (uint32_t i = lane; i < nu; i += 64) {
+      const uint32_t s = sm.occ[i];
+      const uint32_t gs = (uint32_t)sm.klo[s];
+      const uint32_t at = atomicAdd(&sm.rcnt[gs >> p.range_shift], 1u);
+      csr_put(p, base + at, gs, sm.cnt[s], d);
+    }
+    __syncthreads();
+    for (uint32_t i = lane; i < nu; i += 64) {                // reset the occupied slots for the next document
+      const uint32_t s = sm.occ[i];
+      sm.klo[s] = 0; sm.khi[s] = 0; sm.cnt[s] = 0;
+    }
+    if (lane == 0) {
+      p.doc_len[d] = len;
+      p.doc_nuniq[d] = nu;
+      p.doc_norm[d] = (uint8_t)int_to_byte4(len);
+      my_dc += len > 0;
+      my_ttf += len;
+      my_nnz += nu;
+    }
+    __syncthreads();
+    }
+  }
+  if (lane == 0 && (my_ttf | my_nnz)) {
+    atomicAdd(&p.stats[0], my_dc);
+    atomicAdd(&p.stats[1], my_ttf);
+    atomicAdd(&p.stats[2], my_nnz);
+  }
+  if (lane == 0 && my_uni) atomicAdd(p.uni_count, my_uni);
+}
+
+hipError_t launch_tokenize_uwave(const BuildParams &p, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(k_tokenize_uwave, dim3(grid), dim3(64), 0, s, p);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Book-sized documents, units with non-ASCII text (round 4).  k_tokenize_chunk
+// lists a (document, 2 KB core) unit whose window holds a byte >= 0x80; this
+// kernel tokenizes that unit with the Unicode scanner instead of sending the
+// whole book to k_tokenize_long.  One wavefront per unit: the window (core +
+// context margins) is staged in LDS with per-byte classes; the scan starts at
+// a split point (the byte before it is ASCII class OTHER: the scanner's start
+// state holds there) at or before the core, lanes take slices between split
+// points, and only tokens STARTING in the core are counted (a token crossing
+// the core's start belongs to the unit before).  The unit's distinct terms are
+// resolved in the dictionary and stored as its bucketed (slot, tf) pair list,
+// exactly as k_tokenize_chunk stores an ASCII unit's, for k_long_rows.  A unit
+// this cannot take decides its document for the long path (chunk_fail): no
+// split point in the leading margin (e.g. unspaced CJK), a token that reaches
+// the window's end before the document's, a token over 255 UTF-16 units,
+// malformed UTF-8, > kPairWords distinct terms.
+
 // The unit's LDS: a window of at most kPreBytes + kCoreBytes + kPostBytes
 // bytes (+ 15 alignment) and a 512-slot term table (a 2 KB core holds at most
 // kPairWords distinct terms) — 19 KB, eight workgroups per CU (round 4's first
@@ -429,24 +441,6 @@ struct UcSmem {
 
 __device__ __forceinline__ void uc_clear_all(UcSmem &sm, uint32_t lane) {
   for (uint32_t s = lane; s < kUcSlots; s += 64) { sm.klo[s] = 0; sm.khi[s] = 0; sm.cnt[s] = 0; }
-}
-
-// Key of a token of n <= 8 bytes at (aligned) window byte a when they are all
-// ASCII: the lower-cased bytes, as KeyBuilder gives them (uc_token_key's
-// UTF-8 walk is for the rest).  false: a byte >= 0x80.
-__device__ __forceinline__ uint32_t uc_lower4(uint32_t t) {
-  const uint32_t up = (t + 0x3F3F3F3Fu) & ~(t + 0x25252525u) & 0x80808080u;   // 'A'..'Z' (ASCII bytes)
-  return t | (up >> 2);
-}
-__device__ __forceinline__ bool uc_short_ascii_key(const uint8_t *text, uint32_t a, uint32_t n, uint64_t *lo) {
-  const uint32_t *t32 = reinterpret_cast<const uint32_t *>(text);
-  const uint32_t w0 = t32[a >> 2], w1 = t32[(a >> 2) + 1], w2 = t32[(a >> 2) + 2], o = a & 3;
-  uint32_t x0 = __builtin_amdgcn_alignbyte(w1, w0, o), x1 = __builtin_amdgcn_alignbyte(w2, w1, o);
-  x0 &= n >= 4 ? 0xFFFFFFFFu : (1u << (8 * n)) - 1u;
-  x1 &= n >= 8 ? 0xFFFFFFFFu : (n <= 4 ? 0u : (1u << (8 * (n - 4))) - 1u);
-  if ((x0 | x1) & 0x80808080u) return false;
-  *lo = (uint64_t)uc_lower4(x0) | ((uint64_t)uc_lower4(x1) << 32);
-  return true;
 }
 
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_tokenize_uchunk(BuildParams p) {

@@ -792,6 +792,7 @@ static int commit_once(tfidf_index *ix) {
   uint64_t *ctr = ix->counters.as<uint64_t>();
   HIP_TRY(hipMemsetAsync(ix->counters.p, 0, 128, s));
   HIP_TRY(hipMemsetAsync(ix->dict.p, 0, (size_t)3 * C * 8, s));
+  HIP_TRY(hipMemsetAsync(ix->uni_list.p, 0, (size_t)N * 4, s));          // per-document Unicode flags
 
   BuildParams bp{};
   bp.text = ix->text.as<uint8_t>();

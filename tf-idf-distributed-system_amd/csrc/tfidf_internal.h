@@ -45,8 +45,8 @@ struct BuildParams {
   uint32_t *rsplit;           // [n_docs][R] inclusive end of each range segment in the row
   uint32_t *long_list;        // docs deferred to the long path
   uint32_t *long_count;
-  uint32_t *uni_list;         // docs the ASCII wave path found non-ASCII bytes in (Unicode wave path)
-  uint32_t *uni_count;
+  uint32_t *uni_list;         // per document: 1 = the ASCII wave path found non-ASCII bytes (Unicode wave path)
+  uint32_t *uni_count;        // flagged documents
   uint32_t *bad_list;         // docs that are not valid UTF-8 (indexed empty; tfidf_malformed_docs)
   uint32_t *bad_count;
   unsigned long long *stats;  // [0] docCount, [1] sumTotalTermFreq, [2] nnz
