@@ -4,7 +4,8 @@
 # the docs cite: default (cfg 2, with queries, end-to-end and the CPU
 # baseline; roofline.traffic from this run's PMC pass), cfg-5 shape, 300-book
 # shape, books with one non-ASCII word per ~2 KB (chunk path, and with the
-# Unicode chunk path disabled), the cfg-5 PMC summary, and the one-rank RCCL
+# Unicode chunk path disabled), cfg 2 with 10 % / all documents non-ASCII,
+# the cfg-5 PMC summary, and the one-rank RCCL
 # rehearsal of the node path.  Output: gpurun_out/ev_$TAG/.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R
@@ -23,6 +24,8 @@ run bench_line_cfg5_shape 300 --steps 5 --warmup 2 --docs 6250000 --len-min 48 -
 run bench_line_book_shape 200 --steps 10 --warmup 2 --docs 300 --len-min 80000 --len-max 120000 --no-queries --no-e2e --cpu-sample 0
 run bench_line_book_unicode 200 --steps 10 --warmup 2 --docs 300 --len-min 80000 --len-max 120000 --unicode-every 2048 --no-queries --no-e2e --cpu-sample 0
 TFIDF_NO_UCHUNK=1 run bench_line_book_unicode_whole_book 200 --steps 10 --warmup 2 --docs 300 --len-min 80000 --len-max 120000 --unicode-every 2048 --no-queries --no-e2e --cpu-sample 0
+run bench_line_cfg2_unicode10 200 --steps 5 --warmup 2 --unicode-frac 0.1 --no-queries --no-e2e --cpu-sample 0
+run bench_line_cfg2_unicode100 300 --steps 3 --warmup 1 --unicode-frac 1.0 --no-queries --no-e2e --cpu-sample 0
 # cfg-5 PMC: one build, FETCH / WRITE passes, kernel summary
 P=$R/gpurun_out/prof_cfg5_$TAG; mkdir -p $P
 cd /tmp && export TMPDIR=/tmp
