@@ -27,9 +27,9 @@
 namespace tfidf {
 
 constexpr uint32_t kUwWindow = 4096;
-constexpr uint32_t kUwSlots = 1024;
-constexpr uint32_t kUwSlotBits = 10;
-constexpr uint32_t kUwMaxTerms = 768;
+constexpr uint32_t kUwSlots = 512;
+constexpr uint32_t kUwSlotBits = 9;
+constexpr uint32_t kUwMaxTerms = 512;
 constexpr uint32_t kUwMaxRanges = 64;
 
 // Scanner class source over classes precomputed in LDS: per byte, the class
@@ -177,7 +177,7 @@ __device__ __forceinline__ uint32_t uw_incl_add(uint32_t x, uint32_t lane) {
 // dictionary lookups and row writes over the compacted occupied slots only
 // (was: all 1 024 slots, two rounds), occupied slots reset after the document
 // instead of a full table clear.
-__global__ void __launch_bounds__(64) k_tokenize_uwave(BuildParams p) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_tokenize_uwave(BuildParams p) {
   __shared__ UwSmem sm;
   const uint32_t lane = threadIdx.x;
   const uint32_t R = p.n_ranges;
@@ -328,14 +328,15 @@ __global__ void __launch_bounds__(64) k_tokenize_uwave(BuildParams p) {
       continue;
     }
     const uint32_t len = (uint32_t)__builtin_amdgcn_readlane((int)uw_incl_add(ntok, lane), 63);
-    // ---- dictionary slots of the occupied entries (8 lookups per lane in flight), range counts
-    for (uint32_t h = 0; h * 512 < nu; h++) {
-      uint64_t klo[8], khi[8], mine[8];
-      bool act[8], cl[8];
-      uint32_t g[8], sl[8];
+    // ---- dictionary slots of the occupied entries (4 lookups per lane in flight: two
+    // waves per SIMD), range counts
+    for (uint32_t h = 0; h * 256 < nu; h++) {
+      uint64_t klo[4], khi[4], mine[4];
+      bool act[4], cl[4];
+      uint32_t g[4], sl[4];
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
-        const uint32_t i = lane + 64 * (8 * h + k);
+      for (int k = 0; k < 4; k++) {
+        const uint32_t i = lane + 64 * (4 * h + k);
         act[k] = i < nu;
         sl[k] = act[k] ? sm.occ[i] : 0u;
         klo[k] = sm.klo[sl[k]];
@@ -344,9 +345,9 @@ __global__ void __launch_bounds__(64) k_tokenize_uwave(BuildParams p) {
         mine[k] = dict_ref_word(s0 + (kp & 0xFFFFu), (kp >> 16) - (kp & 0xFFFFu));
         if (!act[k]) { klo[k] = 1; khi[k] = kKeyValid; }
       }
-      dict_lookup_multi<8>(p.dict, p.cap_mask, klo, khi, act, g, mine, cl);
+      dict_lookup_multi<4>(p.dict, p.cap_mask, klo, khi, act, g, mine, cl);
 #pragma unroll
-      for (int k = 0; k < 8; k++) {
+      for (int k = 0; k < 4; k++) {
         if (!act[k]) continue;
         if ((klo[k] & kLoHashed) && !cl[k] && g[k] != kInvalidSlot) dict_verify(p, g[k], mine[k], d);
         uint32_t gs = g[k];

@@ -259,7 +259,7 @@ hipError_t launch_tokenize_chunks(const BuildParams &p, int grid, hipStream_t s)
 hipError_t launch_long_rows(const BuildParams &p, uint32_t n_docs, hipStream_t s);
 hipError_t launch_tokenize_uwave(const BuildParams &p, int grid, hipStream_t s);   // kernels_unicode.hip
 hipError_t launch_tokenize_uchunk(const BuildParams &p, int grid, hipStream_t s);  // kernels_unicode.hip
-constexpr uint32_t kUwaveWGsPerCU = 4;    // 64-thread workgroups, ~33 KB LDS each
+constexpr uint32_t kUwaveWGsPerCU = 7;    // 64-thread workgroups, ~22 KB LDS each (two waves per SIMD)
 constexpr uint32_t kUchunkWGsPerCU = 8;   // k_tokenize_uchunk: ~19 KB LDS each
 hipError_t launch_verify_deferred(const BuildParams &p, hipStream_t s);           // kernels_index.hip
 hipError_t launch_df_partial(const PostingParams &p, hipStream_t s);
