@@ -3,7 +3,9 @@ takes units from the eighth b mod 8 of the corpus, kernels_index.hip
 k_tokenize_wave) against the CPU oracle: corpora with at least as many units
 as the persistent grid has workgroups, so the mapping is the one that runs
 (the small parity corpora take the plain grid stride).  Single documents per
-window (cfg-2 shape) and packed short documents (cfg-5 shape)."""
+window (cfg-2 shape), packed short documents (cfg-5 shape), and the cfg-2
+shape with every third document non-ASCII (flagged per document for the
+Unicode document wave, which reads the flags 64 at a time across the grid)."""
 import random
 
 import pytest
@@ -15,10 +17,24 @@ from tfidf_amd.engine import ShardIndex
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("shape", ["single", "packed"])
+def _non_ascii_every_third(texts):
+    """Every third document: the first two letters of its first word become
+    U+00E9 / U+00C9 (same byte length), alternating, so both the lower-cased
+    and the upper-case form reach the Unicode path."""
+    out = []
+    for i, t in enumerate(texts):
+        if i % 3 == 0 and len(t) >= 2 and t[:2].isalpha():
+            t = (b"\xc3\xa9" if i % 2 else b"\xc3\x89") + t[2:]
+        out.append(t)
+    return out
+
+
+@pytest.mark.parametrize("shape", ["single", "packed", "unicode"])
 def test_xcd_contiguous_units_match_oracle(shape):
     if shape == "single":
         texts = synth.corpus(20000, V=50000, len_min=300, len_max=500)
+    elif shape == "unicode":
+        texts = _non_ascii_every_third(synth.corpus(20000, V=50000, len_min=300, len_max=500))
     else:
         texts = synth.corpus(25000, V=60000, len_min=30, len_max=70)
     g = ShardIndex(vocab_capacity_log2=18)
@@ -32,6 +48,8 @@ def test_xcd_contiguous_units_match_oracle(shape):
         s = g.stats()
         if shape == "packed":
             assert s["pack_docs"] > 1
+        if shape == "unicode":
+            assert s["unicode_docs"] == sum(1 for t in texts if max(t) >= 0x80)
         assert (s["doc_count"], s["sum_ttf"], s["num_terms"]) == (o.doc_count, o.sum_ttf, o.num_terms)
         rng = random.Random(11)
         n = len(texts)
