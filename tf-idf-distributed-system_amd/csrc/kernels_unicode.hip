@@ -3,20 +3,24 @@
 // Unicode grammar; unicode_scan.h), hand-written for gfx950.
 //
 //   tokenize_uwave : one wavefront per document (aligned window <= 4 KB), the
-//                    documents the ASCII wave path found a byte >= 0x80 in.
-//                    The document is staged in LDS; lane l scans the slice
-//                    [cut_l, cut_{l+1}) with the longest-match DFA, cuts just
-//                    after ASCII class-OTHER bytes (the scanner's start state
-//                    holds there); every round each lane yields at most one
-//                    token, keyed (lower-cased UTF-8 -> 128-bit key), and the
-//                    wave inserts the round's keys into a 1024-slot LDS table
-//                    (64-bit CAS on lo, then hi; in-order LDS within the wave
-//                    makes the winner's hi visible to the losers of the same
-//                    round).  Distinct terms are resolved in the global
-//                    dictionary (8 lookups per lane in flight) and written as
-//                    a CSR row grouped by dictionary range, as the other
-//                    tokenizer paths do.  Documents that do not fit (window,
-//                    > 768 distinct terms, malformed UTF-8) go to the long path.
+//                    documents the ASCII wave path flagged (a byte >= 0x80).
+//                    The document is staged in LDS with per-byte classes;
+//                    lane l scans the slice [cut_l, cut_{l+1}) with the
+//                    longest-match DFA, cuts just after ASCII class-OTHER
+//                    bytes (the scanner's start state holds there); every
+//                    round each lane yields at most one token, keyed
+//                    (lower-cased UTF-8 -> 128-bit key; <= 8 ASCII bytes
+//                    directly), and the wave inserts the round's keys into a
+//                    512-slot LDS table (64-bit CAS on lo, then hi; in-order
+//                    LDS within the wave makes the winner's hi visible to the
+//                    losers of the same round).  The occupied slots are
+//                    compacted, resolved in the global dictionary (4 lookups
+//                    per lane in flight) and written as a CSR row grouped by
+//                    dictionary range, as the other tokenizer paths do.
+//                    Documents that do not fit (window, > 512 distinct terms,
+//                    malformed UTF-8) go to the long path.
+//   tokenize_uchunk: the same scanner over the (document, 2 KB core) units of
+//                    book-sized documents whose window holds non-ASCII text.
 #include <hip/hip_runtime.h>
 
 #include "dict_device.h"
