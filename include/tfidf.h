@@ -385,8 +385,19 @@ int tfidf_comm_selftest(tfidf_comm *c);
 
 /* ---- process model (2): per-rank calls, collective over the communicator ----
  * Every rank calls each of them, in the same order, after its own
- * tfidf_commit; a rank whose index is not committed still takes part, and then
- * every rank returns TFIDF_E_STATE together.  A query that does not parse
+ * tfidf_commit; a rank that cannot serve still takes part.  Its status rides in
+ * the first collective of the call (a header ahead of its top-k keys, or the
+ * count row of a variable-length gather), so no rank is left waiting:
+ *   commits and GLOBAL searches: every rank returns the failing rank's error
+ *     together (TFIDF_E_STATE for an index not committed, or re-committed since
+ *     the last tfidf_dist_global_commit; TFIDF_E_INVALID_ARG when two ranks'
+ *     [doc_base, doc_base + num_docs) ranges overlap: merge keys would collide);
+ *   SHARD searches: the other ranks' hits are merged without the failing rank
+ *     (Leader.start skips a failed worker, Leader.java:67-69): TFIDF_OK, the
+ *     skipped ranks in tfidf_dist_last_failed and a tfidf_last_error() message
+ *     naming them; only when no rank can serve is the error returned.  A rank
+ *     whose index was re-committed after tfidf_dist_shard_commit is skipped.
+ * A query that does not parse
  * (TFIDF_E_QUERY_SYNTAX / _UNSUPPORTED_QUERY) fails on every rank alike before
  * any collective (the reference's Worker answers [] and its Leader merges
  * nothing, Worker.java:182-185).
@@ -416,6 +427,8 @@ int tfidf_dist_shard_search(tfidf_index *ix, tfidf_comm *c, const uint8_t *q, ui
                             uint64_t *n_bytes);
 /* Results of the communicator's last search (local copies, no collective). */
 int tfidf_dist_last_hits(const tfidf_comm *c, uint64_t *doc_ids, float *scores, uint64_t cap, uint64_t *n_out);
+/* Ranks skipped by the last SHARD search (bit r = rank r; 0 = every rank answered). */
+int tfidf_dist_last_failed(const tfidf_comm *c, uint64_t *rank_mask);
 /* names concatenated into buf (cap bytes), offsets[n + 1], scores[n] (double sums) */
 int tfidf_dist_last_names(const tfidf_comm *c, uint8_t *buf, uint64_t cap, uint64_t *offsets, double *scores,
                           uint64_t n_cap, uint64_t *n_out, uint64_t *n_bytes);
@@ -430,7 +443,10 @@ int tfidf_node_create(const tfidf_config *cfg, uint64_t device_mask, tfidf_node 
 int tfidf_node_create_devices(const tfidf_config *cfg, const int32_t *devices, uint32_t n_devices, uint32_t flags,
                               tfidf_node **out);
 int tfidf_node_destroy(tfidf_node *n);
-/* shard i's index (owned by the node): per-shard calls such as tfidf_add_docs_device */
+/* shard i's index (owned by the node): per-shard calls such as tfidf_add_docs_device.
+ * A shard changed or committed through this handle needs tfidf_node_commit
+ * again: until then GLOBAL searches fail (TFIDF_E_STATE) and SHARD searches
+ * skip that shard. */
 int tfidf_node_shard(tfidf_node *n, uint32_t i, tfidf_index **ix, uint32_t *n_shards);
 /* Documents go to one shard (shard >= 0: the caller routes, as Leader.upload
  * picks a worker, Leader.java:153-207) or are split contiguously over the shards
@@ -444,9 +460,14 @@ int tfidf_node_search(tfidf_node *n, const uint8_t *q, uint64_t q_len, uint32_t 
                       uint64_t cap, uint64_t *n_out);
 int tfidf_node_search_batch(tfidf_node *n, const uint8_t *q_utf8, const uint64_t *q_offsets, uint32_t n_q, uint32_t k,
                             uint64_t *doc_ids, float *scores, uint32_t *counts);
-/* SHARD mode (Leader.start): name-ordered {name: double} of the merged hits. */
+/* SHARD mode (Leader.start): name-ordered {name: double} of the merged hits.
+ * A shard that cannot serve is skipped (Leader.java:67-69): TFIDF_OK with the
+ * other shards' merged hits, tfidf_node_last_failed names the skipped shards
+ * and tfidf_last_error() their reasons. */
 int tfidf_node_search_names(tfidf_node *n, const uint8_t *q, uint64_t q_len, uint8_t *buf, uint64_t cap,
                             uint64_t *offsets, double *scores, uint64_t n_cap, uint64_t *n_out, uint64_t *n_bytes);
+/* Shards skipped by the last tfidf_node_search_names (bit g = shard g). */
+int tfidf_node_last_failed(const tfidf_node *n, uint64_t *shard_mask);
 /* Global doc id -> its document key (Worker.java:235-236, across shards). */
 int tfidf_node_doc_key(tfidf_node *n, uint64_t doc, uint8_t *buf, uint64_t cap, uint64_t *n_out);
 typedef struct tfidf_node_stats {

@@ -106,10 +106,14 @@ def expected():
     return out
 
 
-def expected_shard(world):
+def expected_shard(world, skip=()):
+    """Per-worker oracles + the Leader merge; ranks in `skip` are failed
+    workers whose responses the Leader never sees (Leader.java:67-69)."""
     texts, names = corpus()
     workers = []
     for r in range(world):
+        if r in skip:
+            continue
         lo, hi = D.shard_range(N_DOCS, r, world)
         o = O.OracleIndex()
         for n, t in zip(names[lo:hi], texts[lo:hi]):

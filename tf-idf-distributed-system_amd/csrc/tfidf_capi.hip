@@ -164,6 +164,7 @@ struct tfidf_index {
 
   // committed
   bool committed = false;
+  uint64_t generation = 0;         // successful commits so far (node level: stale name tables / GLOBAL df)
   uint64_t n_docs = 0;
   std::vector<uint32_t> live_map;  // committed -> staged (empty = identity)
   DevBuf d_live_map;
@@ -1190,6 +1191,7 @@ static int commit_once(tfidf_index *ix) {
   ix->has_global = false;
   ix->gdf.clear();
   ix->committed = true;
+  ix->generation++;
   return upload_cache(ix);
 }
 
@@ -2616,4 +2618,5 @@ hipStream_t tfidf::index_stream(tfidf_index *ix) { return ix->stream; }
 int tfidf::index_device(const tfidf_index *ix) { return ix->cfg.device; }
 bool tfidf::index_committed(const tfidf_index *ix) { return ix->committed; }
 uint64_t tfidf::index_num_docs(const tfidf_index *ix) { return ix->committed ? ix->n_docs : 0; }
+uint64_t tfidf::index_generation(const tfidf_index *ix) { return ix->generation; }
 int tfidf::set_error(int code, const char *msg) { return fail(code, "%s", msg); }

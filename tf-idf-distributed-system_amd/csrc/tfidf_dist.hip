@@ -73,13 +73,15 @@ struct DevGuard {
   }
 };
 
-struct DBuf {                      // device scratch, grown on demand (device of the first reserve)
+struct DBuf {                      // device scratch, grown on demand, on the current device
   void *p = nullptr;
   size_t bytes = 0;
   int dev = -1;
   hipError_t reserve(size_t n) {
-    if (n <= bytes && p) return hipSuccess;
-    if (p) { hipFree(p); p = nullptr; bytes = 0; }
+    int cur = -1;
+    hipGetDevice(&cur);
+    if (n <= bytes && p && cur == dev) return hipSuccess;
+    release();                     // too small, or allocated on another device
     n = std::max<size_t>(n, 64);
     hipError_t e = hipMalloc(&p, n);
     if (e == hipSuccess) { bytes = n; hipGetDevice(&dev); }
@@ -294,6 +296,7 @@ struct InprocTransport : Transport {
 
 struct tfidf_comm {
   int rank = 0, world = 1;
+  int device = -1;                  // the communicator's GPU (RCCL), -1: the caller's current device
   std::unique_ptr<Transport> t;
   // staging between the transport's memory and the other kind
   DBuf d_stage_in, d_stage_out;
@@ -306,8 +309,12 @@ struct tfidf_comm {
   std::string names;
   std::vector<uint64_t> name_off{0};
   DBuf d_name_of_doc;
-  uint64_t names_docs = 0;          // local documents the table was built for
+  uint64_t names_gen = ~0ull;       // index commit generation the name table was built for
   bool names_ready = false;
+  uint64_t global_gen = ~0ull;      // index commit generation of the last GLOBAL exchange
+  uint64_t last_failed = 0;         // SHARD search: ranks skipped by the last search (bit r)
+  HBuf h_hdr;                       // status words ahead of a rank's keys (pinned)
+  bool hdr_pending = false;         // an upload out of h_hdr may still be queued (a search that failed)
   // last search results (tfidf_dist_last_hits / _last_names)
   std::vector<uint64_t> last_doc;
   std::vector<float> last_score;
@@ -532,6 +539,7 @@ extern "C" int tfidf_comm_init_rccl(const uint8_t id[128], int32_t rank, int32_t
   tfidf_comm *c = new tfidf_comm();
   c->rank = rank;
   c->world = world;
+  c->device = device;
   c->t.reset(new RcclTransport(comm, world));
   *out = c;
   return TFIDF_OK;
@@ -566,7 +574,10 @@ extern "C" int tfidf_comm_info(const tfidf_comm *c, int32_t *rank, int32_t *worl
 extern "C" int tfidf_comm_selftest(tfidf_comm *c) {
   if (!c) return errf(TFIDF_E_INVALID_ARG, "NULL communicator");
   const int ws = c->world, me = c->rank;
-  hipStream_t s = nullptr;
+  int cur = 0;
+  hipGetDevice(&cur);
+  DevGuard g(c->device >= 0 ? c->device : cur);      // staging buffers on the communicator's GPU
+  hipStream_t s = nullptr;                            // (the null stream of that device)
   // all-gather of (rank, world) rows
   std::vector<uint64_t> rows;
   if (int rc = gather_rows(c, s, {(uint64_t)me, (uint64_t)ws, 0xC0FFEEull}, &rows)) return rc;
@@ -679,6 +690,7 @@ extern "C" int tfidf_dist_global_commit(tfidf_index *ix, tfidf_comm *c, uint64_t
   DHIP(c->d_back.reserve(std::max<uint64_t>(n_rec, 1) * 4));
   if (int rc = coll_a2av(c, s, c->d_ans.p, sb2.data(), so2.data(), c->d_back.p, rb2.data(), ro2.data(), true)) return rc;
   if (int rc = tfidf_set_global_df_device(ix, c->d_back.p, n_rec, gdc, gttf)) return rc;
+  c->global_gen = index_generation(ix);
   if (n_vocab) {
     uint64_t nu = 0;
     DHIP(hipMemcpyAsync(&nu, c->d_nu.p, 8, hipMemcpyDeviceToHost, s));
@@ -696,9 +708,58 @@ extern "C" int tfidf_dist_global_commit(tfidf_index *ix, tfidf_comm *c, uint64_t
 
 namespace {
 
-int check_doc_range(tfidf_index *ix, uint64_t doc_base) {
+// ---- search-time agreement (round-4 advisor finding).  Every rank's local
+// status travels in the first collective of a search — as a header ahead of
+// its top-k keys, or in the count row of a variable-length gather — so a rank
+// that cannot serve (index not committed, re-committed since the last GLOBAL
+// exchange or name table, doc range past 2^32, a failed local search) never
+// leaves the others waiting in the data collective: GLOBAL searches then fail
+// on every rank together; SHARD searches merge the healthy ranks' hits
+// (Leader.start skips a failed worker, Leader.java:67-69).  The header also
+// carries (doc_base, n_docs): GLOBAL merge keys must not collide, so
+// overlapping doc ranges fail on every rank (TFIDF_E_INVALID_ARG).
+constexpr uint64_t kHdr = 4;        // status words per rank: {rc, doc_base, n_docs, 0}
+
+int local_search_status(tfidf_index *ix, tfidf_comm *c, uint64_t doc_base, bool global) {
+  if (!index_committed(ix)) return errf(TFIDF_E_STATE, "index not committed");
   if (doc_base + index_num_docs(ix) > (1ull << 32))
     return errf(TFIDF_E_CAPACITY, "global doc ids must stay below 2^32 (merge keys carry 32-bit ids)");
+  if (global && c->global_gen != index_generation(ix))
+    return errf(TFIDF_E_STATE, "tfidf_dist_global_commit first (after every commit)");
+  if (!global && (!c->names_ready || c->names_gen != index_generation(ix)))
+    return errf(TFIDF_E_STATE, "tfidf_dist_shard_commit first (after every commit)");
+  return TFIDF_OK;
+}
+
+// Verdict over every rank's status words (rows of `stride` u64: rc, base, n):
+// the first failing rank's error (its own message on that rank); GLOBAL mode
+// also checks that the doc ranges do not overlap.  *failed = mask of failing ranks.
+int status_verdict(tfidf_comm *c, const uint64_t *rows, size_t stride, int lrc, const std::string &lmsg,
+                   bool fail_together, uint64_t *failed) {
+  const int ws = c->world;
+  uint64_t mask = 0;
+  int first = -1;
+  for (int r = 0; r < ws; r++)
+    if (rows[(size_t)r * stride]) {
+      if (r < 64) mask |= 1ull << r;
+      if (first < 0) first = r;
+    }
+  if (failed) *failed = mask;
+  if (first >= 0 && fail_together) {
+    if (first == c->rank) return set_error(lrc, lmsg.c_str());
+    return errf((int)rows[(size_t)first * stride], "rank %d cannot serve the search", first);
+  }
+  if (fail_together) {
+    std::vector<std::pair<uint64_t, uint64_t>> rg;
+    for (int r = 0; r < ws; r++)
+      if (rows[(size_t)r * stride + 2]) rg.emplace_back(rows[(size_t)r * stride + 1], rows[(size_t)r * stride + 2]);
+    std::sort(rg.begin(), rg.end());
+    for (size_t i = 1; i < rg.size(); i++)
+      if (rg[i - 1].first + rg[i - 1].second > rg[i].first)
+        return errf(TFIDF_E_INVALID_ARG, "shard doc ranges overlap ([%llu, +%llu) and [%llu, +%llu))",
+                    (unsigned long long)rg[i - 1].first, (unsigned long long)rg[i - 1].second,
+                    (unsigned long long)rg[i].first, (unsigned long long)rg[i].second);
+  }
   return TFIDF_OK;
 }
 
@@ -720,12 +781,20 @@ int all_keys(tfidf_index *ix, tfidf_comm *c, const uint8_t *q, uint64_t q_len, u
 }
 
 // gather variable-length device rows (d_keys[0, h)) from every rank, padded to
-// the longest with `pad` -> d_all [world][maxn]; ns = every rank's count
-int gather_var(tfidf_comm *c, hipStream_t s, uint64_t h, uint64_t pad_byte, std::vector<uint64_t> *ns,
-               uint64_t *maxn) {
-  if (int rc = gather_rows(c, s, {h}, ns)) return rc;
+// the longest with `pad` -> d_all [world][maxn]; ns = every rank's count.  The
+// count row carries the rank's status first (a failing rank sends h = 0).
+int gather_var(tfidf_comm *c, hipStream_t s, uint64_t h, uint64_t pad_byte, int lrc, const std::string &lmsg,
+               uint64_t doc_base, uint64_t n_docs, bool fail_together, std::vector<uint64_t> *ns, uint64_t *maxn) {
+  if (lrc) h = 0;
+  std::vector<uint64_t> rows;
+  if (int rc = gather_rows(c, s, {(uint64_t)lrc, doc_base, n_docs, h}, &rows)) return rc;
+  if (int rc = status_verdict(c, rows.data(), 4, lrc, lmsg, fail_together, &c->last_failed)) return rc;
+  ns->assign(c->world, 0);
   uint64_t mx = 0;
-  for (uint64_t x : *ns) mx = std::max(mx, x);
+  for (int r = 0; r < c->world; r++) {
+    (*ns)[r] = rows[(size_t)r * 4 + 3];
+    mx = std::max(mx, (*ns)[r]);
+  }
   *maxn = mx;
   if (mx == 0) return TFIDF_OK;
   DHIP(c->d_out.reserve(mx * 8));
@@ -733,6 +802,42 @@ int gather_var(tfidf_comm *c, hipStream_t s, uint64_t h, uint64_t pad_byte, std:
   if (mx > h) DHIP(hipMemsetAsync(c->d_out.as<uint64_t>() + h, (int)pad_byte, (mx - h) * 8, s));
   DHIP(c->d_all.reserve((size_t)c->world * mx * 8));
   return coll_gather(c, s, c->d_out.p, c->d_all.p, mx * 8, true);
+}
+
+// Top-k keys of this rank's n_q queries with the status header ahead of them
+// (row = kHdr + n_q k words), all-gathered, merged per query on the device into
+// d_out [n_q][k]; the merged keys and every rank's header are read back into
+// h_out ([n_q k] keys, then [world][kHdr]).  A failing rank sends zero keys.
+int gather_topk(tfidf_index *ix, tfidf_comm *c, hipStream_t s, uint64_t doc_base, const uint8_t *q_utf8,
+                const uint64_t *q_offsets, uint32_t n_q, uint32_t k) {
+  const int ws = c->world;
+  const uint64_t per = (uint64_t)n_q * k, row = kHdr + per;
+  DHIP(c->d_keys.reserve(row * 8));                    // only an allocation failure returns before the exchange
+  DHIP(c->d_all.reserve((size_t)ws * row * 8));
+  DHIP(c->d_out.reserve(per * 8));
+  DHIP(c->h_out.reserve((per + (size_t)ws * kHdr) * 8));
+  DHIP(c->h_hdr.reserve(kHdr * 8));
+  uint64_t *dk = c->d_keys.as<uint64_t>();
+  int lrc = local_search_status(ix, c, doc_base, true);
+  if (!lrc) lrc = tfidf_search_batch_keys_device(ix, q_utf8, q_offsets, n_q, k, doc_base, dk + kHdr);
+  const std::string lmsg = lrc ? tfidf_last_error() : "";
+  if (lrc) DHIP(hipMemsetAsync(dk + kHdr, 0, per * 8, s));
+  uint64_t *hh = c->h_hdr.as<uint64_t>();
+  if (c->hdr_pending) DHIP(hipStreamSynchronize(s));   // a failed search's header upload has left
+  c->hdr_pending = true;
+  hh[0] = (uint64_t)lrc;
+  hh[1] = doc_base;
+  hh[2] = lrc ? 0 : index_num_docs(ix);
+  hh[3] = 0;
+  DHIP(hipMemcpyAsync(dk, hh, kHdr * 8, hipMemcpyHostToDevice, s));
+  if (int rc = coll_gather(c, s, dk, c->d_all.p, row * 8, true)) return rc;
+  DHIP(launch_merge_lists(c->d_all.as<uint64_t>() + kHdr, (uint32_t)ws, row, k, k, n_q, c->d_out.as<uint64_t>(), k, s));
+  uint64_t *ho = c->h_out.as<uint64_t>();
+  DHIP(hipMemcpyAsync(ho, c->d_out.p, per * 8, hipMemcpyDeviceToHost, s));
+  DHIP(hipMemcpy2DAsync(ho + per, kHdr * 8, c->d_all.p, row * 8, kHdr * 8, ws, hipMemcpyDeviceToHost, s));
+  DHIP(hipStreamSynchronize(s));
+  c->hdr_pending = false;
+  return status_verdict(c, ho + per, kHdr, lrc, lmsg, true, nullptr);
 }
 
 }  // namespace
@@ -746,29 +851,23 @@ extern "C" int tfidf_dist_search(tfidf_index *ix, tfidf_comm *c, uint64_t doc_ba
   c->last_doc.clear();
   c->last_score.clear();
   if (int rc = query_status(q, q_len)) return rc;
-  if (int rc = check_doc_range(ix, doc_base)) return rc;
   DevGuard g(index_device(ix));
   hipStream_t s = index_stream(ix);
   const int ws = c->world;
   uint64_t n = 0;
   if (k > 0) {
-    DHIP(c->d_keys.reserve((size_t)k * 8));
     const uint64_t offs[2] = {0, q_len};
-    if (int rc = tfidf_search_batch_keys_device(ix, q, offs, 1, k, doc_base, c->d_keys.p)) return rc;
-    DHIP(c->d_all.reserve((size_t)ws * k * 8));
-    if (int rc = coll_gather(c, s, c->d_keys.p, c->d_all.p, (uint64_t)k * 8, true)) return rc;
-    DHIP(c->d_out.reserve((size_t)k * 8));
-    DHIP(launch_merge_lists(c->d_all.as<uint64_t>(), (uint32_t)ws, k, 0, k, 1, c->d_out.as<uint64_t>(), k, s));
-    DHIP(c->h_out.reserve((size_t)k * 8));
-    DHIP(hipMemcpyAsync(c->h_out.p, c->d_out.p, (size_t)k * 8, hipMemcpyDeviceToHost, s));
-    DHIP(hipStreamSynchronize(s));
+    if (int rc = gather_topk(ix, c, s, doc_base, q, offs, 1, k)) return rc;
     const uint64_t *keys = c->h_out.as<uint64_t>();
     while (n < k && keys[n]) n++;
   } else {
     uint64_t h = 0, maxn = 0;
-    if (int rc = all_keys(ix, c, q, q_len, doc_base, &h)) return rc;
+    int lrc = local_search_status(ix, c, doc_base, true);
+    if (!lrc) lrc = all_keys(ix, c, q, q_len, doc_base, &h);
+    const std::string lmsg = lrc ? tfidf_last_error() : "";
     std::vector<uint64_t> ns;
-    if (int rc = gather_var(c, s, h, 0, &ns, &maxn)) return rc;
+    if (int rc = gather_var(c, s, h, 0, lrc, lmsg, doc_base, lrc ? 0 : index_num_docs(ix), true, &ns, &maxn))
+      return rc;
     for (uint64_t x : ns) n += x;
     if (n) {
       DHIP(c->d_tmp.reserve(n * 8));
@@ -791,20 +890,9 @@ extern "C" int tfidf_dist_search_batch(tfidf_index *ix, tfidf_comm *c, uint64_t 
   if (!q_offsets || (n_q && (!doc_ids || !scores || !counts))) return errf(TFIDF_E_INVALID_ARG, "NULL argument");
   if (k == 0 || k > 1024) return errf(TFIDF_E_INVALID_ARG, "1 <= k <= 1024");
   if (n_q == 0) return TFIDF_OK;
-  if (int rc = check_doc_range(ix, doc_base)) return rc;
   DevGuard g(index_device(ix));
   hipStream_t s = index_stream(ix);
-  const int ws = c->world;
-  const uint64_t per = (uint64_t)n_q * k;
-  DHIP(c->d_keys.reserve(per * 8));
-  if (int rc = tfidf_search_batch_keys_device(ix, q_utf8, q_offsets, n_q, k, doc_base, c->d_keys.p)) return rc;
-  DHIP(c->d_all.reserve((size_t)ws * per * 8));
-  if (int rc = coll_gather(c, s, c->d_keys.p, c->d_all.p, per * 8, true)) return rc;
-  DHIP(c->d_out.reserve(per * 8));
-  DHIP(launch_merge_lists(c->d_all.as<uint64_t>(), (uint32_t)ws, per, k, k, n_q, c->d_out.as<uint64_t>(), k, s));
-  DHIP(c->h_out.reserve(per * 8));
-  DHIP(hipMemcpyAsync(c->h_out.p, c->d_out.p, per * 8, hipMemcpyDeviceToHost, s));
-  DHIP(hipStreamSynchronize(s));
+  if (int rc = gather_topk(ix, c, s, doc_base, q_utf8, q_offsets, n_q, k)) return rc;
   const uint64_t *keys = c->h_out.as<uint64_t>();
   for (uint32_t i = 0; i < n_q; i++) {
     uint32_t m = 0;
@@ -819,6 +907,29 @@ extern "C" int tfidf_dist_search_batch(tfidf_index *ix, tfidf_comm *c, uint64_t 
   return TFIDF_OK;
 }
 
+
+namespace {
+// SHARD search result with skipped ranks: TFIDF_OK (the healthy ranks' hits
+// are the answer, as Leader.start returns the other workers' results), the
+// skipped ranks in tfidf_dist_last_failed and, on every rank, a
+// tfidf_last_error() message naming them (the failing rank's own reason there).
+// When no rank could serve, every rank returns the (first) error instead.
+int shard_partial(tfidf_comm *c, int lrc, const std::string &lmsg) {
+  if (!c->last_failed) return TFIDF_OK;
+  const int ws = std::min(c->world, 64);
+  if (c->last_failed == (ws == 64 ? ~0ull : (1ull << ws) - 1)) {   // no rank answered: an error, not an empty map
+    if (lrc) return set_error(lrc, lmsg.c_str());
+    return errf(TFIDF_E_STATE, "no rank could serve the SHARD search");
+  }
+  std::string m = "SHARD search skipped rank(s)";
+  for (int r = 0; r < c->world && r < 64; r++)
+    if ((c->last_failed >> r) & 1u) m += " " + std::to_string(r);
+  if (lrc) m += ": " + lmsg;
+  set_error(lrc ? lrc : TFIDF_E_STATE, m.c_str());
+  return TFIDF_OK;
+}
+}  // namespace
+
 // SHARD mode name table: each rank sorts its own names (String.compareTo),
 // the sorted lists are all-gathered and merged (distinct names in order);
 // the rank's documents map to their name ids on the device.
@@ -828,6 +939,7 @@ extern "C" int tfidf_dist_shard_commit(tfidf_index *ix, tfidf_comm *c, uint64_t 
   DevGuard g(index_device(ix));
   hipStream_t s = index_stream(ix);
   c->names_ready = false;
+  const uint64_t gen = index_generation(ix);
   int local_err = index_committed(ix) ? TFIDF_OK : errf(TFIDF_E_STATE, "index not committed");
   std::string local_msg = local_err ? tfidf_last_error() : "";
   const uint64_t nd = index_num_docs(ix);
@@ -911,7 +1023,7 @@ extern "C" int tfidf_dist_shard_commit(tfidf_index *ix, tfidf_comm *c, uint64_t 
   DHIP(c->d_name_of_doc.reserve(std::max<uint64_t>(nd, 1) * 4));
   if (nd) DHIP(hipMemcpyAsync(c->d_name_of_doc.p, my_nid.data(), nd * 4, hipMemcpyHostToDevice, s));
   DHIP(hipStreamSynchronize(s));
-  c->names_docs = nd;
+  c->names_gen = gen;
   c->names_ready = true;
   if (n_names) *n_names = c->name_off.size() - 1;
   return TFIDF_OK;
@@ -926,27 +1038,33 @@ extern "C" int tfidf_dist_shard_search(tfidf_index *ix, tfidf_comm *c, const uin
   c->last_name.clear();
   c->last_sum.clear();
   c->last_name_bytes = 0;
-  if (!c->names_ready || c->names_docs != index_num_docs(ix))
-    return errf(TFIDF_E_STATE, "tfidf_dist_shard_commit first (after every commit)");
+  c->last_failed = 0;
   if (int rc = query_status(q, q_len)) return rc;
   DevGuard g(index_device(ix));
   hipStream_t s = index_stream(ix);
   const int ws = c->world;
   uint64_t h = 0, maxn = 0;
-  if (int rc = all_keys(ix, c, q, q_len, 0, &h)) return rc;      // local doc ids
-  if (h) {
-    DHIP(c->d_tmp.reserve(h * 8));
-    hipLaunchKernelGGL(k_name_records, dim3(grid_of(h)), dim3(256), 0, s, c->d_keys.as<uint64_t>(), h,
-                       c->d_name_of_doc.as<uint32_t>(), c->d_tmp.as<uint64_t>());
-    DHIP(hipGetLastError());
-    DHIP(hipMemcpyAsync(c->d_keys.p, c->d_tmp.p, h * 8, hipMemcpyDeviceToDevice, s));
+  // a rank that cannot serve (stale name table, failed local search) is a
+  // failed worker: the others' hits are merged without it (Leader.java:67-69)
+  int lrc = local_search_status(ix, c, 0, false);
+  if (!lrc) lrc = all_keys(ix, c, q, q_len, 0, &h);             // local doc ids
+  if (!lrc && h) {
+    if (hipSuccess != c->d_tmp.reserve(h * 8)) lrc = errf(TFIDF_E_OOM, "name records: out of device memory");
+    if (!lrc) {
+      hipLaunchKernelGGL(k_name_records, dim3(grid_of(h)), dim3(256), 0, s, c->d_keys.as<uint64_t>(), h,
+                         c->d_name_of_doc.as<uint32_t>(), c->d_tmp.as<uint64_t>());
+      if (hipGetLastError() != hipSuccess ||
+          hipMemcpyAsync(c->d_keys.p, c->d_tmp.p, h * 8, hipMemcpyDeviceToDevice, s) != hipSuccess)
+        lrc = errf(TFIDF_E_HIP, "name records: launch failed");
+    }
   }
+  const std::string lmsg = lrc ? tfidf_last_error() : "";
   std::vector<uint64_t> ns;
-  if (int rc = gather_var(c, s, h, 0, &ns, &maxn)) return rc;
+  if (int rc = gather_var(c, s, h, 0, lrc, lmsg, 0, 0, false, &ns, &maxn)) return rc;
   uint64_t n = 0;
   std::vector<uint64_t> base(ws);
   for (int r = 0; r < ws; r++) { base[r] = n; n += ns[r]; }
-  if (n == 0) return TFIDF_OK;
+  if (n == 0) return shard_partial(c, lrc, lmsg);
   if (n >= (1ull << 31)) return errf(TFIDF_E_CAPACITY, "too many hits to merge by name");
   // rank-order (name, score) pairs -> stable sort by name id -> per-name sums in rank order
   DHIP(c->d_srt_k.reserve(n * 16 + 2 * ws * 8));
@@ -990,13 +1108,19 @@ extern "C" int tfidf_dist_shard_search(tfidf_index *ix, tfidf_comm *c, const uin
   c->last_name_bytes = nb;
   *n_out = nu;
   if (n_bytes) *n_bytes = nb;
-  return TFIDF_OK;
+  return shard_partial(c, lrc, lmsg);
 }
 
 extern "C" int tfidf_dist_last_hits(const tfidf_comm *c, uint64_t *doc_ids, float *scores, uint64_t cap,
                                     uint64_t *n_out) {
   if (!c || !n_out) return errf(TFIDF_E_INVALID_ARG, "NULL argument");
   return write_hits(const_cast<tfidf_comm *>(c), doc_ids, scores, cap, n_out);
+}
+
+extern "C" int tfidf_dist_last_failed(const tfidf_comm *c, uint64_t *rank_mask) {
+  if (!c || !rank_mask) return errf(TFIDF_E_INVALID_ARG, "NULL argument");
+  *rank_mask = c->last_failed;
+  return TFIDF_OK;
 }
 
 extern "C" int tfidf_dist_last_names(const tfidf_comm *c, uint8_t *buf, uint64_t cap, uint64_t *offsets,
@@ -1125,6 +1249,7 @@ extern "C" int tfidf_node_create_devices(const tfidf_config *cfg, const int32_t 
   if (inproc) {
     n->comms.resize(n_devices);
     tfidf_comm_create_inproc((int32_t)n_devices, n->comms.data());
+    for (uint32_t i = 0; i < n_devices; i++) n->comms[i]->device = devices[i];
     n->transport = TFIDF_TRANSPORT_INPROC;
   } else {
     RcclApi &api = rccl();
@@ -1142,6 +1267,7 @@ extern "C" int tfidf_node_create_devices(const tfidf_config *cfg, const int32_t 
       tfidf_comm *c = new tfidf_comm();
       c->rank = (int)i;
       c->world = (int)n_devices;
+      c->device = devices[i];
       c->t.reset(new RcclTransport(cm[i], (int)n_devices));
       n->comms.push_back(c);
     }
@@ -1289,12 +1415,28 @@ extern "C" int tfidf_node_search_names(tfidf_node *n, const uint8_t *q, uint64_t
   *n_out = *n_bytes = 0;
   if (!n->committed) return errf(TFIDF_E_STATE, "search before tfidf_node_commit");
   if (n->cfg.stats_mode != TFIDF_STATS_SHARD) return errf(TFIDF_E_STATE, "SHARD mode only (tfidf_node_search)");
+  std::vector<std::string> why(n->shards.size());
   if (int rc = n->pool->run([&](uint32_t g) {
         uint64_t m = 0, b = 0;
-        return tfidf_dist_shard_search(n->shards[g], n->comms[g], q, q_len, &m, &b);
+        const int r = tfidf_dist_shard_search(n->shards[g], n->comms[g], q, q_len, &m, &b);
+        if (r == TFIDF_OK && n->comms[g]->last_failed) why[g] = tfidf_last_error();
+        return r;
       }))
     return rc;
-  return tfidf_dist_last_names(n->comms[0], buf, cap, offsets, scores, n_cap, n_out, n_bytes);
+  const int rc = tfidf_dist_last_names(n->comms[0], buf, cap, offsets, scores, n_cap, n_out, n_bytes);
+  if (rc == TFIDF_OK && n->comms[0]->last_failed) {        // partial answer: say which shards were skipped
+    std::string m = why[0];
+    for (size_t g = 0; g < why.size(); g++)
+      if ((n->comms[0]->last_failed >> g) & 1u) m += "; shard " + std::to_string(g) + ": " + why[g];
+    set_error(TFIDF_OK, m.c_str());
+  }
+  return rc;
+}
+
+extern "C" int tfidf_node_last_failed(const tfidf_node *n, uint64_t *shard_mask) {
+  if (!n || !shard_mask) return errf(TFIDF_E_INVALID_ARG, "NULL argument");
+  *shard_mask = n->comms.empty() ? 0 : n->comms[0]->last_failed;
+  return TFIDF_OK;
 }
 
 extern "C" int tfidf_node_doc_key(tfidf_node *n, uint64_t doc, uint8_t *buf, uint64_t cap, uint64_t *n_out) {

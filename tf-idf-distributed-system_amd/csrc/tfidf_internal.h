@@ -391,6 +391,7 @@ hipStream_t index_stream(tfidf_index *ix);
 int index_device(const tfidf_index *ix);
 bool index_committed(const tfidf_index *ix);
 uint64_t index_num_docs(const tfidf_index *ix);
+uint64_t index_generation(const tfidf_index *ix);   // successful commits so far
 int set_error(int code, const char *msg);       // sets tfidf_last_error() of the calling thread
 // String.compareTo order of two UTF-8 names (UTF-16 code units; Leader.java:80-88 TreeMap)
 int utf16_compare(const uint8_t *a, uint64_t na, const uint8_t *b, uint64_t nb);

@@ -139,6 +139,7 @@ SIGNATURES = {
     "tfidf_dist_shard_commit": (C.c_int, [VP, VP, U64P]),
     "tfidf_dist_shard_search": (C.c_int, [VP, VP, C.c_char_p, C.c_uint64, U64P, U64P]),
     "tfidf_dist_last_hits": (C.c_int, [VP, U64P, F32P, C.c_uint64, U64P]),
+    "tfidf_dist_last_failed": (C.c_int, [VP, U64P]),
     "tfidf_dist_last_names": (C.c_int, [VP, C.c_char_p, C.c_uint64, U64P, F64P, C.c_uint64, U64P, U64P]),
     "tfidf_node_create": (C.c_int, [VP, C.c_uint64, C.POINTER(VP)]),
     "tfidf_node_create_devices": (C.c_int, [VP, C.POINTER(C.c_int32), C.c_uint32, C.c_uint32, C.POINTER(VP)]),
@@ -151,6 +152,7 @@ SIGNATURES = {
     "tfidf_node_search_names": (C.c_int, [VP, C.c_char_p, C.c_uint64, C.c_char_p, C.c_uint64, U64P, F64P,
                                           C.c_uint64, U64P, U64P]),
     "tfidf_node_doc_key": (C.c_int, [VP, C.c_uint64, C.c_char_p, C.c_uint64, U64P]),
+    "tfidf_node_last_failed": (C.c_int, [VP, U64P]),
     "tfidf_node_stats_get": (C.c_int, [VP, VP]),
     "tfidf_device_free": (C.c_int, [C.c_int, VP]),
     "tfidf_device_copy": (C.c_int, [C.c_int, VP, VP, C.c_uint64, C.c_int]),

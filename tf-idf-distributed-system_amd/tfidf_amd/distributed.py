@@ -227,6 +227,13 @@ class DistShard:
         return _last_names(self.comm._h, n.value, nb.value)
 
 
+    def last_failed(self):
+        """Ranks skipped by the last shard_search (bit r = rank r)."""
+        m = C.c_uint64()
+        L.check(L.load().tfidf_dist_last_failed(self.comm._h, C.byref(m)))
+        return m.value
+
+
 def _last_names(h, n, nb):
     buf = C.create_string_buffer(max(nb, 1))
     offs = np.zeros(n + 1, np.uint64)
@@ -322,6 +329,18 @@ class Node:
                                             L.ptr(sc, C.c_double), n.value, C.byref(n), C.byref(nb)))
         raw = buf.raw
         return [(raw[int(offs[i]):int(offs[i + 1])], float(sc[i])) for i in range(n.value)]
+
+    def last_failed(self):
+        """Shards skipped by the last search_names (bit g = shard g)."""
+        m = C.c_uint64()
+        L.check(L.load().tfidf_node_last_failed(self._h, C.byref(m)))
+        return m.value
+
+    def shard(self, i):
+        """Shard i's tfidf_index handle (owned by the node)."""
+        h = C.c_void_p()
+        L.check(L.load().tfidf_node_shard(self._h, i, C.byref(h), None))
+        return h
 
     def doc_key(self, doc):
         buf = C.create_string_buffer(4096)
