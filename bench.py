@@ -203,8 +203,87 @@ def measured_copy_GBs(dev, nbytes=1 << 30, reps=5):
     return 2 * nbytes / (ms * 1e-3) / 1e9
 
 
+def bench_node(args):
+    """TFIDF_BENCH_NODE=1: process model (1) of include/tfidf.h — ONE process
+    owns --gpus N devices through tfidf_node (device mask (1 << N) - 1, RCCL
+    communicator from ncclCommInitAll, one worker thread per shard): the ABI a
+    Java host binds.  Each shard's 1M-doc corpus is
+    generated on its own GPU; a timed step = tfidf_node_commit (every shard's
+    build in parallel + the GLOBAL statistics exchange); then node-level batched
+    and single GLOBAL queries.  Prints one JSON line (not the driver's line)."""
+    import ctypes as C
+    import torch
+    from tfidf_amd import _lib as L
+    from tfidf_amd import synth
+    from tfidf_amd import distributed as D
+    G = args.gpus
+    torch.cuda.set_device(0)
+    cap = args.cap_log2 or 18
+    while not args.cap_log2 and (1 << cap) < 1.6 * args.vocab:
+        cap += 1
+    node = D.Node(devices=list(range(G)), stats_mode=L.STATS_GLOBAL, vocab_capacity_log2=cap)
+    lib = L.load()
+    corpora = []
+    for g in range(G):
+        c = synth.DeviceCorpus(args.docs, V=args.vocab, len_min=args.len_min, len_max=args.len_max,
+                               doc_base=g * args.docs, device=g)
+        L.check(lib.tfidf_add_docs_device(node.shard(g), C.c_void_p(c.d_text), C.c_void_p(c.d_offsets), args.docs,
+                                          c.total_bytes))
+        corpora.append(c)
+    for _ in range(args.warmup):
+        node.commit()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        node.commit()
+    elapsed = time.perf_counter() - t0
+    st = node.stats()
+    per_shard = []
+    for g in range(G):
+        t = L.CommitTiming()
+        L.check(lib.tfidf_get_commit_timing(node.shard(g), C.byref(t)))
+        per_shard.append(t.ms_total)
+    out = {
+        "metric": "docs indexed/sec + queries scored/sec (node) at 1/2/4/8 GPUs; % HBM roofline",
+        "value": st["num_docs"] * args.steps / elapsed, "unit": "docs/s", "n_gpus": G, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None,
+        "dtype": "u8/u32 (integer inversion), f32 BM25 with f64 accumulation",
+        "data": "synthetic (Zipf s=1.0 corpus generated in HBM by tfidf_synth_corpus, seed 20251015)",
+        "config": {"workload": "cfg2 per shard: %d docs/GPU x U[%d,%d] tokens, V=%d; tfidf_node_commit = every "
+                               "shard's build + GLOBAL stats exchange" % (args.docs, args.len_min, args.len_max,
+                                                                          args.vocab),
+                   "process_model": "node: one process, tfidf_node over device mask 0x%x (include/tfidf.h (1))"
+                                    % ((1 << G) - 1),
+                   "transport": {1: "rccl", 2: "inproc"}.get(st["transport"], st["transport"]),
+                   "docs": st["num_docs"], "global_vocab": st["num_terms"], "parallelism": "dp%d" % G},
+        "shard_build_device_ms": per_shard,
+    }
+    if not args.no_queries:
+        bq = synth.queries(args.batch_queries)
+        node.search_batch(bq[:100], 10)
+        for k in (10, 100):
+            t0 = time.perf_counter()
+            node.search_batch(bq, k)
+            out["batch%dk_top%d_qps" % (len(bq) // 1000, k)] = len(bq) / (time.perf_counter() - t0)
+        qs = synth.queries(max(args.queries, 1))
+        node.search(qs[0], 10)
+        lat = []
+        for q in qs:
+            t1 = time.perf_counter()
+            node.search(q, 10)
+            lat.append(time.perf_counter() - t1)
+        out["single_top10_p50_ms"] = float(np.percentile(lat, 50)) * 1e3
+        out["single_top10_qps"] = len(qs) / sum(lat)
+    node.close()
+    for c in corpora:
+        c.free()
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
+    if os.environ.get("TFIDF_BENCH_NODE") == "1":
+        return bench_node(args)
     rc = launch_or_check(args, sys.argv[1:])
     if rc is not None:
         sys.exit(rc)
@@ -423,6 +502,32 @@ def main():
         for q in qs[:n_all]:
             b_all += post_bytes(q)
         b_all += 8 * nh
+        # 16 request threads (Worker.processDocuments on Tomcat threads): each
+        # search runs on the snapshot of the last commit with its own stream
+        # and scratch, concurrently with the others (include/tfidf.h "Threading")
+        import threading
+
+        def threaded_qps(fn, per_thread, n_threads=16):
+            bar = threading.Barrier(n_threads + 1)
+
+            def body(t):
+                bar.wait()
+                for i in range(per_thread):
+                    fn(qs[(t * per_thread + i) % len(qs)])
+            th = [threading.Thread(target=body, args=(t,)) for t in range(n_threads)]
+            for x in th:
+                x.start()
+            bar.wait()
+            t0 = time.perf_counter()
+            for x in th:
+                x.join()
+            return n_threads * per_thread / (time.perf_counter() - t0)
+
+        idx.set_query_timing(False)
+        threaded_qps(idx.search_all_arrays, 2)                      # contexts created
+        mt_all = threaded_qps(idx.search_all_arrays, 25)
+        mt_top = threaded_qps(lambda q: idx.search_arrays(q, 10), 100)
+        idx.set_query_timing(True)
         bq = synth.queries(args.batch_queries)
         idx.search_batch(bq[:100], 10)
         t0 = time.perf_counter()
@@ -443,6 +548,7 @@ def main():
             "single_top10_device_ms_avg": dev_ms / len(qs),
             "single_all_hits_qps": n_all / t_all, "avg_hits": nh / n_all,
             "single_all_hits_device_ms_avg": all_dev / n_all,
+            "threads16_all_hits_qps": mt_all, "threads16_top10_qps": mt_top,
             "batch10k_top10_qps": len(bq) / t_b,
             "batch10k_device_ms": tot_ms, "batch10k_scoring_ms": sc_ms,
             "roofline": {

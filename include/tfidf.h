@@ -33,9 +33,17 @@
  *
  * Conventions: every call returns an int status (TFIDF_OK == 0); the message
  * of the last failure on the calling thread is tfidf_last_error().  Buffers
- * are caller-owned and only borrowed for the duration of a call.  Searches on
- * a committed index are safe to issue from several threads; add/commit are
- * serialised by the caller (Worker.java:136 synchronized(indexWriter)).
+ * are caller-owned and only borrowed for the duration of a call.
+ * Threading (Worker.java:223 opens a DirectoryReader on the last commit per
+ * request while uploads commit beside it, :136-139): every commit publishes an
+ * immutable, refcounted snapshot.  Searches and the other read calls run on
+ * the snapshot published when they start, concurrently with each other (each
+ * on its own stream and scratch) and with tfidf_add_docs / tfidf_commit on
+ * another thread, and never wait for a commit; a snapshot is freed, or rebuilt
+ * by a later commit, when its last reader leaves.  Documents added after a
+ * commit are invisible to searches until the next commit.  Writers (add_docs,
+ * commit, clear, load, the GLOBAL statistics setters) serialise among
+ * themselves (Worker.java:136 synchronized(indexWriter)).
  * Scores are IEEE float32 bit-identical to Lucene 9.8.0 BM25Similarity
  * (k1 = 1.2, b = 0.75); hits are ordered by (score desc, doc asc).
  */
@@ -187,7 +195,24 @@ int tfidf_search_coalesced(tfidf_index *ix, const uint8_t *q, uint64_t q_len, ui
                            float *scores, uint64_t cap, uint64_t *n_out, uint32_t wait_us);
 int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const uint64_t *q_offsets, uint32_t n_q,
                        uint32_t k, uint32_t *doc_ids, float *scores, uint32_t *counts);
-/* Per-query device time of the last search call (HIP events, index stream). */
+/* Readers (Worker.java:223 DirectoryReader.open per request; the hits' stored
+ * "path" fields are read from the same reader, :234-238): a reader pins the
+ * snapshot published when it is opened, so doc ids it returns map to keys
+ * with tfidf_reader_doc_key even while later commits publish other snapshots.
+ * tfidf_reader_search: as tfidf_search, on the reader's snapshot.
+ * tfidf_reader_info: the snapshot's commit generation (1, 2, ... per
+ * successful commit) and document count.  A reader may be used from several
+ * threads; close it once (its snapshot is released with the last user). */
+typedef struct tfidf_reader tfidf_reader;
+int tfidf_reader_open(tfidf_index *ix, tfidf_reader **out);
+int tfidf_reader_close(tfidf_reader *rd);
+int tfidf_reader_info(const tfidf_reader *rd, uint64_t *generation, uint64_t *num_docs);
+int tfidf_reader_search(tfidf_reader *rd, const uint8_t *q, uint64_t q_len, uint32_t k, uint32_t *doc_ids,
+                        float *scores, uint64_t cap, uint64_t *n_out);
+int tfidf_reader_doc_key(const tfidf_reader *rd, uint64_t doc, uint8_t *buf, uint64_t cap, uint64_t *n_out);
+/* tfidf_doc_keys of the reader's snapshot (offsets[num_docs + 1] of tfidf_reader_info). */
+int tfidf_reader_doc_keys(const tfidf_reader *rd, uint8_t *buf, uint64_t cap, uint64_t *offsets, uint64_t *n_bytes);
+/* Per-query device time of the last search call on this index (HIP events on the search's stream). */
 int tfidf_last_search_ms(const tfidf_index *ix, float *ms_scoring, float *ms_total);
 /* Device-time measurement of searches (HIP events around scoring; on by
  * default).  Off for serving: the three event records cost ~17 us per single
@@ -217,7 +242,9 @@ int tfidf_set_stream(tfidf_index *ix, void *stream);
 int tfidf_doc_key(const tfidf_index *ix, uint64_t doc, uint8_t *buf, uint64_t cap, uint64_t *n_out);
 /* Every committed document's key (Worker.java:214 StringField "path"), in doc
  * order: bytes concatenated into buf, offsets[num_docs + 1]; TFIDF_E_BUFFER with
- * *n_bytes = size needed when cap is too small. */
+ * *n_bytes = size needed when cap is too small.  num_docs is that of the
+ * snapshot published at the call: beside concurrent commits, size offsets from
+ * a reader (tfidf_reader_doc_keys). */
 int tfidf_doc_keys(const tfidf_index *ix, uint8_t *buf, uint64_t cap, uint64_t *offsets, uint64_t *n_bytes);
 int tfidf_doc_len(tfidf_index *ix, uint64_t doc, uint32_t *len, uint8_t *norm);
 /* Documents of the last commit whose bytes are not valid UTF-8 (where the

@@ -11,9 +11,11 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -133,49 +135,236 @@ struct DeviceGuard {
 // path's per-range counters), i.e. C <= 64 x 32768
 constexpr uint32_t kMaxBlockCapLog2 = 21;
 
-enum { EV_START, EV_TOK, EV_L0, EV_LONG, EV_D0, EV_DF, EV_BSCAN, EV_CSCAN, EV_SCAT, EV_Q0, EV_Q1, EV_Q2, EV_N };
+enum { EV_START, EV_TOK, EV_L0, EV_LONG, EV_D0, EV_DF, EV_BSCAN, EV_CSCAN, EV_SCAT, EV_N };
+enum { QEV_0, QEV_1, QEV_2, QEV_N };   // search timing events (per search context)
 
 constexpr size_t kCoalesceMaxDefault = 8192;   // tfidf_search_coalesced: requests per batch
 
+// device buffer with an owner's lifetime (freed on its device)
+struct DevMem : DevBuf {
+  int dev = 0;
+  explicit DevMem(int d) : dev(d) {}
+  DevMem(const DevMem &) = delete;
+  DevMem &operator=(const DevMem &) = delete;
+  ~DevMem() {
+    if (p) { DeviceGuard g(dev); release(); }
+  }
+};
+
+// Document keys (relative paths), append-only in chunks that never change
+// once a published snapshot holds them: a snapshot keeps the chunk list it was
+// committed with, the builder appends to its own last chunk (or starts a new
+// one when a snapshot shares it).  Staged id -> chunk by binary search.
+struct KeyChunk {
+  uint64_t first = 0;                // staged id of the chunk's first document
+  std::string arena;
+  std::vector<uint64_t> off{0};
+  std::vector<uint8_t> synth;        // 1 = key is the decimal staged id
+  uint64_t size() const { return synth.size(); }
+};
+struct KeyTable {
+  std::vector<std::shared_ptr<KeyChunk>> ch;
+  const KeyChunk &chunk_of(uint64_t st) const {
+    size_t a = 0, z = ch.size();
+    while (z - a > 1) {
+      const size_t m = (a + z) / 2;
+      if (ch[m]->first <= st) a = m; else z = m;
+    }
+    return *ch[a];
+  }
+  void key(uint64_t st, std::string *out) const {
+    const KeyChunk &c = chunk_of(st);
+    const uint64_t i = st - c.first;
+    if (c.synth[i]) *out = std::to_string(st);
+    else out->assign(c.arena.data() + c.off[i], c.off[i + 1] - c.off[i]);
+  }
+  uint64_t key_len(uint64_t st) const {
+    const KeyChunk &c = chunk_of(st);
+    const uint64_t i = st - c.first;
+    return c.synth[i] ? std::to_string(st).size() : c.off[i + 1] - c.off[i];
+  }
+  // the builder's chunk to append to (a new one when a snapshot shares the last)
+  KeyChunk &tail(uint64_t n_staged) {
+    if (ch.empty() || ch.back().use_count() > 1) {
+      ch.push_back(std::make_shared<KeyChunk>());
+      ch.back()->first = n_staged;
+    }
+    return *ch.back();
+  }
+  // flat copies (persistence)
+  void flatten(std::string *arena, std::vector<uint64_t> *off, std::vector<uint8_t> *synth) const {
+    arena->clear();
+    off->assign(1, 0);
+    synth->clear();
+    for (const auto &c : ch) {
+      for (uint64_t i = 0; i < c->size(); i++) {
+        arena->append(c->arena, c->off[i], c->off[i + 1] - c->off[i]);
+        off->push_back(arena->size());
+      }
+      synth->insert(synth->end(), c->synth.begin(), c->synth.end());
+    }
+  }
+  // many small chunks (one per commit of a single upload): merge them into one
+  void compact() {
+    if (ch.size() <= 64) return;
+    auto one = std::make_shared<KeyChunk>();
+    flatten(&one->arena, &one->off, &one->synth);
+    ch.assign(1, one);
+  }
+};
+
+// Statistics in force for BM25 (the shard's own, or GLOBAL from the node-level
+// exchange).  Never edited once a search can see it: the GLOBAL setters
+// publish a new view.
+struct StatsView {
+  int dev = 0;
+  bool global = false;
+  uint64_t doc_count = 0, sum_ttf = 0;   // docCount / sumTotalTermFreq in force
+  PinnedVec<uint32_t> gdf;               // GLOBAL df per dictionary slot (host mirror)
+  hipEvent_t gdf_ev = nullptr;           // gdf copied (set asynchronously by tfidf_set_global_df_device)
+  bool gdf_pending = false;
+  std::mutex gdf_mu;
+  DevMem cache;                          // 256-entry BM25 norm cache (device)
+  PinnedVec<float> h_cache;
+  explicit StatsView(int d) : dev(d), cache(d) {
+    DeviceGuard g(d);
+    hipEventCreateWithFlags(&gdf_ev, hipEventDisableTiming);
+  }
+  ~StatsView() {
+    DeviceGuard g(dev);
+    if (gdf_ev) {
+      hipEventSynchronize(gdf_ev);
+      hipEventDestroy(gdf_ev);
+    }
+  }
+  int wait_gdf();                        // the GLOBAL df mirror, before its first use
+};
+
+// One committed index: everything a search reads.  Published by tfidf_commit
+// as a refcounted snapshot and never changed afterwards (only its `stats`
+// pointer is replaced, under the index's snap_mu); a search holds a reference
+// for its whole run, so a commit never waits for searches and a search never
+// waits for a commit (the reference opens a DirectoryReader on the last commit
+// per request, Worker.java:223, while uploads commit beside it, :136-139).
+// A snapshot no search holds any more is rebuilt in place by a later commit.
+struct Snapshot {
+  int dev = 0;
+  uint64_t generation = 0;
+  uint32_t cap_log2 = 18, C = 0, range_shift = 15, R = 1, n_blocks = 0;
+  uint64_t n_docs = 0, text_bytes = 0;
+  bool term_major = false;
+  std::vector<uint32_t> live_map;      // committed -> staged (empty = identity)
+  KeyTable keys;                       // document keys of the staged ids
+  std::shared_ptr<DevMem> text, offsets;   // the staged corpus it was built from
+  DevMem dict, csr, csr_esc, post_esc, doc_len, doc_nuniq, doc_norm, rsplit, blk, bbase, post, row_off, toff, tdf;
+  std::vector<uint32_t> malformed;     // ascending committed ids of documents that are not UTF-8
+  std::vector<uint64_t> h_esc;         // CSR tf escapes, sorted (csr_put)
+  std::vector<uint64_t> h_post_esc;    // block-major posting tf escapes, sorted (post_word)
+  uint64_t hash_seed = 0;
+  uint32_t hash_rebuilds = 0;
+  PinnedVec<uint64_t> h_dict;          // host mirrors for query analysis (pinned)
+  PinnedVec<uint32_t> h_df;
+  uint64_t doc_count = 0, sum_ttf = 0, nnz = 0, num_terms = 0, long_docs = 0;
+  uint32_t pack_docs = 1;
+  uint64_t pack_retried = 0, unicode_docs = 0, long_chunked = 0;
+  std::shared_ptr<StatsView> stats;    // replaced under tfidf_index::snap_mu
+  std::unordered_map<uint32_t, std::string> term_cache;   // hashed slots' term strings (slot_term)
+  std::mutex term_mu;
+  explicit Snapshot(int d)
+      : dev(d), dict(d), csr(d), csr_esc(d), post_esc(d), doc_len(d), doc_nuniq(d), doc_norm(d), rsplit(d), blk(d),
+        bbase(d), post(d), row_off(d), toff(d), tdf(d) {}
+  const uint32_t *df_dev() const {
+    return term_major ? tdf.as<uint32_t>() : blk.as<uint32_t>() + (size_t)n_blocks * C;
+  }
+  uint64_t staged_of(uint64_t doc) const { return live_map.empty() ? doc : live_map[doc]; }
+};
+
+// Per-search scratch: a stream (plus a side stream for the batch kernels'
+// fork), timing events and buffers.  Searches take a context from the index's
+// pool, so concurrent searches never share one.
+struct SearchCtx {
+  int dev = 0;
+  hipStream_t own = nullptr, side = nullptr;
+  hipEvent_t ev[QEV_N] = {};
+  hipEvent_t q_ev[2] = {nullptr, nullptr};  // fork / join of the wave-unit kernel on `side`
+  hipEvent_t q_in_ev = nullptr;             // the last upload out of q_host
+  bool q_in_pending = false;
+  bool q_rec_start = true;                  // run_scoring records QEV_0 (false: a later chunk of a batch)
+  bool q_timing = true;
+  DevMem q_in, q_out, cand, cand_n, out_doc, out_score, hits, hits_n, hits_c, hits_s, hits_P, ovf;
+  PinnedVec<uint32_t> q_host, q_res, q_cand_h;   // q_cand_h: fused single query's block candidates (host merge)
+  std::vector<uint64_t> q_merge;
+  std::vector<uint32_t> q_units;            // batch scoring units {q, b0, b1, 0} (run_scoring)
+  uint32_t *res_doc = nullptr, *res_n = nullptr;
+  float *res_score = nullptr;
+  explicit SearchCtx(int d)
+      : dev(d), q_in(d), q_out(d), cand(d), cand_n(d), out_doc(d), out_score(d), hits(d), hits_n(d), hits_c(d),
+        hits_s(d), hits_P(d), ovf(d) {}
+  int init() {
+    DeviceGuard g(dev);
+    if (hipStreamCreateWithFlags(&own, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&side, hipStreamNonBlocking) != hipSuccess)
+      return fail(TFIDF_E_HIP, "hipStreamCreate failed");
+    for (int i = 0; i < QEV_N; i++) hipEventCreate(&ev[i]);
+    for (int i = 0; i < 2; i++) hipEventCreateWithFlags(&q_ev[i], hipEventDisableTiming);
+    hipEventCreateWithFlags(&q_in_ev, hipEventDisableTiming);
+    return TFIDF_OK;
+  }
+  ~SearchCtx() {
+    DeviceGuard g(dev);
+    if (own) hipStreamSynchronize(own);
+    if (side) hipStreamSynchronize(side);
+    for (int i = 0; i < QEV_N; i++) if (ev[i]) hipEventDestroy(ev[i]);
+    for (int i = 0; i < 2; i++) if (q_ev[i]) hipEventDestroy(q_ev[i]);
+    if (q_in_ev) hipEventDestroy(q_in_ev);
+    if (side) hipStreamDestroy(side);
+    if (own) hipStreamDestroy(own);
+  }
+};
+
 struct tfidf_index {
   tfidf_config cfg;
-  std::mutex mu;
-  hipStream_t stream = nullptr;      // stream all work is issued on (own_stream unless tfidf_set_stream)
+  std::mutex mu;                     // writers: add_docs, commit, clear, load, the GLOBAL exchange
+  hipStream_t stream = nullptr;      // the writers' stream (own_stream unless tfidf_set_stream)
   hipStream_t own_stream = nullptr;
+  hipStream_t user_stream = nullptr; // tfidf_set_stream: searches run on it too
   hipEvent_t ev[EV_N];
   // side stream for the dictionary's host mirror: its D2H copy overlaps the inversion
   hipStream_t copy_stream = nullptr;
   hipEvent_t mir_ev[2];            // [0] dictionary final (main stream), [1] mirror copied
   int num_cus = 256;
 
-  // staged corpus
-  DevBuf text, offsets;            // offsets: u64[n_staged + 1]
+  // published snapshot (searches) and the one a commit may rebuild in place
+  std::mutex snap_mu;
+  std::shared_ptr<Snapshot> cur, spare;
+  uint64_t generation = 0;           // successful commits so far
+
+  // search contexts (one per concurrent search)
+  std::mutex ctx_mu;
+  std::vector<std::unique_ptr<SearchCtx>> ctx_free;
+  std::atomic<bool> q_timing{true};  // record HIP events around each search (tfidf_set_query_timing)
+  std::mutex ms_mu;
+  float last_ms_scoring = 0, last_ms_total = 0;
+
+  // staged corpus (builder)
+  std::shared_ptr<DevMem> text, offsets;   // offsets: u64[n_staged + 1]
   // corpus loader: two pinned host staging buffers, refilled while the other one's DMA runs
   void *stage[2] = {nullptr, nullptr};
   hipEvent_t stage_ev[2] = {nullptr, nullptr};
   uint64_t text_bytes = 0, n_staged = 0;
   std::vector<uint64_t> h_offsets{0};
-  std::string key_arena;
-  std::vector<uint64_t> key_off{0};
-  std::vector<uint8_t> key_synth;  // 1 = key is the decimal ordinal
+  KeyTable keys;
   std::vector<uint8_t> staged_live;
   std::unordered_map<std::string, uint64_t> key_to_staged;
   uint64_t n_dead = 0;
 
-  // committed
-  bool committed = false;
-  uint64_t generation = 0;         // successful commits so far (node level: stale name tables / GLOBAL df)
-  uint64_t n_docs = 0;
-  std::vector<uint32_t> live_map;  // committed -> staged (empty = identity)
+  // build scratch (the commit in progress)
+  uint32_t cap_log2 = 18;
   DevBuf d_live_map;
-  uint32_t cap_log2 = 18, C = 0, range_shift = 15, R = 1, n_blocks = 0;
-  DevBuf dict, csr, csr_esc, post_esc, doc_len, doc_nuniq, doc_norm, rsplit, long_list, uni_list, counters, blk, bbase, post, post_tmp;
+  DevBuf long_list, uni_list, counters, post_tmp;
   DevBuf retry_list;                   // packed wave path: documents deferred to the single-document pass
   DevBuf bad_list;                     // documents that are not valid UTF-8 (indexed empty)
-  std::vector<uint32_t> malformed;     // ... of the last commit, ascending committed ids
-  std::vector<uint64_t> h_esc;         // CSR tf escapes of the last build, sorted (csr_put)
-  std::vector<uint64_t> h_post_esc;    // block-major posting tf escapes, sorted (post_word)
-  uint64_t hash_seed = 0;              // KeyBuilder seed of the committed index (0 unless a collision was met)
+  uint64_t hash_seed = 0;              // KeyBuilder seed of the build (0 unless a collision was met)
   uint32_t hash_rebuilds = 0;          // builds redone for a hash collision in the last commit
   uint32_t hash_floor = 0;             // first seed attempt of the next commit (tfidf_set_hash_attempt)
   uint32_t collision_doc = 0;          // a document of the last detected collision (diagnostics)
@@ -186,59 +375,67 @@ struct tfidf_index {
   bool cq_leader = false;
   size_t cq_max = kCoalesceMaxDefault;  // requests per batch
   uint64_t cq_batches = 0, cq_queries = 0;
+  std::atomic<uint64_t> unit_batches{0}, unit_count{0}, fused_queries{0};
   DevBuf verify_defer, lt_pos;
-  std::unordered_map<uint32_t, std::string> term_cache;   // hashed slots' term strings (slot_term)
-  std::mutex term_mu;
-  uint32_t pack_docs = 1;              // documents per wave window in the last commit
-  uint64_t pack_retried = 0;           // documents the packs deferred in the last commit
-  uint64_t unicode_docs = 0;           // documents with non-ASCII text in the last commit
-  // term-major inversion (large vocabularies): compact row offsets, sort values (x2), term offsets, df
-  bool term_major = false;
-  DevBuf row_off, tvals, toff, tdf, term_tmp, term_esc;
-  const uint32_t *df_dev() const {
-    return term_major ? tdf.as<uint32_t>() : blk.as<uint32_t>() + (size_t)n_blocks * C;
-  }
+  DevBuf tvals, term_tmp, term_esc;     // term-major inversion: sort values, scratch, tf escapes
   DevBuf lt_keys, lt_cnt, lt_g;
   DevBuf pairs, pair_ub, chunk_list, chunk_docs, chunk_fail, uchunk;   // book-sized documents (chunk-parallel)
   PinnedVec<uint32_t> ldocs_h, pre_h;                            // their host staging
   PinnedVec<uint64_t> hctr_h;                                    // build counters read back after the tokenizers
-  uint64_t long_chunked = 0;           // long documents the chunk path took in the last commit
   uint32_t lt_log2 = 0, lt_wgs = 64;   // lt_wgs: long-path workgroups always allowed
-  PinnedVec<uint64_t> h_dict;        // host mirrors for query analysis (pinned)
-  PinnedVec<uint32_t> h_df;
-  uint64_t doc_count = 0, sum_ttf = 0, nnz = 0, num_terms = 0, long_docs = 0;
   tfidf_commit_timing timing{};
 
-  // statistics in force
-  bool has_global = false;
-  PinnedVec<uint32_t> gdf;         // per slot (GLOBAL), host mirror
-  hipEvent_t gdf_ev = nullptr;     // gdf mirror copied (tfidf_set_global_df_device is asynchronous)
-  bool gdf_pending = false;
-  PinnedVec<float> h_cache;        // BM25 norm cache staging (pinned: asynchronous upload)
-  uint64_t g_doc_count = 0, g_sum_ttf = 0;
+  // GLOBAL exchange (writers): canonical ids, record order -> slot, owner-side scratch
   DevBuf canon_of_slot;
   uint64_t n_canon = 0;
-  // term-ownership exchange: record order -> slot, owner-side scratch table
-  DevBuf sent_slot, vcounts, vnu, vt_table, vt_sum, vt_rslot, gdf_dev, ovf;
+  DevBuf sent_slot, vcounts, vnu, vt_table, vt_sum, vt_rslot, gdf_dev;
   uint64_t n_sent = 0;
+};
 
-  // query scratch
-  // query upload / top-k results: one pinned staging buffer and one copy each
-  // way per search (q_in: off | slot | w | role | meta; q_out: doc | score | n)
-  DevBuf q_in, q_out;
-  PinnedVec<uint32_t> q_host, q_res, q_cand_h;   // q_cand_h: fused single query's block candidates (host merge)
-  std::vector<uint64_t> q_merge;
-  std::vector<uint32_t> q_units;       // batch scoring units {q, b0, b1, 0} (run_scoring)
-  uint64_t unit_batches = 0, unit_count = 0, fused_queries = 0;
-  bool q_timing = true;                // record HIP events around each search (tfidf_set_query_timing)
-  bool q_rec_start = true;             // run_scoring records EV_Q0 (false: a later chunk of a pipelined batch)
-  hipEvent_t q_ev[2] = {nullptr, nullptr};  // fork / join of the wave-unit kernel on copy_stream
-  hipEvent_t q_in_ev = nullptr;        // the last upload out of q_host
-  bool q_in_pending = false;
-  uint32_t *res_doc = nullptr, *res_n = nullptr;
-  float *res_score = nullptr;
-  DevBuf q_off, q_slot, q_w, q_role, q_meta, cache, cand, cand_n, out_doc, out_score, out_n, hits, hits_n, hits_c, hits_s, hits_P, sort_tmp;   // hits_s: spare for oversized merge groups
-  float last_ms_scoring = 0, last_ms_total = 0;
+int StatsView::wait_gdf() {
+  std::lock_guard<std::mutex> lk(gdf_mu);
+  if (gdf_pending) {
+    HIP_TRY(hipEventSynchronize(gdf_ev));
+    gdf_pending = false;
+  }
+  return TFIDF_OK;
+}
+
+// the published snapshot and its statistics view (both null before the first commit)
+static std::shared_ptr<Snapshot> current(tfidf_index *ix, std::shared_ptr<StatsView> *v = nullptr) {
+  std::lock_guard<std::mutex> lk(ix->snap_mu);
+  if (v) *v = ix->cur ? ix->cur->stats : nullptr;
+  return ix->cur;
+}
+static std::shared_ptr<Snapshot> current(const tfidf_index *ix, std::shared_ptr<StatsView> *v = nullptr) {
+  return current(const_cast<tfidf_index *>(ix), v);
+}
+
+// A search context from the pool (created on demand), returned on scope exit.
+struct CtxLease {
+  tfidf_index *ix;
+  std::unique_ptr<SearchCtx> c;
+  int rc = TFIDF_OK;
+  explicit CtxLease(tfidf_index *x) : ix(x) {
+    {
+      std::lock_guard<std::mutex> lk(ix->ctx_mu);
+      if (!ix->ctx_free.empty()) {
+        c = std::move(ix->ctx_free.back());
+        ix->ctx_free.pop_back();
+      }
+    }
+    if (!c) {
+      c.reset(new SearchCtx(ix->cfg.device));
+      rc = c->init();
+    }
+    c->q_timing = ix->q_timing.load();
+  }
+  ~CtxLease() {
+    if (!c || rc) return;
+    std::lock_guard<std::mutex> lk(ix->ctx_mu);
+    ix->ctx_free.push_back(std::move(c));
+  }
+  hipStream_t stream() const { return ix->user_stream ? ix->user_stream : c->own; }
 };
 
 // ---------------------------------------------------------------------------
@@ -289,13 +486,12 @@ extern "C" int tfidf_create(const tfidf_config *cfg, tfidf_index **out) {
   for (int i = 0; i < EV_N; i++) hipEventCreate(&ix->ev[i]);
   for (int i = 0; i < 2; i++) hipEventCreateWithFlags(&ix->stage_ev[i], hipEventDisableTiming);
   for (int i = 0; i < 2; i++) hipEventCreateWithFlags(&ix->mir_ev[i], hipEventDisableTiming);
-  hipEventCreateWithFlags(&ix->gdf_ev, hipEventDisableTiming);
-  hipEventCreateWithFlags(&ix->q_in_ev, hipEventDisableTiming);
-  for (int i = 0; i < 2; i++) hipEventCreateWithFlags(&ix->q_ev[i], hipEventDisableTiming);
-  hipError_t e = ix->offsets.reserve(64);
+  ix->text = std::make_shared<DevMem>(cfg->device);
+  ix->offsets = std::make_shared<DevMem>(cfg->device);
+  hipError_t e = ix->offsets->reserve(64);
   if (e != hipSuccess) { delete ix; return fail(TFIDF_E_OOM, "hipMalloc offsets"); }
   uint64_t zero = 0;
-  hipMemcpy(ix->offsets.p, &zero, 8, hipMemcpyHostToDevice);
+  hipMemcpy(ix->offsets->p, &zero, 8, hipMemcpyHostToDevice);
   *out = ix;
   return TFIDF_OK;
 }
@@ -305,23 +501,23 @@ extern "C" int tfidf_destroy(tfidf_index *ix) {
   DeviceGuard g(ix->cfg.device);
   hipStreamSynchronize(ix->stream);
   hipStreamSynchronize(ix->copy_stream);
-  DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->d_live_map, &ix->dict, &ix->csr, &ix->csr_esc, &ix->doc_len,
-                    &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->long_list, &ix->uni_list, &ix->counters, &ix->blk,
-                    &ix->retry_list, &ix->bad_list, &ix->bbase, &ix->post, &ix->post_tmp, &ix->post_esc, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->lt_pos, &ix->verify_defer, &ix->pairs, &ix->pair_ub, &ix->chunk_list, &ix->chunk_docs, &ix->chunk_fail, &ix->uchunk, &ix->canon_of_slot,
-                    &ix->q_off, &ix->q_slot, &ix->q_w, &ix->q_role, &ix->q_meta, &ix->cache, &ix->cand, &ix->cand_n, &ix->out_doc,
-                    &ix->out_score, &ix->out_n, &ix->q_in, &ix->q_out, &ix->hits, &ix->hits_n, &ix->hits_c, &ix->hits_s, &ix->hits_P, &ix->sort_tmp,
-                    &ix->row_off, &ix->tvals, &ix->toff, &ix->tdf, &ix->term_tmp, &ix->term_esc, &ix->sent_slot, &ix->vcounts, &ix->vnu,
-                    &ix->vt_table, &ix->vt_sum, &ix->vt_rslot, &ix->gdf_dev, &ix->ovf};
+  ix->cur.reset();
+  ix->spare.reset();
+  ix->ctx_free.clear();
+  ix->text.reset();
+  ix->offsets.reset();
+  DevBuf *bufs[] = {&ix->d_live_map, &ix->long_list, &ix->uni_list, &ix->counters, &ix->retry_list, &ix->bad_list,
+                    &ix->post_tmp, &ix->lt_keys, &ix->lt_cnt, &ix->lt_g, &ix->lt_pos, &ix->verify_defer, &ix->pairs,
+                    &ix->pair_ub, &ix->chunk_list, &ix->chunk_docs, &ix->chunk_fail, &ix->uchunk, &ix->canon_of_slot,
+                    &ix->tvals, &ix->term_tmp, &ix->term_esc, &ix->sent_slot, &ix->vcounts, &ix->vnu, &ix->vt_table,
+                    &ix->vt_sum, &ix->vt_rslot, &ix->gdf_dev};
   for (DevBuf *b : bufs) b->release();
   for (int i = 0; i < EV_N; i++) hipEventDestroy(ix->ev[i]);
-  if (ix->q_in_ev) hipEventDestroy(ix->q_in_ev);
-  for (int i = 0; i < 2; i++) hipEventDestroy(ix->q_ev[i]);
   for (int i = 0; i < 2; i++) {
     if (ix->stage[i]) hipHostFree(ix->stage[i]);
     hipEventDestroy(ix->stage_ev[i]);
   }
   for (int i = 0; i < 2; i++) hipEventDestroy(ix->mir_ev[i]);
-  hipEventDestroy(ix->gdf_ev);
   hipStreamSynchronize(ix->own_stream);
   hipStreamDestroy(ix->copy_stream);
   hipStreamDestroy(ix->own_stream);
@@ -329,49 +525,33 @@ extern "C" int tfidf_destroy(tfidf_index *ix) {
   return TFIDF_OK;
 }
 
-// GLOBAL df host mirror: wait for its asynchronous copy before the first use
-static int wait_gdf(tfidf_index *ix) {
-  if (ix->gdf_pending) {
-    HIP_TRY(hipEventSynchronize(ix->gdf_ev));
-    ix->gdf_pending = false;
-  }
+// grow a device buffer shared with published snapshots: a new buffer with the
+// first `keep` bytes copied (the snapshots keep the old one alive)
+static int grow_shared(tfidf_index *ix, std::shared_ptr<DevMem> *buf, uint64_t need, uint64_t keep, bool zero) {
+  if (need <= (*buf)->bytes) return TFIDF_OK;
+  uint64_t cap = (*buf)->bytes ? (*buf)->bytes : (1ull << 20);
+  while (cap < need) cap = cap + cap / 2 + (1ull << 20);
+  auto nb = std::make_shared<DevMem>(ix->cfg.device);
+  HIP_TRY(nb->reserve(cap));
+  if (zero) HIP_TRY(hipMemsetAsync(nb->p, 0, cap, ix->stream));
+  if ((*buf)->p && keep) HIP_TRY(hipMemcpyAsync(nb->p, (*buf)->p, keep, hipMemcpyDeviceToDevice, ix->stream));
+  HIP_TRY(hipStreamSynchronize(ix->stream));
+  *buf = std::move(nb);
   return TFIDF_OK;
 }
 
 // grow the device corpus to hold `extra` more bytes (plus read slack)
 static int grow_text(tfidf_index *ix, uint64_t extra) {
-  const uint64_t need = ix->text_bytes + extra + 128;
-  if (need <= ix->text.bytes) return TFIDF_OK;
-  uint64_t cap = ix->text.bytes ? ix->text.bytes : (1ull << 20);
-  while (cap < need) cap = cap + cap / 2 + (1ull << 20);
-  void *p = nullptr;
-  HIP_TRY(hipMalloc(&p, cap));
-  HIP_TRY(hipMemsetAsync(p, 0, cap, ix->stream));
-  if (ix->text.p && ix->text_bytes) HIP_TRY(hipMemcpyAsync(p, ix->text.p, ix->text_bytes, hipMemcpyDeviceToDevice, ix->stream));
-  HIP_TRY(hipStreamSynchronize(ix->stream));
-  ix->text.release();
-  ix->text.p = p;
-  ix->text.bytes = cap;
-  return TFIDF_OK;
+  return grow_shared(ix, &ix->text, ix->text_bytes + extra + 128, ix->text_bytes, true);
 }
 
 static int grow_offsets(tfidf_index *ix, uint64_t extra_docs) {
-  const uint64_t need = (ix->n_staged + extra_docs + 1) * 8;
-  if (need <= ix->offsets.bytes) return TFIDF_OK;
-  uint64_t cap = ix->offsets.bytes;
-  while (cap < need) cap = cap * 2 + 64;
-  void *p = nullptr;
-  HIP_TRY(hipMalloc(&p, cap));
-  HIP_TRY(hipMemcpyAsync(p, ix->offsets.p, (ix->n_staged + 1) * 8, hipMemcpyDeviceToDevice, ix->stream));
-  HIP_TRY(hipStreamSynchronize(ix->stream));
-  ix->offsets.release();
-  ix->offsets.p = p;
-  ix->offsets.bytes = cap;
-  return TFIDF_OK;
+  return grow_shared(ix, &ix->offsets, (ix->n_staged + extra_docs + 1) * 8, (ix->n_staged + 1) * 8, false);
 }
 
 static void register_key(tfidf_index *ix, const uint8_t *k, uint64_t n, bool synth) {
   const uint64_t idx = ix->n_staged;
+  KeyChunk &c = ix->keys.tail(idx);
   if (!synth) {
     std::string key((const char *)k, n);
     auto it = ix->key_to_staged.find(key);
@@ -381,10 +561,10 @@ static void register_key(tfidf_index *ix, const uint8_t *k, uint64_t n, bool syn
     } else {
       ix->key_to_staged.emplace(std::move(key), idx);
     }
-    ix->key_arena.append((const char *)k, n);
+    c.arena.append((const char *)k, n);
   }
-  ix->key_off.push_back(ix->key_arena.size());
-  ix->key_synth.push_back(synth ? 1 : 0);
+  c.off.push_back(c.arena.size());
+  c.synth.push_back(synth ? 1 : 0);
   ix->staged_live.push_back(1);
 }
 
@@ -441,17 +621,16 @@ extern "C" int tfidf_clear(tfidf_index *ix) {
   ix->text_bytes = 0;
   ix->n_staged = 0;
   ix->h_offsets.assign(1, 0);
-  ix->key_arena.clear();
-  ix->key_off.assign(1, 0);
-  ix->key_synth.clear();
+  ix->keys = KeyTable();
   ix->staged_live.clear();
   ix->key_to_staged.clear();
   ix->n_dead = 0;
-  ix->committed = false;
-  ix->n_docs = 0;
-  wait_gdf(ix);
-  ix->has_global = false;
-  ix->gdf.clear();
+  std::shared_ptr<Snapshot> old;
+  {
+    std::lock_guard<std::mutex> sl(ix->snap_mu);    // searches from now on: not committed
+    old = std::move(ix->cur);
+  }
+  if (!ix->spare) ix->spare = std::move(old);       // buffers for the next commit
   return TFIDF_OK;
 }
 
@@ -480,12 +659,13 @@ static uint64_t fnv1a(uint64_t h, const void *p, size_t n) {
   return h;
 }
 
-static uint64_t meta_hash(const tfidf_index *ix) {
+static uint64_t meta_hash(const tfidf_index *ix, const std::string &arena, const std::vector<uint64_t> &koff,
+                          const std::vector<uint8_t> &synth) {
   uint64_t h = 0xCBF29CE484222325ull;
   h = fnv1a(h, ix->h_offsets.data(), ix->h_offsets.size() * 8);
-  h = fnv1a(h, ix->key_off.data(), ix->key_off.size() * 8);
-  h = fnv1a(h, ix->key_arena.data(), ix->key_arena.size());
-  h = fnv1a(h, ix->key_synth.data(), ix->key_synth.size());
+  h = fnv1a(h, koff.data(), koff.size() * 8);
+  h = fnv1a(h, arena.data(), arena.size());
+  h = fnv1a(h, synth.data(), synth.size());
   h = fnv1a(h, ix->staged_live.data(), ix->staged_live.size());
   return h;
 }
@@ -495,6 +675,10 @@ extern "C" int tfidf_save(tfidf_index *ix, const char *path) {
   std::lock_guard<std::mutex> lk(ix->mu);
   DeviceGuard g(ix->cfg.device);
   HIP_TRY(hipStreamSynchronize(ix->stream));
+  std::string key_arena;
+  std::vector<uint64_t> key_off;
+  std::vector<uint8_t> key_synth;
+  ix->keys.flatten(&key_arena, &key_off, &key_synth);
   FileHeader h{};
   memcpy(h.magic, kFileMagic, 8);
   h.version = 1;
@@ -505,17 +689,17 @@ extern "C" int tfidf_save(tfidf_index *ix, const char *path) {
   h.vocab_capacity_log2 = ix->cap_log2;
   h.n_staged = ix->n_staged;
   h.text_bytes = ix->text_bytes;
-  h.key_bytes = ix->key_arena.size();
+  h.key_bytes = key_arena.size();
   h.n_dead = ix->n_dead;
-  h.meta_hash = meta_hash(ix);
+  h.meta_hash = meta_hash(ix, key_arena, key_off, key_synth);
   const std::string tmp = std::string(path) + ".tmp";
   FILE *f = fopen(tmp.c_str(), "wb");
   if (!f) return fail(TFIDF_E_INVALID_ARG, "cannot open %s for writing", tmp.c_str());
   bool ok = fwrite(&h, sizeof h, 1, f) == 1;
   ok = ok && fwrite(ix->h_offsets.data(), 8, ix->h_offsets.size(), f) == ix->h_offsets.size();
-  ok = ok && fwrite(ix->key_off.data(), 8, ix->key_off.size(), f) == ix->key_off.size();
-  ok = ok && (ix->key_arena.empty() || fwrite(ix->key_arena.data(), 1, ix->key_arena.size(), f) == ix->key_arena.size());
-  ok = ok && (ix->n_staged == 0 || fwrite(ix->key_synth.data(), 1, ix->n_staged, f) == ix->n_staged);
+  ok = ok && fwrite(key_off.data(), 8, key_off.size(), f) == key_off.size();
+  ok = ok && (key_arena.empty() || fwrite(key_arena.data(), 1, key_arena.size(), f) == key_arena.size());
+  ok = ok && (ix->n_staged == 0 || fwrite(key_synth.data(), 1, ix->n_staged, f) == ix->n_staged);
   ok = ok && (ix->n_staged == 0 || fwrite(ix->staged_live.data(), 1, ix->n_staged, f) == ix->n_staged);
   // corpus text: device -> pinned staging buffer -> file, chunk by chunk
   if (ok && ix->text_bytes) {
@@ -525,7 +709,7 @@ extern "C" int tfidf_save(tfidf_index *ix, const char *path) {
     if (!ix->stage[0]) { fclose(f); remove(tmp.c_str()); return fail(TFIDF_E_OOM, "pinned staging buffer"); }
     for (uint64_t off = 0; ok && off < ix->text_bytes; off += kStageBytes) {
       const size_t n = (size_t)std::min<uint64_t>(kStageBytes, ix->text_bytes - off);
-      if (hipMemcpy(ix->stage[0], ix->text.as<uint8_t>() + off, n, hipMemcpyDeviceToHost) != hipSuccess) {
+      if (hipMemcpy(ix->stage[0], ix->text->as<uint8_t>() + off, n, hipMemcpyDeviceToHost) != hipSuccess) {
         fclose(f);
         remove(tmp.c_str());
         return fail(TFIDF_E_HIP, "copy of the corpus from the device failed");
@@ -583,9 +767,13 @@ extern "C" int tfidf_load(tfidf_index *ix, const char *path) {
   int rc = tfidf_add_docs(ix, n ? text.data() : nullptr, offs.data(), n, nullptr, nullptr);
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(ix->mu);
-  ix->key_arena = arena;
-  ix->key_off.assign(koff.begin(), koff.end());
-  ix->key_synth = synth;
+  {
+    auto one = std::make_shared<KeyChunk>();
+    one->arena = arena;
+    one->off.assign(koff.begin(), koff.end());
+    one->synth = synth;
+    ix->keys.ch.assign(1, one);
+  }
   ix->staged_live = live;
   ix->key_to_staged.clear();
   ix->n_dead = 0;
@@ -593,8 +781,7 @@ extern "C" int tfidf_load(tfidf_index *ix, const char *path) {
     if (!live[i]) { ix->n_dead++; continue; }
     if (!synth[i]) ix->key_to_staged[std::string(arena, koff[i], koff[i + 1] - koff[i])] = i;
   }
-  if (ix->n_dead != h.n_dead || meta_hash(ix) != h.meta_hash) {
-    ix->committed = false;
+  if (ix->n_dead != h.n_dead || meta_hash(ix, arena, koff, synth) != h.meta_hash) {
     return fail(TFIDF_E_INVALID_ARG, "%s: metadata checksum mismatch", path);
   }
   return TFIDF_OK;
@@ -614,11 +801,11 @@ extern "C" int tfidf_add_docs(tfidf_index *ix, const uint8_t *utf8, const uint64
   if (rc) return rc;
   rc = grow_offsets(ix, n_docs);
   if (rc) return rc;
-  if (nbytes) HIP_TRY(h2d_staged(ix, ix->text.as<uint8_t>() + ix->text_bytes, utf8 + offsets[0], nbytes));
+  if (nbytes) HIP_TRY(h2d_staged(ix, ix->text->as<uint8_t>() + ix->text_bytes, utf8 + offsets[0], nbytes));
   std::vector<uint64_t> no(n_docs);
   for (uint64_t i = 0; i < n_docs; i++) no[i] = ix->text_bytes + (offsets[i + 1] - offsets[0]);
   if (n_docs)
-    HIP_TRY(hipMemcpyAsync(ix->offsets.as<uint64_t>() + ix->n_staged + 1, no.data(), n_docs * 8,
+    HIP_TRY(hipMemcpyAsync(ix->offsets->as<uint64_t>() + ix->n_staged + 1, no.data(), n_docs * 8,
                            hipMemcpyHostToDevice, ix->stream));
   HIP_TRY(hipStreamSynchronize(ix->stream));
   for (uint64_t i = 0; i < n_docs; i++) {
@@ -627,8 +814,7 @@ extern "C" int tfidf_add_docs(tfidf_index *ix, const uint8_t *utf8, const uint64
     ix->h_offsets.push_back(no[i]);
     ix->n_staged++;
   }
-  ix->text_bytes += nbytes;
-  ix->committed = false;
+  ix->text_bytes += nbytes;                 // searches keep the last commit's snapshot
   return TFIDF_OK;
 }
 
@@ -646,9 +832,9 @@ extern "C" int tfidf_add_docs_device(tfidf_index *ix, const void *d_utf8, const 
   rc = grow_offsets(ix, n_docs);
   if (rc) return rc;
   if (total_bytes)
-    HIP_TRY(hipMemcpyAsync(ix->text.as<uint8_t>() + ix->text_bytes, (const uint8_t *)d_utf8 + ho[0], total_bytes,
+    HIP_TRY(hipMemcpyAsync(ix->text->as<uint8_t>() + ix->text_bytes, (const uint8_t *)d_utf8 + ho[0], total_bytes,
                            hipMemcpyDeviceToDevice, ix->stream));
-  uint64_t *dst = ix->offsets.as<uint64_t>() + ix->n_staged + 1;
+  uint64_t *dst = ix->offsets->as<uint64_t>() + ix->n_staged + 1;
   HIP_TRY(hipMemcpyAsync(dst, (const uint64_t *)d_offsets + 1, n_docs * 8, hipMemcpyDeviceToDevice, ix->stream));
   HIP_TRY(add_u64(dst, n_docs, ix->text_bytes - ho[0], ix->stream));
   HIP_TRY(hipStreamSynchronize(ix->stream));
@@ -658,7 +844,6 @@ extern "C" int tfidf_add_docs_device(tfidf_index *ix, const void *d_utf8, const 
     ix->n_staged++;
   }
   ix->text_bytes += total_bytes;
-  ix->committed = false;
   return TFIDF_OK;
 }
 
@@ -680,89 +865,100 @@ static float bm25_idf(uint64_t df, uint64_t doc_count) {
   return (float)log(1.0 + x);
 }
 
-static uint64_t eff_doc_count(const tfidf_index *ix) { return ix->has_global ? ix->g_doc_count : ix->doc_count; }
-static uint64_t eff_sum_ttf(const tfidf_index *ix) { return ix->has_global ? ix->g_sum_ttf : ix->sum_ttf; }
-
-static int upload_cache(tfidf_index *ix, bool sync = true) {
-  HIP_TRY(ix->h_cache.resize(256));
+// BM25 norm cache of a statistics view (not yet visible to searches, or
+// owned by the writer), uploaded on stream s
+static int upload_cache(const tfidf_config &cfg, StatsView &v, hipStream_t s, bool sync = true) {
+  HIP_TRY(v.h_cache.resize(256));
   // the previous upload from the staging array must be done before it is rewritten
-  HIP_TRY(hipStreamSynchronize(ix->stream));
-  float *c = ix->h_cache.data();
-  const uint64_t dc = eff_doc_count(ix);
-  if (dc == 0) {
+  HIP_TRY(hipStreamSynchronize(s));
+  float *c = v.h_cache.data();
+  if (v.doc_count == 0) {
     for (int i = 0; i < 256; i++) c[i] = 0.0f;
   } else {
-    const float avgdl = (float)((double)eff_sum_ttf(ix) / (double)dc);
-    norm_cache(ix->cfg.k1, ix->cfg.b, avgdl, c);
+    const float avgdl = (float)((double)v.sum_ttf / (double)v.doc_count);
+    norm_cache(cfg.k1, cfg.b, avgdl, c);
   }
-  HIP_TRY(ix->cache.reserve(256 * 4));
-  HIP_TRY(hipMemcpyAsync(ix->cache.p, c, 256 * 4, hipMemcpyHostToDevice, ix->stream));
-  if (sync) HIP_TRY(hipStreamSynchronize(ix->stream));
+  HIP_TRY(v.cache.reserve(256 * 4));
+  HIP_TRY(hipMemcpyAsync(v.cache.p, c, 256 * 4, hipMemcpyHostToDevice, s));
+  if (sync) HIP_TRY(hipStreamSynchronize(s));
   return TFIDF_OK;
 }
 
 static float ev_ms(tfidf_index *ix, int a, int b) {
   float ms = 0;
-  if (a >= EV_Q0 && !ix->q_timing) return -1.0f;   // query timing off: not measured
   hipEventElapsedTime(&ms, ix->ev[a], ix->ev[b]);
   return ms;
+}
+
+static float qev_ms(const SearchCtx &c, int a, int b) {
+  float ms = 0;
+  if (!c.q_timing) return -1.0f;                   // query timing off: not measured
+  hipEventElapsedTime(&ms, c.ev[a], c.ev[b]);
+  return ms;
+}
+
+static void set_last_ms(tfidf_index *ix, float scoring, float total) {
+  std::lock_guard<std::mutex> lk(ix->ms_mu);
+  ix->last_ms_scoring = scoring;
+  ix->last_ms_total = total;
 }
 
 // One index build with ix->hash_seed; kRcCollision when two different terms
 // met under one hashed key (tfidf_commit then rebuilds with another seed).
 constexpr int kRcCollision = -1000;
+constexpr int kRcNoPublish = -1001;             // TFIDF_DEBUG_STOP (profiling): the rows are incomplete
 constexpr uint32_t kVerifyCap = 1u << 20;      // deferred hashed-key checks per build
-static int commit_once(tfidf_index *ix) {
+static int commit_once(tfidf_index *ix, Snapshot &S) {
   hipStream_t s = ix->stream;
   // live documents
-  ix->n_docs = ix->n_staged - ix->n_dead;
-  ix->live_map.clear();
+  S.n_docs = ix->n_staged - ix->n_dead;
+  S.live_map.clear();
   if (ix->n_dead) {
-    ix->live_map.reserve(ix->n_docs);
+    S.live_map.reserve(S.n_docs);
     for (uint64_t i = 0; i < ix->n_staged; i++)
-      if (ix->staged_live[i]) ix->live_map.push_back((uint32_t)i);
-    HIP_TRY(ix->d_live_map.reserve(ix->n_docs * 4 + 4));
-    HIP_TRY(hipMemcpyAsync(ix->d_live_map.p, ix->live_map.data(), ix->n_docs * 4, hipMemcpyHostToDevice, s));
+      if (ix->staged_live[i]) S.live_map.push_back((uint32_t)i);
+    HIP_TRY(ix->d_live_map.reserve(S.n_docs * 4 + 4));
+    HIP_TRY(hipMemcpyAsync(ix->d_live_map.p, S.live_map.data(), S.n_docs * 4, hipMemcpyHostToDevice, s));
   }
-  const uint64_t N = ix->n_docs;
-  ix->C = 1u << ix->cap_log2;
-  const uint32_t C = ix->C;
-  ix->n_blocks = (uint32_t)((N + kBlockDocs - 1) / kBlockDocs);
+  const uint64_t N = S.n_docs;
+  S.C = 1u << ix->cap_log2;
+  const uint32_t C = S.C;
+  S.n_blocks = (uint32_t)((N + kBlockDocs - 1) / kBlockDocs);
   const uint64_t row_cap = (ix->text_bytes + ix->n_staged) / 2 + 2;
   // Inversion layout: block-major needs a dense (blocks + 1) x C count table;
   // when that outgrows the CSR itself (huge vocabularies, SURVEY §8 cfg 5) the
   // postings are built term-major by a sort instead (kernels_term.hip).
   {
-    const uint64_t blk_bytes = (uint64_t)(ix->n_blocks + 1) * C * 4;
-    if (ix->cfg.inversion == TFIDF_INVERSION_TERM) ix->term_major = true;
-    else if (ix->cfg.inversion == TFIDF_INVERSION_BLOCK) ix->term_major = false;
+    const uint64_t blk_bytes = (uint64_t)(S.n_blocks + 1) * C * 4;
+    if (ix->cfg.inversion == TFIDF_INVERSION_TERM) S.term_major = true;
+    else if (ix->cfg.inversion == TFIDF_INVERSION_BLOCK) S.term_major = false;
     else {
       // Few (block, range) tiles of very long documents (a few hundred books,
       // SURVEY cfg 1): the block-major passes run one workgroup per tile and
       // starve; the sort-based term-major build is parallel in the postings.
-      const uint64_t tiles = (uint64_t)ix->n_blocks * (C < kRangeSlots ? 1u : C / kRangeSlots);
+      const uint64_t tiles = (uint64_t)S.n_blocks * (C < kRangeSlots ? 1u : C / kRangeSlots);
       const bool starved = tiles < ix->num_cus && ix->n_staged && ix->text_bytes / ix->n_staged >= (64u << 10);
-      ix->term_major = ix->cap_log2 > kMaxBlockCapLog2 || (blk_bytes > (1ull << 31) && blk_bytes > row_cap * 4) ||
+      S.term_major = ix->cap_log2 > kMaxBlockCapLog2 || (blk_bytes > (1ull << 31) && blk_bytes > row_cap * 4) ||
                        starved;
     }
   }
   // CSR rows are grouped by dictionary range for the block-major passes only
-  const uint32_t RS = ix->term_major ? C : (C < kRangeSlots ? C : kRangeSlots);
-  ix->range_shift = 0;
-  while ((1u << ix->range_shift) < RS) ix->range_shift++;
-  ix->R = C >> ix->range_shift;
+  const uint32_t RS = S.term_major ? C : (C < kRangeSlots ? C : kRangeSlots);
+  S.range_shift = 0;
+  while ((1u << S.range_shift) < RS) S.range_shift++;
+  S.R = C >> S.range_shift;
 
-  HIP_TRY(ix->dict.reserve((size_t)3 * C * 8));          // lo, hi, reference occurrence (dict_device.h)
+  HIP_TRY(S.dict.reserve((size_t)3 * C * 8));          // lo, hi, reference occurrence (dict_device.h)
   HIP_TRY(ix->verify_defer.reserve((size_t)kVerifyCap * 16));
-  HIP_TRY(ix->csr.reserve(row_cap * 4));
+  HIP_TRY(S.csr.reserve(row_cap * 4));
   // escapes: each needs tf >= the field's escape value, and a row holds at
   // most row_cap tokens in all, so this bounds their number
-  const uint64_t esc_cap = row_cap / csr_esc_value(ix->range_shift) + 64;
-  HIP_TRY(ix->csr_esc.reserve(esc_cap * 8));
-  HIP_TRY(ix->doc_len.reserve(N * 4 + 4));
-  HIP_TRY(ix->doc_nuniq.reserve(N * 4 + 4));
-  HIP_TRY(ix->doc_norm.reserve(N + 16));
-  HIP_TRY(ix->rsplit.reserve(N * ix->R * 4 + 4));
+  const uint64_t esc_cap = row_cap / csr_esc_value(S.range_shift) + 64;
+  HIP_TRY(S.csr_esc.reserve(esc_cap * 8));
+  HIP_TRY(S.doc_len.reserve(N * 4 + 4));
+  HIP_TRY(S.doc_nuniq.reserve(N * 4 + 4));
+  HIP_TRY(S.doc_norm.reserve(N + 16));
+  HIP_TRY(S.rsplit.reserve(N * S.R * 4 + 4));
   HIP_TRY(ix->long_list.reserve(N * 4 + 4));
   HIP_TRY(ix->uni_list.reserve(N * 4 + 4));
   HIP_TRY(ix->counters.reserve(128));
@@ -775,16 +971,16 @@ static int commit_once(tfidf_index *ix) {
     const uint64_t avg = ix->n_staged ? ix->text_bytes / ix->n_staged : 0;
     if (avg) pack = (uint32_t)std::min<uint64_t>(kPackMaxDocs, std::max<uint64_t>(1, kPackBytes / avg));
     if (const char *e = getenv("TFIDF_PACK_DOCS")) pack = (uint32_t)std::max(1, std::min(atoi(e), (int)kPackMaxDocs));
-    pack = std::min(pack, std::max(1u, kWaveGroups / ix->R));   // (document, range) groups per unit
+    pack = std::min(pack, std::max(1u, kWaveGroups / S.R));   // (document, range) groups per unit
   }
   if (pack > 1) HIP_TRY(ix->retry_list.reserve(N * 4 + 4));
-  if (ix->term_major) {
-    HIP_TRY(ix->row_off.reserve(N * 4 + 4));
-    HIP_TRY(ix->toff.reserve(((size_t)C + 1) * 8));
-    HIP_TRY(ix->tdf.reserve((size_t)C * 4));
+  if (S.term_major) {
+    HIP_TRY(S.row_off.reserve(N * 4 + 4));
+    HIP_TRY(S.toff.reserve(((size_t)C + 1) * 8));
+    HIP_TRY(S.tdf.reserve((size_t)C * 4));
   } else {
-    HIP_TRY(ix->blk.reserve((size_t)(ix->n_blocks + 1) * C * 4));
-    HIP_TRY(ix->bbase.reserve((size_t)(ix->n_blocks + 2) * 8));
+    HIP_TRY(S.blk.reserve((size_t)(S.n_blocks + 1) * C * 4));
+    HIP_TRY(S.bbase.reserve((size_t)(S.n_blocks + 2) * 8));
   }
 
   // counters: [0..2] stats u64, [3] err flags u32 + [3].hi first doc, [4] long_count, [5] retry_count,
@@ -792,30 +988,30 @@ static int commit_once(tfidf_index *ix) {
   // escapes, [11] deferred hashed-key checks, [12] term-major tf escapes
   uint64_t *ctr = ix->counters.as<uint64_t>();
   HIP_TRY(hipMemsetAsync(ix->counters.p, 0, 128, s));
-  HIP_TRY(hipMemsetAsync(ix->dict.p, 0, (size_t)3 * C * 8, s));
+  HIP_TRY(hipMemsetAsync(S.dict.p, 0, (size_t)3 * C * 8, s));
   HIP_TRY(hipMemsetAsync(ix->uni_list.p, 0, (size_t)N * 4, s));          // per-document Unicode flags
 
   BuildParams bp{};
-  bp.text = ix->text.as<uint8_t>();
-  bp.offsets = ix->offsets.as<uint64_t>();
+  bp.text = ix->text->as<uint8_t>();
+  bp.offsets = ix->offsets->as<uint64_t>();
   bp.live_map = ix->n_dead ? ix->d_live_map.as<uint32_t>() : nullptr;
   bp.n_docs = N;
-  bp.dict = ix->dict.as<uint64_t>();
+  bp.dict = S.dict.as<uint64_t>();
   bp.cap_mask = C - 1;
-  bp.range_shift = ix->range_shift;
-  bp.n_ranges = ix->R;
+  bp.range_shift = S.range_shift;
+  bp.n_ranges = S.R;
   bp.hash_seed = ix->hash_seed;
   bp.verify_defer = ix->verify_defer.as<uint64_t>();
   bp.verify_count = reinterpret_cast<uint32_t *>(ctr + 11);
   bp.verify_cap = kVerifyCap;
-  bp.csr = ix->csr.as<uint32_t>();
-  bp.csr_esc = ix->csr_esc.as<uint64_t>();
+  bp.csr = S.csr.as<uint32_t>();
+  bp.csr_esc = S.csr_esc.as<uint64_t>();
   bp.esc_count = reinterpret_cast<uint32_t *>(ctr + 9);
   bp.esc_cap = esc_cap;
-  bp.doc_len = ix->doc_len.as<uint32_t>();
-  bp.doc_nuniq = ix->doc_nuniq.as<uint32_t>();
-  bp.doc_norm = ix->doc_norm.as<uint8_t>();
-  bp.rsplit = ix->rsplit.as<uint32_t>();
+  bp.doc_len = S.doc_len.as<uint32_t>();
+  bp.doc_nuniq = S.doc_nuniq.as<uint32_t>();
+  bp.doc_norm = S.doc_norm.as<uint8_t>();
+  bp.rsplit = S.rsplit.as<uint32_t>();
   bp.long_list = ix->long_list.as<uint32_t>();
   bp.long_count = reinterpret_cast<uint32_t *>(ctr + 4);
   bp.uni_list = ix->uni_list.as<uint32_t>();
@@ -828,8 +1024,8 @@ static int commit_once(tfidf_index *ix) {
   bp.pack = pack;
   bp.retry_list = pack > 1 ? ix->retry_list.as<uint32_t>() : nullptr;
   bp.retry_count = reinterpret_cast<uint32_t *>(ctr + 5);
-  ix->pack_docs = pack;
-  ix->pack_retried = 0;
+  S.pack_docs = pack;
+  S.pack_retried = 0;
 
   HIP_TRY(hipEventRecord(ix->ev[EV_START], s));
   if (N) {
@@ -842,7 +1038,7 @@ static int commit_once(tfidf_index *ix) {
       uint32_t n_retry = 0;
       HIP_TRY(hipMemcpyAsync(&n_retry, ctr + 5, 4, hipMemcpyDeviceToHost, s));
       HIP_TRY(hipStreamSynchronize(s));
-      ix->pack_retried = n_retry;
+      S.pack_retried = n_retry;
       if (n_retry) {
         BuildParams rp = bp;
         rp.pack = 1;
@@ -864,8 +1060,7 @@ static int commit_once(tfidf_index *ix) {
     ix->timing.ms_total = ix->timing.ms_tokenize;
     ix->timing.text_bytes = ix->text_bytes;
     ix->timing.num_docs = N;
-    ix->committed = false;
-    return TFIDF_OK;
+    return kRcNoPublish;
   }
   // one read of the counters: stats (0-2), error flags (3), long (4) and
   // non-ASCII (6) document counts, CSR escapes (9) (32-bit counters in the low
@@ -875,9 +1070,9 @@ static int commit_once(tfidf_index *ix) {
   HIP_TRY(hipMemcpyAsync(hctr, ctr, 10 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   const uint32_t n_long = (uint32_t)hctr[4], n_uni = (uint32_t)hctr[6];
-  ix->long_chunked = 0;
-  ix->long_docs = n_long;
-  ix->unicode_docs = n_uni;
+  S.long_chunked = 0;
+  S.long_docs = n_long;
+  S.unicode_docs = n_uni;
   if (n_long) {
     HIP_TRY(hipEventRecord(ix->ev[EV_L0], s));
     // book-sized documents: chunk-parallel (k_tokenize_chunk + k_long_rows),
@@ -899,7 +1094,7 @@ static int commit_once(tfidf_index *ix) {
     std::vector<uint64_t> gpre, gdoc;               // each group's prefix array offset and first document
     uint64_t acc = 0, max_units = 0;
     for (uint64_t i = 0; i < n_long; i++) {
-      const uint64_t st = ix->live_map.empty() ? ldocs[i] : ix->live_map[ldocs[i]];
+      const uint64_t st = S.live_map.empty() ? ldocs[i] : S.live_map[ldocs[i]];
       const uint64_t L = ix->h_offsets[st + 1] - ix->h_offsets[st];
       const uint64_t units = (L + kLongCoreBytes - 1) / kLongCoreBytes;
       if (i == 0 || acc + units > unit_max) {
@@ -954,7 +1149,7 @@ static int commit_once(tfidf_index *ix) {
     uint32_t n_fb = 0;
     HIP_TRY(hipMemcpyAsync(&n_fb, bp.long_count, 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    ix->long_chunked = n_long - n_fb;
+    S.long_chunked = n_long - n_fb;
     if (n_fb) {
       uint32_t lg = ix->cap_log2 + 1;
       // table size needed by the longest long document (2x its token bound)
@@ -987,36 +1182,35 @@ static int commit_once(tfidf_index *ix) {
   const uint32_t err = (uint32_t)(hctr[3] & 0xFFFFFFFFu), err_doc = (uint32_t)(hctr[3] >> 32);
   if (err & kErrCollision) { ix->collision_doc = err_doc; return kRcCollision; }
   if (err) {
-    ix->committed = false;
     if (err & kErrCapacity)
       return fail(TFIDF_E_CAPACITY, "vocabulary exceeds 2^%u dictionary slots (raise vocab_capacity_log2)",
                   ix->cap_log2);
     return fail(TFIDF_E_UNSUPPORTED_INPUT, "index build error flags 0x%x (doc %u)", err, err_doc);
   }
-  ix->doc_count = hctr[0];
-  ix->sum_ttf = hctr[1];
-  ix->nnz = hctr[2];
+  S.doc_count = hctr[0];
+  S.sum_ttf = hctr[1];
+  S.nnz = hctr[2];
   // CSR tf escapes (rare: block-major only for tf >= 2^17): sorted by entry
   // index for the binary searches of the inversion and tfidf_doc_terms
   {
     const uint64_t n_esc = (uint32_t)hctr[9];
     if (n_esc > esc_cap) return fail(TFIDF_E_CAPACITY, "CSR escape list overflow");
-    ix->h_esc.resize(n_esc);
+    S.h_esc.resize(n_esc);
     if (n_esc) {
-      HIP_TRY(hipMemcpyAsync(ix->h_esc.data(), ix->csr_esc.p, n_esc * 8, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipMemcpyAsync(S.h_esc.data(), S.csr_esc.p, n_esc * 8, hipMemcpyDeviceToHost, s));
       HIP_TRY(hipStreamSynchronize(s));
-      std::sort(ix->h_esc.begin(), ix->h_esc.end());
-      HIP_TRY(hipMemcpyAsync(ix->csr_esc.p, ix->h_esc.data(), n_esc * 8, hipMemcpyHostToDevice, s));
+      std::sort(S.h_esc.begin(), S.h_esc.end());
+      HIP_TRY(hipMemcpyAsync(S.csr_esc.p, S.h_esc.data(), n_esc * 8, hipMemcpyHostToDevice, s));
       HIP_TRY(hipStreamSynchronize(s));
     }
   }
-  if (ix->nnz >= 0xFFFFFFFFull) return fail(TFIDF_E_CAPACITY, "more than 2^32 postings per shard");
+  if (S.nnz >= 0xFFFFFFFFull) return fail(TFIDF_E_CAPACITY, "more than 2^32 postings per shard");
   // postings: block-major u32 (post_word), term-major u64; pass-1 temp words u32
   // (term-major: the sort's u64 value buffer)
-  HIP_TRY(ix->post.reserve(ix->nnz * (ix->term_major ? 8 : 4) + 8));
-  HIP_TRY(ix->post_tmp.reserve(ix->nnz * (ix->term_major ? 8 : 4) + 8));
+  HIP_TRY(S.post.reserve(S.nnz * (S.term_major ? 8 : 4) + 8));
+  HIP_TRY(ix->post_tmp.reserve(S.nnz * (S.term_major ? 8 : 4) + 8));
   const uint64_t post_esc_cap = row_cap / kPostTfEsc + 64;       // each needs tf >= 2047 tokens of one doc
-  if (!ix->term_major) HIP_TRY(ix->post_esc.reserve(post_esc_cap * 8));
+  if (!S.term_major) HIP_TRY(S.post_esc.reserve(post_esc_cap * 8));
 
   // the dictionary is final here (wave, Unicode and long paths done): its host
   // mirror, the deferred identity checks and the occupied-slot count run on the
@@ -1024,8 +1218,8 @@ static int commit_once(tfidf_index *ix) {
   // ms per build; cfg 2: the 4 MB mirror, the checks and the count left ~0.2 ms
   // of copies, kernels and launch gaps after the inversion).  TFIDF_MIRROR_MAIN=1
   // keeps a mirror below 32 MB on the main stream after the inversion (A/B).
-  HIP_TRY(ix->h_dict.resize((size_t)2 * C));
-  HIP_TRY(ix->h_df.resize(C));
+  HIP_TRY(S.h_dict.resize((size_t)2 * C));
+  HIP_TRY(S.h_df.resize(C));
   // On a caller's stream (tfidf_set_stream: torch's stream under torch.distributed)
   // the small mirror stays on the main stream: the cross-stream hand-off cost the
   // one-rank RCCL rehearsal ~1 ms per step (tools/ab_dist3.sh: 12.4-12.8 vs 11.4-11.6)
@@ -1040,33 +1234,33 @@ static int commit_once(tfidf_index *ix) {
   pp.live_map = bp.live_map;
   pp.n_docs = N;
   pp.C = C;
-  pp.range_shift = ix->range_shift;
-  pp.n_ranges = ix->R;
-  pp.n_blocks = ix->n_blocks;
+  pp.range_shift = S.range_shift;
+  pp.n_ranges = S.R;
+  pp.n_blocks = S.n_blocks;
   pp.csr = bp.csr;
   pp.csr_esc = bp.csr_esc;
-  pp.n_esc = ix->h_esc.size();
+  pp.n_esc = S.h_esc.size();
   pp.rsplit = bp.rsplit;
   pp.doc_norm = bp.doc_norm;
-  pp.blk = ix->blk.as<uint32_t>();
-  pp.bbase = ix->bbase.as<uint64_t>();
-  pp.post = ix->post.as<uint32_t>();
+  pp.blk = S.blk.as<uint32_t>();
+  pp.bbase = S.bbase.as<uint64_t>();
+  pp.post = S.post.as<uint32_t>();
   pp.post_tmp = ix->post_tmp.as<uint32_t>();
-  pp.post_esc = ix->post_esc.as<uint64_t>();
+  pp.post_esc = S.post_esc.as<uint64_t>();
   pp.post_esc_count = reinterpret_cast<uint32_t *>(ctr + 10);
   pp.post_esc_cap = post_esc_cap;
   pp.sort_spw = 4;
   if (const char *e = getenv("TFIDF_SORT_SPW")) pp.sort_spw = (uint32_t)std::max(1, atoi(e));   // A/B only
   pp.err = bp.err;
   HIP_TRY(hipEventRecord(ix->ev[EV_D0], s));
-  if (ix->term_major) {
+  if (S.term_major) {
     TermParams tp{};
     if (N > kTermMaxDocs)
       return fail(TFIDF_E_CAPACITY, "the term-major layout holds at most 2^26 documents per shard");
     tp.offsets = bp.offsets;
     tp.live_map = bp.live_map;
     tp.n_docs = N;
-    tp.nnz = ix->nnz;
+    tp.nnz = S.nnz;
     tp.C = C;
     tp.slot_bits = ix->cap_log2;
     tp.doc_bits = 1;
@@ -1078,22 +1272,22 @@ static int commit_once(tfidf_index *ix) {
       tp.tf_bits = std::max(1u, std::min(tp.tf_bits, (uint32_t)atoi(e)));
     tp.csr = bp.csr;
     tp.csr_esc = bp.csr_esc;
-    tp.n_esc = ix->h_esc.size();
+    tp.n_esc = S.h_esc.size();
     tp.doc_nuniq = bp.doc_nuniq;
     tp.doc_norm = bp.doc_norm;
-    tp.row_off = ix->row_off.as<uint32_t>();
-    HIP_TRY(ix->tvals.reserve(ix->nnz * 8 + 16));
+    tp.row_off = S.row_off.as<uint32_t>();
+    HIP_TRY(ix->tvals.reserve(S.nnz * 8 + 16));
     tp.keys = ix->post_tmp.as<uint64_t>();
     tp.keys_alt = ix->tvals.as<uint64_t>();
-    tp.post = ix->post.as<uint64_t>();
-    tp.toff = ix->toff.as<uint64_t>();
-    tp.df = ix->tdf.as<uint32_t>();
+    tp.post = S.post.as<uint64_t>();
+    tp.toff = S.toff.as<uint64_t>();
+    tp.df = S.tdf.as<uint32_t>();
     tp.err = bp.err;
     tp.tesc_cap = row_cap / ((1u << tp.tf_bits) - 1) + 64;   // each needs tf >= the escape value
     HIP_TRY(ix->term_esc.reserve(tp.tesc_cap * 16));
     tp.tesc = ix->term_esc.as<uint64_t>();
     tp.tesc_count = reinterpret_cast<uint32_t *>(ctr + 12);
-    HIP_TRY(ix->term_tmp.reserve(term_invert_scratch_words(N, ix->nnz, C) * 4));
+    HIP_TRY(ix->term_tmp.reserve(term_invert_scratch_words(N, S.nnz, C) * 4));
     tp.scratch = ix->term_tmp.as<uint32_t>();
     // the whole inversion is reported under ms_scatter
     HIP_TRY(hipEventRecord(ix->ev[EV_DF], s));
@@ -1116,32 +1310,32 @@ static int commit_once(tfidf_index *ix) {
     HIP_TRY(launch_term_sort(tp, s));
     HIP_TRY(hipEventRecord(ix->ev[EV_SCAT], s));
   } else {
-    if (ix->n_blocks) {
+    if (S.n_blocks) {
       HIP_TRY(launch_df_partial(pp, s));
     } else {
-      HIP_TRY(hipMemsetAsync(ix->blk.p, 0, (size_t)C * 4, s));
+      HIP_TRY(hipMemsetAsync(S.blk.p, 0, (size_t)C * 4, s));
     }
     HIP_TRY(hipEventRecord(ix->ev[EV_DF], s));
     HIP_TRY(launch_df_sum(pp, s));
-    if (ix->n_blocks) HIP_TRY(launch_row_scan(pp, s));
+    if (S.n_blocks) HIP_TRY(launch_row_scan(pp, s));
     HIP_TRY(hipEventRecord(ix->ev[EV_BSCAN], s));
     HIP_TRY(launch_block_base(pp, s));
     HIP_TRY(hipEventRecord(ix->ev[EV_CSCAN], s));
-    if (ix->n_blocks) HIP_TRY(launch_scatter(pp, s));
+    if (S.n_blocks) HIP_TRY(launch_scatter(pp, s));
     HIP_TRY(hipEventRecord(ix->ev[EV_SCAT], s));
   }
   if (mirror_side) {
     HIP_TRY(hipStreamWaitEvent(ix->copy_stream, ix->mir_ev[0], 0));
-    HIP_TRY(hipMemcpyAsync(ix->h_dict.data(), ix->dict.p, (size_t)2 * C * 8, hipMemcpyDeviceToHost, ix->copy_stream));
+    HIP_TRY(hipMemcpyAsync(S.h_dict.data(), S.dict.p, (size_t)2 * C * 8, hipMemcpyDeviceToHost, ix->copy_stream));
     HIP_TRY(launch_verify_deferred(bp, ix->copy_stream));
-    HIP_TRY(launch_count_nonzero(ix->dict.as<uint64_t>(), C, reinterpret_cast<unsigned long long *>(ctr + 7),
+    HIP_TRY(launch_count_nonzero(S.dict.as<uint64_t>(), C, reinterpret_cast<unsigned long long *>(ctr + 7),
                                  ix->copy_stream));
     HIP_TRY(hipEventRecord(ix->mir_ev[1], ix->copy_stream));
   }
   // host mirrors for query analysis: dictionary keys + df
   if (!mirror_side)
-    HIP_TRY(hipMemcpyAsync(ix->h_dict.data(), ix->dict.p, (size_t)2 * C * 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(ix->h_df.data(), ix->df_dev(), (size_t)C * 4,
+    HIP_TRY(hipMemcpyAsync(S.h_dict.data(), S.dict.p, (size_t)2 * C * 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(S.h_df.data(), S.df_dev(), (size_t)C * 4,
                          hipMemcpyDeviceToHost, s));
   if (mirror_side) {
     HIP_TRY(hipStreamWaitEvent(s, ix->mir_ev[1], 0));   // mirror, checks and count (side stream)
@@ -1150,30 +1344,30 @@ static int commit_once(tfidf_index *ix) {
     HIP_TRY(launch_verify_deferred(bp, s));
     // occupied dictionary slots counted on the device (ctr[7]) instead of a host
     // pass over the mirror (8 M slots at 2^23 took milliseconds)
-    HIP_TRY(launch_count_nonzero(ix->dict.as<uint64_t>(), C, reinterpret_cast<unsigned long long *>(ctr + 7), s));
+    HIP_TRY(launch_count_nonzero(S.dict.as<uint64_t>(), C, reinterpret_cast<unsigned long long *>(ctr + 7), s));
   }
   uint64_t tail[8];              // ctr[3] error flags .. ctr[7] occupied slots, [8] malformed, [10] posting escapes
   HIP_TRY(hipMemcpyAsync(tail, ctr + 3, sizeof tail, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   {
-    const uint64_t n_pe = ix->term_major ? 0 : (uint32_t)tail[7];
+    const uint64_t n_pe = S.term_major ? 0 : (uint32_t)tail[7];
     if (n_pe > post_esc_cap) return fail(TFIDF_E_CAPACITY, "posting escape list overflow");
-    ix->h_post_esc.resize(n_pe);
+    S.h_post_esc.resize(n_pe);
     if (n_pe) {                                // rare (tf >= 2047): sorted for the scorer's binary search
-      HIP_TRY(hipMemcpy(ix->h_post_esc.data(), ix->post_esc.p, n_pe * 8, hipMemcpyDeviceToHost));
-      std::sort(ix->h_post_esc.begin(), ix->h_post_esc.end());
-      HIP_TRY(hipMemcpy(ix->post_esc.p, ix->h_post_esc.data(), n_pe * 8, hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(S.h_post_esc.data(), S.post_esc.p, n_pe * 8, hipMemcpyDeviceToHost));
+      std::sort(S.h_post_esc.begin(), S.h_post_esc.end());
+      HIP_TRY(hipMemcpy(S.post_esc.p, S.h_post_esc.data(), n_pe * 8, hipMemcpyHostToDevice));
     }
   }
-  ix->malformed.resize((uint32_t)tail[5]);
-  if (!ix->malformed.empty()) {
-    HIP_TRY(hipMemcpy(ix->malformed.data(), ix->bad_list.p, ix->malformed.size() * 4, hipMemcpyDeviceToHost));
-    std::sort(ix->malformed.begin(), ix->malformed.end());
+  S.malformed.resize((uint32_t)tail[5]);
+  if (!S.malformed.empty()) {
+    HIP_TRY(hipMemcpy(S.malformed.data(), ix->bad_list.p, S.malformed.size() * 4, hipMemcpyDeviceToHost));
+    std::sort(S.malformed.begin(), S.malformed.end());
   }
   const uint32_t err2 = (uint32_t)tail[0];
   if (err2 & kErrCollision) { ix->collision_doc = (uint32_t)(tail[0] >> 32); return kRcCollision; }
   if (err2 & kErrTfTooLarge) return fail(TFIDF_E_UNSUPPORTED_INPUT, "a term frequency exceeds 2^24 - 1");
-  ix->num_terms = tail[4];
+  S.num_terms = tail[4];
 
   tfidf_commit_timing &t = ix->timing;
   t.ms_tokenize = ev_ms(ix, EV_START, EV_TOK);
@@ -1185,22 +1379,43 @@ static int commit_once(tfidf_index *ix) {
   t.ms_total = t.ms_tokenize + t.ms_long + ev_ms(ix, EV_D0, EV_SCAT);   // device time, host syncs excluded
   t.text_bytes = ix->text_bytes;
   t.num_docs = N;
-  t.nnz = ix->nnz;
+  t.nnz = S.nnz;
 
-  if (int rc = wait_gdf(ix)) return rc;
-  ix->has_global = false;
-  ix->gdf.clear();
-  ix->committed = true;
-  ix->generation++;
-  return upload_cache(ix);
+  // what the snapshot was built from
+  S.cap_log2 = ix->cap_log2;
+  S.text_bytes = ix->text_bytes;
+  S.text = ix->text;
+  S.offsets = ix->offsets;
+  ix->keys.compact();
+  S.keys = ix->keys;                 // shares the chunks; the builder appends to a new one
+  S.hash_seed = ix->hash_seed;
+  {
+    std::lock_guard<std::mutex> tl(S.term_mu);
+    S.term_cache.clear();
+  }
+  // statistics in force: the shard's own (a GLOBAL exchange publishes another view)
+  if (!S.stats || S.stats.use_count() > 1) S.stats = std::make_shared<StatsView>(ix->cfg.device);
+  StatsView &V = *S.stats;
+  if (int rc = V.wait_gdf()) return rc;
+  V.global = false;
+  V.gdf.clear();
+  V.doc_count = S.doc_count;
+  V.sum_ttf = S.sum_ttf;
+  return upload_cache(ix->cfg, V, s);
 }
 
 extern "C" int tfidf_commit(tfidf_index *ix) {
   if (!ix) return fail(TFIDF_E_INVALID_ARG, "NULL index");
   std::lock_guard<std::mutex> lk(ix->mu);
   DeviceGuard g(ix->cfg.device);
-  ix->committed = false;                 // a failed rebuild leaves no half-built index behind
-  ix->term_cache.clear();
+  // The build target: the previous snapshot if no search holds it any more
+  // (its buffers are reused as they are), else a new one.  The published
+  // snapshot stays searchable until this build succeeds; a failed build
+  // publishes nothing (the reference's readers keep the last commit).
+  std::shared_ptr<Snapshot> S;
+  if (ix->spare && ix->spare.use_count() == 1) S = std::move(ix->spare);
+  ix->spare.reset();
+  if (!S) S = std::make_shared<Snapshot>(ix->cfg.device);
   // Hash seeds: 0, then 1, 2, 3 after a detected collision (TFIDF_TEST_WEAK_HASH:
   // start from a seed under which equal-length hashed keys collide).  A floor
   // set by tfidf_set_hash_attempt (GLOBAL statistics: every shard must hash
@@ -1209,16 +1424,32 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   ix->hash_seed = ix->hash_floor ? ix->hash_floor : ((weak && atoi(weak)) ? kWeakHashSeed : 0);
   ix->hash_rebuilds = ix->hash_floor;
   for (uint32_t attempt = ix->hash_floor;; attempt++) {
-    const int rc = commit_once(ix);
+    int rc = commit_once(ix, *S);
     if (rc != TFIDF_OK) {
       hipStreamSynchronize(ix->stream);        // nothing of this build may still run on either stream
       hipStreamSynchronize(ix->copy_stream);
     }
-    if (rc != kRcCollision) return rc;
-    if (attempt == 3)
-      return fail(TFIDF_E_UNSUPPORTED_INPUT, "hash collisions under 4 seeds (last in document %u)", ix->collision_doc);
-    ix->hash_seed = attempt + 1;
-    ix->hash_rebuilds++;
+    if (rc == kRcCollision) {
+      if (attempt == 3) {
+        ix->spare = std::move(S);
+        return fail(TFIDF_E_UNSUPPORTED_INPUT, "hash collisions under 4 seeds (last in document %u)", ix->collision_doc);
+      }
+      ix->hash_seed = attempt + 1;
+      ix->hash_rebuilds++;
+      continue;
+    }
+    if (rc != TFIDF_OK) {
+      ix->spare = std::move(S);
+      return rc == kRcNoPublish ? TFIDF_OK : rc;
+    }
+    S->hash_rebuilds = ix->hash_rebuilds;
+    S->generation = ++ix->generation;
+    {
+      std::lock_guard<std::mutex> sl(ix->snap_mu);
+      std::swap(ix->cur, S);                   // published; S = the previous snapshot
+    }
+    ix->spare = std::move(S);                  // rebuilt in place next time if no search holds it
+    return TFIDF_OK;
   }
 }
 
@@ -1238,34 +1469,41 @@ extern "C" int tfidf_get_commit_timing(const tfidf_index *ix, tfidf_commit_timin
 
 extern "C" int tfidf_stats(const tfidf_index *ix, tfidf_index_stats *out) {
   if (!ix || !out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
-  out->num_docs = ix->committed ? ix->n_docs : 0;
-  out->doc_count = ix->doc_count;
-  out->sum_ttf = ix->sum_ttf;
-  out->num_terms = ix->num_terms;
-  out->nnz = ix->nnz;
-  out->long_docs = ix->long_docs;
+  const std::shared_ptr<Snapshot> S = current(ix);
+  *out = tfidf_index_stats{};
   out->text_bytes = ix->text_bytes;
-  out->term_major = ix->committed && ix->term_major;
-  out->pack_docs = ix->pack_docs;
-  out->pack_retried = ix->pack_retried;
-  out->unicode_docs = ix->unicode_docs;
-  out->long_chunked = ix->long_chunked;
-  out->malformed_docs = ix->committed ? ix->malformed.size() : 0;
   out->hash_seed = ix->hash_seed;
   out->hash_rebuilds = ix->hash_rebuilds;
+  if (S) {
+    out->num_docs = S->n_docs;
+    out->doc_count = S->doc_count;
+    out->sum_ttf = S->sum_ttf;
+    out->num_terms = S->num_terms;
+    out->nnz = S->nnz;
+    out->long_docs = S->long_docs;
+    out->term_major = S->term_major;
+    out->pack_docs = S->pack_docs;
+    out->pack_retried = S->pack_retried;
+    out->unicode_docs = S->unicode_docs;
+    out->long_chunked = S->long_chunked;
+    out->malformed_docs = S->malformed.size();
+    out->hash_seed = S->hash_seed;
+    out->hash_rebuilds = S->hash_rebuilds;
+  }
   {
     std::lock_guard<std::mutex> cl(ix->cq_mu);
     out->coalesced_batches = ix->cq_batches;
     out->coalesced_queries = ix->cq_queries;
-    out->unit_batches = ix->unit_batches;
-    out->fused_queries = ix->fused_queries;
-    out->unit_count = ix->unit_count;
   }
-  const DevBuf *bufs[] = {&ix->text, &ix->offsets, &ix->dict, &ix->csr, &ix->csr_esc, &ix->doc_len,
-                          &ix->doc_nuniq, &ix->doc_norm, &ix->rsplit, &ix->blk, &ix->bbase, &ix->post,
-                          &ix->toff, &ix->tdf};
-  uint64_t tot = 0;
-  for (const DevBuf *b : bufs) tot += b->bytes;
+  out->unit_batches = ix->unit_batches.load();
+  out->fused_queries = ix->fused_queries.load();
+  out->unit_count = ix->unit_count.load();
+  uint64_t tot = ix->text->bytes + ix->offsets->bytes;
+  if (S) {
+    const DevBuf *bufs[] = {&S->dict, &S->csr, &S->csr_esc, &S->doc_len, &S->doc_nuniq, &S->doc_norm,
+                            &S->rsplit, &S->blk, &S->bbase, &S->post, &S->toff, &S->tdf};
+    for (const DevBuf *b : bufs) tot += b->bytes;
+  }
   out->device_bytes = tot;
   return TFIDF_OK;
 }
@@ -1273,14 +1511,14 @@ extern "C" int tfidf_stats(const tfidf_index *ix, tfidf_index_stats *out) {
 // ---------------------------------------------------------------------------
 // dictionary (host mirror)
 
-static uint32_t host_lookup(const tfidf_index *ix, uint64_t lo, uint64_t hi) {
-  if (ix->C == 0) return kInvalidSlot;
-  const uint32_t mask = ix->C - 1;
+static uint32_t host_lookup(const Snapshot &S, uint64_t lo, uint64_t hi) {
+  if (S.C == 0) return kInvalidSlot;
+  const uint32_t mask = S.C - 1;
   // same probe order as the device (kernels_index.hip dict_lookup_multi):
   // linear from the aligned 2-slot bucket of the hash; lo[C] then hi[C]
   uint32_t s = dict_home(dict_hash(lo, hi), mask) & ~1u;
   for (uint32_t it = 0; it <= mask; it++) {
-    const uint64_t clo = ix->h_dict[s], chi = ix->h_dict[(size_t)ix->C + s];
+    const uint64_t clo = S.h_dict[s], chi = S.h_dict[(size_t)S.C + s];
     if (clo == 0) return kInvalidSlot;
     if (clo == lo && chi == hi) return s;
     s = (s + 1) & mask;
@@ -1294,35 +1532,35 @@ struct StrSink {
   std::string s;
   void push(uint8_t c) { s.push_back((char)c); }
 };
-static int slot_term(tfidf_index *ix, uint32_t slot, std::string *out) {
+static int slot_term(Snapshot &S, uint32_t slot, std::string *out) {
   char b[32];
-  const uint64_t lo = ix->h_dict[slot], hi = ix->h_dict[(size_t)ix->C + slot];
+  const uint64_t lo = S.h_dict[slot], hi = S.h_dict[(size_t)S.C + slot];
   if (const uint32_t n = key_decode(lo, hi, b)) { out->assign(b, n); return TFIDF_OK; }
-  std::lock_guard<std::mutex> tl(ix->term_mu);             // batch preparation threads share the cache
-  auto it = ix->term_cache.find(slot);
-  if (it != ix->term_cache.end()) { *out = it->second; return TFIDF_OK; }
+  std::lock_guard<std::mutex> tl(S.term_mu);             // batch preparation threads share the cache
+  auto it = S.term_cache.find(slot);
+  if (it != S.term_cache.end()) { *out = it->second; return TFIDF_OK; }
   uint64_t r = 0;
-  HIP_TRY(hipMemcpy(&r, ix->dict.as<uint64_t>() + 2 * (size_t)ix->C + slot, 8, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(&r, S.dict.as<uint64_t>() + 2 * (size_t)S.C + slot, 8, hipMemcpyDeviceToHost));
   if (r == 0) return fail(TFIDF_E_STATE, "dictionary slot %u has no reference occurrence", slot);
   std::vector<uint8_t> raw(dict_ref_len(r));
   if (!raw.empty())
-    HIP_TRY(hipMemcpy(raw.data(), ix->text.as<uint8_t>() + dict_ref_off(r), raw.size(), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(raw.data(), S.text->as<uint8_t>() + dict_ref_off(r), raw.size(), hipMemcpyDeviceToHost));
   StrSink sink;
   uc_token_bytes(raw.data(), raw.size(), 0, raw.size(), sink);
-  ix->term_cache.emplace(slot, sink.s);
+  S.term_cache.emplace(slot, sink.s);
   *out = sink.s;
   return TFIDF_OK;
 }
 
 // Dictionary slot of the (lower-cased) term t, kInvalidSlot if absent; a
 // hashed key must also match the slot's term string.
-static uint32_t lookup_term(tfidf_index *ix, const std::string &t) {
+static uint32_t lookup_term(Snapshot &S, const std::string &t) {
   uint64_t lo, hi;
-  term_key(t, &lo, &hi, ix->hash_seed);
-  const uint32_t s = host_lookup(ix, lo, hi);
+  term_key(t, &lo, &hi, S.hash_seed);
+  const uint32_t s = host_lookup(S, lo, hi);
   if (s == kInvalidSlot || !key_is_hashed(lo)) return s;
   std::string ts;
-  if (slot_term(ix, s, &ts) != TFIDF_OK || ts != t) return kInvalidSlot;
+  if (slot_term(S, s, &ts) != TFIDF_OK || ts != t) return kInvalidSlot;
   return s;
 }
 
@@ -1334,10 +1572,10 @@ struct PreparedQuery {
 };
 
 // upper bound of a query's hits on this shard: the sum of its scoring terms' local df
-static uint64_t hits_bound(const tfidf_index *ix, const PreparedQuery &pq) {
+static uint64_t hits_bound(const Snapshot &S, const PreparedQuery &pq) {
   uint64_t b = 0;
   for (size_t i = 0; i < pq.slot.size(); i++)
-    if ((pq.role[i] >> 24) != kRoleNot) b += ix->h_df[pq.slot[i]];
+    if ((pq.role[i] >> 24) != kRoleNot) b += S.h_df[pq.slot[i]];
   return b;
 }
 
@@ -1346,24 +1584,24 @@ static uint64_t hits_bound(const tfidf_index *ix, const PreparedQuery &pq) {
 // SHOULD or MUST_NOT term is dropped, a MUST clause without any present term
 // leaves the query without hits (BooleanWeight: required scorer missing), and
 // a query with neither MUST clauses nor a present SHOULD term has no hits.
-static int prepare_query(tfidf_index *ix, const uint8_t *q, uint64_t n, PreparedQuery *pq) {
+static int prepare_query(Snapshot &S, StatsView &V, const uint8_t *q, uint64_t n, PreparedQuery *pq) {
   QueryPlan plan;
   const int rc = parse_query(q, n, &plan);
   if (rc == kQBadUtf8) return fail(TFIDF_E_UNSUPPORTED_QUERY, "query is not valid UTF-8");
   if (rc == kQSyntax)
     return fail(TFIDF_E_QUERY_SYNTAX, "query does not parse (QueryParser ParseException / TooManyClauses)");
-  if (int e = wait_gdf(ix)) return e;
-  const uint64_t dc = eff_doc_count(ix);
+  if (int e = V.wait_gdf()) return e;
+  const uint64_t dc = V.doc_count;
   if (dc == 0) return TFIDF_OK;                        // no document holds a token
   std::vector<uint32_t> present(plan.n_groups, 0);
   uint32_t n_should = 0;
   bool has_not = false;
   for (const PlanTerm &t : plan.terms) {
-    const uint32_t s = lookup_term(ix, t.term);
+    const uint32_t s = lookup_term(S, t.term);
     if (s == kInvalidSlot) continue;                   // absent term contributes nothing
     float wv = 0.0f;
     if (t.role != kRoleNot) {
-      const uint64_t df = ix->has_global ? ix->gdf[s] : ix->h_df[s];
+      const uint64_t df = V.global ? V.gdf[s] : S.h_df[s];
       const float idf = bm25_idf(df, dc);
       volatile float w = t.boost * idf;                // BM25Scorer: weight = boost * idf
       wv = w;
@@ -1458,14 +1696,14 @@ static PrepPool *prep_pool() {
   return pool;
 }
 
-static int prepare_batch(tfidf_index *ix, const uint8_t *q_utf8, const uint64_t *q_offsets, uint32_t n_q,
-                         QueryBatch *qb) {
-  if (int e = wait_gdf(ix)) return e;                   // once, before the workers read the mirrors
+static int prepare_batch(tfidf_index *ix, Snapshot &S, StatsView &V, const uint8_t *q_utf8,
+                         const uint64_t *q_offsets, uint32_t n_q, QueryBatch *qb) {
+  if (int e = V.wait_gdf()) return e;                  // once, before the workers read the mirrors
   std::vector<PreparedQuery> pqs(n_q);
   auto work = [&](uint32_t a, uint32_t b) {
     DeviceGuard g(ix->cfg.device);                      // slot_term may read a reference occurrence
     for (uint32_t i = a; i < b; i++)
-      if (prepare_query(ix, q_utf8 + q_offsets[i], q_offsets[i + 1] - q_offsets[i], &pqs[i]) != TFIDF_OK)
+      if (prepare_query(S, V, q_utf8 + q_offsets[i], q_offsets[i + 1] - q_offsets[i], &pqs[i]) != TFIDF_OK)
         pqs[i] = PreparedQuery();
   };
   uint32_t nt = std::min<uint32_t>(std::max(1u, std::thread::hardware_concurrency()), 16u);
@@ -1483,19 +1721,19 @@ static int prepare_batch(tfidf_index *ix, const uint8_t *q_utf8, const uint64_t 
   return TFIDF_OK;
 }
 
-static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint32_t k) {
-  hipStream_t s = ix->stream;
+static int run_scoring(tfidf_index *ix, Snapshot &S, StatsView &V, SearchCtx &X, hipStream_t s, const QueryBatch &qb,
+                       uint32_t n_q, uint32_t k) {
   const std::vector<uint32_t> &qoff = qb.off, &slots = qb.slot;
   const size_t ns = slots.size(), nr = qb.ops ? ns + qb.meta.size() : 0;
-  const size_t npairs = (size_t)n_q * ix->n_blocks;
+  const size_t npairs = (size_t)n_q * S.n_blocks;
   const bool batch = k && npairs >= (size_t)ix->num_cus * 16 && npairs < (1ull << 32);
   // batches of plain disjunctions, k <= 64, block-major: workgroup per
   // (query, block range) unit (k_score_units); units of about unit_post
   // postings, queries above that split into equal block ranges, listed first
   // (heavy units start early, the light tail balances)
-  std::vector<uint32_t> &units = ix->q_units;
+  std::vector<uint32_t> &units = X.q_units;
   units.clear();
-  bool unit_path = batch && k <= kUnitMaxK && !qb.ops && !ix->term_major && !getenv("TFIDF_NO_UNITS");
+  bool unit_path = batch && k <= kUnitMaxK && !qb.ops && !S.term_major && !getenv("TFIDF_NO_UNITS");
   uint32_t n_wunits = 0;                 // the first n_wunits units are wave units
   if (unit_path) {
     std::vector<uint64_t> P(n_q, 0);
@@ -1503,13 +1741,13 @@ static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint
     for (uint32_t q = 0; q < n_q && unit_path; q++) {
       if (qoff[q + 1] - qoff[q] > kUnitMaxTerms) unit_path = false;
       for (uint32_t t = qoff[q]; t < qoff[q + 1]; t++)
-        if (slots[t] != kInvalidSlot) P[q] += ix->h_df[slots[t]];
+        if (slots[t] != kInvalidSlot) P[q] += S.h_df[slots[t]];
       T += P[q];
     }
     // light queries (at most light_post postings per block on average): wave
     // units (k_score_wunits, units of ~16 k postings); heavy ones: workgroup
     // units (k_score_units, dense block accumulator; ~T/4096 postings each)
-    const uint32_t nb = ix->n_blocks;
+    const uint32_t nb = S.n_blocks;
     uint64_t light_post = kWunitLightPost;
     if (const char *e = getenv("TFIDF_WUNIT_LIGHT")) light_post = (uint64_t)atoll(e);   // A/B and test hook
     uint64_t unit_post = std::min<uint64_t>(std::max<uint64_t>(T / 4096, 8192), 1ull << 17);
@@ -1536,9 +1774,9 @@ static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint
   const size_t words = words0 + units.size();
   // one pinned staging buffer, one upload (the previous upload out of it must
   // have left: batch searches return before their copies run)
-  if (ix->q_in_pending) HIP_TRY(hipEventSynchronize(ix->q_in_ev));
-  HIP_TRY(ix->q_host.resize(words));
-  uint32_t *h = ix->q_host.data();
+  if (X.q_in_pending) HIP_TRY(hipEventSynchronize(X.q_in_ev));
+  HIP_TRY(X.q_host.resize(words));
+  uint32_t *h = X.q_host.data();
   memcpy(h, qoff.data(), qoff.size() * 4);
   memcpy(h + qoff.size(), slots.data(), ns * 4);
   memcpy(h + qoff.size() + ns, qb.w.data(), ns * 4);
@@ -1547,28 +1785,28 @@ static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint
     memcpy(h + qoff.size() + 3 * ns, qb.meta.data(), qb.meta.size() * 4);
   }
   if (!units.empty()) memcpy(h + words0, units.data(), units.size() * 4);
-  if (words * 4 + 16 > ix->q_in.bytes) {
+  if (words * 4 + 16 > X.q_in.bytes) {
     // a pending chunk of a pipelined batch may still read q_in: finish it
     // before the buffer is replaced (1.5x headroom, so later chunks rarely grow it)
     HIP_TRY(hipStreamSynchronize(s));
-    HIP_TRY(ix->q_in.reserve(words * 6 + 16));
+    HIP_TRY(X.q_in.reserve(words * 6 + 16));
   }
-  HIP_TRY(hipMemcpyAsync(ix->q_in.p, h, words * 4, hipMemcpyHostToDevice, s));
-  HIP_TRY(hipEventRecord(ix->q_in_ev, s));
-  ix->q_in_pending = true;
-  uint32_t *din = ix->q_in.as<uint32_t>();
+  HIP_TRY(hipMemcpyAsync(X.q_in.p, h, words * 4, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipEventRecord(X.q_in_ev, s));
+  X.q_in_pending = true;
+  uint32_t *din = X.q_in.as<uint32_t>();
   QueryParams qp{};
-  qp.post = ix->post.as<uint64_t>();
-  qp.post32 = ix->post.as<uint32_t>();
-  qp.post_esc = ix->post_esc.as<uint64_t>();
-  qp.n_post_esc = ix->h_post_esc.size();
-  qp.bbase = ix->bbase.as<uint64_t>();
-  qp.blk = ix->blk.as<uint32_t>();
-  qp.toff = ix->term_major ? ix->toff.as<uint64_t>() : nullptr;
-  qp.C = ix->C;
-  qp.n_blocks = ix->n_blocks;
-  qp.n_docs = ix->n_docs;
-  qp.cache = ix->cache.as<float>();
+  qp.post = S.post.as<uint64_t>();
+  qp.post32 = S.post.as<uint32_t>();
+  qp.post_esc = S.post_esc.as<uint64_t>();
+  qp.n_post_esc = S.h_post_esc.size();
+  qp.bbase = S.bbase.as<uint64_t>();
+  qp.blk = S.blk.as<uint32_t>();
+  qp.toff = S.term_major ? S.toff.as<uint64_t>() : nullptr;
+  qp.C = S.C;
+  qp.n_blocks = S.n_blocks;
+  qp.n_docs = S.n_docs;
+  qp.cache = V.cache.as<float>();
   qp.q_off = din;
   qp.q_slot = din + qoff.size();
   qp.q_w = reinterpret_cast<const float *>(din + qoff.size() + ns);
@@ -1579,33 +1817,33 @@ static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint
   qp.k = k;
   {   // enough (block, chunk) workgroups to fill the chip ~4 deep; never more chunks than queries
     const uint32_t want = (uint32_t)ix->num_cus * 4;
-    uint32_t chunks = ix->n_blocks ? (want + ix->n_blocks - 1) / ix->n_blocks : 1;
+    uint32_t chunks = S.n_blocks ? (want + S.n_blocks - 1) / S.n_blocks : 1;
     chunks = std::max(1u, std::min(chunks, n_q));
     qp.q_chunk = (n_q + chunks - 1) / chunks;
   }
   if (k) {
-    HIP_TRY(ix->cand.reserve((size_t)n_q * ix->n_blocks * k * 8 + 8));
-    HIP_TRY(ix->cand_n.reserve((size_t)n_q * ix->n_blocks * 4 + 4));
+    HIP_TRY(X.cand.reserve((size_t)n_q * S.n_blocks * k * 8 + 8));
+    HIP_TRY(X.cand_n.reserve((size_t)n_q * S.n_blocks * 4 + 4));
     // results contiguous (doc | score | n): a single query reads them back in one copy
-    HIP_TRY(ix->q_out.reserve(((size_t)2 * n_q * k + n_q) * 4 + 16));
-    ix->res_doc = ix->q_out.as<uint32_t>();
-    ix->res_score = reinterpret_cast<float *>(ix->res_doc + (size_t)n_q * k);
-    ix->res_n = ix->res_doc + (size_t)2 * n_q * k;
-    qp.cand = ix->cand.as<uint64_t>();
-    qp.cand_n = ix->cand_n.as<uint32_t>();
-    qp.out_doc = ix->res_doc;
-    qp.out_score = ix->res_score;
-    qp.out_n = ix->res_n;
+    HIP_TRY(X.q_out.reserve(((size_t)2 * n_q * k + n_q) * 4 + 16));
+    X.res_doc = X.q_out.as<uint32_t>();
+    X.res_score = reinterpret_cast<float *>(X.res_doc + (size_t)n_q * k);
+    X.res_n = X.res_doc + (size_t)2 * n_q * k;
+    qp.cand = X.cand.as<uint64_t>();
+    qp.cand_n = X.cand_n.as<uint32_t>();
+    qp.out_doc = X.res_doc;
+    qp.out_score = X.res_score;
+    qp.out_n = X.res_n;
   } else {
-    HIP_TRY(ix->hits.reserve((size_t)ix->n_blocks * kBlockDocs * 8 + 8));
-    HIP_TRY(ix->hits_n.reserve((size_t)ix->n_blocks * 4 + 4));
-    qp.hits = ix->hits.as<uint64_t>();
-    qp.hits_n = ix->hits_n.as<uint32_t>();
+    HIP_TRY(X.hits.reserve((size_t)S.n_blocks * kBlockDocs * 8 + 8));
+    HIP_TRY(X.hits_n.reserve((size_t)S.n_blocks * 4 + 4));
+    qp.hits = X.hits.as<uint64_t>();
+    qp.hits_n = X.hits_n.as<uint32_t>();
   }
-  if (ix->q_timing && ix->q_rec_start) HIP_TRY(hipEventRecord(ix->ev[EV_Q0], s));
+  if (X.q_timing && X.q_rec_start) HIP_TRY(hipEventRecord(X.ev[QEV_0], s));
   if (unit_path) {
-    HIP_TRY(ix->ovf.reserve(64));
-    uint32_t *ctr = ix->ovf.as<uint32_t>();
+    HIP_TRY(X.ovf.reserve(64));
+    uint32_t *ctr = X.ovf.as<uint32_t>();
     HIP_TRY(hipMemsetAsync(ctr, 0, 8, s));
     const uint32_t n_units = (uint32_t)(units.size() / 4), n_gunits = n_units - n_wunits;
     ix->unit_batches++;
@@ -1614,10 +1852,10 @@ static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint
     // both kinds at once: the wave units on the side stream (fork / join events),
     // so the two latency-bound kernels share the CUs instead of running in turn
     const bool both = n_wunits && n_gunits;
-    hipStream_t ws = both ? ix->copy_stream : s;
+    hipStream_t ws = both ? X.side : s;
     if (both) {
-      HIP_TRY(hipEventRecord(ix->q_ev[0], s));
-      HIP_TRY(hipStreamWaitEvent(ws, ix->q_ev[0], 0));
+      HIP_TRY(hipEventRecord(X.q_ev[0], s));
+      HIP_TRY(hipStreamWaitEvent(ws, X.q_ev[0], 0));
     }
     if (n_wunits) {
       const int grid = (int)std::min<uint64_t>((n_wunits + kWunitWavesPerWG - 1) / kWunitWavesPerWG,
@@ -1632,12 +1870,12 @@ static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint
       HIP_TRY(launch_score_units(qp, ud + n_wunits, n_gunits, ctr + 1, grid, s));
     }
     if (both) {
-      HIP_TRY(hipEventRecord(ix->q_ev[1], ws));
-      HIP_TRY(hipStreamWaitEvent(s, ix->q_ev[1], 0));
+      HIP_TRY(hipEventRecord(X.q_ev[1], ws));
+      HIP_TRY(hipStreamWaitEvent(s, X.q_ev[1], 0));
     }
-    if (ix->q_timing) HIP_TRY(hipEventRecord(ix->ev[EV_Q1], s));
+    if (X.q_timing) HIP_TRY(hipEventRecord(X.ev[QEV_1], s));
     HIP_TRY(launch_merge_topk(qp, s));
-    if (ix->q_timing) HIP_TRY(hipEventRecord(ix->ev[EV_Q2], s));
+    if (X.q_timing) HIP_TRY(hipEventRecord(X.ev[QEV_2], s));
     return TFIDF_OK;
   }
   if (batch) {
@@ -1647,8 +1885,8 @@ static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint
     // the chip one wave each.
     // plain heavy pairs -> ovf list (k_score_blocks<false>); pairs of operator
     // queries -> ovf2 list (k_score_blocks<true>)
-    HIP_TRY(ix->ovf.reserve(npairs * 8 + 64));
-    qp.ovf_count = ix->ovf.as<uint32_t>();
+    HIP_TRY(X.ovf.reserve(npairs * 8 + 64));
+    qp.ovf_count = X.ovf.as<uint32_t>();
     qp.ovf2_count = qp.ovf_count + 1;
     qp.ovf_list = qp.ovf_count + 16;
     qp.ovf2_list = qp.ovf_list + npairs;
@@ -1668,44 +1906,45 @@ static int run_scoring(tfidf_index *ix, const QueryBatch &qb, uint32_t n_q, uint
     }
   }
   HIP_TRY(launch_score_blocks(qp, s));
-  if (ix->q_timing) HIP_TRY(hipEventRecord(ix->ev[EV_Q1], s));
+  if (X.q_timing) HIP_TRY(hipEventRecord(X.ev[QEV_1], s));
   if (k) HIP_TRY(launch_merge_topk(qp, s));
-  if (ix->q_timing) HIP_TRY(hipEventRecord(ix->ev[EV_Q2], s));
+  if (X.q_timing) HIP_TRY(hipEventRecord(X.ev[QEV_2], s));
   return TFIDF_OK;
 }
 
-extern "C" int tfidf_search(tfidf_index *ix, const uint8_t *q, uint64_t q_len, uint32_t k, uint32_t *doc_ids,
-                            float *scores, uint64_t cap, uint64_t *n_out) {
-  if (!ix || (!q && q_len) || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
-  *n_out = 0;
-  std::lock_guard<std::mutex> lk(ix->mu);
-  if (!ix->committed) return fail(TFIDF_E_STATE, "search before commit");
+// One search on a snapshot (tfidf_search: the published one; tfidf_reader_search:
+// the reader's).
+static int search_on(tfidf_index *ix, Snapshot &S, StatsView &V, const uint8_t *q, uint64_t q_len, uint32_t k,
+                     uint32_t *doc_ids, float *scores, uint64_t cap, uint64_t *n_out) {
+  CtxLease lease(ix);
+  if (lease.rc) return lease.rc;
+  SearchCtx &X = *lease.c;
+  const hipStream_t s = lease.stream();
   if (k > 1024) return fail(TFIDF_E_INVALID_ARG, "k must be <= 1024 (0 = all hits)");
   DeviceGuard g(ix->cfg.device);
   PreparedQuery pq;
-  int rc = prepare_query(ix, q, q_len, &pq);
+  int rc = prepare_query(S, V, q, q_len, &pq);
   if (rc) return rc;
-  if (pq.slot.empty() || ix->n_docs == 0) { ix->last_ms_scoring = ix->last_ms_total = 0; return TFIDF_OK; }
-  hipStream_t s = ix->stream;
+  if (pq.slot.empty() || S.n_docs == 0) { set_last_ms(ix, 0, 0); return TFIDF_OK; }
   // fused path for k <= kFusedMaxK: each block workgroup writes its k
   // candidates to pinned host memory over PCIe and the host merges n_blocks x k
   // keys, a cost that grows with k (larger k: run_scoring + the device merge)
   if (k && k <= kFusedMaxK && pq.slot.size() <= kInlTerms && !getenv("TFIDF_NO_FUSED")) {
     // one launch: query terms in the kernel arguments, block scoring with the
     // candidates written to pinned host memory, merged here
-    HIP_TRY(ix->q_res.resize((size_t)2 * k + 1));
+    HIP_TRY(X.q_res.resize((size_t)2 * k + 1));
     QueryParams qp{};
-    qp.post = ix->post.as<uint64_t>();
-    qp.post32 = ix->post.as<uint32_t>();
-    qp.post_esc = ix->post_esc.as<uint64_t>();
-    qp.n_post_esc = ix->h_post_esc.size();
-    qp.bbase = ix->bbase.as<uint64_t>();
-    qp.blk = ix->blk.as<uint32_t>();
-    qp.toff = ix->term_major ? ix->toff.as<uint64_t>() : nullptr;
-    qp.C = ix->C;
-    qp.n_blocks = ix->n_blocks;
-    qp.n_docs = ix->n_docs;
-    qp.cache = ix->cache.as<float>();
+    qp.post = S.post.as<uint64_t>();
+    qp.post32 = S.post.as<uint32_t>();
+    qp.post_esc = S.post_esc.as<uint64_t>();
+    qp.n_post_esc = S.h_post_esc.size();
+    qp.bbase = S.bbase.as<uint64_t>();
+    qp.blk = S.blk.as<uint32_t>();
+    qp.toff = S.term_major ? S.toff.as<uint64_t>() : nullptr;
+    qp.C = S.C;
+    qp.n_blocks = S.n_blocks;
+    qp.n_docs = S.n_docs;
+    qp.cache = V.cache.as<float>();
     qp.inl_n = (uint32_t)pq.slot.size();
     qp.inl_meta = pq.meta;
     for (size_t i = 0; i < pq.slot.size(); i++) {
@@ -1721,29 +1960,29 @@ extern "C" int tfidf_search(tfidf_index *ix, const uint8_t *q, uint64_t q_len, u
     // host merges them (a merge kernel + copies: p50 0.049 / 0.057 ms, this
     // path 0.034 ms; a last-workgroup merge in the scoring kernel 0.055 ms:
     // its device-scope fences cost more than the launch they save)
-    HIP_TRY(ix->q_cand_h.resize((size_t)ix->n_blocks * k * 2 + ix->n_blocks));
-    qp.cand = reinterpret_cast<uint64_t *>(ix->q_cand_h.data());
-    qp.cand_n = ix->q_cand_h.data() + (size_t)ix->n_blocks * k * 2;
-    if (ix->q_timing) HIP_TRY(hipEventRecord(ix->ev[EV_Q0], s));
+    HIP_TRY(X.q_cand_h.resize((size_t)S.n_blocks * k * 2 + S.n_blocks));
+    qp.cand = reinterpret_cast<uint64_t *>(X.q_cand_h.data());
+    qp.cand_n = X.q_cand_h.data() + (size_t)S.n_blocks * k * 2;
+    if (X.q_timing) HIP_TRY(hipEventRecord(X.ev[QEV_0], s));
     HIP_TRY(launch_score_blocks(qp, s));
-    if (ix->q_timing) {
-      HIP_TRY(hipEventRecord(ix->ev[EV_Q1], s));
-      HIP_TRY(hipEventRecord(ix->ev[EV_Q2], s));
+    if (X.q_timing) {
+      HIP_TRY(hipEventRecord(X.ev[QEV_1], s));
+      HIP_TRY(hipEventRecord(X.ev[QEV_2], s));
     }
     ix->fused_queries++;
     HIP_TRY(hipStreamSynchronize(s));
     {
       // the blocks' candidate keys (score bits << 32 | ~doc: unique, key order =
       // score desc, doc asc) -> top k
-      const uint64_t *ck = reinterpret_cast<const uint64_t *>(ix->q_cand_h.data());
-      const uint32_t *cn = ix->q_cand_h.data() + (size_t)ix->n_blocks * k * 2;
-      std::vector<uint64_t> &all = ix->q_merge;
+      const uint64_t *ck = reinterpret_cast<const uint64_t *>(X.q_cand_h.data());
+      const uint32_t *cn = X.q_cand_h.data() + (size_t)S.n_blocks * k * 2;
+      std::vector<uint64_t> &all = X.q_merge;
       all.clear();
-      for (uint32_t b = 0; b < ix->n_blocks; b++)
+      for (uint32_t b = 0; b < S.n_blocks; b++)
         for (uint32_t i = 0; i < cn[b]; i++) all.push_back(ck[(size_t)b * k + i]);
       const size_t m = std::min<size_t>(k, all.size());
       std::partial_sort(all.begin(), all.begin() + m, all.end(), std::greater<uint64_t>());
-      uint32_t *h = ix->q_res.data();
+      uint32_t *h = X.q_res.data();
       for (size_t i = 0; i < m; i++) {
         h[i] = ~(uint32_t)all[i];
         uint32_t sb = (uint32_t)(all[i] >> 32);
@@ -1751,58 +1990,122 @@ extern "C" int tfidf_search(tfidf_index *ix, const uint8_t *q, uint64_t q_len, u
       }
       h[2 * k] = (uint32_t)m;
     }
-    const uint32_t n = ix->q_res[2 * k];
+    const uint32_t n = X.q_res[2 * k];
     *n_out = n;
     if (n > cap) return fail(TFIDF_E_BUFFER, "need %u result slots", n);
-    memcpy(doc_ids, ix->q_res.data(), n * 4);
-    memcpy(scores, ix->q_res.data() + k, n * 4);
-    ix->last_ms_scoring = ev_ms(ix, EV_Q0, EV_Q1);
-    ix->last_ms_total = ev_ms(ix, EV_Q0, EV_Q2);
+    memcpy(doc_ids, X.q_res.data(), n * 4);
+    memcpy(scores, X.q_res.data() + k, n * 4);
+    set_last_ms(ix, qev_ms(X, QEV_0, QEV_1), qev_ms(X, QEV_0, QEV_2));
     return TFIDF_OK;
   }
   QueryBatch qb;
   qb.add(pq);
-  rc = run_scoring(ix, qb, 1, k);
+  rc = run_scoring(ix, S, V, X, s, qb, 1, k);
   if (rc) return rc;
   if (k) {
     // one copy of (doc[k] | score[k] | n) into pinned memory, one wait
-    HIP_TRY(ix->q_res.resize((size_t)2 * k + 1));
-    HIP_TRY(hipMemcpyAsync(ix->q_res.data(), ix->res_doc, ((size_t)2 * k + 1) * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(X.q_res.resize((size_t)2 * k + 1));
+    HIP_TRY(hipMemcpyAsync(X.q_res.data(), X.res_doc, ((size_t)2 * k + 1) * 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
-    ix->q_in_pending = false;
-    const uint32_t n = ix->q_res[2 * k];
+    X.q_in_pending = false;
+    const uint32_t n = X.q_res[2 * k];
     *n_out = n;
     if (n > cap) return fail(TFIDF_E_BUFFER, "need %u result slots", n);
-    memcpy(doc_ids, ix->q_res.data(), n * 4);
-    memcpy(scores, ix->q_res.data() + k, n * 4);
-    ix->last_ms_scoring = ev_ms(ix, EV_Q0, EV_Q1);
-    ix->last_ms_total = ev_ms(ix, EV_Q0, EV_Q2);
+    memcpy(doc_ids, X.q_res.data(), n * 4);
+    memcpy(scores, X.q_res.data() + k, n * 4);
+    set_last_ms(ix, qev_ms(X, QEV_0, QEV_1), qev_ms(X, QEV_0, QEV_2));
     return TFIDF_OK;
   }
   // all hits: per-block sorted runs -> merge passes on the device -> (doc, score)
-  const uint32_t R = ix->n_blocks;
-  HIP_TRY(ix->hits_c.reserve((size_t)R * kBlockDocs * 8 + 8));
-  HIP_TRY(ix->hits_s.reserve((size_t)R * kBlockDocs * 8 + 8));
-  HIP_TRY(ix->hits_P.reserve(((size_t)R + 1) * 8));
-  HIP_TRY(ix->out_doc.reserve((size_t)R * kBlockDocs * 4 + 4));
-  HIP_TRY(ix->out_score.reserve((size_t)R * kBlockDocs * 4 + 4));
-  HIP_TRY(launch_hits_order(ix->hits.as<uint64_t>(), ix->hits_n.as<uint32_t>(), R, ix->hits_P.as<uint64_t>(),
-                            ix->hits_c.as<uint64_t>(), ix->hits.as<uint64_t>(), ix->hits_s.as<uint64_t>(),
-                            ix->out_doc.as<uint32_t>(),
-                            ix->out_score.as<float>(), nullptr, 0, hits_bound(ix, pq), ix->num_cus * 4, s));
-  if (ix->q_timing) HIP_TRY(hipEventRecord(ix->ev[EV_Q2], s));
+  const uint32_t R = S.n_blocks;
+  HIP_TRY(X.hits_c.reserve((size_t)R * kBlockDocs * 8 + 8));
+  HIP_TRY(X.hits_s.reserve((size_t)R * kBlockDocs * 8 + 8));
+  HIP_TRY(X.hits_P.reserve(((size_t)R + 1) * 8));
+  HIP_TRY(X.out_doc.reserve((size_t)R * kBlockDocs * 4 + 4));
+  HIP_TRY(X.out_score.reserve((size_t)R * kBlockDocs * 4 + 4));
+  HIP_TRY(launch_hits_order(X.hits.as<uint64_t>(), X.hits_n.as<uint32_t>(), R, X.hits_P.as<uint64_t>(),
+                            X.hits_c.as<uint64_t>(), X.hits.as<uint64_t>(), X.hits_s.as<uint64_t>(),
+                            X.out_doc.as<uint32_t>(),
+                            X.out_score.as<float>(), nullptr, 0, hits_bound(S, pq), ix->num_cus * 4, s));
+  if (X.q_timing) HIP_TRY(hipEventRecord(X.ev[QEV_2], s));
   uint64_t H = 0;
-  HIP_TRY(hipMemcpyAsync(&H, ix->hits_P.as<uint64_t>() + R, 8, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(&H, X.hits_P.as<uint64_t>() + R, 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   *n_out = H;
   if (H > cap) return fail(TFIDF_E_BUFFER, "need %llu result slots", (unsigned long long)H);
   if (H) {
-    HIP_TRY(hipMemcpyAsync(doc_ids, ix->out_doc.p, H * 4, hipMemcpyDeviceToHost, s));
-    HIP_TRY(hipMemcpyAsync(scores, ix->out_score.p, H * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(doc_ids, X.out_doc.p, H * 4, hipMemcpyDeviceToHost, s));
+    HIP_TRY(hipMemcpyAsync(scores, X.out_score.p, H * 4, hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
   }
-  ix->last_ms_scoring = ev_ms(ix, EV_Q0, EV_Q1);
-  ix->last_ms_total = ev_ms(ix, EV_Q0, EV_Q2);
+  set_last_ms(ix, qev_ms(X, QEV_0, QEV_1), qev_ms(X, QEV_0, QEV_2));
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_search(tfidf_index *ix, const uint8_t *q, uint64_t q_len, uint32_t k, uint32_t *doc_ids,
+                            float *scores, uint64_t cap, uint64_t *n_out) {
+  if (!ix || (!q && q_len) || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  *n_out = 0;
+  std::shared_ptr<StatsView> view;
+  const std::shared_ptr<Snapshot> snap = current(ix, &view);
+  if (!snap) return fail(TFIDF_E_STATE, "search before commit");
+  return search_on(ix, *snap, *view, q, q_len, k, doc_ids, scores, cap, n_out);
+}
+
+static int doc_keys_of(const Snapshot *S, uint8_t *buf, uint64_t cap, uint64_t *offsets, uint64_t *n_bytes);
+
+// ---- readers (Worker.java:223: DirectoryReader.open on the last commit per
+// request; the hits' stored fields are read from that same reader, :234-238)
+struct tfidf_reader {
+  tfidf_index *ix;
+  std::shared_ptr<Snapshot> S;
+  std::shared_ptr<StatsView> V;
+};
+
+extern "C" int tfidf_reader_open(tfidf_index *ix, tfidf_reader **out) {
+  if (!ix || !out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  *out = nullptr;
+  std::shared_ptr<StatsView> v;
+  std::shared_ptr<Snapshot> S = current(ix, &v);
+  if (!S) return fail(TFIDF_E_STATE, "no commit to read");
+  *out = new tfidf_reader{ix, std::move(S), std::move(v)};
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_reader_close(tfidf_reader *rd) {
+  delete rd;
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_reader_info(const tfidf_reader *rd, uint64_t *generation, uint64_t *num_docs) {
+  if (!rd) return fail(TFIDF_E_INVALID_ARG, "NULL reader");
+  if (generation) *generation = rd->S->generation;
+  if (num_docs) *num_docs = rd->S->n_docs;
+  return TFIDF_OK;
+}
+
+extern "C" int tfidf_reader_search(tfidf_reader *rd, const uint8_t *q, uint64_t q_len, uint32_t k, uint32_t *doc_ids,
+                                   float *scores, uint64_t cap, uint64_t *n_out) {
+  if (!rd || (!q && q_len) || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  *n_out = 0;
+  return search_on(rd->ix, *rd->S, *rd->V, q, q_len, k, doc_ids, scores, cap, n_out);
+}
+
+extern "C" int tfidf_reader_doc_keys(const tfidf_reader *rd, uint8_t *buf, uint64_t cap, uint64_t *offsets,
+                                     uint64_t *n_bytes) {
+  if (!rd || !n_bytes || !offsets) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  return doc_keys_of(rd->S.get(), buf, cap, offsets, n_bytes);
+}
+
+extern "C" int tfidf_reader_doc_key(const tfidf_reader *rd, uint64_t doc, uint8_t *buf, uint64_t cap,
+                                    uint64_t *n_out) {
+  if (!rd || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  if (doc >= rd->S->n_docs) return fail(TFIDF_E_INVALID_ARG, "doc out of range");
+  std::string k;
+  rd->S->keys.key(rd->S->staged_of(doc), &k);
+  *n_out = k.size();
+  if (k.size() > cap) return fail(TFIDF_E_BUFFER, "key needs %zu bytes", k.size());
+  if (buf && !k.empty()) memcpy(buf, k.data(), k.size());
   return TFIDF_OK;
 }
 
@@ -1810,13 +2113,20 @@ extern "C" int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const 
                                   uint32_t k, uint32_t *doc_ids, float *scores, uint32_t *counts) {
   if (!ix || !q_offsets || !doc_ids || !scores || !counts) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
   if (k == 0 || k > 1024) return fail(TFIDF_E_INVALID_ARG, "batch search needs 1 <= k <= 1024");
-  std::lock_guard<std::mutex> lk(ix->mu);
-  if (!ix->committed) return fail(TFIDF_E_STATE, "search before commit");
+  std::shared_ptr<StatsView> view;
+  const std::shared_ptr<Snapshot> snap = current(ix, &view);
+  if (!snap) return fail(TFIDF_E_STATE, "search before commit");
+  Snapshot &S = *snap;
+  StatsView &V = *view;
+  CtxLease lease(ix);
+  if (lease.rc) return lease.rc;
+  SearchCtx &X = *lease.c;
+  const hipStream_t s = lease.stream();
   DeviceGuard g(ix->cfg.device);
   using clk = std::chrono::steady_clock;
   const auto t0 = clk::now();
   if (n_q == 0) return TFIDF_OK;
-  if (ix->n_docs == 0) {
+  if (S.n_docs == 0) {
     memset(counts, 0, (size_t)n_q * 4);
     return TFIDF_OK;
   }
@@ -1833,9 +2143,8 @@ extern "C" int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const 
   uint32_t n_chunks = n_q >= 4096 ? 2 : 1;
   if (const char *e = getenv("TFIDF_BATCH_CHUNKS")) n_chunks = (uint32_t)std::max(1, std::min(atoi(e), 64));
   n_chunks = std::max(1u, std::min(n_chunks, n_q));
-  hipStream_t s = ix->stream;
   const size_t words = (size_t)2 * n_q * k + n_q;
-  HIP_TRY(ix->q_res.resize(words));
+  HIP_TRY(X.q_res.resize(words));
   double t_prep = 0, t_sub = 0;
   bool any = false;
   uint32_t c0 = 0;
@@ -1844,17 +2153,17 @@ extern "C" int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const 
     const uint32_t nc = c1 - c0;                         // the first chunk is the largest (ceil split)
     const auto ta = clk::now();
     QueryBatch qb;
-    if (int e = prepare_batch(ix, q_utf8, q_offsets + c0, nc, &qb)) { ix->q_rec_start = true; return e; }
+    if (int e = prepare_batch(ix, S, V, q_utf8, q_offsets + c0, nc, &qb)) { X.q_rec_start = true; return e; }
     const auto tb = clk::now();
-    uint32_t *hres = ix->q_res.data() + (size_t)2 * c0 * k + c0;
+    uint32_t *hres = X.q_res.data() + (size_t)2 * c0 * k + c0;
     if (qb.slot.empty()) {
       memset(hres + (size_t)2 * nc * k, 0, (size_t)nc * 4);   // no term of the chunk is present
     } else {
-      ix->q_rec_start = !any;
-      const int rc = run_scoring(ix, qb, nc, k);
-      ix->q_rec_start = true;
+      X.q_rec_start = !any;
+      const int rc = run_scoring(ix, S, V, X, s, qb, nc, k);
+      X.q_rec_start = true;
       if (rc) return rc;
-      HIP_TRY(hipMemcpyAsync(hres, ix->res_doc, ((size_t)2 * nc * k + nc) * 4, hipMemcpyDeviceToHost, s));
+      HIP_TRY(hipMemcpyAsync(hres, X.res_doc, ((size_t)2 * nc * k + nc) * 4, hipMemcpyDeviceToHost, s));
       any = true;
     }
     t_prep += std::chrono::duration<double, std::milli>(tb - ta).count();
@@ -1863,23 +2172,23 @@ extern "C" int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const 
   }
   const auto t2 = clk::now();
   HIP_TRY(hipStreamSynchronize(s));
-  ix->q_in_pending = false;
+  X.q_in_pending = false;
   const auto t3 = clk::now();
   c0 = 0;
   for (uint32_t c = 0; c < n_chunks; c++) {
     const uint32_t c1 = (uint32_t)(((uint64_t)n_q * (c + 1) + n_chunks - 1) / n_chunks), nc = c1 - c0;
-    const uint32_t *hres = ix->q_res.data() + (size_t)2 * c0 * k + c0;
+    const uint32_t *hres = X.q_res.data() + (size_t)2 * c0 * k + c0;
     memcpy(doc_ids + (size_t)c0 * k, hres, (size_t)nc * k * 4);
     memcpy(scores + (size_t)c0 * k, hres + (size_t)nc * k, (size_t)nc * k * 4);
     memcpy(counts + c0, hres + (size_t)2 * nc * k, (size_t)nc * 4);
     c0 = c1;
   }
-  ix->last_ms_scoring = any ? ev_ms(ix, EV_Q0, EV_Q1) : 0.0f;
-  ix->last_ms_total = any ? ev_ms(ix, EV_Q0, EV_Q2) : 0.0f;
+  const float ms_total = any ? qev_ms(X, QEV_0, QEV_2) : 0.0f;
+  set_last_ms(ix, any ? qev_ms(X, QEV_0, QEV_1) : 0.0f, ms_total);
   if (getenv("TFIDF_HOST_TIMING")) {          // profiling only
     auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     fprintf(stderr, "batch %u (%u chunks): prepare %.3f  submit %.3f  wait %.3f  copy-out %.3f  total %.3f ms (device %.3f)\n",
-            n_q, n_chunks, t_prep, t_sub, ms(t2, t3), ms(t3, clk::now()), ms(t0, clk::now()), ix->last_ms_total);
+            n_q, n_chunks, t_prep, t_sub, ms(t2, t3), ms(t3, clk::now()), ms(t0, clk::now()), ms_total);
   }
   return TFIDF_OK;
 }
@@ -1990,13 +2299,13 @@ extern "C" int tfidf_search_coalesced(tfidf_index *ix, const uint8_t *q, uint64_
 
 extern "C" int tfidf_set_query_timing(tfidf_index *ix, int on) {
   if (!ix) return fail(TFIDF_E_INVALID_ARG, "NULL index");
-  std::lock_guard<std::mutex> lk(ix->mu);
   ix->q_timing = on != 0;
   return TFIDF_OK;
 }
 
 extern "C" int tfidf_last_search_ms(const tfidf_index *ix, float *ms_scoring, float *ms_total) {
   if (!ix) return fail(TFIDF_E_INVALID_ARG, "NULL index");
+  std::lock_guard<std::mutex> lk(const_cast<tfidf_index *>(ix)->ms_mu);
   if (ms_scoring) *ms_scoring = ix->last_ms_scoring;
   if (ms_total) *ms_total = ix->last_ms_total;
   return TFIDF_OK;
@@ -2008,6 +2317,7 @@ extern "C" int tfidf_set_stream(tfidf_index *ix, void *stream) {
   DeviceGuard g(ix->cfg.device);
   HIP_TRY(hipStreamSynchronize(ix->stream));
   ix->stream = stream == TFIDF_OWN_STREAM ? ix->own_stream : static_cast<hipStream_t>(stream);
+  ix->user_stream = stream == TFIDF_OWN_STREAM ? nullptr : static_cast<hipStream_t>(stream);
   return TFIDF_OK;
 }
 
@@ -2015,25 +2325,30 @@ extern "C" int tfidf_search_batch_keys_device(tfidf_index *ix, const uint8_t *q_
                                               uint32_t n_q, uint32_t k, uint64_t doc_base, void *d_keys) {
   if (!ix || !q_offsets || (n_q && !d_keys)) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
   if (k == 0 || k > 1024) return fail(TFIDF_E_INVALID_ARG, "1 <= k <= 1024");
-  std::lock_guard<std::mutex> lk(ix->mu);
-  if (!ix->committed) return fail(TFIDF_E_STATE, "search before commit");
+  std::shared_ptr<StatsView> view;
+  const std::shared_ptr<Snapshot> snap = current(ix, &view);
+  if (!snap) return fail(TFIDF_E_STATE, "search before commit");
+  Snapshot &S = *snap;
+  StatsView &V = *view;
+  CtxLease lease(ix);
+  if (lease.rc) return lease.rc;
+  SearchCtx &X = *lease.c;
+  const hipStream_t s = lease.stream();
   DeviceGuard g(ix->cfg.device);
   if (n_q == 0) return TFIDF_OK;
-  hipStream_t s = ix->stream;
   QueryBatch qb;
-  if (int e = prepare_batch(ix, q_utf8, q_offsets, n_q, &qb)) return e;
-  if (ix->n_docs == 0 || qb.slot.empty()) {
+  if (int e = prepare_batch(ix, S, V, q_utf8, q_offsets, n_q, &qb)) return e;
+  if (S.n_docs == 0 || qb.slot.empty()) {
     HIP_TRY(hipMemsetAsync(d_keys, 0, (size_t)n_q * k * 8, s));
     HIP_TRY(hipStreamSynchronize(s));
     return TFIDF_OK;
   }
-  int rc = run_scoring(ix, qb, n_q, k);
+  int rc = run_scoring(ix, S, V, X, s, qb, n_q, k);
   if (rc) return rc;
-  HIP_TRY(launch_pack_keys(ix->res_doc, ix->res_score, ix->res_n, n_q, k,
+  HIP_TRY(launch_pack_keys(X.res_doc, X.res_score, X.res_n, n_q, k,
                            doc_base, static_cast<uint64_t *>(d_keys), s));
   HIP_TRY(hipStreamSynchronize(s));
-  ix->last_ms_scoring = ev_ms(ix, EV_Q0, EV_Q1);
-  ix->last_ms_total = ev_ms(ix, EV_Q0, EV_Q2);
+  set_last_ms(ix, qev_ms(X, QEV_0, QEV_1), qev_ms(X, QEV_0, QEV_2));
   return TFIDF_OK;
 }
 
@@ -2041,103 +2356,100 @@ extern "C" int tfidf_search_all_keys_device(tfidf_index *ix, const uint8_t *q, u
                                             void *d_keys, uint64_t cap, uint64_t *n_out) {
   if (!ix || (!q && q_len) || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
   *n_out = 0;
-  std::lock_guard<std::mutex> lk(ix->mu);
-  if (!ix->committed) return fail(TFIDF_E_STATE, "search before commit");
-  if (cap < ix->n_docs || (ix->n_docs && !d_keys))
-    return fail(TFIDF_E_BUFFER, "the key buffer needs num_docs = %llu entries", (unsigned long long)ix->n_docs);
+  std::shared_ptr<StatsView> view;
+  const std::shared_ptr<Snapshot> snap = current(ix, &view);
+  if (!snap) return fail(TFIDF_E_STATE, "search before commit");
+  Snapshot &S = *snap;
+  StatsView &V = *view;
+  CtxLease lease(ix);
+  if (lease.rc) return lease.rc;
+  SearchCtx &X = *lease.c;
+  const hipStream_t s = lease.stream();
+  if (cap < S.n_docs || (S.n_docs && !d_keys))
+    return fail(TFIDF_E_BUFFER, "the key buffer needs num_docs = %llu entries", (unsigned long long)S.n_docs);
   DeviceGuard g(ix->cfg.device);
   PreparedQuery pq;
-  int rc = prepare_query(ix, q, q_len, &pq);
+  int rc = prepare_query(S, V, q, q_len, &pq);
   if (rc) return rc;
-  if (pq.slot.empty() || ix->n_docs == 0) return TFIDF_OK;
+  if (pq.slot.empty() || S.n_docs == 0) return TFIDF_OK;
   QueryBatch qb;
   qb.add(pq);
-  rc = run_scoring(ix, qb, 1, 0);
+  rc = run_scoring(ix, S, V, X, s, qb, 1, 0);
   if (rc) return rc;
-  hipStream_t s = ix->stream;
-  const uint32_t R = ix->n_blocks;
-  HIP_TRY(ix->hits_c.reserve((size_t)R * kBlockDocs * 8 + 8));
-  HIP_TRY(ix->hits_s.reserve((size_t)R * kBlockDocs * 8 + 8));
-  HIP_TRY(ix->hits_P.reserve(((size_t)R + 1) * 8));
-  HIP_TRY(launch_hits_order(ix->hits.as<uint64_t>(), ix->hits_n.as<uint32_t>(), R, ix->hits_P.as<uint64_t>(),
-                            ix->hits_c.as<uint64_t>(), ix->hits.as<uint64_t>(), ix->hits_s.as<uint64_t>(), nullptr, nullptr,
-                            static_cast<uint64_t *>(d_keys), doc_base, hits_bound(ix, pq), ix->num_cus * 4, s));
-  if (ix->q_timing) HIP_TRY(hipEventRecord(ix->ev[EV_Q2], s));
-  HIP_TRY(hipMemcpyAsync(n_out, ix->hits_P.as<uint64_t>() + R, 8, hipMemcpyDeviceToHost, s));
+  const uint32_t R = S.n_blocks;
+  HIP_TRY(X.hits_c.reserve((size_t)R * kBlockDocs * 8 + 8));
+  HIP_TRY(X.hits_s.reserve((size_t)R * kBlockDocs * 8 + 8));
+  HIP_TRY(X.hits_P.reserve(((size_t)R + 1) * 8));
+  HIP_TRY(launch_hits_order(X.hits.as<uint64_t>(), X.hits_n.as<uint32_t>(), R, X.hits_P.as<uint64_t>(),
+                            X.hits_c.as<uint64_t>(), X.hits.as<uint64_t>(), X.hits_s.as<uint64_t>(), nullptr, nullptr,
+                            static_cast<uint64_t *>(d_keys), doc_base, hits_bound(S, pq), ix->num_cus * 4, s));
+  if (X.q_timing) HIP_TRY(hipEventRecord(X.ev[QEV_2], s));
+  HIP_TRY(hipMemcpyAsync(n_out, X.hits_P.as<uint64_t>() + R, 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
-  ix->last_ms_scoring = ev_ms(ix, EV_Q0, EV_Q1);
-  ix->last_ms_total = ev_ms(ix, EV_Q0, EV_Q2);
+  set_last_ms(ix, qev_ms(X, QEV_0, QEV_1), qev_ms(X, QEV_0, QEV_2));
   return TFIDF_OK;
 }
 
 // ---------------------------------------------------------------------------
 // inspection
 
-static uint64_t staged_of(const tfidf_index *ix, uint64_t doc) {
-  return ix->live_map.empty() ? doc : ix->live_map[doc];
-}
-
 extern "C" int tfidf_doc_key(const tfidf_index *ix, uint64_t doc, uint8_t *buf, uint64_t cap, uint64_t *n_out) {
   if (!ix || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
-  if (!ix->committed || doc >= ix->n_docs) return fail(TFIDF_E_INVALID_ARG, "doc out of range");
-  const uint64_t st = staged_of(ix, doc);
+  const std::shared_ptr<Snapshot> S = current(ix);
+  if (!S || doc >= S->n_docs) return fail(TFIDF_E_INVALID_ARG, "doc out of range");
   std::string k;
-  if (ix->key_synth[st]) k = std::to_string(st);
-  else k.assign(ix->key_arena.data() + ix->key_off[st], ix->key_off[st + 1] - ix->key_off[st]);
+  S->keys.key(S->staged_of(doc), &k);
   *n_out = k.size();
   if (k.size() > cap) return fail(TFIDF_E_BUFFER, "key needs %zu bytes", k.size());
   if (buf && !k.empty()) memcpy(buf, k.data(), k.size());
   return TFIDF_OK;
 }
 
-extern "C" int tfidf_doc_keys(const tfidf_index *ix, uint8_t *buf, uint64_t cap, uint64_t *offsets,
-                              uint64_t *n_bytes) {
-  if (!ix || !n_bytes || !offsets) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
-  if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
-  std::string k;
+static int doc_keys_of(const Snapshot *S, uint8_t *buf, uint64_t cap, uint64_t *offsets, uint64_t *n_bytes) {
   uint64_t need = 0;
-  for (uint64_t d = 0; d < ix->n_docs; d++) {
-    const uint64_t st = staged_of(ix, d);
-    need += ix->key_synth[st] ? std::to_string(st).size() : ix->key_off[st + 1] - ix->key_off[st];
-  }
+  for (uint64_t d = 0; d < S->n_docs; d++) need += S->keys.key_len(S->staged_of(d));
   *n_bytes = need;
   if (need > cap || (need && !buf)) return fail(TFIDF_E_BUFFER, "keys need %llu bytes", (unsigned long long)need);
   uint64_t p = 0;
   offsets[0] = 0;
-  for (uint64_t d = 0; d < ix->n_docs; d++) {
-    const uint64_t st = staged_of(ix, d);
-    if (ix->key_synth[st]) {
-      k = std::to_string(st);
-      memcpy(buf + p, k.data(), k.size());
-      p += k.size();
-    } else {
-      const uint64_t n = ix->key_off[st + 1] - ix->key_off[st];
-      memcpy(buf + p, ix->key_arena.data() + ix->key_off[st], n);
-      p += n;
-    }
+  std::string k;
+  for (uint64_t d = 0; d < S->n_docs; d++) {
+    S->keys.key(S->staged_of(d), &k);
+    memcpy(buf + p, k.data(), k.size());
+    p += k.size();
     offsets[d + 1] = p;
   }
   return TFIDF_OK;
 }
 
+extern "C" int tfidf_doc_keys(const tfidf_index *ix, uint8_t *buf, uint64_t cap, uint64_t *offsets,
+                              uint64_t *n_bytes) {
+  if (!ix || !n_bytes || !offsets) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  const std::shared_ptr<Snapshot> S = current(ix);
+  if (!S) return fail(TFIDF_E_STATE, "not committed");
+  return doc_keys_of(S.get(), buf, cap, offsets, n_bytes);
+}
+
 extern "C" int tfidf_malformed_docs(const tfidf_index *ix, uint64_t *docs, uint64_t cap, uint64_t *n_out) {
   if (!ix || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
-  if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
-  *n_out = ix->malformed.size();
-  if (ix->malformed.size() > cap || (cap && !docs && !ix->malformed.empty()))
-    return fail(TFIDF_E_BUFFER, "need %zu entries", ix->malformed.size());
-  for (size_t i = 0; i < ix->malformed.size(); i++) docs[i] = ix->malformed[i];
+  const std::shared_ptr<Snapshot> S = current(ix);
+  if (!S) return fail(TFIDF_E_STATE, "not committed");
+  *n_out = S->malformed.size();
+  if (S->malformed.size() > cap || (cap && !docs && !S->malformed.empty()))
+    return fail(TFIDF_E_BUFFER, "need %zu entries", S->malformed.size());
+  for (size_t i = 0; i < S->malformed.size(); i++) docs[i] = S->malformed[i];
   return TFIDF_OK;
 }
 
 extern "C" int tfidf_doc_len(tfidf_index *ix, uint64_t doc, uint32_t *len, uint8_t *norm) {
   if (!ix) return fail(TFIDF_E_INVALID_ARG, "NULL index");
-  if (!ix->committed || doc >= ix->n_docs) return fail(TFIDF_E_INVALID_ARG, "doc out of range");
+  const std::shared_ptr<Snapshot> S = current(ix);
+  if (!S || doc >= S->n_docs) return fail(TFIDF_E_INVALID_ARG, "doc out of range");
   DeviceGuard g(ix->cfg.device);
   uint32_t l = 0;
   uint8_t n = 0;
-  HIP_TRY(hipMemcpy(&l, ix->doc_len.as<uint32_t>() + doc, 4, hipMemcpyDeviceToHost));
-  HIP_TRY(hipMemcpy(&n, ix->doc_norm.as<uint8_t>() + doc, 1, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(&l, S->doc_len.as<uint32_t>() + doc, 4, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(&n, S->doc_norm.as<uint8_t>() + doc, 1, hipMemcpyDeviceToHost));
   if (len) *len = l;
   if (norm) *norm = n;
   return TFIDF_OK;
@@ -2146,29 +2458,33 @@ extern "C" int tfidf_doc_len(tfidf_index *ix, uint64_t doc, uint32_t *len, uint8
 extern "C" int tfidf_doc_terms(tfidf_index *ix, uint64_t doc, char *terms, uint64_t terms_cap, uint32_t *tfs,
                                uint64_t cap, uint64_t *n_out) {
   if (!ix || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
-  if (!ix->committed || doc >= ix->n_docs) return fail(TFIDF_E_INVALID_ARG, "doc out of range");
+  const std::shared_ptr<Snapshot> snap = current(ix);
+  if (!snap || doc >= snap->n_docs) return fail(TFIDF_E_INVALID_ARG, "doc out of range");
+  Snapshot &S = *snap;
   DeviceGuard g(ix->cfg.device);
   uint32_t nu = 0;
-  HIP_TRY(hipMemcpy(&nu, ix->doc_nuniq.as<uint32_t>() + doc, 4, hipMemcpyDeviceToHost));
-  const uint64_t st = staged_of(ix, doc);
-  const uint64_t base = csr_row_base(ix->h_offsets.data(), st);
+  HIP_TRY(hipMemcpy(&nu, S.doc_nuniq.as<uint32_t>() + doc, 4, hipMemcpyDeviceToHost));
+  const uint64_t st = S.staged_of(doc);
+  uint64_t off_st = 0;                               // the document's corpus offset (its CSR row base)
+  HIP_TRY(hipMemcpy(&off_st, S.offsets->as<uint64_t>() + st, 8, hipMemcpyDeviceToHost));
+  const uint64_t base = (off_st + st) >> 1;          // csr_row_base
   // packed entries: the row's range segments (rsplit) give each slot's range
-  std::vector<uint32_t> ent(nu), col(nu), tf(nu), split(ix->R);
+  std::vector<uint32_t> ent(nu), col(nu), tf(nu), split(S.R);
   if (nu) {
-    HIP_TRY(hipMemcpy(ent.data(), ix->csr.as<uint32_t>() + base, nu * 4, hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(split.data(), ix->rsplit.as<uint32_t>() + doc * ix->R, ix->R * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(ent.data(), S.csr.as<uint32_t>() + base, nu * 4, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(split.data(), S.rsplit.as<uint32_t>() + doc * S.R, S.R * 4, hipMemcpyDeviceToHost));
   }
-  const uint32_t rs = ix->range_shift, esc = csr_esc_value(rs);
+  const uint32_t rs = S.range_shift, esc = csr_esc_value(rs);
   for (uint32_t i = 0, r = 0; i < nu; i++) {
-    while (r + 1 < ix->R && i >= split[r]) r++;
+    while (r + 1 < S.R && i >= split[r]) r++;
     col[i] = (r << rs) | csr_local(ent[i], rs);
     const uint32_t f = csr_tf_field(ent[i], rs);
-    tf[i] = f == esc ? csr_esc_tf(ix->h_esc.data(), ix->h_esc.size(), base + i) : f;
+    tf[i] = f == esc ? csr_esc_tf(S.h_esc.data(), S.h_esc.size(), base + i) : f;
   }
   std::vector<std::pair<std::string, uint32_t>> rows;
   for (uint32_t i = 0; i < nu; i++) {
     std::string t;
-    if (int rc = slot_term(ix, col[i], &t)) return rc;
+    if (int rc = slot_term(S, col[i], &t)) return rc;
     rows.emplace_back(std::move(t), tf[i]);
   }
   std::sort(rows.begin(), rows.end());
@@ -2188,13 +2504,16 @@ extern "C" int tfidf_doc_terms(tfidf_index *ix, uint64_t doc, char *terms, uint6
 extern "C" int tfidf_term_df(tfidf_index *ix, const uint8_t *term, uint64_t len, uint64_t *df_local,
                              uint64_t *df_effective) {
   if (!ix || (!term && len)) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
-  if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
-  if (int e = wait_gdf(ix)) return e;
+  std::shared_ptr<StatsView> V;
+  const std::shared_ptr<Snapshot> S = current(ix, &V);
+  if (!S) return fail(TFIDF_E_STATE, "not committed");
+  if (int e = V->wait_gdf()) return e;
+  DeviceGuard g(ix->cfg.device);
   std::string t((const char *)term, len);
-  const uint32_t s = lookup_term(ix, t);
-  const uint64_t l = s == kInvalidSlot ? 0 : ix->h_df[s];
+  const uint32_t s = lookup_term(*S, t);
+  const uint64_t l = s == kInvalidSlot ? 0 : S->h_df[s];
   if (df_local) *df_local = l;
-  if (df_effective) *df_effective = (s != kInvalidSlot && ix->has_global) ? ix->gdf[s] : l;
+  if (df_effective) *df_effective = (s != kInvalidSlot && V->global) ? V->gdf[s] : l;
   return TFIDF_OK;
 }
 
@@ -2229,23 +2548,25 @@ extern "C" int tfidf_analyze(const uint8_t *text, uint64_t len, char *out, uint6
 
 extern "C" int tfidf_vocab_size(const tfidf_index *ix, uint64_t *n) {
   if (!ix || !n) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
-  *n = ix->committed ? ix->num_terms : 0;
+  const std::shared_ptr<Snapshot> S = current(ix);
+  *n = S ? S->num_terms : 0;
   return TFIDF_OK;
 }
 
 extern "C" int tfidf_vocab_export_device(tfidf_index *ix, void *d_keys, void *d_df, uint64_t cap, uint64_t *n_out) {
   if (!ix || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
-  std::lock_guard<std::mutex> lk(ix->mu);
-  if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
+  const std::shared_ptr<Snapshot> snap = current(ix);
+  if (!snap) return fail(TFIDF_E_STATE, "not committed");
+  const Snapshot &S = *snap;
   DeviceGuard g(ix->cfg.device);
-  *n_out = ix->num_terms;
-  if (ix->num_terms > cap) return fail(TFIDF_E_BUFFER, "need %llu keys", (unsigned long long)ix->num_terms);
+  *n_out = S.num_terms;
+  if (S.num_terms > cap) return fail(TFIDF_E_BUFFER, "need %llu keys", (unsigned long long)S.num_terms);
   // sorted (hi, lo) key list of this shard + df, assembled from the host mirror
   std::vector<std::pair<std::pair<uint64_t, uint64_t>, uint32_t>> v;
-  v.reserve(ix->num_terms);
-  for (uint32_t s = 0; s < ix->C; s++)
-    if (ix->h_dict[s])
-      v.push_back({{ix->h_dict[(size_t)ix->C + s], ix->h_dict[s]}, ix->h_df[s]});
+  v.reserve(S.num_terms);
+  for (uint32_t s = 0; s < S.C; s++)
+    if (S.h_dict[s])
+      v.push_back({{S.h_dict[(size_t)S.C + s], S.h_dict[s]}, S.h_df[s]});
   std::sort(v.begin(), v.end());
   std::vector<uint64_t> keys(2 * v.size());
   std::vector<uint32_t> df(v.size());
@@ -2264,21 +2585,24 @@ extern "C" int tfidf_vocab_export_device(tfidf_index *ix, void *d_keys, void *d_
 extern "C" int tfidf_vocab_export(tfidf_index *ix, uint64_t *keys, uint32_t *df_local, uint32_t *df_effective,
                                   uint64_t cap, uint64_t *n_out) {
   if (!ix || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
-  std::lock_guard<std::mutex> lk(ix->mu);
-  if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
-  if (int e = wait_gdf(ix)) return e;
-  *n_out = ix->num_terms;
-  if (ix->num_terms > cap) return fail(TFIDF_E_BUFFER, "need %llu terms", (unsigned long long)ix->num_terms);
+  std::shared_ptr<StatsView> view;
+  const std::shared_ptr<Snapshot> snap = current(ix, &view);
+  if (!snap) return fail(TFIDF_E_STATE, "not committed");
+  const Snapshot &S = *snap;
+  StatsView &V = *view;
+  if (int e = V.wait_gdf()) return e;
+  *n_out = S.num_terms;
+  if (S.num_terms > cap) return fail(TFIDF_E_BUFFER, "need %llu terms", (unsigned long long)S.num_terms);
   std::vector<std::pair<std::pair<uint64_t, uint64_t>, uint32_t>> v;   // ((hi, lo), slot)
-  v.reserve(ix->num_terms);
-  for (uint32_t s = 0; s < ix->C; s++)
-    if (ix->h_dict[s]) v.push_back({{ix->h_dict[(size_t)ix->C + s], ix->h_dict[s]}, s});
+  v.reserve(S.num_terms);
+  for (uint32_t s = 0; s < S.C; s++)
+    if (S.h_dict[s]) v.push_back({{S.h_dict[(size_t)S.C + s], S.h_dict[s]}, s});
   std::sort(v.begin(), v.end());
   for (size_t i = 0; i < v.size(); i++) {
     const uint32_t s = v[i].second;
     if (keys) { keys[2 * i] = v[i].first.second; keys[2 * i + 1] = v[i].first.first; }
-    if (df_local) df_local[i] = ix->h_df[s];
-    if (df_effective) df_effective[i] = ix->has_global ? ix->gdf[s] : ix->h_df[s];
+    if (df_local) df_local[i] = S.h_df[s];
+    if (df_effective) df_effective[i] = V.global ? V.gdf[s] : S.h_df[s];
   }
   return TFIDF_OK;
 }
@@ -2287,7 +2611,9 @@ extern "C" int tfidf_vocab_canonicalize_device(tfidf_index *ix, const void *d_al
                                                void *d_df_canonical, uint64_t cap, uint64_t *n_canonical) {
   if (!ix || !n_canonical) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
   std::lock_guard<std::mutex> lk(ix->mu);
-  if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
+  const std::shared_ptr<Snapshot> snap = current(ix);
+  if (!snap) return fail(TFIDF_E_STATE, "not committed");
+  const Snapshot &S = *snap;
   DeviceGuard g(ix->cfg.device);
   hipStream_t s = ix->stream;
   DevBuf canon;
@@ -2296,12 +2622,11 @@ extern "C" int tfidf_vocab_canonicalize_device(tfidf_index *ix, const void *d_al
   HIP_TRY(sort_unique_keys128((const uint64_t *)d_all_keys, n_all, canon.as<uint64_t>(), &nu, s));
   *n_canonical = nu;
   if (nu > cap) { canon.release(); return fail(TFIDF_E_BUFFER, "need %llu canonical slots", (unsigned long long)nu); }
-  HIP_TRY(ix->canon_of_slot.reserve((size_t)ix->C * 4));
-  HIP_TRY(slot_to_canon(ix->dict.as<uint64_t>(), ix->C, canon.as<uint64_t>(), nu, ix->canon_of_slot.as<uint32_t>(), s));
+  HIP_TRY(ix->canon_of_slot.reserve((size_t)S.C * 4));
+  HIP_TRY(slot_to_canon(S.dict.as<uint64_t>(), S.C, canon.as<uint64_t>(), nu, ix->canon_of_slot.as<uint32_t>(), s));
   if (d_df_canonical) {
     HIP_TRY(hipMemsetAsync(d_df_canonical, 0, nu * 4, s));
-    HIP_TRY(scatter_df_canon(ix->df_dev(), ix->canon_of_slot.as<uint32_t>(),
-                             ix->C, (uint32_t *)d_df_canonical, s));
+    HIP_TRY(scatter_df_canon(S.df_dev(), ix->canon_of_slot.as<uint32_t>(), S.C, (uint32_t *)d_df_canonical, s));
   }
   HIP_TRY(hipStreamSynchronize(s));
   canon.release();
@@ -2325,21 +2650,23 @@ extern "C" int tfidf_vocab_partition_device(tfidf_index *ix, uint32_t n_ranks, v
   if (!ix || !n_out || !d_counts || n_ranks == 0 || n_ranks > 1024)
     return fail(TFIDF_E_INVALID_ARG, "NULL argument or n_ranks not in [1, 1024]");
   std::lock_guard<std::mutex> lk(ix->mu);
-  if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
+  const std::shared_ptr<Snapshot> snap = current(ix);
+  if (!snap) return fail(TFIDF_E_STATE, "not committed");
+  const Snapshot &S = *snap;
   DeviceGuard g(ix->cfg.device);
-  *n_out = ix->num_terms;
-  if (ix->num_terms > cap) return fail(TFIDF_E_BUFFER, "need %llu records", (unsigned long long)ix->num_terms);
-  if (ix->num_terms && !d_records) return fail(TFIDF_E_INVALID_ARG, "NULL records");
+  *n_out = S.num_terms;
+  if (S.num_terms > cap) return fail(TFIDF_E_BUFFER, "need %llu records", (unsigned long long)S.num_terms);
+  if (S.num_terms && !d_records) return fail(TFIDF_E_INVALID_ARG, "NULL records");
   hipStream_t s = ix->stream;
   HIP_TRY(ix->vcounts.reserve((size_t)n_ranks * 8 + 64));
-  HIP_TRY(ix->sent_slot.reserve(ix->num_terms * 4 + 4));
+  HIP_TRY(ix->sent_slot.reserve(S.num_terms * 4 + 4));
   uint32_t *cnt = ix->vcounts.as<uint32_t>(), *cur = cnt + n_ranks;
   HIP_TRY(hipMemsetAsync(cnt, 0, (size_t)n_ranks * 4, s));
-  HIP_TRY(vocab_count(ix->dict.as<uint64_t>(), ix->C, n_ranks, cnt, s));
+  HIP_TRY(vocab_count(S.dict.as<uint64_t>(), S.C, n_ranks, cnt, s));
   HIP_TRY(vocab_starts(cnt, n_ranks, cur, static_cast<uint64_t *>(d_counts), s));
-  HIP_TRY(vocab_scatter(ix->dict.as<uint64_t>(), ix->df_dev(), ix->C, n_ranks, cur, (uint64_t *)d_records,
+  HIP_TRY(vocab_scatter(S.dict.as<uint64_t>(), S.df_dev(), S.C, n_ranks, cur, (uint64_t *)d_records,
                         ix->sent_slot.as<uint32_t>(), s));
-  ix->n_sent = ix->num_terms;
+  ix->n_sent = S.num_terms;
   return exchange_done(ix);                            // asynchronous on a caller's stream
 }
 
@@ -2370,82 +2697,100 @@ extern "C" int tfidf_vocab_reduce_device(tfidf_index *ix, const void *d_records,
   return exchange_done(ix);                            // asynchronous on a caller's stream
 }
 
+// A new statistics view for the current snapshot (the GLOBAL setters): built
+// aside, complete on the device (norm cache uploaded) before searches see it.
+static int publish_view(tfidf_index *ix, Snapshot &S, const std::shared_ptr<StatsView> &v) {
+  if (int e = upload_cache(ix->cfg, *v, ix->stream)) return e;
+  std::lock_guard<std::mutex> sl(ix->snap_mu);
+  S.stats = v;
+  return TFIDF_OK;
+}
+
 extern "C" int tfidf_set_global_df_device(tfidf_index *ix, const void *d_df, uint64_t n, uint64_t doc_count,
                                           uint64_t sum_ttf) {
   if (!ix || (n && !d_df)) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
   std::lock_guard<std::mutex> lk(ix->mu);
-  if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
+  const std::shared_ptr<Snapshot> snap = current(ix);
+  if (!snap) return fail(TFIDF_E_STATE, "not committed");
+  Snapshot &S = *snap;
   if (n != ix->n_sent) return fail(TFIDF_E_STATE, "expected %llu records (tfidf_vocab_partition_device)",
                                    (unsigned long long)ix->n_sent);
   DeviceGuard g(ix->cfg.device);
   hipStream_t s = ix->stream;
-  if (int e = wait_gdf(ix)) return e;                  // the mirror buffer is about to be rewritten
-  HIP_TRY(ix->gdf_dev.reserve((size_t)ix->C * 4));
-  HIP_TRY(hipMemsetAsync(ix->gdf_dev.p, 0, (size_t)ix->C * 4, s));
+  auto v = std::make_shared<StatsView>(ix->cfg.device);
+  HIP_TRY(ix->gdf_dev.reserve((size_t)S.C * 4));
+  HIP_TRY(hipMemsetAsync(ix->gdf_dev.p, 0, (size_t)S.C * 4, s));
   HIP_TRY(vocab_import(ix->sent_slot.as<uint32_t>(), (const uint32_t *)d_df, n, ix->gdf_dev.as<uint32_t>(), s));
   // host mirror for query analysis: copied asynchronously, waited for by the
   // first query (prepare_query) — the exchange itself needs no host sync
-  HIP_TRY(ix->gdf.resize(ix->C));
-  HIP_TRY(hipMemcpyAsync(ix->gdf.data(), ix->gdf_dev.p, (size_t)ix->C * 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipEventRecord(ix->gdf_ev, s));
-  ix->gdf_pending = true;
-  ix->has_global = true;
-  ix->g_doc_count = doc_count;
-  ix->g_sum_ttf = sum_ttf;
+  HIP_TRY(v->gdf.resize(S.C));
+  HIP_TRY(hipMemcpyAsync(v->gdf.data(), ix->gdf_dev.p, (size_t)S.C * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipEventRecord(v->gdf_ev, s));
+  v->gdf_pending = true;
+  v->global = true;
+  v->doc_count = doc_count;
+  v->sum_ttf = sum_ttf;
   if (int e = exchange_done(ix)) return e;
-  return upload_cache(ix, false);
+  return publish_view(ix, S, v);
 }
 
 extern "C" int tfidf_set_global_stats_device(tfidf_index *ix, const void *d_df_canonical, uint64_t n_canonical,
                                              uint64_t doc_count, uint64_t sum_ttf) {
   if (!ix || !d_df_canonical) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
   std::lock_guard<std::mutex> lk(ix->mu);
-  if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
+  const std::shared_ptr<Snapshot> snap = current(ix);
+  if (!snap) return fail(TFIDF_E_STATE, "not committed");
+  Snapshot &S = *snap;
   if (n_canonical != ix->n_canon) return fail(TFIDF_E_STATE, "canonical vocabulary size mismatch");
   DeviceGuard g(ix->cfg.device);
   hipStream_t s = ix->stream;
+  auto v = std::make_shared<StatsView>(ix->cfg.device);
   DevBuf gd;
-  HIP_TRY(gd.reserve((size_t)ix->C * 4));
-  HIP_TRY(gather_df_canon((const uint32_t *)d_df_canonical, ix->canon_of_slot.as<uint32_t>(), ix->C,
+  HIP_TRY(gd.reserve((size_t)S.C * 4));
+  HIP_TRY(gather_df_canon((const uint32_t *)d_df_canonical, ix->canon_of_slot.as<uint32_t>(), S.C,
                           gd.as<uint32_t>(), s));
-  HIP_TRY(wait_gdf(ix) == TFIDF_OK ? hipSuccess : hipErrorUnknown);
-  HIP_TRY(ix->gdf.resize(ix->C));
-  HIP_TRY(hipMemcpyAsync(ix->gdf.data(), gd.p, (size_t)ix->C * 4, hipMemcpyDeviceToHost, s));
+  HIP_TRY(v->gdf.resize(S.C));
+  HIP_TRY(hipMemcpyAsync(v->gdf.data(), gd.p, (size_t)S.C * 4, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   gd.release();
-  ix->has_global = true;
-  ix->g_doc_count = doc_count;
-  ix->g_sum_ttf = sum_ttf;
-  return upload_cache(ix);
+  v->global = true;
+  v->doc_count = doc_count;
+  v->sum_ttf = sum_ttf;
+  return publish_view(ix, S, v);
 }
 
 extern "C" int tfidf_set_global_stats(tfidf_index *ix, const uint64_t *keys_lohi, const uint64_t *df, uint64_t n,
                                       uint64_t doc_count, uint64_t sum_ttf) {
   if (!ix || (n && (!keys_lohi || !df))) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
   std::lock_guard<std::mutex> lk(ix->mu);
-  if (!ix->committed) return fail(TFIDF_E_STATE, "not committed");
+  const std::shared_ptr<Snapshot> snap = current(ix);
+  if (!snap) return fail(TFIDF_E_STATE, "not committed");
+  Snapshot &S = *snap;
   DeviceGuard g(ix->cfg.device);
-  if (int e = wait_gdf(ix)) return e;
-  HIP_TRY(ix->gdf.assign(ix->C, 0));
-  for (uint32_t s = 0; s < ix->C; s++) ix->gdf[s] = ix->h_df[s];  // keys not listed keep local df
+  auto v = std::make_shared<StatsView>(ix->cfg.device);
+  HIP_TRY(v->gdf.assign(S.C, 0));
+  for (uint32_t s = 0; s < S.C; s++) v->gdf[s] = S.h_df[s];  // keys not listed keep local df
   for (uint64_t i = 0; i < n; i++) {
-    const uint32_t s = host_lookup(ix, keys_lohi[2 * i], keys_lohi[2 * i + 1]);
-    if (s != kInvalidSlot) ix->gdf[s] = (uint32_t)df[i];
+    const uint32_t s = host_lookup(S, keys_lohi[2 * i], keys_lohi[2 * i + 1]);
+    if (s != kInvalidSlot) v->gdf[s] = (uint32_t)df[i];
   }
-  ix->has_global = true;
-  ix->g_doc_count = doc_count;
-  ix->g_sum_ttf = sum_ttf;
-  return upload_cache(ix);
+  v->global = true;
+  v->doc_count = doc_count;
+  v->sum_ttf = sum_ttf;
+  return publish_view(ix, S, v);
 }
 
 extern "C" int tfidf_clear_global_stats(tfidf_index *ix) {
   if (!ix) return fail(TFIDF_E_INVALID_ARG, "NULL index");
   std::lock_guard<std::mutex> lk(ix->mu);
+  const std::shared_ptr<Snapshot> snap = current(ix);
+  if (!snap) return TFIDF_OK;
+  Snapshot &S = *snap;
   DeviceGuard g(ix->cfg.device);
-  if (int e = wait_gdf(ix)) return e;
-  ix->has_global = false;
-  ix->gdf.clear();
-  return ix->committed ? upload_cache(ix) : TFIDF_OK;
+  auto v = std::make_shared<StatsView>(ix->cfg.device);
+  v->doc_count = S.doc_count;
+  v->sum_ttf = S.sum_ttf;
+  return publish_view(ix, S, v);
 }
 
 // ---------------------------------------------------------------------------
@@ -2616,7 +2961,13 @@ extern "C" int tfidf_device_copy(int device, void *dst, const void *src, uint64_
 
 hipStream_t tfidf::index_stream(tfidf_index *ix) { return ix->stream; }
 int tfidf::index_device(const tfidf_index *ix) { return ix->cfg.device; }
-bool tfidf::index_committed(const tfidf_index *ix) { return ix->committed; }
-uint64_t tfidf::index_num_docs(const tfidf_index *ix) { return ix->committed ? ix->n_docs : 0; }
-uint64_t tfidf::index_generation(const tfidf_index *ix) { return ix->generation; }
+bool tfidf::index_committed(const tfidf_index *ix) { return current(ix) != nullptr; }
+uint64_t tfidf::index_num_docs(const tfidf_index *ix) {
+  const std::shared_ptr<Snapshot> S = current(ix);
+  return S ? S->n_docs : 0;
+}
+uint64_t tfidf::index_generation(const tfidf_index *ix) {
+  const std::shared_ptr<Snapshot> S = current(ix);
+  return S ? S->generation : 0;
+}
 int tfidf::set_error(int code, const char *msg) { return fail(code, "%s", msg); }

@@ -140,6 +140,12 @@ SIGNATURES = {
     "tfidf_dist_shard_search": (C.c_int, [VP, VP, C.c_char_p, C.c_uint64, U64P, U64P]),
     "tfidf_dist_last_hits": (C.c_int, [VP, U64P, F32P, C.c_uint64, U64P]),
     "tfidf_dist_last_failed": (C.c_int, [VP, U64P]),
+    "tfidf_reader_open": (C.c_int, [VP, C.POINTER(VP)]),
+    "tfidf_reader_close": (C.c_int, [VP]),
+    "tfidf_reader_info": (C.c_int, [VP, U64P, U64P]),
+    "tfidf_reader_search": (C.c_int, [VP, C.c_char_p, C.c_uint64, C.c_uint32, U32P, F32P, C.c_uint64, U64P]),
+    "tfidf_reader_doc_key": (C.c_int, [VP, C.c_uint64, C.c_char_p, C.c_uint64, U64P]),
+    "tfidf_reader_doc_keys": (C.c_int, [VP, C.c_char_p, C.c_uint64, U64P, U64P]),
     "tfidf_dist_last_names": (C.c_int, [VP, C.c_char_p, C.c_uint64, U64P, F64P, C.c_uint64, U64P, U64P]),
     "tfidf_node_create": (C.c_int, [VP, C.c_uint64, C.POINTER(VP)]),
     "tfidf_node_create_devices": (C.c_int, [VP, C.POINTER(C.c_int32), C.c_uint32, C.c_uint32, C.POINTER(VP)]),

@@ -121,16 +121,22 @@ class ShardIndex:
     # -- search (Worker.searchIndex) ------------------------------------------
     def search(self, query: bytes, k=0):
         """[(doc, float score)] in (score desc, doc asc); k == 0 -> all hits."""
+        if k == 0:                              # sized by the snapshot the search runs on
+            with self.reader() as rd:
+                return rd.search(query, 0)
         lib = L.load()
-        cap = max(k, 1) if k else max(self.stats()["num_docs"], 1)
-        docs = np.zeros(cap, np.uint32)
-        scores = np.zeros(cap, np.float32)
+        docs = np.zeros(k, np.uint32)
+        scores = np.zeros(k, np.float32)
         n = C.c_uint64()
         rc = lib.tfidf_search(self._h, query, len(query), k, L.ptr(docs, C.c_uint32), L.ptr(scores, C.c_float),
-                              cap, C.byref(n))
+                              k, C.byref(n))
         L.check(rc)
         m = n.value
         return list(zip(docs[:m].tolist(), scores[:m].tolist()))
+
+    def reader(self):
+        """A Reader on the snapshot published now (tfidf_reader_open)."""
+        return Reader(self)
 
     def search_coalesced(self, query: bytes, k, wait_us=50):
         """Thread-safe top-k search that shares one batched scoring launch with
@@ -146,14 +152,8 @@ class ShardIndex:
     def search_all_arrays(self, query: bytes):
         """All hits as (doc uint32[], score float32[]) in (score desc, doc asc)
         — searcher.search(q, Integer.MAX_VALUE) without per-hit Python objects."""
-        lib = L.load()
-        cap = max(self.stats()["num_docs"], 1)
-        docs = np.empty(cap, np.uint32)
-        scores = np.empty(cap, np.float32)
-        n = C.c_uint64()
-        L.check(lib.tfidf_search(self._h, query, len(query), 0, L.ptr(docs, C.c_uint32), L.ptr(scores, C.c_float),
-                                 cap, C.byref(n)))
-        return docs[:n.value], scores[:n.value]
+        with self.reader() as rd:
+            return rd.search_arrays(query, 0)
 
     def search_arrays(self, query: bytes, k):
         lib = L.load()
@@ -214,16 +214,8 @@ class ShardIndex:
 
     def doc_keys(self):
         """Every committed document's key: (uint8 blob, uint64 offsets[num_docs + 1])."""
-        lib = L.load()
-        n = self.stats()["num_docs"]
-        offs = np.zeros(n + 1, np.uint64)
-        need = C.c_uint64()
-        rc = lib.tfidf_doc_keys(self._h, None, 0, L.ptr(offs, C.c_uint64), C.byref(need))
-        if rc not in (L.OK, L.E_BUFFER):
-            L.check(rc)
-        buf = C.create_string_buffer(max(need.value, 1))
-        L.check(lib.tfidf_doc_keys(self._h, buf, need.value, L.ptr(offs, C.c_uint64), C.byref(need)))
-        return np.frombuffer(buf.raw[:need.value], np.uint8).copy(), offs
+        with self.reader() as rd:
+            return rd.doc_keys()
 
     def malformed_docs(self):
         """Committed doc ids whose bytes are not valid UTF-8 (indexed empty)."""
@@ -347,3 +339,64 @@ def leader_merge(responses):
     L.check(L.load().tfidf_leader_merge(names, L.ptr(offs, C.c_uint64), n, L.ptr(sc, C.c_double),
                                         L.ptr(first, C.c_uint64), L.ptr(sums, C.c_double), C.byref(m)))
     return [(flat[int(first[i])][0], float(sums[i])) for i in range(m.value)]
+
+
+class Reader:
+    """A pinned snapshot (tfidf_reader_*): Worker.java:223 opens a
+    DirectoryReader on the last commit per request and reads the hits' stored
+    "path" from it (:234-238); searches and doc keys here all see the commit
+    published when the reader was opened, whatever commits follow."""
+
+    def __init__(self, index):
+        self._h = C.c_void_p()
+        L.check(L.load().tfidf_reader_open(index._h, C.byref(self._h)))
+        g, n = C.c_uint64(), C.c_uint64()
+        L.check(L.load().tfidf_reader_info(self._h, C.byref(g), C.byref(n)))
+        self.generation, self.num_docs = g.value, n.value
+
+    def close(self):
+        if self._h:
+            L.load().tfidf_reader_close(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def search_arrays(self, query: bytes, k=0):
+        cap = max(k if k else self.num_docs, 1)
+        docs = np.empty(cap, np.uint32)
+        scores = np.empty(cap, np.float32)
+        n = C.c_uint64()
+        L.check(L.load().tfidf_reader_search(self._h, query, len(query), k, L.ptr(docs, C.c_uint32),
+                                             L.ptr(scores, C.c_float), cap, C.byref(n)))
+        return docs[:n.value], scores[:n.value]
+
+    def search(self, query: bytes, k=0):
+        d, s = self.search_arrays(query, k)
+        return list(zip(d.tolist(), s.tolist()))
+
+    def doc_key(self, doc):
+        buf = C.create_string_buffer(4096)
+        n = C.c_uint64()
+        L.check(L.load().tfidf_reader_doc_key(self._h, doc, buf, 4096, C.byref(n)))
+        return buf.raw[:n.value]
+
+    def doc_keys(self):
+        lib = L.load()
+        offs = np.zeros(self.num_docs + 1, np.uint64)
+        need = C.c_uint64()
+        rc = lib.tfidf_reader_doc_keys(self._h, None, 0, L.ptr(offs, C.c_uint64), C.byref(need))
+        if rc not in (L.OK, L.E_BUFFER):
+            L.check(rc)
+        buf = C.create_string_buffer(max(need.value, 1))
+        L.check(lib.tfidf_reader_doc_keys(self._h, buf, need.value, L.ptr(offs, C.c_uint64), C.byref(need)))
+        return np.frombuffer(buf.raw[:need.value], np.uint8).copy(), offs

@@ -136,8 +136,10 @@ class Worker:
 
     # Worker.java:222-241 searchIndex: every hit, score desc / doc asc
     def search_index(self, query: str):
-        hits = self.index.search(query.encode(), k=0)
-        return [document_score_info(self.index.doc_key(d).decode(), s) for d, s in hits]
+        # one reader per request: hits and their stored paths from the same commit (:223, :234-238)
+        with self.index.reader() as rd:
+            hits = rd.search(query.encode(), 0)
+            return [document_score_info(rd.doc_key(d).decode(), s) for d, s in hits]
 
     # Worker.java:175-186 /worker/process: any exception -> empty list
     def process_documents(self, search_query: str):
