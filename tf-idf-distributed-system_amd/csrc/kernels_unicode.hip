@@ -160,6 +160,8 @@ struct UwSmem {
   uint32_t rcnt[kUwMaxRanges];        // per-range counts, then cursors
   uint8_t tr[kUwStates * kUwClasses]; // WORD DFA transitions
   uint8_t asc[128];                   // ASCII byte -> scanner class
+  uint32_t isl[64];                   // sparse path: islands (window start | end << 16)
+  uint32_t n_isl, n_tok;              // sparse path: counters
 };
 
 __device__ __forceinline__ uint32_t uw_incl_add(uint32_t x, uint32_t lane) {
@@ -169,6 +171,245 @@ __device__ __forceinline__ uint32_t uw_incl_add(uint32_t x, uint32_t lane) {
     if (lane >= (uint32_t)o) x += y;
   }
   return x;
+}
+
+
+// ---------------------------------------------------------------------------
+// Sparse non-ASCII documents (round 5): most of a real document is ASCII
+// words with a few non-ASCII chars (accents, curly quotes).  A token never
+// crosses an ASCII byte of class OTHER (a split byte) and JFlex never looks
+// behind, so the document splits into pieces between split bytes that scan
+// independently from the start state.  Pieces without a byte >= 0x80 take the
+// ASCII word rules of the wave tokenizer (SWAR word masks, token spans by bit
+// operations: the same tokens as the scanner there); only the "islands" —
+// pieces holding a non-ASCII byte — go through the longest-match scanner, one
+// island per lane.  Every token lands in a dense list, inserted into the
+// document's table 64 per round (no lane waits on another lane's scan).
+// Documents whose non-ASCII text is not sparse (more than kUwIslands islands,
+// a piece over kUwMaxPiece bytes, more island bytes than the class buffer, an
+// ASCII token over 255 chars, more than kUwTokens tokens, malformed UTF-8)
+// take the full per-lane scan below.
+constexpr uint32_t kUwTokens = 1024;       // token list (in the class-byte area)
+constexpr uint32_t kUwIslands = 64;
+constexpr uint32_t kUwIslandBytes = kUwSlots * 2 - 32;   // island class bytes (in the occ area, + read slack)
+constexpr uint32_t kUwMaxPiece = 512;
+static_assert(kUwTokens * 4 <= kUwWindow, "token list in cls");
+
+__device__ __forceinline__ uint32_t uw_eq(uint32_t x, uint32_t c4) { return ~((x ^ c4) + 0x7F7F7F7Fu) & 0x80808080u; }
+__device__ __forceinline__ uint32_t uw_letter(uint32_t x) {
+  const uint32_t lw = x | 0x20202020u;
+  return (lw + 0x1F1F1F1Fu) & ~(lw + 0x05050505u) & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t uw_digit(uint32_t x) { return (x + 0x50505050u) & ~(x + 0x46464646u) & 0x80808080u; }
+__device__ __forceinline__ uint32_t uw_nib(uint32_t w) {
+  const uint32_t f = (w >> 7) & 0x01010101u;
+  const uint32_t g = f | (f >> 7);
+  return (g | (g >> 14)) & 0xFu;
+}
+__device__ __forceinline__ uint32_t uw_keep(uint32_t q, uint32_t lo, uint32_t hi) {   // bytes of dword q in [lo, hi)
+  const uint32_t a = q >= lo ? 0xFFFFFFFFu : (lo - q >= 4 ? 0u : (0xFFFFFFFFu << (8 * (lo - q))));
+  const uint32_t b = q + 4 <= hi ? 0xFFFFFFFFu : (hi <= q ? 0u : (0xFFFFFFFFu >> (8 * (q + 4 - hi))));
+  return a & b;
+}
+__device__ __forceinline__ bool uw_split_at(const uint8_t *text, uint32_t w, uint32_t lo, uint32_t hi) {
+  return w < lo || w >= hi || uc_split_byte(text[w]);
+}
+
+// Masks of window bytes [64 lane, 64 lane + 64), document bytes [lo, hi):
+// *W ASCII word bytes (letters, digits, '_', joiners between letters / digits:
+// the wave tokenizer's rules), *NA bytes >= 0x80, *SP split bytes (ASCII class
+// OTHER, and every byte outside the document).  Non-ASCII bytes are cleared
+// before the byte-wise arithmetic (no carries) and are never word bytes here.
+__device__ __forceinline__ void uw_lane_masks(const uint8_t *text, uint32_t lane, uint32_t lo, uint32_t hi,
+                                              uint64_t *W, uint64_t *NA, uint64_t *SP) {
+  uint32_t x[16];
+  {
+    const uint4 *t = reinterpret_cast<const uint4 *>(text + lane * 64);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint4 v = t[k];
+      x[4 * k] = v.x; x[4 * k + 1] = v.y; x[4 * k + 2] = v.z; x[4 * k + 3] = v.w;
+    }
+  }
+  uint32_t LD[16];
+  uint64_t na = 0, sp = 0;
+  bool mid = false;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    x[i] &= uw_keep(64 * lane + 4 * i, lo, hi);
+    const uint32_t hb = x[i] & 0x80808080u;
+    na |= (uint64_t)uw_nib(hb) << (4 * i);
+    x[i] &= ~((hb >> 7) * 0xFFu);
+    const uint32_t D = uw_digit(x[i]), Lt = uw_letter(x[i]);
+    LD[i] = Lt | (D >> 1);
+    const uint32_t j = uw_eq(x[i], 0x3A3A3A3Au) | uw_eq(x[i], 0x2E2E2E2Eu) | uw_eq(x[i], 0x2C2C2C2Cu) |
+                       uw_eq(x[i], 0x3B3B3B3Bu) | uw_eq(x[i], 0x27272727u);
+    mid |= j != 0;
+    const uint32_t keep = Lt | D | j | uw_eq(x[i], 0x5F5F5F5Fu) | uw_eq(x[i], 0x22222222u);
+    sp |= (uint64_t)uw_nib(~keep & 0x80808080u) << (4 * i);
+  }
+  uint32_t ldp = (uint32_t)__shfl_up((int)LD[15], 1, 64);
+  uint32_t ldn = (uint32_t)__shfl_down((int)LD[0], 1, 64);
+  if (lane == 0) ldp = 0;
+  if (lane == 63) ldn = 0;
+  const bool mids = __any(mid);
+  uint64_t w = 0;
+#pragma unroll
+  for (int i = 0; i < 16; i++) {
+    uint32_t c = LD[i] | (LD[i] << 1) | uw_eq(x[i], 0x5F5F5F5Fu);
+    if (mids) {
+      const uint32_t prev4 = i ? LD[i - 1] : ldp;
+      const uint32_t next4 = i < 15 ? LD[i + 1] : ldn;
+      const uint32_t pf = __builtin_amdgcn_alignbyte(LD[i], prev4, 3);
+      const uint32_t nf = __builtin_amdgcn_alignbyte(next4, LD[i], 1);
+      const uint32_t both = pf & nf;
+      const uint32_t dq = uw_eq(x[i], 0x2E2E2E2Eu) | uw_eq(x[i], 0x27272727u);
+      const uint32_t ml = dq | uw_eq(x[i], 0x3A3A3A3Au);
+      const uint32_t mn = dq | uw_eq(x[i], 0x2C2C2C2Cu) | uw_eq(x[i], 0x3B3B3B3Bu);
+      c |= (ml & both) | (mn & (both << 1));
+    }
+    w |= (uint64_t)uw_nib(c & 0x80808080u) << (4 * i);
+  }
+  *W = w;
+  *NA = na;
+  *SP = sp & ~na;
+}
+
+// The sparse path's token list: sm.cls as u32 entries (document start | end
+// << 16).  Returns false (wave-uniform) when the document must take the full
+// scan; else *ntok entries are listed.
+__device__ __forceinline__ bool uw_sparse_tokens(UwSmem &sm, const BuildParams &p, uint32_t lane, uint32_t shift, uint32_t L,
+                                 uint32_t *ntok) {
+  const uint32_t lo = shift, hi = shift + L;
+  uint64_t W, NA, SP;
+  uw_lane_masks(sm.text, lane, lo, hi, &W, &NA, &SP);
+  if (lane == 0) { sm.n_isl = 0; sm.n_tok = 0; }
+  __syncthreads();
+  // islands: the first non-ASCII byte of each piece finds the piece's ends
+  bool fb = false;
+  {
+    uint64_t m = NA;
+    uint32_t prev = 0xFFFFFFFFu;                        // previous non-ASCII bit of this lane
+    while (m) {
+      const uint32_t b = (uint32_t)__builtin_ctzll(m);
+      m &= m - 1;
+      // a non-ASCII byte of this lane before it with no split byte in between: same piece
+      if (prev != 0xFFFFFFFFu && ((SP >> prev) & ((1ull << (b - prev)) - 1)) == 0) { prev = b; continue; }
+      prev = b;
+      const uint32_t w = 64 * lane + b;
+      uint32_t a = w;                                   // piece start: after the last split byte
+      bool first = true;
+      while (!uw_split_at(sm.text, a - 1, lo, hi)) {
+        if (sm.text[a - 1] >= 0x80u) { first = false; break; }
+        if (w - a >= kUwMaxPiece) { fb = true; break; }
+        a--;
+      }
+      if (!first || fb) continue;
+      uint32_t z = w + 1;                               // piece end: the next split byte
+      while (!uw_split_at(sm.text, z, lo, hi)) {
+        if (z - a >= kUwMaxPiece) { fb = true; break; }
+        z++;
+      }
+      if (fb) continue;
+      const uint32_t at = atomicAdd(&sm.n_isl, 1u);
+      if (at < kUwIslands) sm.isl[at] = a | (z << 16);
+      else fb = true;
+    }
+  }
+  __syncthreads();
+  const uint32_t n_isl = sm.n_isl;
+  if (__any(fb) || n_isl > kUwIslands) return false;
+  // ASCII tokens outside the islands
+  {
+    const uint32_t w0 = 64 * lane;
+    uint64_t I = 0;
+    for (uint32_t j = 0; j < n_isl; j++) {
+      const uint32_t e = sm.isl[j], a = max(e & 0xFFFFu, w0), z = min(e >> 16, w0 + 64);
+      if (a < z) I |= (z - a == 64 ? ~0ull : ((1ull << (z - a)) - 1)) << (a - w0);
+    }
+    W &= ~I;
+  }
+  const uint64_t wlast = __ballot((W >> 63) & 1ull);
+  const uint64_t prevW = lane ? (wlast >> (lane - 1)) & 1ull : 0ull;
+  const uint64_t S = W & ~((W << 1) | prevW);
+  uint64_t E = ~W & ((W << 1) | prevW);
+  const uint32_t firstE = E ? lane * 64 + (uint32_t)__builtin_ctzll(E) : kUwWindow;
+  const uint64_t hasE = __ballot(E != 0);
+  const uint64_t later = lane == 63 ? 0ull : (hasE & (~0ull << (lane + 1)));
+  const uint32_t srcl = later ? (uint32_t)__builtin_ctzll(later) : lane;
+  uint32_t nz = (uint32_t)__shfl((int)firstE, (int)srcl, 64);
+  if (!later) nz = kUwWindow;
+  if (prevW) E &= E - 1;                                // closes the token open from lane - 1
+  const uint32_t nts = (uint32_t)__popcll(S);
+  const uint32_t incl = uw_incl_add(nts, lane);
+  const uint32_t nasc = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+  if (nasc > kUwTokens) return false;
+  uint32_t *tok = reinterpret_cast<uint32_t *>(sm.cls);
+  bool toolong = false;
+  {
+    uint32_t at = incl - nts;
+    uint64_t s = S, e = E;
+    while (s) {
+      const uint32_t tp = lane * 64 + (uint32_t)__builtin_ctzll(s);
+      const uint32_t te = e ? lane * 64 + (uint32_t)__builtin_ctzll(e) : nz;
+      s &= s - 1;
+      e &= e - 1;
+      toolong |= te - tp > kMaxTokenLen;
+      tok[at++] = (tp - shift) | ((te - shift) << 16);
+    }
+  }
+  if (__any(toolong)) return false;                     // the 255-char cut: the full scan does it
+  if (lane == 0) sm.n_tok = nasc;
+  // island class bytes (in the occ area): island j at an offset congruent to
+  // its document start mod 4, so the scanner's aligned 4-byte class reads line up
+  uint8_t *cb = reinterpret_cast<uint8_t *>(sm.occ);
+  uint32_t a = 0, z = 0;
+  const bool mine = lane < n_isl;
+  if (mine) {
+    const uint32_t e = sm.isl[lane];
+    a = (e & 0xFFFFu) - shift;
+    z = (e >> 16) - shift;
+  }
+  const uint32_t need = mine ? ((z - a + 1 + 3) & ~3u) + 8 : 0u;
+  const uint32_t ni = uw_incl_add(need, lane);
+  if ((uint32_t)__builtin_amdgcn_readlane((int)ni, 63) > kUwIslandBytes) return false;
+  const uint32_t off = ni - need + (a & 3);
+  bool bad = false;
+  if (mine) {
+    const uint8_t *doc = sm.text + shift;
+    const uint32_t zc = min(z + 1, L);                  // the split byte at z closes the scan
+    for (uint32_t i = a; i < zc; i++) {
+      const uint32_t x = doc[i];
+      uint32_t v;
+      if (x < 0x80u) v = sm.asc[x];
+      else if ((x & 0xC0u) == 0x80u) v = 0xFFu;
+      else {
+        uint32_t l;
+        const uint32_t cp = utf8_decode(doc, L, i, &l);
+        v = cp == kUcBad ? 0xFFu : (uc_class(cp) | ((l - 1) << 5));
+      }
+      cb[off + (i - a)] = (uint8_t)v;
+    }
+  }
+  __syncthreads();
+  if (mine) {
+    const uint8_t *cl = cb + off - a;                   // class byte of document position i: cl[i]
+    const uint32_t n = min(z + 1, L);
+    uint32_t pos = a, ts, te;
+    bool at_end = false;
+    while (pos < z && uc_window_span(cl, sm.tr, n, &pos, z, &ts, &te, &bad, &at_end)) {
+      if (te - ts > kMaxTokenLen) {                     // > 255 bytes: maybe > 255 UTF-16 units (cut)
+        uint64_t klo, khi;
+        const uint64_t cut = uc_token_key(sm.text + shift, L, ts, te, &klo, &khi, p.hash_seed);
+        if (cut < te) { te = (uint32_t)cut; pos = te; }
+      }
+      const uint32_t at = atomicAdd(&sm.n_tok, 1u);
+      if (at < kUwTokens) tok[at] = ts | (te << 16);
+    }
+  }
+  __syncthreads();
+  *ntok = sm.n_tok;
+  return !__any(bad) && *ntok <= kUwTokens;
 }
 
 // Documents flagged by k_tokenize_wave (uni_list[d] != 0: a flag per
@@ -219,69 +460,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     for (uint32_t c = lane; c < nchunks; c += 64) dst[c] = gsrc[c];
     sm.rcnt[lane] = 0;
     __syncthreads();
+    if (p.debug_stop == 10) continue;                       // profiling only: phase stops 10..13
     const uint8_t *doc = sm.text + shift;
-    // ---- classes, four consecutive bytes per lane per step
-    for (uint32_t i0 = 4 * lane; i0 < L; i0 += 256) {
-      uint32_t w = 0;
-#pragma unroll
-      for (int b = 0; b < 4; b++) w |= (i0 + b < L ? (uint32_t)doc[i0 + b] : 0x20u) << (8 * b);
-      uint32_t out = 0;
-      if ((w & 0x80808080u) == 0) {
-#pragma unroll
-        for (int b = 0; b < 4; b++) out |= (uint32_t)sm.asc[(w >> (8 * b)) & 0x7Fu] << (8 * b);
-      } else {
-#pragma unroll
-        for (int b = 0; b < 4; b++) {
-          const uint32_t x = (w >> (8 * b)) & 0xFFu;
-          uint32_t v;
-          if (x < 0x80u) v = sm.asc[x];
-          else if ((x & 0xC0u) == 0x80u || i0 + b >= L) v = 0xFFu;
-          else {
-            uint32_t l;
-            const uint32_t cp = utf8_decode(doc, L, i0 + b, &l);
-            v = cp == kUcBad ? 0xFFu : (uc_class(cp) | ((l - 1) << 5));
-          }
-          out |= v << (8 * b);
-        }
-      }
-      *reinterpret_cast<uint32_t *>(&sm.cls[i0]) = out;      // bytes past L: never taken
-    }
-    __syncthreads();
-
-    // ---- slices: lane l scans tokens starting in [cut(l), cut(l + 1))
-    const uint64_t seg = (L + 63) >> 6;
-    auto cut = [&](uint64_t t) -> uint64_t {
-      if (t == 0) return 0;
-      uint64_t q = t * seg;
-      if (q >= L) return L;
-      while (q < L && !uc_split_byte(doc[q - 1])) q++;
-      return q;
-    };
-    uint32_t pos = (uint32_t)cut(lane);
-    const uint32_t stop = (uint32_t)cut(lane + 1);
-    bool active = pos < stop, ubad = false, overflow = false, at_end = false;
+    bool ubad = false, overflow = false, at_end = false, collide = false;
     uint32_t ntok = 0;
-    bool collide = false;
-    while (__any(active)) {
-      uint64_t lo = 0, hi = 0;
-      bool have = false;
-      uint32_t ts32 = 0, te32 = 0;
-      if (active) {
-        uint32_t p32 = pos;
-        have = uc_window_span(sm.cls, sm.tr, (uint32_t)L, &p32, stop, &ts32, &te32, &ubad, &at_end);
-        if (have) {
-          if (te32 - ts32 <= 8 && uc_short_ascii_key(sm.text, shift + ts32, te32 - ts32, &lo)) {
-            hi = kKeyValid;                                   // most tokens: <= 8 ASCII bytes
-          } else {
-            const uint64_t cutp = uc_token_key(doc, L, ts32, te32, &lo, &hi, p.hash_seed);
-            if (cutp < te32) { p32 = (uint32_t)cutp; te32 = (uint32_t)cutp; }   // 255-unit cut: rescan from the cut
-          }
-        }
-        pos = p32;
-        active = have;
-      }
-      ntok += have;
-      // round insert: probe from the key's home slot, linear
+    // round insert of each lane's token (have): probe from the key's home slot, linear
+    auto insert = [&](uint64_t lo, uint64_t hi, bool have, uint32_t ts32, uint32_t te32) {
       uint32_t slot = dict_hash(lo, hi) >> (32 - kUwSlotBits);
       bool done = !have;
       for (uint32_t r = 0; r < kUwSlots && __any(!done); r++) {
@@ -304,7 +488,99 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         }
       }
       overflow |= !done;
+    };
+    // ---- sparse non-ASCII text (round 5): ASCII words by the wave rules, the
+    // islands around non-ASCII bytes by the scanner; tokens inserted 64 a round
+    uint32_t nlist = 0;
+    const bool sparse = !p.debug_uw_full && shift + (uint32_t)L <= kUwWindow &&
+                        uw_sparse_tokens(sm, p, lane, shift, (uint32_t)L, &nlist);
+    if (p.debug_stop == 11) continue;
+    uint32_t pos = 0, stop = 0;
+    if (!sparse) {
+      // ---- classes, four consecutive bytes per lane per step
+      for (uint32_t i0 = 4 * lane; i0 < L; i0 += 256) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) w |= (i0 + b < L ? (uint32_t)doc[i0 + b] : 0x20u) << (8 * b);
+        uint32_t out = 0;
+        if ((w & 0x80808080u) == 0) {
+#pragma unroll
+          for (int b = 0; b < 4; b++) out |= (uint32_t)sm.asc[(w >> (8 * b)) & 0x7Fu] << (8 * b);
+        } else {
+#pragma unroll
+          for (int b = 0; b < 4; b++) {
+            const uint32_t x = (w >> (8 * b)) & 0xFFu;
+            uint32_t v;
+            if (x < 0x80u) v = sm.asc[x];
+            else if ((x & 0xC0u) == 0x80u || i0 + b >= L) v = 0xFFu;
+            else {
+              uint32_t l;
+              const uint32_t cp = utf8_decode(doc, L, i0 + b, &l);
+              v = cp == kUcBad ? 0xFFu : (uc_class(cp) | ((l - 1) << 5));
+            }
+            out |= v << (8 * b);
+          }
+        }
+        *reinterpret_cast<uint32_t *>(&sm.cls[i0]) = out;      // bytes past L: never taken
+      }
+      __syncthreads();
+      // ---- slices: lane l scans tokens starting in [cut(l), cut(l + 1))
+      const uint64_t seg = (L + 63) >> 6;
+      auto cut = [&](uint64_t t) -> uint64_t {
+        if (t == 0) return 0;
+        uint64_t q = t * seg;
+        if (q >= L) return L;
+        while (q < L && !uc_split_byte(doc[q - 1])) q++;
+        return q;
+      };
+      pos = (uint32_t)cut(lane);
+      stop = (uint32_t)cut(lane + 1);
     }
+    // ---- tokens, one per lane per round: the sparse path's list, or the
+    // full scan of the lane's slice; each round inserted into the table
+    bool active = sparse ? nlist > 0 : pos < stop;
+    const uint32_t *tok = reinterpret_cast<const uint32_t *>(sm.cls);
+    for (uint32_t t0 = 0; __any(active); t0 += 64) {
+      uint64_t lo = 0, hi = 0;
+      bool have = false;
+      uint32_t ts32 = 0, te32 = 0;
+      if (sparse) {
+        const uint32_t i = t0 + lane;
+        have = i < nlist;
+        if (have) {
+          const uint32_t e = tok[i];
+          ts32 = e & 0xFFFFu;
+          te32 = e >> 16;
+        }
+        active = t0 + 64 < nlist;
+      } else if (active) {
+        uint32_t p32 = pos;
+        have = uc_window_span(sm.cls, sm.tr, (uint32_t)L, &p32, stop, &ts32, &te32, &ubad, &at_end);
+        pos = p32;
+        active = have;
+      }
+      if (have) {
+        const uint32_t n = te32 - ts32;
+        if (n <= 8 && uc_short_ascii_key(sm.text, shift + ts32, n, &lo)) {
+          hi = kKeyValid;                                     // most tokens: <= 8 ASCII bytes
+          // sparse list: a run of '_' alone is not a token (the scanner never yields one)
+          have = lo != (0x5F5F5F5F5F5F5F5Full >> (8 * (8 - n)));
+        } else {
+          if (sparse && doc[ts32] == '_') {
+            bool under = true;
+            for (uint32_t j = ts32 + 1; under && j < te32; j++) under = doc[j] == '_';
+            have = !under;
+          }
+          if (have) {
+            const uint64_t cutp = uc_token_key(doc, L, ts32, te32, &lo, &hi, p.hash_seed);
+            if (cutp < te32) { pos = (uint32_t)cutp; te32 = (uint32_t)cutp; }   // 255-unit cut: rescan from the cut
+          }
+        }
+      }
+      ntok += have;
+      insert(lo, hi, have, ts32, te32);
+    }
+    (void)at_end;
     if (collide) set_build_err(p.err, kErrCollision, d);
     // ---- occupied slots, compacted (lane l: slots [16 l, 16 l + 16))
     uint32_t nu;
@@ -322,8 +598,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       }
     }
     __syncthreads();
-    if (__any(ubad) || __any(overflow) || nu > kUwMaxTerms) {   // wave-uniform: the long path
-      if (lane == 0) p.long_list[atomicAdd(p.long_count, 1u)] = d;
+    if (__any(ubad) || __any(overflow) || nu > kUwMaxTerms || p.debug_stop == 12) {   // wave-uniform: the long path
+      if (lane == 0 && p.debug_stop != 12) p.long_list[atomicAdd(p.long_count, 1u)] = d;
       for (uint32_t i = lane; i < nu; i += 64) {
         const uint32_t s = sm.occ[i];
         sm.klo[s] = 0; sm.khi[s] = 0; sm.cnt[s] = 0;
@@ -361,6 +637,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       }
     }
     __syncthreads();
+    if (p.debug_stop == 13) {
+      for (uint32_t i = lane; i < nu; i += 64) {
+        const uint32_t s = sm.occ[i];
+        sm.klo[s] = 0; sm.khi[s] = 0; sm.cnt[s] = 0;
+      }
+      __syncthreads();
+      continue;
+    }
     // ---- row segments: inclusive ends per range, cursors = exclusive starts
     {
       const uint32_t c = lane < R ? sm.rcnt[lane] : 0u;

@@ -1021,6 +1021,7 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
   bp.stats = reinterpret_cast<unsigned long long *>(ctr);
   bp.err = reinterpret_cast<uint32_t *>(ctr + 3);
   if (const char *ds = getenv("TFIDF_DEBUG_STOP")) bp.debug_stop = (uint32_t)atoi(ds);   // profiling only
+  if (const char *uf = getenv("TFIDF_UW_FULL")) bp.debug_uw_full = (uint32_t)atoi(uf);   // A/B only
   bp.pack = pack;
   bp.retry_list = pack > 1 ? ix->retry_list.as<uint32_t>() : nullptr;
   bp.retry_count = reinterpret_cast<uint32_t *>(ctr + 5);
@@ -1049,7 +1050,7 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
       }
     }
     // documents with non-ASCII text (count read on the device; exits at once when none)
-    if (!bp.debug_stop)
+    if (!bp.debug_stop || bp.debug_stop >= 10)          // (stops 10..13: the Unicode wave path's phases)
       HIP_TRY(launch_tokenize_uwave(bp, (int)std::min<uint64_t>(N, (uint64_t)ix->num_cus * kUwaveWGsPerCU), s));
   }
   HIP_TRY(hipEventRecord(ix->ev[EV_TOK], s));

@@ -58,6 +58,7 @@ struct BuildParams {
   uint32_t *lt_g;             // lt_slots per workgroup
   uint32_t lt_slots_log2;     // table slots per workgroup (max)
   uint32_t debug_stop;        // profiling only (TFIDF_DEBUG_STOP): end each document after phase N
+  uint32_t debug_uw_full;     // A/B only (TFIDF_UW_FULL): the Unicode wave path always scans whole documents
   // wave path units: pack > 1 = packs of `pack` consecutive documents per
   // window (short-document corpora); documents a pack cannot take go to
   // retry_list.  doc_list (pack <= 1): process these documents only
