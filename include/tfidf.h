@@ -107,7 +107,7 @@ typedef struct tfidf_index_stats {
   uint64_t term_major;    /* 1 if the last commit built the term-major layout (TFIDF_INVERSION_TERM) */
   uint64_t pack_docs;     /* documents per tokenizer window in the last commit (1 = one per window) */
   uint64_t pack_retried;  /* documents the packed windows handed to the one-per-window pass */
-  uint64_t unicode_docs;  /* documents (window <= 4 KB) the ASCII wave path handed to the Unicode wave path */
+  uint64_t unicode_docs;  /* documents (window <= 4 KB) the ASCII wave path found non-ASCII text in */
   uint64_t long_chunked;  /* long documents indexed chunk-parallel (the rest of long_docs: k_tokenize_long) */
   uint64_t malformed_docs;/* documents that are not valid UTF-8, indexed empty (tfidf_malformed_docs) */
   uint64_t hash_seed;     /* seed of the hashed term keys (> 16-byte and non-ASCII terms); 0 unless a
@@ -120,6 +120,8 @@ typedef struct tfidf_index_stats {
   uint64_t unit_batches;   /* batched top-k searches scored by query units (k_score_units) / units run */
   uint64_t unit_count;
   uint64_t fused_queries;  /* tfidf_search top-k calls served by the one-launch fused path (index lifetime) */
+  uint64_t unicode_wave_docs;  /* of unicode_docs: those the wave rules took (non-ASCII letters that are
+                                  ALetter and lower case only); the rest went to the Unicode wave path */
 } tfidf_index_stats;
 
 /* Per-phase device times of the last commit, measured with HIP events on the

@@ -1,0 +1,127 @@
+"""Non-ASCII documents by the wave rules (round 5, kernels_index.hip
+k_tokenize_wave<UNI>): a document the ASCII pass flagged whose non-ASCII
+chars are all well-formed ALetter code points that are their own lower case
+(é ü ñ ß ø α я ...) is tokenized by the SWAR word rules with those bytes read
+as letters; its tokens holding a non-ASCII byte take folded table keys and the
+Unicode key builder.  Everything else (upper case, Han, Katakana, Hebrew,
+combining marks, emoji, malformed bytes) stays with k_tokenize_uwave.
+
+Checked against the CPU oracle (oracle/tfidf_oracle.c, the checker) with the
+wave rules on and off (TFIDF_NO_UNIWAVE=1: every flagged document to the
+Unicode wave path), on documents that put simple letters next to every
+joiner, at the 64-byte lane edges (a char split across two lanes), in tokens
+of <= 8 and > 8 bytes, mixed with ASCII case variants of the same term, and
+next to documents the wave rules must decline.  Bar: TF / DF / lengths /
+norms / hits bit-exact, and the declined documents counted apart.
+"""
+import random
+
+import pytest
+
+from oracle import oracle as O
+from tfidf_amd import synth
+from tfidf_amd.engine import ShardIndex
+
+from test_gpu_parity import assert_hits_equal
+from test_gpu_unicode_sparse import build_pair, check
+
+pytestmark = pytest.mark.gpu
+
+SIMPLE = ["é", "ü", "ñ", "ß", "ø", "å", "ł", "ş", "α", "ω", "я", "ж", "ə", "ŋ", "ǆ", "ﬁ"]
+WORDS = ["café", "naïve", "über", "mañana", "straße", "smørrebrød", "kraków", "ελλάδα", "москва",
+         "résumé", "déjà", "façade", "jalapeño", "crème", "brûlée", "coöperate", "zoë", "fiancée"]
+JOIN = ["l'été", "café's", "end.é", "é.end", "a.é.b", "3,é", "é3,5", "__é__", "_é", "é_", "naïve_user",
+        "über.cool", "a:é", "é:a", "1.é", "é'1", "ab;é;cd", "a_1_é", "Café", "CAFÉ".lower(), "NAÏVE".lower(),
+        "CaFé", "x.y.ü", "ü,3", "a'b'é"]
+DECLINE = ["É", "Über", "中文", "カタカナ", "שלום", "é́", "😀", "İ", "ΣΟΦΙΑ", "­"]
+SEPS = [" ", " ", "\n", ", ", ". ", " - ", "(", ") ", "\t", "; ", ": ", "'"]
+
+
+def doc(rng, n_words, n_uni, pool):
+    words = [synth.word(rng.randint(1, 3000)).decode() for _ in range(n_words)]
+    for _ in range(n_uni):
+        words.insert(rng.randint(0, len(words)), rng.choice(pool))
+    out = []
+    for w in words:
+        out.append(w)
+        out.append(rng.choice(SEPS))
+    return "".join(out).encode()
+
+
+def edge_docs():
+    docs = []
+    for w in WORDS + JOIN + SIMPLE:
+        docs += [w, w + " tail", "head " + w, w + w, w + "." + w, w.upper().lower() + " " + w]
+    # a 2-, 3- or 4-byte char across every lane edge and the window's end
+    for ch in ["é", "я", "ǆ", "ə"]:
+        for pad in range(58, 70):
+            docs.append("a" * pad + ch + "b" * 12)
+            docs.append("x " * (pad // 2) + "z" + ch + "z")
+    docs.append(("word " * 800)[:4090] + " é")
+    docs.append("é " + "z" * 300 + " abc")                         # > 255 chars: the long path cuts it
+    docs.append("é" * 200)                                           # 400 bytes, 200 units: one token
+    docs.append(" ".join("é%d" % i for i in range(300)))             # many distinct non-ASCII terms
+    return [d.encode() for d in docs]
+
+
+@pytest.mark.parametrize("uniwave", [True, False])
+def test_simple_non_ascii_docs_equal_oracle(monkeypatch, uniwave):
+    if not uniwave:
+        monkeypatch.setenv("TFIDF_NO_UNIWAVE", "1")
+    rng = random.Random(71)
+    texts = edge_docs()
+    simple = [doc(rng, rng.randint(20, 500), rng.randint(1, 8), WORDS + JOIN + SIMPLE) for _ in range(900)]
+    declined = [doc(rng, rng.randint(20, 300), 1, DECLINE) for _ in range(150)]
+    texts += simple + declined
+    texts += synth.corpus(200, V=3000, len_min=50, len_max=400)     # pure ASCII
+    rng.shuffle(texts)
+    g, o = build_pair(texts)
+    st = g.stats()
+    assert st["unicode_docs"] >= 900 + 150
+    if uniwave:
+        assert st["unicode_wave_docs"] >= 900                         # the simple ones went the wave way
+        assert st["unicode_docs"] - st["unicode_wave_docs"] >= 150    # the declined ones did not
+    else:
+        assert st["unicode_wave_docs"] == 0
+    check(g, o, texts)
+    for q in ["café", "naïve", "über cool", "straße", "ελλάδα", "москва", "résumé déjà", "l'été", "a_1_é",
+              "CAFÉ", "Über", "中文", synth.word(5).decode() + " é", "é"]:
+        qb = q.encode()
+        for k in (0, 10):
+            assert_hits_equal(g.search(qb, k), o.search(qb, k))
+    g.close()
+    o.close()
+
+
+def test_same_term_across_paths():
+    """A term spelled in a document the wave rules take and in one they decline
+    (an upper-case É elsewhere in it) is one dictionary term: df 2, one
+    posting list."""
+    texts = [b"caf\xc3\xa9 au lait", "CAFÉ noir É".encode(), "Café crème".encode(), "café".encode() * 3]
+    g, o = build_pair(texts)
+    st = g.stats()
+    assert st["unicode_wave_docs"] >= 2 and st["unicode_docs"] - st["unicode_wave_docs"] >= 1
+    check(g, o, texts)
+    assert_hits_equal(g.search("café".encode(), 0), o.search("café".encode(), 0))
+    g.close()
+    o.close()
+
+
+def test_cfg2_share_of_simple_docs_equal_oracle():
+    """bench.py --unicode-frac's documents (one é word each) at a reduced size."""
+    texts = synth.corpus(3000, V=5000, len_min=100, len_max=300)
+    rng = random.Random(5)
+    out = []
+    for t in texts:
+        if rng.random() < 0.5:
+            w = t.split(b" ")
+            i = rng.randrange(len(w))
+            w[i] = w[i] + "é".encode()
+            t = b" ".join(w)
+        out.append(t)
+    g, o = build_pair(out)
+    st = g.stats()
+    assert st["unicode_wave_docs"] == st["unicode_docs"] > 1000
+    check(g, o, out)
+    g.close()
+    o.close()

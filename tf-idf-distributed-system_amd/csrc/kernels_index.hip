@@ -512,7 +512,14 @@ __device__ __forceinline__ uint64_t lane_word_mask(const uint8_t *text, uint32_t
 // of the text (the round-3 classify's bank conflicts) and no work on the rows
 // past the document.  Neighbour bytes across chunks by wave shuffles, across
 // rows from the staged text (lanes 0 / 63).
-template <bool PACK>
+// UNI (round 5, documents the ASCII pass flagged): bytes >= 0x80 read as
+// letters — right once uni_simple_span has passed the document (every
+// non-ASCII char a well-formed ALetter that is its own lower case); the SWAR
+// tests run on the low 7 bits with the high bytes masked out (their adds
+// would carry into the next byte).
+__device__ __forceinline__ uint32_t ld_byte_u(uint32_t c) { return c >= 0x80u ? 0x80u : ld_byte(c); }
+
+template <bool PACK, bool UNI = false>
 __device__ __forceinline__ uint64_t regs_word_mask(const uint4 *v, uint32_t nrows, const uint8_t *text,
                                                    uint16_t *wm16, uint16_t *wb16, uint32_t lane, bool *bad,
                                                    bool *under, uint64_t *wbase, bool *upper) {
@@ -520,26 +527,33 @@ __device__ __forceinline__ uint64_t regs_word_mask(const uint4 *v, uint32_t nrow
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     if ((uint32_t)k >= nrows) break;                          // wave-uniform
-    const uint32_t x[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+    const uint32_t xr[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+    uint32_t x[4], hb[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      hb[i] = UNI ? xr[i] & 0x80808080u : 0u;
+      x[i] = UNI ? xr[i] & 0x7F7F7F7Fu : xr[i];
+    }
     uint32_t LD[4], P = 0;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      const uint32_t D = swar_digit(x[i]);
-      const uint32_t Lt = swar_letter(x[i]);
+      const uint32_t D = UNI ? swar_digit(x[i]) & ~hb[i] : swar_digit(x[i]);
+      const uint32_t La = UNI ? swar_letter(x[i]) & ~hb[i] : swar_letter(x[i]);
+      const uint32_t Lt = La | hb[i];
       LD[i] = Lt | (D >> 1);
-      U |= Lt & ~(x[i] << 2);
-      badacc |= x[i];
-      P |= (x[i] + 0x59595959u) & ~(x[i] + 0x44444444u) & ~D;
+      U |= La & ~(x[i] << 2);
+      badacc |= xr[i];
+      P |= (x[i] + 0x59595959u) & ~(x[i] + 0x44444444u) & ~D & ~hb[i];
     }
     uint32_t ldp = (uint32_t)__shfl_up((int)LD[3], 1, 64);
     uint32_t ldn = (uint32_t)__shfl_down((int)LD[0], 1, 64);
-    if (lane == 0) ldp = k ? ld_byte(text[1024 * k - 1]) << 24 : 0u;
-    if (lane == 63) ldn = k < 3 ? ld_byte(text[1024 * k + 1024]) : 0u;
+    if (lane == 0) ldp = k ? (UNI ? ld_byte_u(text[1024 * k - 1]) : ld_byte(text[1024 * k - 1])) << 24 : 0u;
+    if (lane == 63) ldn = k < 3 ? (UNI ? ld_byte_u(text[1024 * k + 1024]) : ld_byte(text[1024 * k + 1024])) : 0u;
     const bool mids = __any((P & 0x80808080u) != 0);
     uint32_t W = 0, WB = 0;
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      const uint32_t u = swar_eq(x[i], 0x5F5F5F5Fu);
+      const uint32_t u = UNI ? swar_eq(x[i], 0x5F5F5F5Fu) & ~hb[i] : swar_eq(x[i], 0x5F5F5F5Fu);
       us |= u;
       uint32_t c = LD[i] | (LD[i] << 1) | u;
       if (PACK) WB |= swar_nib(c & 0x80808080u) << (4 * i);
@@ -550,8 +564,8 @@ __device__ __forceinline__ uint64_t regs_word_mask(const uint4 *v, uint32_t nrow
         const uint32_t nf = __builtin_amdgcn_alignbyte(next4, LD[i], 1);
         const uint32_t both = pf & nf;
         const uint32_t dq = swar_eq(x[i], 0x2E2E2E2Eu) | swar_eq(x[i], 0x27272727u);
-        const uint32_t ml = dq | swar_eq(x[i], 0x3A3A3A3Au);
-        const uint32_t mn = dq | swar_eq(x[i], 0x2C2C2C2Cu) | swar_eq(x[i], 0x3B3B3B3Bu);
+        const uint32_t ml = (dq | swar_eq(x[i], 0x3A3A3A3Au)) & ~hb[i];
+        const uint32_t mn = (dq | swar_eq(x[i], 0x2C2C2C2Cu) | swar_eq(x[i], 0x3B3B3B3Bu)) & ~hb[i];
         c |= (ml & both) | (mn & (both << 1));
       }
       W |= swar_nib(c & 0x80808080u) << (4 * i);
@@ -569,16 +583,21 @@ __device__ __forceinline__ uint64_t regs_word_mask(const uint4 *v, uint32_t nrow
 }
 
 // Folded table key of a token of 9..255 bytes at tp (see above); *h slot hash.
+// UNI: any length; bit 8 (free outside packs) set when the token holds a
+// non-ASCII byte (its dictionary key then comes from the Unicode key builder).
+constexpr uint64_t kFoldUni = 1ull << 8;
+template <bool UNI = false>
 __device__ __noinline__ uint64_t fold_key(const uint8_t *text, uint32_t tp, uint32_t n, uint32_t *h, bool *valid) {
   const uint32_t *tw = reinterpret_cast<const uint32_t *>(text);
   const uint32_t a0 = tp >> 2, o = tp & 3;
-  uint32_t h1 = 0x243F6A88u ^ n, h2 = 0x85A308D3u + n, nu = 0;
+  uint32_t h1 = 0x243F6A88u ^ n, h2 = 0x85A308D3u + n, nu = 0, hib = 0;
   uint32_t prev = tw[a0];
   for (uint32_t i = 0; 4 * i < n; i++) {
     const uint32_t nx = tw[a0 + i + 1];
     const uint32_t k = keep_bytes(n, i);
     const uint32_t t = __builtin_amdgcn_alignbyte(nx, prev, o) & k;
     prev = nx;
+    if (UNI) hib |= t;
     nu |= (t ^ 0x5F5F5F5Fu) & k;
     const uint32_t l = lower4(t);
     h1 = (h1 ^ l) * 0x9E3779B1u; h1 = __builtin_rotateleft32(h1, 13);
@@ -588,7 +607,8 @@ __device__ __noinline__ uint64_t fold_key(const uint8_t *text, uint32_t tp, uint
   h2 ^= h2 >> 16; h2 *= 0x297A2D39u; h2 ^= h2 >> 13;
   *h = h2;
   *valid = nu != 0;
-  return kFoldBit | (uint64_t)n | ((uint64_t)tp << 13) | ((uint64_t)h1 << 26) | (((uint64_t)(h1 ^ h2) & 31ull) << 58);
+  return kFoldBit | (uint64_t)n | ((uint64_t)tp << 13) | ((uint64_t)h1 << 26) | (((uint64_t)(h1 ^ h2) & 31ull) << 58) |
+         ((hib & 0x80808080u) ? kFoldUni : 0ull);
 }
 
 // Lower-cased byte equality of the n-byte spans at p1 and p2.
@@ -829,6 +849,10 @@ __device__ __forceinline__ uint32_t table_slot(uint32_t l0, uint32_t l1) {
   const uint32_t x = l0 ^ __builtin_amdgcn_alignbit(l1, l1, 16);
   return (uint32_t)__umul24(x ^ (x >> 11), 0x2C1B3Du) >> (32 - kWaveSlotBits);
 }
+__device__ __forceinline__ uint64_t shfl_down64(uint64_t v) {   // lane l gets lane l + 1's (lane 63: 0)
+  const uint32_t lo = (uint32_t)__shfl_down((int)(uint32_t)v, 1, 64), hi = (uint32_t)__shfl_down((int)(uint32_t)(v >> 32), 1, 64);
+  return threadIdx.x % 64 == 63 ? 0ull : (((uint64_t)hi << 32) | lo);
+}
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -857,7 +881,10 @@ __device__ __forceinline__ uint32_t probe_round(SM &sm, uint32_t lane, const uin
   for (int j = 0; j < J; j++) {
     const uint64_t zm = __ballot(old[j] == 0) & pm[j];
     uint64_t hm = (__ballot(old[j] == tk[j]) & pm[j]) | zm;
-    if (FOLD) {   // same length and folded hash, other position: compare the bytes
+    // same length and folded hash, other position: compare the bytes (only
+    // while a pending lane holds a folded key: one compare + mask test per
+    // round otherwise)
+    if (FOLD && (__ballot((int32_t)(uint32_t)(tk[j] >> 32) < 0) & pm[j] & ~hm)) {
       const uint64_t fm = __ballot((((old[j] & tk[j]) >> 63) != 0) & (((old[j] ^ tk[j]) & ~kFoldPosMask) == 0)) &
                           pm[j] & ~hm;
       if (fm) {
@@ -881,7 +908,11 @@ __device__ __forceinline__ uint32_t probe_round(SM &sm, uint32_t lane, const uin
 // One batch of 64 K tokens [tb, tb + 64 K) of the list (entries past ntok
 // are ignored).  claims / toks: wave-uniform running counts of distinct
 // terms / counted tokens.
-template <int K, bool FOLD, bool PACK>
+// UNI: a token holding a byte >= 0x80 takes a folded key whatever its length
+// (fold_key / span_same lower-case the ASCII bytes only; a UNI document's
+// non-ASCII chars are their own lower case, and lower4's byte adds leave the
+// bytes of well-formed UTF-8 unchanged).
+template <int K, bool FOLD, bool PACK, bool UNI = false>
 __device__ __forceinline__ void hist2(WaveSmem &sm, uint32_t lane, uint32_t tb, uint32_t ntok, bool under, bool upper,
                                       uint32_t &claims, uint32_t &toks, bool &overflow) {
   const uint32_t *tw = reinterpret_cast<const uint32_t *>(sm.text);
@@ -921,8 +952,9 @@ __device__ __forceinline__ void hist2(WaveSmem &sm, uint32_t lane, uint32_t tb, 
     const uint32_t l0 = t0[k] | (PACK ? pack_tag(span_doc(ent[k])) : 0u);
     tkey[k] = (uint64_t)l0 | ((uint64_t)t1[k] << 32);
     slot[k] = table_slot(l0, t1[k]);
-    pm[k] = __ballot(in & (n <= 8) & valid);
-    if (FOLD) lm |= (uint64_t)(__ballot(in & (n > 8)) != 0) << k;
+    const bool hh = UNI && (ent[k] >> 31) != 0;          // UNI: may hold a non-ASCII byte (span list flag)
+    pm[k] = __ballot(in & (n <= 8) & valid & !hh);
+    if (FOLD) lm |= (uint64_t)(__ballot(in & ((n > 8) | hh)) != 0) << k;
   }
   if (FOLD && lm) {                                      // tokens of 9..255 bytes: folded keys
     bool toolong = false;
@@ -932,12 +964,12 @@ __device__ __forceinline__ void hist2(WaveSmem &sm, uint32_t lane, uint32_t tb, 
         const uint32_t e = ent[k];
         const uint32_t tp = e & kSpanMask, n = ((e >> 16) & kSpanMask) - tp;
         bool ok = false;
-        if (lane + 64u * k < left && n > 8) {
+        if (lane + 64u * k < left && (n > 8 || (UNI && (e >> 31) != 0))) {
           if (n > kMaxTokenLen) {
             toolong = true;
           } else {
             uint32_t h;
-            tkey[k] = fold_key(sm.text, tp, n, &h, &ok);
+            tkey[k] = fold_key<UNI>(sm.text, tp, n, &h, &ok);
             if (PACK) {
               tkey[k] |= (uint64_t)span_doc(e) << 8;
               h ^= span_doc(e) * 0x9E3779B1u;
@@ -1000,10 +1032,96 @@ __device__ __forceinline__ void hist2(WaveSmem &sm, uint32_t lane, uint32_t tb, 
 // lengths / term counts accumulated into pk_len / pk_nu).  Short keys by
 // bucket probes with all of a lane's loads in flight, unresolved ones through
 // a one-per-lane retry queue; folded (> 8 byte) keys one per lane at a time.
-template <bool PACK, bool G4>
+// UNI: dictionary slot of a folded term (128-bit key lo / hi, occurrence
+// mine) with its identity check, in fewer dependent round trips than
+// dict_find_or_insert + verify_lds: each probe loads the bucket's keys lo, hi
+// AND reference words together, so a term found in its home bucket costs one
+// round trip plus one for the spelling check.  Returns slot | status << 32:
+// 0 nothing to check (claimed, exact key, or the reference spelled the same),
+// 1 found with no reference visible yet (the caller defers through
+// dict_verify), 2 another term under the key (a collision); slot
+// kInvalidSlot: dictionary full.
+__device__ __noinline__ uint64_t uni_find_verify(uint64_t *dict, uint32_t mask, uint64_t lo, uint64_t hi,
+                                                 uint64_t mine, const uint8_t *text, const uint8_t *wtext, uint32_t tp) {
+  uint64_t *dlo = dict, *dhi = dict + (size_t)mask + 1, *dref = dict + 2 * ((size_t)mask + 1);
+  uint32_t s = dict_home(dict_hash(lo, hi), mask) & ~1u;     // probing starts at the bucket (dict_lookup_multi)
+  uint32_t slot = kInvalidSlot;
+  uint64_t r = 0;
+  for (uint32_t it = 0; it < mask + 1 + 4096 && slot == kInvalidSlot; it++) {
+    const uint32_t b = s & ~1u;
+    const ulonglong2 el = *reinterpret_cast<const ulonglong2 *>(dlo + b);
+    const ulonglong2 eh = *reinterpret_cast<const ulonglong2 *>(dhi + b);
+    const ulonglong2 er = *reinterpret_cast<const ulonglong2 *>(dref + b);
+    uint32_t next = (b + 2) & mask;
+    for (uint32_t q = s & 1u; q < 2 && slot == kInvalidSlot; q++) {
+      const uint32_t js = b + q;
+      uint64_t v = q ? el.y : el.x;
+      if (v == 0) {                                        // empty (or stale): claim
+        v = atomicCAS(reinterpret_cast<unsigned long long *>(dlo + js), 0ull, (unsigned long long)lo);
+        if (v == 0) {
+          if (lo & kLoHashed) __hip_atomic_store(dref + js, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(dhi + js, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          return js;                                       // claimed: this occurrence is the reference
+        }
+      }
+      if (v != lo) continue;
+      uint64_t h = q ? eh.y : eh.x;
+      for (uint32_t w = 0; h == 0 && w < (1u << 20); w++)   // claimed, hi not published yet
+        h = __hip_atomic_load(dhi + js, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (h == hi) {
+        slot = js;
+        r = q ? er.y : er.x;
+      } else if (h == 0) {
+        next = js;                                         // (bounded wait over) probe it again
+        break;
+      }
+    }
+    s = next;
+  }
+  if (slot == kInvalidSlot || !(lo & kLoHashed)) return slot;
+  if (r == 0) r = __hip_atomic_load(dref + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (r == mine) return slot;
+  if (r == 0) return slot | (1ull << 32);
+  const uint32_t n = dict_ref_len(mine);
+  if (n == dict_ref_len(r) && n <= 32) {
+    const uint64_t off = dict_ref_off(r);
+    const uint32_t o = (uint32_t)(off & 3u), lo4 = tp & 3u;
+    const uint32_t *g = reinterpret_cast<const uint32_t *>(text + (off & ~3ull));
+    const uint32_t *l = reinterpret_cast<const uint32_t *>(wtext + (tp & ~3u));
+    uint32_t gw[9], lw[9];
+#pragma unroll
+    for (int j = 0; j < 9; j++) {
+      gw[j] = 4u * j < o + n ? g[j] : 0u;
+      lw[j] = 4u * j < lo4 + n ? l[j] : 0u;
+    }
+    uint32_t diff = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++)
+      diff |= (__builtin_amdgcn_alignbyte(gw[j + 1], gw[j], o) ^ __builtin_amdgcn_alignbyte(lw[j + 1], lw[j], lo4)) &
+              keep_bytes(n, j);
+    if (diff == 0) return slot;
+  }
+  const bool same = uc_same_term(text + dict_ref_off(r), dict_ref_len(r), text + dict_ref_off(mine), n);
+  return slot | (same ? 0ull : (2ull << 32));
+}
+
+// UNI: folded terms keyed by the Unicode key builder (lower-cased code
+// points; the same key the Unicode and long paths give the term).
+// The document passed uni_simple_char, so its non-ASCII chars are their own
+// lower case: the key builder's bytes are the token's with ASCII lower-cased
+// (what uc_token_key would push, without decoding or the case tables).
+__device__ __noinline__ void uni_dict_key(const uint8_t *text, uint32_t tp, uint32_t n, uint64_t *lo, uint64_t *hi,
+                                          uint64_t seed) {
+  KeyBuilder kb;
+  for (uint32_t j = tp; j < tp + n; j++) kb.push(ascii_lower(text[j]));
+  kb.finish(lo, hi, seed);
+}
+
+template <bool PACK, bool G4, bool UNI = false>
 __device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p, uint32_t lane, uint32_t nu,
                                               uint32_t doc, uint32_t *g, uint32_t *tf, uint32_t *tdoc,
-                                              uint32_t &actm, uint32_t *pk_len, uint32_t *pk_nu, uint64_t wbase) {
+                                              uint32_t &actm, uint32_t *pk_len, uint32_t *pk_nu, uint64_t wbase,
+                                              uint32_t wlen = 0) {
   const uint32_t dmask = p.cap_mask;
   const uint16_t *slots = reinterpret_cast<const uint16_t *>(sm.list);
   if (PACK && lane < kPackMax) { pk_len[lane] = 0; pk_nu[lane] = 0; }
@@ -1045,12 +1163,25 @@ __device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p
         const uint64_t key = sm.key[slots[lane + 64 * k]];
         const uint32_t n = (uint32_t)key & 0xFFu, tp = (uint32_t)(key >> 13) & 0x1FFFu;
         bool valid;
-        token_key(sm.text, tp, tp + n, &flo, &fhi, &valid, TFIDF_COLD(hash_seed));
+        if (UNI && (key & kFoldUni)) uni_dict_key(sm.text, tp, n, &flo, &fhi, TFIDF_COLD(hash_seed));
+        else token_key(sm.text, tp, tp + n, &flo, &fhi, &valid, TFIDF_COLD(hash_seed));
         mine = dict_ref_word(wbase + tp, n);
       }
-      bool cl;
-      const uint32_t gg = dict_find_or_insert(p.dict, dmask, flo, fhi, fa, &mine, &cl);
-      if (fa && (flo & kLoHashed) && !cl && gg != kInvalidSlot) dict_verify(p, gg, mine, doc);   // > 16 bytes
+      uint32_t gg;
+      if (UNI) {
+        gg = kInvalidSlot;
+        if (fa) {
+          const uint64_t res = uni_find_verify(p.dict, dmask, flo, fhi, mine, p.text, sm.text,
+                                               (uint32_t)(sm.key[slots[lane + 64 * k]] >> 13) & 0x1FFFu);
+          gg = (uint32_t)res;
+          if ((res >> 32) == 1) dict_verify(p, gg, mine, doc);   // defers (or finds the reference published by now)
+          else if ((res >> 32) == 2) set_build_err(TFIDF_COLD(err), kErrCollision, doc);
+        }
+      } else {
+        bool cl;
+        gg = dict_find_or_insert(p.dict, dmask, flo, fhi, fa, &mine, &cl);
+        if (fa && (flo & kLoHashed) && !cl && gg != kInvalidSlot) dict_verify(p, gg, mine, doc);   // > 16 bytes
+      }
 #pragma unroll
       for (int kk = 0; kk < (int)kWaveK; kk++)
         if (fa && (uint32_t)kk == k) g[kk] = gg;
@@ -1161,6 +1292,43 @@ __device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p
 // array is an argument: a called function has no kernarg pointer (TFIDF_COLD).
 __device__ __noinline__ void flag_unicode(uint32_t *flags, uint64_t d) { flags[d] = 1u; }
 
+// UNI (round 5): can the wave rules take this document?  Yes when every
+// non-ASCII char is well-formed UTF-8, of word-break class ALetter (UAX#29:
+// the class of the ASCII letters, so the ASCII rules with its bytes read as
+// letters give the scanner's tokens) and its own lower case (so ASCII
+// lower-casing decides term identity in the document's table), and no
+// continuation byte is an orphan.  Anything else (Han, Katakana, Hebrew,
+// combining marks, upper case, malformed bytes) stays flagged for
+// k_tokenize_uwave.  One char: its lead byte and the three after it in w
+// (little-endian), avail = bytes of the window from the lead on; returns its
+// byte length, 0 if it does not qualify.  (Bytes come in registers: a
+// generic pointer into LDS would be flat loads, one dependent round trip per
+// byte — 4.6 ms at cfg 2 with every document non-ASCII.)
+__device__ __noinline__ uint32_t uni_simple_char(uint32_t w, uint32_t avail) {
+  const uint32_t b0 = w & 0xFFu, b1 = (w >> 8) & 0xFFu, b2 = (w >> 16) & 0xFFu, b3 = w >> 24;
+  auto cont = [](uint32_t b, uint32_t lo, uint32_t hi) { return b >= lo && b <= hi; };
+  uint32_t cp, len;
+  if (b0 >= 0xC2u && b0 < 0xE0u && avail >= 2 && cont(b1, 0x80u, 0xBFu)) {
+    cp = ((b0 & 0x1Fu) << 6) | (b1 & 0x3Fu);
+    len = 2;
+  } else if (b0 >= 0xE0u && b0 < 0xF0u && avail >= 3 && cont(b1, b0 == 0xE0u ? 0xA0u : 0x80u, b0 == 0xEDu ? 0x9Fu : 0xBFu) &&
+             cont(b2, 0x80u, 0xBFu)) {
+    cp = ((b0 & 0x0Fu) << 12) | ((b1 & 0x3Fu) << 6) | (b2 & 0x3Fu);
+    len = 3;
+  } else if (b0 >= 0xF0u && b0 < 0xF5u && avail >= 4 && cont(b1, b0 == 0xF0u ? 0x90u : 0x80u, b0 == 0xF4u ? 0x8Fu : 0xBFu) &&
+             cont(b2, 0x80u, 0xBFu) && cont(b3, 0x80u, 0xBFu)) {
+    cp = ((b0 & 0x07u) << 18) | ((b1 & 0x3Fu) << 12) | ((b2 & 0x3Fu) << 6) | (b3 & 0x3Fu);
+    len = 4;
+  } else {
+    return 0;
+  }
+  // both table walks issued together (index loads, then data loads)
+  const uint32_t ci = kUcClassIndex[cp >> 8], li = kUcLowerIndex[cp >> 8];
+  const uint32_t cls = kUcClassData[ci * 256u + (cp & 255u)];
+  const int32_t dl = kUcLowerData[li * 256u + (cp & 255u)];
+  return (cls == kUcALetter && dl == 0) ? len : 0u;
+}
+
 // Units: PACK = false, one document per unit (documents 0..n_docs-1, or the
 // doc_list entries); PACK = true, unit u = documents [u * pack, u * pack + pack)
 // sharing one window.  A pack that cannot take the packed path (window or
@@ -1169,7 +1337,11 @@ __device__ __noinline__ void flag_unicode(uint32_t *flags, uint64_t d) { flags[d
 #ifndef TFIDF_WAVE_XCD
 #define TFIDF_WAVE_XCD 1
 #endif
-template <bool PACK, bool G4>
+// UNI = true (round 5): the documents the ASCII pass flagged (uni_list), one
+// wave each, by the same rules with non-ASCII bytes read as letters when
+// uni_simple_span passes the document (its flag is then cleared); the rest
+// stay flagged for k_tokenize_uwave.
+template <bool PACK, bool G4, bool UNI = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_tokenize_wave(BuildParams p) {
   __shared__ WaveSmem sm;
   const uint32_t lane = threadIdx.x;
@@ -1187,9 +1359,51 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   const uint64_t ubeg = xm ? (blockIdx.x & 7u) * per + (blockIdx.x >> 3) : blockIdx.x;
   const uint64_t uend = xm ? min(n_units, ((blockIdx.x & 7u) + 1) * per) : n_units;
   const uint64_t ustep = xm ? gridDim.x >> 3 : gridDim.x;
+  // UNI: units = the flagged documents, 64 flags per ballot (workgroup b
+  // takes flag chunks b, b + grid, ...); kNoUnit ends.  The only state kept
+  // across documents is the current chunk's remaining flags (fmk): the chunk
+  // base is the current document's (SGPRs are the scarce resource here).
+  constexpr uint64_t kNoUnit = ~0ull;
+  uint64_t fmk = 0;
+  uint32_t my_uni = 0;                                      // lane 0 counts (a VGPR)
+  auto uni_scan = [&](uint64_t cb) __attribute__((always_inline)) -> uint64_t {
+    for (; cb < p.n_docs; cb += (uint64_t)gridDim.x * 64) {
+      fmk = __ballot(cb + lane < p.n_docs && TFIDF_COLD(uni_list)[cb + lane] != 0u);
+      if (fmk) {
+        const uint64_t dd = cb + (uint64_t)__builtin_ctzll(fmk);
+        fmk &= fmk - 1;
+        return dd;
+      }
+    }
+    return kNoUnit;
+  };
+  auto uni_next = [&](uint64_t cur) __attribute__((always_inline)) -> uint64_t {
+    if (fmk) {
+      const uint64_t dd = (cur & ~63ull) + (uint64_t)__builtin_ctzll(fmk);
+      fmk &= fmk - 1;
+      return dd;
+    }
+    return uni_scan((cur & ~63ull) + (uint64_t)gridDim.x * 64);
+  };
+  const uint64_t u0 = UNI ? uni_scan((uint64_t)blockIdx.x * 64) : ubeg;
+  // UNI: which 2-byte chars (U+0080..U+07FF) uni_simple_char passes, one bit
+  // each: lane l holds U+0080 + 32 l .. + 31 (lanes >= 60: none)
+  uint32_t simple2 = 0;
+  if (UNI && u0 != kNoUnit) {
+    const uint32_t c0 = min(0x80u + 32u * lane, 0x7E0u);    // (lanes >= 60: masked below)
+    const uint32_t ci = kUcClassIndex[c0 >> 8], li = kUcLowerIndex[c0 >> 8];   // 32-aligned: one table row
+#pragma unroll 8
+    for (uint32_t b = 0; b < 32; b++) {
+      const uint32_t cp = c0 + b;
+      const bool ok2 = kUcClassData[ci * 256u + (cp & 255u)] == kUcALetter && kUcLowerData[li * 256u + (cp & 255u)] == 0;
+      simple2 |= (ok2 ? 1u : 0u) << b;
+    }
+    if (lane >= 60) simple2 = 0;
+  }
+  const uint64_t ulim = UNI ? kNoUnit : uend;
   DocMeta meta;
-  if (ubeg < uend) {
-    meta = unit_meta<PACK>(p, ubeg, lane);
+  if (u0 < ulim) {
+    meta = unit_meta<PACK>(p, u0, lane);
     prefetch_wave(p, meta, lane, v);
   }
   const uint32_t R = p.n_ranges;
@@ -1199,16 +1413,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
            *pk_start = pk_len + 2 * kPackMax;
   uint64_t *pk_row = sm.qkey + 2 * kPackMax;
 
-  for (uint64_t u = ubeg; u < uend; u += ustep) {
+  uint64_t un = 0;
+  for (uint64_t u = u0; u < ulim; u = un) {
     const uint64_t d = meta.d, src = meta.src, L = meta.L, s0 = meta.s0;
     const uint32_t shift = meta.shift, np = meta.np;
     const uint64_t pofs = meta.pofs;
     const bool fits = fits_wave(meta);
-    const uint64_t un = u + ustep;
+    un = UNI ? uni_next(u) : u + ustep;
     if (!fits) {
       if (PACK) defer_pack(p, d, np, lane);
+      else if (UNI) {}                                      // (flagged documents fit: the ASCII pass staged them)
       else if (lane == 0) TFIDF_COLD(long_list)[atomicAdd(TFIDF_COLD(long_count), 1u)] = (uint32_t)d;
-      if (un < uend) { meta = unit_meta<PACK>(p, un, lane); prefetch_wave(p, meta, lane, v); }
+      if (un < ulim) { meta = unit_meta<PACK>(p, un, lane); prefetch_wave(p, meta, lane, v); }
       continue;                                             // wave-uniform
     }
     // ---- stage: registers -> LDS (whole window; bytes outside the document
@@ -1241,10 +1457,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     {
       const uint32_t nrows = (shift + (uint32_t)L + 1023) >> 10;
       uint16_t *wm16 = reinterpret_cast<uint16_t *>(sm.list);            // the token list is written after
-      W = regs_word_mask<PACK>(v, nrows, sm.text, wm16, wm16 + 256, lane, &bad, &under, &wbase, &upper);
+      W = regs_word_mask<PACK, UNI>(v, nrows, sm.text, wm16, wm16 + 256, lane, &bad, &under, &wbase, &upper);
     }
     // the next document's window, now that this one's registers are consumed
-    if (un < uend) { meta = unit_meta<PACK>(p, un, lane); prefetch_wave(p, meta, lane, v); }
+    if (un < ulim) { meta = unit_meta<PACK>(p, un, lane); prefetch_wave(p, meta, lane, v); }
     asm volatile("" ::: "memory");
     if (p.debug_stop == 1) continue;
     // PACK: document boundaries q_j (window position of document j's first
@@ -1268,7 +1484,46 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       }
       W &= ~(jm & ~wbase);
     }
-    if (bad) {                                              // non-ASCII: the Unicode wave path
+    uint64_t hbm = 0;                                       // UNI: this lane's non-ASCII bytes
+    if (bad && UNI) {                                       // simple non-ASCII text: taken here
+      // lane l: window bytes [64 l, 64 l + 64); lead bytes (11xxxxxx) are
+      // checked one by one, and the continuation bytes (10xxxxxx) must be
+      // exactly those the leads claim (no orphans)
+      const uint32_t *seg = reinterpret_cast<const uint32_t *>(sm.text + 64 * lane);
+      uint64_t lead = 0;
+      uint32_t ncont = 0;
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        const uint32_t x = seg[j], hb = x & 0x80808080u, ld = hb & (x << 1);
+        ncont += (uint32_t)__popc(hb & ~ld);
+        lead |= (uint64_t)swar_nib(ld) << (4 * j);
+        hbm |= (uint64_t)swar_nib(hb) << (4 * j);
+      }
+      const uint32_t wl = shift + (uint32_t)L;
+      const uint32_t *tw = reinterpret_cast<const uint32_t *>(sm.text);
+      bool ok = true;
+      uint32_t claimed = 0;
+      while (__any(lead != 0)) {                            // one lead per lane per step
+        const bool has = lead != 0;
+        const uint32_t pos = 64 * lane + (has ? (uint32_t)__builtin_ctzll(lead) : 0u);
+        lead &= lead - 1;
+        const uint32_t w = __builtin_amdgcn_alignbyte(tw[(pos >> 2) + 1], tw[pos >> 2], pos & 3);
+        const uint32_t b0 = w & 0xFFu, b1 = (w >> 8) & 0xFFu;
+        // 2-byte chars (U+0080..U+07FF: Latin, Greek, Cyrillic, ...) from the
+        // wave's bitmap, the others through the tables
+        const bool two = has && b0 >= 0xC2u && b0 < 0xE0u && (b1 & 0xC0u) == 0x80u && wl - pos >= 2;
+        const uint32_t cp = ((b0 & 0x1Fu) << 6) | (b1 & 0x3Fu);
+        const uint32_t bits = (uint32_t)__shfl((int)simple2, two ? (int)((cp - 0x80u) >> 5) : 0, 64);
+        uint32_t len = 0;
+        if (two) len = ((bits >> (cp & 31u)) & 1u) ? 2u : 0u;
+        else if (has) len = uni_simple_char(w, wl - pos);
+        ok &= !has || len != 0;
+        claimed += len ? len - 1 : 0u;
+      }
+      if (!__all(ok) || wave_sum(claimed) != wave_sum(ncont)) continue;   // stays flagged: k_tokenize_uwave
+      if (lane == 0) TFIDF_COLD(uni_list)[d] = 0u;
+      my_uni += lane == 0;
+    } else if (bad) {                                       // non-ASCII: the Unicode wave path
       if (PACK) defer_pack(p, d, np, lane);
       else if (lane == 0) flag_unicode(TFIDF_COLD(uni_list), d);
       continue;
@@ -1304,6 +1559,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       uint32_t at = tincl - nts;
       uint32_t s0 = (uint32_t)S, s1 = (uint32_t)(S >> 32), e0 = (uint32_t)E, e1 = (uint32_t)(E >> 32);
       const uint32_t l64 = lane * 64;
+      // UNI: bit 31 of a span entry = a token of <= 8 bytes holding a
+      // non-ASCII byte (exact: such a token reaches at most into the next
+      // lane's segment; longer tokens take folded keys anyway, and fold_key
+      // finds their non-ASCII bytes itself)
+      const uint64_t hbn = UNI ? shfl_down64(hbm) : 0ull;
+      auto hflag = [&](uint32_t tp, uint32_t te) __attribute__((always_inline)) -> uint32_t {
+        if (!UNI || te - tp > 8) return 0u;
+        const uint32_t r = tp - l64;
+        const uint32_t own = min(te - tp, 64u - r), spill = te - tp - own;   // bytes here / in the next lane
+        bool h = ((hbm >> r) & ((1ull << own) - 1ull)) != 0;
+        h |= (hbn & ((1ull << spill) - 1ull)) != 0;
+        return h ? 0x80000000u : 0u;
+      };
       while (s0) {
         const uint32_t tp = l64 + (uint32_t)__builtin_ctz(s0);
         const uint32_t te = e0 ? l64 + (uint32_t)__builtin_ctz(e0) : (e1 ? l64 + 32 + (uint32_t)__builtin_ctz(e1) : nz);
@@ -1311,7 +1579,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         if (e0) e0 &= e0 - 1; else e1 &= e1 - 1;
         longtok |= te - tp > 8;
         const uint32_t j = PACK ? dbase + (uint32_t)__popcll(bm & ((2ull << (tp - l64)) - 1)) : 0u;
-        sm.list[at++] = span_entry(tp, te, j);
+        sm.list[at++] = span_entry(tp, te, j) | hflag(tp, te);
       }
       while (s1) {
         const uint32_t tp = l64 + 32 + (uint32_t)__builtin_ctz(s1);
@@ -1320,7 +1588,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         e1 &= e1 - 1;
         longtok |= te - tp > 8;
         const uint32_t j = PACK ? dbase + (uint32_t)__popcll(bm & ((2ull << (tp - l64)) - 1)) : 0u;
-        sm.list[at++] = span_entry(tp, te, j);
+        sm.list[at++] = span_entry(tp, te, j) | hflag(tp, te);
       }
     }
     asm volatile("" ::: "memory");
@@ -1328,16 +1596,16 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
 
     // ---- per-document histogram in LDS (folded-key and '_'-only checks only
     // when the document holds a token of more than 8 bytes or a '_')
-    const bool anylong = __any(longtok) || under;
+    const bool anylong = __any(longtok) || under || (UNI && bad);
     uint32_t nu = 0, len = 0;
     bool overflow = false;
     for (uint32_t tb = 0; tb < ntok && !overflow;) {       // batch width by what is left
       const uint32_t rem = ntok - tb;
       if (anylong) {
-        if (TFIDF_HIST10 && !PACK && rem > 512 && rem <= 640) { hist2<10, true, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 640; }
-        else if (rem > 256) { hist2<8, true, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 512; }
-        else if (rem > 128) { hist2<4, true, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 256; }
-        else { hist2<2, true, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 128; }
+        if (TFIDF_HIST10 && !PACK && rem > 512 && rem <= 640) { hist2<10, true, PACK, UNI>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 640; }
+        else if (rem > 256) { hist2<8, true, PACK, UNI>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 512; }
+        else if (rem > 128) { hist2<4, true, PACK, UNI>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 256; }
+        else { hist2<2, true, PACK, UNI>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 128; }
       } else {
         // 513..640 tokens (U[400, 600]-token documents: ~40 % of cfg 2) in one batch
         if (TFIDF_HIST10 && !PACK && rem > 512 && rem <= 640) { hist2<10, false, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 640; }
@@ -1380,7 +1648,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     // ---- dictionary slots of terms lane + 64k
     uint32_t g[kWaveK], tf[kWaveK], tdoc[kWaveK];
     uint32_t actm = 0;
-    resolve_terms<PACK, G4>(sm, p, lane, nu, (uint32_t)d, g, tf, tdoc, actm, pk_len, pk_nu, s0 - shift);
+    resolve_terms<PACK, G4, UNI>(sm, p, lane, nu, (uint32_t)d, g, tf, tdoc, actm, pk_len, pk_nu, s0 - shift,
+                                 shift + (uint32_t)L);
     if (p.debug_stop == 4) { clear_table(sm, lane); continue; }
 
     // ---- CSR row grouped by dictionary range (PACK: by (document, range)),
@@ -1478,6 +1747,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     atomicAdd(&TFIDF_COLD(stats)[1], my_ttf);
     atomicAdd(&TFIDF_COLD(stats)[2], my_nnz);
   }
+  if (UNI && my_uni) atomicAdd(TFIDF_COLD(uni_wave_count), my_uni);   // lane 0
 }
 
 // ---------------------------------------------------------------------------
@@ -2474,6 +2744,14 @@ hipError_t launch_tokenize_wave(const BuildParams &p, int grid, hipStream_t s) {
     if (g4) hipLaunchKernelGGL((k_tokenize_wave<false, true>), dim3(grid), dim3(64), 0, s, p);
     else hipLaunchKernelGGL((k_tokenize_wave<false, false>), dim3(grid), dim3(64), 0, s, p);
   }
+  return hipGetLastError();
+}
+// The flagged (non-ASCII) documents by the wave rules where they allow
+// (k_tokenize_wave<UNI>); before k_tokenize_uwave, which takes the rest.
+hipError_t launch_tokenize_wave_uni(const BuildParams &p, int grid, hipStream_t s) {
+  const bool g4 = (uint64_t)p.cap_mask + 1 >= (1ull << TFIDF_G4_BITS);
+  if (g4) hipLaunchKernelGGL((k_tokenize_wave<false, true, true>), dim3(grid), dim3(64), 0, s, p);
+  else hipLaunchKernelGGL((k_tokenize_wave<false, false, true>), dim3(grid), dim3(64), 0, s, p);
   return hipGetLastError();
 }
 hipError_t launch_tokenize_chunks(const BuildParams &p, int grid, hipStream_t s) {

@@ -266,7 +266,7 @@ struct Snapshot {
   PinnedVec<uint32_t> h_df;
   uint64_t doc_count = 0, sum_ttf = 0, nnz = 0, num_terms = 0, long_docs = 0;
   uint32_t pack_docs = 1;
-  uint64_t pack_retried = 0, unicode_docs = 0, long_chunked = 0;
+  uint64_t pack_retried = 0, unicode_docs = 0, unicode_wave_docs = 0, long_chunked = 0;
   std::shared_ptr<StatsView> stats;    // replaced under tfidf_index::snap_mu
   std::unordered_map<uint32_t, std::string> term_cache;   // hashed slots' term strings (slot_term)
   std::mutex term_mu;
@@ -985,7 +985,8 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
 
   // counters: [0..2] stats u64, [3] err flags u32 + [3].hi first doc, [4] long_count, [5] retry_count,
   // [6] uni_count, [7] occupied dictionary slots, [8] bad_count, [9] CSR escape count, [10] posting
-  // escapes, [11] deferred hashed-key checks, [12] term-major tf escapes
+  // escapes, [11] deferred hashed-key checks, [12] term-major tf escapes, [13] flagged documents
+  // the wave rules took (k_tokenize_wave<UNI>)
   uint64_t *ctr = ix->counters.as<uint64_t>();
   HIP_TRY(hipMemsetAsync(ix->counters.p, 0, 128, s));
   HIP_TRY(hipMemsetAsync(S.dict.p, 0, (size_t)3 * C * 8, s));
@@ -1016,6 +1017,7 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
   bp.long_count = reinterpret_cast<uint32_t *>(ctr + 4);
   bp.uni_list = ix->uni_list.as<uint32_t>();
   bp.uni_count = reinterpret_cast<uint32_t *>(ctr + 6);
+  bp.uni_wave_count = reinterpret_cast<uint32_t *>(ctr + 13);
   bp.bad_list = ix->bad_list.as<uint32_t>();
   bp.bad_count = reinterpret_cast<uint32_t *>(ctr + 8);
   bp.stats = reinterpret_cast<unsigned long long *>(ctr);
@@ -1049,7 +1051,13 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
         HIP_TRY(launch_tokenize_wave(rp, (int)rgrid, s));
       }
     }
-    // documents with non-ASCII text (count read on the device; exits at once when none)
+    // documents with non-ASCII text (flags read on the device; both exit at once
+    // when none): the wave rules with non-ASCII letters where the document's
+    // characters allow (k_tokenize_wave<UNI>), then the Unicode wave path for
+    // the rest.  TFIDF_NO_UNIWAVE: the Unicode wave path for all (A/B).
+    const char *nouw = getenv("TFIDF_NO_UNIWAVE");
+    if (bp.debug_stop < 10 && !(nouw && *nouw && *nouw != '0'))
+      HIP_TRY(launch_tokenize_wave_uni(bp, (int)std::min<uint64_t>((N + 63) / 64, (uint64_t)ix->num_cus * kWaveWGsPerCU), s));
     if (!bp.debug_stop || bp.debug_stop >= 10)          // (stops 10..13: the Unicode wave path's phases)
       HIP_TRY(launch_tokenize_uwave(bp, (int)std::min<uint64_t>(N, (uint64_t)ix->num_cus * kUwaveWGsPerCU), s));
   }
@@ -1066,14 +1074,15 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
   // one read of the counters: stats (0-2), error flags (3), long (4) and
   // non-ASCII (6) document counts, CSR escapes (9) (32-bit counters in the low
   // halves); read again only when the long path ran
-  HIP_TRY(ix->hctr_h.resize(10));                      // pinned: a pageable read is staged by the runtime
+  HIP_TRY(ix->hctr_h.resize(14));                      // pinned: a pageable read is staged by the runtime
   uint64_t *hctr = ix->hctr_h.data();
-  HIP_TRY(hipMemcpyAsync(hctr, ctr, 10 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipMemcpyAsync(hctr, ctr, 14 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
   HIP_TRY(hipStreamSynchronize(s));
   const uint32_t n_long = (uint32_t)hctr[4], n_uni = (uint32_t)hctr[6];
   S.long_chunked = 0;
   S.long_docs = n_long;
-  S.unicode_docs = n_uni;
+  S.unicode_docs = n_uni + (uint32_t)hctr[13];
+  S.unicode_wave_docs = (uint32_t)hctr[13];
   if (n_long) {
     HIP_TRY(hipEventRecord(ix->ev[EV_L0], s));
     // book-sized documents: chunk-parallel (k_tokenize_chunk + k_long_rows),
@@ -1486,6 +1495,7 @@ extern "C" int tfidf_stats(const tfidf_index *ix, tfidf_index_stats *out) {
     out->pack_docs = S->pack_docs;
     out->pack_retried = S->pack_retried;
     out->unicode_docs = S->unicode_docs;
+    out->unicode_wave_docs = S->unicode_wave_docs;
     out->long_chunked = S->long_chunked;
     out->malformed_docs = S->malformed.size();
     out->hash_seed = S->hash_seed;

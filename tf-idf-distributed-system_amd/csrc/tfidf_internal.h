@@ -47,6 +47,7 @@ struct BuildParams {
   uint32_t *long_count;
   uint32_t *uni_list;         // per document: 1 = the ASCII wave path found non-ASCII bytes (Unicode wave path)
   uint32_t *uni_count;        // flagged documents
+  uint32_t *uni_wave_count;   // flagged documents k_tokenize_wave<UNI> took (the rest: k_tokenize_uwave)
   uint32_t *bad_list;         // docs that are not valid UTF-8 (indexed empty; tfidf_malformed_docs)
   uint32_t *bad_count;
   unsigned long long *stats;  // [0] docCount, [1] sumTotalTermFreq, [2] nnz
@@ -229,6 +230,7 @@ inline void allow_dyn_lds(const void *fn, int bytes, std::atomic<uint64_t> &done
 
 // --- launch wrappers (kernels_index.hip) ---
 hipError_t launch_tokenize_wave(const BuildParams &p, int grid, hipStream_t s);
+hipError_t launch_tokenize_wave_uni(const BuildParams &p, int grid, hipStream_t s);   // flagged non-ASCII documents
 constexpr uint32_t kWaveWGsPerCU = 8;       // 64-thread workgroups per CU (2 waves/SIMD: VGPR- and LDS-bound)
 constexpr uint32_t kWaveGroups = 128;     // CSR row groups per wave unit (documents x ranges, k_tokenize_wave)
 constexpr uint32_t kPackMaxDocs = 16;     // documents per packed window (<= kPackMax, kernels_index.hip)

@@ -43,7 +43,8 @@ class IndexStats(C.Structure):
                                           "device_bytes", "long_docs", "text_bytes", "term_major",
                                           "pack_docs", "pack_retried", "unicode_docs", "long_chunked",
                                           "malformed_docs", "hash_seed", "hash_rebuilds",
-                                          "coalesced_batches", "coalesced_queries", "unit_batches", "unit_count", "fused_queries")]
+                                          "coalesced_batches", "coalesced_queries", "unit_batches", "unit_count", "fused_queries",
+                                          "unicode_wave_docs")]
 
 
 class CommitTiming(C.Structure):

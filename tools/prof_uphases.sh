@@ -1,20 +1,18 @@
 #!/bin/bash
 # PMC counters of the wave tokenize kernel per phase: runs with
 # TFIDF_DEBUG_STOP in STOPS (default "2 3 4 0") and prints per-doc deltas
-# between consecutive stops.  DOCS docs (default 200k).  KRE: kernel name
-# regex (default tokenize_wave; "tokenize_wave<false, false, true>" for the
-# UNI pass alone), BARGS: extra bench.py arguments (e.g. --unicode-frac 1.0).
+# between consecutive stops.  DOCS docs (default 200k).
 set -o pipefail
-R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/prof_phases; mkdir -p $O
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/prof_uphases; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-STOPS=${STOPS:-"2 3 4 0"}; DOCS=${DOCS:-200000}; KRE=${KRE:-tokenize_wave}; BARGS=${BARGS:-}
+STOPS=${STOPS:-"2 3 4 0"}; DOCS=${DOCS:-200000}
 [ -f $O/counters.txt ] || timeout -s KILL 60 rocprofv3 -L > $O/counters.txt 2>&1 || true
 G1="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
 G2="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM SQ_BUSY_CYCLES"
 for s in $STOPS; do
  for g in 1 2; do
   if [ $g = 1 ]; then C=$G1; else C=$G2; fi
-  TFIDF_DEBUG_STOP=$s timeout -s KILL 90 rocprofv3 --pmc $C --kernel-include-regex "$KRE" -d $O/s${s}g$g -o p --output-format csv -- python3 $R/bench.py --docs $DOCS --steps 1 --warmup 0 --no-queries --cpu-sample 0 $BARGS > $O/s${s}g$g.log 2>&1 || { echo "pmc s=$s g=$g failed"; tail -3 $O/s${s}g$g.log; exit 2; }
+  TFIDF_DEBUG_STOP=$s timeout -s KILL 90 rocprofv3 --pmc $C --kernel-include-regex tokenize_uwave -d $O/s${s}g$g -o p --output-format csv -- python3 $R/bench.py --docs $DOCS --steps 1 --warmup 0 --no-queries --cpu-sample 0 --no-e2e --unicode-frac 1.0 > $O/s${s}g$g.log 2>&1 || { echo "pmc s=$s g=$g failed"; tail -3 $O/s${s}g$g.log; exit 2; }
  done
 done
 python3 - $O $DOCS $STOPS <<'PY'
