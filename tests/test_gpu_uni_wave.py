@@ -125,3 +125,27 @@ def test_cfg2_share_of_simple_docs_equal_oracle():
     check(g, o, out)
     g.close()
     o.close()
+
+
+@pytest.mark.parametrize("uniwave", [True, False])
+def test_books_with_simple_non_ascii_words_equal_oracle(monkeypatch, uniwave):
+    """Book-sized documents (the chunk path, 2 KB core units): units holding
+    simple non-ASCII words go the wave way (k_tokenize_chunk<UNI>), units
+    with other non-ASCII text to k_tokenize_uchunk, in one book."""
+    if not uniwave:
+        monkeypatch.setenv("TFIDF_NO_UNIWAVE", "1")
+    rng = random.Random(13)
+    texts = []
+    for b in range(24):
+        n_words = rng.randint(4000, 12000)
+        pool = WORDS + JOIN + SIMPLE + (DECLINE if b % 4 == 0 else [])
+        texts.append(doc(rng, n_words, n_words // 300, pool))
+    texts += [doc(rng, rng.randint(20, 200), 1, WORDS) for _ in range(100)]
+    g, o = build_pair(texts)
+    check(g, o, texts)
+    for q in ["café", "naïve", "straße", "москва", "l'été", "CAFÉ", "中文", synth.word(9).decode()]:
+        qb = q.encode()
+        for k in (0, 10):
+            assert_hits_equal(g.search(qb, k), o.search(qb, k))
+    g.close()
+    o.close()

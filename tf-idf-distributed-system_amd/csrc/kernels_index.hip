@@ -445,10 +445,10 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 // the document were zeroed at staging (class Other).  Wave-uniform flags:
 // *bad = a byte >= 0x80 in the document, *under = a '_' in the document.
 // PACK: *wbase = the same mask before the joiner rules (letters, digits, '_').
-template <bool PACK>
+template <bool PACK, bool UNI = false>
 __device__ __forceinline__ uint64_t lane_word_mask(const uint8_t *text, uint32_t lane, bool *bad, bool *under,
                                                    uint64_t *wbase, bool *upper) {
-  uint32_t x[16];
+  uint32_t x[16], hb[16];
   {
     const uint4 *t = reinterpret_cast<const uint4 *>(text + lane * 64);
 #pragma unroll
@@ -458,16 +458,21 @@ __device__ __forceinline__ uint64_t lane_word_mask(const uint8_t *text, uint32_t
     }
   }
   // pass 1: letter/digit flags (neighbour context), non-ASCII, joiner presence
+  // (UNI: non-ASCII bytes are letters, the SWAR tests on the low 7 bits, as
+  // in regs_word_mask)
   uint32_t LD[16];
   uint32_t badacc = 0, P = 0, U = 0;
 #pragma unroll
   for (int i = 0; i < 16; i++) {
-    const uint32_t D = swar_digit(x[i]);
-    const uint32_t Lt = swar_letter(x[i]);
-    LD[i] = Lt | (D >> 1);
-    U |= Lt & ~(x[i] << 2);                                     // letters without the 0x20 bit: 'A'..'Z'
     badacc |= x[i];
-    P |= (x[i] + 0x59595959u) & ~(x[i] + 0x44444444u) & ~D;   // ' ( ) * + , - . / : ; (candidate joiners)
+    hb[i] = UNI ? x[i] & 0x80808080u : 0u;
+    if (UNI) x[i] &= 0x7F7F7F7Fu;
+    const uint32_t D = swar_digit(x[i]) & ~hb[i];
+    const uint32_t La = swar_letter(x[i]) & ~hb[i];
+    const uint32_t Lt = La | hb[i];
+    LD[i] = Lt | (D >> 1);
+    U |= La & ~(x[i] << 2);                                     // letters without the 0x20 bit: 'A'..'Z'
+    P |= (x[i] + 0x59595959u) & ~(x[i] + 0x44444444u) & ~D & ~hb[i];   // ' ( ) * + , - . / : ; (candidate joiners)
   }
   *upper = __any(U != 0);
   uint32_t ldp = __shfl_up(LD[15], 1, 64);
@@ -480,7 +485,7 @@ __device__ __forceinline__ uint64_t lane_word_mask(const uint8_t *text, uint32_t
   uint32_t us = 0;
 #pragma unroll
   for (int i = 0; i < 16; i++) {
-    const uint32_t u = swar_eq(x[i], 0x5F5F5F5Fu);
+    const uint32_t u = swar_eq(x[i], 0x5F5F5F5Fu) & ~hb[i];
     us |= u;
     uint32_t c = LD[i] | (LD[i] << 1) | u;                          // letter | digit | '_' (bit 7)
     if (PACK) WB |= (uint64_t)swar_nib(c & 0x80808080u) << (4 * i);
@@ -491,8 +496,8 @@ __device__ __forceinline__ uint64_t lane_word_mask(const uint8_t *text, uint32_t
       const uint32_t nf = __builtin_amdgcn_alignbyte(next4, LD[i], 1);   // flags of byte i+1
       const uint32_t both = pf & nf;                                     // bit7 letters, bit6 digits
       const uint32_t dq = swar_eq(x[i], 0x2E2E2E2Eu) | swar_eq(x[i], 0x27272727u);   // '.' '\''
-      const uint32_t ml = dq | swar_eq(x[i], 0x3A3A3A3Au);                            // ':'
-      const uint32_t mn = dq | swar_eq(x[i], 0x2C2C2C2Cu) | swar_eq(x[i], 0x3B3B3B3Bu);  // ',' ';'
+      const uint32_t ml = (dq | swar_eq(x[i], 0x3A3A3A3Au)) & ~hb[i];                 // ':'
+      const uint32_t mn = (dq | swar_eq(x[i], 0x2C2C2C2Cu) | swar_eq(x[i], 0x3B3B3B3Bu)) & ~hb[i];  // ',' ';'
       c |= (ml & both) | (mn & (both << 1));
     }
     W |= (uint64_t)swar_nib(c & 0x80808080u) << (4 * i);
@@ -1337,6 +1342,77 @@ __device__ __noinline__ uint32_t uni_simple_char(uint32_t w, uint32_t avail) {
 #ifndef TFIDF_WAVE_XCD
 #define TFIDF_WAVE_XCD 1
 #endif
+// UNI: which 2-byte chars (U+0080..U+07FF) uni_simple_char passes, one bit
+// each: lane l returns U+0080 + 32 l .. + 31 (lanes >= 60: none).
+__device__ __forceinline__ uint32_t uni_simple2_bitmap(uint32_t lane) {
+  uint32_t bm = 0;
+  const uint32_t c0 = min(0x80u + 32u * lane, 0x7E0u);
+  const uint32_t ci = kUcClassIndex[c0 >> 8], li = kUcLowerIndex[c0 >> 8];   // 32-aligned: one table row
+#pragma unroll 8
+  for (uint32_t b = 0; b < 32; b++) {
+    const uint32_t cp = c0 + b;
+    const bool ok = kUcClassData[ci * 256u + (cp & 255u)] == kUcALetter && kUcLowerData[li * 256u + (cp & 255u)] == 0;
+    bm |= (ok ? 1u : 0u) << b;
+  }
+  return lane >= 60 ? 0u : bm;
+}
+
+// UNI: span list flag (bit 31) of a token [tp, te) starting in the segment of
+// the lane at l64: a token of <= 8 bytes holding a non-ASCII byte (exact:
+// such a token reaches at most into the next lane's segment, whose
+// non-ASCII bytes are hbn; longer tokens take folded keys anyway, and
+// fold_key finds their non-ASCII bytes itself).
+__device__ __forceinline__ uint32_t uni_span_flag(uint32_t tp, uint32_t te, uint32_t l64, uint64_t hbm, uint64_t hbn) {
+  if (te - tp > 8) return 0u;
+  const uint32_t r = tp - l64;
+  const uint32_t own = min(te - tp, 64u - r), spill = te - tp - own;   // bytes here / in the next lane
+  const bool h = ((hbm >> r) & ((1ull << own) - 1ull)) != 0 || (hbn & ((1ull << spill) - 1ull)) != 0;
+  return h ? 0x80000000u : 0u;
+}
+
+// UNI: does the staged window (LDS bytes [0, wl), zero past wl) pass
+// uni_simple_char?  Lane l checks window bytes [64 l, 64 l + 64): its lead
+// bytes (11xxxxxx) one per step (2-byte chars from the wave's bitmap simple2,
+// lane l holding U+0080 + 32 l .. + 31; the others through the tables), and
+// the wave's continuation bytes (10xxxxxx) must be exactly those the leads
+// claim (no orphans).  *hbm = this lane's non-ASCII bytes (bit per byte).
+// Wave-uniform result.
+__device__ __forceinline__ bool uni_window_simple(const uint8_t *text, uint32_t wl, uint32_t lane, uint32_t simple2,
+                                                  uint64_t *hbm) {
+  const uint32_t *seg = reinterpret_cast<const uint32_t *>(text + 64 * lane);
+  uint64_t lead = 0, hm = 0;
+  uint32_t ncont = 0;
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    const uint32_t x = seg[j], hb = x & 0x80808080u, ld = hb & (x << 1);
+    ncont += (uint32_t)__popc(hb & ~ld);
+    lead |= (uint64_t)swar_nib(ld) << (4 * j);
+    hm |= (uint64_t)swar_nib(hb) << (4 * j);
+  }
+  *hbm = hm;
+  const uint32_t *tw = reinterpret_cast<const uint32_t *>(text);
+  bool ok = true;
+  uint32_t claimed = 0;
+  while (__any(lead != 0)) {                            // one lead per lane per step
+    const bool has = lead != 0;
+    const uint32_t pos = 64 * lane + (has ? (uint32_t)__builtin_ctzll(lead) : 0u);
+    lead &= lead - 1;
+    const uint32_t w = __builtin_amdgcn_alignbyte(tw[(pos >> 2) + 1], tw[pos >> 2], pos & 3);
+    const uint32_t b0 = w & 0xFFu, b1 = (w >> 8) & 0xFFu;
+    // 2-byte chars (U+0080..U+07FF: Latin, Greek, Cyrillic, ...) from the
+    // wave's bitmap, the others through the tables
+    const bool two = has && b0 >= 0xC2u && b0 < 0xE0u && (b1 & 0xC0u) == 0x80u && wl - pos >= 2;
+    const uint32_t cp = ((b0 & 0x1Fu) << 6) | (b1 & 0x3Fu);
+    const uint32_t bits = (uint32_t)__shfl((int)simple2, two ? (int)((cp - 0x80u) >> 5) : 0, 64);
+    uint32_t len = 0;
+    if (two) len = ((bits >> (cp & 31u)) & 1u) ? 2u : 0u;
+    else if (has) len = uni_simple_char(w, wl - pos);
+    ok &= !has || len != 0;
+    claimed += len ? len - 1 : 0u;
+  }
+  return __all(ok) && wave_sum(claimed) == wave_sum(ncont);
+}
+
 // UNI = true (round 5): the documents the ASCII pass flagged (uni_list), one
 // wave each, by the same rules with non-ASCII bytes read as letters when
 // uni_simple_span passes the document (its flag is then cleared); the rest
@@ -1386,20 +1462,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     return uni_scan((cur & ~63ull) + (uint64_t)gridDim.x * 64);
   };
   const uint64_t u0 = UNI ? uni_scan((uint64_t)blockIdx.x * 64) : ubeg;
-  // UNI: which 2-byte chars (U+0080..U+07FF) uni_simple_char passes, one bit
-  // each: lane l holds U+0080 + 32 l .. + 31 (lanes >= 60: none)
-  uint32_t simple2 = 0;
-  if (UNI && u0 != kNoUnit) {
-    const uint32_t c0 = min(0x80u + 32u * lane, 0x7E0u);    // (lanes >= 60: masked below)
-    const uint32_t ci = kUcClassIndex[c0 >> 8], li = kUcLowerIndex[c0 >> 8];   // 32-aligned: one table row
-#pragma unroll 8
-    for (uint32_t b = 0; b < 32; b++) {
-      const uint32_t cp = c0 + b;
-      const bool ok2 = kUcClassData[ci * 256u + (cp & 255u)] == kUcALetter && kUcLowerData[li * 256u + (cp & 255u)] == 0;
-      simple2 |= (ok2 ? 1u : 0u) << b;
-    }
-    if (lane >= 60) simple2 = 0;
-  }
+  const uint32_t simple2 = UNI && u0 != kNoUnit ? uni_simple2_bitmap(lane) : 0u;
   const uint64_t ulim = UNI ? kNoUnit : uend;
   DocMeta meta;
   if (u0 < ulim) {
@@ -1486,41 +1549,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     }
     uint64_t hbm = 0;                                       // UNI: this lane's non-ASCII bytes
     if (bad && UNI) {                                       // simple non-ASCII text: taken here
-      // lane l: window bytes [64 l, 64 l + 64); lead bytes (11xxxxxx) are
-      // checked one by one, and the continuation bytes (10xxxxxx) must be
-      // exactly those the leads claim (no orphans)
-      const uint32_t *seg = reinterpret_cast<const uint32_t *>(sm.text + 64 * lane);
-      uint64_t lead = 0;
-      uint32_t ncont = 0;
-#pragma unroll
-      for (int j = 0; j < 16; j++) {
-        const uint32_t x = seg[j], hb = x & 0x80808080u, ld = hb & (x << 1);
-        ncont += (uint32_t)__popc(hb & ~ld);
-        lead |= (uint64_t)swar_nib(ld) << (4 * j);
-        hbm |= (uint64_t)swar_nib(hb) << (4 * j);
-      }
-      const uint32_t wl = shift + (uint32_t)L;
-      const uint32_t *tw = reinterpret_cast<const uint32_t *>(sm.text);
-      bool ok = true;
-      uint32_t claimed = 0;
-      while (__any(lead != 0)) {                            // one lead per lane per step
-        const bool has = lead != 0;
-        const uint32_t pos = 64 * lane + (has ? (uint32_t)__builtin_ctzll(lead) : 0u);
-        lead &= lead - 1;
-        const uint32_t w = __builtin_amdgcn_alignbyte(tw[(pos >> 2) + 1], tw[pos >> 2], pos & 3);
-        const uint32_t b0 = w & 0xFFu, b1 = (w >> 8) & 0xFFu;
-        // 2-byte chars (U+0080..U+07FF: Latin, Greek, Cyrillic, ...) from the
-        // wave's bitmap, the others through the tables
-        const bool two = has && b0 >= 0xC2u && b0 < 0xE0u && (b1 & 0xC0u) == 0x80u && wl - pos >= 2;
-        const uint32_t cp = ((b0 & 0x1Fu) << 6) | (b1 & 0x3Fu);
-        const uint32_t bits = (uint32_t)__shfl((int)simple2, two ? (int)((cp - 0x80u) >> 5) : 0, 64);
-        uint32_t len = 0;
-        if (two) len = ((bits >> (cp & 31u)) & 1u) ? 2u : 0u;
-        else if (has) len = uni_simple_char(w, wl - pos);
-        ok &= !has || len != 0;
-        claimed += len ? len - 1 : 0u;
-      }
-      if (!__all(ok) || wave_sum(claimed) != wave_sum(ncont)) continue;   // stays flagged: k_tokenize_uwave
+      if (!uni_window_simple(sm.text, shift + (uint32_t)L, lane, simple2, &hbm)) continue;   // stays flagged: k_tokenize_uwave
       if (lane == 0) TFIDF_COLD(uni_list)[d] = 0u;
       my_uni += lane == 0;
     } else if (bad) {                                       // non-ASCII: the Unicode wave path
@@ -1559,18 +1588,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       uint32_t at = tincl - nts;
       uint32_t s0 = (uint32_t)S, s1 = (uint32_t)(S >> 32), e0 = (uint32_t)E, e1 = (uint32_t)(E >> 32);
       const uint32_t l64 = lane * 64;
-      // UNI: bit 31 of a span entry = a token of <= 8 bytes holding a
-      // non-ASCII byte (exact: such a token reaches at most into the next
-      // lane's segment; longer tokens take folded keys anyway, and fold_key
-      // finds their non-ASCII bytes itself)
+      // UNI: bit 31 of a span entry (uni_span_flag)
       const uint64_t hbn = UNI ? shfl_down64(hbm) : 0ull;
       auto hflag = [&](uint32_t tp, uint32_t te) __attribute__((always_inline)) -> uint32_t {
-        if (!UNI || te - tp > 8) return 0u;
-        const uint32_t r = tp - l64;
-        const uint32_t own = min(te - tp, 64u - r), spill = te - tp - own;   // bytes here / in the next lane
-        bool h = ((hbm >> r) & ((1ull << own) - 1ull)) != 0;
-        h |= (hbn & ((1ull << spill) - 1ull)) != 0;
-        return h ? 0x80000000u : 0u;
+        return UNI ? uni_span_flag(tp, te, l64, hbm, hbn) : 0u;
       };
       while (s0) {
         const uint32_t tp = l64 + (uint32_t)__builtin_ctz(s0);
@@ -1767,6 +1788,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
 // that cannot take this path (non-ASCII
 // text, a token of more than 255 characters, more than 512 distinct terms)
 // marks its document, which then goes to k_tokenize_long as a whole.
+// UNI = true (round 5): the units this kernel flagged for non-ASCII text
+// (uchunk_list), by the same rules with non-ASCII bytes read as letters when
+// uni_window_simple passes the window (its flag is then cleared); the rest
+// stay flagged for k_tokenize_uchunk.
+template <bool UNI = false>
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_tokenize_chunk(BuildParams p) {
   __shared__ WaveSmem sm;
   const uint32_t lane = threadIdx.x;
@@ -1784,10 +1810,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       if (lane + 64 * k < nchunks) v[k] = gload16(src + lane + 64 * k);
   };
   uint32_t my_uc = 0;                                        // units this wave flagged for k_tokenize_uchunk
-  if (blockIdx.x < n_units) { meta = chunk_meta(p, blockIdx.x); prefetch(meta); }
-  for (uint64_t u = blockIdx.x; u < n_units; u += gridDim.x) {
+  // UNI: the flagged units of this workgroup's stride
+  auto next_flagged = [&](uint64_t v) __attribute__((always_inline)) -> uint64_t {
+    while (v < n_units && p.uchunk_list[v] == 0) v += gridDim.x;
+    return v;
+  };
+  if (UNI && *p.uchunk_count == 0) return;                   // wave-uniform
+  const uint64_t u0 = UNI ? next_flagged(blockIdx.x) : blockIdx.x;
+  const uint32_t simple2 = UNI && u0 < n_units ? uni_simple2_bitmap(lane) : 0u;
+  if (u0 < n_units) { meta = chunk_meta(p, u0); prefetch(meta); }
+  uint64_t un = 0;
+  for (uint64_t u = u0; u < n_units; u = un) {
     const ChunkMeta m = meta;
-    const uint64_t un = u + gridDim.x;
+    un = UNI ? next_flagged(u + gridDim.x) : u + gridDim.x;
     uint32_t hib = 0;                                          // OR of the window's bytes: bit 7s = non-ASCII
     {   // stage (bytes outside the window zeroed), then fetch the next unit
       const uint32_t hi_b = m.shift + (uint32_t)m.L;
@@ -1814,7 +1849,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     // such a unit is not classified here): flagged for the Unicode chunk kernel
     // (a flag per unit, counted once per wave at the end — a list appended
     // with one atomic per unit serialised 15 k units on one counter)
-    if (__any((hib & 0x80808080u) != 0)) {
+    uint64_t hbm = 0;                                          // UNI: this lane's non-ASCII bytes
+    const bool nonascii = __any((hib & 0x80808080u) != 0);
+    if (UNI && nonascii) {                                     // simple non-ASCII text: taken here
+      if (!uni_window_simple(sm.text, m.shift + (uint32_t)m.L, lane, simple2, &hbm)) continue;   // k_tokenize_uchunk
+      if (lane == 0) p.uchunk_list[u] = 0u;
+    } else if (nonascii) {
       if (lane == 0) {
         if (p.uchunk_list) { p.uchunk_list[u] = 1u; my_uc++; }
         else p.chunk_fail[fail_at] = 1u;
@@ -1824,7 +1864,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     bool bad, under;
     uint64_t wbase = 0;
     bool upper;
-    const uint64_t W = lane_word_mask<false>(sm.text, lane, &bad, &under, &wbase, &upper);
+    const uint64_t W = lane_word_mask<false, UNI>(sm.text, lane, &bad, &under, &wbase, &upper);
     const uint64_t wlast = __ballot((W >> 63) & 1ull);
     const uint64_t prevW = lane ? (wlast >> (lane - 1)) & 1ull : 0ull;
     const uint64_t S = W & ~((W << 1) | prevW);
@@ -1848,6 +1888,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     {
       uint32_t at = tincl - nts;
       uint32_t s0 = (uint32_t)S, s1 = (uint32_t)(S >> 32), e0 = (uint32_t)E, e1 = (uint32_t)(E >> 32);
+      const uint64_t hbn = UNI ? shfl_down64(hbm) : 0ull;
       while (s0 | s1) {
         const uint32_t tp = lane * 64 + (s0 ? (uint32_t)__builtin_ctz(s0) : 32 + (uint32_t)__builtin_ctz(s1));
         const uint32_t te = (e0 | e1) ? lane * 64 + (e0 ? (uint32_t)__builtin_ctz(e0) : 32 + (uint32_t)__builtin_ctz(e1))
@@ -1856,20 +1897,20 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         if (e0) e0 &= e0 - 1; else e1 &= e1 - 1;
         if (tp >= A && tp < B) {
           longtok |= te - tp > 8;
-          sm.list[at++] = span_entry(tp, te, 0);
+          sm.list[at++] = span_entry(tp, te, 0) | (UNI ? uni_span_flag(tp, te, lane * 64, hbm, hbn) : 0u);
         }
       }
     }
     asm volatile("" ::: "memory");
-    const bool anylong = __any(longtok) || under;
+    const bool anylong = __any(longtok) || under || (UNI && nonascii);
     uint32_t nu = 0, toks = 0;
     bool overflow = false;
     for (uint32_t tb = 0; tb < ntok && !overflow;) {
       const uint32_t rem = ntok - tb;
       if (anylong) {
-        if (rem > 256) { hist2<8, true, false>(sm, lane, tb, ntok, under, upper, nu, toks, overflow); tb += 512; }
-        else if (rem > 128) { hist2<4, true, false>(sm, lane, tb, ntok, under, upper, nu, toks, overflow); tb += 256; }
-        else { hist2<2, true, false>(sm, lane, tb, ntok, under, upper, nu, toks, overflow); tb += 128; }
+        if (rem > 256) { hist2<8, true, false, UNI>(sm, lane, tb, ntok, under, upper, nu, toks, overflow); tb += 512; }
+        else if (rem > 128) { hist2<4, true, false, UNI>(sm, lane, tb, ntok, under, upper, nu, toks, overflow); tb += 256; }
+        else { hist2<2, true, false, UNI>(sm, lane, tb, ntok, under, upper, nu, toks, overflow); tb += 128; }
       } else {
         if (rem > 256) { hist2<8, false, false>(sm, lane, tb, ntok, under, upper, nu, toks, overflow); tb += 512; }
         else if (rem > 128) { hist2<4, false, false>(sm, lane, tb, ntok, under, upper, nu, toks, overflow); tb += 256; }
@@ -1901,7 +1942,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     }
     uint32_t g[kWaveK], tf[kWaveK], tdoc[kWaveK];
     uint32_t actm = 0;
-    resolve_terms<false, false>(sm, p, lane, nu, (uint32_t)m.d, g, tf, tdoc, actm, nullptr, nullptr, m.s0 - m.shift);
+    resolve_terms<false, false, UNI>(sm, p, lane, nu, (uint32_t)m.d, g, tf, tdoc, actm, nullptr, nullptr, m.s0 - m.shift,
+                                     m.shift + (uint32_t)m.L);
     {   // the unit's (slot, tf) pairs, counting-sorted by slot bucket in LDS (text and retry
         // queue are dead here), stored as one contiguous run; bucket starts to pair_ub
       uint32_t *bcnt = reinterpret_cast<uint32_t *>(sm.qkey);          // [0, 64) counts, [64, 128) starts
@@ -2755,7 +2797,13 @@ hipError_t launch_tokenize_wave_uni(const BuildParams &p, int grid, hipStream_t 
   return hipGetLastError();
 }
 hipError_t launch_tokenize_chunks(const BuildParams &p, int grid, hipStream_t s) {
-  hipLaunchKernelGGL(k_tokenize_chunk, dim3(grid), dim3(64), 0, s, p);
+  hipLaunchKernelGGL(k_tokenize_chunk<false>, dim3(grid), dim3(64), 0, s, p);
+  return hipGetLastError();
+}
+// The units k_tokenize_chunk flagged for non-ASCII text, by the wave rules
+// where they allow (k_tokenize_chunk<UNI>); before k_tokenize_uchunk.
+hipError_t launch_tokenize_chunks_uni(const BuildParams &p, int grid, hipStream_t s) {
+  hipLaunchKernelGGL(k_tokenize_chunk<true>, dim3(grid), dim3(64), 0, s, p);
   return hipGetLastError();
 }
 hipError_t launch_long_rows(const BuildParams &p, uint32_t n_docs, hipStream_t s) {

@@ -1152,6 +1152,10 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
       if (uch) HIP_TRY(hipMemsetAsync(ix->uchunk.p, 0, (size_t)(cp.n_chunks + 4) * 4, s));
       const uint64_t grid = std::min<uint64_t>(cp.n_chunks, (uint64_t)ix->num_cus * kWaveWGsPerCU);
       HIP_TRY(launch_tokenize_chunks(cp, (int)grid, s));
+      // flagged units by the wave rules where their text allows (TFIDF_NO_UNIWAVE: all
+      // of them to the Unicode chunk kernel; A/B only), then the rest
+      const char *nouw = getenv("TFIDF_NO_UNIWAVE");
+      if (uch && !(nouw && *nouw && *nouw != '0')) HIP_TRY(launch_tokenize_chunks_uni(cp, (int)grid, s));
       if (uch)      // the count is read on the device: exits at once when no unit was listed
         HIP_TRY(launch_tokenize_uchunk(cp, (int)std::min<uint64_t>(cp.n_chunks, (uint64_t)ix->num_cus * kUchunkWGsPerCU), s));
       HIP_TRY(launch_long_rows(cp, (uint32_t)n, s));

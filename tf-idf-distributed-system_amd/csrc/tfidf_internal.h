@@ -231,6 +231,7 @@ inline void allow_dyn_lds(const void *fn, int bytes, std::atomic<uint64_t> &done
 // --- launch wrappers (kernels_index.hip) ---
 hipError_t launch_tokenize_wave(const BuildParams &p, int grid, hipStream_t s);
 hipError_t launch_tokenize_wave_uni(const BuildParams &p, int grid, hipStream_t s);   // flagged non-ASCII documents
+hipError_t launch_tokenize_chunks_uni(const BuildParams &p, int grid, hipStream_t s);  // flagged non-ASCII book units
 constexpr uint32_t kWaveWGsPerCU = 8;       // 64-thread workgroups per CU (2 waves/SIMD: VGPR- and LDS-bound)
 constexpr uint32_t kWaveGroups = 128;     // CSR row groups per wave unit (documents x ranges, k_tokenize_wave)
 constexpr uint32_t kPackMaxDocs = 16;     // documents per packed window (<= kPackMax, kernels_index.hip)
