@@ -19,14 +19,14 @@ O = sys.argv[1]
 order = [l.split() for l in open(O + "/order.txt") if l.strip() and not l.startswith("dispatch")]
 vals = collections.defaultdict(dict)        # dispatch index -> counter -> value
 for f in sorted(glob.glob(O + "/p*/**/*counter_collection.csv", recursive=True)):
-    rows = list(csv.DictReader(open(f)))
+    rows = [r for r in csv.DictReader(open(f)) if "k_" in r["Kernel_Name"]]   # (not the memset's fill kernel)
     ids = sorted({int(r["Dispatch_Id"]) for r in rows})
     rank = {d: k for k, d in enumerate(ids)}
     for r in rows:
         vals[rank[int(r["Dispatch_Id"])]][r["Counter_Name"]] = vals[rank[int(r["Dispatch_Id"])]].get(r["Counter_Name"], 0) + float(r["Counter_Value"])
 dur = []
 for f in glob.glob(O + "/kt/**/*kernel_trace.csv", recursive=True):
-    rows = sorted(csv.DictReader(open(f)), key=lambda r: int(r["Dispatch_Id"]))
+    rows = sorted([r for r in csv.DictReader(open(f)) if "k_" in r["Kernel_Name"]], key=lambda r: int(r["Dispatch_Id"]))
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows]
 print("%-22s %12s %8s %10s %10s %10s %10s %10s %10s %9s" % ("launch", "bytes req", "ms", "FETCH/req", "RDREQ", "RDREQ32", "RDREQ64", "DRAM", "DRAM32", "L2 hit%"))
 for k, (name, probes, req) in enumerate(order):
