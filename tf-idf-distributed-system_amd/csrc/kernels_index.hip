@@ -1476,13 +1476,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
            *pk_start = pk_len + 2 * kPackMax;
   uint64_t *pk_row = sm.qkey + 2 * kPackMax;
 
-  uint64_t un = 0;
-  for (uint64_t u = u0; u < ulim; u = un) {
+  uint64_t unext = 0;                                       // UNI: the next flagged document
+  for (uint64_t u = u0; u < ulim; u = UNI ? unext : u + ustep) {
     const uint64_t d = meta.d, src = meta.src, L = meta.L, s0 = meta.s0;
     const uint32_t shift = meta.shift, np = meta.np;
     const uint64_t pofs = meta.pofs;
     const bool fits = fits_wave(meta);
-    un = UNI ? uni_next(u) : u + ustep;
+    const uint64_t un = UNI ? uni_next(u) : u + ustep;
+    if (UNI) unext = un;
     if (!fits) {
       if (PACK) defer_pack(p, d, np, lane);
       else if (UNI) {}                                      // (flagged documents fit: the ASCII pass staged them)
@@ -1590,9 +1591,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       const uint32_t l64 = lane * 64;
       // UNI: bit 31 of a span entry (uni_span_flag)
       const uint64_t hbn = UNI ? shfl_down64(hbm) : 0ull;
-      auto hflag = [&](uint32_t tp, uint32_t te) __attribute__((always_inline)) -> uint32_t {
-        return UNI ? uni_span_flag(tp, te, l64, hbm, hbn) : 0u;
-      };
       while (s0) {
         const uint32_t tp = l64 + (uint32_t)__builtin_ctz(s0);
         const uint32_t te = e0 ? l64 + (uint32_t)__builtin_ctz(e0) : (e1 ? l64 + 32 + (uint32_t)__builtin_ctz(e1) : nz);
@@ -1600,7 +1598,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         if (e0) e0 &= e0 - 1; else e1 &= e1 - 1;
         longtok |= te - tp > 8;
         const uint32_t j = PACK ? dbase + (uint32_t)__popcll(bm & ((2ull << (tp - l64)) - 1)) : 0u;
-        sm.list[at++] = span_entry(tp, te, j) | hflag(tp, te);
+        sm.list[at++] = span_entry(tp, te, j) | (UNI ? uni_span_flag(tp, te, l64, hbm, hbn) : 0u);
       }
       while (s1) {
         const uint32_t tp = l64 + 32 + (uint32_t)__builtin_ctz(s1);
@@ -1609,7 +1607,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         e1 &= e1 - 1;
         longtok |= te - tp > 8;
         const uint32_t j = PACK ? dbase + (uint32_t)__popcll(bm & ((2ull << (tp - l64)) - 1)) : 0u;
-        sm.list[at++] = span_entry(tp, te, j) | hflag(tp, te);
+        sm.list[at++] = span_entry(tp, te, j) | (UNI ? uni_span_flag(tp, te, l64, hbm, hbn) : 0u);
       }
     }
     asm volatile("" ::: "memory");
