@@ -56,7 +56,7 @@ def parse():
                     help="fraction of documents made non-ASCII (Unicode tokenizer path); 0 = the cfg-2 corpus")
     ap.add_argument("--no-e2e", dest="e2e", action="store_false",
                     help="skip the PCIe-inclusive (host corpus -> HBM -> index) measurement")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r04", "traffic.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r05", "traffic.json"),
                     help="per-kernel HBM bytes from tools/prof_round.sh (rocprofv3 PMC passes of this workload)")
     return ap.parse_args()
 
