@@ -110,7 +110,7 @@ typedef struct tfidf_index_stats {
   uint64_t unicode_docs;  /* documents (window <= 4 KB) the ASCII wave path found non-ASCII text in */
   uint64_t long_chunked;  /* long documents indexed chunk-parallel (the rest of long_docs: k_tokenize_long) */
   uint64_t malformed_docs;/* documents that are not valid UTF-8, indexed empty (tfidf_malformed_docs) */
-  uint64_t hash_seed;     /* seed of the hashed term keys (> 16-byte and non-ASCII terms); 0 unless a
+  uint64_t hash_seed;     /* seed of the hashed term keys (> 16-byte terms, > 14-byte non-ASCII ones); 0 unless a
                              hash collision was detected and the build redone (term identity stays
                              exact: every merge under a hashed key compares the strings) */
   uint64_t hash_rebuilds; /* seed attempt in force (0 = first seed): builds redone in the last commit because of

@@ -161,8 +161,11 @@ def seed_corpus():
     rng = np.random.default_rng(11)
     base = synth.corpus(400, V=3000, len_min=10, len_max=60)
     longw = [bytes(rng.integers(97, 123, int(rng.integers(17, 21))).astype(np.uint8)) for _ in range(40)]
+    # (the last two: non-ASCII terms over 14 bytes, so hashed keys — of equal
+    # length, so they collide under TFIDF_TEST_WEAK_HASH; shorter ones are exact)
     uni = [w.encode() for w in ("café", "naïve", "über", "façade", "señor", "ångström", "smörgåsbord",
-                                 "crème", "brûlée", "jalapeño", "Ελλάδα", "москва", "日本語")]
+                                 "crème", "brûlée", "jalapeño", "Ελλάδα", "москва", "日本語",
+                                 "übernationalität", "übernationalitát")]
     texts = []
     for i, t in enumerate(base):
         extra = [longw[int(j)] for j in rng.integers(0, len(longw), 3)] + [uni[int(j)] for j in

@@ -1,5 +1,6 @@
 """Exact term identity for hashed keys (terms of more than 16 bytes, and
-every non-ASCII term): the engine never lets two different terms share a
+non-ASCII terms of more than 14; shorter non-ASCII terms have exact keys
+since round 5): the engine never lets two different terms share a
 key.  Every merge under a hashed key compares the lower-cased strings (the
 per-document tables of the Unicode wave path and of the long path, and the
 global dictionary through each slot's reference occurrence); a mismatch makes

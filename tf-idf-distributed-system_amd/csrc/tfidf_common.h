@@ -38,6 +38,12 @@ constexpr uint32_t kExactKeyChars = 16;         // longer keys carry a hash in h
 constexpr uint64_t kKeyValid = 1ull << 63;      // in hi
 constexpr uint64_t kLoLong = 1ull << 63;        // in lo: more than 8 bytes
 constexpr uint64_t kLoHashed = 1ull << 55;      // in lo: more than 16 bytes (hi is a hash)
+// Non-ASCII terms of <= kExactUniChars bytes (round 5): an exact key too — their
+// bytes and length packed into hi's 63 bits and 53 bits of lo around the flags,
+// with kLoUniExact set (bit 7 of byte 5 is clear in every other long key: ASCII
+// bytes, or a hash masked with 0x7F bytes).  Longer non-ASCII terms are hashed.
+constexpr uint64_t kLoUniExact = 1ull << 47;
+constexpr uint32_t kExactUniChars = 14;
 constexpr uint32_t kRangeBits = 15;             // 32768 dictionary slots per LDS range tile
 constexpr uint32_t kRangeSlots = 1u << kRangeBits;
 constexpr uint32_t kBlockDocs = 8192;           // doc block of the inverted index / scorer
@@ -134,6 +140,12 @@ struct KeyBuilder {
   // seed: the index's hash seed (0 unless a build met a hash collision and
   // was redone, tfidf_capi.hip); it changes the hashed forms only.
   TFIDF_HD void finish(uint64_t *klo, uint64_t *khi, uint64_t seed = 0) const {
+    if (na && n <= kExactUniChars) {                                // round 5: exact, no identity check
+      const uint64_t r = (w0 >> 63) | ((w1 & 0xFFFFFFFFFFFFull) << 1) | ((uint64_t)n << 49);   // 53 bits
+      *klo = kLoLong | kLoUniExact | (r & ((1ull << 47) - 1)) | ((r >> 47) << 48);
+      *khi = (w0 & ~kKeyValid) | kKeyValid;
+      return;
+    }
     if (seed == kWeakHashSeed && (na || n > kExactKeyChars)) {      // tests: every same-length pair collides
       *klo = (na ? 0ull : (w0 & 0x7F7F7F7F7F7F7F7Full)) | kLoLong | kLoHashed;
       *khi = (uint64_t)n | kKeyValid;
@@ -162,6 +174,13 @@ TFIDF_HD bool key_is_hashed(uint64_t lo) { return (lo & kLoHashed) != 0; }
 // Decode an exact key back to bytes; returns length (0 if hashed).
 TFIDF_HD uint32_t key_decode(uint64_t lo, uint64_t hi, char *out) {
   if (key_is_hashed(lo)) return 0;
+  if ((lo & kLoLong) && (lo & kLoUniExact)) {                       // exact non-ASCII form
+    const uint64_t r = (lo & ((1ull << 47) - 1)) | (((lo >> 48) & 0x3Full) << 47);
+    const uint32_t n = (uint32_t)(r >> 49) & 0xFu;
+    const uint64_t w[2] = {(hi & ~kKeyValid) | ((r & 1ull) << 63), (r >> 1) & 0xFFFFFFFFFFFFull};
+    for (uint32_t i = 0; i < n; i++) out[i] = (char)(uint8_t)(w[i >> 3] >> (8 * (i & 7)));
+    return n;
+  }
   const uint64_t w[2] = {lo & ~kLoLong, (lo & kLoLong) ? (hi & ~kKeyValid) : 0ull};
   uint32_t n = 0;
   for (int i = 0; i < 16; i++) {
