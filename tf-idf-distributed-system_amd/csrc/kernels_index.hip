@@ -1519,9 +1519,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     bool upper;
     uint64_t W;
     {
-      const uint32_t nrows = (shift + (uint32_t)L + 1023) >> 10;
+      // a byte >= 0x80 (in the staged registers): the document goes to the UNI
+      // pass unclassified (nrows 0; flagged below as `bad`)
+      bool skipc = false;
+      if (!UNI && !PACK) {
+        uint32_t hx = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) hx |= v[k].x | v[k].y | v[k].z | v[k].w;
+        skipc = __any((hx & 0x80808080u) != 0);
+      }
+      const uint32_t nrows = skipc ? 0u : (shift + (uint32_t)L + 1023) >> 10;
       uint16_t *wm16 = reinterpret_cast<uint16_t *>(sm.list);            // the token list is written after
       W = regs_word_mask<PACK, UNI>(v, nrows, sm.text, wm16, wm16 + 256, lane, &bad, &under, &wbase, &upper);
+      bad |= skipc;
     }
     // the next document's window, now that this one's registers are consumed
     if (un < ulim) { meta = unit_meta<PACK>(p, un, lane); prefetch_wave(p, meta, lane, v); }
