@@ -957,7 +957,10 @@ __device__ __forceinline__ void hist2(WaveSmem &sm, uint32_t lane, uint32_t tb, 
     const uint32_t l0 = t0[k] | (PACK ? pack_tag(span_doc(ent[k])) : 0u);
     tkey[k] = (uint64_t)l0 | ((uint64_t)t1[k] << 32);
     slot[k] = table_slot(l0, t1[k]);
-    const bool hh = UNI && (ent[k] >> 31) != 0;          // UNI: may hold a non-ASCII byte (span list flag)
+    // UNI: an 8-byte token holding a non-ASCII byte takes a folded key (its byte
+    // 7 may have bit 63's place); shorter ones keep their bytes as the table key
+    // (bit 63 clear: exact identity, their dictionary key derived from it)
+    const bool hh = UNI && (ent[k] >> 31) != 0 && n == 8;
     pm[k] = __ballot(in & (n <= 8) & valid & !hh);
     if (FOLD) lm |= (uint64_t)(__ballot(in & ((n > 8) | hh)) != 0) << k;
   }
@@ -969,7 +972,7 @@ __device__ __forceinline__ void hist2(WaveSmem &sm, uint32_t lane, uint32_t tb, 
         const uint32_t e = ent[k];
         const uint32_t tp = e & kSpanMask, n = ((e >> 16) & kSpanMask) - tp;
         bool ok = false;
-        if (lane + 64u * k < left && (n > 8 || (UNI && (e >> 31) != 0))) {
+        if (lane + 64u * k < left && (n > 8 || (UNI && (e >> 31) != 0 && n == 8))) {
           if (n > kMaxTokenLen) {
             toolong = true;
           } else {
@@ -1112,6 +1115,19 @@ __device__ __noinline__ uint64_t uni_find_verify(uint64_t *dict, uint32_t mask, 
 
 // UNI: folded terms keyed by the Unicode key builder (lower-cased code
 // points; the same key the Unicode and long paths give the term).
+// UNI: dictionary key of a short table key holding a non-ASCII byte (the
+// token's lower-cased bytes, <= 7 of them: an exact key, no identity check,
+// so no occurrence is needed).
+__device__ __noinline__ void uni_key_from_short(uint64_t key, uint64_t *lo, uint64_t *hi) {
+  KeyBuilder kb;
+  for (uint32_t i = 0; i < 8; i++) {
+    const uint8_t c = (uint8_t)(key >> (8 * i));
+    if (!c) break;
+    kb.push(c);
+  }
+  kb.finish(lo, hi, 0);
+}
+
 // The document passed uni_simple_char, so its non-ASCII chars are their own
 // lower case: the key builder's bytes are the token's with ASCII lower-cased
 // (what uc_token_key would push, without decoding or the case tables).
@@ -1146,7 +1162,8 @@ __device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p
         const uint32_t s = slots[in ? idx : 0u] & (kWaveSlots - 1);
         const uint64_t key = sm.key[s];
         tf[k] = (sm.cnt[s >> 1] >> (16 * (s & 1))) & 0xFFFFu;
-        const bool f = in & ((key & kFoldBit) != 0);
+        // UNI: a short table key holding a non-ASCII byte is not its dictionary key
+        const bool f = in & (((key & kFoldBit) != 0) | (UNI && (key & 0x8080808080808080ull) != 0));
         const bool sh = in & !f;
         tdoc[k] = PACK ? key_doc(key) : 0u;
         if (PACK && in) { atomicAdd(&pk_len[tdoc[k]], tf[k]); atomicAdd(&pk_nu[tdoc[k]], 1u); }
@@ -1168,9 +1185,13 @@ __device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p
         const uint64_t key = sm.key[slots[lane + 64 * k]];
         const uint32_t n = (uint32_t)key & 0xFFu, tp = (uint32_t)(key >> 13) & 0x1FFFu;
         bool valid;
-        if (UNI && (key & kFoldUni)) uni_dict_key(sm.text, tp, n, &flo, &fhi, TFIDF_COLD(hash_seed));
-        else token_key(sm.text, tp, tp + n, &flo, &fhi, &valid, TFIDF_COLD(hash_seed));
-        mine = dict_ref_word(wbase + tp, n);
+        if (UNI && !(key & kFoldBit)) {                    // short non-ASCII term: exact key from its bytes
+          uni_key_from_short(key, &flo, &fhi);
+        } else {
+          if (UNI && (key & kFoldUni)) uni_dict_key(sm.text, tp, n, &flo, &fhi, TFIDF_COLD(hash_seed));
+          else token_key(sm.text, tp, tp + n, &flo, &fhi, &valid, TFIDF_COLD(hash_seed));
+          mine = dict_ref_word(wbase + tp, n);
+        }
       }
       uint32_t gg;
       if (UNI) {
@@ -1606,18 +1627,20 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         const uint32_t te = e0 ? l64 + (uint32_t)__builtin_ctz(e0) : (e1 ? l64 + 32 + (uint32_t)__builtin_ctz(e1) : nz);
         s0 &= s0 - 1;
         if (e0) e0 &= e0 - 1; else e1 &= e1 - 1;
-        longtok |= te - tp > 8;
+        const uint32_t fl = UNI ? uni_span_flag(tp, te, l64, hbm, hbn) : 0u;
+        longtok |= te - tp > 8 || (UNI && fl && te - tp == 8);
         const uint32_t j = PACK ? dbase + (uint32_t)__popcll(bm & ((2ull << (tp - l64)) - 1)) : 0u;
-        sm.list[at++] = span_entry(tp, te, j) | (UNI ? uni_span_flag(tp, te, l64, hbm, hbn) : 0u);
+        sm.list[at++] = span_entry(tp, te, j) | fl;
       }
       while (s1) {
         const uint32_t tp = l64 + 32 + (uint32_t)__builtin_ctz(s1);
         const uint32_t te = e1 ? l64 + 32 + (uint32_t)__builtin_ctz(e1) : nz;
         s1 &= s1 - 1;
         e1 &= e1 - 1;
-        longtok |= te - tp > 8;
+        const uint32_t fl = UNI ? uni_span_flag(tp, te, l64, hbm, hbn) : 0u;
+        longtok |= te - tp > 8 || (UNI && fl && te - tp == 8);
         const uint32_t j = PACK ? dbase + (uint32_t)__popcll(bm & ((2ull << (tp - l64)) - 1)) : 0u;
-        sm.list[at++] = span_entry(tp, te, j) | (UNI ? uni_span_flag(tp, te, l64, hbm, hbn) : 0u);
+        sm.list[at++] = span_entry(tp, te, j) | fl;
       }
     }
     asm volatile("" ::: "memory");
@@ -1625,7 +1648,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
 
     // ---- per-document histogram in LDS (folded-key and '_'-only checks only
     // when the document holds a token of more than 8 bytes or a '_')
-    const bool anylong = __any(longtok) || under || (UNI && bad);
+    const bool anylong = __any(longtok) || under;
     uint32_t nu = 0, len = 0;
     bool overflow = false;
     for (uint32_t tb = 0; tb < ntok && !overflow;) {       // batch width by what is left
@@ -1904,13 +1927,14 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         if (s0) s0 &= s0 - 1; else s1 &= s1 - 1;
         if (e0) e0 &= e0 - 1; else e1 &= e1 - 1;
         if (tp >= A && tp < B) {
-          longtok |= te - tp > 8;
-          sm.list[at++] = span_entry(tp, te, 0) | (UNI ? uni_span_flag(tp, te, lane * 64, hbm, hbn) : 0u);
+          const uint32_t fl = UNI ? uni_span_flag(tp, te, lane * 64, hbm, hbn) : 0u;
+          longtok |= te - tp > 8 || (UNI && fl && te - tp == 8);
+          sm.list[at++] = span_entry(tp, te, 0) | fl;
         }
       }
     }
     asm volatile("" ::: "memory");
-    const bool anylong = __any(longtok) || under || (UNI && nonascii);
+    const bool anylong = __any(longtok) || under;
     uint32_t nu = 0, toks = 0;
     bool overflow = false;
     for (uint32_t tb = 0; tb < ntok && !overflow;) {
