@@ -854,10 +854,6 @@ __device__ __forceinline__ uint32_t table_slot(uint32_t l0, uint32_t l1) {
   const uint32_t x = l0 ^ __builtin_amdgcn_alignbit(l1, l1, 16);
   return (uint32_t)__umul24(x ^ (x >> 11), 0x2C1B3Du) >> (32 - kWaveSlotBits);
 }
-__device__ __forceinline__ uint64_t shfl_down64(uint64_t v) {   // lane l gets lane l + 1's (lane 63: 0)
-  const uint32_t lo = (uint32_t)__shfl_down((int)(uint32_t)v, 1, 64), hi = (uint32_t)__shfl_down((int)(uint32_t)(v >> 32), 1, 64);
-  return threadIdx.x % 64 == 63 ? 0ull : (((uint64_t)hi << 32) | lo);
-}
 __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
   return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
@@ -958,9 +954,12 @@ __device__ __forceinline__ void hist2(WaveSmem &sm, uint32_t lane, uint32_t tb, 
     tkey[k] = (uint64_t)l0 | ((uint64_t)t1[k] << 32);
     slot[k] = table_slot(l0, t1[k]);
     // UNI: an 8-byte token holding a non-ASCII byte takes a folded key (its byte
-    // 7 may have bit 63's place); shorter ones keep their bytes as the table key
-    // (bit 63 clear: exact identity, their dictionary key derived from it)
-    const bool hh = UNI && (ent[k] >> 31) != 0 && n == 8;
+    // 7 may have bit 63's place; marked in the entry's spare bit 31 for the fold
+    // block); shorter ones keep their bytes as the table key (bit 63 clear:
+    // exact identity, their dictionary key derived from it).  (A document with
+    // an 8-byte token runs the folded histogram: the span loop counts them long.)
+    const bool hh = UNI && n == 8 && ((t0[k] | t1[k]) & 0x80808080u) != 0;
+    if (UNI) ent[k] |= hh ? 0x80000000u : 0u;
     pm[k] = __ballot(in & (n <= 8) & valid & !hh);
     if (FOLD) lm |= (uint64_t)(__ballot(in & ((n > 8) | hh)) != 0) << k;
   }
@@ -1378,39 +1377,22 @@ __device__ __forceinline__ uint32_t uni_simple2_bitmap(uint32_t lane) {
   return lane >= 60 ? 0u : bm;
 }
 
-// UNI: span list flag (bit 31) of a token [tp, te) starting in the segment of
-// the lane at l64: a token of <= 8 bytes holding a non-ASCII byte (exact:
-// such a token reaches at most into the next lane's segment, whose
-// non-ASCII bytes are hbn; longer tokens take folded keys anyway, and
-// fold_key finds their non-ASCII bytes itself).
-__device__ __forceinline__ uint32_t uni_span_flag(uint32_t tp, uint32_t te, uint32_t l64, uint64_t hbm, uint64_t hbn) {
-  if (te - tp > 8) return 0u;
-  const uint32_t r = tp - l64;
-  const uint32_t own = min(te - tp, 64u - r), spill = te - tp - own;   // bytes here / in the next lane
-  const bool h = ((hbm >> r) & ((1ull << own) - 1ull)) != 0 || (hbn & ((1ull << spill) - 1ull)) != 0;
-  return h ? 0x80000000u : 0u;
-}
-
 // UNI: does the staged window (LDS bytes [0, wl), zero past wl) pass
 // uni_simple_char?  Lane l checks window bytes [64 l, 64 l + 64): its lead
 // bytes (11xxxxxx) one per step (2-byte chars from the wave's bitmap simple2,
 // lane l holding U+0080 + 32 l .. + 31; the others through the tables), and
 // the wave's continuation bytes (10xxxxxx) must be exactly those the leads
-// claim (no orphans).  *hbm = this lane's non-ASCII bytes (bit per byte).
-// Wave-uniform result.
-__device__ __forceinline__ bool uni_window_simple(const uint8_t *text, uint32_t wl, uint32_t lane, uint32_t simple2,
-                                                  uint64_t *hbm) {
+// claim (no orphans).  Wave-uniform result.
+__device__ __forceinline__ bool uni_window_simple(const uint8_t *text, uint32_t wl, uint32_t lane, uint32_t simple2) {
   const uint32_t *seg = reinterpret_cast<const uint32_t *>(text + 64 * lane);
-  uint64_t lead = 0, hm = 0;
+  uint64_t lead = 0;
   uint32_t ncont = 0;
 #pragma unroll
   for (int j = 0; j < 16; j++) {
     const uint32_t x = seg[j], hb = x & 0x80808080u, ld = hb & (x << 1);
     ncont += (uint32_t)__popc(hb & ~ld);
     lead |= (uint64_t)swar_nib(ld) << (4 * j);
-    hm |= (uint64_t)swar_nib(hb) << (4 * j);
   }
-  *hbm = hm;
   const uint32_t *tw = reinterpret_cast<const uint32_t *>(text);
   bool ok = true;
   uint32_t claimed = 0;
@@ -1579,9 +1561,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       }
       W &= ~(jm & ~wbase);
     }
-    uint64_t hbm = 0;                                       // UNI: this lane's non-ASCII bytes
     if (bad && UNI) {                                       // simple non-ASCII text: taken here
-      if (!uni_window_simple(sm.text, shift + (uint32_t)L, lane, simple2, &hbm)) continue;   // stays flagged: k_tokenize_uwave
+      if (!uni_window_simple(sm.text, shift + (uint32_t)L, lane, simple2)) continue;   // stays flagged: k_tokenize_uwave
       if (lane == 0) TFIDF_COLD(uni_list)[d] = 0u;
       my_uni += lane == 0;
     } else if (bad) {                                       // non-ASCII: the Unicode wave path
@@ -1620,27 +1601,23 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       uint32_t at = tincl - nts;
       uint32_t s0 = (uint32_t)S, s1 = (uint32_t)(S >> 32), e0 = (uint32_t)E, e1 = (uint32_t)(E >> 32);
       const uint32_t l64 = lane * 64;
-      // UNI: bit 31 of a span entry (uni_span_flag)
-      const uint64_t hbn = UNI ? shfl_down64(hbm) : 0ull;
       while (s0) {
         const uint32_t tp = l64 + (uint32_t)__builtin_ctz(s0);
         const uint32_t te = e0 ? l64 + (uint32_t)__builtin_ctz(e0) : (e1 ? l64 + 32 + (uint32_t)__builtin_ctz(e1) : nz);
         s0 &= s0 - 1;
         if (e0) e0 &= e0 - 1; else e1 &= e1 - 1;
-        const uint32_t fl = UNI ? uni_span_flag(tp, te, l64, hbm, hbn) : 0u;
-        longtok |= te - tp > 8 || (UNI && fl && te - tp == 8);
+        longtok |= te - tp > (UNI ? 7u : 8u);
         const uint32_t j = PACK ? dbase + (uint32_t)__popcll(bm & ((2ull << (tp - l64)) - 1)) : 0u;
-        sm.list[at++] = span_entry(tp, te, j) | fl;
+        sm.list[at++] = span_entry(tp, te, j);
       }
       while (s1) {
         const uint32_t tp = l64 + 32 + (uint32_t)__builtin_ctz(s1);
         const uint32_t te = e1 ? l64 + 32 + (uint32_t)__builtin_ctz(e1) : nz;
         s1 &= s1 - 1;
         e1 &= e1 - 1;
-        const uint32_t fl = UNI ? uni_span_flag(tp, te, l64, hbm, hbn) : 0u;
-        longtok |= te - tp > 8 || (UNI && fl && te - tp == 8);
+        longtok |= te - tp > (UNI ? 7u : 8u);
         const uint32_t j = PACK ? dbase + (uint32_t)__popcll(bm & ((2ull << (tp - l64)) - 1)) : 0u;
-        sm.list[at++] = span_entry(tp, te, j) | fl;
+        sm.list[at++] = span_entry(tp, te, j);
       }
     }
     asm volatile("" ::: "memory");
@@ -1880,10 +1857,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     // such a unit is not classified here): flagged for the Unicode chunk kernel
     // (a flag per unit, counted once per wave at the end — a list appended
     // with one atomic per unit serialised 15 k units on one counter)
-    uint64_t hbm = 0;                                          // UNI: this lane's non-ASCII bytes
     const bool nonascii = __any((hib & 0x80808080u) != 0);
     if (UNI && nonascii) {                                     // simple non-ASCII text: taken here
-      if (!uni_window_simple(sm.text, m.shift + (uint32_t)m.L, lane, simple2, &hbm)) continue;   // k_tokenize_uchunk
+      if (!uni_window_simple(sm.text, m.shift + (uint32_t)m.L, lane, simple2)) continue;   // k_tokenize_uchunk
       if (lane == 0) p.uchunk_list[u] = 0u;
     } else if (nonascii) {
       if (lane == 0) {
@@ -1919,7 +1895,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     {
       uint32_t at = tincl - nts;
       uint32_t s0 = (uint32_t)S, s1 = (uint32_t)(S >> 32), e0 = (uint32_t)E, e1 = (uint32_t)(E >> 32);
-      const uint64_t hbn = UNI ? shfl_down64(hbm) : 0ull;
       while (s0 | s1) {
         const uint32_t tp = lane * 64 + (s0 ? (uint32_t)__builtin_ctz(s0) : 32 + (uint32_t)__builtin_ctz(s1));
         const uint32_t te = (e0 | e1) ? lane * 64 + (e0 ? (uint32_t)__builtin_ctz(e0) : 32 + (uint32_t)__builtin_ctz(e1))
@@ -1927,9 +1902,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
         if (s0) s0 &= s0 - 1; else s1 &= s1 - 1;
         if (e0) e0 &= e0 - 1; else e1 &= e1 - 1;
         if (tp >= A && tp < B) {
-          const uint32_t fl = UNI ? uni_span_flag(tp, te, lane * 64, hbm, hbn) : 0u;
-          longtok |= te - tp > 8 || (UNI && fl && te - tp == 8);
-          sm.list[at++] = span_entry(tp, te, 0) | fl;
+          longtok |= te - tp > (UNI ? 7u : 8u);
+          sm.list[at++] = span_entry(tp, te, 0);
         }
       }
     }
