@@ -1,10 +1,10 @@
 #!/bin/bash
-# Per-phase SQ counters (tools/prof_phases.sh) for the in-tree library and each tools/variants/*.so
+# Per-phase SQ counters (tools/prof_phases.sh) for the in-tree library and each tools/archive/variants/*.so
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out
 L=tf-idf-distributed-system_amd/lib/libtfidf.so
 cp $L /tmp/libtfidf_base.so
-for v in base ${VARIANTS:-tools/variants/*.so}; do
+for v in base ${VARIANTS:-tools/archive/variants/*.so}; do
   n=$(basename $v .so)
   if [ "$v" = base ]; then cp /tmp/libtfidf_base.so $L; else cp $v $L; fi
   rm -rf gpurun_out/prof_phases

@@ -7,4 +7,4 @@ rc=$?; tail -3 gpurun_out/wg_p1.log; [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -u -m pytest -x -q -m gpu --timeout 200 --timeout-method thread tests/test_gpu_unicode.py tests/test_gpu_books.py > gpurun_out/uchunk.log 2>&1
 rc=$?; tail -3 gpurun_out/uchunk.log; [ $rc -ne 0 ] && { grep -nE "FAIL|Error|assert" gpurun_out/uchunk.log | head -20; exit $rc; }
 TESTS="tests/test_gpu_parity.py tests/test_gpu_identity.py tests/test_gpu_unicode.py tests/test_gpu_pack.py tests/test_gpu_books.py" ROUNDS=1 bash tools/gpu_wg_ab.sh || exit $?
-NOBENCH=1 bash tools/gpu_node.sh
+NOBENCH=1 bash tools/archive/gpu_node.sh

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Tokenizer A/B: in-tree build vs tools/variants/*.so, cfg 2 and cfg-5 shape
+# Tokenizer A/B: in-tree build vs tools/archive/variants/*.so, cfg 2 and cfg-5 shape
 # builds alternated (ROUNDS), after the wave-path parity tests (TESTS).
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out
@@ -10,7 +10,7 @@ fi
 L=tf-idf-distributed-system_amd/lib/libtfidf.so
 cp $L /tmp/libtfidf_base.so
 for rnd in $(seq 1 ${ROUNDS:-2}); do
-for v in base tools/variants/*.so; do
+for v in base tools/archive/variants/*.so; do
   if [ "$v" = base ]; then cp /tmp/libtfidf_base.so $L; else cp $v $L; fi
   for shape in ${BASESHAPE-cfg2} ${SHAPES:-cfg5}; do
     A="--steps 5 --warmup 2"

@@ -1,17 +1,17 @@
 #!/bin/bash
 # Variant A/B with parity per variant: for the in-tree build and each
-# tools/variants/*.so, run TESTS (bounded) then the bench SHAPES, ROUNDS times.
+# tools/archive/variants/*.so, run TESTS (bounded) then the bench SHAPES, ROUNDS times.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out
 L=tf-idf-distributed-system_amd/lib/libtfidf.so
 cp $L /tmp/libtfidf_base.so
-for v in base tools/variants/*.so; do
+for v in base tools/archive/variants/*.so; do
   if [ "$v" = base ]; then cp /tmp/libtfidf_base.so $L; else cp $v $L; fi
   timeout -k 10 300 python -u -m pytest -x -q -m gpu --timeout 200 --timeout-method thread $TESTS > gpurun_out/var_tests.log 2>&1
   rc=$?; echo "$v tests: $(tail -1 gpurun_out/var_tests.log)"; [ $rc -ne 0 ] && { grep -nE "FAIL|Error|assert" gpurun_out/var_tests.log | head -20; cp /tmp/libtfidf_base.so $L; exit $rc; }
 done
 for rnd in $(seq 1 ${ROUNDS:-2}); do
-for v in base tools/variants/*.so; do
+for v in base tools/archive/variants/*.so; do
   if [ "$v" = base ]; then cp /tmp/libtfidf_base.so $L; else cp $v $L; fi
   for shape in ${SHAPES:-cfg2}; do
     A="--steps 5 --warmup 2"

@@ -8,7 +8,7 @@ timeout -k 10 400 python -u -m pytest -x -q -m gpu --timeout 200 --timeout-metho
 rc=$?; tail -1 gpurun_out/w10_tests.log; [ $rc -ne 0 ] && { grep -nE "FAIL|Error|assert" gpurun_out/w10_tests.log | head -20; exit $rc; }
 cp $L /tmp/base.so
 for rnd in 1 2; do
-for cfg in "base 10" "base 8" "tools/variants/w2.so 8" "tools/variants/head.so 8"; do
+for cfg in "base 10" "base 8" "tools/archive/variants/w2.so 8" "tools/archive/variants/head.so 8"; do
   set -- $cfg
   if [ $1 = base ]; then cp /tmp/base.so $L; else cp $1 $L; fi
   for shape in cfg2 cfg5; do

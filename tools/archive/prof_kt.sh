@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprofv3 kernel-trace summary of one bench command (GPU box).
-# Usage: TAG=name ARGS="--steps 1 ..." bash tools/prof_kt.sh
+# Usage: TAG=name ARGS="--steps 1 ..." bash tools/archive/prof_kt.sh
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/kt_${TAG:-q}

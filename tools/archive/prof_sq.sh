@@ -1,6 +1,6 @@
 #!/bin/bash
 # SQ counters per dispatch of the tokenizer kernels for one small build (GPU box).
-# Usage: LIB=path TOK=lf|wave bash tools/prof_sq.sh
+# Usage: LIB=path TOK=lf|wave bash tools/archive/prof_sq.sh
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/sq_${TAG:-x}

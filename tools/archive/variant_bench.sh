@@ -1,11 +1,11 @@
 #!/bin/bash
-# Bench library variants (tools/variants/*.so) against the in-tree build:
+# Bench library variants (tools/archive/variants/*.so) against the in-tree build:
 # each variant is swapped in for lib/libtfidf.so for one short bench run.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out
 L=tf-idf-distributed-system_amd/lib/libtfidf.so
 cp $L /tmp/libtfidf_base.so
-for v in base tools/variants/*.so; do
+for v in base tools/archive/variants/*.so; do
   if [ "$v" = base ]; then cp /tmp/libtfidf_base.so $L; else cp $v $L; fi
   timeout -k 10 200 python -u bench.py --steps 3 --warmup 1 ${VAR_QUERIES:---no-queries} --no-e2e --cpu-sample 0 > gpurun_out/var.log 2>&1 || { echo "$v failed"; tail -3 gpurun_out/var.log; cp /tmp/libtfidf_base.so $L; exit 1; }
   python3 -c "import json; r=json.loads(open('gpurun_out/var.log').read().strip().splitlines()[-1]); print('%-40s' % '$v', {k: round(v, 3) for k, v in r['phases_ms'].items()}, r.get('queries'))"
