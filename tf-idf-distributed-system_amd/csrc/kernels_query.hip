@@ -969,8 +969,14 @@ constexpr uint32_t kUnitWaves = kUnitThreads / 64;
 constexpr uint32_t kUnitScanWords = kBlockDocs / 32 / kUnitWaves;
 constexpr uint32_t kUnitLanesPerWord = 64 / kUnitScanWords;
 static_assert(kUnitScanWords * kUnitWaves == kBlockDocs / 32 && kUnitLanesPerWord * kUnitScanWords == 64, "scan layout");
-constexpr uint32_t kUnitU = 4;                 // postings per thread in flight
-constexpr uint32_t kUnitPre = 4;               // query terms whose first chunk is prefetched per block
+#ifndef TFIDF_UNIT_U
+#define TFIDF_UNIT_U 4
+#endif
+#ifndef TFIDF_UNIT_PRE
+#define TFIDF_UNIT_PRE 4
+#endif
+constexpr uint32_t kUnitU = TFIDF_UNIT_U;      // postings per thread in flight
+constexpr uint32_t kUnitPre = TFIDF_UNIT_PRE;  // query terms whose first chunk is prefetched per block
 
 struct UnitSmem {
   double acc[kBlockDocs];                      // valid where bits is set
