@@ -9,7 +9,7 @@
 # rehearsal of the node path.  Output: gpurun_out/ev_$TAG/.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R
-TAG=${TAG:-r04}; O=$R/gpurun_out/ev_$TAG; mkdir -p $O
+TAG=${TAG:-r05}; O=$R/gpurun_out/ev_$TAG; mkdir -p $O
 TAG=$TAG SQ=1 bash tools/prof_round.sh > $O/prof_round.log 2>&1 || { echo "prof_round failed"; tail -5 $O/prof_round.log; exit 1; }
 tail -3 $O/prof_round.log
 TJ=$R/gpurun_out/prof_$TAG/traffic.json
