@@ -2662,8 +2662,16 @@ __device__ uint32_t csr_tf_of(const PostingParams &p, uint64_t d, uint32_t r, ui
 // workgroup takes sort_spw = 4 streams in turn, so few streams per CU are open
 // at a time and the regions being written stay L2-resident (cfg-2 inversion:
 // one stream per 1024-thread workgroup 3.11 ms, 8 per 1024 2.87, 4 per 512 2.52)
+#ifndef TFIDF_SORT_STAGE
+#define TFIDF_SORT_STAGE 8192
+#endif
+// Round 5: a stream of at most kSortStage entries is assembled in LDS and
+// written out contiguous (its region is [lo, hi) of the block's postings);
+// scattered 4-byte global stores only for larger streams.
+constexpr uint32_t kSortStage = TFIDF_SORT_STAGE;
 __global__ void __launch_bounds__(1024) k_scatter_sort(PostingParams p) {
   __shared__ uint32_t cur[kSubSlots + 1];                   // + no-op cursor for idle lanes
+  __shared__ uint32_t ostage[kSortStage > 0 ? kSortStage : 1];
   __shared__ uint8_t bnorm[kBlockDocs];                     // the block's norm bytes: an LDS read per entry
                                                             // instead of a global load that waits on the temp word
   const uint32_t b = blockIdx.x, r = blockIdx.y;
@@ -2689,6 +2697,7 @@ __global__ void __launch_bounds__(1024) k_scatter_sort(PostingParams p) {
     for (uint32_t i = threadIdx.x; i < BS; i += blockDim.x) cur[i] = row[s0 + i];
     const uint32_t lo = row[s0];
     const uint32_t hi = s0 + BS < p.C ? row[s0 + BS] : (uint32_t)(p.bbase[b + 1] - bb);
+    const bool staged = kSortStage > 0 && hi - lo <= kSortStage;   // workgroup-uniform
     __syncthreads();
     constexpr int U = 8;              // entries per thread in flight (8: a ~5 k-entry stream in one round; 4 was 3.4% slower)
     for (uint32_t e0 = lo; e0 < hi; e0 += U * blockDim.x) {   // uniform trip count: all lanes ballot
@@ -2714,7 +2723,9 @@ __global__ void __launch_bounds__(1024) k_scatter_sort(PostingParams p) {
         uint32_t tf = x[u] >> kTmpTfShift;
         if (in && tf == kTmpTfEsc) tf = csr_tf_of(p, doc, r, (uint32_t)s0 + sl);      // rare: tf >= 1023
         if (in) {
-          p.post[bb + pos] = post_word(x[u] & (kBlockDocs - 1), tf, nrm[u]);
+          const uint32_t w = post_word(x[u] & (kBlockDocs - 1), tf, nrm[u]);
+          if (staged) ostage[pos - lo] = w;
+          else p.post[bb + pos] = w;
           if (tf >= kPostTfEsc) {                                                 // rare: tf >= 2047
             const uint32_t at = atomicAdd(p.post_esc_count, 1u);
             if (at < p.post_esc_cap) p.post_esc[at] = ((bb + pos) << 24) | tf;
@@ -2722,7 +2733,10 @@ __global__ void __launch_bounds__(1024) k_scatter_sort(PostingParams p) {
         }
       }
     }
-    __syncthreads();                                      // cursors reused by the next stream
+    __syncthreads();                                      // the stream's words are in ostage
+    if (staged)
+      for (uint32_t i = threadIdx.x; i < hi - lo; i += blockDim.x) p.post[bb + lo + i] = ostage[i];
+    __syncthreads();                                      // cursors and ostage reused by the next stream
   }
 }
 
