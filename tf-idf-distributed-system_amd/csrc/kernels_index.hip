@@ -2603,6 +2603,96 @@ __device__ __forceinline__ void part_group_staged(const PostingParams &p, uint32
   }
 }
 
+#ifndef TFIDF_PART_WG
+#define TFIDF_PART_WG 1
+#endif
+#if TFIDF_PART_WG
+// Round 5: workgroup-wide staging.  All the workgroup's waves take their next
+// document group together (a round: nw * kInvDocs documents, up to 8 192
+// entries); the round's entries are counting-sorted by sub-range stream in LDS
+// and stored stream run by stream run, ~16x longer runs than the wave-local
+// staging (one to two lines per store instruction instead of ~13).
+__global__ void __launch_bounds__(1024) k_scatter_part(PostingParams p) {
+  __shared__ uint32_t bcur[kRangeSlots / kSubSlots + 1];
+  __shared__ uint32_t cnt[kPartStreams], soff[kPartStreams], gb[kPartStreams], tot_sh;
+  __shared__ uint32_t stage[16 * kInvDocs * 64];
+  __shared__ uint8_t sid[16 * kInvDocs * 64];
+  const uint32_t lane = threadIdx.x & 63, nw = blockDim.x >> 6;
+  const uint32_t wid = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  uint32_t b, r;
+  if (!tile_of(blockIdx.x, p.n_blocks, p.n_ranges, &b, &r)) return;
+  const uint32_t RS = 1u << p.range_shift, rmask = RS - 1;
+  const uint32_t nsub = RS > kSubSlots ? RS / kSubSlots : 1u;
+  const uint32_t *row = p.blk + (size_t)b * p.C + ((size_t)r << p.range_shift);
+  if (threadIdx.x < nsub) bcur[threadIdx.x] = row[threadIdx.x * kSubSlots];
+  if (threadIdx.x < kPartStreams) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t bb = p.bbase[b];
+  const uint64_t d0 = (uint64_t)b * kBlockDocs;
+  const uint64_t d1 = d0 + kBlockDocs < p.n_docs ? d0 + kBlockDocs : p.n_docs;
+  const uint64_t step = (uint64_t)nw * kInvDocs;
+  const uint32_t rounds = (uint32_t)((d1 - d0 + step - 1) / step);   // workgroup-uniform
+  uint64_t dd = d0 + wid;
+  InvGroup g = inv_group(p, dd, d1, nw, r, false);
+  uint32_t c[kInvDocs];
+  if (dd < d1) inv_load(p, g, lane, c);
+  else
+#pragma unroll
+    for (int j = 0; j < kInvDocs; j++) c[j] = 0;
+  for (uint32_t k = 0; k < rounds; k++) {
+    const uint64_t dn = dd + step;
+    const InvGroup gn = inv_group(p, dn, d1, nw, r, false);
+    uint32_t cn[kInvDocs];
+#pragma unroll
+    for (int j = 0; j < kInvDocs; j++) cn[j] = 0;
+    if (dn < d1) inv_load(p, gn, lane, cn);                       // next group in flight
+    uint32_t val[kInvDocs], rank[kInvDocs], sj[kInvDocs];
+#pragma unroll
+    for (int j = 0; j < kInvDocs; j++) {
+      const uint32_t sl = c[j] & rmask;
+      sj[j] = sl >> kSubBits;
+      const uint32_t dl = (uint32_t)(dd + (uint64_t)nw * j - d0);
+      const uint32_t tf = csr_tf_field(c[j], p.range_shift);
+      val[j] = dl | ((sl & (kSubSlots - 1)) << 13) | (min(tf, kTmpTfEsc) << kTmpTfShift);
+      rank[j] = c[j] != 0 ? atomicAdd(&cnt[sj[j]], 1u) : 0u;
+    }
+    __syncthreads();                                              // the round's counts are complete
+    if (wid == 0) {
+      const uint32_t n = cnt[lane];
+      const uint32_t incl = wave_incl_add(n);
+      soff[lane] = incl - n;
+      gb[lane] = n ? atomicAdd(&bcur[lane], n) : 0u;
+      cnt[lane] = 0;
+      if (lane == 63) tot_sh = incl;
+    }
+    __syncthreads();                                              // offsets known
+#pragma unroll
+    for (int j = 0; j < kInvDocs; j++)
+      if (c[j] != 0) {
+        const uint32_t at = soff[sj[j]] + rank[j];
+        stage[at] = val[j];
+        sid[at] = (uint8_t)sj[j];
+      }
+    __syncthreads();                                              // the round's entries are staged
+    const uint32_t T = tot_sh;
+    for (uint32_t ti = threadIdx.x; ti < T; ti += blockDim.x) {
+      const uint32_t st = sid[ti];
+      p.post_tmp[bb + gb[st] + (ti - soff[st])] = stage[ti];
+    }
+    for (uint32_t off = lane + 64; off < g.maxn; off += 64) {    // segments longer than 64
+      inv_load(p, g, off, c);
+      part_entries(p, bcur, rmask, bb, g, dd, (uint32_t)d0, nw, c);
+    }
+    g = gn;
+#pragma unroll
+    for (int j = 0; j < kInvDocs; j++) c[j] = cn[j];
+    dd = dn;
+    // the next round's counts go to cnt (reset above); its stage / soff / gb
+    // writes come after its first barrier, when every thread has left this
+    // round's store loop
+  }
+}
+#else
 __global__ void __launch_bounds__(1024) k_scatter_part(PostingParams p) {
   __shared__ uint32_t bcur[kRangeSlots / kSubSlots + 1];
   __shared__ PartWave pwave[16];
@@ -2640,6 +2730,7 @@ __global__ void __launch_bounds__(1024) k_scatter_part(PostingParams p) {
     dd = dn;
   }
 }
+#endif
 
 // tf of (doc, slot) from the document's CSR row segment of range r (the
 // escape path of the 10-bit temp tf field)
