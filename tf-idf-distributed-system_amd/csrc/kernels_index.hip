@@ -2977,8 +2977,9 @@ hipError_t launch_block_base(const PostingParams &p, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t launch_scatter(const PostingParams &p, hipStream_t s) {
-  static const uint32_t pthreads = [] {
-    const char *e = getenv("TFIDF_PART_THREADS");                 // A/B only
+  // launch-shape knobs, read per build (A/B and tests/test_gpu_inversion_shapes.py)
+  const uint32_t pthreads = [] {
+    const char *e = getenv("TFIDF_PART_THREADS");
     const int t = e ? atoi(e) : 1024;
     return (uint32_t)(t == 256 || t == 512 ? t : 1024);
   }();
@@ -2987,8 +2988,8 @@ hipError_t launch_scatter(const PostingParams &p, hipStream_t s) {
   if (e != hipSuccess) return e;
   const uint32_t RS = 1u << p.range_shift;
   const uint32_t nsub = RS > kSubSlots ? RS / kSubSlots : 1u;
-  static const uint32_t threads = [] {
-    const char *e = getenv("TFIDF_SORT_THREADS");                 // A/B only
+  const uint32_t threads = [] {
+    const char *e = getenv("TFIDF_SORT_THREADS");
     const int t = e ? atoi(e) : 512;                             // 512: 2.89 -> 2.52 ms (cfg 2)
     return (uint32_t)(t == 256 || t == 512 ? t : 1024);
   }();
