@@ -19,6 +19,10 @@ for p in (REPO, PKG_DIR):
 
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
+# The library reads its TFIDF_* test knobs (forced paths, small batches, weak
+# hashes) only while TFIDF_DEBUG is set; the tests set knobs per case.
+os.environ.setdefault("TFIDF_DEBUG", "1")
+
 # One HIP runtime per process: PyTorch bundles its own libamdhip64 /
 # libhsa-runtime64 (same soname as /opt/rocm's).  Loaded first, it is the one
 # libtfidf binds to; loaded after libtfidf it is a second runtime that finds no

@@ -174,3 +174,102 @@ def test_reader_keeps_its_snapshot_across_commits():
     idx.commit()
     assert len(idx.search(b"qqqq", 0)) == 1
     idx.close()
+
+
+LONG = b"supercalifragilisticexpialidocious"      # > 16 bytes: a hashed key, checked against its corpus spelling
+
+
+def test_reader_keeps_its_snapshot_across_clear():
+    """tfidf_clear restarts the staged corpus at offset 0: a reader pinned
+    before it must keep reading its own corpus bytes (the spelling of hashed
+    terms comes from the snapshot's text), not the new documents'."""
+    idx = ShardIndex(device=0)
+    texts = [b"%s alpha beta %d" % (LONG, i) for i in range(50)] + [b"gamma delta"] * 10
+    idx.add_documents(texts, [b"a%03d" % i for i in range(60)])
+    idx.commit()
+    rd = idx.reader()
+    before_long = rd.search(LONG, 0)
+    before_alpha = rd.search(b"alpha", 5)
+    assert len(before_long) == 50
+    idx.clear()
+    # different bytes over the same offsets (same lengths, other letters)
+    idx.add_documents([b"x" * len(t) for t in texts], [b"b%03d" % i for i in range(60)])
+    idx.commit()
+    assert idx.search(LONG, 0) == []
+    assert rd.search(LONG, 0) == before_long
+    assert rd.search(b"alpha", 5) == before_alpha
+    assert rd.doc_key(0) == b"a000"
+    rd.close()
+    idx.close()
+
+
+def test_failed_searches_drain_before_their_snapshot_is_rebuilt(monkeypatch):
+    """Every third scoring call fails after its kernels are queued
+    (TFIDF_TEST_FAIL_SCORING, a test knob) while a writer re-commits states of
+    different sizes, so the commit rebuilds (and regrows) the snapshots the
+    failed searches held: no fault, and every search that succeeds equals the
+    oracle of one committed state."""
+    monkeypatch.setenv("TFIDF_TEST_FAIL_SCORING", "3")
+    keys, base, _ = states()
+    big = synth.corpus(R, V=5000, len_min=400, len_max=600, seed=778)
+    state_b = big + base[R:]
+    want = [oracle_maps(keys, base), oracle_maps(keys, state_b)]
+    idx = ShardIndex(device=0)
+    idx.add_documents(base, keys)
+    idx.commit()
+    stop = threading.Event()
+    errors, fails, oks = [], [0], [0]
+
+    def writer():
+        try:
+            for i in range(12):
+                idx.add_documents(big if i % 2 == 0 else base[:R], keys[:R])
+                idx.commit()
+        except Exception as e:          # noqa: BLE001
+            errors.append(("writer", repr(e)))
+        finally:
+            stop.set()
+
+    def searcher(t):
+        i = 0
+        while not stop.is_set() or i < 3:
+            qi = (t + i) % len(QUERIES)
+            i += 1
+            try:
+                if t % 2:
+                    hits = idx.search(QUERIES[qi], 0)              # all hits: through run_scoring
+                    got = sorted((np.float32(s) for _, s in hits), reverse=True)
+                    if not any(got == sorted(want[s][qi].values(), reverse=True) for s in (0, 1)):
+                        errors.append(("all hits", t, qi))
+                        return
+                else:
+                    d, sc, cnt = idx.search_batch(QUERIES, K)
+                    ok = [set(s for s in (0, 1)
+                              if [np.float32(x) for x in sc[q, :cnt[q]].tolist()] == topk_scores(want[s][q], K))
+                          for q in range(len(QUERIES))]
+                    if not set.intersection(*ok):
+                        errors.append(("batch", t))
+                        return
+                oks[0] += 1
+            except Exception as e:      # noqa: BLE001
+                if "injected scoring failure" not in str(e):
+                    errors.append(("search", t, repr(e)))
+                    return
+                fails[0] += 1
+
+    th = [threading.Thread(target=searcher, args=(i,), daemon=True) for i in range(8)]
+    w = threading.Thread(target=writer, daemon=True)
+    for x in th:
+        x.start()
+    w.start()
+    w.join(120)
+    for x in th:
+        x.join(120)
+    assert not w.is_alive() and not any(x.is_alive() for x in th), "a thread did not finish"
+    assert not errors, errors[:5]
+    assert fails[0] > 0 and oks[0] > 0, (fails, oks)
+    monkeypatch.delenv("TFIDF_TEST_FAIL_SCORING")
+    idx.commit()
+    with idx.reader() as rd:
+        assert {rd.doc_key(d): np.float32(s) for d, s in rd.search(QUERIES[0], 0)} == want[0][0]
+    idx.close()

@@ -2983,7 +2983,7 @@ hipError_t launch_block_base(const PostingParams &p, hipStream_t s) {
 hipError_t launch_scatter(const PostingParams &p, hipStream_t s) {
   // launch-shape knobs, read per build (A/B and tests/test_gpu_inversion_shapes.py)
   const uint32_t pthreads = [] {
-    const char *e = getenv("TFIDF_PART_THREADS");
+    const char *e = knob("TFIDF_PART_THREADS");
     const int t = e ? atoi(e) : 1024;
     return (uint32_t)(t == 256 || t == 512 ? t : 1024);
   }();
@@ -2993,7 +2993,7 @@ hipError_t launch_scatter(const PostingParams &p, hipStream_t s) {
   const uint32_t RS = 1u << p.range_shift;
   const uint32_t nsub = RS > kSubSlots ? RS / kSubSlots : 1u;
   const uint32_t threads = [] {
-    const char *e = getenv("TFIDF_SORT_THREADS");
+    const char *e = knob("TFIDF_SORT_THREADS");
     const int t = e ? atoi(e) : 512;                             // 512: 2.89 -> 2.52 ms (cfg 2)
     return (uint32_t)(t == 256 || t == 512 ? t : 1024);
   }();

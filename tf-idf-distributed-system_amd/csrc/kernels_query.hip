@@ -1610,8 +1610,8 @@ hipError_t launch_hits_order(const uint64_t *hits, const uint32_t *hits_n, uint3
   // global memory (slow: k_merge_group 22 us on average with the bench's heavy
   // queries included).  TFIDF_HITS_PAIRWISE / TFIDF_HITS_GROUPS force a path (tests).
   bool groups = hits_bound * kGroupRuns <= (uint64_t)R * kHitsGroupAvg;
-  if (getenv("TFIDF_HITS_PAIRWISE")) groups = false;
-  if (getenv("TFIDF_HITS_GROUPS")) groups = true;
+  if (knob("TFIDF_HITS_PAIRWISE")) groups = false;
+  if (knob("TFIDF_HITS_GROUPS")) groups = true;
   if (groups) {                                                 // levels 0-2: one workgroup per 8 runs
     static std::atomic<uint64_t> big{0};
     allow_dyn_lds((const void *)k_merge_group, 2 * kGroupCap * 8, big);
@@ -1702,7 +1702,7 @@ __global__ void __launch_bounds__(64 * kMergeWavesPerWG) k_merge_topk_wave(Query
 }
 
 hipError_t launch_merge_topk(const QueryParams &p, hipStream_t s) {
-  if (p.k <= 64 && (uint64_t)p.n_blocks * p.k <= 64u * kMergeWaveRegs && !getenv("TFIDF_MERGE_WG"))
+  if (p.k <= 64 && (uint64_t)p.n_blocks * p.k <= 64u * kMergeWaveRegs && !knob("TFIDF_MERGE_WG"))
     hipLaunchKernelGGL(k_merge_topk_wave, dim3((p.n_q + kMergeWavesPerWG - 1) / kMergeWavesPerWG),
                        dim3(64 * kMergeWavesPerWG), 0, s, p);
   else

@@ -520,7 +520,7 @@ uint64_t term_invert_scratch_words(uint64_t n_docs, uint64_t nnz, uint32_t C) {
 // Book-sized rows (SURVEY cfg 1) keep the row kernels (k_term_pairs_wide: many
 // workgroups per row) and the first k_rs_hist pass; TFIDF_TERM_PAIRS_ROWS forces them (A/B)
 static bool term_rows_path(const TermParams &p) {
-  return getenv("TFIDF_TERM_PAIRS_ROWS") != nullptr || (p.n_docs && p.nnz / p.n_docs > 2048);
+  return knob("TFIDF_TERM_PAIRS_ROWS") != nullptr || (p.n_docs && p.nnz / p.n_docs > 2048);
 }
 
 hipError_t launch_term_pairs(const TermParams &p, hipStream_t s) {

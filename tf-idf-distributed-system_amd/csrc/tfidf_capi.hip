@@ -430,8 +430,20 @@ struct CtxLease {
     }
     c->q_timing = ix->q_timing.load();
   }
+  // A search returns its snapshot reference after its lease (declared later,
+  // destroyed first): no kernel of a failed search may still read the
+  // snapshot's buffers when a commit rebuilds that snapshot as its spare
+  // (use_count() == 1).  Successful searches have synchronised already; an
+  // error return (HIP_TRY, a failed preparation after earlier chunks were
+  // queued) is drained here.
   ~CtxLease() {
     if (!c || rc) return;
+    {
+      DeviceGuard g(ix->cfg.device);
+      const hipStream_t st = stream();
+      if (hipStreamQuery(st) != hipSuccess) hipStreamSynchronize(st);
+      if (c->side && hipStreamQuery(c->side) != hipSuccess) hipStreamSynchronize(c->side);
+    }
     std::lock_guard<std::mutex> lk(ix->ctx_mu);
     ix->ctx_free.push_back(std::move(c));
   }
@@ -477,7 +489,7 @@ extern "C" int tfidf_create(const tfidf_config *cfg, tfidf_index **out) {
     return fail(TFIDF_E_HIP, "hipStreamCreate failed");
   }
   ix->stream = ix->own_stream;
-  if (const char *cm = getenv("TFIDF_COALESCE_MAX")) ix->cq_max = std::max(1, atoi(cm));   // tests: small batches
+  if (const char *cm = knob("TFIDF_COALESCE_MAX")) ix->cq_max = std::max(1, atoi(cm));   // tests: small batches
   if (hipStreamCreateWithFlags(&ix->copy_stream, hipStreamNonBlocking) != hipSuccess) {
     hipStreamDestroy(ix->own_stream);
     delete ix;
@@ -618,6 +630,16 @@ extern "C" int tfidf_clear(tfidf_index *ix) {
   std::lock_guard<std::mutex> lk(ix->mu);
   DeviceGuard g(ix->cfg.device);
   HIP_TRY(hipStreamSynchronize(ix->stream));
+  // The staged corpus restarts at offset 0: buffers a published snapshot (an
+  // open reader, an in-flight search) still reads are replaced, not rewritten.
+  if (ix->text.use_count() > 1) ix->text = std::make_shared<DevMem>(ix->cfg.device);
+  if (ix->offsets.use_count() > 1) {
+    auto no = std::make_shared<DevMem>(ix->cfg.device);
+    HIP_TRY(no->reserve(64));
+    HIP_TRY(hipMemsetAsync(no->p, 0, 8, ix->stream));
+    HIP_TRY(hipStreamSynchronize(ix->stream));
+    ix->offsets = std::move(no);
+  }
   ix->text_bytes = 0;
   ix->n_staged = 0;
   ix->h_offsets.assign(1, 0);
@@ -970,7 +992,7 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
   {
     const uint64_t avg = ix->n_staged ? ix->text_bytes / ix->n_staged : 0;
     if (avg) pack = (uint32_t)std::min<uint64_t>(kPackMaxDocs, std::max<uint64_t>(1, kPackBytes / avg));
-    if (const char *e = getenv("TFIDF_PACK_DOCS")) pack = (uint32_t)std::max(1, std::min(atoi(e), (int)kPackMaxDocs));
+    if (const char *e = knob("TFIDF_PACK_DOCS")) pack = (uint32_t)std::max(1, std::min(atoi(e), (int)kPackMaxDocs));
     pack = std::min(pack, std::max(1u, kWaveGroups / S.R));   // (document, range) groups per unit
   }
   if (pack > 1) HIP_TRY(ix->retry_list.reserve(N * 4 + 4));
@@ -1022,8 +1044,8 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
   bp.bad_count = reinterpret_cast<uint32_t *>(ctr + 8);
   bp.stats = reinterpret_cast<unsigned long long *>(ctr);
   bp.err = reinterpret_cast<uint32_t *>(ctr + 3);
-  if (const char *ds = getenv("TFIDF_DEBUG_STOP")) bp.debug_stop = (uint32_t)atoi(ds);   // profiling only
-  if (const char *uf = getenv("TFIDF_UW_FULL")) bp.debug_uw_full = (uint32_t)atoi(uf);   // A/B only
+  if (const char *ds = knob("TFIDF_DEBUG_STOP")) bp.debug_stop = (uint32_t)atoi(ds);   // profiling only
+  if (const char *uf = knob("TFIDF_UW_FULL")) bp.debug_uw_full = (uint32_t)atoi(uf);   // A/B only
   bp.pack = pack;
   bp.retry_list = pack > 1 ? ix->retry_list.as<uint32_t>() : nullptr;
   bp.retry_count = reinterpret_cast<uint32_t *>(ctr + 5);
@@ -1034,7 +1056,7 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
   if (N) {
     const uint64_t units = (N + pack - 1) / pack;
     uint64_t wpc = kWaveWGsPerCU;
-    if (const char *e = getenv("TFIDF_WAVE_WGS_PER_CU")) wpc = (uint64_t)std::max(1, atoi(e));   // profiling only
+    if (const char *e = knob("TFIDF_WAVE_WGS_PER_CU")) wpc = (uint64_t)std::max(1, atoi(e));   // profiling only
     const uint64_t grid = std::min<uint64_t>(units, (uint64_t)ix->num_cus * wpc);
     HIP_TRY(launch_tokenize_wave(bp, (int)grid, s));
     if (pack > 1 && !bp.debug_stop) {       // documents the packs could not take: one per wave
@@ -1055,7 +1077,7 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
     // when none): the wave rules with non-ASCII letters where the document's
     // characters allow (k_tokenize_wave<UNI>), then the Unicode wave path for
     // the rest.  TFIDF_NO_UNIWAVE: the Unicode wave path for all (A/B).
-    const char *nouw = getenv("TFIDF_NO_UNIWAVE");
+    const char *nouw = knob("TFIDF_NO_UNIWAVE");
     if (bp.debug_stop < 10 && !(nouw && *nouw && *nouw != '0'))
       HIP_TRY(launch_tokenize_wave_uni(bp, (int)std::min<uint64_t>((N + 63) / 64, (uint64_t)ix->num_cus * kWaveWGsPerCU), s));
     if (!bp.debug_stop || bp.debug_stop >= 10)          // (stops 10..13: the Unicode wave path's phases)
@@ -1098,7 +1120,7 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
     const uint32_t bsh = std::max<uint32_t>(wlog, ix->cap_log2 > 6 ? ix->cap_log2 - 6 : 0);
     const uint32_t nb = 1u << (ix->cap_log2 - bsh);
     uint64_t unit_max = std::max<uint64_t>(1, kPairBudget / ((uint64_t)kPairWords * 4));
-    if (const char *e = getenv("TFIDF_TEST_PAIR_UNITS")) unit_max = std::max(1, atoi(e));   // tests: many groups
+    if (const char *e = knob("TFIDF_TEST_PAIR_UNITS")) unit_max = std::max(1, atoi(e));   // tests: many groups
     // per group: the first unit (document, core) of each document, prefix form
     std::vector<uint32_t> pre;
     std::vector<uint64_t> gpre, gdoc;               // each group's prefix array offset and first document
@@ -1146,7 +1168,7 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
       cp.pair_nb = nb;
       // units with non-ASCII text: the Unicode chunk kernel (TFIDF_NO_UCHUNK: their
       // documents go to k_tokenize_long whole, as before round 4; A/B only)
-      const bool uch = !getenv("TFIDF_NO_UCHUNK");
+      const bool uch = !knob("TFIDF_NO_UCHUNK");
       cp.uchunk_count = uch ? ix->uchunk.as<uint32_t>() : nullptr;
       cp.uchunk_list = uch ? ix->uchunk.as<uint32_t>() + 4 : nullptr;
       if (uch) HIP_TRY(hipMemsetAsync(ix->uchunk.p, 0, (size_t)(cp.n_chunks + 4) * 4, s));
@@ -1154,7 +1176,7 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
       HIP_TRY(launch_tokenize_chunks(cp, (int)grid, s));
       // flagged units by the wave rules where their text allows (TFIDF_NO_UNIWAVE: all
       // of them to the Unicode chunk kernel; A/B only), then the rest
-      const char *nouw = getenv("TFIDF_NO_UNIWAVE");
+      const char *nouw = knob("TFIDF_NO_UNIWAVE");
       if (uch && !(nouw && *nouw && *nouw != '0')) HIP_TRY(launch_tokenize_chunks_uni(cp, (int)grid, s));
       if (uch)      // the count is read on the device: exits at once when no unit was listed
         HIP_TRY(launch_tokenize_uchunk(cp, (int)std::min<uint64_t>(cp.n_chunks, (uint64_t)ix->num_cus * kUchunkWGsPerCU), s));
@@ -1237,7 +1259,7 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
   // On a caller's stream (tfidf_set_stream: torch's stream under torch.distributed)
   // the small mirror stays on the main stream: the cross-stream hand-off cost the
   // one-rank RCCL rehearsal ~1 ms per step (tools/ab_dist3.sh: 12.4-12.8 vs 11.4-11.6)
-  static const bool mirror_main = getenv("TFIDF_MIRROR_MAIN") != nullptr;
+  static const bool mirror_main = knob("TFIDF_MIRROR_MAIN") != nullptr;
   const bool mirror_side = (!mirror_main && s == ix->own_stream) || (size_t)2 * C * 8 >= (32u << 20);
   // (the side-stream work is enqueued after the inversion's launches, so the
   // host's enqueue time does not delay the first inversion kernel)
@@ -1264,7 +1286,7 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
   pp.post_esc_count = reinterpret_cast<uint32_t *>(ctr + 10);
   pp.post_esc_cap = post_esc_cap;
   pp.sort_spw = 4;
-  if (const char *e = getenv("TFIDF_SORT_SPW")) pp.sort_spw = (uint32_t)std::max(1, atoi(e));   // A/B only
+  if (const char *e = knob("TFIDF_SORT_SPW")) pp.sort_spw = (uint32_t)std::max(1, atoi(e));   // A/B only
   pp.err = bp.err;
   HIP_TRY(hipEventRecord(ix->ev[EV_D0], s));
   if (S.term_major) {
@@ -1282,7 +1304,7 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
     // >= 4 (slot, doc <= 26 bits); at most 24 (tf <= kMaxTf): a small shard
     // (40 books: 56 - 18 - 6 = 32) must not reach a 32-bit shift in tf_esc
     tp.tf_bits = std::min(56u - tp.slot_bits - tp.doc_bits, 24u);
-    if (const char *e = getenv("TFIDF_TEST_TERM_TF_BITS"))      // tests: exercise the tf escape list
+    if (const char *e = knob("TFIDF_TEST_TERM_TF_BITS"))      // tests: exercise the tf escape list
       tp.tf_bits = std::max(1u, std::min(tp.tf_bits, (uint32_t)atoi(e)));
     tp.csr = bp.csr;
     tp.csr_esc = bp.csr_esc;
@@ -1434,7 +1456,7 @@ extern "C" int tfidf_commit(tfidf_index *ix) {
   // start from a seed under which equal-length hashed keys collide).  A floor
   // set by tfidf_set_hash_attempt (GLOBAL statistics: every shard must hash
   // with one seed) skips the earlier attempts.
-  const char *weak = getenv("TFIDF_TEST_WEAK_HASH");
+  const char *weak = knob("TFIDF_TEST_WEAK_HASH");
   ix->hash_seed = ix->hash_floor ? ix->hash_floor : ((weak && atoi(weak)) ? kWeakHashSeed : 0);
   ix->hash_rebuilds = ix->hash_floor;
   for (uint32_t attempt = ix->hash_floor;; attempt++) {
@@ -1485,9 +1507,15 @@ extern "C" int tfidf_stats(const tfidf_index *ix, tfidf_index_stats *out) {
   if (!ix || !out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
   const std::shared_ptr<Snapshot> S = current(ix);
   *out = tfidf_index_stats{};
-  out->text_bytes = ix->text_bytes;
-  out->hash_seed = ix->hash_seed;
-  out->hash_rebuilds = ix->hash_rebuilds;
+  uint64_t staged_bytes = 0;
+  {
+    // builder-side fields: add_docs / clear / commit replace them under mu
+    std::lock_guard<std::mutex> lk(const_cast<tfidf_index *>(ix)->mu);
+    out->text_bytes = ix->text_bytes;
+    out->hash_seed = ix->hash_seed;
+    out->hash_rebuilds = ix->hash_rebuilds;
+    staged_bytes = ix->text->bytes + ix->offsets->bytes;
+  }
   if (S) {
     out->num_docs = S->n_docs;
     out->doc_count = S->doc_count;
@@ -1513,7 +1541,7 @@ extern "C" int tfidf_stats(const tfidf_index *ix, tfidf_index_stats *out) {
   out->unit_batches = ix->unit_batches.load();
   out->fused_queries = ix->fused_queries.load();
   out->unit_count = ix->unit_count.load();
-  uint64_t tot = ix->text->bytes + ix->offsets->bytes;
+  uint64_t tot = staged_bytes;
   if (S) {
     const DevBuf *bufs[] = {&S->dict, &S->csr, &S->csr_esc, &S->doc_len, &S->doc_nuniq, &S->doc_norm,
                             &S->rsplit, &S->blk, &S->bbase, &S->post, &S->toff, &S->tdf};
@@ -1736,6 +1764,19 @@ static int prepare_batch(tfidf_index *ix, Snapshot &S, StatsView &V, const uint8
   return TFIDF_OK;
 }
 
+// Test hook (TFIDF_TEST_FAIL_SCORING = n): every n-th scoring call fails after
+// its kernels are queued, as a HIP error in a later launch would
+// (tests/test_gpu_snapshot.py: the failed search must drain before its
+// snapshot can be rebuilt by a commit).
+static int scoring_done() {
+  const char *e = knob("TFIDF_TEST_FAIL_SCORING");
+  if (!e) return TFIDF_OK;
+  static std::atomic<uint64_t> calls{0};
+  const uint64_t n = (uint64_t)std::max(1, atoi(e));
+  if (++calls % n) return TFIDF_OK;
+  return fail(TFIDF_E_HIP, "injected scoring failure (TFIDF_TEST_FAIL_SCORING)");
+}
+
 static int run_scoring(tfidf_index *ix, Snapshot &S, StatsView &V, SearchCtx &X, hipStream_t s, const QueryBatch &qb,
                        uint32_t n_q, uint32_t k) {
   const std::vector<uint32_t> &qoff = qb.off, &slots = qb.slot;
@@ -1748,7 +1789,7 @@ static int run_scoring(tfidf_index *ix, Snapshot &S, StatsView &V, SearchCtx &X,
   // (heavy units start early, the light tail balances)
   std::vector<uint32_t> &units = X.q_units;
   units.clear();
-  bool unit_path = batch && k <= kUnitMaxK && !qb.ops && !S.term_major && !getenv("TFIDF_NO_UNITS");
+  bool unit_path = batch && k <= kUnitMaxK && !qb.ops && !S.term_major && !knob("TFIDF_NO_UNITS");
   uint32_t n_wunits = 0;                 // the first n_wunits units are wave units
   if (unit_path) {
     std::vector<uint64_t> P(n_q, 0);
@@ -1764,10 +1805,10 @@ static int run_scoring(tfidf_index *ix, Snapshot &S, StatsView &V, SearchCtx &X,
     // units (k_score_units, dense block accumulator; ~T/4096 postings each)
     const uint32_t nb = S.n_blocks;
     uint64_t light_post = kWunitLightPost;
-    if (const char *e = getenv("TFIDF_WUNIT_LIGHT")) light_post = (uint64_t)atoll(e);   // A/B and test hook
+    if (const char *e = knob("TFIDF_WUNIT_LIGHT")) light_post = (uint64_t)atoll(e);   // A/B and test hook
     uint64_t unit_post = std::min<uint64_t>(std::max<uint64_t>(T / 4096, 8192), 1ull << 17);
     uint64_t wunit_post = 16384;
-    if (const char *e = getenv("TFIDF_UNIT_POST")) unit_post = wunit_post = std::max(1, atoi(e));   // test hook: force splits
+    if (const char *e = knob("TFIDF_UNIT_POST")) unit_post = wunit_post = std::max(1, atoi(e));   // test hook: force splits
     for (int pass = 0; pass < 3 && unit_path; pass++)        // light; heavy split; heavy whole
       for (uint32_t q = 0; q < n_q; q++) {
         const bool light = P[q] <= light_post * nb;
@@ -1880,7 +1921,7 @@ static int run_scoring(tfidf_index *ix, Snapshot &S, StatsView &V, SearchCtx &X,
     if (n_gunits) {
       // (one per CU next to the wave units measured slower: 6.3 -> 7.8 ms at cfg 4)
       uint32_t per_cu = kUnitWGsPerCU;
-      if (const char *e = getenv("TFIDF_UNIT_WG_PER_CU")) per_cu = (uint32_t)std::max(1, atoi(e));   // A/B
+      if (const char *e = knob("TFIDF_UNIT_WG_PER_CU")) per_cu = (uint32_t)std::max(1, atoi(e));   // A/B
       const int grid = (int)std::min<uint64_t>(n_gunits, (uint64_t)ix->num_cus * per_cu);
       HIP_TRY(launch_score_units(qp, ud + n_wunits, n_gunits, ctr + 1, grid, s));
     }
@@ -1891,7 +1932,7 @@ static int run_scoring(tfidf_index *ix, Snapshot &S, StatsView &V, SearchCtx &X,
     if (X.q_timing) HIP_TRY(hipEventRecord(X.ev[QEV_1], s));
     HIP_TRY(launch_merge_topk(qp, s));
     if (X.q_timing) HIP_TRY(hipEventRecord(X.ev[QEV_2], s));
-    return TFIDF_OK;
+    return scoring_done();
   }
   if (batch) {
     // batches: wave per (block, query) pair; pairs with many postings are
@@ -1924,7 +1965,7 @@ static int run_scoring(tfidf_index *ix, Snapshot &S, StatsView &V, SearchCtx &X,
   if (X.q_timing) HIP_TRY(hipEventRecord(X.ev[QEV_1], s));
   if (k) HIP_TRY(launch_merge_topk(qp, s));
   if (X.q_timing) HIP_TRY(hipEventRecord(X.ev[QEV_2], s));
-  return TFIDF_OK;
+  return scoring_done();
 }
 
 // One search on a snapshot (tfidf_search: the published one; tfidf_reader_search:
@@ -1944,7 +1985,7 @@ static int search_on(tfidf_index *ix, Snapshot &S, StatsView &V, const uint8_t *
   // fused path for k <= kFusedMaxK: each block workgroup writes its k
   // candidates to pinned host memory over PCIe and the host merges n_blocks x k
   // keys, a cost that grows with k (larger k: run_scoring + the device merge)
-  if (k && k <= kFusedMaxK && pq.slot.size() <= kInlTerms && !getenv("TFIDF_NO_FUSED")) {
+  if (k && k <= kFusedMaxK && pq.slot.size() <= kInlTerms && !knob("TFIDF_NO_FUSED")) {
     // one launch: query terms in the kernel arguments, block scoring with the
     // candidates written to pinned host memory, merged here
     HIP_TRY(X.q_res.resize((size_t)2 * k + 1));
@@ -2156,7 +2197,7 @@ extern "C" int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const 
   // (prepare 1.5 on the pool, device 5.65), 2 chunks 7.0 (device 6.05), 4
   // chunks 7.45 (device 6.9: every chunk pays the unit kernels' tail)
   uint32_t n_chunks = n_q >= 4096 ? 2 : 1;
-  if (const char *e = getenv("TFIDF_BATCH_CHUNKS")) n_chunks = (uint32_t)std::max(1, std::min(atoi(e), 64));
+  if (const char *e = knob("TFIDF_BATCH_CHUNKS")) n_chunks = (uint32_t)std::max(1, std::min(atoi(e), 64));
   n_chunks = std::max(1u, std::min(n_chunks, n_q));
   const size_t words = (size_t)2 * n_q * k + n_q;
   HIP_TRY(X.q_res.resize(words));
@@ -2200,7 +2241,7 @@ extern "C" int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const 
   }
   const float ms_total = any ? qev_ms(X, QEV_0, QEV_2) : 0.0f;
   set_last_ms(ix, any ? qev_ms(X, QEV_0, QEV_1) : 0.0f, ms_total);
-  if (getenv("TFIDF_HOST_TIMING")) {          // profiling only
+  if (knob("TFIDF_HOST_TIMING")) {          // profiling only
     auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     fprintf(stderr, "batch %u (%u chunks): prepare %.3f  submit %.3f  wait %.3f  copy-out %.3f  total %.3f ms (device %.3f)\n",
             n_q, n_chunks, t_prep, t_sub, ms(t2, t3), ms(t3, clk::now()), ms(t0, clk::now()), ms_total);

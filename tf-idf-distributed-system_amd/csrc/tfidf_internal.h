@@ -3,12 +3,23 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include <atomic>
 
 #include "tfidf_common.h"
 
 namespace tfidf {
+
+// Debug, test and A/B knobs (TFIDF_* environment variables other than
+// TFIDF_DEBUG): read only while TFIDF_DEBUG is set, so a stray variable in a
+// host process's environment (a JVM inherits its parent's) never changes the
+// kernel path of the library.  Without TFIDF_DEBUG every knob is unset.
+inline const char *knob(const char *name) {
+  const char *d = getenv("TFIDF_DEBUG");
+  if (!d || !*d || (d[0] == '0' && !d[1])) return nullptr;
+  return getenv(name);
+}
 
 // Error flags raised by kernels (device word err[0]; err[1] = first doc).
 constexpr uint32_t kErrCapacity = 4u;

@@ -3,6 +3,7 @@
 # SETS is a ';'-separated list of settings ("" = defaults), each run twice,
 # interleaved.  Example: SETS='; TFIDF_SORT_SPW=2; TFIDF_SORT_THREADS=1024'.
 # CMD: the measurement (default: the build bench).
+export TFIDF_DEBUG=1   # the library reads its TFIDF_* knobs only under TFIDF_DEBUG
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out
 CMD=${CMD:-"bash tools/bench_brief.sh"}

@@ -7,6 +7,7 @@
 # Unicode chunk path disabled), cfg 2 with 10 % / all documents non-ASCII,
 # the cfg-5 PMC summary, and the one-rank RCCL
 # rehearsal of the node path.  Output: gpurun_out/ev_$TAG/.
+export TFIDF_DEBUG=1   # the library reads its TFIDF_* knobs only under TFIDF_DEBUG
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R
 TAG=${TAG:-r05}; O=$R/gpurun_out/ev_$TAG; mkdir -p $O

@@ -2,6 +2,7 @@
 # Round 5: book units with non-ASCII words by the wave rules
 # (k_tokenize_chunk<UNI>) — parity, then 300 books with one é word per
 # 2 KB with the wave rules on / off (TFIDF_NO_UNIWAVE=1) and the ASCII books.
+export TFIDF_DEBUG=1   # the library reads its TFIDF_* knobs only under TFIDF_DEBUG
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest -x -q -m gpu --timeout 300 --timeout-method thread tests/test_gpu_uni_wave.py tests/test_gpu_books.py tests/test_gpu_unicode.py tests/test_gpu_identity.py > gpurun_out/unib_tests.log 2>&1

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 5: phase stops (TFIDF_DEBUG_STOP 1..4, 0) at cfg 2 with all documents
 # non-ASCII (one simple é word each: k_tokenize_wave<UNI>) and all ASCII.
+export TFIDF_DEBUG=1   # the library reads its TFIDF_* knobs only under TFIDF_DEBUG
 set -o pipefail
 mkdir -p gpurun_out
 for f in 1.0 0.0; do

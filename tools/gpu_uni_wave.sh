@@ -3,6 +3,7 @@
 # parity (new + the existing Unicode suites), then cfg 2 with 10 % / 100 %
 # non-ASCII documents with the wave rules on and off (TFIDF_NO_UNIWAVE=1),
 # and the all-ASCII cfg-2 step.  Every GPU step bounded.
+export TFIDF_DEBUG=1   # the library reads its TFIDF_* knobs only under TFIDF_DEBUG
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 900 python -u -m pytest -x -q -m gpu --timeout 300 --timeout-method thread tests/test_gpu_uni_wave.py tests/test_gpu_unicode_sparse.py tests/test_gpu_unicode.py tests/test_gpu_identity.py tests/test_gpu_xcd_units.py tests/test_gpu_books.py tests/test_gpu_pack.py > gpurun_out/uniw_tests.log 2>&1

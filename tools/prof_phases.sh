@@ -4,6 +4,7 @@
 # between consecutive stops.  DOCS docs (default 200k).  KRE: kernel name
 # regex (default tokenize_wave; "tokenize_wave<false, false, true>" for the
 # UNI pass alone), BARGS: extra bench.py arguments (e.g. --unicode-frac 1.0).
+export TFIDF_DEBUG=1   # the library reads its TFIDF_* knobs only under TFIDF_DEBUG
 set -o pipefail
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/prof_phases; mkdir -p $O
 cd /tmp && export TMPDIR=/tmp

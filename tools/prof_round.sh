@@ -3,6 +3,7 @@
 # traffic (FETCH_SIZE / WRITE_SIZE, separate passes) and SQ counters for every
 # kernel of one index build, then the tokenize ablation if ABLATE is set.
 # Every GPU step bounded.  Usage (GPU box): TAG=r01 bash tools/prof_round.sh
+export TFIDF_DEBUG=1   # the library reads its TFIDF_* knobs only under TFIDF_DEBUG
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${TAG:-r01}
