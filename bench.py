@@ -34,6 +34,22 @@ import numpy as np  # noqa: E402
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
+
+def default_cap(vocab):
+    """Dictionary slots (log2) for a vocabulary: load <= 0.25 while the
+    block-major inversion applies (<= 2^21 slots; its count table is sized by
+    the vocabulary, so a sparser probe table costs only the table itself and
+    resolves nearly every tokenizer lookup in its first probe round), else
+    the smallest power of two >= 1.6 x vocab (term-major, cfg 5)."""
+    cap = 18
+    while (1 << cap) < 4 * vocab and cap < 21:
+        cap += 1
+    if (1 << cap) < 4 * vocab:
+        cap = 18
+        while (1 << cap) < 1.6 * vocab:
+            cap += 1
+    return cap
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -48,7 +64,7 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=25_000, help="docs in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--no-queries", action="store_true")
     ap.add_argument("--cap-log2", type=int, default=0,
-                    help="dictionary slots 2^x (0 = smallest power of two >= 1.6 x vocab, at least 2^18)")
+                    help="dictionary slots 2^x (0 = default_cap(vocab))")
     ap.add_argument("--inversion", choices=("auto", "block", "term"), default="auto")
     ap.add_argument("--unicode-every", type=int, default=0,
                     help="one non-ASCII word per this many bytes of every document (book-like text)")
@@ -218,9 +234,7 @@ def bench_node(args):
     from tfidf_amd import distributed as D
     G = args.gpus
     torch.cuda.set_device(0)
-    cap = args.cap_log2 or 18
-    while not args.cap_log2 and (1 << cap) < 1.6 * args.vocab:
-        cap += 1
+    cap = args.cap_log2 or default_cap(args.vocab)
     node = D.Node(devices=list(range(G)), stats_mode=L.STATS_GLOBAL, vocab_capacity_log2=cap)
     lib = L.load()
     corpora = []
@@ -320,11 +334,7 @@ def main():
     corpus = synth.DeviceCorpus(n_docs, V=args.vocab, len_min=args.len_min, len_max=args.len_max,
                                 doc_base=doc_base, device=local)
     n_unicode = corpus.inject_unicode(args.unicode_frac) + corpus.inject_unicode_every(args.unicode_every)
-    cap = args.cap_log2
-    if not cap:
-        cap = 18
-        while (1 << cap) < 1.6 * args.vocab:
-            cap += 1
+    cap = args.cap_log2 or default_cap(args.vocab)
     inv = {"auto": 0, "block": 1, "term": 2}[args.inversion]
     idx = ShardIndex(device=local, vocab_capacity_log2=cap, inversion=inv,
                      stats_mode=STATS_GLOBAL if dist_on else 0)

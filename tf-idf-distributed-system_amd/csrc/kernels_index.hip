@@ -2392,16 +2392,18 @@ __device__ __forceinline__ bool tile_of(uint32_t w, uint32_t n_blocks, uint32_t 
 }
 static uint32_t tiles_grid(uint32_t n_blocks, uint32_t R) { return (n_blocks + 7) / 8 * 8 * R; }
 
-// one workgroup (1024 threads) per (block, range) tile (tile_of), LDS
-// histogram of the range's slots (128 KiB; 16-bit counters, two tiles per CU,
-// measured 0.50 -> 0.52 ms).  Wave w handles documents d0 + w + 16
-// (kInvDocs i + j), j < kInvDocs.
+// one workgroup (1024 threads) per (block, range) tile (tile_of): LDS
+// histogram of the range's 65536 slots in 16-bit counters (two per word; a
+// block's count of one slot is at most kBlockDocs = 8192), 128 KiB.  Wave w
+// handles documents d0 + w + 16 (kInvDocs i + j), j < kInvDocs.  The counts
+// of the range's occupied slots are written at their columns (col_rank), so
+// the count table follows the vocabulary, not the dictionary's probe table.
 __global__ void __launch_bounds__(1024) k_df_partial(PostingParams p) {
   extern __shared__ uint32_t hist[];
   uint32_t b, r;
   if (!tile_of(blockIdx.x, p.n_blocks, p.n_ranges, &b, &r)) return;
   const uint32_t RS = 1u << p.range_shift;
-  for (uint32_t i = threadIdx.x; i < RS; i += blockDim.x) hist[i] = 0;
+  for (uint32_t i = threadIdx.x; i < RS / 2; i += blockDim.x) hist[i] = 0;
   __syncthreads();
   const uint64_t d0 = (uint64_t)b * kBlockDocs;
   const uint64_t d1 = d0 + kBlockDocs < p.n_docs ? d0 + kBlockDocs : p.n_docs;
@@ -2413,6 +2415,10 @@ __global__ void __launch_bounds__(1024) k_df_partial(PostingParams p) {
   InvGroup cur = inv_group(p, dd, d1, nw, r, false);
   uint32_t c[kInvDocs];
   if (dd < d1) inv_load(p, cur, lane, c);
+  auto count = [&](uint32_t e) __attribute__((always_inline)) {
+    const uint32_t sl = e & rmask;
+    atomicAdd(&hist[sl >> 1], 1u << ((sl & 1u) << 4));
+  };
   while (dd < d1) {
     const uint64_t dn = dd + step;
     const InvGroup nxt = inv_group(p, dn, d1, nw, r, false);
@@ -2420,12 +2426,12 @@ __global__ void __launch_bounds__(1024) k_df_partial(PostingParams p) {
     if (dn < d1) inv_load(p, nxt, lane, cn);                       // next group in flight
 #pragma unroll
     for (int j = 0; j < kInvDocs; j++)
-      if (c[j]) atomicAdd(&hist[c[j] & rmask], 1u);
+      if (c[j]) count(c[j]);
     for (uint32_t off = lane + 64; off < cur.maxn; off += 64) {     // segments longer than 64
       inv_load(p, cur, off, c);
 #pragma unroll
       for (int j = 0; j < kInvDocs; j++)
-        if (c[j]) atomicAdd(&hist[c[j] & rmask], 1u);
+        if (c[j]) count(c[j]);
     }
     cur = nxt;
 #pragma unroll
@@ -2433,35 +2439,46 @@ __global__ void __launch_bounds__(1024) k_df_partial(PostingParams p) {
     dd = dn;
   }
   __syncthreads();
-  uint32_t *out = p.blk + (size_t)b * p.C + ((size_t)r << p.range_shift);
-  for (uint32_t i = threadIdx.x; i < RS; i += blockDim.x) out[i] = hist[i];
+  // occupied slots of the range -> their columns (a word's slots hold
+  // consecutive columns from its prefix count)
+  uint32_t *out = p.blk + (size_t)b * p.NC;
+  const uint32_t w0 = (r << p.range_shift) >> 5;
+  for (uint32_t w = threadIdx.x; w < (RS >> 5); w += blockDim.x) {
+    const uint2 e = p.crank[w0 + w];
+    uint32_t bits = e.x, col = e.y;
+    while (bits) {
+      const uint32_t sl = 32 * w + (uint32_t)__builtin_ctz(bits);
+      bits &= bits - 1;
+      out[col++] = (hist[sl >> 1] >> ((sl & 1u) << 4)) & 0xFFFFu;
+    }
+  }
 }
 
-// per slot: df = sum of the per-block counts (row n_blocks).
+// per column: df = sum of the per-block counts (row n_blocks).
 __global__ void __launch_bounds__(256) k_df_sum(PostingParams p) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= p.C) return;
+  if (t >= p.NC) return;
   uint32_t run = 0;
-  for (uint32_t b = 0; b < p.n_blocks; b++) run += p.blk[(size_t)b * p.C + t];
-  p.blk[(size_t)p.n_blocks * p.C + t] = run;
+  for (uint32_t b = 0; b < p.n_blocks; b++) run += p.blk[(size_t)b * p.NC + t];
+  p.blk[(size_t)p.n_blocks * p.NC + t] = run;
 }
 
-// per block row: exclusive scan over slots in place (one workgroup per row);
+// per block row: exclusive scan over columns in place (one workgroup per row);
 // the row total goes to bbase[b + 1] (turned into bases by k_block_scan).
-// Tiles of 16384 slots: each thread loads 16 consecutive counts with four
+// Tiles of 16384 columns: each thread loads 16 consecutive counts with four
 // 16 B loads (coalesced across the workgroup), scans them in registers, and a
 // workgroup scan of the 1024 thread totals gives the offsets.
 __global__ void __launch_bounds__(1024) k_row_scan(PostingParams p) {
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t carry_sh;
-  uint32_t *row = p.blk + (size_t)blockIdx.x * p.C;
+  uint32_t *row = p.blk + (size_t)blockIdx.x * p.NC;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   if (tid == 0) carry_sh = 0;
   __syncthreads();
-  for (uint32_t t0 = 0; t0 < p.C; t0 += 16384) {
+  for (uint32_t t0 = 0; t0 < p.NC; t0 += 16384) {
     const uint32_t i0 = t0 + tid * 16;
     uint32_t v[16];
-    if (i0 + 16 <= p.C) {
+    if (i0 + 16 <= p.NC) {
       const uint4 *src = reinterpret_cast<const uint4 *>(row + i0);
 #pragma unroll
       for (int q = 0; q < 4; q++) {
@@ -2470,7 +2487,7 @@ __global__ void __launch_bounds__(1024) k_row_scan(PostingParams p) {
       }
     } else {
 #pragma unroll
-      for (int q = 0; q < 16; q++) v[q] = (i0 + q < p.C) ? row[i0 + q] : 0u;
+      for (int q = 0; q < 16; q++) v[q] = (i0 + q < p.NC) ? row[i0 + q] : 0u;
     }
     uint32_t tot = 0;
 #pragma unroll
@@ -2496,14 +2513,14 @@ __global__ void __launch_bounds__(1024) k_row_scan(PostingParams p) {
     uint32_t o[16];
 #pragma unroll
     for (int q = 0; q < 16; q++) { o[q] = run; run += v[q]; }
-    if (i0 + 16 <= p.C) {
+    if (i0 + 16 <= p.NC) {
       uint4 *dst = reinterpret_cast<uint4 *>(row + i0);
 #pragma unroll
       for (int q = 0; q < 4; q++) dst[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
     } else {
 #pragma unroll
       for (int q = 0; q < 16; q++)
-        if (i0 + q < p.C) row[i0 + q] = o[q];
+        if (i0 + q < p.NC) row[i0 + q] = o[q];
     }
     __syncthreads();
   }
@@ -2512,31 +2529,30 @@ __global__ void __launch_bounds__(1024) k_row_scan(PostingParams p) {
 
 // Inversion in two passes so that every store stream stays L2-resident.
 // A (block, range) tile's postings span ~10 k term regions: storing each
-// posting straight to its final slot keeps that many partial lines open per
+// posting straight to its final column keeps that many partial lines open per
 // workgroup and writes back ~3x the bytes.  Instead:
 //   k_scatter_part : per tile, each posting is appended to one of the tile's
-//                    sub-range streams (kSubSlots slots each) in a temporary
-//                    buffer laid out exactly like the postings (stream k's
-//                    region = the final region of its slots, from blk), one
-//                    32-bit word doc_local(13) | slot_low(9) | tf(10); tf >=
-//                    1023 is stored as 1023 and re-read from the CSR row in
-//                    pass 2, the norm is re-read from doc_norm there;
-//   k_scatter_sort : per stream (~86 KB), LDS cursor per slot, final postings
-//                    written inside the stream's own region.
-#ifndef TFIDF_SUB_BITS
-#define TFIDF_SUB_BITS 9
-#endif
-constexpr uint32_t kSubBits = TFIDF_SUB_BITS;
+//                    64 sub-range streams (kSubSlots dictionary slots each) in
+//                    a temporary buffer laid out exactly like the postings
+//                    (stream k's region = the final region of its slots'
+//                    columns, from blk), one 32-bit word doc_local(13) |
+//                    slot_low(10) | tf(9); tf >= 511 is stored as 511 and
+//                    re-read from the CSR row in pass 2, the norm is re-read
+//                    from doc_norm there;
+//   k_scatter_sort : per stream, LDS cursor per slot, final postings written
+//                    inside the stream's own region.
+constexpr uint32_t kSubBits = 10;
 constexpr uint32_t kSubSlots = 1u << kSubBits;
-constexpr uint32_t kTmpTfShift = 13 + kSubBits;              // temp word: doc_local(13) | slot_low | tf(10)
+constexpr uint32_t kTmpTfShift = 13 + kSubBits;              // temp word: doc_local(13) | slot_low | tf(9)
 constexpr uint32_t kTmpTfEsc = (1u << (32 - kTmpTfShift)) - 1; // tf field value meaning "tf >= this: see the CSR"
-static_assert(kTmpTfShift <= 22, "temp word layout");
+constexpr uint32_t kPartStreams = kRangeSlots / kSubSlots;  // 64
+static_assert(kTmpTfShift <= 23 && kPartStreams == 64, "temp word layout");
 
 __device__ __forceinline__ void part_entries(const PostingParams &p, uint32_t *bcur, uint32_t rmask, uint64_t bb,
                                              const InvGroup &g, uint64_t dd, uint32_t d0l, uint32_t stride,
                                              const uint32_t *c) {
   const uint32_t lane = threadIdx.x & 63;
-  constexpr uint32_t kNoop = kRangeSlots / kSubSlots;       // idle lanes bump a spare cursor
+  constexpr uint32_t kNoop = kPartStreams;                    // idle lanes bump a spare cursor
 #pragma unroll
   for (int j = 0; j < kInvDocs; j++) {
     const bool in = c[j] != 0;
@@ -2550,70 +2566,13 @@ __device__ __forceinline__ void part_entries(const PostingParams &p, uint32_t *b
   }
 }
 
-// Wave-local staging of one document group's entries (first 64 of each
-// segment): entries are counting-sorted by sub-range stream in the wave's LDS
-// area, then stored stream run by stream run, so consecutive lanes write
-// consecutive addresses (one store request per line instead of one per
-// entry).  The stream id rides in bits 56..61 of the temp word (pass 2 ignores
-// them).
-constexpr uint32_t kPartStreams = kRangeSlots / kSubSlots;  // 64
-static_assert(kPartStreams <= 64, "temp word layout");
-struct PartWave {
-  uint64_t stage[kInvDocs * 64];
-  uint32_t cnt[64], soff[64], gb[64];
-};
-
-__device__ __forceinline__ void part_group_staged(const PostingParams &p, uint32_t *bcur, PartWave &w, uint32_t rmask,
-                                                  uint64_t bb, const InvGroup &g, uint64_t dd, uint32_t d0l,
-                                                  uint32_t stride, const uint32_t *c) {
-  const uint32_t lane = threadIdx.x & 63;
-  uint64_t val[kInvDocs];
-  uint32_t rank[kInvDocs], sj[kInvDocs];
-#pragma unroll
-  for (int j = 0; j < kInvDocs; j++) {
-    const bool in = c[j] != 0;
-    const uint32_t sl = c[j] & rmask;
-    sj[j] = sl >> kSubBits;
-    rank[j] = 0;
-    val[j] = 0;
-    if (in) {
-      const uint32_t dl = (uint32_t)(dd + (uint64_t)stride * j) - d0l;
-      const uint32_t tf = csr_tf_field(c[j], p.range_shift);
-      val[j] = (uint64_t)(dl | ((sl & (kSubSlots - 1)) << 13) | (min(tf, kTmpTfEsc) << kTmpTfShift)) |
-               ((uint64_t)sj[j] << 56);
-      rank[j] = atomicAdd(&w.cnt[sj[j]], 1u);
-    }
-  }
-  const uint32_t n = w.cnt[lane];
-  const uint32_t incl = wave_incl_add(n);
-  const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-  w.soff[lane] = incl - n;
-  w.gb[lane] = n ? atomicAdd(&bcur[lane], n) : 0u;
-  w.cnt[lane] = 0;
-#pragma unroll
-  for (int j = 0; j < kInvDocs; j++)
-    if (c[j] != 0) w.stage[w.soff[sj[j]] + rank[j]] = val[j];
-  for (uint32_t t0 = 0; t0 < T; t0 += 64) {
-    const uint32_t ti = t0 + lane;
-    if (ti < T) {
-      const uint64_t v = w.stage[ti];
-      const uint32_t st = (uint32_t)(v >> 56);
-      p.post_tmp[bb + w.gb[st] + (ti - w.soff[st])] = (uint32_t)v;
-    }
-  }
-}
-
-#ifndef TFIDF_PART_WG
-#define TFIDF_PART_WG 1
-#endif
-#if TFIDF_PART_WG
-// Round 5: workgroup-wide staging.  All the workgroup's waves take their next
+// Workgroup-wide staging (round 5).  All the workgroup's waves take their next
 // document group together (a round: nw * kInvDocs documents, up to 8 192
 // entries); the round's entries are counting-sorted by sub-range stream in LDS
-// and stored stream run by stream run, ~16x longer runs than the wave-local
+// and stored stream run by stream run, ~16x longer runs than wave-local
 // staging (one to two lines per store instruction instead of ~13).
 __global__ void __launch_bounds__(1024) k_scatter_part(PostingParams p) {
-  __shared__ uint32_t bcur[kRangeSlots / kSubSlots + 1];
+  __shared__ uint32_t bcur[kPartStreams + 1];
   __shared__ uint32_t cnt[kPartStreams], soff[kPartStreams], gb[kPartStreams], tot_sh;
   __shared__ uint32_t stage[16 * kInvDocs * 64];
   __shared__ uint8_t sid[16 * kInvDocs * 64];
@@ -2623,8 +2582,13 @@ __global__ void __launch_bounds__(1024) k_scatter_part(PostingParams p) {
   if (!tile_of(blockIdx.x, p.n_blocks, p.n_ranges, &b, &r)) return;
   const uint32_t RS = 1u << p.range_shift, rmask = RS - 1;
   const uint32_t nsub = RS > kSubSlots ? RS / kSubSlots : 1u;
-  const uint32_t *row = p.blk + (size_t)b * p.C + ((size_t)r << p.range_shift);
-  if (threadIdx.x < nsub) bcur[threadIdx.x] = row[threadIdx.x * kSubSlots];
+  const uint32_t *row = p.blk + (size_t)b * p.NC;
+  if (threadIdx.x < nsub) {
+    // stream k's region starts at the column of its first occupied slot (=
+    // the occupied slots before it, col_rank); an empty stream is never bumped
+    const uint32_t c0 = p.crank[((r << p.range_shift) + threadIdx.x * kSubSlots) >> 5].y;
+    bcur[threadIdx.x] = c0 < p.NC ? row[c0] : 0u;
+  }
   if (threadIdx.x < kPartStreams) cnt[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t bb = p.bbase[b];
@@ -2692,48 +2656,9 @@ __global__ void __launch_bounds__(1024) k_scatter_part(PostingParams p) {
     // round's store loop
   }
 }
-#else
-__global__ void __launch_bounds__(1024) k_scatter_part(PostingParams p) {
-  __shared__ uint32_t bcur[kRangeSlots / kSubSlots + 1];
-  __shared__ PartWave pwave[16];
-  const uint32_t lane = threadIdx.x & 63, nw = blockDim.x >> 6;
-  const uint32_t wid = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  uint32_t b, r;
-  if (!tile_of(blockIdx.x, p.n_blocks, p.n_ranges, &b, &r)) return;
-  const uint32_t RS = 1u << p.range_shift, rmask = RS - 1;
-  const uint32_t nsub = RS > kSubSlots ? RS / kSubSlots : 1u;
-  const uint32_t *row = p.blk + (size_t)b * p.C + ((size_t)r << p.range_shift);
-  if (threadIdx.x < nsub) bcur[threadIdx.x] = row[threadIdx.x * kSubSlots];
-  if (threadIdx.x < 16 * 64) pwave[threadIdx.x >> 6].cnt[threadIdx.x & 63] = 0;
-  __syncthreads();
-  const uint64_t bb = p.bbase[b];
-  const uint64_t d0 = (uint64_t)b * kBlockDocs;
-  const uint64_t d1 = d0 + kBlockDocs < p.n_docs ? d0 + kBlockDocs : p.n_docs;
-  const uint64_t step = (uint64_t)nw * kInvDocs;
-  uint64_t dd = d0 + wid;
-  InvGroup g = inv_group(p, dd, d1, nw, r, false);
-  uint32_t c[kInvDocs];
-  if (dd < d1) inv_load(p, g, lane, c);
-  while (dd < d1) {
-    const uint64_t dn = dd + step;
-    const InvGroup gn = inv_group(p, dn, d1, nw, r, false);
-    uint32_t cn[kInvDocs];
-    if (dn < d1) inv_load(p, gn, lane, cn);                       // next group in flight
-    part_group_staged(p, bcur, pwave[wid], rmask, bb, g, dd, (uint32_t)d0, nw, c);
-    for (uint32_t off = lane + 64; off < g.maxn; off += 64) {    // segments longer than 64
-      inv_load(p, g, off, c);
-      part_entries(p, bcur, rmask, bb, g, dd, (uint32_t)d0, nw, c);
-    }
-    g = gn;
-#pragma unroll
-    for (int j = 0; j < kInvDocs; j++) c[j] = cn[j];
-    dd = dn;
-  }
-}
-#endif
 
 // tf of (doc, slot) from the document's CSR row segment of range r (the
-// escape path of the 10-bit temp tf field)
+// escape path of the 9-bit temp tf field; rare)
 __device__ uint32_t csr_tf_of(const PostingParams &p, uint64_t d, uint32_t r, uint32_t slot) {
   uint64_t base;
   uint32_t lo, hi;
@@ -2753,28 +2678,30 @@ __device__ uint32_t csr_tf_of(const PostingParams &p, uint64_t d, uint32_t r, ui
 // workgroup takes sort_spw = 4 streams in turn, so few streams per CU are open
 // at a time and the regions being written stay L2-resident (cfg-2 inversion:
 // one stream per 1024-thread workgroup 3.11 ms, 8 per 1024 2.87, 4 per 512 2.52)
-#ifndef TFIDF_SORT_STAGE
-#define TFIDF_SORT_STAGE 8192
-#endif
-#ifndef TFIDF_SORT_PLAIN
-#define TFIDF_SORT_PLAIN 1
-#endif
 // Round 5: a stream of at most kSortStage entries is assembled in LDS and
 // written out contiguous (its region is [lo, hi) of the block's postings);
-// scattered 4-byte global stores only for larger streams.
-constexpr uint32_t kSortStage = TFIDF_SORT_STAGE;
+// scattered 4-byte global stores only for larger streams (4 096 / 6 144 /
+// 8 192 / 16 384 measured 2.03 / 1.93 / 1.85 / 1.97 ms scatter at cfg 2).
+constexpr uint32_t kSortStage = 8192;
+constexpr uint32_t kSortMaxSpw = 8;
 __global__ void __launch_bounds__(1024) k_scatter_sort(PostingParams p) {
   __shared__ uint32_t cur[kSubSlots + 1];                   // + no-op cursor for idle lanes
-  __shared__ uint32_t ostage[kSortStage > 0 ? kSortStage : 1];
+  __shared__ uint32_t ostage[kSortStage];
   __shared__ uint8_t bnorm[kBlockDocs];                     // the block's norm bytes: an LDS read per entry
                                                             // instead of a global load that waits on the temp word
+  __shared__ uint2 wk[kSortMaxSpw * (kSubSlots / 32) + 1];  // the streams' column ranks (col_rank)
   const uint32_t b = blockIdx.x, r = blockIdx.y;
   const uint32_t RS = 1u << p.range_shift;
   const uint32_t BS = RS < kSubSlots ? RS : kSubSlots;
   const uint32_t nsub = RS / BS;
-  const uint32_t *row = p.blk + (size_t)b * p.C;
+  const uint32_t k0 = blockIdx.z * p.sort_spw, k1 = min(nsub, k0 + p.sort_spw);
+  if (k0 >= k1) return;
+  const uint32_t *row = p.blk + (size_t)b * p.NC;
   const uint64_t bb = p.bbase[b];
+  const uint32_t btot = (uint32_t)(p.bbase[b + 1] - bb);
   const uint32_t d0 = b * kBlockDocs;
+  const uint32_t sw0 = ((r << p.range_shift) + k0 * BS) >> 5, nwk = (k1 - k0) * BS / 32 + 1;
+  for (uint32_t i = threadIdx.x; i < nwk; i += blockDim.x) wk[i] = p.crank[sw0 + i];   // (+1: the sentinel / next word)
   {
     const uint32_t nd = (uint32_t)min((uint64_t)kBlockDocs, p.n_docs - d0);
     for (uint32_t i = threadIdx.x * 16; i < nd; i += blockDim.x * 16) {
@@ -2785,17 +2712,23 @@ __global__ void __launch_bounds__(1024) k_scatter_sort(PostingParams p) {
       }
     }
   }
-  for (uint32_t k = blockIdx.z * p.sort_spw; k < min(nsub, (blockIdx.z + 1) * p.sort_spw); k++) {
-    const size_t s0 = ((size_t)r << p.range_shift) + (size_t)k * BS;
-    for (uint32_t i = threadIdx.x; i < BS; i += blockDim.x) cur[i] = row[s0 + i];
-    const uint32_t lo = row[s0];
-    const uint32_t hi = s0 + BS < p.C ? row[s0 + BS] : (uint32_t)(p.bbase[b + 1] - bb);
-    const bool staged = kSortStage > 0 && hi - lo <= kSortStage;   // workgroup-uniform
+  __syncthreads();
+  for (uint32_t k = k0; k < k1; k++) {
+    // the stream's slots s0 .. s0 + BS - 1 hold columns c0 .. c1 - 1
+    const uint32_t s0 = (r << p.range_shift) + k * BS;
+    const uint2 *kw = wk + (k - k0) * (BS / 32);
+    const uint32_t c0 = kw[0].y, c1 = kw[BS / 32].y;
+    if (c0 == c1) continue;                                   // workgroup-uniform: no occupied slot
+    for (uint32_t i = threadIdx.x; i < BS; i += blockDim.x) {
+      const uint2 e = kw[i >> 5];
+      const uint32_t bit = 1u << (i & 31u);
+      if (e.x & bit) cur[i] = row[e.y + __popc(e.x & (bit - 1u))];
+    }
+    const uint32_t lo = row[c0];
+    const uint32_t hi = c1 < p.NC ? row[c1] : btot;
+    const bool staged = hi - lo <= kSortStage;                // workgroup-uniform
     __syncthreads();
-#ifndef TFIDF_SORT_U
-#define TFIDF_SORT_U 8
-#endif
-    constexpr int U = TFIDF_SORT_U;   // entries per thread in flight (8: a ~5 k-entry stream in one round; round 5 with
+    constexpr int U = 8;              // entries per thread in flight (8: a ~5 k-entry stream in one round; round 5 with
                                       // staging + plain atomics: 4 / 8 / 12 / 16 = 1.91 / 1.86 / 1.84 / 1.84 ms scatter)
     for (uint32_t e0 = lo; e0 < hi; e0 += U * blockDim.x) {   // uniform trip count: all lanes ballot
       uint32_t x[U], nrm[U];
@@ -2819,14 +2752,10 @@ __global__ void __launch_bounds__(1024) k_scatter_sort(PostingParams p) {
         // segment is free); with the LDS-staged output they beat the wave
         // peer-mask bump (10 ballots per entry): scatter 2.34 -> 1.99 ms at cfg 2
         // (without staging the peer-mask bump was 4 % faster)
-#if TFIDF_SORT_PLAIN
         const uint32_t pos = atomicAdd(&cur[sl], 1u);
-#else
-        const uint32_t pos = cursor_bump<kSubBits + 1>(cur, sl, threadIdx.x & 63);
-#endif
         const uint32_t doc = d0 + (x[u] & (kBlockDocs - 1));
         uint32_t tf = x[u] >> kTmpTfShift;
-        if (in && tf == kTmpTfEsc) tf = csr_tf_of(p, doc, r, (uint32_t)s0 + sl);      // rare: tf >= 1023
+        if (in && tf == kTmpTfEsc) tf = csr_tf_of(p, doc, r, s0 + sl);                // rare: tf >= 511
         if (in) {
           const uint32_t w = post_word(x[u] & (kBlockDocs - 1), tf, nrm[u]);
           if (staged) ostage[pos - lo] = w;
@@ -2944,17 +2873,18 @@ hipError_t launch_tokenize_long(const BuildParams &p, int grid, hipStream_t s) {
 }
 static void allow_big_lds() {
   static std::atomic<uint64_t> done{0};
-  allow_dyn_lds((const void *)k_df_partial, 4 << kRangeBits, done);
+  allow_dyn_lds((const void *)k_df_partial, 2 << kRangeBits, done);
 }
 
 hipError_t launch_df_partial(const PostingParams &p, hipStream_t s) {
   allow_big_lds();
-  const size_t lds = sizeof(uint32_t) << p.range_shift;
+  const size_t lds = (size_t)2 << p.range_shift;             // 16-bit counters
   hipLaunchKernelGGL(k_df_partial, dim3(tiles_grid(p.n_blocks, p.n_ranges)), dim3(1024), lds, s, p);
   return hipGetLastError();
 }
 hipError_t launch_df_sum(const PostingParams &p, hipStream_t s) {
-  hipLaunchKernelGGL(k_df_sum, dim3((p.C + 255) / 256), dim3(256), 0, s, p);
+  if (p.NC == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_df_sum, dim3((p.NC + 255) / 256), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 hipError_t launch_row_scan(const PostingParams &p, hipStream_t s) {
@@ -2976,6 +2906,80 @@ hipError_t launch_count_nonzero(const uint64_t *a, uint32_t n, unsigned long lon
   hipLaunchKernelGGL(k_count_nonzero, dim3(grid), dim3(256), 0, s, a, n, out);
   return hipGetLastError();
 }
+// ---- columns of the block-major inversion (round 6).  The dictionary is a
+// probe table (load 0.2-0.4: fewer dependent probe rounds in the tokenizer);
+// the count table, its scans and the postings are indexed by the rank of an
+// occupied slot ("column", 0 .. num_terms - 1), so their size follows the
+// vocabulary, not the probe table.  crank[w] = {occupancy bits of slots 32 w
+// .. 32 w + 31, occupied slots before 32 w}; crank[C / 32] = {0, num_terms}.
+// Column of occupied slot s: crank[s / 32].y + popc(bits below s).
+__global__ void __launch_bounds__(256) k_crank_bits(const uint64_t *lo, uint32_t C, uint2 *crank) {
+  const uint32_t s0 = (blockIdx.x * blockDim.x + threadIdx.x) & ~63u, lane = threadIdx.x & 63;
+  if (s0 >= C) return;                                        // wave-uniform (C is a multiple of 64)
+  const uint64_t m = __ballot(lo[s0 + lane] != 0);
+  if (lane < 2) crank[(s0 >> 5) + lane] = make_uint2(lane ? (uint32_t)(m >> 32) : (uint32_t)m, 0u);
+}
+// exclusive scan of the words' popcounts (one workgroup; 16 words per thread
+// per tile, as k_row_scan); the total = columns
+__global__ void __launch_bounds__(1024) k_crank_scan(uint2 *crank, uint32_t W, unsigned long long *n_cols) {
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t carry_sh;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) carry_sh = 0;
+  __syncthreads();
+  for (uint32_t t0 = 0; t0 < W; t0 += 16384) {
+    const uint32_t i0 = t0 + tid * 16;
+    uint32_t v[16], tot = 0;
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+      v[q] = i0 + q < W ? (uint32_t)__popc(crank[i0 + q].x) : 0u;
+      tot += v[q];
+    }
+    const uint32_t x = wave_incl_add(tot);
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    uint32_t base = carry_sh, all = 0;
+    for (uint32_t w = 0; w < 16; w++) {
+      const uint32_t sw = wsum[w];
+      if (w < wid) base += sw;
+      all += sw;
+    }
+    base += x - tot;
+    __syncthreads();
+    if (tid == 0) carry_sh += all;
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+      if (i0 + q < W) crank[i0 + q].y = base;
+      base += v[q];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    crank[W] = make_uint2(0u, carry_sh);
+    *n_cols = carry_sh;
+  }
+}
+hipError_t launch_col_rank(const uint64_t *dict_lo, uint32_t C, uint2 *crank, unsigned long long *n_cols,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(k_crank_bits, dim3((C + 255) / 256), dim3(256), 0, s, dict_lo, C, crank);
+  hipLaunchKernelGGL(k_crank_scan, dim3(1), dim3(1024), 0, s, crank, C >> 5, n_cols);
+  return hipGetLastError();
+}
+// per-slot df (the host mirror, vocabulary export, GLOBAL exchange) from the
+// per-column df
+__global__ void __launch_bounds__(256) k_df_slots(const uint2 *crank, const uint32_t *df_col, uint32_t C,
+                                                  uint32_t *df_slot) {
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= C) return;
+  const uint2 e = crank[t >> 5];
+  const uint32_t bit = 1u << (t & 31u);
+  df_slot[t] = (e.x & bit) ? df_col[e.y + __popc(e.x & (bit - 1u))] : 0u;
+}
+hipError_t launch_df_slots(const uint2 *crank, const uint32_t *df_col, uint32_t C, uint32_t *df_slot, hipStream_t s) {
+  hipLaunchKernelGGL(k_df_slots, dim3((C + 255) / 256), dim3(256), 0, s, crank, df_col, C, df_slot);
+  return hipGetLastError();
+}
+
 hipError_t launch_block_base(const PostingParams &p, hipStream_t s) {
   hipLaunchKernelGGL(k_block_scan, dim3(1), dim3(1024), 0, s, p);   // (serial k_block_base: 15 us at 123 blocks)
   return hipGetLastError();

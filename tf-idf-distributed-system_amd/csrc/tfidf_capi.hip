@@ -257,6 +257,11 @@ struct Snapshot {
   KeyTable keys;                       // document keys of the staged ids
   std::shared_ptr<DevMem> text, offsets;   // the staged corpus it was built from
   DevMem dict, csr, csr_esc, post_esc, doc_len, doc_nuniq, doc_norm, rsplit, blk, bbase, post, row_off, toff, tdf;
+  // block-major columns (kernels_index.hip col_rank): occupancy bits and
+  // prefix counts per 32 slots, the per-slot df, and the host copy of crank
+  DevMem crank, sdf;
+  PinnedVec<uint2> h_crank;
+  uint32_t NC = 0;                     // block-major columns (= num_terms)
   std::vector<uint32_t> malformed;     // ascending committed ids of documents that are not UTF-8
   std::vector<uint64_t> h_esc;         // CSR tf escapes, sorted (csr_put)
   std::vector<uint64_t> h_post_esc;    // block-major posting tf escapes, sorted (post_word)
@@ -272,10 +277,16 @@ struct Snapshot {
   std::mutex term_mu;
   explicit Snapshot(int d)
       : dev(d), dict(d), csr(d), csr_esc(d), post_esc(d), doc_len(d), doc_nuniq(d), doc_norm(d), rsplit(d), blk(d),
-        bbase(d), post(d), row_off(d), toff(d), tdf(d) {}
-  const uint32_t *df_dev() const {
-    return term_major ? tdf.as<uint32_t>() : blk.as<uint32_t>() + (size_t)n_blocks * C;
+        bbase(d), post(d), row_off(d), toff(d), tdf(d), crank(d), sdf(d) {}
+  const uint32_t *df_dev() const { return term_major ? tdf.as<uint32_t>() : sdf.as<uint32_t>(); }   // per slot
+  // what the scorers index a term's postings by: its column (block-major) or
+  // its dictionary slot (term-major); the scorers' C is the matching count
+  uint32_t col_of(uint32_t slot) const {
+    if (term_major) return slot;
+    const uint2 e = h_crank[slot >> 5];
+    return e.y + (uint32_t)__builtin_popcount(e.x & ((1u << (slot & 31u)) - 1u));
   }
+  uint32_t qcols() const { return term_major ? C : NC; }
   uint64_t staged_of(uint64_t doc) const { return live_map.empty() ? doc : live_map[doc]; }
 };
 
@@ -1001,8 +1012,10 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
     HIP_TRY(S.toff.reserve(((size_t)C + 1) * 8));
     HIP_TRY(S.tdf.reserve((size_t)C * 4));
   } else {
-    HIP_TRY(S.blk.reserve((size_t)(S.n_blocks + 1) * C * 4));
+    // (the count table blk is sized by the columns, known after the tokenizers)
     HIP_TRY(S.bbase.reserve((size_t)(S.n_blocks + 2) * 8));
+    HIP_TRY(S.crank.reserve(((size_t)C / 32 + 1) * 8));
+    HIP_TRY(S.sdf.reserve((size_t)C * 4));
   }
 
   // counters: [0..2] stats u64, [3] err flags u32 + [3].hi first doc, [4] long_count, [5] retry_count,
@@ -1093,9 +1106,18 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
     ix->timing.num_docs = N;
     return kRcNoPublish;
   }
+  // block-major: columns of the dictionary as it stands (final unless the
+  // long path runs below, which recomputes them); their count lands in ctr[7]
+  auto col_rank = [&]() -> int {
+    if (!S.term_major)
+      HIP_TRY(launch_col_rank(S.dict.as<uint64_t>(), C, S.crank.as<uint2>(),
+                              reinterpret_cast<unsigned long long *>(ctr + 7), s));
+    return TFIDF_OK;
+  };
+  if (int rc = col_rank()) return rc;
   // one read of the counters: stats (0-2), error flags (3), long (4) and
-  // non-ASCII (6) document counts, CSR escapes (9) (32-bit counters in the low
-  // halves); read again only when the long path ran
+  // non-ASCII (6) document counts, columns (7), CSR escapes (9) (32-bit
+  // counters in the low halves); read again only when the long path ran
   HIP_TRY(ix->hctr_h.resize(14));                      // pinned: a pageable read is staged by the runtime
   uint64_t *hctr = ix->hctr_h.data();
   HIP_TRY(hipMemcpyAsync(hctr, ctr, 14 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
@@ -1212,6 +1234,7 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
       HIP_TRY(launch_tokenize_long(bp, (int)wgs, s));
     }
     HIP_TRY(hipEventRecord(ix->ev[EV_LONG], s));
+    if (int rc = col_rank()) return rc;
     HIP_TRY(hipMemcpyAsync(hctr, ctr, 10 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIP_TRY(hipStreamSynchronize(s));
   }
@@ -1226,6 +1249,8 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
   S.doc_count = hctr[0];
   S.sum_ttf = hctr[1];
   S.nnz = hctr[2];
+  S.NC = S.term_major ? 0u : (uint32_t)hctr[7];
+  if (!S.term_major) HIP_TRY(S.blk.reserve((size_t)(S.n_blocks + 1) * S.NC * 4 + 16));
   // CSR tf escapes (rare: block-major only for tf >= 2^17): sorted by entry
   // index for the binary searches of the inversion and tfidf_doc_terms
   {
@@ -1270,6 +1295,8 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
   pp.live_map = bp.live_map;
   pp.n_docs = N;
   pp.C = C;
+  pp.NC = S.NC;
+  pp.crank = S.crank.as<uint2>();
   pp.range_shift = S.range_shift;
   pp.n_ranges = S.R;
   pp.n_blocks = S.n_blocks;
@@ -1286,7 +1313,7 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
   pp.post_esc_count = reinterpret_cast<uint32_t *>(ctr + 10);
   pp.post_esc_cap = post_esc_cap;
   pp.sort_spw = 4;
-  if (const char *e = knob("TFIDF_SORT_SPW")) pp.sort_spw = (uint32_t)std::max(1, atoi(e));   // A/B only
+  if (const char *e = knob("TFIDF_SORT_SPW")) pp.sort_spw = (uint32_t)std::max(1, std::min(8, atoi(e)));   // A/B only (<= kSortMaxSpw)
   pp.err = bp.err;
   HIP_TRY(hipEventRecord(ix->ev[EV_D0], s));
   if (S.term_major) {
@@ -1349,10 +1376,12 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
     if (S.n_blocks) {
       HIP_TRY(launch_df_partial(pp, s));
     } else {
-      HIP_TRY(hipMemsetAsync(S.blk.p, 0, (size_t)C * 4, s));
+      HIP_TRY(hipMemsetAsync(S.blk.p, 0, (size_t)S.NC * 4, s));
     }
     HIP_TRY(hipEventRecord(ix->ev[EV_DF], s));
     HIP_TRY(launch_df_sum(pp, s));
+    HIP_TRY(launch_df_slots(S.crank.as<uint2>(), S.blk.as<uint32_t>() + (size_t)S.n_blocks * S.NC, C,
+                            S.sdf.as<uint32_t>(), s));
     if (S.n_blocks) HIP_TRY(launch_row_scan(pp, s));
     HIP_TRY(hipEventRecord(ix->ev[EV_BSCAN], s));
     HIP_TRY(launch_block_base(pp, s));
@@ -1364,8 +1393,9 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
     HIP_TRY(hipStreamWaitEvent(ix->copy_stream, ix->mir_ev[0], 0));
     HIP_TRY(hipMemcpyAsync(S.h_dict.data(), S.dict.p, (size_t)2 * C * 8, hipMemcpyDeviceToHost, ix->copy_stream));
     HIP_TRY(launch_verify_deferred(bp, ix->copy_stream));
-    HIP_TRY(launch_count_nonzero(S.dict.as<uint64_t>(), C, reinterpret_cast<unsigned long long *>(ctr + 7),
-                                 ix->copy_stream));
+    if (S.term_major)       // (block-major: col_rank counted the columns)
+      HIP_TRY(launch_count_nonzero(S.dict.as<uint64_t>(), C, reinterpret_cast<unsigned long long *>(ctr + 7),
+                                   ix->copy_stream));
     HIP_TRY(hipEventRecord(ix->mir_ev[1], ix->copy_stream));
   }
   // host mirrors for query analysis: dictionary keys + df
@@ -1373,6 +1403,10 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
     HIP_TRY(hipMemcpyAsync(S.h_dict.data(), S.dict.p, (size_t)2 * C * 8, hipMemcpyDeviceToHost, s));
   HIP_TRY(hipMemcpyAsync(S.h_df.data(), S.df_dev(), (size_t)C * 4,
                          hipMemcpyDeviceToHost, s));
+  if (!S.term_major) {                                 // slot -> column for query preparation
+    HIP_TRY(S.h_crank.resize((size_t)C / 32 + 1));
+    HIP_TRY(hipMemcpyAsync(S.h_crank.data(), S.crank.p, ((size_t)C / 32 + 1) * 8, hipMemcpyDeviceToHost, s));
+  }
   if (mirror_side) {
     HIP_TRY(hipStreamWaitEvent(s, ix->mir_ev[1], 0));   // mirror, checks and count (side stream)
   } else {
@@ -1380,7 +1414,8 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
     HIP_TRY(launch_verify_deferred(bp, s));
     // occupied dictionary slots counted on the device (ctr[7]) instead of a host
     // pass over the mirror (8 M slots at 2^23 took milliseconds)
-    HIP_TRY(launch_count_nonzero(S.dict.as<uint64_t>(), C, reinterpret_cast<unsigned long long *>(ctr + 7), s));
+    if (S.term_major)
+      HIP_TRY(launch_count_nonzero(S.dict.as<uint64_t>(), C, reinterpret_cast<unsigned long long *>(ctr + 7), s));
   }
   uint64_t tail[8];              // ctr[3] error flags .. ctr[7] occupied slots, [8] malformed, [10] posting escapes
   HIP_TRY(hipMemcpyAsync(tail, ctr + 3, sizeof tail, hipMemcpyDeviceToHost, s));
@@ -1544,7 +1579,7 @@ extern "C" int tfidf_stats(const tfidf_index *ix, tfidf_index_stats *out) {
   uint64_t tot = staged_bytes;
   if (S) {
     const DevBuf *bufs[] = {&S->dict, &S->csr, &S->csr_esc, &S->doc_len, &S->doc_nuniq, &S->doc_norm,
-                            &S->rsplit, &S->blk, &S->bbase, &S->post, &S->toff, &S->tdf};
+                            &S->rsplit, &S->blk, &S->bbase, &S->post, &S->toff, &S->tdf, &S->crank, &S->sdf};
     for (const DevBuf *b : bufs) tot += b->bytes;
   }
   out->device_bytes = tot;
@@ -1608,7 +1643,8 @@ static uint32_t lookup_term(Snapshot &S, const std::string &t) {
 }
 
 struct PreparedQuery {
-  std::vector<uint32_t> slot;
+  std::vector<uint32_t> slot;    // per term: what the scorers index it by (Snapshot::col_of)
+  std::vector<uint32_t> ldf;     // per term: the shard's own df
   std::vector<float> w;
   std::vector<uint32_t> role;    // role << 24 | MUST clause index
   uint32_t meta = 0;             // MUST clause count | has MUST_NOT << 31
@@ -1618,7 +1654,7 @@ struct PreparedQuery {
 static uint64_t hits_bound(const Snapshot &S, const PreparedQuery &pq) {
   uint64_t b = 0;
   for (size_t i = 0; i < pq.slot.size(); i++)
-    if ((pq.role[i] >> 24) != kRoleNot) b += S.h_df[pq.slot[i]];
+    if ((pq.role[i] >> 24) != kRoleNot) b += pq.ldf[i];
   return b;
 }
 
@@ -1652,7 +1688,8 @@ static int prepare_query(Snapshot &S, StatsView &V, const uint8_t *q, uint64_t n
     if (t.role == kRoleMust) present[t.group]++;
     if (t.role == kRoleShould) n_should++;
     if (t.role == kRoleNot) has_not = true;
-    pq->slot.push_back(s);
+    pq->slot.push_back(S.col_of(s));
+    pq->ldf.push_back(S.h_df[s]);
     pq->w.push_back(wv);
     pq->role.push_back(t.role << 24 | t.group);
   }
@@ -1660,6 +1697,7 @@ static int prepare_query(Snapshot &S, StatsView &V, const uint8_t *q, uint64_t n
   for (uint32_t c : present) empty |= c == 0;
   if (empty) {
     pq->slot.clear();
+    pq->ldf.clear();
     pq->w.clear();
     pq->role.clear();
     return TFIDF_OK;
@@ -1670,11 +1708,12 @@ static int prepare_query(Snapshot &S, StatsView &V, const uint8_t *q, uint64_t n
 
 // Batch of prepared queries in device layout.
 struct QueryBatch {
-  std::vector<uint32_t> off{0}, slot, role, meta;
+  std::vector<uint32_t> off{0}, slot, role, meta, ldf;
   std::vector<float> w;
   bool ops = false;                // some query has MUST / MUST_NOT clauses
   void add(const PreparedQuery &pq) {
     slot.insert(slot.end(), pq.slot.begin(), pq.slot.end());
+    ldf.insert(ldf.end(), pq.ldf.begin(), pq.ldf.end());
     w.insert(w.end(), pq.w.begin(), pq.w.end());
     role.insert(role.end(), pq.role.begin(), pq.role.end());
     off.push_back((uint32_t)slot.size());
@@ -1756,6 +1795,7 @@ static int prepare_batch(tfidf_index *ix, Snapshot &S, StatsView &V, const uint8
   size_t ns = 0;
   for (const PreparedQuery &pq : pqs) ns += pq.slot.size();
   qb->slot.reserve(ns);
+  qb->ldf.reserve(ns);
   qb->w.reserve(ns);
   qb->role.reserve(ns);
   qb->off.reserve(n_q + 1);
@@ -1797,7 +1837,7 @@ static int run_scoring(tfidf_index *ix, Snapshot &S, StatsView &V, SearchCtx &X,
     for (uint32_t q = 0; q < n_q && unit_path; q++) {
       if (qoff[q + 1] - qoff[q] > kUnitMaxTerms) unit_path = false;
       for (uint32_t t = qoff[q]; t < qoff[q + 1]; t++)
-        if (slots[t] != kInvalidSlot) P[q] += S.h_df[slots[t]];
+        if (slots[t] != kInvalidSlot) P[q] += qb.ldf[t];
       T += P[q];
     }
     // light queries (at most light_post postings per block on average): wave
@@ -1859,7 +1899,7 @@ static int run_scoring(tfidf_index *ix, Snapshot &S, StatsView &V, SearchCtx &X,
   qp.bbase = S.bbase.as<uint64_t>();
   qp.blk = S.blk.as<uint32_t>();
   qp.toff = S.term_major ? S.toff.as<uint64_t>() : nullptr;
-  qp.C = S.C;
+  qp.C = S.qcols();
   qp.n_blocks = S.n_blocks;
   qp.n_docs = S.n_docs;
   qp.cache = V.cache.as<float>();
@@ -1997,7 +2037,7 @@ static int search_on(tfidf_index *ix, Snapshot &S, StatsView &V, const uint8_t *
     qp.bbase = S.bbase.as<uint64_t>();
     qp.blk = S.blk.as<uint32_t>();
     qp.toff = S.term_major ? S.toff.as<uint64_t>() : nullptr;
-    qp.C = S.C;
+    qp.C = S.qcols();
     qp.n_blocks = S.n_blocks;
     qp.n_docs = S.n_docs;
     qp.cache = V.cache.as<float>();

@@ -44,7 +44,10 @@ constexpr uint64_t kLoHashed = 1ull << 55;      // in lo: more than 16 bytes (hi
 // bytes, or a hash masked with 0x7F bytes).  Longer non-ASCII terms are hashed.
 constexpr uint64_t kLoUniExact = 1ull << 47;
 constexpr uint32_t kExactUniChars = 14;
-constexpr uint32_t kRangeBits = 15;             // 32768 dictionary slots per LDS range tile
+// Dictionary range of the block-major inversion: a (doc block, range) tile
+// counts its slots in 16-bit LDS counters (a block holds 8192 documents), so
+// 65536 slots fill 128 KiB (round 6; was 32768 32-bit counters).
+constexpr uint32_t kRangeBits = 16;
 constexpr uint32_t kRangeSlots = 1u << kRangeBits;
 constexpr uint32_t kBlockDocs = 8192;           // doc block of the inverted index / scorer
 constexpr uint32_t kInvalidSlot = 0xFFFFFFFFu;

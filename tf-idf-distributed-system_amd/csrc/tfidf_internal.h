@@ -213,11 +213,13 @@ struct PostingParams {
   const uint64_t *csr_esc;    // sorted escape list (csr_put)
   uint64_t n_esc;
   const uint8_t *doc_norm;
-  uint32_t *blk;              // [(n_blocks + 1) * C]: per-block term counts -> per-block exclusive
-                              // offsets over slots; row n_blocks = df
+  uint32_t NC;                // columns: occupied dictionary slots (block-major: num_terms)
+  const uint2 *crank;         // [C / 32 + 1] {occupancy bits, occupied slots before} per 32 slots (col_rank)
+  uint32_t *blk;              // [(n_blocks + 1) * NC]: per-block term counts -> per-block exclusive
+                              // offsets over columns; row n_blocks = df per column
   uint64_t *bbase;            // [n_blocks + 1]: first posting of each block (block-major postings)
-  uint32_t *post;             // [nnz] block-major postings (post_word); block b, slot s at
-                              // bbase[b] + blk[b][s]
+  uint32_t *post;             // [nnz] block-major postings (post_word); block b, column c at
+                              // bbase[b] + blk[b][c]
   uint64_t *post_esc;         // (posting index << 24) | tf for tf >= kPostTfEsc
   uint32_t *post_esc_count;
   uint64_t post_esc_cap;
@@ -282,6 +284,9 @@ hipError_t launch_df_sum(const PostingParams &p, hipStream_t s);
 hipError_t launch_row_scan(const PostingParams &p, hipStream_t s);
 hipError_t launch_block_base(const PostingParams &p, hipStream_t s);
 hipError_t launch_count_nonzero(const uint64_t *a, uint32_t n, unsigned long long *out, hipStream_t s);
+// block-major columns: crank over the final dictionary (total -> *n_cols), per-slot df from the column df
+hipError_t launch_col_rank(const uint64_t *dict_lo, uint32_t C, uint2 *crank, unsigned long long *n_cols, hipStream_t s);
+hipError_t launch_df_slots(const uint2 *crank, const uint32_t *df_col, uint32_t C, uint32_t *df_slot, hipStream_t s);
 hipError_t launch_scatter(const PostingParams &p, hipStream_t s);
 
 // --- term-major inversion for large vocabularies (kernels_term.hip) ---
@@ -321,14 +326,14 @@ struct QueryParams {
   const uint64_t *post_esc;   // block-major tf escapes, sorted
   uint64_t n_post_esc;
   const uint64_t *bbase;      // [n_blocks + 1] first posting of each block
-  const uint32_t *blk;        // per-block exclusive offsets over slots [n_blocks * C]
+  const uint32_t *blk;        // per-block exclusive offsets over columns [n_blocks * C]
   const uint64_t *toff;       // term-major layout: [C + 1] first posting per slot (nullptr = block-major)
-  uint32_t C;
+  uint32_t C;                 // block-major: columns (num_terms); term-major: dictionary slots
   uint32_t n_blocks;
   uint64_t n_docs;
   const float *cache;         // 256 floats (BM25 norm cache)
   const uint32_t *q_off;      // [n_q + 1] into q_slot / q_w
-  const uint32_t *q_slot;     // dictionary slot per query term (kInvalidSlot = absent)
+  const uint32_t *q_slot;     // per query term: block-major column / term-major slot (kInvalidSlot = absent)
   const float *q_w;           // BM25 weight per query term (boost * idf)
   const uint32_t *q_role;     // per query term: role << 24 | MUST clause index (kRole*, tfidf_common.h)
   const uint32_t *q_meta;     // per query: MUST clause count | has MUST_NOT << 31 (0 = plain disjunction)
