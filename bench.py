@@ -68,6 +68,9 @@ def parse():
     ap.add_argument("--inversion", choices=("auto", "block", "term"), default="auto")
     ap.add_argument("--unicode-every", type=int, default=0,
                     help="one non-ASCII word per this many bytes of every document (book-like text)")
+    ap.add_argument("--prose", type=float, default=0.0,
+                    help="prose typography (curly quotes, apostrophes, dashes, accented and capital letters) "
+                         "at this multiple of synth.DeviceCorpus.PROSE's rates (0 = plain synthetic words)")
     ap.add_argument("--unicode-frac", type=float, default=0.0,
                     help="fraction of documents made non-ASCII (Unicode tokenizer path); 0 = the cfg-2 corpus")
     ap.add_argument("--no-e2e", dest="e2e", action="store_false",
@@ -334,6 +337,7 @@ def main():
     corpus = synth.DeviceCorpus(n_docs, V=args.vocab, len_min=args.len_min, len_max=args.len_max,
                                 doc_base=doc_base, device=local)
     n_unicode = corpus.inject_unicode(args.unicode_frac) + corpus.inject_unicode_every(args.unicode_every)
+    n_prose = corpus.inject_prose(args.prose)
     cap = args.cap_log2 or default_cap(args.vocab)
     inv = {"auto": 0, "block": 1, "term": 2}[args.inversion]
     idx = ShardIndex(device=local, vocab_capacity_log2=cap, inversion=inv,
@@ -456,7 +460,11 @@ def main():
         "global_exchange_ms_per_step": exch[0] * 1e3 / args.steps if dist_on else None,
         "global_exchange_frac_of_step": (exch[0] / elapsed) if dist_on else None,
         "long_docs": st["long_docs"],
+        "long_chunked": st["long_chunked"],
+        "engine_unicode_docs": st["unicode_docs"],
+        "engine_unicode_wave_docs": st["unicode_wave_docs"],
         "unicode_docs": n_unicode,
+        "prose_words": n_prose,
         "tokenizer_docs_per_window": st["pack_docs"],
         "pack_retried_docs": st["pack_retried"],
     }

@@ -33,7 +33,17 @@ WORDS = ["café", "naïve", "über", "mañana", "straße", "smørrebrød", "krak
 JOIN = ["l'été", "café's", "end.é", "é.end", "a.é.b", "3,é", "é3,5", "__é__", "_é", "é_", "naïve_user",
         "über.cool", "a:é", "é:a", "1.é", "é'1", "ab;é;cd", "a_1_é", "Café", "CAFÉ".lower(), "NAÏVE".lower(),
         "CaFé", "x.y.ü", "ü,3", "a'b'é"]
-DECLINE = ["É", "Über", "中文", "カタカナ", "שלום", "é́", "😀", "İ", "ΣΟΦΙΑ", "­"]
+DECLINE = ["中文", "カタカナ", "שלום", "é́", "😀", "İ", "­", "١٢٣", "a\u202fb", "©", "™", "x\u200dy", "‿"]
+# Round 6, real prose: upper-case letters whose lower case has the same UTF-8
+# length (lowered in the staged window), separators of class Other (curly
+# double quotes, dashes, ellipsis, no-break space, guillemets: spaces), and
+# non-ASCII mid chars (’ ‘ · ‧ ․ ＇: joined as ASCII ' . : are) — next to
+# letters, digits, '_', ASCII joiners, each other, and at token edges.
+PROSE = ["don’t", "it’s", "‘quoted’", "“quote”", "a—b", "x–y", "wait…", "non\u00a0breaking", "«guillemets»",
+         "É", "Über", "ΣΟΦΙΑ", "École", "ÀÉÎÕÜ", "l’été", "3’4", "a’’b", "’tis", "rock’n’roll", "o’", "’",
+         "a·b", "1·2", "x‧y", "a’1", "1’a", "a’.b", "a.’b", "_’a", "a’_", "Ça va", "QUÉBEC", "naïve—ok",
+         "end.”", "“start", "a\u00a0’b", "‘a’", "9’", "’9", "A’B", "Ünïcödé’s", "x․y", "1․5", "x＇y", "a”b",
+         "“É”", "—", "…", "a…b", "ΑΒΓ’δ", "Straße’s", "‘’", "a‘b", "1‘2", "a·1", "I’m", "O’NEIL", "L’ÉTÉ"]
 SEPS = [" ", " ", "\n", ", ", ". ", " - ", "(", ") ", "\t", "; ", ": ", "'"]
 
 
@@ -97,7 +107,7 @@ def test_same_term_across_paths():
     """A term spelled in a document the wave rules take and in one they decline
     (an upper-case É elsewhere in it) is one dictionary term: df 2, one
     posting list."""
-    texts = [b"caf\xc3\xa9 au lait", "CAFÉ noir É".encode(), "Café crème".encode(), "café".encode() * 3]
+    texts = [b"caf\xc3\xa9 au lait", "CAFÉ noir 中".encode(), "Café crème".encode(), "café".encode() * 3]
     g, o = build_pair(texts)
     st = g.stats()
     assert st["unicode_wave_docs"] >= 2 and st["unicode_docs"] - st["unicode_wave_docs"] >= 1
@@ -144,6 +154,73 @@ def test_books_with_simple_non_ascii_words_equal_oracle(monkeypatch, uniwave):
     g, o = build_pair(texts)
     check(g, o, texts)
     for q in ["café", "naïve", "straße", "москва", "l'été", "CAFÉ", "中文", synth.word(9).decode()]:
+        qb = q.encode()
+        for k in (0, 10):
+            assert_hits_equal(g.search(qb, k), o.search(qb, k))
+    g.close()
+    o.close()
+
+
+def prose_edge_docs():
+    docs = []
+    for w in PROSE:
+        docs += [w, w + " tail", "head " + w, w + w, w + "." + w, "x" + w + "y", "1" + w + "2"]
+    # each prose char across every lane edge and the window's end
+    for ch in ["’", "—", "“", "\u00a0", "É", "·", "…", "Ω"]:
+        for pad in range(58, 71):
+            docs.append("a" * pad + ch + "b" * 12)
+            docs.append("3" * pad + ch + "4" * 5)
+            docs.append("x " * (pad // 2) + "z" + ch + "z")
+    docs.append(("word " * 800)[:4088] + "’s")
+    return [d.encode() for d in docs]
+
+
+@pytest.mark.parametrize("uniwave", [True, False])
+def test_prose_docs_equal_oracle(monkeypatch, uniwave):
+    """Real prose (round 6): curly quotes and apostrophes, dashes, no-break
+    spaces and capitalised accented letters take the wave rules too; declined
+    characters still go to the Unicode wave path."""
+    if not uniwave:
+        monkeypatch.setenv("TFIDF_NO_UNIWAVE", "1")
+    rng = random.Random(97)
+    texts = prose_edge_docs()
+    prose = [doc(rng, rng.randint(20, 500), rng.randint(1, 12), PROSE + WORDS + JOIN) for _ in range(900)]
+    declined = [doc(rng, rng.randint(20, 300), 2, PROSE) + " 中文".encode() for _ in range(100)]
+    texts += prose + declined
+    texts += synth.corpus(200, V=3000, len_min=50, len_max=400)
+    rng.shuffle(texts)
+    g, o = build_pair(texts)
+    st = g.stats()
+    if uniwave:
+        assert st["unicode_wave_docs"] >= 900
+        assert st["unicode_docs"] - st["unicode_wave_docs"] >= 100
+    else:
+        assert st["unicode_wave_docs"] == 0
+    check(g, o, texts)
+    for q in ["don’t", "l’été", "québec", "École", "rock’n’roll", "a·b", "3’4", "“quote”", "Über", "ΣΟΦΙΑ",
+              "o’neil", "wait", "naïve", "i’m"]:
+        qb = q.encode()
+        for k in (0, 10):
+            assert_hits_equal(g.search(qb, k), o.search(qb, k))
+    g.close()
+    o.close()
+
+
+@pytest.mark.parametrize("uniwave", [True, False])
+def test_prose_books_equal_oracle(monkeypatch, uniwave):
+    """Book-sized prose (the chunk units): no book goes to the long path when
+    its non-ASCII text is prose."""
+    if not uniwave:
+        monkeypatch.setenv("TFIDF_NO_UNIWAVE", "1")
+    rng = random.Random(31)
+    texts = [doc(rng, rng.randint(4000, 12000), rng.randint(40, 120), PROSE + WORDS) for _ in range(16)]
+    texts += [doc(rng, rng.randint(20, 200), 2, PROSE) for _ in range(100)]
+    g, o = build_pair(texts)
+    check(g, o, texts)
+    if uniwave:
+        st = g.stats()
+        assert st["long_chunked"] == st["long_docs"] >= 16          # every book by its chunk units
+    for q in ["don’t", "l’été", "québec", "rock’n’roll", synth.word(9).decode()]:
         qb = q.encode()
         for k in (0, 10):
             assert_hits_equal(g.search(qb, k), o.search(qb, k))

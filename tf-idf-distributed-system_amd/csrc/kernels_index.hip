@@ -445,9 +445,14 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 // the document were zeroed at staging (class Other).  Wave-uniform flags:
 // *bad = a byte >= 0x80 in the document, *under = a '_' in the document.
 // PACK: *wbase = the same mask before the joiner rules (letters, digits, '_').
+// UNI (round 6): jl / jd = this lane's non-ASCII mid chars (lead byte bits,
+// uni_window_prose) that join letters (MidLetter, MidNumLet) / digits
+// (MidNum, MidNumLet): their bytes are classified as Other, then each one
+// joins its token when both neighbour chars are letters (WB6/7) / digits
+// (WB11/12) — the ASCII rule of a single mid char, with a 2-3 byte char.
 template <bool PACK, bool UNI = false>
 __device__ __forceinline__ uint64_t lane_word_mask(const uint8_t *text, uint32_t lane, bool *bad, bool *under,
-                                                   uint64_t *wbase, bool *upper) {
+                                                   uint64_t *wbase, bool *upper, uint64_t jl = 0, uint64_t jd = 0) {
   uint32_t x[16], hb[16];
   {
     const uint4 *t = reinterpret_cast<const uint4 *>(text + lane * 64);
@@ -455,6 +460,26 @@ __device__ __forceinline__ uint64_t lane_word_mask(const uint8_t *text, uint32_t
     for (int k = 0; k < 4; k++) {
       const uint4 v = t[k];
       x[4 * k] = v.x; x[4 * k + 1] = v.y; x[4 * k + 2] = v.z; x[4 * k + 3] = v.w;
+    }
+  }
+  // UNI: the mid chars' bytes (leads of 3-byte chars: 111xxxxx) read as class Other
+  uint64_t mid3 = 0;
+  const bool anymid = UNI && __any((jl | jd) != 0);
+  if (anymid) {
+    uint64_t t3 = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) t3 |= (uint64_t)swar_nib(x[i] & (x[i] << 1) & (x[i] << 2) & 0x80808080u) << (4 * i);
+    const uint64_t m = jl | jd;
+    mid3 = m & t3;
+    uint64_t ex = m | (m << 1) | (mid3 << 2);
+    const uint64_t spill = (m >> 63) | (mid3 >> 62);               // continuation bytes in the next lane
+    // (every cross-lane read unconditional: a lane outside EXEC reads as 0 to the others)
+    const uint32_t sp = (uint32_t)__shfl_up((int)(uint32_t)spill, 1, 64);
+    ex |= lane ? (uint64_t)sp : 0ull;
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const uint32_t nb = (uint32_t)(ex >> (4 * i)) & 0xFu;
+      x[i] &= ~((nb & 1u) * 0xFFu | (nb & 2u) * 0x7F80u | (nb & 4u) * 0x3FC000u | (nb & 8u) * 0x1FE00000u);
     }
   }
   // pass 1: letter/digit flags (neighbour context), non-ASCII, joiner presence
@@ -501,6 +526,38 @@ __device__ __forceinline__ uint64_t lane_word_mask(const uint8_t *text, uint32_t
       c |= (ml & both) | (mn & (both << 1));
     }
     W |= (uint64_t)swar_nib(c & 0x80808080u) << (4 * i);
+  }
+  if (anymid) {
+    // letter / digit bits of the lane's bytes, and of the neighbours across lanes
+    uint64_t Lm = 0, Dm = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      Lm |= (uint64_t)swar_nib(LD[i] & 0x80808080u) << (4 * i);
+      Dm |= (uint64_t)swar_nib((LD[i] << 1) & 0x80808080u) << (4 * i);
+    }
+    const uint32_t pl0 = (uint32_t)__shfl_up((int)(uint32_t)(Lm >> 63), 1, 64);
+    const uint32_t pd0 = (uint32_t)__shfl_up((int)(uint32_t)(Dm >> 63), 1, 64);
+    const uint32_t nl0 = (uint32_t)__shfl_down((int)(uint32_t)Lm, 1, 64);
+    const uint32_t nd0 = (uint32_t)__shfl_down((int)(uint32_t)Dm, 1, 64);
+    const uint32_t pl = lane ? pl0 & 1u : 0u, pd = lane ? pd0 & 1u : 0u;
+    const uint32_t nl = lane < 63 ? nl0 & 7u : 0u, nd = lane < 63 ? nd0 & 7u : 0u;
+    uint64_t m = jl | jd, add = 0;
+    uint32_t carry = 0;
+    while (m) {
+      const uint32_t b = (uint32_t)__builtin_ctzll(m);
+      m &= m - 1;
+      const uint32_t len = ((mid3 >> b) & 1u) ? 3u : 2u, a = b + len;
+      const uint32_t lb = b ? (uint32_t)(Lm >> (b - 1)) & 1u : pl, db = b ? (uint32_t)(Dm >> (b - 1)) & 1u : pd;
+      const uint32_t la = a < 64 ? (uint32_t)(Lm >> a) & 1u : (nl >> (a - 64)) & 1u;
+      const uint32_t da = a < 64 ? (uint32_t)(Dm >> a) & 1u : (nd >> (a - 64)) & 1u;
+      const bool join = (((jl >> b) & 1u) && lb && la) || (((jd >> b) & 1u) && db && da);
+      if (join) {
+        add |= ((1ull << len) - 1) << b;
+        if (a > 64) carry |= (1u << (a - 64)) - 1u;
+      }
+    }
+    const uint32_t cin = (uint32_t)__shfl_up((int)carry, 1, 64);
+    W |= add | (uint64_t)(lane ? cin : 0u);
   }
   *bad = __any((badacc & 0x80808080u) != 0);
   *under = __any(us != 0);
@@ -1317,19 +1374,32 @@ __device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p
 // array is an argument: a called function has no kernarg pointer (TFIDF_COLD).
 __device__ __noinline__ void flag_unicode(uint32_t *flags, uint64_t d) { flags[d] = 1u; }
 
-// UNI (round 5): can the wave rules take this document?  Yes when every
-// non-ASCII char is well-formed UTF-8, of word-break class ALetter (UAX#29:
-// the class of the ASCII letters, so the ASCII rules with its bytes read as
-// letters give the scanner's tokens) and its own lower case (so ASCII
-// lower-casing decides term identity in the document's table), and no
-// continuation byte is an orphan.  Anything else (Han, Katakana, Hebrew,
-// combining marks, upper case, malformed bytes) stays flagged for
-// k_tokenize_uwave.  One char: its lead byte and the three after it in w
-// (little-endian), avail = bytes of the window from the lead on; returns its
-// byte length, 0 if it does not qualify.  (Bytes come in registers: a
-// generic pointer into LDS would be flat loads, one dependent round trip per
-// byte — 4.6 ms at cfg 2 with every document non-ASCII.)
-__device__ __noinline__ uint32_t uni_simple_char(uint32_t w, uint32_t avail) {
+// UNI (rounds 5-6): can the wave rules take this document?  Every non-ASCII
+// char must be well-formed UTF-8 (no orphan continuation bytes) and one of
+//   * an ALetter that is its own lower case (é ü ñ ß α я …): UAX#29 treats it
+//     as it treats an ASCII letter (ALetter is the ASCII letters' class), so
+//     the ASCII rules with its bytes read as letters give the scanner's tokens;
+//   * an ALetter whose lower case (JDK Character.toLowerCase) has the same
+//     UTF-8 length and is such a letter (É Ö Ç Σ Я …): its bytes are
+//     lowered in the staged window, so term identity is again decided by
+//     ASCII lower-casing (round 6);
+//   * a char of class Other (no-break space, curly double quotes, dashes,
+//     ellipsis, guillemets …): a break on both sides, exactly as an ASCII
+//     space — its bytes become spaces in the staged window (round 6);
+//   * MidLetter / MidNum / MidNumLet (’ ‘ · …): kept in the window, read as
+//     class Other by the classifier, and joined afterwards where UAX#29 joins
+//     them (WB6/7: a letter on both sides; WB11/12: a digit on both sides;
+//     lane_word_mask) (round 6).
+// Anything else (Han, Katakana, Hebrew, combining marks, non-ASCII digits or
+// ExtendNumLet, emoji, malformed bytes) stays flagged for k_tokenize_uwave.
+// One char through the tables: its lead byte and the three after it in w
+// (little-endian), avail = bytes of the window from the lead on; returns
+// kind | byte length << 4 | (kPrUpper) the lower case's UTF-8 bytes << 8.
+// (Bytes come in registers: a generic pointer into LDS would be flat loads,
+// one dependent round trip per byte — 4.6 ms at cfg 2 with every document
+// non-ASCII.)
+enum : uint32_t { kPrNo = 0, kPrLetter, kPrUpper, kPrSep, kPrMidL, kPrMidN, kPrMidNL };
+__device__ __noinline__ uint32_t uni_prose_char(uint32_t w, uint32_t avail) {
   const uint32_t b0 = w & 0xFFu, b1 = (w >> 8) & 0xFFu, b2 = (w >> 16) & 0xFFu, b3 = w >> 24;
   auto cont = [](uint32_t b, uint32_t lo, uint32_t hi) { return b >= lo && b <= hi; };
   uint32_t cp, len;
@@ -1345,45 +1415,69 @@ __device__ __noinline__ uint32_t uni_simple_char(uint32_t w, uint32_t avail) {
     cp = ((b0 & 0x07u) << 18) | ((b1 & 0x3Fu) << 12) | ((b2 & 0x3Fu) << 6) | (b3 & 0x3Fu);
     len = 4;
   } else {
-    return 0;
+    return kPrNo;
   }
   // both table walks issued together (index loads, then data loads)
   const uint32_t ci = kUcClassIndex[cp >> 8], li = kUcLowerIndex[cp >> 8];
   const uint32_t cls = kUcClassData[ci * 256u + (cp & 255u)];
   const int32_t dl = kUcLowerData[li * 256u + (cp & 255u)];
-  return (cls == kUcALetter && dl == 0) ? len : 0u;
+  if (cls == kUcALetter) {
+    if (dl == 0) return kPrLetter | (len << 4);
+    const uint32_t lc = (uint32_t)((int32_t)cp + dl);
+    const uint32_t ll = lc < 0x80u ? 1u : (lc < 0x800u ? 2u : (lc < 0x10000u ? 3u : 4u));
+    if (ll != len || len > 3 || uc_class(lc) != kUcALetter || uc_lower(lc) != lc) return kPrNo;
+    const uint32_t by = len == 2 ? ((0xC0u | (lc >> 6)) | ((0x80u | (lc & 0x3Fu)) << 8))
+                                 : ((0xE0u | (lc >> 12)) | ((0x80u | ((lc >> 6) & 0x3Fu)) << 8) |
+                                    ((0x80u | (lc & 0x3Fu)) << 16));
+    return kPrUpper | (len << 4) | (by << 8);
+  }
+  if (cls == kUcOther) return kPrSep | (len << 4);
+  if (cls == kUcMidLetter) return kPrMidL | (len << 4);
+  if (cls == kUcMidNum) return kPrMidN | (len << 4);
+  if (cls == kUcMidNumLet) return kPrMidNL | (len << 4);
+  return kPrNo;
 }
 
-// Units: PACK = false, one document per unit (documents 0..n_docs-1, or the
-// doc_list entries); PACK = true, unit u = documents [u * pack, u * pack + pack)
-// sharing one window.  A pack that cannot take the packed path (window or
-// token/term capacity, non-contiguous sources, an empty or non-ASCII document)
-// sends its documents to retry_list for a PACK = false pass.
-#ifndef TFIDF_WAVE_XCD
-#define TFIDF_WAVE_XCD 1
-#endif
-// UNI: which 2-byte chars (U+0080..U+07FF) uni_simple_char passes, one bit
-// each: lane l returns U+0080 + 32 l .. + 31 (lanes >= 60: none).
-__device__ __forceinline__ uint32_t uni_simple2_bitmap(uint32_t lane) {
-  uint32_t bm = 0;
+// UNI: per-wave bitmaps of the common non-ASCII chars, so most of them take
+// no table walk: 2-byte chars (U+0080..U+07FF; lane l holds U+0080 + 32 l ..
+// + 31, lanes >= 60 none) that are ALetters and their own lower case
+// (simple2) or of class Other (other2); General Punctuation U+2000..U+207F
+// (curly quotes, dashes, ellipsis) two bits each in lanes 0..7 (punct):
+// 1 class Other, 2 MidNumLet, 3 MidLetter, 0 through the tables.
+__device__ __forceinline__ void uni_prose_bitmaps(uint32_t lane, uint32_t *simple2, uint32_t *other2, uint32_t *punct) {
+  uint32_t bm = 0, om = 0;
   const uint32_t c0 = min(0x80u + 32u * lane, 0x7E0u);
   const uint32_t ci = kUcClassIndex[c0 >> 8], li = kUcLowerIndex[c0 >> 8];   // 32-aligned: one table row
 #pragma unroll 8
   for (uint32_t b = 0; b < 32; b++) {
     const uint32_t cp = c0 + b;
-    const bool ok = kUcClassData[ci * 256u + (cp & 255u)] == kUcALetter && kUcLowerData[li * 256u + (cp & 255u)] == 0;
-    bm |= (ok ? 1u : 0u) << b;
+    const uint32_t cls = kUcClassData[ci * 256u + (cp & 255u)];
+    bm |= (cls == kUcALetter && kUcLowerData[li * 256u + (cp & 255u)] == 0 ? 1u : 0u) << b;
+    om |= (cls == kUcOther ? 1u : 0u) << b;
   }
-  return lane >= 60 ? 0u : bm;
+  *simple2 = lane >= 60 ? 0u : bm;
+  *other2 = lane >= 60 ? 0u : om;
+  uint32_t pm = 0;
+  const uint32_t g0 = 0x2000u + 16u * (lane & 7u), gi = kUcClassIndex[g0 >> 8];
+#pragma unroll 4
+  for (uint32_t b = 0; b < 16; b++) {
+    const uint32_t cls = kUcClassData[gi * 256u + ((g0 + b) & 255u)];
+    const uint32_t code = cls == kUcOther ? 1u : (cls == kUcMidNumLet ? 2u : (cls == kUcMidLetter ? 3u : 0u));
+    pm |= code << (2 * b);
+  }
+  *punct = lane < 8 ? pm : 0u;
 }
 
-// UNI: does the staged window (LDS bytes [0, wl), zero past wl) pass
-// uni_simple_char?  Lane l checks window bytes [64 l, 64 l + 64): its lead
-// bytes (11xxxxxx) one per step (2-byte chars from the wave's bitmap simple2,
-// lane l holding U+0080 + 32 l .. + 31; the others through the tables), and
-// the wave's continuation bytes (10xxxxxx) must be exactly those the leads
-// claim (no orphans).  Wave-uniform result.
-__device__ __forceinline__ bool uni_window_simple(const uint8_t *text, uint32_t wl, uint32_t lane, uint32_t simple2) {
+// UNI: does the staged window (LDS bytes [0, wl), zero past wl) pass (see
+// uni_prose_char)?  Lane l checks window bytes [64 l, 64 l + 64): its lead
+// bytes (11xxxxxx) one per step, common chars from the wave's bitmaps, the
+// others through the tables, and the wave's continuation bytes (10xxxxxx)
+// must be exactly those the leads claim (no orphans).  On the way separators
+// become spaces and upper-case letters their lower case in the window; the
+// lane's mid chars (lead bits within its 64 bytes) that join letters / digits
+// go to *jl / *jd for the classifier.  Wave-uniform result.
+__device__ __forceinline__ bool uni_window_prose(uint8_t *text, uint32_t wl, uint32_t lane, uint32_t simple2,
+                                                 uint32_t other2, uint32_t punct, uint64_t *jl, uint64_t *jd) {
   const uint32_t *seg = reinterpret_cast<const uint32_t *>(text + 64 * lane);
   uint64_t lead = 0;
   uint32_t ncont = 0;
@@ -1396,25 +1490,53 @@ __device__ __forceinline__ bool uni_window_simple(const uint8_t *text, uint32_t 
   const uint32_t *tw = reinterpret_cast<const uint32_t *>(text);
   bool ok = true;
   uint32_t claimed = 0;
+  uint64_t ml = 0, mn = 0;
   while (__any(lead != 0)) {                            // one lead per lane per step
     const bool has = lead != 0;
-    const uint32_t pos = 64 * lane + (has ? (uint32_t)__builtin_ctzll(lead) : 0u);
+    const uint32_t bt = has ? (uint32_t)__builtin_ctzll(lead) : 0u, pos = 64 * lane + bt;
     lead &= lead - 1;
     const uint32_t w = __builtin_amdgcn_alignbyte(tw[(pos >> 2) + 1], tw[pos >> 2], pos & 3);
-    const uint32_t b0 = w & 0xFFu, b1 = (w >> 8) & 0xFFu;
-    // 2-byte chars (U+0080..U+07FF: Latin, Greek, Cyrillic, ...) from the
-    // wave's bitmap, the others through the tables
+    const uint32_t b0 = w & 0xFFu, b1 = (w >> 8) & 0xFFu, b2 = (w >> 16) & 0xFFu;
     const bool two = has && b0 >= 0xC2u && b0 < 0xE0u && (b1 & 0xC0u) == 0x80u && wl - pos >= 2;
-    const uint32_t cp = ((b0 & 0x1Fu) << 6) | (b1 & 0x3Fu);
-    const uint32_t bits = (uint32_t)__shfl((int)simple2, two ? (int)((cp - 0x80u) >> 5) : 0, 64);
-    uint32_t len = 0;
-    if (two) len = ((bits >> (cp & 31u)) & 1u) ? 2u : 0u;
-    else if (has) len = uni_simple_char(w, wl - pos);
-    ok &= !has || len != 0;
+    const bool gp = has && b0 == 0xE2u && (b1 == 0x80u || b1 == 0x81u) && (b2 & 0xC0u) == 0x80u && wl - pos >= 3;
+    const uint32_t cp = ((b0 & 0x1Fu) << 6) | (b1 & 0x3Fu), gi = ((b1 & 1u) << 6) | (b2 & 0x3Fu);
+    const int src2 = two ? (int)((cp - 0x80u) >> 5) : 0;
+    const uint32_t sb = (uint32_t)__shfl((int)simple2, src2, 64), ob = (uint32_t)__shfl((int)other2, src2, 64);
+    const uint32_t pb = (uint32_t)__shfl((int)punct, gp ? (int)(gi >> 4) : 0, 64);
+    const uint32_t pc = (pb >> (2 * (gi & 15u))) & 3u;
+    uint32_t kind = kPrNo, len = 0, lw = 0;
+    if (two && ((sb >> (cp & 31u)) & 1u)) { kind = kPrLetter; len = 2; }
+    else if (two && ((ob >> (cp & 31u)) & 1u)) { kind = kPrSep; len = 2; }
+    else if (gp && pc) { kind = pc == 1u ? kPrSep : (pc == 2u ? kPrMidNL : kPrMidL); len = 3; }
+    else if (has) {
+      const uint32_t r = uni_prose_char(w, wl - pos);
+      kind = r & 15u;
+      len = (r >> 4) & 15u;
+      lw = r >> 8;
+    }
+    ok &= !has || kind != kPrNo;
+    if (kind == kPrSep)
+      for (uint32_t i = 0; i < len; i++) text[pos + i] = 0x20u;
+    else if (kind == kPrUpper)
+      for (uint32_t i = 0; i < len; i++) text[pos + i] = (uint8_t)(lw >> (8 * i));
+    const uint64_t bit = 1ull << bt;
+    if (kind == kPrMidL || kind == kPrMidNL) ml |= bit;
+    if (kind == kPrMidN || kind == kPrMidNL) mn |= bit;
     claimed += len ? len - 1 : 0u;
   }
+  *jl = ml;
+  *jd = mn;
   return __all(ok) && wave_sum(claimed) == wave_sum(ncont);
 }
+
+// Units: PACK = false, one document per unit (documents 0..n_docs-1, or the
+// doc_list entries); PACK = true, unit u = documents [u * pack, u * pack + pack)
+// sharing one window.  A pack that cannot take the packed path (window or
+// token/term capacity, non-contiguous sources, an empty or non-ASCII document)
+// sends its documents to retry_list for a PACK = false pass.
+#ifndef TFIDF_WAVE_XCD
+#define TFIDF_WAVE_XCD 1
+#endif
 
 // UNI = true (round 5): the documents the ASCII pass flagged (uni_list), one
 // wave each, by the same rules with non-ASCII bytes read as letters when
@@ -1465,7 +1587,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     return uni_scan((cur & ~63ull) + (uint64_t)gridDim.x * 64);
   };
   const uint64_t u0 = UNI ? uni_scan((uint64_t)blockIdx.x * 64) : ubeg;
-  const uint32_t simple2 = UNI && u0 != kNoUnit ? uni_simple2_bitmap(lane) : 0u;
+  uint32_t simple2 = 0, other2 = 0, punct = 0;
+  if (UNI && u0 != kNoUnit) uni_prose_bitmaps(lane, &simple2, &other2, &punct);
   const uint64_t ulim = UNI ? kNoUnit : uend;
   DocMeta meta;
   if (u0 < ulim) {
@@ -1521,7 +1644,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     uint64_t wbase = 0;
     bool upper;
     uint64_t W;
-    {
+    if constexpr (UNI) {
+      // flagged document: the prose check rewrites the staged window, which is
+      // then classified from LDS (the next window's fetch goes out first)
+      if (un < ulim) { meta = unit_meta<PACK>(p, un, lane); prefetch_wave(p, meta, lane, v); }
+      uint64_t jl, jd;
+      if (!uni_window_prose(sm.text, shift + (uint32_t)L, lane, simple2, other2, punct, &jl, &jd)) continue;
+      if (lane == 0) TFIDF_COLD(uni_list)[d] = 0u;           // taken here (else: k_tokenize_uwave)
+      my_uni += lane == 0;
+      W = lane_word_mask<false, true>(sm.text, lane, &bad, &under, &wbase, &upper, jl, jd);
+      bad = false;
+    } else {
       // a byte >= 0x80 (in the staged registers): the document goes to the UNI
       // pass unclassified (nrows 0; flagged below as `bad`)
       bool skipc = false;
@@ -1533,11 +1666,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       }
       const uint32_t nrows = skipc ? 0u : (shift + (uint32_t)L + 1023) >> 10;
       uint16_t *wm16 = reinterpret_cast<uint16_t *>(sm.list);            // the token list is written after
-      W = regs_word_mask<PACK, UNI>(v, nrows, sm.text, wm16, wm16 + 256, lane, &bad, &under, &wbase, &upper);
+      W = regs_word_mask<PACK>(v, nrows, sm.text, wm16, wm16 + 256, lane, &bad, &under, &wbase, &upper);
       bad |= skipc;
+      // the next document's window, now that this one's registers are consumed
+      if (un < ulim) { meta = unit_meta<PACK>(p, un, lane); prefetch_wave(p, meta, lane, v); }
     }
-    // the next document's window, now that this one's registers are consumed
-    if (un < ulim) { meta = unit_meta<PACK>(p, un, lane); prefetch_wave(p, meta, lane, v); }
     asm volatile("" ::: "memory");
     if (p.debug_stop == 1) continue;
     // PACK: document boundaries q_j (window position of document j's first
@@ -1561,11 +1694,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
       }
       W &= ~(jm & ~wbase);
     }
-    if (bad && UNI) {                                       // simple non-ASCII text: taken here
-      if (!uni_window_simple(sm.text, shift + (uint32_t)L, lane, simple2)) continue;   // stays flagged: k_tokenize_uwave
-      if (lane == 0) TFIDF_COLD(uni_list)[d] = 0u;
-      my_uni += lane == 0;
-    } else if (bad) {                                       // non-ASCII: the Unicode wave path
+    if (bad) {                                              // non-ASCII: the Unicode wave path
       if (PACK) defer_pack(p, d, np, lane);
       else if (lane == 0) flag_unicode(TFIDF_COLD(uni_list), d);
       continue;
@@ -1825,7 +1954,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
   };
   if (UNI && *p.uchunk_count == 0) return;                   // wave-uniform
   const uint64_t u0 = UNI ? next_flagged(blockIdx.x) : blockIdx.x;
-  const uint32_t simple2 = UNI && u0 < n_units ? uni_simple2_bitmap(lane) : 0u;
+  uint32_t simple2 = 0, other2 = 0, punct = 0;
+  if (UNI && u0 < n_units) uni_prose_bitmaps(lane, &simple2, &other2, &punct);
   if (u0 < n_units) { meta = chunk_meta(p, u0); prefetch(meta); }
   uint64_t un = 0;
   for (uint64_t u = u0; u < n_units; u = un) {
@@ -1858,8 +1988,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     // (a flag per unit, counted once per wave at the end — a list appended
     // with one atomic per unit serialised 15 k units on one counter)
     const bool nonascii = __any((hib & 0x80808080u) != 0);
+    uint64_t jl = 0, jd = 0;
     if (UNI && nonascii) {                                     // simple non-ASCII text: taken here
-      if (!uni_window_simple(sm.text, m.shift + (uint32_t)m.L, lane, simple2)) continue;   // k_tokenize_uchunk
+      if (!uni_window_prose(sm.text, m.shift + (uint32_t)m.L, lane, simple2, other2, punct, &jl, &jd))
+        continue;                                              // k_tokenize_uchunk
       if (lane == 0) p.uchunk_list[u] = 0u;
     } else if (nonascii) {
       if (lane == 0) {
@@ -1871,7 +2003,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     bool bad, under;
     uint64_t wbase = 0;
     bool upper;
-    const uint64_t W = lane_word_mask<false, UNI>(sm.text, lane, &bad, &under, &wbase, &upper);
+    const uint64_t W = lane_word_mask<false, UNI>(sm.text, lane, &bad, &under, &wbase, &upper, jl, jd);
     const uint64_t wlast = __ballot((W >> 63) & 1ull);
     const uint64_t prevW = lane ? (wlast >> (lane - 1)) & 1ull : 0ull;
     const uint64_t S = W & ~((W << 1) | prevW);

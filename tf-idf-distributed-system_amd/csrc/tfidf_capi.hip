@@ -401,6 +401,9 @@ struct tfidf_index {
   uint64_t n_canon = 0;
   DevBuf sent_slot, vcounts, vnu, vt_table, vt_sum, vt_rslot, gdf_dev;
   uint64_t n_sent = 0;
+  // the statistics view a GLOBAL setter replaced, reused by the next one once
+  // no search holds it (its pinned df mirror and device cache stay allocated)
+  std::shared_ptr<StatsView> view_spare;
 };
 
 int StatsView::wait_gdf() {
@@ -899,11 +902,13 @@ static float bm25_idf(uint64_t df, uint64_t doc_count) {
 }
 
 // BM25 norm cache of a statistics view (not yet visible to searches, or
-// owned by the writer), uploaded on stream s
+// owned by the writer), uploaded on stream s.  sync = false: the caller
+// guarantees no earlier upload out of v.h_cache is pending and orders the
+// view's first use after this one (StatsView::gdf_ev).
 static int upload_cache(const tfidf_config &cfg, StatsView &v, hipStream_t s, bool sync = true) {
   HIP_TRY(v.h_cache.resize(256));
   // the previous upload from the staging array must be done before it is rewritten
-  HIP_TRY(hipStreamSynchronize(s));
+  if (sync) HIP_TRY(hipStreamSynchronize(s));
   float *c = v.h_cache.data();
   if (v.doc_count == 0) {
     for (int i = 0; i < 256; i++) c[i] = 0.0f;
@@ -2417,15 +2422,10 @@ extern "C" int tfidf_set_stream(tfidf_index *ix, void *stream) {
   return TFIDF_OK;
 }
 
-extern "C" int tfidf_search_batch_keys_device(tfidf_index *ix, const uint8_t *q_utf8, const uint64_t *q_offsets,
-                                              uint32_t n_q, uint32_t k, uint64_t doc_base, void *d_keys) {
+static int batch_keys_on(tfidf_index *ix, Snapshot &S, StatsView &V, const uint8_t *q_utf8,
+                         const uint64_t *q_offsets, uint32_t n_q, uint32_t k, uint64_t doc_base, void *d_keys) {
   if (!ix || !q_offsets || (n_q && !d_keys)) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
   if (k == 0 || k > 1024) return fail(TFIDF_E_INVALID_ARG, "1 <= k <= 1024");
-  std::shared_ptr<StatsView> view;
-  const std::shared_ptr<Snapshot> snap = current(ix, &view);
-  if (!snap) return fail(TFIDF_E_STATE, "search before commit");
-  Snapshot &S = *snap;
-  StatsView &V = *view;
   CtxLease lease(ix);
   if (lease.rc) return lease.rc;
   SearchCtx &X = *lease.c;
@@ -2448,15 +2448,19 @@ extern "C" int tfidf_search_batch_keys_device(tfidf_index *ix, const uint8_t *q_
   return TFIDF_OK;
 }
 
-extern "C" int tfidf_search_all_keys_device(tfidf_index *ix, const uint8_t *q, uint64_t q_len, uint64_t doc_base,
-                                            void *d_keys, uint64_t cap, uint64_t *n_out) {
-  if (!ix || (!q && q_len) || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
-  *n_out = 0;
+extern "C" int tfidf_search_batch_keys_device(tfidf_index *ix, const uint8_t *q_utf8, const uint64_t *q_offsets,
+                                              uint32_t n_q, uint32_t k, uint64_t doc_base, void *d_keys) {
+  if (!ix) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
   std::shared_ptr<StatsView> view;
   const std::shared_ptr<Snapshot> snap = current(ix, &view);
   if (!snap) return fail(TFIDF_E_STATE, "search before commit");
-  Snapshot &S = *snap;
-  StatsView &V = *view;
+  return batch_keys_on(ix, *snap, *view, q_utf8, q_offsets, n_q, k, doc_base, d_keys);
+}
+
+static int all_keys_on(tfidf_index *ix, Snapshot &S, StatsView &V, const uint8_t *q, uint64_t q_len,
+                       uint64_t doc_base, void *d_keys, uint64_t cap, uint64_t *n_out) {
+  if (!ix || (!q && q_len) || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  *n_out = 0;
   CtxLease lease(ix);
   if (lease.rc) return lease.rc;
   SearchCtx &X = *lease.c;
@@ -2484,6 +2488,27 @@ extern "C" int tfidf_search_all_keys_device(tfidf_index *ix, const uint8_t *q, u
   HIP_TRY(hipStreamSynchronize(s));
   set_last_ms(ix, qev_ms(X, QEV_0, QEV_1), qev_ms(X, QEV_0, QEV_2));
   return TFIDF_OK;
+}
+
+extern "C" int tfidf_search_all_keys_device(tfidf_index *ix, const uint8_t *q, uint64_t q_len, uint64_t doc_base,
+                                            void *d_keys, uint64_t cap, uint64_t *n_out) {
+  if (!ix || !n_out) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
+  *n_out = 0;
+  std::shared_ptr<StatsView> view;
+  const std::shared_ptr<Snapshot> snap = current(ix, &view);
+  if (!snap) return fail(TFIDF_E_STATE, "search before commit");
+  return all_keys_on(ix, *snap, *view, q, q_len, doc_base, d_keys, cap, n_out);
+}
+
+// the same on a reader's pinned snapshot (the node-level searches: status
+// check, local search and document count from one snapshot)
+int tfidf::reader_batch_keys_device(tfidf_reader *rd, const uint8_t *q_utf8, const uint64_t *q_offsets, uint32_t n_q,
+                                    uint32_t k, uint64_t doc_base, void *d_keys) {
+  return batch_keys_on(rd->ix, *rd->S, *rd->V, q_utf8, q_offsets, n_q, k, doc_base, d_keys);
+}
+int tfidf::reader_all_keys_device(tfidf_reader *rd, const uint8_t *q, uint64_t q_len, uint64_t doc_base, void *d_keys,
+                                  uint64_t cap, uint64_t *n_out) {
+  return all_keys_on(rd->ix, *rd->S, *rd->V, q, q_len, doc_base, d_keys, cap, n_out);
 }
 
 // ---------------------------------------------------------------------------
@@ -2741,8 +2766,8 @@ static int exchange_done(tfidf_index *ix) {
   return TFIDF_OK;
 }
 
-extern "C" int tfidf_vocab_partition_device(tfidf_index *ix, uint32_t n_ranks, void *d_records, uint64_t cap,
-                                            void *d_counts, uint64_t *n_out) {
+static int vocab_partition(tfidf_index *ix, uint32_t n_ranks, void *d_records, uint64_t cap, void *d_counts,
+                           uint64_t *n_out, bool sync) {
   if (!ix || !n_out || !d_counts || n_ranks == 0 || n_ranks > 1024)
     return fail(TFIDF_E_INVALID_ARG, "NULL argument or n_ranks not in [1, 1024]");
   std::lock_guard<std::mutex> lk(ix->mu);
@@ -2763,11 +2788,19 @@ extern "C" int tfidf_vocab_partition_device(tfidf_index *ix, uint32_t n_ranks, v
   HIP_TRY(vocab_scatter(S.dict.as<uint64_t>(), S.df_dev(), S.C, n_ranks, cur, (uint64_t *)d_records,
                         ix->sent_slot.as<uint32_t>(), s));
   ix->n_sent = S.num_terms;
-  return exchange_done(ix);                            // asynchronous on a caller's stream
+  return sync ? exchange_done(ix) : TFIDF_OK;          // asynchronous on a caller's stream
+}
+extern "C" int tfidf_vocab_partition_device(tfidf_index *ix, uint32_t n_ranks, void *d_records, uint64_t cap,
+                                            void *d_counts, uint64_t *n_out) {
+  return vocab_partition(ix, n_ranks, d_records, cap, d_counts, n_out, true);
+}
+int tfidf::vocab_partition_async(tfidf_index *ix, uint32_t n_ranks, void *d_records, uint64_t cap, void *d_counts,
+                                 uint64_t *n_out) {
+  return vocab_partition(ix, n_ranks, d_records, cap, d_counts, n_out, false);
 }
 
-extern "C" int tfidf_vocab_reduce_device(tfidf_index *ix, const void *d_records, uint64_t n, void *d_df_out,
-                                         void *d_n_unique) {
+static int vocab_reduce_dev(tfidf_index *ix, const void *d_records, uint64_t n, void *d_df_out, void *d_n_unique,
+                            bool sync) {
   if (!ix || (n && (!d_records || !d_df_out))) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
   std::lock_guard<std::mutex> lk(ix->mu);
   DeviceGuard g(ix->cfg.device);
@@ -2790,20 +2823,62 @@ extern "C" int tfidf_vocab_reduce_device(tfidf_index *ix, const void *d_records,
   HIP_TRY(vocab_reduce((const uint64_t *)d_records, n, ix->vt_table.as<uint64_t>(), (uint32_t)(T - 1),
                        ix->vt_sum.as<uint32_t>(), ix->vt_rslot.as<uint32_t>(), (uint32_t *)d_df_out, nu, s));
   if (d_n_unique) HIP_TRY(hipMemcpyAsync(d_n_unique, nu, 8, hipMemcpyDeviceToDevice, s));
-  return exchange_done(ix);                            // asynchronous on a caller's stream
+  return sync ? exchange_done(ix) : TFIDF_OK;          // asynchronous on a caller's stream
+}
+extern "C" int tfidf_vocab_reduce_device(tfidf_index *ix, const void *d_records, uint64_t n, void *d_df_out,
+                                         void *d_n_unique) {
+  return vocab_reduce_dev(ix, d_records, n, d_df_out, d_n_unique, true);
+}
+int tfidf::vocab_reduce_async(tfidf_index *ix, const void *d_records, uint64_t n, void *d_df_out, void *d_n_unique) {
+  return vocab_reduce_dev(ix, d_records, n, d_df_out, d_n_unique, false);
 }
 
 // A new statistics view for the current snapshot (the GLOBAL setters): built
 // aside, complete on the device (norm cache uploaded) before searches see it.
-static int publish_view(tfidf_index *ix, Snapshot &S, const std::shared_ptr<StatsView> &v) {
-  if (int e = upload_cache(ix->cfg, *v, ix->stream)) return e;
-  std::lock_guard<std::mutex> sl(ix->snap_mu);
-  S.stats = v;
+// The view it replaces is kept as the next setter's spare.  async: the cache
+// upload (and whatever the caller queued for the view before) completes
+// behind the view's event, which every search waits for before its first use
+// (StatsView::wait_gdf) — the setter itself never waits for the device.
+static int publish_view(tfidf_index *ix, Snapshot &S, const std::shared_ptr<StatsView> &v, bool async = false) {
+  if (int e = upload_cache(ix->cfg, *v, ix->stream, !async)) return e;
+  if (async) {
+    std::lock_guard<std::mutex> gl(v->gdf_mu);
+    HIP_TRY(hipEventRecord(v->gdf_ev, ix->stream));
+    v->gdf_pending = true;
+  }
+  std::shared_ptr<StatsView> old;
+  {
+    std::lock_guard<std::mutex> sl(ix->snap_mu);
+    old = std::move(S.stats);
+    S.stats = v;
+  }
+  if (old && old != v) ix->view_spare = std::move(old);
   return TFIDF_OK;
 }
 
-extern "C" int tfidf_set_global_df_device(tfidf_index *ix, const void *d_df, uint64_t n, uint64_t doc_count,
-                                          uint64_t sum_ttf) {
+// A statistics view to fill: the spare one once no search holds it (ADVICE
+// r05: a fresh view per GLOBAL exchange pinned C x 4 bytes of host memory and
+// freed the previous view's, which synchronises the device), else a new one.
+static std::shared_ptr<StatsView> take_view(tfidf_index *ix) {
+  std::shared_ptr<StatsView> v;
+  if (ix->view_spare && ix->view_spare.use_count() == 1) {
+    v = std::move(ix->view_spare);
+    if (v->wait_gdf() != TFIDF_OK) v.reset();          // its last uploads have left h_cache / gdf
+  }
+  ix->view_spare.reset();
+  if (!v) v = std::make_shared<StatsView>(ix->cfg.device);
+  v->global = false;
+  v->gdf.clear();
+  return v;
+}
+
+// tfidf_set_global_df_device (sync: the public call, which returns when the
+// caller's df buffer has been read on the index's own stream) and its
+// asynchronous form for tfidf_dist_global_commit (every buffer is the
+// communicator's, ordered on the index's stream).  *generation: the commit
+// generation of the snapshot the GLOBAL view was published on.
+static int set_global_df(tfidf_index *ix, const void *d_df, uint64_t n, uint64_t doc_count, uint64_t sum_ttf,
+                         bool sync, uint64_t *generation) {
   if (!ix || (n && !d_df)) return fail(TFIDF_E_INVALID_ARG, "NULL argument");
   std::lock_guard<std::mutex> lk(ix->mu);
   const std::shared_ptr<Snapshot> snap = current(ix);
@@ -2813,7 +2888,7 @@ extern "C" int tfidf_set_global_df_device(tfidf_index *ix, const void *d_df, uin
                                    (unsigned long long)ix->n_sent);
   DeviceGuard g(ix->cfg.device);
   hipStream_t s = ix->stream;
-  auto v = std::make_shared<StatsView>(ix->cfg.device);
+  std::shared_ptr<StatsView> v = take_view(ix);
   HIP_TRY(ix->gdf_dev.reserve((size_t)S.C * 4));
   HIP_TRY(hipMemsetAsync(ix->gdf_dev.p, 0, (size_t)S.C * 4, s));
   HIP_TRY(vocab_import(ix->sent_slot.as<uint32_t>(), (const uint32_t *)d_df, n, ix->gdf_dev.as<uint32_t>(), s));
@@ -2821,13 +2896,30 @@ extern "C" int tfidf_set_global_df_device(tfidf_index *ix, const void *d_df, uin
   // first query (prepare_query) — the exchange itself needs no host sync
   HIP_TRY(v->gdf.resize(S.C));
   HIP_TRY(hipMemcpyAsync(v->gdf.data(), ix->gdf_dev.p, (size_t)S.C * 4, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipEventRecord(v->gdf_ev, s));
-  v->gdf_pending = true;
+  {
+    std::lock_guard<std::mutex> gl(v->gdf_mu);
+    HIP_TRY(hipEventRecord(v->gdf_ev, s));
+    v->gdf_pending = true;
+  }
   v->global = true;
   v->doc_count = doc_count;
   v->sum_ttf = sum_ttf;
-  if (int e = exchange_done(ix)) return e;
-  return publish_view(ix, S, v);
+  if (generation) *generation = S.generation;
+  if (sync) {
+    if (int e = exchange_done(ix)) return e;
+    return publish_view(ix, S, v);
+  }
+  return publish_view(ix, S, v, true);
+}
+
+extern "C" int tfidf_set_global_df_device(tfidf_index *ix, const void *d_df, uint64_t n, uint64_t doc_count,
+                                          uint64_t sum_ttf) {
+  return set_global_df(ix, d_df, n, doc_count, sum_ttf, true, nullptr);
+}
+
+int tfidf::set_global_df_async(tfidf_index *ix, const void *d_df, uint64_t n, uint64_t doc_count, uint64_t sum_ttf,
+                               uint64_t *generation) {
+  return set_global_df(ix, d_df, n, doc_count, sum_ttf, false, generation);
 }
 
 extern "C" int tfidf_set_global_stats_device(tfidf_index *ix, const void *d_df_canonical, uint64_t n_canonical,
@@ -2840,7 +2932,7 @@ extern "C" int tfidf_set_global_stats_device(tfidf_index *ix, const void *d_df_c
   if (n_canonical != ix->n_canon) return fail(TFIDF_E_STATE, "canonical vocabulary size mismatch");
   DeviceGuard g(ix->cfg.device);
   hipStream_t s = ix->stream;
-  auto v = std::make_shared<StatsView>(ix->cfg.device);
+  std::shared_ptr<StatsView> v = take_view(ix);
   DevBuf gd;
   HIP_TRY(gd.reserve((size_t)S.C * 4));
   HIP_TRY(gather_df_canon((const uint32_t *)d_df_canonical, ix->canon_of_slot.as<uint32_t>(), S.C,
@@ -2863,7 +2955,7 @@ extern "C" int tfidf_set_global_stats(tfidf_index *ix, const uint64_t *keys_lohi
   if (!snap) return fail(TFIDF_E_STATE, "not committed");
   Snapshot &S = *snap;
   DeviceGuard g(ix->cfg.device);
-  auto v = std::make_shared<StatsView>(ix->cfg.device);
+  std::shared_ptr<StatsView> v = take_view(ix);
   HIP_TRY(v->gdf.assign(S.C, 0));
   for (uint32_t s = 0; s < S.C; s++) v->gdf[s] = S.h_df[s];  // keys not listed keep local df
   for (uint64_t i = 0; i < n; i++) {
@@ -2883,7 +2975,7 @@ extern "C" int tfidf_clear_global_stats(tfidf_index *ix) {
   if (!snap) return TFIDF_OK;
   Snapshot &S = *snap;
   DeviceGuard g(ix->cfg.device);
-  auto v = std::make_shared<StatsView>(ix->cfg.device);
+  std::shared_ptr<StatsView> v = take_view(ix);
   v->doc_count = S.doc_count;
   v->sum_ttf = S.sum_ttf;
   return publish_view(ix, S, v);

@@ -314,6 +314,8 @@ struct tfidf_comm {
   uint64_t global_gen = ~0ull;      // index commit generation of the last GLOBAL exchange
   uint64_t last_failed = 0;         // SHARD search: ranks skipped by the last search (bit r)
   HBuf h_hdr;                       // status words ahead of a rank's keys (pinned)
+  DBuf d_meta, d_M;                 // GLOBAL exchange: this rank's meta row / every rank's (device)
+  HBuf h_meta, h_M;                 // their pinned host sides
   bool hdr_pending = false;         // an upload out of h_hdr may still be queued (a search that failed)
   // last search results (tfidf_dist_last_hits / _last_names)
   std::vector<uint64_t> last_doc;
@@ -611,37 +613,44 @@ extern "C" int tfidf_comm_selftest(tfidf_comm *c) {
 // GLOBAL statistics by term ownership.  Meta row per rank: [records per owner
 // (world) | docCount | sumTTF | seed attempt | error] — one host read; the
 // ranks see each other's errors and seed attempts in it, so they fail, or
-// re-commit under one seed, together.
+// re-commit under one seed, together.  Round 6: one host synchronisation per
+// exchange (the gathered meta rows): the owner counts stay on the device
+// (written by the partition straight into the meta row), the partition,
+// reduction and df import queue without waiting, and the new statistics view
+// is published behind an event the first search waits for.
 extern "C" int tfidf_dist_global_commit(tfidf_index *ix, tfidf_comm *c, uint64_t *n_vocab, uint64_t *doc_count,
                                         uint64_t *sum_ttf) {
   if (int rc = check_comm(ix, c)) return rc;
   const int ws = c->world, me = c->rank;
+  const size_t W = ws + 4;
   DevGuard g(index_device(ix));
   hipStream_t s = index_stream(ix);
   int local_err = index_committed(ix) ? TFIDF_OK : errf(TFIDF_E_STATE, "index not committed");
   std::string local_msg = local_err ? tfidf_last_error() : "";
-  std::vector<uint64_t> M;
+  DHIP(c->d_meta.reserve(W * 8));
+  DHIP(c->d_M.reserve((size_t)ws * W * 8));
+  DHIP(c->h_meta.reserve(W * 8));
+  DHIP(c->h_M.reserve((size_t)ws * W * 8));
+  uint64_t *meta = c->h_meta.as<uint64_t>();
+  const uint64_t *M = c->h_M.as<uint64_t>();
   uint64_t n_rec = 0;
   for (int round = 0;; round++) {
-    std::vector<uint64_t> meta(ws + 4, 0);
     tfidf_index_stats st{};
     if (!local_err) local_err = tfidf_stats(ix, &st);
     if (!local_err) {
       DHIP(c->d_rec.reserve(std::max<uint64_t>(st.num_terms, 1) * 24));
-      DHIP(c->d_cnt.reserve((size_t)ws * 8));
-      local_err = tfidf_vocab_partition_device(ix, (uint32_t)ws, c->d_rec.p, c->d_rec.bytes / 24, c->d_cnt.p, &n_rec);
-      if (!local_err) {
-        DHIP(hipMemcpyAsync(meta.data(), c->d_cnt.p, (size_t)ws * 8, hipMemcpyDeviceToHost, s));
-        DHIP(hipStreamSynchronize(s));
-      }
+      local_err = vocab_partition_async(ix, (uint32_t)ws, c->d_rec.p, c->d_rec.bytes / 24, c->d_meta.p, &n_rec);
     }
     if (local_err && local_msg.empty()) local_msg = tfidf_last_error();
+    if (local_err) DHIP(hipMemsetAsync(c->d_meta.p, 0, (size_t)ws * 8, s));
     meta[ws] = st.doc_count;
     meta[ws + 1] = st.sum_ttf;
     meta[ws + 2] = st.hash_rebuilds;
     meta[ws + 3] = local_err ? (uint64_t)local_err : 0;
-    if (int rc = gather_rows(c, s, meta, &M)) return rc;
-    const size_t W = ws + 4;
+    DHIP(hipMemcpyAsync(c->d_meta.as<uint64_t>() + ws, meta + ws, 4 * 8, hipMemcpyHostToDevice, s));
+    if (int rc = coll_gather(c, s, c->d_meta.p, c->d_M.p, W * 8, true)) return rc;
+    DHIP(hipMemcpyAsync(c->h_M.p, c->d_M.p, (size_t)ws * W * 8, hipMemcpyDeviceToHost, s));
+    DHIP(hipStreamSynchronize(s));                    // the one host read (meta rows; h_meta reusable)
     for (int r = 0; r < ws; r++)
       if (M[r * W + ws + 3]) {
         if (r == me) return set_error(local_err, local_msg.c_str());
@@ -663,7 +672,6 @@ extern "C" int tfidf_dist_global_commit(tfidf_index *ix, tfidf_comm *c, uint64_t
       if (local_err) local_msg = tfidf_last_error();
     }
   }
-  const size_t W = ws + 4;
   std::vector<uint64_t> sb(ws), so(ws), rb(ws), ro(ws), sb2(ws), so2(ws), rb2(ws), ro2(ws);
   uint64_t gdc = 0, gttf = 0, n_got = 0, at = 0, at2 = 0;
   for (int r = 0; r < ws; r++) {
@@ -686,11 +694,14 @@ extern "C" int tfidf_dist_global_commit(tfidf_index *ix, tfidf_comm *c, uint64_t
   if (int rc = coll_a2av(c, s, c->d_rec.p, sb.data(), so.data(), c->d_got.p, rb.data(), ro.data(), true)) return rc;
   DHIP(c->d_ans.reserve(std::max<uint64_t>(n_got, 1) * 4));
   DHIP(c->d_nu.reserve(8));
-  if (int rc = tfidf_vocab_reduce_device(ix, c->d_got.p, n_got, c->d_ans.p, c->d_nu.p)) return rc;
+  if (int rc = vocab_reduce_async(ix, c->d_got.p, n_got, c->d_ans.p, c->d_nu.p)) return rc;
   DHIP(c->d_back.reserve(std::max<uint64_t>(n_rec, 1) * 4));
   if (int rc = coll_a2av(c, s, c->d_ans.p, sb2.data(), so2.data(), c->d_back.p, rb2.data(), ro2.data(), true)) return rc;
-  if (int rc = tfidf_set_global_df_device(ix, c->d_back.p, n_rec, gdc, gttf)) return rc;
-  c->global_gen = index_generation(ix);
+  // the generation the view was published on (not re-read: a commit on another
+  // thread may have landed since)
+  uint64_t gen = 0;
+  if (int rc = set_global_df_async(ix, c->d_back.p, n_rec, gdc, gttf, &gen)) return rc;
+  c->global_gen = gen;
   if (n_vocab) {
     uint64_t nu = 0;
     DHIP(hipMemcpyAsync(&nu, c->d_nu.p, 8, hipMemcpyDeviceToHost, s));
@@ -720,13 +731,29 @@ namespace {
 // overlapping doc ranges fail on every rank (TFIDF_E_INVALID_ARG).
 constexpr uint64_t kHdr = 4;        // status words per rank: {rc, doc_base, n_docs, 0}
 
-int local_search_status(tfidf_index *ix, tfidf_comm *c, uint64_t doc_base, bool global) {
-  if (!index_committed(ix)) return errf(TFIDF_E_STATE, "index not committed");
-  if (doc_base + index_num_docs(ix) > (1ull << 32))
+// One snapshot for a whole node-level search: the status check,
+// the local search and the document count all read the reader it pins, so a
+// commit landing on another thread meanwhile cannot mix generations.
+struct Pinned {
+  tfidf_reader *rd = nullptr;
+  uint64_t gen = 0, nd = 0;
+  Pinned() = default;
+  Pinned(const Pinned &) = delete;
+  Pinned &operator=(const Pinned &) = delete;
+  ~Pinned() { if (rd) tfidf_reader_close(rd); }
+  int open(tfidf_index *ix) {
+    if (tfidf_reader_open(ix, &rd) != TFIDF_OK) { rd = nullptr; return errf(TFIDF_E_STATE, "index not committed"); }
+    return tfidf_reader_info(rd, &gen, &nd);
+  }
+};
+
+int local_search_status(Pinned &pin, tfidf_index *ix, tfidf_comm *c, uint64_t doc_base, bool global) {
+  if (int rc = pin.open(ix)) return rc;
+  if (doc_base + pin.nd > (1ull << 32))
     return errf(TFIDF_E_CAPACITY, "global doc ids must stay below 2^32 (merge keys carry 32-bit ids)");
-  if (global && c->global_gen != index_generation(ix))
+  if (global && c->global_gen != pin.gen)
     return errf(TFIDF_E_STATE, "tfidf_dist_global_commit first (after every commit)");
-  if (!global && (!c->names_ready || c->names_gen != index_generation(ix)))
+  if (!global && (!c->names_ready || c->names_gen != pin.gen))
     return errf(TFIDF_E_STATE, "tfidf_dist_shard_commit first (after every commit)");
   return TFIDF_OK;
 }
@@ -774,10 +801,10 @@ int write_hits(tfidf_comm *c, uint64_t *doc_ids, float *scores, uint64_t cap, ui
 }
 
 // every hit's merge key of one query on this shard -> d_keys; *h = hits
-int all_keys(tfidf_index *ix, tfidf_comm *c, const uint8_t *q, uint64_t q_len, uint64_t doc_base, uint64_t *h) {
-  const uint64_t nd = std::max<uint64_t>(index_num_docs(ix), 1);
+int all_keys(Pinned &pin, tfidf_comm *c, const uint8_t *q, uint64_t q_len, uint64_t doc_base, uint64_t *h) {
+  const uint64_t nd = std::max<uint64_t>(pin.nd, 1);
   DHIP(c->d_keys.reserve(nd * 8));
-  return tfidf_search_all_keys_device(ix, q, q_len, doc_base, c->d_keys.p, nd, h);
+  return reader_all_keys_device(pin.rd, q, q_len, doc_base, c->d_keys.p, nd, h);
 }
 
 // gather variable-length device rows (d_keys[0, h)) from every rank, padded to
@@ -818,8 +845,9 @@ int gather_topk(tfidf_index *ix, tfidf_comm *c, hipStream_t s, uint64_t doc_base
   DHIP(c->h_out.reserve((per + (size_t)ws * kHdr) * 8));
   DHIP(c->h_hdr.reserve(kHdr * 8));
   uint64_t *dk = c->d_keys.as<uint64_t>();
-  int lrc = local_search_status(ix, c, doc_base, true);
-  if (!lrc) lrc = tfidf_search_batch_keys_device(ix, q_utf8, q_offsets, n_q, k, doc_base, dk + kHdr);
+  Pinned pin;
+  int lrc = local_search_status(pin, ix, c, doc_base, true);
+  if (!lrc) lrc = reader_batch_keys_device(pin.rd, q_utf8, q_offsets, n_q, k, doc_base, dk + kHdr);
   const std::string lmsg = lrc ? tfidf_last_error() : "";
   if (lrc) DHIP(hipMemsetAsync(dk + kHdr, 0, per * 8, s));
   uint64_t *hh = c->h_hdr.as<uint64_t>();
@@ -827,7 +855,7 @@ int gather_topk(tfidf_index *ix, tfidf_comm *c, hipStream_t s, uint64_t doc_base
   c->hdr_pending = true;
   hh[0] = (uint64_t)lrc;
   hh[1] = doc_base;
-  hh[2] = lrc ? 0 : index_num_docs(ix);
+  hh[2] = lrc ? 0 : pin.nd;
   hh[3] = 0;
   DHIP(hipMemcpyAsync(dk, hh, kHdr * 8, hipMemcpyHostToDevice, s));
   if (int rc = coll_gather(c, s, dk, c->d_all.p, row * 8, true)) return rc;
@@ -862,11 +890,12 @@ extern "C" int tfidf_dist_search(tfidf_index *ix, tfidf_comm *c, uint64_t doc_ba
     while (n < k && keys[n]) n++;
   } else {
     uint64_t h = 0, maxn = 0;
-    int lrc = local_search_status(ix, c, doc_base, true);
-    if (!lrc) lrc = all_keys(ix, c, q, q_len, doc_base, &h);
+    Pinned pin;
+    int lrc = local_search_status(pin, ix, c, doc_base, true);
+    if (!lrc) lrc = all_keys(pin, c, q, q_len, doc_base, &h);
     const std::string lmsg = lrc ? tfidf_last_error() : "";
     std::vector<uint64_t> ns;
-    if (int rc = gather_var(c, s, h, 0, lrc, lmsg, doc_base, lrc ? 0 : index_num_docs(ix), true, &ns, &maxn))
+    if (int rc = gather_var(c, s, h, 0, lrc, lmsg, doc_base, lrc ? 0 : pin.nd, true, &ns, &maxn))
       return rc;
     for (uint64_t x : ns) n += x;
     if (n) {
@@ -1046,8 +1075,9 @@ extern "C" int tfidf_dist_shard_search(tfidf_index *ix, tfidf_comm *c, const uin
   uint64_t h = 0, maxn = 0;
   // a rank that cannot serve (stale name table, failed local search) is a
   // failed worker: the others' hits are merged without it (Leader.java:67-69)
-  int lrc = local_search_status(ix, c, 0, false);
-  if (!lrc) lrc = all_keys(ix, c, q, q_len, 0, &h);             // local doc ids
+  Pinned pin;
+  int lrc = local_search_status(pin, ix, c, 0, false);
+  if (!lrc) lrc = all_keys(pin, c, q, q_len, 0, &h);            // local doc ids
   if (!lrc && h) {
     if (hipSuccess != c->d_tmp.reserve(h * 8)) lrc = errf(TFIDF_E_OOM, "name records: out of device memory");
     if (!lrc) {

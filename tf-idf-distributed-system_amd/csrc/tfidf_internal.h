@@ -407,6 +407,7 @@ hipError_t vocab_import(const uint32_t *sent_slot, const uint32_t *gdf_in, uint6
 // --- index internals the node-level orchestration reads (tfidf_capi.hip) ---
 }  // namespace tfidf
 struct tfidf_index;
+struct tfidf_reader;
 namespace tfidf {
 hipStream_t index_stream(tfidf_index *ix);
 int index_device(const tfidf_index *ix);
@@ -414,6 +415,18 @@ bool index_committed(const tfidf_index *ix);
 uint64_t index_num_docs(const tfidf_index *ix);
 uint64_t index_generation(const tfidf_index *ix);   // successful commits so far
 int set_error(int code, const char *msg);       // sets tfidf_last_error() of the calling thread
+// device-key searches on a reader's pinned snapshot (tfidf_reader_open)
+int reader_batch_keys_device(tfidf_reader *rd, const uint8_t *q_utf8, const uint64_t *q_offsets, uint32_t n_q,
+                             uint32_t k, uint64_t doc_base, void *d_keys);
+int reader_all_keys_device(tfidf_reader *rd, const uint8_t *q, uint64_t q_len, uint64_t doc_base, void *d_keys,
+                           uint64_t cap, uint64_t *n_out);
+// GLOBAL exchange steps without the public calls' host synchronisation (every
+// buffer is the communicator's, ordered on the index's stream)
+int vocab_partition_async(tfidf_index *ix, uint32_t n_ranks, void *d_records, uint64_t cap, void *d_counts,
+                          uint64_t *n_out);
+int vocab_reduce_async(tfidf_index *ix, const void *d_records, uint64_t n, void *d_df_out, void *d_n_unique);
+int set_global_df_async(tfidf_index *ix, const void *d_df, uint64_t n, uint64_t doc_count, uint64_t sum_ttf,
+                        uint64_t *generation);
 // String.compareTo order of two UTF-8 names (UTF-16 code units; Leader.java:80-88 TreeMap)
 int utf16_compare(const uint8_t *a, uint64_t na, const uint8_t *b, uint64_t nb);
 

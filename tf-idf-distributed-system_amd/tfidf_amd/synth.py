@@ -169,6 +169,66 @@ class DeviceCorpus:
         _h2d(self.d_text, text, text.nbytes, self.device)
         return int(pos.size)
 
+    # Prose typography (round 6, bench.py --prose): per word, at most one of
+    # these same-length substitutions, at rates near typeset English prose
+    # (per word: apostrophe 1.5 %, opening / closing curly double quote 1 %
+    # each, em dash 0.5 %, ellipsis 0.2 %, no-break space 0.2 %, é 0.3 %, É
+    # 0.05 %, an ASCII capital 5 %).  (offset in the word, bytes); offset -1 =
+    # the separator before the word, "end" = the word's last bytes.
+    PROSE = (
+        (0.015, 1, "’".encode()),            # "a’cd…" (joined) / "a’" + sep
+        (0.010, 0, "“".encode()),
+        (0.010, "end", "”".encode()),
+        (0.005, 1, "—".encode()),
+        (0.002, "end", "…".encode()),
+        (0.002, -1, "\u00a0".encode()),
+        (0.003, 0, "é".encode()),
+        (0.0005, 0, "É".encode()),
+        (0.05, 0, None),                      # ASCII capital
+    )
+
+    def inject_prose(self, scale=1.0, seed=SEED + 13, chunk=64 << 20):
+        """Same-length prose substitutions (PROSE) at `scale` x their rates, in
+        place; the text is processed in chunks cut at separators.  Returns the
+        number of words changed."""
+        if scale <= 0:
+            return 0
+        text, offs = self.to_host()
+        rng = np.random.default_rng(seed)
+        cum = np.cumsum([r * scale for r, _, _ in self.PROSE])
+        n = len(text)
+        changed = 0
+        a = 0
+        while a < n:
+            z = min(n, a + chunk)
+            while z < n and text[z - 1] not in (32, 10):
+                z += 1
+            t = text[a:z]
+            is_l = (t >= 97) & (t <= 122)
+            prev = np.concatenate(([False], is_l[:-1]))
+            nxt = np.concatenate((is_l[1:], [False]))
+            st = np.nonzero(is_l & ~prev)[0]
+            en = np.nonzero(is_l & ~nxt)[0] + 1
+            ok = (en - st >= 4) & (st >= 1)
+            st, en = st[ok], en[ok]
+            u = rng.random(st.size)
+            cat = np.searchsorted(cum, u, side="right")
+            for ci, (_, at, by) in enumerate(self.PROSE):
+                sel = cat == ci
+                if not sel.any():
+                    continue
+                ws, we = st[sel], en[sel]
+                if by is None:
+                    t[ws] -= 32
+                else:
+                    pos = we - len(by) if at == "end" else ws + at
+                    for j, b in enumerate(by):
+                        t[pos + j] = b
+                changed += int(sel.sum())
+            a = z
+        _h2d(self.d_text, text, text.nbytes, self.device)
+        return changed
+
     def free(self):
         from . import _lib as L
         if self.d_text:
