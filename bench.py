@@ -461,6 +461,7 @@ def main():
         "global_exchange_frac_of_step": (exch[0] / elapsed) if dist_on else None,
         "long_docs": st["long_docs"],
         "long_chunked": st["long_chunked"],
+        "hash_rebuilds": st["hash_rebuilds"],
         "engine_unicode_docs": st["unicode_docs"],
         "engine_unicode_wave_docs": st["unicode_wave_docs"],
         "unicode_docs": n_unicode,

@@ -226,3 +226,37 @@ def test_prose_books_equal_oracle(monkeypatch, uniwave):
             assert_hits_equal(g.search(qb, k), o.search(qb, k))
     g.close()
     o.close()
+
+
+@pytest.mark.parametrize("unifirst", [True, False])
+def test_uni_first_recommit_equals_oracle(monkeypatch, unifirst):
+    """A re-commit after a commit whose documents were mostly non-ASCII runs
+    UNI-first (round 6): every document starts flagged and the UNI wave pass
+    takes the ASCII ones too (no ASCII pass); documents it declines (Han, too
+    long for a wave window, malformed) still reach the Unicode wave and long
+    paths.  Both commits, and the same re-commit without the mode
+    (TFIDF_NO_UNIFIRST), equal the oracle; the non-ASCII count is unchanged."""
+    if not unifirst:
+        monkeypatch.setenv("TFIDF_NO_UNIFIRST", "1")
+    rng = random.Random(113)
+    texts = [doc(rng, rng.randint(20, 500), rng.randint(1, 12), PROSE + WORDS + JOIN) for _ in range(700)]
+    texts += [doc(rng, rng.randint(20, 300), 2, PROSE) + " 中文".encode() for _ in range(60)]
+    texts += synth.corpus(300, V=3000, len_min=50, len_max=400)                       # ASCII
+    texts += [(" ".join(synth.word(rng.randint(1, 3000)).decode() for _ in range(2500))).encode()]   # > 4 KB
+    texts += [b"bad \xff byte", ("word " * 820).encode(), prose_edge_docs()[7]]
+    rng.shuffle(texts)
+    g, o = build_pair(texts)
+    st1 = g.stats()
+    check(g, o, texts)
+    g.commit()                                        # the same documents again: UNI-first unless disabled
+    st2 = g.stats()
+    check(g, o, texts)
+    for k in ("unicode_docs", "unicode_wave_docs", "long_docs", "nnz", "num_terms"):
+        if k in st1:
+            assert st1[k] == st2[k], k
+    for q in ["don’t", "québec", "École", "Über", "中文", synth.word(11).decode(), "word"]:
+        qb = q.encode()
+        for kk in (0, 10):
+            assert_hits_equal(g.search(qb, kk), o.search(qb, kk))
+    g.close()
+    o.close()

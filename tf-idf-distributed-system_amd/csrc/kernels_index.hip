@@ -445,14 +445,10 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t x) {
 // the document were zeroed at staging (class Other).  Wave-uniform flags:
 // *bad = a byte >= 0x80 in the document, *under = a '_' in the document.
 // PACK: *wbase = the same mask before the joiner rules (letters, digits, '_').
-// UNI (round 6): jl / jd = this lane's non-ASCII mid chars (lead byte bits,
-// uni_window_prose) that join letters (MidLetter, MidNumLet) / digits
-// (MidNum, MidNumLet): their bytes are classified as Other, then each one
-// joins its token when both neighbour chars are letters (WB6/7) / digits
-// (WB11/12) — the ASCII rule of a single mid char, with a 2-3 byte char.
+// UNI: bytes >= 0x80 read as letters (a window uni_window_prose passed).
 template <bool PACK, bool UNI = false>
 __device__ __forceinline__ uint64_t lane_word_mask(const uint8_t *text, uint32_t lane, bool *bad, bool *under,
-                                                   uint64_t *wbase, bool *upper, uint64_t jl = 0, uint64_t jd = 0) {
+                                                   uint64_t *wbase, bool *upper) {
   uint32_t x[16], hb[16];
   {
     const uint4 *t = reinterpret_cast<const uint4 *>(text + lane * 64);
@@ -460,26 +456,6 @@ __device__ __forceinline__ uint64_t lane_word_mask(const uint8_t *text, uint32_t
     for (int k = 0; k < 4; k++) {
       const uint4 v = t[k];
       x[4 * k] = v.x; x[4 * k + 1] = v.y; x[4 * k + 2] = v.z; x[4 * k + 3] = v.w;
-    }
-  }
-  // UNI: the mid chars' bytes (leads of 3-byte chars: 111xxxxx) read as class Other
-  uint64_t mid3 = 0;
-  const bool anymid = UNI && __any((jl | jd) != 0);
-  if (anymid) {
-    uint64_t t3 = 0;
-#pragma unroll
-    for (int i = 0; i < 16; i++) t3 |= (uint64_t)swar_nib(x[i] & (x[i] << 1) & (x[i] << 2) & 0x80808080u) << (4 * i);
-    const uint64_t m = jl | jd;
-    mid3 = m & t3;
-    uint64_t ex = m | (m << 1) | (mid3 << 2);
-    const uint64_t spill = (m >> 63) | (mid3 >> 62);               // continuation bytes in the next lane
-    // (every cross-lane read unconditional: a lane outside EXEC reads as 0 to the others)
-    const uint32_t sp = (uint32_t)__shfl_up((int)(uint32_t)spill, 1, 64);
-    ex |= lane ? (uint64_t)sp : 0ull;
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-      const uint32_t nb = (uint32_t)(ex >> (4 * i)) & 0xFu;
-      x[i] &= ~((nb & 1u) * 0xFFu | (nb & 2u) * 0x7F80u | (nb & 4u) * 0x3FC000u | (nb & 8u) * 0x1FE00000u);
     }
   }
   // pass 1: letter/digit flags (neighbour context), non-ASCII, joiner presence
@@ -526,38 +502,6 @@ __device__ __forceinline__ uint64_t lane_word_mask(const uint8_t *text, uint32_t
       c |= (ml & both) | (mn & (both << 1));
     }
     W |= (uint64_t)swar_nib(c & 0x80808080u) << (4 * i);
-  }
-  if (anymid) {
-    // letter / digit bits of the lane's bytes, and of the neighbours across lanes
-    uint64_t Lm = 0, Dm = 0;
-#pragma unroll
-    for (int i = 0; i < 16; i++) {
-      Lm |= (uint64_t)swar_nib(LD[i] & 0x80808080u) << (4 * i);
-      Dm |= (uint64_t)swar_nib((LD[i] << 1) & 0x80808080u) << (4 * i);
-    }
-    const uint32_t pl0 = (uint32_t)__shfl_up((int)(uint32_t)(Lm >> 63), 1, 64);
-    const uint32_t pd0 = (uint32_t)__shfl_up((int)(uint32_t)(Dm >> 63), 1, 64);
-    const uint32_t nl0 = (uint32_t)__shfl_down((int)(uint32_t)Lm, 1, 64);
-    const uint32_t nd0 = (uint32_t)__shfl_down((int)(uint32_t)Dm, 1, 64);
-    const uint32_t pl = lane ? pl0 & 1u : 0u, pd = lane ? pd0 & 1u : 0u;
-    const uint32_t nl = lane < 63 ? nl0 & 7u : 0u, nd = lane < 63 ? nd0 & 7u : 0u;
-    uint64_t m = jl | jd, add = 0;
-    uint32_t carry = 0;
-    while (m) {
-      const uint32_t b = (uint32_t)__builtin_ctzll(m);
-      m &= m - 1;
-      const uint32_t len = ((mid3 >> b) & 1u) ? 3u : 2u, a = b + len;
-      const uint32_t lb = b ? (uint32_t)(Lm >> (b - 1)) & 1u : pl, db = b ? (uint32_t)(Dm >> (b - 1)) & 1u : pd;
-      const uint32_t la = a < 64 ? (uint32_t)(Lm >> a) & 1u : (nl >> (a - 64)) & 1u;
-      const uint32_t da = a < 64 ? (uint32_t)(Dm >> a) & 1u : (nd >> (a - 64)) & 1u;
-      const bool join = (((jl >> b) & 1u) && lb && la) || (((jd >> b) & 1u) && db && da);
-      if (join) {
-        add |= ((1ull << len) - 1) << b;
-        if (a > 64) carry |= (1u << (a - 64)) - 1u;
-      }
-    }
-    const uint32_t cin = (uint32_t)__shfl_up((int)carry, 1, 64);
-    W |= add | (uint64_t)(lane ? cin : 0u);
   }
   *bad = __any((badacc & 0x80808080u) != 0);
   *under = __any(us != 0);
@@ -1473,24 +1417,40 @@ __device__ __forceinline__ void uni_prose_bitmaps(uint32_t lane, uint32_t *simpl
 // bytes (11xxxxxx) one per step, common chars from the wave's bitmaps, the
 // others through the tables, and the wave's continuation bytes (10xxxxxx)
 // must be exactly those the leads claim (no orphans).  On the way separators
-// become spaces and upper-case letters their lower case in the window; the
-// lane's mid chars (lead bits within its 64 bytes) that join letters / digits
-// go to *jl / *jd for the classifier.  Wave-uniform result.
+// become spaces and upper-case letters their lower case in the window.  Then
+// each mid char joins where UAX#29 joins it (MidLetter / MidNumLet: a letter
+// on both sides, WB6/7; MidNum / MidNumLet: a digit on both sides, WB11/12)
+// and is kept — its bytes >= 0x80 then read as letters, so the classifier
+// makes it part of the word — or becomes spaces.  (A kept mid char never
+// touches an ASCII joiner: its neighbours are letters or digits, so the
+// classifier's rules around it are unchanged.)  Wave-uniform result.
 __device__ __forceinline__ bool uni_window_prose(uint8_t *text, uint32_t wl, uint32_t lane, uint32_t simple2,
-                                                 uint32_t other2, uint32_t punct, uint64_t *jl, uint64_t *jd) {
-  const uint32_t *seg = reinterpret_cast<const uint32_t *>(text + 64 * lane);
+                                                 uint32_t other2, uint32_t punct, bool *nonascii = nullptr) {
+  const uint4 *seg = reinterpret_cast<const uint4 *>(text + 64 * lane);
   uint64_t lead = 0;
   uint32_t ncont = 0;
+  // the lane's four 16 B pieces in an order rotated by lane / 2: every group
+  // of 8 lanes of a ds_read_b128 then covers 8 distinct bank groups (in the
+  // plain order lanes 64 B apart collide: 2.2 ms of cfg-2 prose in this step)
 #pragma unroll
-  for (int j = 0; j < 16; j++) {
-    const uint32_t x = seg[j], hb = x & 0x80808080u, ld = hb & (x << 1);
-    ncont += (uint32_t)__popc(hb & ~ld);
-    lead |= (uint64_t)swar_nib(ld) << (4 * j);
+  for (int q = 0; q < 4; q++) {
+    const uint32_t qq = (q + (lane >> 1)) & 3u;
+    const uint4 v = seg[qq];
+    const uint32_t xs[4] = {v.x, v.y, v.z, v.w};
+    uint32_t m16 = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const uint32_t x = xs[i], hb = x & 0x80808080u, ld = hb & (x << 1);
+      ncont += (uint32_t)__popc(hb & ~ld);
+      m16 |= swar_nib(ld) << (4 * i);
+    }
+    lead |= (uint64_t)m16 << (16 * qq);
   }
+  if (nonascii) *nonascii = __any(lead != 0) || __any(ncont != 0);
   const uint32_t *tw = reinterpret_cast<const uint32_t *>(text);
   bool ok = true;
   uint32_t claimed = 0;
-  uint64_t ml = 0, mn = 0;
+  uint64_t ml = 0, mn = 0, m3 = 0;
   while (__any(lead != 0)) {                            // one lead per lane per step
     const bool has = lead != 0;
     const uint32_t bt = has ? (uint32_t)__builtin_ctzll(lead) : 0u, pos = 64 * lane + bt;
@@ -1522,11 +1482,51 @@ __device__ __forceinline__ bool uni_window_prose(uint8_t *text, uint32_t wl, uin
     const uint64_t bit = 1ull << bt;
     if (kind == kPrMidL || kind == kPrMidNL) ml |= bit;
     if (kind == kPrMidN || kind == kPrMidNL) mn |= bit;
+    if (len == 3) m3 |= bit;
     claimed += len ? len - 1 : 0u;
   }
-  *jl = ml;
-  *jd = mn;
-  return __all(ok) && wave_sum(claimed) == wave_sum(ncont);
+  if (!(__all(ok) && wave_sum(claimed) == wave_sum(ncont))) return false;
+  // mid chars: the window now holds lowered letters and spaced separators; a
+  // neighbour byte >= 0x80 is a letter unless it belongs to another mid char
+  const uint64_t mid = ml | mn, mid3 = mid & m3;
+  if (__any(mid != 0)) {
+    __syncthreads();                                    // (one-wave workgroup) the rewrites above are visible
+    // neighbours' mid leads across the lane edges (shuffles unconditional: a
+    // lane outside EXEC reads as 0)
+    const uint64_t pm = (uint64_t)__shfl_up((long long)mid, 1, 64), pm3 = (uint64_t)__shfl_up((long long)mid3, 1, 64);
+    const uint64_t nm = (uint64_t)__shfl_down((long long)mid, 1, 64);
+    const uint64_t P = lane ? pm : 0ull, P3 = lane ? pm3 : 0ull, N = lane < 63 ? nm : 0ull;
+    uint64_t m = mid, drop = 0;
+    while (m) {
+      const uint32_t b = (uint32_t)__builtin_ctzll(m);
+      m &= m - 1;
+      const uint32_t len = ((mid3 >> b) & 1u) ? 3u : 2u, pos = 64 * lane + b;
+      // mid lead bits at offsets -2 (2-byte char) / -3 (3-byte char) and +len
+      const auto midat = [&](int o, bool three) -> bool {
+        const int q = (int)b + o;
+        const uint64_t mm = three ? (q < 0 ? P3 : mid3) : (q < 0 ? P : (q < 64 ? mid : N));
+        const uint32_t qq = (uint32_t)(q < 0 ? q + 64 : (q < 64 ? q : q - 64));
+        return (mm >> qq) & 1u;
+      };
+      const uint32_t pb = pos ? text[pos - 1] : 0u, nb = text[pos + len];
+      const bool pmid = pb >= 0x80u && (midat(-2, false) || midat(-3, true));
+      const bool nmid = nb >= 0x80u && midat((int)len, false);
+      const bool pl = (pb >= 0x80u && !pmid) || ((pb | 0x20u) - 0x61u < 26u);
+      const bool nl = (nb >= 0x80u && !nmid) || ((nb | 0x20u) - 0x61u < 26u);
+      const bool pd = pb - 0x30u < 10u, nd = nb - 0x30u < 10u;
+      const bool join = (((ml >> b) & 1u) && pl && nl) || (((mn >> b) & 1u) && pd && nd);
+      if (!join) drop |= 1ull << b;
+    }
+    __syncthreads();                                    // every decision read the window as it was
+    while (drop) {
+      const uint32_t b = (uint32_t)__builtin_ctzll(drop);
+      drop &= drop - 1;
+      const uint32_t len = ((mid3 >> b) & 1u) ? 3u : 2u, pos = 64 * lane + b;
+      for (uint32_t i = 0; i < len; i++) text[pos + i] = 0x20u;
+    }
+    __syncthreads();
+  }
+  return true;
 }
 
 // Units: PACK = false, one document per unit (documents 0..n_docs-1, or the
@@ -1645,15 +1645,36 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     bool upper;
     uint64_t W;
     if constexpr (UNI) {
-      // flagged document: the prose check rewrites the staged window, which is
-      // then classified from LDS (the next window's fetch goes out first)
-      if (un < ulim) { meta = unit_meta<PACK>(p, un, lane); prefetch_wave(p, meta, lane, v); }
-      uint64_t jl, jd;
-      if (!uni_window_prose(sm.text, shift + (uint32_t)L, lane, simple2, other2, punct, &jl, &jd)) continue;
+      // flagged document: the prose check rewrites the staged window, whose
+      // chunks are read back into the registers (lane l: chunks l + 64 k, no
+      // bank conflicts) and classified there as an ASCII window is; then the
+      // next window's fetch goes out
+      // (round 6 first form: classified from LDS by 64-byte lane segments,
+      // with the mid chars joined in the classifier — 2.3 ms of cfg-2 prose
+      // in that step alone, the strided 16 B reads' bank conflicts)
+#pragma unroll
+      for (int k = 0; k < 4; k++) v[k] = make_uint4(0, 0, 0, 0);   // (staged: no registers held over the check)
+      bool na;                                              // (UNI-first builds: ASCII documents come here too)
+      const bool pass = uni_window_prose(sm.text, shift + (uint32_t)L, lane, simple2, other2, punct, &na);
+      if (!pass || p.debug_stop == 5) {                     // (profiling stops 5, 6: this pass's phases)
+        if (un < ulim) { meta = unit_meta<PACK>(p, un, lane); prefetch_wave(p, meta, lane, v); }
+        if (pass && lane == 0) TFIDF_COLD(uni_list)[d] = 0u;
+        continue;
+      }
       if (lane == 0) TFIDF_COLD(uni_list)[d] = 0u;           // taken here (else: k_tokenize_uwave)
-      my_uni += lane == 0;
-      W = lane_word_mask<false, true>(sm.text, lane, &bad, &under, &wbase, &upper, jl, jd);
+      my_uni += lane == 0 && na;
+      __syncthreads();                                      // (one wave) the window's rewrites are visible
+      {
+        const uint4 *src = reinterpret_cast<const uint4 *>(sm.text);
+#pragma unroll
+        for (int k = 0; k < 4; k++) v[k] = src[lane + 64 * k];
+      }
+      const uint32_t nrows = (shift + (uint32_t)L + 1023) >> 10;
+      uint16_t *wm16 = reinterpret_cast<uint16_t *>(sm.qkey);            // (histogram queue: written before read)
+      W = regs_word_mask<false, true>(v, nrows, sm.text, wm16, wm16 + 256, lane, &bad, &under, &wbase, &upper);
       bad = false;
+      if (un < ulim) { meta = unit_meta<PACK>(p, un, lane); prefetch_wave(p, meta, lane, v); }
+      if (p.debug_stop == 6) continue;
     } else {
       // a byte >= 0x80 (in the staged registers): the document goes to the UNI
       // pass unclassified (nrows 0; flagged below as `bad`)
@@ -1760,13 +1781,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     for (uint32_t tb = 0; tb < ntok && !overflow;) {       // batch width by what is left
       const uint32_t rem = ntok - tb;
       if (anylong) {
-        if (TFIDF_HIST10 && !PACK && rem > 512 && rem <= 640) { hist2<10, true, PACK, UNI>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 640; }
+        if (TFIDF_HIST10 && !PACK && !UNI && rem > 512 && rem <= 640) { hist2<10, true, PACK, UNI>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 640; }
         else if (rem > 256) { hist2<8, true, PACK, UNI>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 512; }
         else if (rem > 128) { hist2<4, true, PACK, UNI>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 256; }
         else { hist2<2, true, PACK, UNI>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 128; }
       } else {
         // 513..640 tokens (U[400, 600]-token documents: ~40 % of cfg 2) in one batch
-        if (TFIDF_HIST10 && !PACK && rem > 512 && rem <= 640) { hist2<10, false, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 640; }
+        if (TFIDF_HIST10 && !PACK && !UNI && rem > 512 && rem <= 640) { hist2<10, false, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 640; }
         else if (rem > 256) { hist2<8, false, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 512; }
         else if (rem > 128) { hist2<4, false, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 256; }
         else { hist2<2, false, PACK>(sm, lane, tb, ntok, under, upper, nu, len, overflow); tb += 128; }
@@ -1988,9 +2009,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     // (a flag per unit, counted once per wave at the end — a list appended
     // with one atomic per unit serialised 15 k units on one counter)
     const bool nonascii = __any((hib & 0x80808080u) != 0);
-    uint64_t jl = 0, jd = 0;
     if (UNI && nonascii) {                                     // simple non-ASCII text: taken here
-      if (!uni_window_prose(sm.text, m.shift + (uint32_t)m.L, lane, simple2, other2, punct, &jl, &jd))
+      if (!uni_window_prose(sm.text, m.shift + (uint32_t)m.L, lane, simple2, other2, punct))
         continue;                                              // k_tokenize_uchunk
       if (lane == 0) p.uchunk_list[u] = 0u;
     } else if (nonascii) {
@@ -2003,7 +2023,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     bool bad, under;
     uint64_t wbase = 0;
     bool upper;
-    const uint64_t W = lane_word_mask<false, UNI>(sm.text, lane, &bad, &under, &wbase, &upper, jl, jd);
+    const uint64_t W = lane_word_mask<false, UNI>(sm.text, lane, &bad, &under, &wbase, &upper);
     const uint64_t wlast = __ballot((W >> 63) & 1ull);
     const uint64_t prevW = lane ? (wlast >> (lane - 1)) & 1ull : 0ull;
     const uint64_t S = W & ~((W << 1) | prevW);

@@ -449,6 +449,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     const uint64_t L = p.offsets[src + 1] - s0;
     if (L > kUwWindow || R > kUwMaxRanges) {                // wave-uniform
       if (lane == 0) p.long_list[atomicAdd(p.long_count, 1u)] = d;
+      if (L > kUwWindow) my_uni--;                          // (UNI-first builds flag long documents too: a long
+                                                            // document is not counted as non-ASCII, as the ASCII pass has it)
       continue;
     }
     // ---- stage (aligned 16 B loads); the table is empty here

@@ -205,11 +205,18 @@ class DeviceCorpus:
                 z += 1
             t = text[a:z]
             is_l = (t >= 97) & (t <= 122)
-            prev = np.concatenate(([False], is_l[:-1]))
-            nxt = np.concatenate((is_l[1:], [False]))
+            # documents are concatenated without separators: a word never runs
+            # across a document start, and the first word of a document is
+            # left alone (offset -1 would write into the document before, and a
+            # multi-byte character split over two documents is malformed UTF-8)
+            ds = offs[(offs > a) & (offs < z)].astype(np.int64) - a
+            dstart = np.zeros(len(t), bool)
+            dstart[ds] = True
+            prev = np.concatenate(([False], is_l[:-1])) & ~dstart
+            nxt = np.concatenate((is_l[1:], [False])) & ~np.concatenate((dstart[1:], [False]))
             st = np.nonzero(is_l & ~prev)[0]
             en = np.nonzero(is_l & ~nxt)[0] + 1
-            ok = (en - st >= 4) & (st >= 1)
+            ok = (en - st >= 4) & (st >= 1) & ~dstart[st]
             st, en = st[ok], en[ok]
             u = rng.random(st.size)
             cat = np.searchsorted(cum, u, side="right")
