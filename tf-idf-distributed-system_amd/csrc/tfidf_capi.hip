@@ -2828,11 +2828,10 @@ static int vocab_reduce_dev(tfidf_index *ix, const void *d_records, uint64_t n, 
   HIP_TRY(hipMemsetAsync(ix->vt_table.p, 0, T * 16, s));
   HIP_TRY(hipMemsetAsync(ix->vt_sum.p, 0, T * 4, s));
   HIP_TRY(ix->vnu.reserve(64));
-  unsigned long long *nu = reinterpret_cast<unsigned long long *>(ix->vnu.p);
+  unsigned long long *nu = reinterpret_cast<unsigned long long *>(d_n_unique ? d_n_unique : ix->vnu.p);   // counted in place
   HIP_TRY(hipMemsetAsync(nu, 0, 8, s));
   HIP_TRY(vocab_reduce((const uint64_t *)d_records, n, ix->vt_table.as<uint64_t>(), (uint32_t)(T - 1),
                        ix->vt_sum.as<uint32_t>(), ix->vt_rslot.as<uint32_t>(), (uint32_t *)d_df_out, nu, s));
-  if (d_n_unique) HIP_TRY(hipMemcpyAsync(d_n_unique, nu, 8, hipMemcpyDeviceToDevice, s));
   return sync ? exchange_done(ix) : TFIDF_OK;          // asynchronous on a caller's stream
 }
 extern "C" int tfidf_vocab_reduce_device(tfidf_index *ix, const void *d_records, uint64_t n, void *d_df_out,
