@@ -1655,10 +1655,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
 #pragma unroll
       for (int k = 0; k < 4; k++) v[k] = make_uint4(0, 0, 0, 0);   // (staged: no registers held over the check)
       bool na;                                              // (UNI-first builds: ASCII documents come here too)
-      // (profiling stop 7: no prose check — the window taken as it is, tokens
-      // then differ; the check's cost is the difference to a full build)
-      na = true;
-      const bool pass = p.debug_stop == 7 || uni_window_prose(sm.text, shift + (uint32_t)L, lane, simple2, other2, punct, &na);
+      const bool pass = uni_window_prose(sm.text, shift + (uint32_t)L, lane, simple2, other2, punct, &na);
       if (!pass || p.debug_stop == 5) {                     // (profiling stops 5, 6: this pass's phases)
         if (un < ulim) { meta = unit_meta<PACK>(p, un, lane); prefetch_wave(p, meta, lane, v); }
         if (pass && lane == 0) TFIDF_COLD(uni_list)[d] = 0u;

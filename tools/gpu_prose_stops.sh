@@ -10,6 +10,6 @@ run() {
   rc=$?; [ $rc -ne 0 ] && { tail -5 gpurun_out/prst_$1_$2.err; return $rc; }
   python3 -c "import json; r=json.loads(open('gpurun_out/prst_$1_$2.log').read().strip().splitlines()[-1]); print('prose $1 stop $2 tokenize %.2f' % r['phases_ms']['ms_tokenize'])"
 }
-for st in 7 5 6 2 3 4 0; do run 1 $st || exit $?; done
+for st in 5 6 2 3 4 0; do run 1 $st || exit $?; done
 TFIDF_NO_UNIFIRST=1 run 1 0 || exit $?
 for st in 1 2 0; do run 0 $st || exit $?; done
