@@ -1118,14 +1118,15 @@ __device__ __noinline__ uint64_t uni_find_verify(uint64_t *dict, uint32_t mask, 
 // UNI: dictionary key of a short table key holding a non-ASCII byte (the
 // token's lower-cased bytes, <= 7 of them: an exact key, no identity check,
 // so no occurrence is needed).
-__device__ __noinline__ void uni_key_from_short(uint64_t key, uint64_t *lo, uint64_t *hi) {
-  KeyBuilder kb;
-  for (uint32_t i = 0; i < 8; i++) {
-    const uint8_t c = (uint8_t)(key >> (8 * i));
-    if (!c) break;
-    kb.push(c);
-  }
-  kb.finish(lo, hi, 0);
+__device__ __forceinline__ void uni_key_from_short(uint64_t key, uint64_t *lo, uint64_t *hi) {
+  // KeyBuilder over the key's bytes, in closed form: a non-ASCII key of <= 7
+  // bytes takes KeyBuilder::finish's exact branch (w0 = the bytes, w1 = 0).
+  // (Inline: the call it replaces saved the resolve phase's live registers
+  // to scratch around every folded term.)
+  const uint64_t n = key ? (uint64_t)((71 - __builtin_clzll(key)) >> 3) : 0ull;
+  const uint64_t r = (key >> 63) | (n << 49);
+  *lo = kLoLong | kLoUniExact | (r & ((1ull << 47) - 1)) | ((r >> 47) << 48);
+  *hi = (key & ~kKeyValid) | kKeyValid;
 }
 
 // The document passed uni_simple_char, so its non-ASCII chars are their own
@@ -1195,8 +1196,14 @@ __device__ __forceinline__ void resolve_terms(WaveSmem &sm, const BuildParams &p
       }
       uint32_t gg;
       if (UNI) {
-        gg = kInvalidSlot;
-        if (fa) {
+        // exact keys (non-ASCII terms of <= kExactUniChars bytes: nearly all)
+        // by the inline probe, all lanes together; hashed ones by the verifying
+        // lookup (a call: the caller's live registers go to scratch around it —
+        // cfg-2 prose with every term through it: 750 VMEM instructions per
+        // document against the ASCII pass's 22, SQ counters)
+        const bool hashed = fa && (flo & kLoHashed);
+        gg = dict_find_or_insert(p.dict, dmask, flo, fhi, fa && !hashed);
+        if (__any(hashed) && hashed) {
           const uint64_t res = uni_find_verify(p.dict, dmask, flo, fhi, mine, p.text, sm.text,
                                                (uint32_t)(sm.key[slots[lane + 64 * k]] >> 13) & 0x1FFFu);
           gg = (uint32_t)res;
