@@ -2017,6 +2017,30 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) k_
     // with one atomic per unit serialised 15 k units on one counter)
     const bool nonascii = __any((hib & 0x80808080u) != 0);
     if (UNI && nonascii) {                                     // simple non-ASCII text: taken here
+      // A window that starts or ends inside its document can cut a multi-byte
+      // char in its margin: those bytes are blanked (class Other) — they lie
+      // 64 bytes before the core or 320 after it, so the core's tokens keep
+      // their boundaries (round 6: prose books sent such units to
+      // k_tokenize_uchunk, ~0.36 ms)
+      if (lane == 0) {
+        const uint64_t src = p.live_map ? p.live_map[m.d] : m.d;
+        uint8_t *t = sm.text + m.shift;
+        const uint32_t L = (uint32_t)m.L;
+        if (m.s0 > p.offsets[src])
+          for (uint32_t i = 0; i < 3 && i < L && (t[i] & 0xC0u) == 0x80u; i++) t[i] = 0;
+        if (m.s0 + m.L < p.offsets[src + 1])
+          for (uint32_t j = 1; j <= 3 && j <= L; j++) {
+            const uint32_t c = t[L - j];
+            if ((c & 0xC0u) == 0xC0u) {                        // the last lead: is its char complete?
+              const uint32_t need = c >= 0xF0u ? 4u : (c >= 0xE0u ? 3u : 2u);
+              if (need > j)
+                for (uint32_t i = L - j; i < L; i++) t[i] = 0;
+              break;
+            }
+            if ((c & 0x80u) == 0) break;
+          }
+      }
+      __syncthreads();
       if (!uni_window_prose(sm.text, m.shift + (uint32_t)m.L, lane, simple2, other2, punct))
         continue;                                              // k_tokenize_uchunk
       if (lane == 0) p.uchunk_list[u] = 0u;
