@@ -1326,50 +1326,74 @@ __global__ void __launch_bounds__(kWunitWaves * 64) k_score_wunits(QueryParams p
       const uint32_t rsh = np == 1 ? 13u : 9u;
       for (uint32_t ps = 0; ps < np; ps++) {
         uint32_t nlist = 0;
-        auto insert = [&](uint32_t e, bool in, float wj, uint64_t i) {
-          uint32_t claimed = kPairEmpty;
-          if (in) {
-            uint32_t ld, tf, nrm;
-            post_decode<false>(p, e, i, d0, &ld, &tf, &nrm);
-            if ((ld >> rsh) == ps) {
-              const float sc = bm25_term(wj, tf, sm.cache[nrm]);
-              uint32_t s = (ld * 0x9E3779B1u) >> 22;
-              for (;;) {
-                const uint32_t old = atomicCAS(&key[s], kPairEmpty, ld);
-                if (old == kPairEmpty) { val[s] = (double)sc; claimed = s; break; }
-                if (old == ld) { val[s] += (double)sc; break; }
-                s = (s + 1) & (kPairSlots - 1);
+        // N postings per lane of one term (distinct documents): their first
+        // table probes (CAS) all issued before any result is used — one LDS
+        // round trip per N postings instead of per posting — then the rare
+        // collisions probe on one at a time
+        auto insert = [&](auto const &e, auto const &in, float wj, uint64_t i0, uint32_t stride) {
+          constexpr int N = sizeof(e) / sizeof(e[0]);
+          uint32_t ld[N], s[N], old[N];
+          float sc[N];
+          bool act[N];
+#pragma unroll
+          for (int v = 0; v < N; v++) {
+            act[v] = false;
+            ld[v] = 0;
+            s[v] = 0;
+            sc[v] = 0.f;
+            if (in[v]) {
+              uint32_t tf, nrm;
+              post_decode<false>(p, e[v], i0 + (uint64_t)stride * v, d0, &ld[v], &tf, &nrm);
+              if ((ld[v] >> rsh) == ps) {
+                sc[v] = bm25_term(wj, tf, sm.cache[nrm]);
+                s[v] = (ld[v] * 0x9E3779B1u) >> 22;
+                act[v] = true;
               }
             }
           }
-          const bool c = claimed != kPairEmpty;
-          const uint64_t m = __ballot(c);
-          if (c) list[nlist + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint16_t)claimed;
-          nlist += (uint32_t)__popcll(m);
+#pragma unroll
+          for (int v = 0; v < N; v++) old[v] = act[v] ? atomicCAS(&key[s[v]], kPairEmpty, ld[v]) : 0u;
+#pragma unroll
+          for (int v = 0; v < N; v++) {
+            uint32_t claimed = kPairEmpty;
+            if (act[v]) {
+              uint32_t o = old[v], sl = s[v];
+              for (;;) {
+                if (o == kPairEmpty) { val[sl] = (double)sc[v]; claimed = sl; break; }
+                if (o == ld[v]) { val[sl] += (double)sc[v]; break; }
+                sl = (sl + 1) & (kPairSlots - 1);
+                o = atomicCAS(&key[sl], kPairEmpty, ld[v]);
+              }
+            }
+            const bool c = claimed != kPairEmpty;
+            const uint64_t m = __ballot(c);
+            if (c) list[nlist + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint16_t)claimed;
+            nlist += (uint32_t)__popcll(m);
+          }
         };
         for (uint32_t j = 0; j < nt; j++) {
           const uint64_t ja = readlane64(a, j), jz = readlane64(z, j);
           const float wj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tw), (int)j));
           uint64_t i0 = ja;
           if (ps == 0 && j < kQTermsFast) {
-            uint32_t e0 = pre[0][0], e1 = pre[0][1];
+            uint32_t e2[2] = {pre[0][0], pre[0][1]};
 #pragma unroll
             for (uint32_t jj = 1; jj < kQTermsFast; jj++)
-              if (jj == j) { e0 = pre[jj][0]; e1 = pre[jj][1]; }
-            insert(e0, ja + lane < jz, wj, ja + lane);
-            if (ja + 64 < jz) insert(e1, ja + 64 + lane < jz, wj, ja + 64 + lane);     // uniform
+              if (jj == j) { e2[0] = pre[jj][0]; e2[1] = pre[jj][1]; }
+            const bool in2[2] = {ja + lane < jz, ja + 64 + lane < jz};
+            insert(e2, in2, wj, ja + lane, 64);
             i0 = ja + 128;
           }
           for (; i0 < jz; i0 += 256) {
             uint32_t e[4];
+            bool in4[4];
 #pragma unroll
             for (int v = 0; v < 4; v++) {
               const uint64_t i = i0 + 64 * v + lane;
-              e[v] = i < jz ? p.post32[i] : 0u;
+              in4[v] = i < jz;
+              e[v] = in4[v] ? p.post32[i] : 0u;
             }
-#pragma unroll
-            for (int v = 0; v < 4; v++)
-              if (i0 + 64 * v < jz) insert(e[v], i0 + 64 * v + lane < jz, wj, i0 + 64 * v + lane);
+            insert(e, in4, wj, i0 + lane, 64);
           }
         }
         if (ps + 1 == np) {                                       // next block's loads in flight during the walk

@@ -1969,8 +1969,10 @@ static int run_scoring(tfidf_index *ix, Snapshot &S, StatsView &V, SearchCtx &X,
       HIP_TRY(hipStreamWaitEvent(ws, X.q_ev[0], 0));
     }
     if (n_wunits) {
+      uint32_t wper_cu = kWunitWGsPerCU;
+      if (const char *e = knob("TFIDF_WUNIT_WG_PER_CU")) wper_cu = (uint32_t)std::max(1, atoi(e));   // A/B
       const int grid = (int)std::min<uint64_t>((n_wunits + kWunitWavesPerWG - 1) / kWunitWavesPerWG,
-                                               (uint64_t)ix->num_cus * kWunitWGsPerCU);
+                                               (uint64_t)ix->num_cus * wper_cu);
       HIP_TRY(launch_score_wunits(qp, ud, n_wunits, ctr, grid, ws));
     }
     if (n_gunits) {
@@ -2251,6 +2253,11 @@ extern "C" int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const 
   // 10 k queries at cfg 2 (tools/gpu_batch_ab.sh): 1 chunk 7.6 ms end to end
   // (prepare 1.5 on the pool, device 5.65), 2 chunks 7.0 (device 6.05), 4
   // chunks 7.45 (device 6.9: every chunk pays the unit kernels' tail)
+  // Chunks interleave the queries (chunk c: queries c, c + n_chunks, ...), so
+  // each holds the batch's mix of heavy (k_score_units) and light
+  // (k_score_wunits) queries and its two concurrent kernels end together
+  // (round 6; a contiguous split gave cfg 2's two chunks 3.0 / 1.4 ms and
+  // 1.2 / 2.6 ms of heavy / light work: 5.6 ms device)
   uint32_t n_chunks = n_q >= 4096 ? 2 : 1;
   if (const char *e = knob("TFIDF_BATCH_CHUNKS")) n_chunks = (uint32_t)std::max(1, std::min(atoi(e), 64));
   n_chunks = std::max(1u, std::min(n_chunks, n_q));
@@ -2258,13 +2265,27 @@ extern "C" int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const 
   HIP_TRY(X.q_res.resize(words));
   double t_prep = 0, t_sub = 0;
   bool any = false;
-  uint32_t c0 = 0;
+  uint32_t c0 = 0;                                       // results of chunk c start at row c0
+  std::vector<uint8_t> cq;                               // chunk c's queries, contiguous
+  std::vector<uint64_t> co;
   for (uint32_t c = 0; c < n_chunks; c++) {
-    const uint32_t c1 = (uint32_t)(((uint64_t)n_q * (c + 1) + n_chunks - 1) / n_chunks);
-    const uint32_t nc = c1 - c0;                         // the first chunk is the largest (ceil split)
+    const uint32_t nc = (n_q - c + n_chunks - 1) / n_chunks;   // the first chunk is the largest
     const auto ta = clk::now();
+    const uint8_t *cu = q_utf8;
+    const uint64_t *coffs = q_offsets;
+    if (n_chunks > 1) {
+      cq.clear();
+      co.assign(1, 0);
+      for (uint32_t i = 0; i < nc; i++) {
+        const uint32_t q = c + i * n_chunks;
+        cq.insert(cq.end(), q_utf8 + q_offsets[q], q_utf8 + q_offsets[q + 1]);
+        co.push_back(cq.size());
+      }
+      cu = cq.data();
+      coffs = co.data();
+    }
     QueryBatch qb;
-    if (int e = prepare_batch(ix, S, V, q_utf8, q_offsets + c0, nc, &qb)) { X.q_rec_start = true; return e; }
+    if (int e = prepare_batch(ix, S, V, cu, coffs, nc, &qb)) { X.q_rec_start = true; return e; }
     const auto tb = clk::now();
     uint32_t *hres = X.q_res.data() + (size_t)2 * c0 * k + c0;
     if (qb.slot.empty()) {
@@ -2279,7 +2300,7 @@ extern "C" int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const 
     }
     t_prep += std::chrono::duration<double, std::milli>(tb - ta).count();
     t_sub += std::chrono::duration<double, std::milli>(clk::now() - tb).count();
-    c0 = c1;
+    c0 += nc;
   }
   const auto t2 = clk::now();
   HIP_TRY(hipStreamSynchronize(s));
@@ -2287,12 +2308,15 @@ extern "C" int tfidf_search_batch(tfidf_index *ix, const uint8_t *q_utf8, const 
   const auto t3 = clk::now();
   c0 = 0;
   for (uint32_t c = 0; c < n_chunks; c++) {
-    const uint32_t c1 = (uint32_t)(((uint64_t)n_q * (c + 1) + n_chunks - 1) / n_chunks), nc = c1 - c0;
+    const uint32_t nc = (n_q - c + n_chunks - 1) / n_chunks;
     const uint32_t *hres = X.q_res.data() + (size_t)2 * c0 * k + c0;
-    memcpy(doc_ids + (size_t)c0 * k, hres, (size_t)nc * k * 4);
-    memcpy(scores + (size_t)c0 * k, hres + (size_t)nc * k, (size_t)nc * k * 4);
-    memcpy(counts + c0, hres + (size_t)2 * nc * k, (size_t)nc * 4);
-    c0 = c1;
+    for (uint32_t i = 0; i < nc; i++) {
+      const uint32_t q = c + i * n_chunks;
+      memcpy(doc_ids + (size_t)q * k, hres + (size_t)i * k, (size_t)k * 4);
+      memcpy(scores + (size_t)q * k, hres + (size_t)nc * k + (size_t)i * k, (size_t)k * 4);
+      counts[q] = hres[(size_t)2 * nc * k + i];
+    }
+    c0 += nc;
   }
   const float ms_total = any ? qev_ms(X, QEV_0, QEV_2) : 0.0f;
   set_last_ms(ix, any ? qev_ms(X, QEV_0, QEV_1) : 0.0f, ms_total);

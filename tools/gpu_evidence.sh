@@ -10,7 +10,7 @@
 export TFIDF_DEBUG=1   # the library reads its TFIDF_* knobs only under TFIDF_DEBUG
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R
-TAG=${TAG:-r05}; O=$R/gpurun_out/ev_$TAG; mkdir -p $O
+TAG=${TAG:-r06}; O=$R/gpurun_out/ev_$TAG; mkdir -p $O
 TAG=$TAG SQ=1 bash tools/prof_round.sh > $O/prof_round.log 2>&1 || { echo "prof_round failed"; tail -5 $O/prof_round.log; exit 1; }
 tail -3 $O/prof_round.log
 TJ=$R/gpurun_out/prof_$TAG/traffic.json
@@ -27,6 +27,10 @@ run bench_line_book_unicode 200 --steps 10 --warmup 2 --docs 300 --len-min 80000
 TFIDF_NO_UCHUNK=1 run bench_line_book_unicode_whole_book 200 --steps 10 --warmup 2 --docs 300 --len-min 80000 --len-max 120000 --unicode-every 2048 --no-queries --no-e2e --cpu-sample 0
 run bench_line_cfg2_unicode10 200 --steps 5 --warmup 2 --unicode-frac 0.1 --no-queries --no-e2e --cpu-sample 0
 run bench_line_cfg2_unicode100 300 --steps 3 --warmup 1 --unicode-frac 1.0 --no-queries --no-e2e --cpu-sample 0
+run bench_line_cfg2_prose 300 --steps 10 --warmup 2 --prose 1 --no-queries --no-e2e --cpu-sample 0
+TFIDF_NO_UNIFIRST=1 run bench_line_cfg2_prose_ascii_first 300 --steps 10 --warmup 2 --prose 1 --no-queries --no-e2e --cpu-sample 0
+TFIDF_NO_UNIWAVE=1 run bench_line_cfg2_prose_uwave_only 300 --steps 5 --warmup 1 --prose 1 --no-queries --no-e2e --cpu-sample 0
+run bench_line_books_prose 200 --steps 10 --warmup 2 --docs 300 --len-min 80000 --len-max 120000 --prose 1 --no-queries --no-e2e --cpu-sample 0
 # cfg-5 PMC: one build, FETCH / WRITE passes, kernel summary
 P=$R/gpurun_out/prof_cfg5_$TAG; mkdir -p $P
 cd /tmp && export TMPDIR=/tmp
