@@ -30,6 +30,7 @@ run bench_line_cfg2_unicode100 300 --steps 3 --warmup 1 --unicode-frac 1.0 --no-
 run bench_line_cfg2_prose 300 --steps 10 --warmup 2 --prose 1 --no-queries --no-e2e --cpu-sample 0
 TFIDF_NO_UNIFIRST=1 run bench_line_cfg2_prose_ascii_first 300 --steps 10 --warmup 2 --prose 1 --no-queries --no-e2e --cpu-sample 0
 TFIDF_NO_UNIWAVE=1 run bench_line_cfg2_prose_uwave_only 300 --steps 5 --warmup 1 --prose 1 --no-queries --no-e2e --cpu-sample 0
+TFIDF_BENCH_NODE=1 run bench_line_node1 300 --steps 5 --warmup 2 --cpu-sample 0 --no-e2e
 run bench_line_books_prose 200 --steps 10 --warmup 2 --docs 300 --len-min 80000 --len-max 120000 --prose 1 --no-queries --no-e2e --cpu-sample 0
 # cfg-5 PMC: one build, FETCH / WRITE passes, kernel summary
 P=$R/gpurun_out/prof_cfg5_$TAG; mkdir -p $P
