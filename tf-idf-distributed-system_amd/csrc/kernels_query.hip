@@ -1249,10 +1249,15 @@ hipError_t launch_score_units(const QueryParams &p, const uint4 *units, uint32_t
 constexpr uint32_t kWunitWaves = kPairWavesPerWG;
 constexpr uint32_t kWunitPassPost = 700;
 
+#ifndef TFIDF_WUNIT_LIST
+#define TFIDF_WUNIT_LIST 0   // 1: round-5 claim list (29 KiB per workgroup, 5 per CU) — A/B
+#endif
 struct WunitSmem {
   uint32_t key[kWunitWaves][kPairSlots];          // doc - d0 per slot (kPairEmpty = free)
   double val[kWunitWaves][kPairSlots];
+#if TFIDF_WUNIT_LIST
   uint16_t list[kWunitWaves][kPairSlots];         // claimed slots of the current pass
+#endif
   float cache[256];
 };
 
@@ -1264,7 +1269,9 @@ __global__ void __launch_bounds__(kWunitWaves * 64) k_score_wunits(QueryParams p
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) sm.cache[i] = p.cache[i];
   uint32_t *key = sm.key[w];
   double *val = sm.val[w];
+#if TFIDF_WUNIT_LIST
   uint16_t *list = sm.list[w];
+#endif
   {
     uint4 *kw = reinterpret_cast<uint4 *>(key);
 #pragma unroll
@@ -1365,10 +1372,14 @@ __global__ void __launch_bounds__(kWunitWaves * 64) k_score_wunits(QueryParams p
                 o = atomicCAS(&key[sl], kPairEmpty, ld[v]);
               }
             }
+#if TFIDF_WUNIT_LIST
             const bool c = claimed != kPairEmpty;
             const uint64_t m = __ballot(c);
             if (c) list[nlist + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint16_t)claimed;
             nlist += (uint32_t)__popcll(m);
+#else
+            (void)claimed;
+#endif
           }
         };
         for (uint32_t j = 0; j < nt; j++) {
@@ -1402,6 +1413,7 @@ __global__ void __launch_bounds__(kWunitWaves * 64) k_score_wunits(QueryParams p
           if (b + 2 < bend) segment(b + 2, &na, &nz);
           if (b + 1 < bend) prefetch(a, z, pre);
         }
+#if TFIDF_WUNIT_LIST
         for (uint32_t h = 0; h < nlist; h += 64) {
           const uint32_t idx = h + lane;
           uint64_t kv = 0;
@@ -1413,6 +1425,35 @@ __global__ void __launch_bounds__(kWunitWaves * 64) k_score_wunits(QueryParams p
           }
           topk_insert(__ballot(kv > theta), kv, tk, theta, k, lane);
         }
+#else
+        // walk the table itself: lane l owns slots [16 l, 16 l + 16), read as
+        // four 16 B pieces in an order rotated by l / 2 (conflict-free), then
+        // its occupied slots one per step; each is reset as it is read.  No
+        // claim list: the workgroup's LDS is 25 KiB, six per CU instead of five
+        (void)nlist;
+        uint32_t occ = 0;
+        {
+          const uint4 *kq = reinterpret_cast<const uint4 *>(key + 16 * lane);
+#pragma unroll
+          for (uint32_t q = 0; q < 4; q++) {
+            const uint32_t qq = (q + (lane >> 1)) & 3u;
+            const uint4 t = kq[qq];
+            occ |= ((uint32_t)(t.x != kPairEmpty) | ((uint32_t)(t.y != kPairEmpty) << 1) |
+                    ((uint32_t)(t.z != kPairEmpty) << 2) | ((uint32_t)(t.w != kPairEmpty) << 3)) << (4 * qq);
+          }
+        }
+        while (__any(occ != 0)) {
+          uint64_t kv = 0;
+          if (occ) {
+            const uint32_t sl = 16 * lane + (uint32_t)__builtin_ctz(occ);
+            occ &= occ - 1;
+            const uint32_t ld = key[sl];
+            kv = ((uint64_t)__float_as_uint((float)val[sl]) << 32) | (uint64_t)(~(d0 + ld));
+            key[sl] = kPairEmpty;
+          }
+          topk_insert(__ballot(kv > theta), kv, tk, theta, k, lane);
+        }
+#endif
       }
     }
     const bool has = lane < k && tk != 0;

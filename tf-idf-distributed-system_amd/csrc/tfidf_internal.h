@@ -378,7 +378,7 @@ hipError_t launch_score_units(const QueryParams &p, const uint4 *units, uint32_t
                               hipStream_t s);
 // light queries of such batches: wave per unit (hash table per block)
 constexpr uint32_t kWunitWavesPerWG = kPairWavesPerWG;
-constexpr uint32_t kWunitWGsPerCU = 5;    // ~28 KiB LDS each
+constexpr uint32_t kWunitWGsPerCU = 6;    // 25 KiB LDS each (round 6: no claim list; 5 at 29 KiB before)
 constexpr uint32_t kWunitLightPost = 550; // postings per block (query average) up to which a query is light (400: batch 5.80 ms, 500: 5.62, 600: 5.53, 700: 6.6 — past kWunitPassPost blocks take 16 passes;
                                           // round 5, 10 k queries at cfg 2: 450 / 500 / 550 / 600 / 650 / 700 = 5.95 / 5.94 / 5.52 / 5.53 / 5.69 / 6.53 ms device; 550 keeps a margin from the cliff)
 hipError_t launch_score_wunits(const QueryParams &p, const uint4 *units, uint32_t n_units, uint32_t *unit_ctr, int grid,
