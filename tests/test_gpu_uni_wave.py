@@ -260,3 +260,40 @@ def test_uni_first_recommit_equals_oracle(monkeypatch, unifirst):
             assert_hits_equal(g.search(qb, kk), o.search(qb, kk))
     g.close()
     o.close()
+
+
+def test_prose_chars_cut_by_chunk_windows_equal_oracle():
+    """Round 6: a book unit's window (64 B before its 2 KB core, 320 B after)
+    that cuts a multi-byte character in its margin blanks the cut bytes
+    instead of declining the unit.  Books with a 2-, 3- or 4-byte character
+    at every offset around each window edge (and around the core edges),
+    inside words and between them: tokens equal the oracle's."""
+    rng = random.Random(211)
+    chars = ["’", "—", "é", "É", "…", " ", "·", "𝐀"]
+    texts = []
+    for b in range(12):
+        n = 9000 + 500 * b
+        buf = bytearray()
+        while len(buf) < n:
+            buf += synth.word(rng.randint(1, 3000)) + b" "
+        buf = buf[:n]
+        edges = []
+        for k in range(1, n // 2048 + 1):
+            edges += [2048 * k - 64, 2048 * k, 2048 * k + 2048 + 320, 2048 * k + 2048]
+        ch = chars[b % len(chars)].encode()
+        last = -10
+        for e in sorted(set(edges)):
+            p = e - rng.randint(0, len(ch)) - (b % 3)          # the char straddles (or touches) the edge
+            if max(1, last + 1) <= p and p + len(ch) < len(buf) - 1:
+                buf[p:p + len(ch)] = ch
+                last = p + len(ch)
+        t = bytes(buf)
+        t.decode()                                             # still well-formed UTF-8
+        texts.append(t)
+    texts += [doc(rng, rng.randint(20, 200), 2, PROSE) for _ in range(50)]
+    g, o = build_pair(texts)
+    check(g, o, texts)
+    st = g.stats()
+    assert st["long_chunked"] == st["long_docs"] >= 12
+    g.close()
+    o.close()
