@@ -342,7 +342,7 @@ struct tfidf_index {
   hipEvent_t ev[EV_N];
   // side stream for the dictionary's host mirror: its D2H copy overlaps the inversion
   hipStream_t copy_stream = nullptr;
-  hipEvent_t mir_ev[2];            // [0] dictionary final (main stream), [1] mirror copied
+  hipEvent_t mir_ev[3];            // [0] dictionary final (main stream), [1] mirror copied, [2] df final
   int num_cus = 256;
 
   // published snapshot (searches) and the one a commit may rebuild in place
@@ -512,7 +512,7 @@ extern "C" int tfidf_create(const tfidf_config *cfg, tfidf_index **out) {
   }
   for (int i = 0; i < EV_N; i++) hipEventCreate(&ix->ev[i]);
   for (int i = 0; i < 2; i++) hipEventCreateWithFlags(&ix->stage_ev[i], hipEventDisableTiming);
-  for (int i = 0; i < 2; i++) hipEventCreateWithFlags(&ix->mir_ev[i], hipEventDisableTiming);
+  for (int i = 0; i < 3; i++) hipEventCreateWithFlags(&ix->mir_ev[i], hipEventDisableTiming);
   ix->text = std::make_shared<DevMem>(cfg->device);
   ix->offsets = std::make_shared<DevMem>(cfg->device);
   hipError_t e = ix->offsets->reserve(64);
@@ -544,7 +544,7 @@ extern "C" int tfidf_destroy(tfidf_index *ix) {
     if (ix->stage[i]) hipHostFree(ix->stage[i]);
     hipEventDestroy(ix->stage_ev[i]);
   }
-  for (int i = 0; i < 2; i++) hipEventDestroy(ix->mir_ev[i]);
+  for (int i = 0; i < 3; i++) hipEventDestroy(ix->mir_ev[i]);
   hipStreamSynchronize(ix->own_stream);
   hipStreamDestroy(ix->copy_stream);
   hipStreamDestroy(ix->own_stream);
@@ -1397,6 +1397,7 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
     HIP_TRY(launch_df_sum(pp, s));
     HIP_TRY(launch_df_slots(S.crank.as<uint2>(), S.blk.as<uint32_t>() + (size_t)S.n_blocks * S.NC, C,
                             S.sdf.as<uint32_t>(), s));
+    if (mirror_side) HIP_TRY(hipEventRecord(ix->mir_ev[2], s));   // df final: its host mirror copies beside the scatter
     if (S.n_blocks) HIP_TRY(launch_row_scan(pp, s));
     HIP_TRY(hipEventRecord(ix->ev[EV_BSCAN], s));
     HIP_TRY(launch_block_base(pp, s));
@@ -1411,14 +1412,24 @@ static int commit_once(tfidf_index *ix, Snapshot &S) {
     if (S.term_major)       // (block-major: col_rank counted the columns)
       HIP_TRY(launch_count_nonzero(S.dict.as<uint64_t>(), C, reinterpret_cast<unsigned long long *>(ctr + 7),
                                    ix->copy_stream));
+    if (!S.term_major) {
+      // block-major: df and the slot -> column map are final before the
+      // scatter, so their host mirrors copy while it runs (on the main stream
+      // after it they cost ~0.1 ms of the cfg-2 step)
+      HIP_TRY(hipStreamWaitEvent(ix->copy_stream, ix->mir_ev[2], 0));
+      HIP_TRY(hipMemcpyAsync(S.h_df.data(), S.df_dev(), (size_t)C * 4, hipMemcpyDeviceToHost, ix->copy_stream));
+      HIP_TRY(S.h_crank.resize((size_t)C / 32 + 1));
+      HIP_TRY(hipMemcpyAsync(S.h_crank.data(), S.crank.p, ((size_t)C / 32 + 1) * 8, hipMemcpyDeviceToHost,
+                             ix->copy_stream));
+    }
     HIP_TRY(hipEventRecord(ix->mir_ev[1], ix->copy_stream));
   }
   // host mirrors for query analysis: dictionary keys + df
   if (!mirror_side)
     HIP_TRY(hipMemcpyAsync(S.h_dict.data(), S.dict.p, (size_t)2 * C * 8, hipMemcpyDeviceToHost, s));
-  HIP_TRY(hipMemcpyAsync(S.h_df.data(), S.df_dev(), (size_t)C * 4,
-                         hipMemcpyDeviceToHost, s));
-  if (!S.term_major) {                                 // slot -> column for query preparation
+  if (!mirror_side || S.term_major)
+    HIP_TRY(hipMemcpyAsync(S.h_df.data(), S.df_dev(), (size_t)C * 4, hipMemcpyDeviceToHost, s));
+  if (!S.term_major && !mirror_side) {                 // slot -> column for query preparation
     HIP_TRY(S.h_crank.resize((size_t)C / 32 + 1));
     HIP_TRY(hipMemcpyAsync(S.h_crank.data(), S.crank.p, ((size_t)C / 32 + 1) * 8, hipMemcpyDeviceToHost, s));
   }
