@@ -1238,10 +1238,11 @@ hipError_t launch_score_units(const QueryParams &p, const uint4 *units, uint32_t
 // (few postings per block; the host sends queries averaging more than
 // kWunitLightPost postings per block to k_score_units).  Per block the wave
 // inserts each term's segment (query order) into its private 1024-slot LDS
-// hash table (doc -> double sum, as k_score_pairs), then walks the list of
-// claimed slots: keys above the running k-th best go into the lane-held top-k
-// list (topk_insert), and every claimed slot is reset — no table clear, no
-// per-block selection, no candidate array per (query, block).  A block with
+// hash table (doc -> double sum, as k_score_pairs), then walks the table's
+// occupied slots (round 6; a claim list before): keys above the running k-th
+// best go into the lane-held top-k list (topk_insert), and every slot is reset
+// on the way — no separate table clear, no per-block selection, no candidate
+// array per (query, block).  A block with
 // more than kWunitPassPost postings is done in 16 passes over doc sub-ranges
 // of 512 documents (at most 512 distinct documents per pass, so the table
 // never fills).  The next block's segments and first posting chunks are
@@ -1249,15 +1250,9 @@ hipError_t launch_score_units(const QueryParams &p, const uint4 *units, uint32_t
 constexpr uint32_t kWunitWaves = kPairWavesPerWG;
 constexpr uint32_t kWunitPassPost = 700;
 
-#ifndef TFIDF_WUNIT_LIST
-#define TFIDF_WUNIT_LIST 0   // 1: round-5 claim list (29 KiB per workgroup, 5 per CU) — A/B
-#endif
 struct WunitSmem {
   uint32_t key[kWunitWaves][kPairSlots];          // doc - d0 per slot (kPairEmpty = free)
   double val[kWunitWaves][kPairSlots];
-#if TFIDF_WUNIT_LIST
-  uint16_t list[kWunitWaves][kPairSlots];         // claimed slots of the current pass
-#endif
   float cache[256];
 };
 
@@ -1269,9 +1264,6 @@ __global__ void __launch_bounds__(kWunitWaves * 64) k_score_wunits(QueryParams p
   for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) sm.cache[i] = p.cache[i];
   uint32_t *key = sm.key[w];
   double *val = sm.val[w];
-#if TFIDF_WUNIT_LIST
-  uint16_t *list = sm.list[w];
-#endif
   {
     uint4 *kw = reinterpret_cast<uint4 *>(key);
 #pragma unroll
@@ -1332,7 +1324,6 @@ __global__ void __launch_bounds__(kWunitWaves * 64) k_score_wunits(QueryParams p
       const uint32_t np = P > kWunitPassPost ? 16u : 1u;          // 16 passes: 512 documents each
       const uint32_t rsh = np == 1 ? 13u : 9u;
       for (uint32_t ps = 0; ps < np; ps++) {
-        uint32_t nlist = 0;
         // N postings per lane of one term (distinct documents): their first
         // table probes (CAS) all issued before any result is used — one LDS
         // round trip per N postings instead of per posting — then the rare
@@ -1362,24 +1353,15 @@ __global__ void __launch_bounds__(kWunitWaves * 64) k_score_wunits(QueryParams p
           for (int v = 0; v < N; v++) old[v] = act[v] ? atomicCAS(&key[s[v]], kPairEmpty, ld[v]) : 0u;
 #pragma unroll
           for (int v = 0; v < N; v++) {
-            uint32_t claimed = kPairEmpty;
             if (act[v]) {
               uint32_t o = old[v], sl = s[v];
               for (;;) {
-                if (o == kPairEmpty) { val[sl] = (double)sc[v]; claimed = sl; break; }
-                if (o == ld[v]) { val[sl] += (double)sc[v]; break; }
+                if (o == kPairEmpty) { val[sl] = (double)sc[v]; break; }   // claimed
+                if (o == ld[v]) { val[sl] += (double)sc[v]; break; }       // found
                 sl = (sl + 1) & (kPairSlots - 1);
                 o = atomicCAS(&key[sl], kPairEmpty, ld[v]);
               }
             }
-#if TFIDF_WUNIT_LIST
-            const bool c = claimed != kPairEmpty;
-            const uint64_t m = __ballot(c);
-            if (c) list[nlist + (uint32_t)__popcll(m & ((1ull << lane) - 1))] = (uint16_t)claimed;
-            nlist += (uint32_t)__popcll(m);
-#else
-            (void)claimed;
-#endif
           }
         };
         for (uint32_t j = 0; j < nt; j++) {
@@ -1413,24 +1395,10 @@ __global__ void __launch_bounds__(kWunitWaves * 64) k_score_wunits(QueryParams p
           if (b + 2 < bend) segment(b + 2, &na, &nz);
           if (b + 1 < bend) prefetch(a, z, pre);
         }
-#if TFIDF_WUNIT_LIST
-        for (uint32_t h = 0; h < nlist; h += 64) {
-          const uint32_t idx = h + lane;
-          uint64_t kv = 0;
-          if (idx < nlist) {
-            const uint32_t s = list[idx];
-            const uint32_t ld = key[s];
-            kv = ((uint64_t)__float_as_uint((float)val[s]) << 32) | (uint64_t)(~(d0 + ld));
-            key[s] = kPairEmpty;
-          }
-          topk_insert(__ballot(kv > theta), kv, tk, theta, k, lane);
-        }
-#else
         // walk the table itself: lane l owns slots [16 l, 16 l + 16), read as
         // four 16 B pieces in an order rotated by l / 2 (conflict-free), then
         // its occupied slots one per step; each is reset as it is read.  No
         // claim list: the workgroup's LDS is 25 KiB, six per CU instead of five
-        (void)nlist;
         uint32_t occ = 0;
         {
           const uint4 *kq = reinterpret_cast<const uint4 *>(key + 16 * lane);
@@ -1453,7 +1421,6 @@ __global__ void __launch_bounds__(kWunitWaves * 64) k_score_wunits(QueryParams p
           }
           topk_insert(__ballot(kv > theta), kv, tk, theta, k, lane);
         }
-#endif
       }
     }
     const bool has = lane < k && tk != 0;
